@@ -1,0 +1,148 @@
+/*
+ * khst — MI355X batch state-root engine for khipu's Merkle-Patricia trie.
+ * C ABI of libkhst.so (khipu_amd/libkhst.so).  Plain pointers and sizes only.
+ *
+ * Every entry point replaces a reference interface on the state-root path
+ * (paths relative to /root/reference/khipu-base/src/main/scala/khipu/ unless
+ * they start with khipu-eth/):
+ *
+ *   kh_kec256_batch         crypto.kec256(Array[Byte]*)            crypto/package.scala:37-47
+ *                           (one call per message today; here one call per batch,
+ *                           e.g. NodeDatasRequest.processResponse,
+ *                           khipu-eth/.../blockchain/sync/package.scala:88-90)
+ *   kh_trie_root            foldLeft(put) + rootHash over a fresh trie:
+ *                           MerklePatriciaTrie.put/rootHash  trie/MerklePatriciaTrie.scala:78,157-281
+ *                           as driven by TrieAccounts.flush   khipu-eth/.../ledger/TrieAccounts.scala:22-28
+ *                           and GenesisDataLoader             khipu-eth/.../blockchain/data/GenesisDataLoader.scala:139-147
+ *   kh_trie_roots_segmented many independent tries (TrieStorage.flush per contract,
+ *                           khipu-eth/.../ledger/TrieStorage.scala:52-60; BlockWorldState.scala:243-252)
+ *   kh_trie_root_nodes      rootHash + the write-back node set of MerklePatriciaTrie.changes/persist
+ *                           (MerklePatriciaTrie.scala:491-516,544-554 -> NodeStorage.update,
+ *                           khipu-eth/.../storage/NodeStorage.scala:16-19)
+ *   kh_trie_root_sharded    the same root computed from per-GPU top-nibble shards
+ *
+ * Semantics shared by every trie entry point:
+ *   - input i is a put(key_i, value_i); later inputs overwrite earlier ones with the
+ *     same key (the foldLeft order of TrieAccounts.flush);
+ *   - keys are `klen` bytes each; with KH_HASH_KEYS the trie key is kec256(key)
+ *     (Address.hashedAddressEncoder, khipu-eth/.../domain/Address.scala:15-17;
+ *     trie/package.scala:34-36), otherwise klen must be 32 (already keccak'd);
+ *   - values are the serialised bytes (vSerializer.toBytes), packed: value i is
+ *     vals[voff[i] .. voff[i+1]);
+ *   - the root is kec256(encoding of the root node) even when that encoding is
+ *     shorter than 32 bytes (MerklePatriciaTrie.scala:169); an empty trie has root
+ *     EMPTY_TRIE_HASH = kec256(0x80) (trie/package.scala:41).
+ *
+ * Errors: int status; message via kh_last_error() (thread-local).  KH_EDEVICE means
+ * the GPU path failed; the caller decides what to do (there is no silent fallback).
+ * Threading: every call is reentrant; host entry points share one lazily created,
+ * mutex-guarded device context per device.
+ */
+#ifndef KHST_H
+#define KHST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KH_OK 0
+#define KH_EINVAL -1     /* bad argument (RLPException / MPTException analogue) */
+#define KH_ENOMEM -2     /* device allocation failed */
+#define KH_EDEVICE -3    /* HIP runtime / kernel failure, or no device */
+#define KH_ENODE -4      /* missing node (MPTNodeMissingException analogue) */
+#define KH_EINTERNAL -5
+#define KH_ENOSPC -6     /* caller's output buffer too small; required sizes returned */
+
+/* flags */
+#define KH_HASH_KEYS 0x1u   /* trie key = kec256(input key) */
+
+typedef struct kh_stats {
+  uint64_t n_inputs;       /* puts received */
+  uint64_t n_leaves;       /* distinct keys (leaves) */
+  uint64_t n_branches;
+  uint64_t n_extensions;
+  uint64_t n_inline;       /* nodes embedded in their parent (encoding < 32 B) */
+  uint64_t n_node_hashes;  /* Keccak-256 of node encodings >= 32 B, plus one per root */
+  uint64_t n_node_perms;   /* Keccak-f[1600] permutations spent on node encodings */
+  uint64_t n_key_perms;    /* permutations spent hashing keys (KH_HASH_KEYS) */
+  uint64_t arena_bytes;    /* bytes of node RLP produced */
+  uint32_t n_levels;       /* bottom-up branch levels launched */
+  uint32_t full_sort;      /* 1 if the 64-bit-prefix sort had ties and a full-key sort ran */
+  double t_total_ms;       /* device time of the whole build (HIP events) */
+  double t_keys_ms;        /* key hashing */
+  double t_sort_ms;        /* radix sort + gather + dedup */
+  double t_topo_ms;        /* LCP + topology */
+  double t_leaf_ms;        /* leaf encode + hash */
+  double t_branch_ms;      /* all branch levels */
+} kh_stats;
+
+const char* kh_last_error(void);
+const char* kh_version(void);
+int kh_device_count(void);
+
+/* Batched kec256 over n messages packed as data[off[i] .. off[i+1]).  Host buffers. */
+int kh_kec256_batch(const uint8_t* data, const uint64_t* off, uint64_t n, uint8_t* out32);
+
+/* Root of the trie holding puts (key_i, val_i), i < n.  Host buffers. */
+int kh_trie_root(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const uint64_t* voff, uint64_t n,
+                 uint32_t flags, uint8_t root32[32], kh_stats* stats);
+
+/* nseg independent tries; trie s holds inputs seg_off[s] .. seg_off[s+1).  roots32: nseg*32 bytes. */
+int kh_trie_roots_segmented(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const uint64_t* voff,
+                            const uint64_t* seg_off, uint64_t nseg, uint32_t flags, uint8_t* roots32,
+                            kh_stats* stats);
+
+/* Root plus every node a fresh node store needs: each node reachable from the root
+ * whose encoding is >= 32 B, plus the root node (MerklePatriciaTrie.scala:505-511).
+ * Node j: hash hashes32[32j..), encoding rlp[off[j] .. off[j+1]) (off has n_nodes+1
+ * entries).  Nodes are ordered leaves first, then branches/extensions bottom-up, the
+ * root last.  On KH_ENOSPC, *n_nodes and *rlp_len report the sizes needed. */
+int kh_trie_root_nodes(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const uint64_t* voff, uint64_t n,
+                       uint32_t flags, uint8_t root32[32], uint8_t* hashes32, uint64_t node_cap, uint8_t* rlp,
+                       uint64_t rlp_cap, uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len, kh_stats* stats);
+
+/* ---- device-resident interface (inputs already in HBM; used by bench.py and the
+ *      multi-GPU driver).  One context per device; a context is not shared across
+ *      threads without external synchronisation. ---- */
+typedef struct kh_ctx kh_ctx;
+
+int kh_ctx_create(int device, kh_ctx** out);
+int kh_ctx_destroy(kh_ctx* ctx);
+/* Use an existing HIP stream (hipStream_t passed as void*); NULL = the context's own stream. */
+int kh_ctx_set_stream(kh_ctx* ctx, void* hip_stream);
+
+int kh_dev_kec256_batch(kh_ctx* ctx, const uint8_t* d_data, const uint64_t* d_off, uint64_t n, uint8_t* d_out32);
+
+/* Build over device inputs.  depth0 = 0: one trie (or one per segment when d_seg is
+ * non-NULL: d_seg[i] = segment id of input i, ids < nseg).  depth0 = 1, d_seg NULL:
+ * the 16 top-nibble subtries of one trie, paths starting at nibble 1 (the shard
+ * unit of the multi-GPU path).  Per result r (nseg or 16 of them):
+ *   h_hash32[32r..)  kec256 of the top node's encoding (the root for depth0 = 0);
+ *   h_enc_len[r]     that encoding's length (0 = empty);
+ *   h_inline32[32r..) the encoding itself when shorter than 32 B (capped reference).
+ * Outputs are host buffers; h_inline32 may be NULL. */
+int kh_dev_trie_build(kh_ctx* ctx, const uint8_t* d_keys, uint32_t klen, const uint8_t* d_vals,
+                      const uint64_t* d_voff, uint64_t n, const uint32_t* d_seg, uint64_t nseg, uint32_t depth0,
+                      uint32_t flags, uint8_t* h_hash32, uint32_t* h_enc_len, uint8_t* h_inline32,
+                      kh_stats* stats);
+
+/* Fold 16 capped top-nibble references (as produced by kh_dev_trie_build with depth0 = 1,
+ * gathered from every shard) into the root: kec256(RLP[ref_0..ref_15, ""]).
+ * Requires >= 2 non-empty references (otherwise the root is not a branch: returns KH_EINVAL
+ * and the caller builds on one device). */
+int kh_fold_root16(const uint8_t* hash32x16, const uint32_t* enc_len16, const uint8_t* inline32x16,
+                   uint8_t root32[32]);
+
+/* Synthetic account generator (pinned in khipu_amd/csrc/synth.h): writes
+ * accounts [first, first+n) of config `cfg` — 20-byte addresses (d_addr, n*20 B) and RLP
+ * account bodies packed at d_vals with d_voff[n+1] (offsets relative to d_vals; d_vals
+ * must hold n*96 B).  Deterministic; the CPU restatement lives in tests. */
+int kh_dev_synth_accounts(kh_ctx* ctx, uint32_t cfg, uint64_t first, uint64_t n, uint8_t* d_addr,
+                          uint8_t* d_vals, uint64_t* d_voff);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KHST_H */

@@ -1,0 +1,1057 @@
+// libkhst.so — MI355X batch state-root engine for khipu's Merkle-Patricia trie.
+// HIP kernels for gfx950 + the C ABI declared in include/khst.h.
+//
+// Pipeline of one build (all on one HIP stream; DESIGN.md has the roofline of each):
+//   1. keys      kec256 of raw keys (KH_HASH_KEYS)                       k_hash_keys
+//   2. sort      64-bit key-prefix LSD radix sort of (prefix, index)     prims.h
+//                + tie check; full 256-bit sort + dedup only on ties     k_tie/k_word_key/k_dup
+//   3. topology  adjacent LCP -> min pyramid -> nearest smaller values
+//                -> groups (branches), parents, child ordinals            k_lcp..k_leaf_topo
+//   4. leaves    RLP-encode into the node arena + Keccak-256              k_leaf_emit
+//   5. branches  one launch per depth, deepest first: gather child refs,
+//                RLP-encode branch (+ extension) + Keccak-256             k_branch_emit
+// Results: the top node of every segment (root / subtrie reference).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/khst.h"
+#include "keccak.h"
+#include "prims.h"
+#include "synth.h"
+#include "trie_ops.h"
+
+using namespace khst;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_err;
+static int set_err(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+struct KhError {
+  int code;
+  std::string msg;
+};
+#define HIPCHK(x)                                                                                  \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess)                                                                          \
+      throw KhError{e_ == hipErrorOutOfMemory ? KH_ENOMEM : KH_EDEVICE,                            \
+                    std::string(#x) + ": " + hipGetErrorString(e_)};                               \
+  } while (0)
+#define LAUNCH_CHECK() HIPCHK(hipGetLastError())
+
+#define GRID(n, bs) dim3((unsigned)(((n) + (bs)-1) / (bs)))
+constexpr int BS = 256;
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(BS) k_kec_batch(const uint8_t* data, const uint64_t* off, uint64_t n,
+                                                  uint64_t* out) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h[4];
+  uint64_t o = off[i];
+  kec256_msg<false>(data + o, (uint32_t)(off[i + 1] - o), h);
+  for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
+}
+
+__global__ void __launch_bounds__(BS) k_hash_keys(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h[4];
+  kec256_msg<false>(keys + i * klen, klen, h);
+  for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
+}
+
+// composite sort key: segment id in the top sb bits, then the key's leading bits (big-endian)
+__global__ void __launch_bounds__(BS) k_make_ck(const uint64_t* K, const uint32_t* seg, uint32_t sb, uint64_t n,
+                                                uint64_t* ck, uint32_t* idx) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  uint64_t be = bswap64(K[4 * i]);
+  uint64_t c = be;
+  if (sb) c = ((uint64_t)seg[i] << (64 - sb)) | (be >> sb);
+  ck[i] = c;
+  idx[i] = (uint32_t)i;
+}
+
+__global__ void __launch_bounds__(BS) k_tie(const uint64_t* ck, uint64_t n, unsigned long long* flag) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  bool t = (i + 1 < n) && ck[i] == ck[i + 1];
+  if (__any(t) && __lane_id() == 0) atomicOr(flag, 1ULL);
+}
+
+__global__ void __launch_bounds__(BS) k_gather(const uint64_t* K, const uint32_t* seg, const uint32_t* idx,
+                                               uint64_t n, uint64_t* skey, uint32_t* sseg) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s = idx[i];
+  const uint64_t* p = K + 4 * (uint64_t)s;
+  uint64_t* q = skey + 4 * i;
+  q[0] = p[0];
+  q[1] = p[1];
+  q[2] = p[2];
+  q[3] = p[3];
+  if (seg) sseg[i] = seg[s];
+}
+
+__global__ void __launch_bounds__(BS) k_word_key(const uint64_t* K, const uint32_t* idx, int word, uint64_t n,
+                                                 uint64_t* ck) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  ck[i] = bswap64(K[4 * (uint64_t)idx[i] + word]);
+}
+
+__global__ void __launch_bounds__(BS) k_seg_key(const uint32_t* seg, const uint32_t* idx, uint64_t n, uint64_t* ck) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  ck[i] = seg[idx[i]];
+}
+
+// keep the LAST of equal keys (later puts win, TrieAccounts.scala:23-27)
+__global__ void __launch_bounds__(BS) k_dup(const uint64_t* skey, const uint32_t* sseg, uint64_t n, uint32_t* keep) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k = 1;
+  if (i + 1 < n) {
+    const uint64_t* a = skey + 4 * i;
+    const uint64_t* b = a + 4;
+    bool eq = a[0] == b[0] && a[1] == b[1] && a[2] == b[2] && a[3] == b[3];
+    if (sseg && sseg[i] != sseg[i + 1]) eq = false;
+    k = eq ? 0 : 1;
+  }
+  keep[i] = k;
+}
+
+__global__ void __launch_bounds__(BS) k_compact(const uint64_t* skey, const uint32_t* sidx, const uint32_t* sseg,
+                                                const uint32_t* keep_pos, const uint32_t* keep, uint64_t n,
+                                                uint64_t* okey, uint32_t* oidx, uint32_t* oseg) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n || !keep[i]) return;
+  uint64_t p = keep_pos[i];
+  for (int j = 0; j < 4; ++j) okey[4 * p + j] = skey[4 * i + j];
+  oidx[p] = sidx[i];
+  if (sseg) oseg[p] = sseg[i];
+}
+
+__global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb) {
+  uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (b < nb) op_lcp(T, b);
+}
+
+__global__ void __launch_bounds__(BS) k_min64(const uint8_t* in, uint64_t nin, uint8_t* out, uint64_t nout) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < nout) op_min64(in, nin, out, i);
+}
+
+__global__ void __launch_bounds__(BS) k_ansv(Topo T, Pyr P, uint64_t nb) {
+  uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (b < nb) op_ansv(T, P, b);
+}
+
+__global__ void __launch_bounds__(BS) k_chain(Topo T, uint64_t nb) {
+  uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (b < nb) op_chain(T, b);
+}
+
+__global__ void __launch_bounds__(BS) k_group(Topo T, uint64_t nb) {
+  uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (b >= nb) return;
+  if (T.u[b] == 0) {
+    T.grp[b] = NONE;
+    return;
+  }
+  uint32_t g = T.isrep_bid[T.rep[b]];
+  T.grp[b] = g;
+  atomicMax(&T.br_k[g], (uint32_t)T.ord[b] + 2u);
+}
+
+__global__ void __launch_bounds__(BS) k_branch_topo(Topo T, uint64_t nb) {
+  uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (b >= nb) return;
+  op_branch_topo(T, b);
+  if (T.u[b] != 0 && T.rep[b] == (uint32_t)b) {
+    uint32_t j = T.isrep_bid[b];
+    atomicAdd(&T.depth_hist[T.br_depth[j]], 1u);
+    if (T.br_ext[j]) atomicAdd(&T.ctr[CTR_EXT], 1ULL);
+  }
+}
+
+__global__ void __launch_bounds__(BS) k_leaf_topo(Topo T) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < T.m) op_leaf_topo(T, i);
+}
+
+__global__ void __launch_bounds__(BS) k_branch_alen(Topo T, uint64_t B) {
+  uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (j < B) T.br_aoff[j] = branch_arena_bytes(T, (uint32_t)j);
+}
+
+__global__ void __launch_bounds__(BS) k_level_scatter(Topo T, uint64_t B, const uint32_t* level_base,
+                                                      uint32_t* cursor, uint32_t* order) {
+  uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (j >= B) return;
+  uint32_t d = T.br_depth[j];
+  uint32_t p = atomicAdd(&cursor[d], 1u);
+  order[level_base[d] + p] = (uint32_t)j;
+}
+
+__global__ void __launch_bounds__(BS) k_leaf_emit(Topo T) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  unsigned long long perms = 0, hashes = 0, inl = 0;
+  if (i < T.m) {
+    uint32_t in1 = 0;
+    perms = op_leaf_emit(T, i, &in1);
+    hashes = perms ? 1 : 0;
+    inl = in1;
+  }
+  wave_atomic_add(&T.ctr[CTR_PERMS], perms);
+  wave_atomic_add(&T.ctr[CTR_HASHES], hashes);
+  wave_atomic_add(&T.ctr[CTR_INLINE], inl);
+}
+
+__global__ void __launch_bounds__(BS) k_branch_emit(Topo T, const uint32_t* order, uint64_t cnt) {
+  uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  unsigned long long perms = 0, hashes = 0, inl = 0;
+  if (t < cnt) {
+    uint32_t j = order[t];
+    uint32_t in1 = 0;
+    perms = op_branch_emit(T, j, &in1);
+    // hashes: branch hashed if len >= 32 or top; extension likewise
+    uint32_t L = T.br_len[j];
+    bool top = T.br_parent[j] == NONE;
+    bool ext = T.br_ext[j] != 0;
+    hashes = (L >= 32 || (top && !ext)) ? 1 : 0;
+    if (ext) hashes += (T.ex_len[j] >= 32 || top) ? 1 : 0;
+    inl = in1;
+  }
+  wave_atomic_add(&T.ctr[CTR_PERMS], perms);
+  wave_atomic_add(&T.ctr[CTR_HASHES], hashes);
+  wave_atomic_add(&T.ctr[CTR_INLINE], inl);
+}
+
+// write-back emission: node q in [0, m + 2B): leaf q, or branch / extension of branch (q-m)/2
+__device__ __forceinline__ bool emit_node(const Topo& T, uint64_t B, uint64_t q, uint64_t* aoff, uint32_t* len,
+                                          const uint64_t** hash) {
+  if (q < T.m) {
+    uint32_t L = T.lf_len[q];
+    bool top = T.lf_parent[q] == NONE;
+    *aoff = T.lf_aoff[q];
+    *len = L;
+    *hash = T.lf_hash + 4 * q;
+    return L >= 32 || top;
+  }
+  uint64_t j = (q - T.m) >> 1;
+  bool top = T.br_parent[j] == NONE;
+  bool has_ext = T.br_ext[j] != 0;
+  if (((q - T.m) & 1) == 0) {
+    uint32_t L = T.br_len[j];
+    *aoff = T.br_arena_base + T.br_aoff[j];
+    *len = L;
+    *hash = T.br_hash + 4 * j;
+    return L >= 32 || (top && !has_ext);
+  }
+  if (!has_ext) return false;
+  uint32_t L = T.ex_len[j];
+  *aoff = T.br_arena_base + T.br_aoff[j] + branch_bound(T.br_k[j]);
+  *len = L;
+  *hash = T.ex_hash + 4 * j;
+  return L >= 32 || top;
+}
+
+__global__ void __launch_bounds__(BS) k_emit_sizes(Topo T, uint64_t B, uint32_t* flag, uint64_t* bytes) {
+  uint64_t q = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (q >= T.m + 2 * B) return;
+  uint64_t aoff;
+  uint32_t len;
+  const uint64_t* h;
+  bool e = emit_node(T, B, q, &aoff, &len, &h);
+  flag[q] = e ? 1 : 0;
+  bytes[q] = e ? len : 0;
+}
+
+__global__ void __launch_bounds__(BS) k_emit_copy(Topo T, uint64_t B, const uint32_t* pos, const uint64_t* boff,
+                                                  uint8_t* out_hash, uint8_t* out_rlp, uint64_t* out_off) {
+  uint64_t q = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (q >= T.m + 2 * B) return;
+  uint64_t aoff;
+  uint32_t len;
+  const uint64_t* h;
+  if (!emit_node(T, B, q, &aoff, &len, &h)) return;
+  uint64_t p = pos[q];
+  uint64_t* oh = (uint64_t*)(out_hash + 32 * p);
+  for (int j = 0; j < 4; ++j) oh[j] = h[j];
+  const uint8_t* src = T.arena + aoff;
+  uint8_t* dst = out_rlp + boff[q];
+  for (uint32_t b = 0; b < len; ++b) dst[b] = src[b];
+  out_off[p] = boff[q];
+}
+
+__global__ void __launch_bounds__(BS) k_synth_len(uint32_t cfg, uint64_t first, uint64_t n, uint64_t* voff) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i > n) return;
+  voff[i] = (i < n) ? synth_body_len(synth_acct(cfg, first + i)) : 0;
+}
+
+__global__ void __launch_bounds__(BS) k_synth_write(uint32_t cfg, uint64_t first, uint64_t n, const uint64_t* voff,
+                                                    uint8_t* addr, uint8_t* vals) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  SynthAcct a = synth_acct(cfg, first + i);
+  synth_addr_write(a, addr + 20 * i);
+  synth_body_write(a, first + i, vals + voff[i]);
+}
+
+// ---------------------------------------------------------------------------
+// device workspace
+// ---------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  void ensure(size_t bytes) {
+    if (bytes <= cap) return;
+    if (p) HIPCHK(hipFree(p));
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes + bytes / 8 + 4096;
+    HIPCHK(hipMalloc(&p, want));
+    cap = want;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// bump carving inside one DevBuf
+struct Carver {
+  char* base;
+  size_t off = 0;
+  size_t cap;
+  template <typename T>
+  T* take(size_t count) {
+    off = (off + 255) & ~(size_t)255;
+    T* r = (T*)(base + off);
+    off += count * sizeof(T) + 16;  // +16: slack for 8-byte word over-reads
+    if (off > cap) throw KhError{KH_EINTERNAL, "workspace carve overflow"};
+    return r;
+  }
+};
+static size_t carve_size(const std::vector<size_t>& items) {
+  size_t s = 0;
+  for (size_t b : items) s = ((s + 255) & ~(size_t)255) + b + 16;
+  return s + 256;
+}
+
+struct kh_ctx {
+  int dev = 0;
+  hipStream_t own = nullptr;
+  hipStream_t st = nullptr;
+  std::mutex mu;
+  DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, out_emit;
+  hipEvent_t ev[8] = {};
+  unsigned long long* h_pinned = nullptr;  // small pinned staging for syncs
+  // last build (for emission)
+  Topo T{};
+  uint64_t last_B = 0;
+  uint64_t last_nres = 0;
+};
+
+// ---------------------------------------------------------------------------
+// the build
+// ---------------------------------------------------------------------------
+struct BuildArgs {
+  const uint8_t* keys;
+  uint32_t klen;
+  const uint8_t* vals;
+  const uint64_t* voff;
+  uint64_t n;
+  const uint32_t* seg;  // nullable
+  uint64_t nseg;
+  uint32_t depth0;
+  uint32_t flags;
+  bool emit;
+};
+struct BuildOut {
+  std::vector<uint64_t> res_hash;  // nres*4
+  std::vector<uint32_t> res_len;
+  std::vector<uint64_t> res_inl;
+};
+
+static uint32_t bits_for(uint64_t nseg) {
+  uint32_t b = 0;
+  while (b < 64 && (1ULL << b) < nseg) ++b;
+  return b;
+}
+
+static float ev_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
+  return ms;
+}
+
+static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats) {
+  hipStream_t st = c->st;
+  const uint64_t n = A.n;
+  const bool segmented = A.seg != nullptr;
+  const uint64_t nres = segmented ? A.nseg : (A.depth0 == 1 ? 16 : 1);
+  if (n >= (1ULL << 31)) throw KhError{KH_EINVAL, "n must be < 2^31 per device"};
+  if (A.depth0 > 1) throw KhError{KH_EINVAL, "depth0 must be 0 or 1"};
+  if (segmented && A.depth0 != 0) throw KhError{KH_EINVAL, "segmented builds use depth0 = 0"};
+  if (!(A.flags & KH_HASH_KEYS) && A.klen != 32) throw KhError{KH_EINVAL, "keys must be 32 bytes unless KH_HASH_KEYS"};
+  if (A.klen == 0 || A.klen > 4096) throw KhError{KH_EINVAL, "bad key length"};
+  const uint32_t sb = segmented ? bits_for(A.nseg) : 0;
+  if (sb > 32) throw KhError{KH_EINVAL, "too many segments"};
+
+  O.res_hash.assign(nres * 4, 0);
+  O.res_len.assign(nres, 0);
+  O.res_inl.assign(nres * 4, 0);
+  if (stats) {
+    memset(stats, 0, sizeof(*stats));
+    stats->n_inputs = n;
+  }
+  if (n == 0) return;
+
+  // ---- phase-1 workspace (sized by n)
+  const uint64_t nb1 = n;  // boundaries <= n-1; round up
+  std::vector<size_t> sz = {
+      (A.flags & KH_HASH_KEYS) ? n * 32 : 0,  // K32
+      n * 8, n * 8, n * 4, n * 4,             // ck0 ck1 idx0 idx1
+      n * 32, segmented ? n * 4 : 0,          // skey sseg
+      radix_scratch_bytes(n), scan_scratch_bytes(n, 8),
+      nb1, nb1 / 32 + 1024,                   // u, pyramid
+      nb1 * 4, nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1 * 4, nb1 * 4,  // psv nsv pse rep ord isrep grp
+      nb1 * 4, nb1 * 4, nb1, nb1, nb1 * 4, nb1, nb1 * 4, nb1 * 8, nb1 * 4, nb1 * 4,  // branches
+      n * 4, n, n, n * 8, n * 4,              // leaves
+      A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
+      nres * 32, nres * 4, nres * 32,         // results
+      CTR_N * 8, 64 * 4, 64 * 4, 64 * 4, nb1 * 4,  // ctr hist level_base cursor order
+  };
+  c->ws1.ensure(carve_size(sz));
+  Carver cv{(char*)c->ws1.p, 0, c->ws1.cap};
+  uint64_t* K32 = (A.flags & KH_HASH_KEYS) ? cv.take<uint64_t>(n * 4) : (uint64_t*)A.keys;
+  uint64_t* ck0 = cv.take<uint64_t>(n);
+  uint64_t* ck1 = cv.take<uint64_t>(n);
+  uint32_t* idx0 = cv.take<uint32_t>(n);
+  uint32_t* idx1 = cv.take<uint32_t>(n);
+  uint64_t* skey = cv.take<uint64_t>(n * 4);
+  uint32_t* sseg = segmented ? cv.take<uint32_t>(n) : nullptr;
+  void* rs_scratch = cv.take<char>(radix_scratch_bytes(n));
+  void* scan_scratch = cv.take<char>(scan_scratch_bytes(n, 8));
+  Topo T{};
+  T.u = cv.take<uint8_t>(nb1);
+  uint8_t* pyr = cv.take<uint8_t>(nb1 / 32 + 1024);
+  T.psv = cv.take<int32_t>(nb1);
+  T.nsv = cv.take<int32_t>(nb1);
+  T.pse = cv.take<int32_t>(nb1);
+  T.rep = cv.take<uint32_t>(nb1);
+  T.ord = cv.take<uint8_t>(nb1);
+  T.isrep_bid = cv.take<uint32_t>(nb1);
+  T.grp = cv.take<uint32_t>(nb1);
+  T.br_k = cv.take<uint32_t>(nb1);
+  T.br_cbase = cv.take<uint32_t>(nb1);
+  T.br_depth = cv.take<uint8_t>(nb1);
+  T.br_ext = cv.take<uint8_t>(nb1);
+  T.br_parent = cv.take<uint32_t>(nb1);
+  T.br_pord = cv.take<uint8_t>(nb1);
+  T.br_first = cv.take<uint32_t>(nb1);
+  T.br_aoff = cv.take<uint64_t>(nb1);
+  T.br_len = cv.take<uint32_t>(nb1);
+  T.ex_len = cv.take<uint32_t>(nb1);
+  T.lf_parent = cv.take<uint32_t>(n);
+  T.lf_pord = cv.take<uint8_t>(n);
+  T.lf_pd = cv.take<int8_t>(n);
+  T.lf_aoff = cv.take<uint64_t>(n);
+  T.lf_len = cv.take<uint32_t>(n);
+  T.lf_hash = A.emit ? cv.take<uint64_t>(n * 4) : nullptr;
+  T.br_hash = A.emit ? cv.take<uint64_t>(nb1 * 4) : nullptr;
+  T.ex_hash = A.emit ? cv.take<uint64_t>(nb1 * 4) : nullptr;
+  T.res_hash = cv.take<uint64_t>(nres * 4);
+  T.res_len = cv.take<uint32_t>(nres);
+  T.res_inl = cv.take<uint64_t>(nres * 4);
+  T.ctr = cv.take<unsigned long long>(CTR_N);
+  T.depth_hist = cv.take<uint32_t>(64);
+  uint32_t* level_base = cv.take<uint32_t>(64);
+  uint32_t* cursor = cv.take<uint32_t>(64);
+  uint32_t* order = cv.take<uint32_t>(nb1);
+  T.depth0 = A.depth0;
+  T.segmented = segmented ? 1 : 0;
+  T.vals = A.vals;
+  T.voff = A.voff;
+
+  HIPCHK(hipMemsetAsync(T.ctr, 0, CTR_N * 8, st));
+  HIPCHK(hipMemsetAsync(T.depth_hist, 0, 64 * 4, st));
+  HIPCHK(hipMemsetAsync(cursor, 0, 64 * 4, st));
+  HIPCHK(hipMemsetAsync(T.res_len, 0, nres * 4, st));
+  HIPCHK(hipMemsetAsync(T.res_hash, 0, nres * 32, st));
+  HIPCHK(hipMemsetAsync(T.res_inl, 0, nres * 32, st));
+
+  HIPCHK(hipEventRecord(c->ev[0], st));
+  // ---- 1. keys
+  if (A.flags & KH_HASH_KEYS) {
+    hipLaunchKernelGGL(k_hash_keys, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32);
+    LAUNCH_CHECK();
+  }
+  HIPCHK(hipEventRecord(c->ev[1], st));
+
+  // ---- 2. sort on the 64-bit composite prefix
+  hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, sb, n, ck0, idx0);
+  LAUNCH_CHECK();
+  bool flip = radix_sort_pairs(ck0, idx0, ck1, idx1, n, 0, 64, rs_scratch, st);
+  uint64_t* cks = flip ? ck1 : ck0;
+  uint32_t* idxs = flip ? idx1 : idx0;
+  uint32_t* idxo = flip ? idx0 : idx1;
+  uint64_t* cko = flip ? ck0 : ck1;
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_tie, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, n, T.ctr + CTR_TIE);
+  LAUNCH_CHECK();
+  HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  bool ties = c->h_pinned[0] != 0;
+  uint64_t m = n;
+  uint32_t* sidx = idxs;
+  if (!ties) {
+    hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, (const uint32_t*)idxs,
+                       n, skey, sseg);
+    LAUNCH_CHECK();
+  } else {
+    // full 256-bit (+segment) LSD sort from the input order, then keep the last duplicate
+    uint32_t* ia = idx0;
+    uint32_t* ib = idx1;
+    uint64_t* ka = ck0;
+    uint64_t* kb = ck1;
+    std::vector<uint32_t> ident;  // identity via kernel: reuse k_make_ck to fill idx
+    hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, 0u, n, ka, ia);
+    LAUNCH_CHECK();
+    auto pass = [&](int word, int bits) {
+      if (word >= 0)
+        hipLaunchKernelGGL(k_word_key, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, (const uint32_t*)ia, word,
+                           n, ka);
+      else
+        hipLaunchKernelGGL(k_seg_key, GRID(n, BS), dim3(BS), 0, st, A.seg, (const uint32_t*)ia, n, ka);
+      LAUNCH_CHECK();
+      if (radix_sort_pairs(ka, ia, kb, ib, n, 0, bits, rs_scratch, st)) {
+        std::swap(ka, kb);
+        std::swap(ia, ib);
+      }
+    };
+    for (int w = 3; w >= 0; --w) pass(w, 64);
+    if (segmented) pass(-1, ((sb + 7) / 8) * 8);
+    // gather in full order into skey (ib/kb are free now)
+    hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, (const uint32_t*)ia, n,
+                       skey, sseg);
+    LAUNCH_CHECK();
+    uint32_t* keep = (uint32_t*)kb;  // n*8 bytes available
+    uint32_t* keep_pos = ib;
+    hipLaunchKernelGGL(k_dup, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)skey, (const uint32_t*)sseg, n, keep);
+    LAUNCH_CHECK();
+    uint32_t* mtot = (uint32_t*)(T.ctr + CTR_M);
+    scan_exclusive<uint32_t>(keep, keep_pos, n, mtot, scan_scratch, st);
+    HIPCHK(hipMemcpyAsync(c->h_pinned, mtot, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    m = (uint32_t)c->h_pinned[0];
+    if (m < n) {
+      // compact into a second key buffer carved from ws3
+      c->ws3.ensure(carve_size({n * 32, n * 4, n * 4}));
+      Carver c3{(char*)c->ws3.p, 0, c->ws3.cap};
+      uint64_t* skey2 = c3.take<uint64_t>(n * 4);
+      uint32_t* sidx2 = c3.take<uint32_t>(n);
+      uint32_t* sseg2 = segmented ? c3.take<uint32_t>(n) : nullptr;
+      hipLaunchKernelGGL(k_compact, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)skey, (const uint32_t*)ia,
+                         (const uint32_t*)sseg, (const uint32_t*)keep_pos, (const uint32_t*)keep, n, skey2, sidx2,
+                         sseg2);
+      LAUNCH_CHECK();
+      skey = skey2;
+      sidx = sidx2;
+      sseg = sseg2;
+    } else {
+      sidx = ia;
+    }
+    (void)idxo;
+    (void)cko;
+  }
+  T.m = m;
+  T.skey = skey;
+  T.sidx = sidx;
+  T.sseg = sseg;
+  HIPCHK(hipEventRecord(c->ev[2], st));
+
+  // ---- 3. topology
+  const uint64_t nb = m - 1;
+  uint64_t B = 0;
+  std::vector<uint32_t> hist(64, 0);
+  if (nb > 0) {
+    hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb);
+    LAUNCH_CHECK();
+    Pyr P{};
+    P.lv[0] = T.u;
+    P.sz[0] = nb;
+    P.nl = 1;
+    uint8_t* pp = pyr;
+    while (P.sz[P.nl - 1] > 64) {
+      if (P.nl >= 8) throw KhError{KH_EINTERNAL, "pyramid too deep"};
+      uint64_t nin = P.sz[P.nl - 1], nout = (nin + 63) / 64;
+      hipLaunchKernelGGL(k_min64, GRID(nout, BS), dim3(BS), 0, st, P.lv[P.nl - 1], nin, pp, nout);
+      LAUNCH_CHECK();
+      P.lv[P.nl] = pp;
+      P.sz[P.nl] = nout;
+      P.nl++;
+      pp += (nout + 255) & ~(uint64_t)255;
+    }
+    hipLaunchKernelGGL(k_ansv, GRID(nb, BS), dim3(BS), 0, st, T, P, nb);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_chain, GRID(nb, BS), dim3(BS), 0, st, T, nb);
+    LAUNCH_CHECK();
+    uint32_t* btot = (uint32_t*)(T.ctr + CTR_B);
+    scan_exclusive<uint32_t>(T.isrep_bid, T.isrep_bid, nb, btot, scan_scratch, st);
+    HIPCHK(hipMemsetAsync(T.br_k, 0, nb * 4, st));
+    hipLaunchKernelGGL(k_group, GRID(nb, BS), dim3(BS), 0, st, T, nb);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_branch_topo, GRID(nb, BS), dim3(BS), 0, st, T, nb);
+    LAUNCH_CHECK();
+    HIPCHK(hipMemcpyAsync(c->h_pinned, btot, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned + 1, T.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned + 8, T.depth_hist, 64 * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    B = (uint32_t)c->h_pinned[0];
+    if (c->h_pinned[1]) throw KhError{KH_EINTERNAL, "topology invariant violated (group chain > 15)"};
+    memcpy(hist.data(), c->h_pinned + 8, 64 * 4);
+  }
+  hipLaunchKernelGGL(k_leaf_topo, GRID(m, BS), dim3(BS), 0, st, T);
+  LAUNCH_CHECK();
+  // ---- child bases and arena offsets
+  unsigned long long* ctr = T.ctr;
+  HIPCHK(hipMemsetAsync(ctr + CTR_BRBYTES, 0, 24, st));
+  if (B > 0) {
+    scan_exclusive<uint32_t>(T.br_k, T.br_cbase, B, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
+    hipLaunchKernelGGL(k_branch_alen, GRID(B, BS), dim3(BS), 0, st, T, B);
+    LAUNCH_CHECK();
+    scan_exclusive<uint64_t>(T.br_aoff, T.br_aoff, B, (uint64_t*)(ctr + CTR_BRBYTES), scan_scratch, st);
+  }
+  scan_exclusive<uint64_t>(T.lf_aoff, T.lf_aoff, m, (uint64_t*)(ctr + CTR_LFBYTES), scan_scratch, st);
+  HIPCHK(hipMemcpyAsync(c->h_pinned, ctr + CTR_BRBYTES, 24, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint64_t br_bytes = c->h_pinned[0];
+  const uint64_t lf_bytes = c->h_pinned[1];
+  const uint64_t C = (uint32_t)c->h_pinned[2];
+
+  // ---- phase-2 workspace: child records + node arena
+  c->ws2.ensure(carve_size({C * 32, C * 2, lf_bytes + br_bytes + 64}));
+  Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
+  T.cref = cv2.take<uint64_t>(C * 4);
+  T.cmeta = cv2.take<uint16_t>(C);
+  T.arena = cv2.take<uint8_t>(lf_bytes + br_bytes + 64);
+  T.br_arena_base = lf_bytes;
+
+  // level order: branches grouped by depth, deepest first
+  std::vector<uint32_t> base(64, 0);
+  {
+    uint32_t run = 0;
+    for (int d = 0; d < 64; ++d) {
+      base[d] = run;
+      run += hist[d];
+    }
+  }
+  if (B > 0) {
+    HIPCHK(hipMemcpyAsync(level_base, base.data(), 64 * 4, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_level_scatter, GRID(B, BS), dim3(BS), 0, st, T, B, (const uint32_t*)level_base, cursor,
+                       order);
+    LAUNCH_CHECK();
+  }
+  HIPCHK(hipEventRecord(c->ev[3], st));
+
+  // ---- 4. leaves
+  hipLaunchKernelGGL(k_leaf_emit, GRID(m, BS), dim3(BS), 0, st, T);
+  LAUNCH_CHECK();
+  HIPCHK(hipEventRecord(c->ev[4], st));
+
+  // ---- 5. branch levels, deepest first
+  uint32_t levels = 0;
+  for (int d = 63; d >= 0; --d) {
+    if (!hist[d]) continue;
+    hipLaunchKernelGGL(k_branch_emit, GRID(hist[d], BS), dim3(BS), 0, st, T, (const uint32_t*)(order + base[d]),
+                       (uint64_t)hist[d]);
+    LAUNCH_CHECK();
+    ++levels;
+  }
+  HIPCHK(hipEventRecord(c->ev[5], st));
+
+  // ---- results
+  HIPCHK(hipMemcpyAsync(O.res_hash.data(), T.res_hash, nres * 32, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(O.res_len.data(), T.res_len, nres * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(O.res_inl.data(), T.res_inl, nres * 32, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(c->h_pinned, ctr, CTR_N * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  c->T = T;
+  c->last_B = B;
+  c->last_nres = nres;
+  if (stats) {
+    stats->n_leaves = m;
+    stats->n_branches = B;
+    stats->n_node_hashes = c->h_pinned[CTR_HASHES];
+    stats->n_node_perms = c->h_pinned[CTR_PERMS];
+    stats->n_inline = c->h_pinned[CTR_INLINE];
+    stats->n_extensions = c->h_pinned[CTR_EXT];
+    stats->n_key_perms = (A.flags & KH_HASH_KEYS) ? n * (uint64_t)(A.klen / 136 + 1) : 0;
+    stats->arena_bytes = lf_bytes + br_bytes;
+    stats->n_levels = levels;
+    stats->full_sort = ties ? 1 : 0;
+    stats->t_keys_ms = ev_ms(c->ev[0], c->ev[1]);
+    stats->t_sort_ms = ev_ms(c->ev[1], c->ev[2]);
+    stats->t_topo_ms = ev_ms(c->ev[2], c->ev[3]);
+    stats->t_leaf_ms = ev_ms(c->ev[3], c->ev[4]);
+    stats->t_branch_ms = ev_ms(c->ev[4], c->ev[5]);
+    stats->t_total_ms = ev_ms(c->ev[0], c->ev[5]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// context management
+// ---------------------------------------------------------------------------
+static std::mutex g_ctx_mu;
+static std::vector<kh_ctx*> g_ctx;
+
+static kh_ctx* ctx_new(int dev) {
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (dev < 0 || dev >= ndev) throw KhError{KH_EDEVICE, "no such device"};
+  HIPCHK(hipSetDevice(dev));
+  kh_ctx* c = new kh_ctx();
+  c->dev = dev;
+  HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+  c->st = c->own;
+  for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipHostMalloc((void**)&c->h_pinned, 4096, hipHostMallocDefault));
+  return c;
+}
+
+static kh_ctx* shared_ctx(int dev) {
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  if ((int)g_ctx.size() <= dev) g_ctx.resize(dev + 1, nullptr);
+  if (!g_ctx[dev]) g_ctx[dev] = ctx_new(dev);
+  return g_ctx[dev];
+}
+
+static int current_device() {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return 0;
+  return d;
+}
+
+#define API_TRY(...)                                                    \
+  try {                                                                 \
+    __VA_ARGS__;                                                        \
+    return KH_OK;                                                       \
+  } catch (KhError & e) {                                               \
+    return set_err(e.code, e.msg);                                      \
+  } catch (std::bad_alloc&) {                                           \
+    return set_err(KH_ENOMEM, "host allocation failed");                \
+  } catch (std::exception & e) {                                        \
+    return set_err(KH_EINTERNAL, e.what());                             \
+  }
+
+// copy host inputs into the context's staging buffers
+struct Staged {
+  const uint8_t* keys;
+  const uint8_t* vals;
+  const uint64_t* voff;
+  const uint32_t* seg;
+};
+static Staged stage_inputs(kh_ctx* c, const uint8_t* keys, uint32_t klen, const uint8_t* vals, const uint64_t* voff,
+                           uint64_t n, const std::vector<uint32_t>* seg) {
+  uint64_t v0 = voff[0], vbytes = voff[n] - v0;
+  c->in_keys.ensure(n * klen + 64);
+  c->in_vals.ensure(vbytes + 64);
+  c->in_voff.ensure((n + 1) * 8 + 64);
+  std::vector<uint64_t> rel(voff, voff + n + 1);
+  for (auto& x : rel) x -= v0;
+  hipStream_t st = c->st;
+  if (n) HIPCHK(hipMemcpyAsync(c->in_keys.p, keys, n * klen, hipMemcpyHostToDevice, st));
+  if (vbytes) HIPCHK(hipMemcpyAsync(c->in_vals.p, vals + v0, vbytes, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c->in_voff.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+  const uint32_t* dseg = nullptr;
+  if (seg) {
+    c->in_seg.ensure(n * 4 + 64);
+    if (n) HIPCHK(hipMemcpyAsync(c->in_seg.p, seg->data(), n * 4, hipMemcpyHostToDevice, st));
+    dseg = (const uint32_t*)c->in_seg.p;
+  }
+  HIPCHK(hipStreamSynchronize(st));  // `rel` and `seg` are host temporaries
+  return Staged{(const uint8_t*)c->in_keys.p, (const uint8_t*)c->in_vals.p, (const uint64_t*)c->in_voff.p, dseg};
+}
+
+static const uint8_t EMPTY_TRIE_HASH[32] = {0x56, 0xe8, 0x1f, 0x17, 0x1b, 0xcc, 0x55, 0xa6, 0xff, 0x83, 0x45,
+                                            0xe6, 0x92, 0xc0, 0xf8, 0x6e, 0x5b, 0x48, 0xe0, 0x1b, 0x99, 0x6c,
+                                            0xad, 0xc0, 0x01, 0x62, 0x2f, 0xb5, 0xe3, 0x63, 0xb4, 0x21};
+
+static void copy_root(const BuildOut& O, uint64_t r, uint8_t* out32) {
+  if (O.res_len[r] == 0)
+    memcpy(out32, EMPTY_TRIE_HASH, 32);
+  else
+    memcpy(out32, &O.res_hash[4 * r], 32);
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char* kh_last_error(void) { return g_err.c_str(); }
+const char* kh_version(void) { return "khst 0.1 (gfx950)"; }
+int kh_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int kh_ctx_create(int device, kh_ctx** out) { API_TRY(*out = ctx_new(device)) }
+
+int kh_ctx_destroy(kh_ctx* c) {
+  if (!c) return KH_OK;
+  API_TRY({
+    (void)hipSetDevice(c->dev);
+    (void)hipStreamSynchronize(c->st);
+    for (DevBuf* b : {&c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->out_emit})
+      b->release();
+    for (auto& e : c->ev)
+      if (e) (void)hipEventDestroy(e);
+    if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+  })
+}
+
+int kh_ctx_set_stream(kh_ctx* c, void* s) {
+  if (!c) return set_err(KH_EINVAL, "null context");
+  c->st = s ? (hipStream_t)s : c->own;
+  return KH_OK;
+}
+
+int kh_dev_kec256_batch(kh_ctx* c, const uint8_t* d_data, const uint64_t* d_off, uint64_t n, uint8_t* d_out32) {
+  if (!c) return set_err(KH_EINVAL, "null context");
+  API_TRY({
+    HIPCHK(hipSetDevice(c->dev));
+    if (n) {
+      hipLaunchKernelGGL(k_kec_batch, GRID(n, BS), dim3(BS), 0, c->st, d_data, d_off, n, (uint64_t*)d_out32);
+      LAUNCH_CHECK();
+    }
+  })
+}
+
+int kh_kec256_batch(const uint8_t* data, const uint64_t* off, uint64_t n, uint8_t* out32) {
+  API_TRY({
+    kh_ctx* c = shared_ctx(current_device());
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->dev));
+    if (n == 0) return KH_OK;
+    uint64_t o0 = off[0], bytes = off[n] - o0;
+    c->in_vals.ensure(bytes + 64);
+    c->in_voff.ensure((n + 1) * 8 + 64);
+    c->in_keys.ensure(n * 32 + 64);
+    std::vector<uint64_t> rel(off, off + n + 1);
+    for (auto& x : rel) x -= o0;
+    if (bytes) HIPCHK(hipMemcpyAsync(c->in_vals.p, data + o0, bytes, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(c->in_voff.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->st));
+    hipLaunchKernelGGL(k_kec_batch, GRID(n, BS), dim3(BS), 0, c->st, (const uint8_t*)c->in_vals.p,
+                       (const uint64_t*)c->in_voff.p, n, (uint64_t*)c->in_keys.p);
+    LAUNCH_CHECK();
+    HIPCHK(hipMemcpyAsync(out32, c->in_keys.p, n * 32, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+  })
+}
+
+int kh_trie_root(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const uint64_t* voff, uint64_t n,
+                 uint32_t flags, uint8_t root32[32], kh_stats* stats) {
+  API_TRY({
+    if (n && (!keys || !voff)) throw KhError{KH_EINVAL, "null input"};
+    if (n == 0) {
+      if (stats) memset(stats, 0, sizeof(*stats));
+      memcpy(root32, EMPTY_TRIE_HASH, 32);
+      return KH_OK;
+    }
+    kh_ctx* c = shared_ctx(current_device());
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->dev));
+    Staged S = stage_inputs(c, keys, klen, vals, voff, n, nullptr);
+    BuildArgs A{S.keys, klen, S.vals, S.voff, n, nullptr, 1, 0, flags, false};
+    BuildOut O;
+    run_build(c, A, O, stats);
+    copy_root(O, 0, root32);
+  })
+}
+
+int kh_trie_roots_segmented(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const uint64_t* voff,
+                            const uint64_t* seg_off, uint64_t nseg, uint32_t flags, uint8_t* roots32,
+                            kh_stats* stats) {
+  API_TRY({
+    if (nseg == 0) return KH_OK;
+    uint64_t n = seg_off[nseg] - seg_off[0];
+    std::vector<uint32_t> seg(n);
+    for (uint64_t s = 0; s < nseg; ++s) {
+      if (seg_off[s + 1] < seg_off[s]) throw KhError{KH_EINVAL, "seg_off not monotone"};
+      for (uint64_t i = seg_off[s]; i < seg_off[s + 1]; ++i) seg[i - seg_off[0]] = (uint32_t)s;
+    }
+    if (n == 0) {
+      for (uint64_t s = 0; s < nseg; ++s) memcpy(roots32 + 32 * s, EMPTY_TRIE_HASH, 32);
+      if (stats) memset(stats, 0, sizeof(*stats));
+      return KH_OK;
+    }
+    kh_ctx* c = shared_ctx(current_device());
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->dev));
+    const uint64_t* vo = voff + seg_off[0];
+    Staged S = stage_inputs(c, keys + seg_off[0] * klen, klen, vals, vo, n, &seg);
+    BuildArgs A{S.keys, klen, S.vals, S.voff, n, S.seg, nseg, 0, flags, false};
+    BuildOut O;
+    run_build(c, A, O, stats);
+    for (uint64_t s = 0; s < nseg; ++s) copy_root(O, s, roots32 + 32 * s);
+  })
+}
+
+int kh_trie_root_nodes(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const uint64_t* voff, uint64_t n,
+                       uint32_t flags, uint8_t root32[32], uint8_t* hashes32, uint64_t node_cap, uint8_t* rlp,
+                       uint64_t rlp_cap, uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len, kh_stats* stats) {
+  API_TRY({
+    *n_nodes = 0;
+    *rlp_len = 0;
+    if (n == 0) {
+      memcpy(root32, EMPTY_TRIE_HASH, 32);
+      if (stats) memset(stats, 0, sizeof(*stats));
+      if (off && node_cap + 1 > 0) off[0] = 0;
+      return KH_OK;
+    }
+    kh_ctx* c = shared_ctx(current_device());
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->dev));
+    Staged S = stage_inputs(c, keys, klen, vals, voff, n, nullptr);
+    BuildArgs A{S.keys, klen, S.vals, S.voff, n, nullptr, 1, 0, flags, true};
+    BuildOut O;
+    run_build(c, A, O, stats);
+    copy_root(O, 0, root32);
+    // emission
+    Topo& T = c->T;
+    uint64_t B = c->last_B;
+    uint64_t Q = T.m + 2 * B;
+    c->ws3.ensure(carve_size({Q * 4, Q * 8, Q * 8 + 64}));
+    Carver c3{(char*)c->ws3.p, 0, c->ws3.cap};
+    uint32_t* flag = c3.take<uint32_t>(Q);
+    uint64_t* bytes = c3.take<uint64_t>(Q);
+    char* sscr = c3.take<char>(scan_scratch_bytes(Q, 8));
+    (void)sscr;
+    hipStream_t st = c->st;
+    hipLaunchKernelGGL(k_emit_sizes, GRID(Q, BS), dim3(BS), 0, st, T, B, flag, bytes);
+    LAUNCH_CHECK();
+    // totals: reuse the build's counter block
+    uint64_t* totb = (uint64_t*)(T.ctr + CTR_E0);
+    uint32_t* totn = (uint32_t*)(T.ctr + CTR_E1);
+    HIPCHK(hipMemsetAsync(T.ctr + CTR_E0, 0, 16, st));
+    // scan scratch: ws1's scan scratch may be too small for Q; use a dedicated buffer
+    c->out_emit.ensure(scan_scratch_bytes(Q, 8) + 256);
+    scan_exclusive<uint64_t>(bytes, bytes, Q, totb, c->out_emit.p, st);
+    scan_exclusive<uint32_t>(flag, flag, Q, totn, c->out_emit.p, st);
+    HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_E0, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    uint64_t tb = c->h_pinned[0];
+    uint64_t tn = (uint32_t)c->h_pinned[1];
+    *n_nodes = tn;
+    *rlp_len = tb;
+    if (tn > node_cap || tb > rlp_cap || !hashes32 || !rlp || !off) return set_err(KH_ENOSPC, "output too small");
+    // device output: hashes | rlp | off
+    DevBuf outb;
+    outb.ensure(tn * 32 + tb + (tn + 1) * 8 + 1024);
+    uint8_t* oh = (uint8_t*)outb.p;
+    uint8_t* orlp = oh + ((tn * 32 + 255) & ~255ULL);
+    uint64_t* ooff = (uint64_t*)(orlp + ((tb + 255) & ~255ULL));
+    // re-derive flags (scan overwrote them with positions; emission re-tests each node)
+    hipLaunchKernelGGL(k_emit_copy, GRID(Q, BS), dim3(BS), 0, st, T, B, (const uint32_t*)flag,
+                       (const uint64_t*)bytes, oh, orlp, ooff);
+    LAUNCH_CHECK();
+    HIPCHK(hipMemcpyAsync(hashes32, oh, tn * 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(rlp, orlp, tb, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(off, ooff, tn * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    off[tn] = tb;
+    outb.release();
+  })
+}
+
+int kh_dev_trie_build(kh_ctx* c, const uint8_t* d_keys, uint32_t klen, const uint8_t* d_vals, const uint64_t* d_voff,
+                      uint64_t n, const uint32_t* d_seg, uint64_t nseg, uint32_t depth0, uint32_t flags,
+                      uint8_t* h_hash32, uint32_t* h_enc_len, uint8_t* h_inline32, kh_stats* stats) {
+  if (!c) return set_err(KH_EINVAL, "null context");
+  API_TRY({
+    HIPCHK(hipSetDevice(c->dev));
+    BuildArgs A{d_keys, klen, d_vals, d_voff, n, d_seg, d_seg ? nseg : 1, depth0, flags, false};
+    BuildOut O;
+    run_build(c, A, O, stats);
+    uint64_t nres = O.res_len.size();
+    if (h_hash32) memcpy(h_hash32, O.res_hash.data(), nres * 32);
+    if (h_enc_len) memcpy(h_enc_len, O.res_len.data(), nres * 4);
+    if (h_inline32) memcpy(h_inline32, O.res_inl.data(), nres * 32);
+  })
+}
+
+int kh_fold_root16(const uint8_t* hash32x16, const uint32_t* enc_len16, const uint8_t* inline32x16,
+                   uint8_t root32[32]) {
+  API_TRY({
+    uint64_t refs[64];
+    uint32_t lens[16];
+    int nonempty = 0;
+    for (int i = 0; i < 16; ++i) {
+      uint32_t L = enc_len16[i];
+      if (L == 0) {
+        lens[i] = 0;
+        memset(refs + 4 * i, 0, 32);
+        continue;
+      }
+      ++nonempty;
+      if (L >= 32) {
+        lens[i] = 32;
+        memcpy(refs + 4 * i, hash32x16 + 32 * i, 32);
+      } else {
+        if (!inline32x16) throw KhError{KH_EINVAL, "inline reference without inline bytes"};
+        lens[i] = L;
+        memcpy(refs + 4 * i, inline32x16 + 32 * i, 32);
+      }
+    }
+    if (nonempty < 2) throw KhError{KH_EINVAL, "fewer than 2 occupied top nibbles: root is not a branch"};
+    alignas(8) uint8_t enc[640];
+    uint32_t L = encode_branch16(refs, lens, enc);
+    uint64_t h[4];
+    kec256_msg<true>(enc, L, h);  // host-side Keccak (same code as the device path)
+    memcpy(root32, h, 32);
+  })
+}
+
+int kh_dev_synth_accounts(kh_ctx* c, uint32_t cfg, uint64_t first, uint64_t n, uint8_t* d_addr, uint8_t* d_vals,
+                          uint64_t* d_voff) {
+  if (!c) return set_err(KH_EINVAL, "null context");
+  API_TRY({
+    HIPCHK(hipSetDevice(c->dev));
+    if (n == 0) {
+      HIPCHK(hipMemsetAsync(d_voff, 0, 8, c->st));
+      return KH_OK;
+    }
+    hipStream_t st = c->st;
+    hipLaunchKernelGGL(k_synth_len, GRID(n + 1, BS), dim3(BS), 0, st, cfg, first, n, d_voff);
+    LAUNCH_CHECK();
+    c->out_emit.ensure(scan_scratch_bytes(n + 1, 8) + 256);
+    scan_exclusive<uint64_t>(d_voff, d_voff, n + 1, (uint64_t*)nullptr, c->out_emit.p, st);
+    hipLaunchKernelGGL(k_synth_write, GRID(n, BS), dim3(BS), 0, st, cfg, first, n, (const uint64_t*)d_voff, d_addr,
+                       d_vals);
+    LAUNCH_CHECK();
+    HIPCHK(hipStreamSynchronize(st));
+  })
+}
+
+}  // extern "C"

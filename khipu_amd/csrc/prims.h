@@ -1,0 +1,247 @@
+// Device primitives for the state-root pipeline: wave reductions, exclusive scan,
+// and a stable LSD radix sort of (uint64 key, uint32 value) pairs.
+//
+// Radix sort: 8-bit digits, one (histogram, scan, scatter) triple per pass.  A
+// tile is 256 threads x 16 items = 4096 keys; each 64-lane wave owns a
+// contiguous 1024-key slice of the tile and ranks its keys with a ballot-based
+// wave-level multisplit (8 ballots give the mask of lanes holding the same
+// digit), so the scatter is stable without an LDS sort.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace khst {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  uint32_t lane = __lane_id();
+  return lane == 0 ? 0ULL : (~0ULL >> (64 - lane));
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// add v (per lane) into *dst with one atomic per wave
+__device__ __forceinline__ void wave_atomic_add(unsigned long long* dst, unsigned long long v) {
+  v = wave_sum(v);
+  if (__lane_id() == 0 && v) atomicAdd(dst, v);
+}
+
+// ---------------------------------------------------------------------------
+// Exclusive scan (T = uint32_t or uint64_t).  256 threads x 8 items per tile.
+// ---------------------------------------------------------------------------
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ITEMS = 8;
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+
+template <typename T>
+__device__ __forceinline__ T block_exclusive_scan(T v, T* lds_waves, T* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  T x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds_waves[w] = x;
+  __syncthreads();
+  T wbase = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_THREADS / 64; ++i) {
+    T s = lds_waves[i];
+    if (i < w) wbase += s;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return wbase + x - v;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const T* in, T* out, uint64_t n, T* tile_sums) {
+  __shared__ T lw[SCAN_THREADS / 64];
+  uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+  T v[SCAN_ITEMS];
+  T s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; ++i) {
+    v[i] = (base + i < n) ? in[base + i] : (T)0;
+    s += v[i];
+  }
+  T tot;
+  T ex = block_exclusive_scan<T>(s, lw, &tot);
+#pragma unroll
+  for (int i = 0; i < SCAN_ITEMS; ++i) {
+    if (base + i < n) out[base + i] = ex;
+    ex += v[i];
+  }
+  if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_add(T* out, uint64_t n, const T* tile_off) {
+  uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+  T add = tile_off[blockIdx.x];
+  for (int i = threadIdx.x; i < SCAN_TILE; i += SCAN_THREADS)
+    if (base + i < n) out[base + i] += add;
+}
+
+template <typename T>
+__global__ void k_scan_total(const T* in_last, const T* out_last, T* total) {
+  *total = *in_last + *out_last;
+}
+
+// Scratch needed by scan_exclusive for n elements (bytes).
+inline size_t scan_scratch_bytes(uint64_t n, size_t elem) {
+  size_t b = 0;
+  while (n > 1) {
+    n = (n + SCAN_TILE - 1) / SCAN_TILE;
+    b += ((n + 1) * elem + 63) / 64 * 64 + 64;
+  }
+  return b + 128;
+}
+
+// out[i] = sum_{j<i} in[i]; in == out allowed.  If total != nullptr, *total (device)
+// receives the sum of all n inputs.  scratch: scan_scratch_bytes(n) bytes.
+template <typename T>
+void scan_exclusive(const T* in, T* out, uint64_t n, T* total, void* scratch, hipStream_t st) {
+  if (n == 0) {
+    if (total) (void)hipMemsetAsync(total, 0, sizeof(T), st);
+    return;
+  }
+  uint64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  // keep the last input element before it may be overwritten (in == out)
+  T* sums = (T*)scratch;
+  T* last_in = sums + tiles;  // one slot after the tile sums
+  (void)hipMemcpyAsync(last_in, in + (n - 1), sizeof(T), hipMemcpyDeviceToDevice, st);
+  hipLaunchKernelGGL(k_scan_tiles<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, in, out, n, sums);
+  if (tiles > 1) {
+    char* next = (char*)scratch + (((tiles + 1) * sizeof(T) + 63) / 64) * 64 + 64;
+    scan_exclusive<T>(sums, sums, tiles, (T*)nullptr, next, st);
+    hipLaunchKernelGGL(k_scan_add<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, out, n, (const T*)sums);
+  }
+  if (total) hipLaunchKernelGGL(k_scan_total<T>, dim3(1), dim3(1), 0, st, (const T*)last_in, (const T*)(out + n - 1), total);
+}
+
+// ---------------------------------------------------------------------------
+// Radix sort of (uint64 key, uint32 val) pairs on key bits [lo_bit, hi_bit).
+// ---------------------------------------------------------------------------
+constexpr int RS_THREADS = 256;
+constexpr int RS_ITEMS = 16;
+constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096
+constexpr int RS_WAVES = RS_THREADS / 64;
+constexpr int RS_WSLICE = RS_TILE / RS_WAVES;   // 1024 keys per wave
+
+__global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const uint64_t* keys, uint64_t n, int shift, uint32_t* counts,
+                                                        uint32_t ntiles) {
+  __shared__ uint32_t h[RS_WAVES][256];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
+  __syncthreads();
+  uint64_t base = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * RS_WSLICE;
+#pragma unroll 4
+  for (int it = 0; it < RS_WSLICE / 64; ++it) {
+    uint64_t i = base + (uint64_t)it * 64 + lane;
+    if (i < n) atomicAdd(&h[w][(keys[i] >> shift) & 0xFF], 1u);
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < 256; d += RS_THREADS) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < RS_WAVES; ++q) s += h[q][d];
+    counts[(uint64_t)d * ntiles + blockIdx.x] = s;
+  }
+}
+
+__global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const uint64_t* keys, const uint32_t* vals, uint64_t* okeys,
+                                                           uint32_t* ovals, uint64_t n, int shift,
+                                                           const uint32_t* offs, uint32_t ntiles) {
+  __shared__ uint32_t wc[RS_WAVES][256];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&wc[0][0])[i] = 0;
+  __syncthreads();
+  uint64_t base = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * RS_WSLICE;
+  uint64_t k[RS_ITEMS];
+  uint32_t v[RS_ITEMS];
+  uint32_t r[RS_ITEMS];
+  const uint64_t lt = lanemask_lt();
+#pragma unroll
+  for (int it = 0; it < RS_ITEMS; ++it) {
+    uint64_t i = base + (uint64_t)it * 64 + lane;
+    bool valid = i < n;
+    k[it] = valid ? keys[i] : 0;
+    v[it] = valid ? vals[i] : 0;
+    uint32_t d = (uint32_t)(k[it] >> shift) & 0xFF;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      bool bit = (d >> b) & 1;
+      uint64_t bb = __ballot(bit);
+      peers &= bit ? bb : ~bb;
+    }
+    uint32_t cnt = valid ? wc[w][d] : 0;
+    uint32_t below = (uint32_t)__popcll(peers & lt);
+    r[it] = cnt + below;
+    // the lowest lane of each peer group bumps the wave's digit counter
+    if (valid && below == 0) wc[w][d] = cnt + (uint32_t)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < 256; d += RS_THREADS) {
+    uint32_t run = offs[(uint64_t)d * ntiles + blockIdx.x];
+#pragma unroll
+    for (int q = 0; q < RS_WAVES; ++q) {
+      uint32_t t = wc[q][d];
+      wc[q][d] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < RS_ITEMS; ++it) {
+    uint64_t i = base + (uint64_t)it * 64 + lane;
+    if (i < n) {
+      uint32_t d = (uint32_t)(k[it] >> shift) & 0xFF;
+      uint32_t pos = wc[w][d] + r[it];
+      okeys[pos] = k[it];
+      ovals[pos] = v[it];
+    }
+  }
+}
+
+inline size_t radix_scratch_bytes(uint64_t n) {
+  uint64_t tiles = (n + RS_TILE - 1) / RS_TILE;
+  uint64_t c = tiles * 256;
+  return c * sizeof(uint32_t) + 256 + scan_scratch_bytes(c, sizeof(uint32_t));
+}
+
+// Sorts (k0, v0) on bits [lo_bit, hi_bit) (multiples of 8), using (k1, v1) as
+// ping-pong buffers.  Returns true if the result ended in (k1, v1).
+// n must be < 2^32.
+inline bool radix_sort_pairs(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, uint64_t n, int lo_bit,
+                             int hi_bit, void* scratch, hipStream_t st) {
+  if (n <= 1) return false;
+  uint32_t tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+  uint32_t* counts = (uint32_t*)scratch;
+  void* scan_ws = (char*)scratch + (((uint64_t)tiles * 256 * sizeof(uint32_t) + 255) / 256) * 256;
+  bool flip = false;
+  for (int sh = lo_bit; sh < hi_bit; sh += 8) {
+    uint64_t* ik = flip ? k1 : k0;
+    uint32_t* iv = flip ? v1 : v0;
+    uint64_t* ok = flip ? k0 : k1;
+    uint32_t* ov = flip ? v0 : v1;
+    hipLaunchKernelGGL(k_rs_hist, dim3(tiles), dim3(RS_THREADS), 0, st, (const uint64_t*)ik, n, sh, counts, tiles);
+    scan_exclusive<uint32_t>(counts, counts, (uint64_t)tiles * 256, (uint32_t*)nullptr, scan_ws, st);
+    hipLaunchKernelGGL(k_rs_scatter, dim3(tiles), dim3(RS_THREADS), 0, st, (const uint64_t*)ik, (const uint32_t*)iv, ok,
+                       ov, n, sh, (const uint32_t*)counts, tiles);
+    flip = !flip;
+  }
+  return flip;
+}
+
+}  // namespace khst

@@ -1,0 +1,621 @@
+// Per-element operations of the batch state-root pipeline.  Each function is the
+// body of one GPU thread (kernels in khst.hip call them with their global thread
+// index); they are __host__ __device__ so tests/emu can replay the exact same
+// code on the CPU against the oracle.
+//
+// Trie shape from sorted keys (no pointer chasing).  Sorted distinct keys
+// K_0 < ... < K_{m-1}; boundary b (between K_b and K_{b+1}) carries
+//   u[b] = LCP_nibbles(K_b, K_{b+1}) + 1, or 0 at a segment break.
+// A branch node is a maximal run of boundaries with equal u and only larger u
+// between them (its "group"); its depth is u-1, its children are the key
+// ranges the group's boundaries separate, so a branch with k children has k-1
+// boundaries.  The group's leftmost boundary (rep) is the one whose previous
+// smaller-or-equal boundary (PSE) is strictly smaller.  A node spanning keys
+// [s, e] hangs under the group of the larger of u[s-1], u[e] (its parent), at
+// child ordinal ord[s-1]+1 or ord[e].  An extension sits between a branch at
+// depth d and its parent at depth pd when d > pd+1 (nibbles pd+1 .. d-1); a
+// leaf's path is nibbles pd+1 .. 63.  This reproduces exactly the canonical
+// trie that khipu's sequential put/fix builds (MerklePatriciaTrie.scala:157-281,
+// 430-477): branches only where keys diverge, extensions only above branches.
+//
+// Node encodings (trie/Node.scala:21-44, rlp/RLP.scala:116-169,
+// trie/HexPrefix.scala:11-21): leaf = [HP(path, leaf), value],
+// extension = [HP(shared, ext), ref], branch = [ref_0 .. ref_15, ""]; a child
+// is referenced by its kec256 when its encoding is >= 32 B, else embedded
+// verbatim (Node.scala:114, 128-131, 158-163, 188-190).
+#pragma once
+#include "keccak.h"
+
+namespace khst {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+// ---- key helpers (keys: 4 little-endian u64 words = the 32 key bytes in order)
+struct Key4 {
+  uint64_t w0, w1, w2, w3;
+};
+KH_HD Key4 load_key(const uint64_t* k, uint64_t i) {
+  const uint64_t* p = k + 4 * i;
+  return Key4{p[0], p[1], p[2], p[3]};
+}
+KH_HD uint64_t key_word(const Key4& k, int j) { return j == 0 ? k.w0 : j == 1 ? k.w1 : j == 2 ? k.w2 : k.w3; }
+KH_HD uint32_t key_byte(const Key4& k, int j) { return (uint32_t)(key_word(k, j >> 3) >> (8 * (j & 7))) & 0xFF; }
+KH_HD uint32_t key_nibble(const Key4& k, int i) {
+  uint32_t b = key_byte(k, i >> 1);
+  return (i & 1) ? (b & 0xF) : (b >> 4);
+}
+KH_HD uint64_t bswap64(uint64_t x) {
+#ifdef __HIPCC__
+  return __builtin_bswap64(x);
+#else
+  return __builtin_bswap64(x);
+#endif
+}
+KH_HD int clz64(uint64_t x) { return x ? __builtin_clzll(x) : 64; }
+
+// Number of equal leading nibbles of two keys (64 if equal).
+KH_HD int lcp_nibbles(const Key4& a, const Key4& b) {
+  uint64_t x;
+  if ((x = a.w0 ^ b.w0)) return clz64(bswap64(x)) >> 2;
+  if ((x = a.w1 ^ b.w1)) return 16 + (clz64(bswap64(x)) >> 2);
+  if ((x = a.w2 ^ b.w2)) return 32 + (clz64(bswap64(x)) >> 2);
+  if ((x = a.w3 ^ b.w3)) return 48 + (clz64(bswap64(x)) >> 2);
+  return 64;
+}
+
+// ---- RLP length helpers (RLP.scala:157-169)
+KH_HD uint32_t be_nbytes(uint64_t v) {
+  uint32_t n = 0;
+  while (v) {
+    ++n;
+    v >>= 8;
+  }
+  return n;
+}
+KH_HD uint32_t rlp_hdr_len(uint64_t payload) { return payload < 56 ? 1 : 1 + be_nbytes(payload); }
+// encoded length of an RLP string of len bytes whose first byte is b0
+KH_HD uint64_t rlp_str_len(uint64_t len, uint32_t b0) {
+  if (len == 1 && b0 < 0x80) return 1;
+  return rlp_hdr_len(len) + len;
+}
+
+// ---- byte writer into an 8-byte-aligned buffer (whole-word stores)
+struct BW {
+  uint64_t* dst;
+  uint64_t acc;
+  uint32_t fill;
+  KH_HD void put(uint64_t w, uint32_t nb) {  // nb in [1, 8]; low nb bytes of w
+    w &= low_bytes_mask(nb);
+    acc |= w << (8 * fill);
+    uint32_t nf = fill + nb;
+    if (nf >= 8) {
+      *dst++ = acc;
+      acc = fill ? (w >> (8 * (8 - fill))) : 0;
+      nf -= 8;
+    }
+    fill = nf;
+  }
+  KH_HD void put1(uint32_t b) { put(b, 1); }
+  KH_HD void flush() {
+    if (fill) *dst = acc;
+  }
+  KH_HD void len_prefix(uint64_t len, uint32_t offset) {  // RLP.encodeLength
+    if (len < 56) {
+      put1((uint32_t)(len + offset));
+    } else {
+      uint32_t nb = be_nbytes(len);
+      put1(nb + offset + 55);
+      for (int i = (int)nb - 1; i >= 0; --i) put1((uint32_t)(len >> (8 * i)) & 0xFF);
+    }
+  }
+  // copy key bytes [from, 32)
+  KH_HD void key_suffix(const Key4& k, uint32_t from) {
+    while (from < 32) {
+      uint32_t nb = 8 - (from & 7);
+      put(key_word(k, from >> 3) >> (8 * (from & 7)), nb);
+      from += nb;
+    }
+  }
+  // copy n bytes from an arbitrary global address
+  KH_HD void bytes(const uint8_t* p, uint64_t n) {
+    while (n) {
+      uint32_t nb = n < 8 ? (uint32_t)n : 8;
+      put(load64u_n(p, nb), nb);
+      p += nb;
+      n -= nb;
+    }
+  }
+  // copy n (< 32) bytes held little-endian in 4 words
+  KH_HD void words(const uint64_t* w, uint32_t n) {
+    for (int j = 0; j < 4 && n; ++j) {
+      uint32_t nb = n < 8 ? n : 8;
+      put(w[j], nb);
+      n -= nb;
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Build state shared by all stages (device pointers; sizes in comments).
+// ---------------------------------------------------------------------------
+struct Topo {
+  uint64_t m;        // distinct keys (leaves)
+  uint32_t depth0;   // 0: whole tries; 1: top-nibble subtries (shard unit)
+  uint32_t segmented;
+  const uint64_t* skey;   // [m*4] sorted keys
+  const uint32_t* sidx;   // [m] input index of sorted key i
+  const uint32_t* sseg;   // [m] segment id (segmented only)
+  const uint8_t* vals;    // input values
+  const uint64_t* voff;   // [n+1]
+  uint8_t* u;             // [m-1] boundary values
+  int32_t* psv;           // [m-1] previous strictly smaller boundary (-1: none)
+  int32_t* nsv;           // [m-1] next strictly smaller boundary (-1: none)
+  int32_t* pse;           // [m-1] previous smaller-or-equal boundary (-1: none)
+  uint32_t* rep;          // [m-1] group representative of b
+  uint8_t* ord;           // [m-1] ordinal of b within its group
+  uint32_t* isrep_bid;    // [m-1] 1 if rep, then (after scan) branch id of rep
+  uint32_t* grp;          // [m-1] branch id of b's group
+  // branches (B <= m-1)
+  uint32_t* br_k;         // child count (then scanned into br_cbase)
+  uint32_t* br_cbase;     // first child record
+  uint8_t* br_depth;
+  uint8_t* br_ext;        // extension nibbles above the branch (0: none)
+  uint32_t* br_parent;    // parent branch id or NONE (top of a segment)
+  uint8_t* br_pord;       // ordinal in parent
+  uint32_t* br_first;     // first key index of the branch's range
+  uint64_t* br_aoff;      // arena bytes reserved, scanned in place into the arena offset
+                          // (the extension follows the branch at +branch_bound(k))
+  uint32_t* br_len;       // encoding length of the branch
+  uint32_t* ex_len;       // encoding length of the extension
+  // leaves
+  uint32_t* lf_parent;
+  uint8_t* lf_pord;
+  int8_t* lf_pd;          // parent depth (depth0-1 for a top leaf)
+  uint64_t* lf_aoff;      // aligned length, scanned in place into the arena offset
+  uint32_t* lf_len;
+  // child references: 32 B each + meta (len | nibble << 8); len 32 = hash
+  uint64_t* cref;
+  uint16_t* cmeta;
+  // per-node hashes for write-back emission (nullable)
+  uint64_t* lf_hash;
+  uint64_t* br_hash;
+  uint64_t* ex_hash;
+  // arena
+  uint8_t* arena;
+  uint64_t br_arena_base;  // branch region starts here
+  // per-result outputs
+  uint64_t* res_hash;  // [nres*4]
+  uint32_t* res_len;   // [nres]
+  uint64_t* res_inl;   // [nres*4]
+  // counters
+  unsigned long long* ctr;  // [0] node hashes, [1] node perms, [2] inline nodes, [3] arena bytes, [4] error
+  uint32_t* depth_hist;     // [64]
+};
+
+enum {
+  CTR_HASHES = 0, CTR_PERMS = 1, CTR_INLINE = 2, CTR_ARENA = 3, CTR_ERR = 4, CTR_EXT = 5,
+  // scratch slots for device-side totals read back by the host
+  CTR_TIE = 8, CTR_M = 9, CTR_B = 10, CTR_BRBYTES = 11, CTR_LFBYTES = 12, CTR_C = 13, CTR_E0 = 14, CTR_E1 = 15,
+  CTR_N = 16
+};
+
+KH_HD uint32_t branch_bound(uint32_t k) { return 24 + 32 * k; }  // >= 3 + 33k + (16-k) + 1, 8-aligned
+constexpr uint32_t EXT_BOUND = 72;                               // >= 2 + 33 + 33
+
+KH_HD uint32_t result_index(const Topo& T, uint64_t first_key) {
+  if (T.segmented) return T.sseg[first_key];
+  if (T.depth0 == 1) return (uint32_t)(T.skey[4 * first_key] & 0xFF) >> 4;
+  return 0;
+}
+
+// ---- stage: boundary values
+KH_HD void op_lcp(const Topo& T, uint64_t b) {
+  Key4 a = load_key(T.skey, b), c = load_key(T.skey, b + 1);
+  int l = lcp_nibbles(a, c);
+  uint8_t v = (uint8_t)(l + 1);
+  if (l < (int)T.depth0 || l > 63) v = 0;  // 64 cannot occur after dedup
+  if (T.segmented && T.sseg[b] != T.sseg[b + 1]) v = 0;
+  T.u[b] = v;
+}
+
+// ---- stage: all nearest smaller values over a 64-ary min pyramid
+struct Pyr {
+  const uint8_t* lv[8];
+  uint64_t sz[8];
+  int nl;
+};
+
+// largest j < b with u[j] < t (strict) or <= t; -1 if none
+KH_HD int64_t ansv_left(const Pyr& P, uint64_t b, uint32_t t, bool strict) {
+  uint64_t pos = b;
+  int L = 0;
+  int64_t found = -1;
+  for (; L < P.nl; ++L) {
+    const uint8_t* a = P.lv[L];
+    uint64_t start = pos & ~(uint64_t)63;
+    for (uint64_t j = pos; j > start;) {
+      --j;
+      uint32_t x = a[j];
+      if (strict ? x < t : x <= t) {
+        found = (int64_t)j;
+        break;
+      }
+    }
+    if (found >= 0) break;
+    pos >>= 6;
+  }
+  if (found < 0) return -1;
+  for (; L > 0; --L) {
+    const uint8_t* a = P.lv[L - 1];
+    uint64_t lo = (uint64_t)found * 64;
+    uint64_t hi = lo + 63 < P.sz[L - 1] - 1 ? lo + 63 : P.sz[L - 1] - 1;
+    for (uint64_t j = hi + 1; j > lo;) {
+      --j;
+      uint32_t x = a[j];
+      if (strict ? x < t : x <= t) {
+        found = (int64_t)j;
+        break;
+      }
+    }
+  }
+  return found;
+}
+
+// smallest j > b with u[j] < t; -1 if none
+KH_HD int64_t ansv_right(const Pyr& P, uint64_t b, uint32_t t) {
+  uint64_t pos = b;
+  int L = 0;
+  int64_t found = -1;
+  for (; L < P.nl; ++L) {
+    const uint8_t* a = P.lv[L];
+    uint64_t end = (pos | 63) + 1;
+    if (end > P.sz[L]) end = P.sz[L];
+    for (uint64_t j = pos + 1; j < end; ++j) {
+      if (a[j] < t) {
+        found = (int64_t)j;
+        break;
+      }
+    }
+    if (found >= 0) break;
+    pos >>= 6;
+  }
+  if (found < 0) return -1;
+  for (; L > 0; --L) {
+    const uint8_t* a = P.lv[L - 1];
+    uint64_t lo = (uint64_t)found * 64;
+    uint64_t hi = lo + 63 < P.sz[L - 1] - 1 ? lo + 63 : P.sz[L - 1] - 1;
+    for (uint64_t j = lo; j <= hi; ++j) {
+      if (a[j] < t) {
+        found = (int64_t)j;
+        break;
+      }
+    }
+  }
+  return found;
+}
+
+KH_HD void op_min64(const uint8_t* in, uint64_t nin, uint8_t* out, uint64_t i) {
+  uint64_t lo = i * 64, hi = lo + 64 < nin ? lo + 64 : nin;
+  uint32_t mn = 255;
+  for (uint64_t j = lo; j < hi; ++j) mn = in[j] < mn ? in[j] : mn;
+  out[i] = (uint8_t)mn;
+}
+
+KH_HD void op_ansv(const Topo& T, const Pyr& P, uint64_t b) {
+  uint32_t t = T.u[b];
+  if (t == 0) {
+    T.psv[b] = T.nsv[b] = T.pse[b] = -1;
+    return;
+  }
+  T.psv[b] = (int32_t)ansv_left(P, b, t, true);
+  T.pse[b] = (int32_t)ansv_left(P, b, t, false);
+  T.nsv[b] = (int32_t)ansv_right(P, b, t);
+}
+
+// ---- stage: group representative and ordinal (walk the PSE chain, <= 14 steps)
+KH_HD void op_chain(const Topo& T, uint64_t b) {
+  uint32_t t = T.u[b];
+  if (t == 0) {
+    T.rep[b] = NONE;
+    T.ord[b] = 0;
+    T.isrep_bid[b] = 0;
+    return;
+  }
+  int64_t j = (int64_t)b;
+  uint32_t o = 0;
+  for (;;) {
+    int32_t q = T.pse[j];
+    if (q < 0 || T.u[q] != t) break;
+    j = q;
+    if (++o > 15) {  // impossible for a 16-ary trie: flag corruption
+      T.ctr[CTR_ERR] = 1;
+      break;
+    }
+  }
+  T.rep[b] = (uint32_t)j;
+  T.ord[b] = (uint8_t)o;
+  T.isrep_bid[b] = (o == 0) ? 1u : 0u;
+}
+
+// after exclusive scan of isrep_bid (which now holds branch ids of reps)
+KH_HD uint32_t op_group(const Topo& T, uint64_t b) {  // returns k candidate (ord+2) or 0
+  if (T.u[b] == 0) {
+    T.grp[b] = NONE;
+    return 0;
+  }
+  uint32_t g = T.isrep_bid[T.rep[b]];
+  T.grp[b] = g;
+  return g;
+}
+
+// parent resolution for a node whose key range is [s, e]: boundaries s-1 and e
+struct Parent {
+  uint32_t bid;  // NONE: top of its segment
+  int32_t pd;    // parent depth (depth0-1 for a top)
+  uint32_t pord;
+};
+KH_HD Parent resolve_parent(const Topo& T, int64_t a, int64_t c) {
+  uint32_t va = a >= 0 ? T.u[a] : 0, vc = c >= 0 ? T.u[c] : 0;
+  Parent P;
+  if (va == 0 && vc == 0) {
+    P.bid = NONE;
+    P.pd = (int32_t)T.depth0 - 1;
+    P.pord = 0;
+  } else if (va >= vc) {
+    P.bid = T.grp[a];
+    P.pd = (int32_t)va - 1;
+    P.pord = T.ord[a] + 1u;
+  } else {
+    P.bid = T.grp[c];
+    P.pd = (int32_t)vc - 1;
+    P.pord = T.ord[c];
+  }
+  return P;
+}
+
+// ---- stage: branch records (thread per boundary; only reps act)
+KH_HD void op_branch_topo(const Topo& T, uint64_t b) {
+  if (T.u[b] == 0 || T.rep[b] != (uint32_t)b) return;
+  uint32_t j = T.isrep_bid[b];
+  uint32_t d = T.u[b] - 1u;
+  int64_t a = T.psv[b], c = T.nsv[b];
+  Parent P = resolve_parent(T, a, c);
+  T.br_depth[j] = (uint8_t)d;
+  T.br_ext[j] = (uint8_t)((int32_t)d - P.pd - 1);
+  T.br_parent[j] = P.bid;
+  T.br_pord[j] = (uint8_t)P.pord;
+  T.br_first[j] = (uint32_t)(a + 1);
+}
+
+KH_HD uint32_t branch_arena_bytes(const Topo& T, uint32_t j) {
+  return branch_bound(T.br_k[j]) + (T.br_ext[j] ? EXT_BOUND : 0);
+}
+
+// ---- leaf geometry
+KH_HD void leaf_value(const Topo& T, uint64_t i, const uint8_t** p, uint64_t* len) {
+  uint32_t src = T.sidx[i];
+  uint64_t o = T.voff[src];
+  *p = T.vals + o;
+  *len = T.voff[src + 1] - o;
+}
+
+// encoded leaf length for path start nibble s
+KH_HD uint64_t leaf_enc_len(uint32_t s, uint64_t vlen, uint32_t v0) {
+  uint32_t p = 64 - s;
+  uint32_t h = p / 2 + 1;                   // HP bytes; first byte 0x2_/0x3_ < 0x80
+  uint64_t hp = h == 1 ? 1 : 1 + h;         // h <= 33 < 56
+  uint64_t payload = hp + rlp_str_len(vlen, v0);
+  return rlp_hdr_len(payload) + payload;
+}
+
+KH_HD void op_leaf_topo(const Topo& T, uint64_t i) {
+  int64_t a = (int64_t)i - 1, c = (i + 1 < T.m) ? (int64_t)i : -1;
+  Parent P = resolve_parent(T, a, c);
+  T.lf_parent[i] = P.bid;
+  T.lf_pord[i] = (uint8_t)P.pord;
+  T.lf_pd[i] = (int8_t)P.pd;
+  const uint8_t* vp;
+  uint64_t vlen;
+  leaf_value(T, i, &vp, &vlen);
+  uint32_t v0 = vlen ? (uint32_t)load64u_n(vp, 1) & 0xFF : 0;
+  uint64_t L = leaf_enc_len((uint32_t)(P.pd + 1), vlen, v0);
+  T.lf_aoff[i] = (L + 7) & ~(uint64_t)7;
+}
+
+// ---- publishing a finished node's reference
+// enc: node encoding in the arena (8-aligned), L: its length, h: its hash (valid
+// when L >= 32 or top).  Writes into the parent's child record or the result.
+KH_HD void publish_ref(const Topo& T, uint32_t parent, uint32_t pord, uint32_t nib, uint64_t first_key,
+                       const uint8_t* enc, uint32_t L, const uint64_t h[4]) {
+  uint64_t w[4];
+  if (L >= 32) {
+    w[0] = h[0];
+    w[1] = h[1];
+    w[2] = h[2];
+    w[3] = h[3];
+  } else {
+    const uint64_t* e = (const uint64_t*)enc;
+    for (int j = 0; j < 4; ++j) {
+      uint32_t base = 8u * (uint32_t)j;
+      w[j] = base < L ? (e[j] & low_bytes_mask(L - base < 8 ? L - base : 8)) : 0;
+    }
+  }
+  if (parent == NONE) {
+    uint32_t r = result_index(T, first_key);
+    for (int j = 0; j < 4; ++j) {
+      T.res_hash[4 * r + j] = h[j];
+      T.res_inl[4 * r + j] = L < 32 ? w[j] : 0;
+    }
+    T.res_len[r] = L;
+  } else {
+    uint64_t slot = (uint64_t)T.br_cbase[parent] + pord;
+    for (int j = 0; j < 4; ++j) T.cref[4 * slot + j] = w[j];
+    T.cmeta[slot] = (uint16_t)((L >= 32 ? 32u : L) | (nib << 8));
+  }
+}
+
+// returns perms spent (0 if the node is inline and not a top)
+KH_HD uint32_t hash_node(const uint8_t* enc, uint32_t L, bool top, uint64_t h[4]) {
+  if (L < 32 && !top) {
+    h[0] = h[1] = h[2] = h[3] = 0;
+    return 0;
+  }
+  kec256_msg<true>(enc, L, h);
+  return perms_for_len(L);
+}
+
+// ---- stage: leaf encode + hash (thread per leaf).  Returns perms spent.
+KH_HD uint32_t op_leaf_emit(const Topo& T, uint64_t i, uint32_t* inl) {
+  Key4 k = load_key(T.skey, i);
+  int32_t pd = T.lf_pd[i];
+  uint32_t s = (uint32_t)(pd + 1);
+  const uint8_t* vp;
+  uint64_t vlen;
+  leaf_value(T, i, &vp, &vlen);
+  uint32_t v0 = vlen ? (uint32_t)load64u_n(vp, 1) & 0xFF : 0;
+  uint32_t p = 64 - s, h = p / 2 + 1;
+  uint32_t hp0 = (p & 1) ? (0x30u | key_nibble(k, (int)s)) : 0x20u;
+  uint64_t hpl = h == 1 ? 1 : 1 + h;
+  uint64_t payload = hpl + rlp_str_len(vlen, v0);
+  uint8_t* enc = T.arena + T.lf_aoff[i];
+  BW w{(uint64_t*)enc, 0, 0};
+  w.len_prefix(payload, 0xC0);
+  if (h > 1) w.put1(0x80 + h);
+  w.put1(hp0);
+  w.key_suffix(k, (s + 1) / 2);
+  if (!(vlen == 1 && v0 < 0x80)) w.len_prefix(vlen, 0x80);
+  w.bytes(vp, vlen);
+  w.flush();
+  uint32_t L = (uint32_t)(rlp_hdr_len(payload) + payload);
+  T.lf_len[i] = L;
+  bool top = T.lf_parent[i] == NONE;
+  uint64_t hh[4];
+  uint32_t perms = hash_node(enc, L, top, hh);
+  if (T.lf_hash)
+    for (int j = 0; j < 4; ++j) T.lf_hash[4 * i + j] = hh[j];
+  uint32_t nib = top ? 0 : key_nibble(k, pd);
+  publish_ref(T, T.lf_parent[i], T.lf_pord[i], nib, i, enc, L, hh);
+  *inl = (L < 32 && !top) ? 1 : 0;
+  return perms;
+}
+
+// ---- stage: branch (+ extension) encode + hash (thread per branch of one level)
+KH_HD uint32_t op_branch_emit(const Topo& T, uint32_t j, uint32_t* inl) {
+  uint32_t k = T.br_k[j];
+  uint64_t cb = T.br_cbase[j];
+  uint32_t payload = 1 + (16 - k);  // terminator "" + empty slots
+  uint32_t mask = 0;
+  for (uint32_t c = 0; c < k; ++c) {
+    uint32_t m = T.cmeta[cb + c];
+    uint32_t len = m & 0xFF;
+    payload += (len == 32) ? 33 : len;
+    mask |= 1u << (m >> 8);
+  }
+  uint8_t* enc = T.arena + T.br_arena_base + T.br_aoff[j];
+  BW w{(uint64_t*)enc, 0, 0};
+  w.len_prefix(payload, 0xC0);
+  uint32_t c = 0;
+  for (uint32_t nib = 0; nib < 16; ++nib) {
+    if ((mask >> nib) & 1) {
+      const uint64_t* r = T.cref + 4 * (cb + c);
+      uint32_t len = T.cmeta[cb + c] & 0xFF;
+      if (len == 32) {
+        w.put1(0xA0);
+        w.put(r[0], 8);
+        w.put(r[1], 8);
+        w.put(r[2], 8);
+        w.put(r[3], 8);
+      } else {
+        w.words(r, len);
+      }
+      ++c;
+    } else {
+      w.put1(0x80);
+    }
+  }
+  w.put1(0x80);
+  w.flush();
+  uint32_t L = rlp_hdr_len(payload) + payload;
+  T.br_len[j] = L;
+  uint32_t ext = T.br_ext[j];
+  uint32_t parent = T.br_parent[j];
+  uint64_t first = T.br_first[j];
+  uint32_t d = T.br_depth[j];
+  int32_t pd = (int32_t)d - (int32_t)ext - 1;
+  bool top = parent == NONE;
+  uint64_t hb[4];
+  uint32_t perms = hash_node(enc, L, top && ext == 0, hb);
+  uint32_t ninl = (L < 32 && !(top && ext == 0)) ? 1 : 0;
+  if (T.br_hash)
+    for (int q = 0; q < 4; ++q) T.br_hash[4 * j + q] = hb[q];
+  Key4 key = load_key(T.skey, first);
+  uint32_t nib = top ? 0 : key_nibble(key, pd);
+  if (ext == 0) {
+    publish_ref(T, parent, T.br_pord[j], nib, first, enc, L, hb);
+    *inl = ninl;
+    return perms;
+  }
+  // extension: [HP(nibbles pd+1 .. d-1, ext), ref(branch)]
+  uint8_t* xenc = enc + branch_bound(k);
+  uint32_t s = (uint32_t)(pd + 1);
+  uint32_t hl = ext / 2 + 1;  // HP bytes
+  uint32_t refl = L >= 32 ? 33 : L;
+  uint32_t hpl = hl == 1 ? 1 : 1 + hl;  // first HP byte 0x00 / 0x1_ < 0x80
+  uint32_t xpay = hpl + refl;
+  BW x{(uint64_t*)xenc, 0, 0};
+  x.len_prefix(xpay, 0xC0);
+  if (hl > 1) x.put1(0x80 + hl);
+  uint32_t q = s;
+  if (ext & 1) {
+    x.put1(0x10u | key_nibble(key, (int)q));
+    ++q;
+  } else {
+    x.put1(0x00);
+  }
+  for (; q < d; q += 2) x.put1((key_nibble(key, (int)q) << 4) | key_nibble(key, (int)q + 1));
+  if (L >= 32) {
+    x.put1(0xA0);
+    x.put(hb[0], 8);
+    x.put(hb[1], 8);
+    x.put(hb[2], 8);
+    x.put(hb[3], 8);
+  } else {
+    x.words((const uint64_t*)enc, L);
+  }
+  x.flush();
+  uint32_t XL = rlp_hdr_len(xpay) + xpay;
+  T.ex_len[j] = XL;
+  uint64_t hx[4];
+  perms += hash_node(xenc, XL, top, hx);
+  if (T.ex_hash)
+    for (int q2 = 0; q2 < 4; ++q2) T.ex_hash[4 * j + q2] = hx[q2];
+  ninl += (XL < 32 && !top) ? 1 : 0;
+  publish_ref(T, parent, T.br_pord[j], nib, first, xenc, XL, hx);
+  *inl = ninl;
+  return perms;
+}
+
+// Root branch over 16 capped references (the host fold of the sharded path).
+// refs: 16 x 4 words, lens: 0 = empty, 32 = hash, else inline length.
+// Writes the encoding into out (>= 600 B, 8-aligned); returns its length.
+KH_HD uint32_t encode_branch16(const uint64_t* refs, const uint32_t* lens, uint8_t* out) {
+  uint32_t payload = 1;
+  for (int i = 0; i < 16; ++i) payload += lens[i] == 0 ? 1 : lens[i] == 32 ? 33 : lens[i];
+  BW w{(uint64_t*)out, 0, 0};
+  w.len_prefix(payload, 0xC0);
+  for (int i = 0; i < 16; ++i) {
+    if (lens[i] == 0) {
+      w.put1(0x80);
+    } else if (lens[i] == 32) {
+      w.put1(0xA0);
+      for (int q = 0; q < 4; ++q) w.put(refs[4 * i + q], 8);
+    } else {
+      w.words(refs + 4 * i, lens[i]);
+    }
+  }
+  w.put1(0x80);
+  w.flush();
+  return rlp_hdr_len(payload) + payload;
+}
+
+}  // namespace khst

@@ -1,0 +1,206 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes wrapper over oracle/liboracle.so, the CPU restatement of khipu's
+Keccak-256 / RLP / hex-prefix / MerklePatriciaTrie (see khipu_oracle.cc for the
+reference file:line each function follows).  Only tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg may import this module, and only as the checker.
+The product path (khipu_amd/, libkhst.so) never imports or calls it.
+"""
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
+                os.path.join(_HERE, "khipu_oracle.cc")):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u8p = ctypes.c_char_p
+        L.or_kec256.argtypes = [u8p, ctypes.c_uint64, ctypes.c_void_p]
+        L.or_keccak256_pad.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint8, ctypes.c_void_p]
+        L.or_last_error.restype = ctypes.c_char_p
+        L.or_perm_count.restype = ctypes.c_uint64
+        for f in ("or_rlp_str", "or_rlp_list"):
+            getattr(L, f).argtypes = [u8p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+            getattr(L, f).restype = ctypes.c_int64
+        L.or_hp_encode.argtypes = [u8p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64]
+        L.or_hp_encode.restype = ctypes.c_int64
+        L.or_trie_new.restype = ctypes.c_void_p
+        L.or_trie_free.argtypes = [ctypes.c_void_p]
+        L.or_trie_put.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint64, u8p, ctypes.c_uint64]
+        L.or_trie_remove.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint64]
+        L.or_trie_get.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+        L.or_trie_get.restype = ctypes.c_int64
+        L.or_trie_root.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.or_trie_persist.argtypes = [ctypes.c_void_p]
+        L.or_trie_reopen.argtypes = [ctypes.c_void_p]
+        L.or_trie_updated_count.argtypes = [ctypes.c_void_p]
+        L.or_trie_updated_count.restype = ctypes.c_uint64
+        L.or_trie_updated_dump.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                           ctypes.c_void_p]
+        L.or_trie_reachable.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                        ctypes.c_uint64, ctypes.c_void_p]
+        L.or_trie_reachable.restype = ctypes.c_int64
+        L.or_seq_root.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+def kec256(data: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().or_kec256(data, len(data), out)
+    return out.raw
+
+
+def keccak256_pad(data: bytes, pad: int) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().or_keccak256_pad(data, len(data), pad, out)
+    return out.raw
+
+
+def _call_buf(fn, data, *extra):
+    cap = 64 + 2 * len(data)
+    out = ctypes.create_string_buffer(cap)
+    n = fn(data, len(data), *extra, out, cap)
+    assert n >= 0
+    return out.raw[:n]
+
+
+def rlp_str(b: bytes) -> bytes:
+    return _call_buf(lib().or_rlp_str, b)
+
+
+def rlp_list(payload: bytes) -> bytes:
+    return _call_buf(lib().or_rlp_list, payload)
+
+
+def hp_encode(nibbles: bytes, is_leaf: bool) -> bytes:
+    return _call_buf(lib().or_hp_encode, nibbles, 1 if is_leaf else 0)
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+class Trie:
+    """khipu-faithful sequential MerklePatriciaTrie (MerklePatriciaTrie.scala:68-558)."""
+
+    def __init__(self):
+        self._t = lib().or_trie_new()
+
+    def __del__(self):
+        if getattr(self, "_t", None):
+            lib().or_trie_free(self._t)
+            self._t = None
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise OracleError(lib().or_last_error().decode())
+
+    def put(self, k: bytes, v: bytes):
+        self._chk(lib().or_trie_put(self._t, k, len(k), v, len(v)))
+        return self
+
+    def remove(self, k: bytes):
+        self._chk(lib().or_trie_remove(self._t, k, len(k)))
+        return self
+
+    def get(self, k: bytes):
+        buf = ctypes.create_string_buffer(4096)
+        n = lib().or_trie_get(self._t, k, len(k), buf, 4096)
+        if n == -2:
+            return None
+        if n < 0:
+            raise OracleError(lib().or_last_error().decode())
+        return buf.raw[:n]
+
+    def root_hash(self) -> bytes:
+        out = ctypes.create_string_buffer(32)
+        lib().or_trie_root(self._t, out)
+        return out.raw
+
+    def persist(self):
+        lib().or_trie_persist(self._t)
+        return self
+
+    def reopen(self):
+        lib().or_trie_reopen(self._t)
+        return self
+
+    def updated(self):
+        """dict hash -> encoding of the Updated log entries (the write-back set)."""
+        n = lib().or_trie_updated_count(self._t)
+        hs = ctypes.create_string_buffer(32 * max(n, 1))
+        cap = 1024 * max(n, 1)
+        enc = ctypes.create_string_buffer(cap)
+        off = (ctypes.c_uint64 * (n + 1))()
+        assert lib().or_trie_updated_dump(self._t, hs, enc, cap, off) == 0
+        return {hs.raw[32 * i:32 * i + 32]: enc.raw[off[i]:off[i + 1]] for i in range(n)}
+
+    def reachable(self):
+        """dict hash -> encoding for every node reachable from the root with encoding >= 32 B, plus the root."""
+        n = lib().or_trie_reachable(self._t, None, 0, None, 0, None)
+        if n < 0:
+            raise OracleError(lib().or_last_error().decode())
+        hs = ctypes.create_string_buffer(32 * max(n, 1))
+        cap = 600 * max(n, 1)
+        enc = ctypes.create_string_buffer(cap)
+        off = (ctypes.c_uint64 * (n + 1))()
+        m = lib().or_trie_reachable(self._t, hs, n, enc, cap, off)
+        assert m == n
+        return {hs.raw[32 * i:32 * i + 32]: enc.raw[off[i]:off[i + 1]] for i in range(n)}
+
+
+def seq_root(keys, vals, dels=None, mode=0) -> bytes:
+    """Sequential root over a batch of puts (and removes where dels[i]) in order.
+
+    mode 0: TrieAccounts.flush pattern (TrieAccounts.scala:22-28), one instance.
+    mode 1: GenesisDataLoader pattern (GenesisDataLoader.scala:139-147).
+    keys: list of equal-length bytes; vals: list of bytes.
+    """
+    import numpy as np
+    n = len(keys)
+    klen = len(keys[0]) if n else 32
+    kb = b"".join(keys)
+    vb = b"".join(vals)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    if n:
+        off[1:] = np.cumsum([len(v) for v in vals])
+    d = None
+    if dels is not None:
+        d = np.asarray(dels, dtype=np.uint8)
+    out = ctypes.create_string_buffer(32)
+    rc = lib().or_seq_root(kb, klen, vb if vb else None, off.ctypes.data,
+                           d.ctypes.data if d is not None else None, n, mode, out)
+    if rc != 0:
+        raise OracleError(lib().or_last_error().decode())
+    return out.raw
+
+
+def seq_root_packed(keys_u8, klen, vals_u8, voff_u64, n, mode=0) -> bytes:
+    """Same as seq_root over numpy buffers (keys n*klen bytes, vals packed with voff[n+1])."""
+    out = ctypes.create_string_buffer(32)
+    rc = lib().or_seq_root(keys_u8.ctypes.data, klen, vals_u8.ctypes.data, voff_u64.ctypes.data, None, n, mode, out)
+    if rc != 0:
+        raise OracleError(lib().or_last_error().decode())
+    return out.raw
+
+
+def perm_count() -> int:
+    return lib().or_perm_count()
+
+
+def perm_reset():
+    lib().or_perm_reset()

@@ -1,0 +1,72 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes wrapper of tests/emu/libkhst_emu.so (host
+replay of the device per-thread code, see khst_emu.cc)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "libkhst_emu.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+        L = ctypes.CDLL(_LIB)
+        vp = ctypes.c_void_p
+        L.emu_build.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, ctypes.c_uint32, vp, vp, vp, vp]
+        L.emu_kec256.argtypes = [vp, ctypes.c_uint64, vp]
+        L.emu_synth.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp]
+        L.emu_fold16.argtypes = [vp, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _buf(b):
+    a = np.frombuffer(b, dtype=np.uint8) if len(b) else np.zeros(1, np.uint8)
+    return np.ascontiguousarray(a)
+
+
+def pack(vals):
+    off = np.zeros(len(vals) + 1, dtype=np.uint64)
+    if vals:
+        off[1:] = np.cumsum([len(v) for v in vals])
+    return _buf(b"".join(vals) + b"\0" * 16), off
+
+
+def build(keys32, vals, seg=None, nseg=1, depth0=0):
+    """Returns (results, stats): results = list of (hash32, enc_len, inline_bytes)."""
+    n = len(keys32)
+    kb = _buf(b"".join(keys32) + b"\0" * 16)
+    vb, off = pack(vals)
+    nres = nseg if seg is not None else (16 if depth0 == 1 else 1)
+    oh = np.zeros(32 * nres, np.uint8)
+    ol = np.zeros(nres, np.uint32)
+    oi = np.zeros(32 * nres, np.uint8)
+    st = np.zeros(8, np.uint64)
+    sg = np.asarray(seg, dtype=np.uint32) if seg is not None else None
+    rc = lib().emu_build(kb.ctypes.data, vb.ctypes.data, off.ctypes.data, n,
+                         sg.ctypes.data if sg is not None else None, nseg, depth0,
+                         oh.ctypes.data, ol.ctypes.data, oi.ctypes.data, st.ctypes.data)
+    assert rc == 0, rc
+    res = [(oh[32 * r:32 * r + 32].tobytes(), int(ol[r]), oi[32 * r:32 * r + int(ol[r])].tobytes() if ol[r] < 32 else b"")
+           for r in range(nres)]
+    return res, st
+
+
+def kec256(b: bytes) -> bytes:
+    out = np.zeros(32, np.uint8)
+    buf = _buf(b + b"\0" * 16)
+    lib().emu_kec256(buf.ctypes.data, len(b), out.ctypes.data)
+    return out.tobytes()
+
+
+def synth(cfg, first, n):
+    addr = np.zeros(20 * n + 16, np.uint8)
+    vals = np.zeros(96 * n + 16, np.uint8)
+    off = np.zeros(n + 1, np.uint64)
+    lib().emu_synth(cfg, first, n, addr.ctypes.data, vals.ctypes.data, off.ctypes.data)
+    return addr[:20 * n].reshape(n, 20), vals[:int(off[n])], off

@@ -1,0 +1,236 @@
+// TEST INFRASTRUCTURE ONLY — host replay of the device pipeline.
+//
+// Compiles khipu_amd/csrc/trie_ops.h (the per-thread bodies of the HIP kernels)
+// with g++ and drives them with plain loops, std::stable_sort in place of the
+// radix sort and std::partial_sum in place of the device scan.  It lets the CPU
+// test suite check the topology / RLP / Keccak logic of the GPU path against the
+// oracle without a GPU.  It is never linked into libkhst.so and the product
+// never calls it; the GPU parity tests (tests/test_gpu_parity.py) exercise the
+// real kernels.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../khipu_amd/csrc/synth.h"
+
+using namespace khst;
+
+extern "C" {
+
+// keys: n*32 (already keccak'd), vals/voff packed; seg nullable.
+// Outputs per result r: hash (32 B), enc length, inline bytes (32 B).
+// stats_out[0..5] = m, B, node hashes, node perms, inline nodes, extensions.
+int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, uint64_t n, const uint32_t* seg,
+              uint64_t nseg, uint32_t depth0, uint8_t* out_hash, uint32_t* out_len, uint8_t* out_inl,
+              uint64_t* stats_out) {
+  const bool segmented = seg != nullptr;
+  const uint64_t nres = segmented ? nseg : (depth0 == 1 ? 16 : 1);
+  std::vector<uint64_t> res_hash(nres * 4, 0), res_inl(nres * 4, 0);
+  std::vector<uint32_t> res_len(nres, 0);
+  if (n == 0) {
+    memset(out_len, 0, nres * 4);
+    return 0;
+  }
+  // sort (stable, by segment then key bytes), keep the last duplicate
+  std::vector<uint32_t> order(n);
+  std::iota(order.begin(), order.end(), 0u);
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+    if (segmented && seg[a] != seg[b]) return seg[a] < seg[b];
+    return memcmp(keys + 32ull * a, keys + 32ull * b, 32) < 0;
+  });
+  std::vector<uint32_t> sidx;
+  for (uint64_t i = 0; i < n; ++i) {
+    bool dup_next = i + 1 < n && memcmp(keys + 32ull * order[i], keys + 32ull * order[i + 1], 32) == 0 &&
+                    (!segmented || seg[order[i]] == seg[order[i + 1]]);
+    if (!dup_next) sidx.push_back(order[i]);
+  }
+  const uint64_t m = sidx.size(), nb = m - 1;
+  std::vector<uint64_t> skey(4 * m);
+  std::vector<uint32_t> sseg(m);
+  for (uint64_t i = 0; i < m; ++i) {
+    memcpy(&skey[4 * i], keys + 32ull * sidx[i], 32);
+    if (segmented) sseg[i] = seg[sidx[i]];
+  }
+  Topo T{};
+  T.m = m;
+  T.depth0 = depth0;
+  T.segmented = segmented;
+  T.skey = skey.data();
+  T.sidx = sidx.data();
+  T.sseg = sseg.data();
+  T.vals = vals;
+  T.voff = voff;
+  const uint64_t nbb = nb + 1;
+  std::vector<uint8_t> u(nbb), ord(nbb), br_depth(nbb), br_ext(nbb), br_pord(nbb), lf_pord(m);
+  std::vector<int32_t> psv(nbb), nsv(nbb), pse(nbb);
+  std::vector<uint32_t> rep(nbb), isrep(nbb), grp(nbb), br_k(nbb, 0), br_cbase(nbb), br_parent(nbb), br_first(nbb),
+      br_len(nbb), ex_len(nbb), lf_parent(m), lf_len(m);
+  std::vector<int8_t> lf_pd(m);
+  std::vector<uint64_t> br_aoff(nbb), lf_aoff(m);
+  std::vector<unsigned long long> ctr(CTR_N, 0);
+  std::vector<uint32_t> hist(64, 0);
+  T.u = u.data();
+  T.psv = psv.data();
+  T.nsv = nsv.data();
+  T.pse = pse.data();
+  T.rep = rep.data();
+  T.ord = ord.data();
+  T.isrep_bid = isrep.data();
+  T.grp = grp.data();
+  T.br_k = br_k.data();
+  T.br_cbase = br_cbase.data();
+  T.br_depth = br_depth.data();
+  T.br_ext = br_ext.data();
+  T.br_parent = br_parent.data();
+  T.br_pord = br_pord.data();
+  T.br_first = br_first.data();
+  T.br_aoff = br_aoff.data();
+  T.br_len = br_len.data();
+  T.ex_len = ex_len.data();
+  T.lf_parent = lf_parent.data();
+  T.lf_pord = lf_pord.data();
+  T.lf_pd = lf_pd.data();
+  T.lf_aoff = lf_aoff.data();
+  T.lf_len = lf_len.data();
+  T.res_hash = res_hash.data();
+  T.res_len = res_len.data();
+  T.res_inl = res_inl.data();
+  T.ctr = ctr.data();
+  T.depth_hist = hist.data();
+  uint64_t B = 0;
+  std::vector<std::vector<uint8_t>> pyr;
+  if (nb > 0) {
+    for (uint64_t b = 0; b < nb; ++b) op_lcp(T, b);
+    Pyr P{};
+    P.lv[0] = T.u;
+    P.sz[0] = nb;
+    P.nl = 1;
+    pyr.reserve(8);
+    while (P.sz[P.nl - 1] > 64) {
+      uint64_t nin = P.sz[P.nl - 1], nout = (nin + 63) / 64;
+      pyr.emplace_back(nout);
+      for (uint64_t i = 0; i < nout; ++i) op_min64(P.lv[P.nl - 1], nin, pyr.back().data(), i);
+      P.lv[P.nl] = pyr.back().data();
+      P.sz[P.nl] = nout;
+      P.nl++;
+    }
+    for (uint64_t b = 0; b < nb; ++b) op_ansv(T, P, b);
+    for (uint64_t b = 0; b < nb; ++b) op_chain(T, b);
+    if (ctr[CTR_ERR]) return -5;
+    uint32_t run = 0;
+    for (uint64_t b = 0; b < nb; ++b) {
+      uint32_t f = isrep[b];
+      isrep[b] = run;
+      run += f;
+    }
+    B = run;
+    for (uint64_t b = 0; b < nb; ++b) {
+      if (u[b] == 0) {
+        grp[b] = NONE;
+        continue;
+      }
+      uint32_t g = isrep[rep[b]];
+      grp[b] = g;
+      br_k[g] = std::max(br_k[g], (uint32_t)ord[b] + 2u);
+    }
+    for (uint64_t b = 0; b < nb; ++b) {
+      op_branch_topo(T, b);
+      if (u[b] != 0 && rep[b] == b) {
+        uint32_t j = isrep[b];
+        hist[br_depth[j]]++;
+        if (br_ext[j]) ctr[CTR_EXT]++;
+      }
+    }
+  }
+  for (uint64_t i = 0; i < m; ++i) op_leaf_topo(T, i);
+  uint64_t C = 0;
+  for (uint64_t j = 0; j < B; ++j) {
+    br_cbase[j] = (uint32_t)C;
+    C += br_k[j];
+  }
+  uint64_t brb = 0;
+  for (uint64_t j = 0; j < B; ++j) {
+    uint64_t a = branch_arena_bytes(T, (uint32_t)j);
+    br_aoff[j] = brb;
+    brb += a;
+  }
+  uint64_t lfb = 0;
+  for (uint64_t i = 0; i < m; ++i) {
+    uint64_t a = lf_aoff[i];
+    lf_aoff[i] = lfb;
+    lfb += a;
+  }
+  std::vector<uint64_t> cref(4 * C + 4), arena((lfb + brb + 64) / 8 + 1);
+  std::vector<uint16_t> cmeta(C + 1);
+  T.cref = cref.data();
+  T.cmeta = cmeta.data();
+  T.arena = (uint8_t*)arena.data();
+  T.br_arena_base = lfb;
+  uint64_t perms = 0, hashes = 0, inl = 0;
+  for (uint64_t i = 0; i < m; ++i) {
+    uint32_t in1 = 0;
+    uint32_t p = op_leaf_emit(T, i, &in1);
+    perms += p;
+    hashes += p ? 1 : 0;
+    inl += in1;
+  }
+  for (int d = 63; d >= 0; --d)
+    for (uint64_t j = 0; j < B; ++j) {
+      if (br_depth[j] != d) continue;
+      uint32_t in1 = 0;
+      perms += op_branch_emit(T, (uint32_t)j, &in1);
+      bool top = br_parent[j] == NONE, ext = br_ext[j] != 0;
+      hashes += (br_len[j] >= 32 || (top && !ext)) ? 1 : 0;
+      if (ext) hashes += (ex_len[j] >= 32 || top) ? 1 : 0;
+      inl += in1;
+    }
+  memcpy(out_hash, res_hash.data(), nres * 32);
+  memcpy(out_len, res_len.data(), nres * 4);
+  memcpy(out_inl, res_inl.data(), nres * 32);
+  if (stats_out) {
+    stats_out[0] = m;
+    stats_out[1] = B;
+    stats_out[2] = hashes;
+    stats_out[3] = perms;
+    stats_out[4] = inl;
+    stats_out[5] = ctr[CTR_EXT];
+  }
+  return 0;
+}
+
+void emu_kec256(const uint8_t* p, uint64_t len, uint8_t* out) {
+  uint64_t h[4];
+  kec256_msg<false>(p, (uint32_t)len, h);
+  memcpy(out, h, 32);
+}
+
+void emu_synth(uint32_t cfg, uint64_t first, uint64_t n, uint8_t* addr, uint8_t* vals, uint64_t* voff) {
+  uint64_t o = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    SynthAcct a = synth_acct(cfg, first + i);
+    synth_addr_write(a, addr + 20 * i);
+    voff[i] = o;
+    o += synth_body_write(a, first + i, vals + o);
+  }
+  voff[n] = o;
+}
+
+int emu_fold16(const uint8_t* hash32x16, const uint32_t* len16, const uint8_t* inl32x16, uint8_t* out) {
+  uint64_t refs[64];
+  uint32_t lens[16];
+  for (int i = 0; i < 16; ++i) {
+    uint32_t L = len16[i];
+    lens[i] = L == 0 ? 0 : (L >= 32 ? 32 : L);
+    memcpy(refs + 4 * i, (L >= 32 ? hash32x16 : inl32x16) + 32 * i, 32);
+  }
+  alignas(8) uint8_t enc[640];
+  uint32_t L = encode_branch16(refs, lens, enc);
+  uint64_t h[4];
+  kec256_msg<true>(enc, L, h);
+  memcpy(out, h, 32);
+  return 0;
+}
+
+}  // extern "C"
