@@ -15,21 +15,38 @@
 #ifdef __HIPCC__
 #include <hip/hip_runtime.h>
 #define KH_HD __host__ __device__ __forceinline__
-#define KH_CONST __constant__ static const
 #else  // host-only compilation of the same code (tests/emu)
 #define KH_HD inline
-#define KH_CONST static const
 #endif
 
 namespace khst {
 
-KH_CONST uint64_t kRC[24] = {
+// Round constants.  The device reads its own __constant__ copy; host code (the
+// root fold, tests/emu) reads a plain array: the host shadow of a __constant__
+// variable is not the initialised table.
+#ifdef __HIPCC__
+__constant__ static const uint64_t kRC_dev[24] = {
     0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,
     0x000000000000808BULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
     0x000000000000008AULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000AULL,
     0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
     0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
     0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+#endif
+static const uint64_t kRC_host[24] = {
+    0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,
+    0x000000000000808BULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+    0x000000000000008AULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000AULL,
+    0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+    0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
+    0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+KH_HD uint64_t round_constant(int r) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return kRC_dev[r];
+#else
+  return kRC_host[r];
+#endif
+}
 
 KH_HD uint64_t rotl64(uint64_t x, int n) { return (x << n) | (x >> (64 - n)); }
 
@@ -107,7 +124,7 @@ KH_HD void keccakf(KState& s) {
            a14 = s.a14, a15 = s.a15, a16 = s.a16, a17 = s.a17, a18 = s.a18, a19 = s.a19, a20 = s.a20,
            a21 = s.a21, a22 = s.a22, a23 = s.a23, a24 = s.a24;
 #pragma unroll 2
-  for (int r = 0; r < 24; ++r) KH_ROUND(kRC[r]);
+  for (int r = 0; r < 24; ++r) KH_ROUND(round_constant(r));
   s.a00 = a00; s.a01 = a01; s.a02 = a02; s.a03 = a03; s.a04 = a04; s.a05 = a05; s.a06 = a06;
   s.a07 = a07; s.a08 = a08; s.a09 = a09; s.a10 = a10; s.a11 = a11; s.a12 = a12; s.a13 = a13;
   s.a14 = a14; s.a15 = a15; s.a16 = a16; s.a17 = a17; s.a18 = a18; s.a19 = a19; s.a20 = a20;

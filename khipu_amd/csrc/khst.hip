@@ -177,14 +177,23 @@ __global__ void __launch_bounds__(BS) k_group(Topo T, uint64_t nb) {
 }
 
 __global__ void __launch_bounds__(BS) k_branch_topo(Topo T, uint64_t nb) {
+  // depth histogram: LDS atomics per block, one global atomic per (block, depth)
+  __shared__ uint32_t h[64];
+  if (threadIdx.x < 64) h[threadIdx.x] = 0;
+  __syncthreads();
   uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (b >= nb) return;
-  op_branch_topo(T, b);
-  if (T.u[b] != 0 && T.rep[b] == (uint32_t)b) {
-    uint32_t j = T.isrep_bid[b];
-    atomicAdd(&T.depth_hist[T.br_depth[j]], 1u);
-    if (T.br_ext[j]) atomicAdd(&T.ctr[CTR_EXT], 1ULL);
+  unsigned long long ext = 0;
+  if (b < nb) {
+    op_branch_topo(T, b);
+    if (T.u[b] != 0 && T.rep[b] == (uint32_t)b) {
+      uint32_t j = T.isrep_bid[b];
+      atomicAdd(&h[T.br_depth[j]], 1u);
+      ext = T.br_ext[j] ? 1 : 0;
+    }
   }
+  wave_atomic_add(&T.ctr[CTR_EXT], ext);
+  __syncthreads();
+  if (threadIdx.x < 64 && h[threadIdx.x]) atomicAdd(&T.depth_hist[threadIdx.x], h[threadIdx.x]);
 }
 
 __global__ void __launch_bounds__(BS) k_leaf_topo(Topo T) {
@@ -199,11 +208,21 @@ __global__ void __launch_bounds__(BS) k_branch_alen(Topo T, uint64_t B) {
 
 __global__ void __launch_bounds__(BS) k_level_scatter(Topo T, uint64_t B, const uint32_t* level_base,
                                                       uint32_t* cursor, uint32_t* order) {
+  // bucket branch ids by depth: rank inside the block via LDS atomics, one global
+  // atomic per (block, depth) for the block's base in that depth's bucket
+  __shared__ uint32_t cnt[64], base[64];
+  if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+  __syncthreads();
   uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (j >= B) return;
-  uint32_t d = T.br_depth[j];
-  uint32_t p = atomicAdd(&cursor[d], 1u);
-  order[level_base[d] + p] = (uint32_t)j;
+  uint32_t d = 0, r = 0;
+  if (j < B) {
+    d = T.br_depth[j];
+    r = atomicAdd(&cnt[d], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 64 && cnt[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]);
+  __syncthreads();
+  if (j < B) order[level_base[d] + base[d] + r] = (uint32_t)j;
 }
 
 __global__ void __launch_bounds__(BS) k_leaf_emit(Topo T) {
@@ -1025,10 +1044,10 @@ int kh_fold_root16(const uint8_t* hash32x16, const uint32_t* enc_len16, const ui
       }
     }
     if (nonempty < 2) throw KhError{KH_EINVAL, "fewer than 2 occupied top nibbles: root is not a branch"};
-    alignas(8) uint8_t enc[640];
-    uint32_t L = encode_branch16(refs, lens, enc);
+    uint64_t enc[80];  // uint64_t storage: BW stores and Keccak loads are both 8-byte words
+    uint32_t L = encode_branch16(refs, lens, (uint8_t*)enc);
     uint64_t h[4];
-    kec256_msg<true>(enc, L, h);  // host-side Keccak (same code as the device path)
+    kec256_msg<true>((const uint8_t*)enc, L, h);  // host-side Keccak (same code as the device path)
     memcpy(root32, h, 32);
   })
 }

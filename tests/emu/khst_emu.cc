@@ -225,10 +225,10 @@ int emu_fold16(const uint8_t* hash32x16, const uint32_t* len16, const uint8_t* i
     lens[i] = L == 0 ? 0 : (L >= 32 ? 32 : L);
     memcpy(refs + 4 * i, (L >= 32 ? hash32x16 : inl32x16) + 32 * i, 32);
   }
-  alignas(8) uint8_t enc[640];
-  uint32_t L = encode_branch16(refs, lens, enc);
+  uint64_t enc[80];
+  uint32_t L = encode_branch16(refs, lens, (uint8_t*)enc);
   uint64_t h[4];
-  kec256_msg<true>(enc, L, h);
+  kec256_msg<true>((const uint8_t*)enc, L, h);
   memcpy(out, h, 32);
   return 0;
 }
