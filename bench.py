@@ -44,6 +44,7 @@ def parse():
     p.add_argument("--cfg", type=int, default=5, help="synthetic config id (SURVEY §8d seed)")
     p.add_argument("--cpu-sample", type=int, default=150_000, help="accounts in the CPU-baseline sample")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--sharded", action="store_true", help="force the nibble-sharded RCCL path (any N)")
     return p.parse_args()
 
 
@@ -138,7 +139,7 @@ def single(args):
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 or args.gpus > 1:
+    if world > 1 or args.gpus > 1 or args.sharded:
         from khipu_amd import sharded
         sharded.bench_main(args)
     else:

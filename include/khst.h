@@ -135,6 +135,18 @@ int kh_dev_trie_build(kh_ctx* ctx, const uint8_t* d_keys, uint32_t klen, const u
 int kh_fold_root16(const uint8_t* hash32x16, const uint32_t* enc_len16, const uint8_t* inline32x16,
                    uint8_t root32[32]);
 
+/* kec256 of n keys of klen bytes (device buffers; the KH_HASH_KEYS step on its own). */
+int kh_dev_hash_keys(kh_ctx* ctx, const uint8_t* d_keys, uint32_t klen, uint64_t n, uint8_t* d_out32);
+
+/* Multi-GPU routing: stable partition of n records (32-byte trie keys + packed values) by
+ * owner = top nibble * nparts / 16 (nparts <= 16).  Writes the records grouped by owner
+ * (input order kept inside a group, so later puts still win after the exchange):
+ * d_out_keys (n*32 B), d_out_vals (total value bytes), d_out_vlen (n value lengths);
+ * h_counts[p] / h_bytes[p] = records / value bytes for owner p (host). */
+int kh_dev_partition(kh_ctx* ctx, const uint8_t* d_keys32, const uint8_t* d_vals, const uint64_t* d_voff,
+                     uint64_t n, uint32_t nparts, uint8_t* d_out_keys, uint8_t* d_out_vals, uint64_t* d_out_vlen,
+                     uint64_t* h_counts, uint64_t* h_bytes);
+
 /* Synthetic account generator (pinned in khipu_amd/csrc/synth.h): writes
  * accounts [first, first+n) of config `cfg` — 20-byte addresses (d_addr, n*20 B) and RLP
  * account bodies packed at d_vals with d_voff[n+1] (offsets relative to d_vals; d_vals

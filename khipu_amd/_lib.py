@@ -23,7 +23,8 @@ KH_HASH_KEYS = 0x1
 EXPORTS = (
     "kh_last_error", "kh_version", "kh_device_count", "kh_kec256_batch", "kh_trie_root",
     "kh_trie_roots_segmented", "kh_trie_root_nodes", "kh_ctx_create", "kh_ctx_destroy", "kh_ctx_set_stream",
-    "kh_dev_kec256_batch", "kh_dev_trie_build", "kh_fold_root16", "kh_dev_synth_accounts",
+    "kh_dev_kec256_batch", "kh_dev_trie_build", "kh_fold_root16", "kh_dev_synth_accounts", "kh_dev_hash_keys",
+    "kh_dev_partition",
 )
 
 
@@ -95,6 +96,8 @@ def lib():
     L.kh_dev_trie_build.argtypes = [vp, vp, u32, vp, vp, u64, vp, u64, u32, u32, vp, vp, vp, vp]
     L.kh_fold_root16.argtypes = [vp, vp, vp, vp]
     L.kh_dev_synth_accounts.argtypes = [vp, u32, u64, u64, vp, vp, vp]
+    L.kh_dev_hash_keys.argtypes = [vp, vp, u32, u64, vp]
+    L.kh_dev_partition.argtypes = [vp, vp, vp, vp, u64, u32, vp, vp, vp, vp, vp]
     for name in EXPORTS:
         fn = getattr(L, name)
         if fn.restype is ctypes.c_int or name not in ("kh_last_error", "kh_version"):

@@ -226,11 +226,12 @@ __global__ void __launch_bounds__(BS) k_level_scatter(Topo T, uint64_t B, const 
 }
 
 __global__ void __launch_bounds__(BS) k_leaf_emit(Topo T) {
+  __shared__ uint64_t lds[STREAM_WORDS * BS];
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (i < T.m) {
     uint32_t in1 = 0;
-    perms = op_leaf_emit(T, i, &in1);
+    perms = op_leaf_emit<BS>(T, i, lds + threadIdx.x, &in1);
     hashes = perms ? 1 : 0;
     inl = in1;
   }
@@ -240,12 +241,13 @@ __global__ void __launch_bounds__(BS) k_leaf_emit(Topo T) {
 }
 
 __global__ void __launch_bounds__(BS) k_branch_emit(Topo T, const uint32_t* order, uint64_t cnt) {
+  __shared__ uint64_t lds[STREAM_WORDS * BS];
   uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (t < cnt) {
     uint32_t j = order[t];
     uint32_t in1 = 0;
-    perms = op_branch_emit(T, j, &in1);
+    perms = op_branch_emit<BS>(T, j, lds + threadIdx.x, &in1);
     // hashes: branch hashed if len >= 32 or top; extension likewise
     uint32_t L = T.br_len[j];
     bool top = T.br_parent[j] == NONE;
@@ -314,6 +316,51 @@ __global__ void __launch_bounds__(BS) k_emit_copy(Topo T, uint64_t B, const uint
   uint8_t* dst = out_rlp + boff[q];
   for (uint32_t b = 0; b < len; ++b) dst[b] = src[b];
   out_off[p] = boff[q];
+}
+
+
+// ---- multi-GPU routing: stable partition of records by top-nibble owner
+__device__ __forceinline__ uint32_t nibble_owner(uint64_t w0, uint32_t nparts) {
+  return (((uint32_t)(w0 & 0xFF) >> 4) * nparts) >> 4;
+}
+__global__ void __launch_bounds__(BS) k_owner_key(const uint64_t* K, uint64_t n, uint32_t nparts, uint64_t* ck,
+                                                  uint32_t* idx) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  ck[i] = nibble_owner(K[4 * i], nparts);
+  idx[i] = (uint32_t)i;
+}
+__global__ void __launch_bounds__(BS) k_part_len(const uint32_t* idx, const uint64_t* voff, uint64_t n,
+                                                 uint64_t* vlen) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s = idx[i];
+  vlen[i] = voff[s + 1] - voff[s];
+}
+__global__ void __launch_bounds__(BS) k_part_copy(const uint64_t* K, const uint8_t* vals, const uint64_t* voff,
+                                                  const uint32_t* idx, const uint64_t* ooff, uint64_t n,
+                                                  const uint64_t* ck, uint64_t* okeys, uint8_t* ovals,
+                                                  unsigned long long* cnt, unsigned long long* bytes) {
+  __shared__ unsigned long long c[16], b[16];
+  if (threadIdx.x < 16) c[threadIdx.x] = b[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < n) {
+    uint32_t s = idx[i];
+    for (int j = 0; j < 4; ++j) okeys[4 * i + j] = K[4 * (uint64_t)s + j];
+    uint64_t o = voff[s], L = voff[s + 1] - o;
+    const uint8_t* src = vals + o;
+    uint8_t* dst = ovals + ooff[i];
+    for (uint64_t q = 0; q < L; ++q) dst[q] = src[q];
+    uint32_t p = (uint32_t)ck[i];
+    atomicAdd(&c[p], 1ULL);
+    atomicAdd(&b[p], (unsigned long long)L);
+  }
+  __syncthreads();
+  if (threadIdx.x < 16 && c[threadIdx.x]) {
+    atomicAdd(&cnt[threadIdx.x], c[threadIdx.x]);
+    atomicAdd(&bytes[threadIdx.x], b[threadIdx.x]);
+  }
 }
 
 __global__ void __launch_bounds__(BS) k_synth_len(uint32_t cfg, uint64_t first, uint64_t n, uint64_t* voff) {
@@ -654,23 +701,25 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   HIPCHK(hipMemsetAsync(ctr + CTR_BRBYTES, 0, 24, st));
   if (B > 0) {
     scan_exclusive<uint32_t>(T.br_k, T.br_cbase, B, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
-    hipLaunchKernelGGL(k_branch_alen, GRID(B, BS), dim3(BS), 0, st, T, B);
-    LAUNCH_CHECK();
-    scan_exclusive<uint64_t>(T.br_aoff, T.br_aoff, B, (uint64_t*)(ctr + CTR_BRBYTES), scan_scratch, st);
+    if (A.emit) {  // node arena only for write-back emission
+      hipLaunchKernelGGL(k_branch_alen, GRID(B, BS), dim3(BS), 0, st, T, B);
+      LAUNCH_CHECK();
+      scan_exclusive<uint64_t>(T.br_aoff, T.br_aoff, B, (uint64_t*)(ctr + CTR_BRBYTES), scan_scratch, st);
+    }
   }
-  scan_exclusive<uint64_t>(T.lf_aoff, T.lf_aoff, m, (uint64_t*)(ctr + CTR_LFBYTES), scan_scratch, st);
+  if (A.emit) scan_exclusive<uint64_t>(T.lf_aoff, T.lf_aoff, m, (uint64_t*)(ctr + CTR_LFBYTES), scan_scratch, st);
   HIPCHK(hipMemcpyAsync(c->h_pinned, ctr + CTR_BRBYTES, 24, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const uint64_t br_bytes = c->h_pinned[0];
   const uint64_t lf_bytes = c->h_pinned[1];
   const uint64_t C = (uint32_t)c->h_pinned[2];
 
-  // ---- phase-2 workspace: child records + node arena
-  c->ws2.ensure(carve_size({C * 32, C * 2, lf_bytes + br_bytes + 64}));
+  // ---- phase-2 workspace: child records (+ node arena for emission)
+  c->ws2.ensure(carve_size({C * 32, C * 2, A.emit ? lf_bytes + br_bytes + 64 : 0}));
   Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
   T.cref = cv2.take<uint64_t>(C * 4);
   T.cmeta = cv2.take<uint16_t>(C);
-  T.arena = cv2.take<uint8_t>(lf_bytes + br_bytes + 64);
+  T.arena = A.emit ? cv2.take<uint8_t>(lf_bytes + br_bytes + 64) : nullptr;
   T.br_arena_base = lf_bytes;
 
   // level order: branches grouped by depth, deepest first
@@ -723,7 +772,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     stats->n_inline = c->h_pinned[CTR_INLINE];
     stats->n_extensions = c->h_pinned[CTR_EXT];
     stats->n_key_perms = (A.flags & KH_HASH_KEYS) ? n * (uint64_t)(A.klen / 136 + 1) : 0;
-    stats->arena_bytes = lf_bytes + br_bytes;
+    stats->arena_bytes = A.emit ? lf_bytes + br_bytes : 0;
     stats->n_levels = levels;
     stats->full_sort = ties ? 1 : 0;
     stats->t_keys_ms = ev_ms(c->ev[0], c->ev[1]);
@@ -1049,6 +1098,64 @@ int kh_fold_root16(const uint8_t* hash32x16, const uint32_t* enc_len16, const ui
     uint64_t h[4];
     kec256_msg<true>((const uint8_t*)enc, L, h);  // host-side Keccak (same code as the device path)
     memcpy(root32, h, 32);
+  })
+}
+
+int kh_dev_partition(kh_ctx* c, const uint8_t* d_keys32, const uint8_t* d_vals, const uint64_t* d_voff, uint64_t n,
+                     uint32_t nparts, uint8_t* d_out_keys, uint8_t* d_out_vals, uint64_t* d_out_vlen,
+                     uint64_t* h_counts, uint64_t* h_bytes) {
+  if (!c) return set_err(KH_EINVAL, "null context");
+  API_TRY({
+    if (nparts < 1 || nparts > 16) throw KhError{KH_EINVAL, "nparts must be in [1, 16]"};
+    HIPCHK(hipSetDevice(c->dev));
+    memset(h_counts, 0, nparts * 8);
+    memset(h_bytes, 0, nparts * 8);
+    if (n == 0) return KH_OK;
+    if (n >= (1ULL << 31)) throw KhError{KH_EINVAL, "n must be < 2^31 per device"};
+    hipStream_t st = c->st;
+    c->ws3.ensure(carve_size({n * 8, n * 8, n * 4, n * 4, n * 8, radix_scratch_bytes(n), scan_scratch_bytes(n, 8),
+                              256}));
+    Carver cv{(char*)c->ws3.p, 0, c->ws3.cap};
+    uint64_t* ck0 = cv.take<uint64_t>(n);
+    uint64_t* ck1 = cv.take<uint64_t>(n);
+    uint32_t* i0 = cv.take<uint32_t>(n);
+    uint32_t* i1 = cv.take<uint32_t>(n);
+    uint64_t* ooff = cv.take<uint64_t>(n);
+    void* rs = cv.take<char>(radix_scratch_bytes(n));
+    void* sc = cv.take<char>(scan_scratch_bytes(n, 8));
+    unsigned long long* tot = cv.take<unsigned long long>(32);
+    const uint64_t* K = (const uint64_t*)d_keys32;
+    hipLaunchKernelGGL(k_owner_key, GRID(n, BS), dim3(BS), 0, st, K, n, nparts, ck0, i0);
+    LAUNCH_CHECK();
+    if (radix_sort_pairs(ck0, i0, ck1, i1, n, 0, 8, rs, st)) {  // one stable pass
+      std::swap(ck0, ck1);
+      std::swap(i0, i1);
+    }
+    hipLaunchKernelGGL(k_part_len, GRID(n, BS), dim3(BS), 0, st, (const uint32_t*)i0, d_voff, n, d_out_vlen);
+    LAUNCH_CHECK();
+    scan_exclusive<uint64_t>(d_out_vlen, ooff, n, (uint64_t*)nullptr, sc, st);
+    HIPCHK(hipMemsetAsync(tot, 0, 256, st));
+    hipLaunchKernelGGL(k_part_copy, GRID(n, BS), dim3(BS), 0, st, K, d_vals, d_voff, (const uint32_t*)i0,
+                       (const uint64_t*)ooff, n, (const uint64_t*)ck0, (uint64_t*)d_out_keys, d_out_vals, tot,
+                       tot + 16);
+    LAUNCH_CHECK();
+    HIPCHK(hipMemcpyAsync(c->h_pinned, tot, 256, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (uint32_t p = 0; p < nparts; ++p) {
+      h_counts[p] = c->h_pinned[p];
+      h_bytes[p] = c->h_pinned[16 + p];
+    }
+  })
+}
+
+int kh_dev_hash_keys(kh_ctx* c, const uint8_t* d_keys, uint32_t klen, uint64_t n, uint8_t* d_out32) {
+  if (!c) return set_err(KH_EINVAL, "null context");
+  API_TRY({
+    HIPCHK(hipSetDevice(c->dev));
+    if (n) {
+      hipLaunchKernelGGL(k_hash_keys, GRID(n, BS), dim3(BS), 0, c->st, d_keys, klen, n, (uint64_t*)d_out32);
+      LAUNCH_CHECK();
+    }
   })
 }
 

@@ -1,0 +1,212 @@
+"""Multi-GPU state root: the trie sharded by top key nibble over one process per GPU.
+
+SURVEY §8(e).  Rank r of N owns top nibbles q with q * N // 16 == r (2 per GPU at
+N = 8).  One step, from (address, account body) records spread over the ranks:
+
+  1. kec256 of the local addresses                         (libkhst, k_hash_keys)
+  2. stable partition of the local records by owner rank   (libkhst, kh_dev_partition)
+  3. exchange: all-to-all of counts, keys, value lengths and value bytes
+     (torch.distributed = RCCL over xGMI; rank-major order keeps "later put wins")
+  4. build the owned subtries from nibble 1 down           (libkhst, depth0 = 1)
+  5. all-gather the 16 capped references, fold into the root branch on the host
+     (kh_fold_root16; MerklePatriciaTrie.scala:169 — the root is always hashed)
+
+If fewer than two top nibbles are occupied the root is not a branch: the owner of
+the single occupied nibble holds every key and builds the whole trie (depth0 = 0).
+
+The communication code is backend-agnostic: GpuBackend runs libkhst on the
+rank's GPU with NCCL(RCCL) tensors; tests use a CPU backend with gloo.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REF_BYTES = 32 + 32 + 8  # hash | inline encoding | length (LE u64)
+
+
+def owner_of_nibble(q, world):
+    return (q * world) >> 4
+
+
+class GpuBackend:
+    """libkhst.so on the rank's GPU; tensors live in HBM (torch is the allocator)."""
+
+    def __init__(self, device):
+        from .device import Ctx
+        self.ctx = Ctx(device)
+        self.device = torch.device(f"cuda:{device}")
+        self.last_stats = None
+
+    def hash_keys(self, addr, n, klen=20):
+        from ._lib import check, lib
+        from .device import _ptr
+        out = torch.empty(n * 32 + 64, dtype=torch.uint8, device=self.device)
+        torch.cuda.synchronize(self.device)
+        check(lib().kh_dev_hash_keys(self.ctx.h, _ptr(addr), klen, n, _ptr(out)))
+        return out
+
+    def partition(self, keys32, vals, voff, n, nparts):
+        from ._lib import check, lib
+        from .device import _ptr
+        pk = torch.empty(n * 32 + 64, dtype=torch.uint8, device=self.device)
+        pv = torch.empty(vals.numel() + 64, dtype=torch.uint8, device=self.device)
+        pl = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        cnt = np.zeros(16, np.uint64)
+        nb = np.zeros(16, np.uint64)
+        torch.cuda.synchronize(self.device)
+        check(lib().kh_dev_partition(self.ctx.h, _ptr(keys32), _ptr(vals), _ptr(voff), n, nparts, _ptr(pk), _ptr(pv),
+                                     _ptr(pl), cnt.ctypes.data, nb.ctypes.data))
+        return pk, pv, pl, cnt[:nparts].astype(np.int64), nb[:nparts].astype(np.int64)
+
+    def build(self, keys32, vals, voff, n, depth0):
+        hh, ll, ii, st = self.ctx.build(keys32, 32, vals, voff, n, depth0=depth0)
+        self.last_stats = st
+        return hh, ll, ii
+
+    def fold(self, hh, ll, ii):
+        from .device import fold_root16
+        return fold_root16(hh, ll, ii)
+
+    def empty(self, nbytes, dtype=torch.uint8):
+        return torch.empty(nbytes, dtype=dtype, device=self.device)
+
+    def sync(self):
+        torch.cuda.synchronize(self.device)
+
+
+def exchange(be, pkeys, pvals, pvlen, counts, nbytes):
+    """All-to-all of the partitioned records.  Returns (keys32, vals, voff, m) of the
+    records this rank owns, ordered by source rank then source order."""
+    world = dist.get_world_size()
+    dev = pkeys.device
+    sc = torch.tensor(np.concatenate([counts, nbytes]).astype(np.int64), device=dev)
+    meta = torch.empty(2 * world, dtype=torch.int64, device=dev)
+    # counts and byte counts in one all-to-all: rank p receives (counts[p], nbytes[p]) pairs
+    send = torch.stack([sc[:world], sc[world:]], 1).reshape(-1).contiguous()
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, [2] * world, [2] * world)
+    rr = recv.cpu().numpy().reshape(world, 2)
+    rc, rb = rr[:, 0].astype(np.int64), rr[:, 1].astype(np.int64)
+    del meta
+    m = int(rc.sum())
+    tot_b = int(rb.sum())
+    cl, bl = [int(x) for x in counts], [int(x) for x in nbytes]
+    n_send = sum(cl)
+    b_send = sum(bl)
+    rkeys = be.empty(m * 32 + 64)
+    dist.all_to_all_single(rkeys[:m * 32], pkeys[:n_send * 32], [int(c) * 32 for c in rc], [c * 32 for c in cl])
+    rlen = be.empty(max(m, 1), torch.int64)
+    dist.all_to_all_single(rlen[:m], pvlen[:n_send], [int(c) for c in rc], cl)
+    rvals = be.empty(tot_b + 64)
+    dist.all_to_all_single(rvals[:tot_b], pvals[:b_send], [int(b) for b in rb], bl)
+    voff = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+    if m:
+        torch.cumsum(rlen[:m], 0, out=voff[1:])
+    return rkeys, rvals, voff, m
+
+
+def gather_refs(be, hh, ll, ii):
+    """All-gather the 16 subtrie references of every rank; each nibble's reference is
+    taken from its owner."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    buf = np.zeros((16, REF_BYTES), np.uint8)
+    buf[:, :32] = hh
+    buf[:, 32:64] = ii
+    buf[:, 64:72] = ll.astype(np.uint64).view(np.uint8).reshape(16, 8)
+    mine = torch.from_numpy(buf.reshape(-1).copy()).to(be.empty(1).device)
+    allb = be.empty(world * 16 * REF_BYTES)
+    dist.all_gather_into_tensor(allb, mine)
+    a = allb.cpu().numpy().reshape(world, 16, REF_BYTES)
+    H = np.zeros((16, 32), np.uint8)
+    I = np.zeros((16, 32), np.uint8)
+    L = np.zeros(16, np.uint32)
+    for q in range(16):
+        o = owner_of_nibble(q, world)
+        H[q] = a[o, q, :32]
+        I[q] = a[o, q, 32:64]
+        L[q] = int(a[o, q, 64:72].view(np.uint64)[0])
+    return H, L, I
+
+
+def sharded_root(be, addr, vals, voff, n, klen=20, keys_prehashed=False):
+    """One sharded state-root step.  Every rank calls it with its slice of the records;
+    every rank returns the root (bytes) and the number of node hashes it computed."""
+    world = dist.get_world_size()
+    keys32 = addr if keys_prehashed else be.hash_keys(addr, n, klen)
+    pk, pv, pl, cnt, nb = be.partition(keys32, vals, voff, n, world)
+    rk, rv, ro, m = exchange(be, pk, pv, pl, cnt, nb)
+    hh, ll, ii = be.build(rk, rv, ro, m, depth0=1)
+    H, L, I = gather_refs(be, hh, ll, ii)
+    occupied = [q for q in range(16) if L[q] > 0]
+    if len(occupied) >= 2:
+        return be.fold(H, L, I)
+    # root is not a branch: the owner of the one occupied nibble has every key
+    from .trie import EMPTY_TRIE_HASH
+    if not occupied:
+        return EMPTY_TRIE_HASH
+    o = owner_of_nibble(occupied[0], world)
+    root = torch.zeros(32, dtype=torch.uint8, device=be.empty(1).device)
+    if dist.get_rank() == o:
+        h, _, _ = be.build(rk, rv, ro, m, depth0=0)
+        root.copy_(torch.from_numpy(h[0].copy()))
+    dist.broadcast(root, o)
+    return root.cpu().numpy().tobytes()
+
+
+def bench_main(args):
+    """bench.py --gpus N under torch.distributed.run: strong scaling of the fixed
+    args.accounts trie over WORLD_SIZE GPUs (one rank per GPU, RCCL)."""
+    import json
+    import os
+    import time
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    be = GpuBackend(local)
+    n_total = args.accounts
+    first = n_total * rank // world
+    n = n_total * (rank + 1) // world - first
+    addr, vals, voff = be.ctx.synth_accounts(args.cfg, first, n)
+    be.sync()
+
+    def step():
+        return sharded_root(be, addr, vals, voff, n)
+
+    for _ in range(args.warmup):
+        step()
+    be.sync()
+    dist.barrier()
+    be.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        root = step()
+    be.sync()
+    dist.barrier()
+    be.sync()
+    dt = torch.tensor([(time.perf_counter() - t0) / args.steps], dtype=torch.float64, device=f"cuda:{local}")
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    st = be.last_stats
+    hashes = torch.tensor([st.n_node_hashes, st.n_leaves, st.n_branches], dtype=torch.int64, device=f"cuda:{local}")
+    dist.all_reduce(hashes)
+    dt = float(dt.item())
+    node_hashes = int(hashes[0].item()) + 1  # + the folded root branch
+    if rank == 0:
+        out = {
+            "metric": "node-hashes/sec (full state root, 100M-account trie)",
+            "value": node_hashes / dt, "unit": "node-hashes/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (counter-based accounts, SURVEY §8d, csrc/synth.h)",
+            "config": {"workload": f"{n_total} synthetic accounts -> state root, sharded by top key nibble",
+                       "accounts": n_total, "parallelism": f"nibble-shard x{world} (RCCL all-to-all + gather)"},
+            "state_root": root.hex(),
+            "topology": {"n_leaves": int(hashes[1].item()), "n_branches": int(hashes[2].item()) + 1,
+                         "n_node_hashes": node_hashes},
+            "roofline": None,
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -171,7 +171,8 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
   uint64_t perms = 0, hashes = 0, inl = 0;
   for (uint64_t i = 0; i < m; ++i) {
     uint32_t in1 = 0;
-    uint32_t p = op_leaf_emit(T, i, &in1);
+    uint64_t lb[STREAM_WORDS];
+    uint32_t p = op_leaf_emit<1>(T, i, lb, &in1);
     perms += p;
     hashes += p ? 1 : 0;
     inl += in1;
@@ -180,7 +181,8 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
     for (uint64_t j = 0; j < B; ++j) {
       if (br_depth[j] != d) continue;
       uint32_t in1 = 0;
-      perms += op_branch_emit(T, (uint32_t)j, &in1);
+      uint64_t lb[STREAM_WORDS];
+      perms += op_branch_emit<1>(T, (uint32_t)j, lb, &in1);
       bool top = br_parent[j] == NONE, ext = br_ext[j] != 0;
       hashes += (br_len[j] >= 32 || (top && !ext)) ? 1 : 0;
       if (ext) hashes += (ex_len[j] >= 32 || top) ? 1 : 0;

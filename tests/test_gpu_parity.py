@@ -179,3 +179,27 @@ def test_full_size_1m(khst, oracle):
     rv = vb[gather]
     rk = np.ascontiguousarray(keys.reshape(n, 32)[::-1]).reshape(-1)
     assert khst.trie_root(rk, (rv, new_off), klen=32) == root
+
+
+def test_sharded_driver_rccl_world1(khst, oracle):
+    """khipu_amd/sharded.py over RCCL (world size 1 on this box; the routing logic at
+    world sizes 2 and 3 is covered with gloo in tests/test_multigpu.py)."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    from khipu_amd import sharded
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda:0"))
+    try:
+        be = sharded.GpuBackend(0)
+        n = 50_000
+        addr, vals, voff = be.ctx.synth_accounts(7, 0, n)
+        root = sharded.sharded_root(be, addr, vals, voff, n)
+        hh, _, _, _ = be.ctx.build(addr, 20, vals, voff, n, hash_keys=True)
+        assert root == hh[0].tobytes()
+    finally:
+        dist.destroy_process_group()
