@@ -1,15 +1,17 @@
 // Keccak-256 (legacy 0x01 padding) for gfx950: one message per lane, the 25-lane
-// Keccak-f[1600] state held in 50 VGPRs.
+// Keccak-f[1600] state held in 50 VGPRs (25 lanes x 32-bit halves).
 //
 // Reference behaviour: khipu-base/.../crypto/hash/KeccakCore.scala:39-52 (RC),
 // :103-531 (processBlock), :534-562 (doPadding: 0x01 .. 0x80, 0x81 if one byte
 // is left), :570 (rate 136 B); DigestEngine.scala:102-166 (a block is absorbed
 // as soon as 136 bytes are buffered, so L bytes cost floor(L/136)+1 permutations).
 //
-// gfx950 has no 64-bit logic or rotate instructions: the compiler splits each
-// 64-bit op into two 32-bit halves (v_xor3_b32 for theta's 5-way XOR,
-// v_alignbit_b32 pairs for rho, v_bfi_b32 + v_xor_b32 for chi).  All state
-// indices are compile-time constants so the state never leaves registers.
+// gfx950's VALU is 32-bit: the permutation is written on 32-bit halves so that
+// theta's 5-way XOR becomes v_xor3_b32 pairs, every 64-bit rotate two
+// v_alignbit_b32 (funnel shifts); gfx950's v_bitop3_b32 does theta's 3-way XOR and
+// chi's a ^ (~b & c) in one instruction each: 190 VALU ops per round against the
+// canonical 240 of SURVEY §8d (which assumes v_xor3 + v_bfi + v_xor).  Every state index is a
+// compile-time constant after unrolling, so the state never leaves registers.
 #pragma once
 #include <stdint.h>
 #ifdef __HIPCC__
@@ -48,110 +50,95 @@ KH_HD uint64_t round_constant(int r) {
 #endif
 }
 
-KH_HD uint64_t rotl64(uint64_t x, int n) { return (x << n) | (x >> (64 - n)); }
+// 32-bit funnel shift: low 32 bits of ({a, b} >> s), s in [1, 31] -> v_alignbit_b32.
+KH_HD uint32_t funnel(uint32_t a, uint32_t b, uint32_t s) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_alignbit(a, b, s);
+#else
+  return (uint32_t)((((uint64_t)a << 32) | b) >> s);
+#endif
+}
 
-// chi term a ^ (~b & c), written as a bit-select so it lowers to v_bfi_b32.
-KH_HD uint64_t chi(uint64_t a, uint64_t b, uint64_t c) { return a ^ (~b & c); }
+// a ^ b ^ c in one instruction (v_bitop3_b32, truth table 0x96) on gfx950.
+KH_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
 
-// One Keccak-f[1600] round on named state words (rho/pi folded into renaming).
-#define KH_ROUND(rc)                                                                   \
-  {                                                                                    \
-    uint64_t C0 = a00 ^ a05 ^ a10 ^ a15 ^ a20, C1 = a01 ^ a06 ^ a11 ^ a16 ^ a21;       \
-    uint64_t C2 = a02 ^ a07 ^ a12 ^ a17 ^ a22, C3 = a03 ^ a08 ^ a13 ^ a18 ^ a23;       \
-    uint64_t C4 = a04 ^ a09 ^ a14 ^ a19 ^ a24;                                         \
-    uint64_t D0 = C4 ^ rotl64(C1, 1), D1 = C0 ^ rotl64(C2, 1), D2 = C1 ^ rotl64(C3, 1); \
-    uint64_t D3 = C2 ^ rotl64(C4, 1), D4 = C3 ^ rotl64(C0, 1);                         \
-    uint64_t b00 = a00 ^ D0;                                                           \
-    uint64_t b10 = rotl64(a01 ^ D1, 1);                                                \
-    uint64_t b20 = rotl64(a02 ^ D2, 62);                                               \
-    uint64_t b05 = rotl64(a03 ^ D3, 28);                                               \
-    uint64_t b15 = rotl64(a04 ^ D4, 27);                                               \
-    uint64_t b16 = rotl64(a05 ^ D0, 36);                                               \
-    uint64_t b01 = rotl64(a06 ^ D1, 44);                                               \
-    uint64_t b11 = rotl64(a07 ^ D2, 6);                                                \
-    uint64_t b21 = rotl64(a08 ^ D3, 55);                                               \
-    uint64_t b06 = rotl64(a09 ^ D4, 20);                                               \
-    uint64_t b07 = rotl64(a10 ^ D0, 3);                                                \
-    uint64_t b17 = rotl64(a11 ^ D1, 10);                                               \
-    uint64_t b02 = rotl64(a12 ^ D2, 43);                                               \
-    uint64_t b12 = rotl64(a13 ^ D3, 25);                                               \
-    uint64_t b22 = rotl64(a14 ^ D4, 39);                                               \
-    uint64_t b23 = rotl64(a15 ^ D0, 41);                                               \
-    uint64_t b08 = rotl64(a16 ^ D1, 45);                                               \
-    uint64_t b18 = rotl64(a17 ^ D2, 15);                                               \
-    uint64_t b03 = rotl64(a18 ^ D3, 21);                                               \
-    uint64_t b13 = rotl64(a19 ^ D4, 8);                                                \
-    uint64_t b14 = rotl64(a20 ^ D0, 18);                                               \
-    uint64_t b24 = rotl64(a21 ^ D1, 2);                                                \
-    uint64_t b09 = rotl64(a22 ^ D2, 61);                                               \
-    uint64_t b19 = rotl64(a23 ^ D3, 56);                                               \
-    uint64_t b04 = rotl64(a24 ^ D4, 14);                                               \
-    a00 = chi(b00, b01, b02) ^ (rc);                                                   \
-    a01 = chi(b01, b02, b03);                                                          \
-    a02 = chi(b02, b03, b04);                                                          \
-    a03 = chi(b03, b04, b00);                                                          \
-    a04 = chi(b04, b00, b01);                                                          \
-    a05 = chi(b05, b06, b07);                                                          \
-    a06 = chi(b06, b07, b08);                                                          \
-    a07 = chi(b07, b08, b09);                                                          \
-    a08 = chi(b08, b09, b05);                                                          \
-    a09 = chi(b09, b05, b06);                                                          \
-    a10 = chi(b10, b11, b12);                                                          \
-    a11 = chi(b11, b12, b13);                                                          \
-    a12 = chi(b12, b13, b14);                                                          \
-    a13 = chi(b13, b14, b10);                                                          \
-    a14 = chi(b14, b10, b11);                                                          \
-    a15 = chi(b15, b16, b17);                                                          \
-    a16 = chi(b16, b17, b18);                                                          \
-    a17 = chi(b17, b18, b19);                                                          \
-    a18 = chi(b18, b19, b15);                                                          \
-    a19 = chi(b19, b15, b16);                                                          \
-    a20 = chi(b20, b21, b22);                                                          \
-    a21 = chi(b21, b22, b23);                                                          \
-    a22 = chi(b22, b23, b24);                                                          \
-    a23 = chi(b23, b24, b20);                                                          \
-    a24 = chi(b24, b20, b21);                                                          \
+// rotate-left of the 64-bit lane (h:l) by n (a compile-time constant after unrolling)
+KH_HD void rotl_hl(uint32_t& l, uint32_t& h, int n) {
+  uint32_t nl, nh;
+  if (n == 0) return;
+  if (n < 32) {
+    nh = funnel(h, l, 32 - n);
+    nl = funnel(l, h, 32 - n);
+  } else if (n == 32) {
+    nh = l;
+    nl = h;
+  } else {
+    nh = funnel(l, h, 64 - n);
+    nl = funnel(h, l, 64 - n);
   }
+  l = nl;
+  h = nh;
+}
 
 struct KState {
-  uint64_t a00, a01, a02, a03, a04, a05, a06, a07, a08, a09, a10, a11, a12, a13, a14, a15, a16, a17, a18,
-      a19, a20, a21, a22, a23, a24;
+  uint32_t lo[25], hi[25];
 };
 
-KH_HD void keccakf(KState& s) {
-  uint64_t a00 = s.a00, a01 = s.a01, a02 = s.a02, a03 = s.a03, a04 = s.a04, a05 = s.a05, a06 = s.a06,
-           a07 = s.a07, a08 = s.a08, a09 = s.a09, a10 = s.a10, a11 = s.a11, a12 = s.a12, a13 = s.a13,
-           a14 = s.a14, a15 = s.a15, a16 = s.a16, a17 = s.a17, a18 = s.a18, a19 = s.a19, a20 = s.a20,
-           a21 = s.a21, a22 = s.a22, a23 = s.a23, a24 = s.a24;
-#pragma unroll 2
-  for (int r = 0; r < 24; ++r) KH_ROUND(round_constant(r));
-  s.a00 = a00; s.a01 = a01; s.a02 = a02; s.a03 = a03; s.a04 = a04; s.a05 = a05; s.a06 = a06;
-  s.a07 = a07; s.a08 = a08; s.a09 = a09; s.a10 = a10; s.a11 = a11; s.a12 = a12; s.a13 = a13;
-  s.a14 = a14; s.a15 = a15; s.a16 = a16; s.a17 = a17; s.a18 = a18; s.a19 = a19; s.a20 = a20;
-  s.a21 = a21; s.a22 = a22; s.a23 = a23; s.a24 = a24;
+KH_HD void keccak_round(KState& S, uint64_t rc) {
+  constexpr int ROT[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+  uint32_t CL[5], CH[5], DL[5], DH[5], BL[25], BH[25];
+#pragma unroll
+  for (int x = 0; x < 5; ++x) {  // theta: column parities
+    CL[x] = xor3(xor3(S.lo[x], S.lo[x + 5], S.lo[x + 10]), S.lo[x + 15], S.lo[x + 20]);
+    CH[x] = xor3(xor3(S.hi[x], S.hi[x + 5], S.hi[x + 10]), S.hi[x + 15], S.hi[x + 20]);
+  }
+#pragma unroll
+  for (int x = 0; x < 5; ++x) {  // D[x] = C[x-1] ^ rot(C[x+1], 1)
+    uint32_t rl = CL[(x + 1) % 5], rh = CH[(x + 1) % 5];
+    rotl_hl(rl, rh, 1);
+    DL[x] = CL[(x + 4) % 5] ^ rl;
+    DH[x] = CH[(x + 4) % 5] ^ rh;
+  }
+#pragma unroll
+  for (int x = 0; x < 5; ++x)
+#pragma unroll
+    for (int y = 0; y < 5; ++y) {  // theta apply, rho, pi
+      const int i = x + 5 * y;
+      uint32_t l = S.lo[i] ^ DL[x], h = S.hi[i] ^ DH[x];
+      rotl_hl(l, h, ROT[i]);
+      const int d = y + 5 * ((2 * x + 3 * y) % 5);
+      BL[d] = l;
+      BH[d] = h;
+    }
+#pragma unroll
+  for (int y = 0; y < 5; ++y)
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {  // chi
+      const int i = x + 5 * y, i1 = (x + 1) % 5 + 5 * y, i2 = (x + 2) % 5 + 5 * y;
+      S.lo[i] = BL[i] ^ (~BL[i1] & BL[i2]);
+      S.hi[i] = BH[i] ^ (~BH[i1] & BH[i2]);
+    }
+  S.lo[0] ^= (uint32_t)rc;  // iota
+  S.hi[0] ^= (uint32_t)(rc >> 32);
 }
+
+KH_HD void keccakf(KState& s) {
+#pragma unroll 8  // 3 iterations: the pi renaming costs ~5 moves/round (42 per back-edge)
+  for (int r = 0; r < 24; ++r) keccak_round(s, round_constant(r));
+}
+
+KH_HD uint64_t lane(const KState& s, int i) { return ((uint64_t)s.hi[i] << 32) | s.lo[i]; }
 
 // XOR word w into rate lane i (i compile-time after unrolling).
 KH_HD void kxor(KState& s, int i, uint64_t w) {
-  switch (i) {
-    case 0: s.a00 ^= w; break;
-    case 1: s.a01 ^= w; break;
-    case 2: s.a02 ^= w; break;
-    case 3: s.a03 ^= w; break;
-    case 4: s.a04 ^= w; break;
-    case 5: s.a05 ^= w; break;
-    case 6: s.a06 ^= w; break;
-    case 7: s.a07 ^= w; break;
-    case 8: s.a08 ^= w; break;
-    case 9: s.a09 ^= w; break;
-    case 10: s.a10 ^= w; break;
-    case 11: s.a11 ^= w; break;
-    case 12: s.a12 ^= w; break;
-    case 13: s.a13 ^= w; break;
-    case 14: s.a14 ^= w; break;
-    case 15: s.a15 ^= w; break;
-    case 16: s.a16 ^= w; break;
-  }
+  s.lo[i] ^= (uint32_t)w;
+  s.hi[i] ^= (uint32_t)(w >> 32);
 }
 
 // nb (1..8) little-endian bytes from an arbitrary address via aligned 8-byte
@@ -197,10 +184,10 @@ KH_HD void kec256_msg(const uint8_t* p, uint32_t len, uint64_t out[4]) {
     kxor(s, i, w);
   }
   keccakf(s);
-  out[0] = s.a00;
-  out[1] = s.a01;
-  out[2] = s.a02;
-  out[3] = s.a03;
+  out[0] = lane(s, 0);
+  out[1] = lane(s, 1);
+  out[2] = lane(s, 2);
+  out[3] = lane(s, 3);
 }
 
 KH_HD uint32_t perms_for_len(uint32_t len) { return len / 136 + 1; }

@@ -319,6 +319,16 @@ __global__ void __launch_bounds__(BS) k_emit_copy(Topo T, uint64_t B, const uint
 }
 
 
+// copy L bytes between arbitrary byte addresses: word loads (load64u_n), then
+// whole-word stores where the destination is aligned, bytes at the unaligned ends
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t L) {
+  uint64_t q = 0;
+  uint32_t head = (uint32_t)((8 - ((uintptr_t)dst & 7)) & 7);
+  for (; q < L && q < head; ++q) dst[q] = src[q];
+  for (; q + 8 <= L; q += 8) *(uint64_t*)(dst + q) = load64u_n(src + q, 8);
+  for (; q < L; ++q) dst[q] = src[q];
+}
+
 // ---- multi-GPU routing: stable partition of records by top-nibble owner
 __device__ __forceinline__ uint32_t nibble_owner(uint64_t w0, uint32_t nparts) {
   return (((uint32_t)(w0 & 0xFF) >> 4) * nparts) >> 4;
@@ -349,9 +359,7 @@ __global__ void __launch_bounds__(BS) k_part_copy(const uint64_t* K, const uint8
     uint32_t s = idx[i];
     for (int j = 0; j < 4; ++j) okeys[4 * i + j] = K[4 * (uint64_t)s + j];
     uint64_t o = voff[s], L = voff[s + 1] - o;
-    const uint8_t* src = vals + o;
-    uint8_t* dst = ovals + ooff[i];
-    for (uint64_t q = 0; q < L; ++q) dst[q] = src[q];
+    copy_bytes(ovals + ooff[i], vals + o, L);
     uint32_t p = (uint32_t)ck[i];
     atomicAdd(&c[p], 1ULL);
     atomicAdd(&b[p], (unsigned long long)L);

@@ -524,10 +524,10 @@ struct Stream {
       kxor(s, i, w);
     }
     keccakf(s);
-    h[0] = s.a00;
-    h[1] = s.a01;
-    h[2] = s.a02;
-    h[3] = s.a03;
+    h[0] = lane(s, 0);
+    h[1] = lane(s, 1);
+    h[2] = lane(s, 2);
+    h[3] = lane(s, 3);
     return nblk + 1;
   }
 };
@@ -571,6 +571,14 @@ KH_HD uint32_t op_leaf_emit(const Topo& T, uint64_t i, uint64_t* lbuf, uint32_t*
   uint64_t hpl = h == 1 ? 1 : 1 + h;
   uint64_t payload = hpl + rlp_str_len(vlen, v0);
   uint32_t L = (uint32_t)(rlp_hdr_len(payload) + payload);
+  // issue every load of the value up front (one exposed memory latency, not one per word)
+  constexpr uint32_t NVW = 14;
+  const uint64_t* vq = (const uint64_t*)((uintptr_t)vp & ~(uintptr_t)7);
+  const uint32_t voffb = (uint32_t)((uintptr_t)vp & 7);
+  const uint64_t vwords = (voffb + vlen + 7) / 8;
+  uint64_t vw[NVW];
+#pragma unroll
+  for (uint32_t q = 0; q < NVW; ++q) vw[q] = q < vwords ? vq[q] : 0;
   Stream<NT> w;
   w.init(lbuf, T.arena ? (uint64_t*)(T.arena + T.lf_aoff[i]) : nullptr);
   w.len_prefix(payload, 0xC0);
@@ -578,13 +586,25 @@ KH_HD uint32_t op_leaf_emit(const Topo& T, uint64_t i, uint64_t* lbuf, uint32_t*
   w.put1(hp0);
   w.key_suffix(k, (s + 1) / 2);
   if (!(vlen == 1 && v0 < 0x80)) w.len_prefix(vlen, 0x80);
-  // value bytes, absorbing each full block as it completes
-  while (vlen) {
-    uint32_t nb = vlen < 8 ? (uint32_t)vlen : 8;
-    w.put(load64u_n(vp, nb), nb);
-    vp += nb;
-    vlen -= nb;
-    if (w.wi >= 17) w.drain();
+  if (L <= 135 && vwords <= NVW) {
+    // one-block leaf (every account leaf): straight from registers, no drain needed
+#pragma unroll
+    for (uint32_t q = 0; q + 1 < NVW; ++q) {
+      if (8 * q < vlen) {
+        uint64_t x = voffb ? ((vw[q] >> (8 * voffb)) | (vw[q + 1] << (64 - 8 * voffb))) : vw[q];
+        uint64_t rem = vlen - 8 * q;
+        w.put(x, rem < 8 ? (uint32_t)rem : 8);
+      }
+    }
+  } else {
+    // long value: stream it, absorbing each full block as it completes
+    while (vlen) {
+      uint32_t nb = vlen < 8 ? (uint32_t)vlen : 8;
+      w.put(load64u_n(vp, nb), nb);
+      vp += nb;
+      vlen -= nb;
+      if (w.wi >= 17) w.drain();
+    }
   }
   T.lf_len[i] = L;
   bool top = T.lf_parent[i] == NONE;
@@ -606,31 +626,49 @@ KH_HD uint32_t op_branch_emit(const Topo& T, uint32_t j, uint64_t* lbuf, uint32_
   uint32_t k = T.br_k[j];
   uint64_t cb = T.br_cbase[j];
   uint32_t payload = 1 + (16 - k);  // terminator "" + empty slots
-  uint32_t mask = 0;
   for (uint32_t c = 0; c < k; ++c) {
-    uint32_t m = T.cmeta[cb + c];
-    uint32_t len = m & 0xFF;
+    uint32_t len = T.cmeta[cb + c] & 0xFF;
     payload += (len == 32) ? 33 : len;
-    mask |= 1u << (m >> 8);
   }
   uint32_t L = rlp_hdr_len(payload) + payload;
   uint64_t* garena = T.arena ? (uint64_t*)(T.arena + T.br_arena_base + T.br_aoff[j]) : nullptr;
   Stream<NT> w;
   w.init(lbuf, garena);
   w.len_prefix(payload, 0xC0);
-  uint32_t c = 0;
-  for (uint32_t nib = 0; nib < 16; ++nib) {
-    if ((mask >> nib) & 1) {
-      const uint64_t* r = T.cref + 4 * (cb + c);
-      uint64_t rr[4] = {r[0], r[1], r[2], r[3]};
-      w.ref(rr, T.cmeta[cb + c] & 0xFF);
-      ++c;
-    } else {
-      w.put1(0x80);
+  // walk the children in nibble order; each child's reference is loaded two
+  // children ahead so its memory latency overlaps the encoding/absorbing work
+  const uint64_t* cr = T.cref + 4 * cb;
+  const uint16_t* cm = T.cmeta + cb;
+  uint64_t ra[4] = {0, 0, 0, 0}, rb[4] = {0, 0, 0, 0};
+  uint32_t ma = 0, mb = 0;
+  if (k > 0) {
+    ma = cm[0];
+    ra[0] = cr[0]; ra[1] = cr[1]; ra[2] = cr[2]; ra[3] = cr[3];
+  }
+  if (k > 1) {
+    mb = cm[1];
+    rb[0] = cr[4]; rb[1] = cr[5]; rb[2] = cr[6]; rb[3] = cr[7];
+  }
+  int32_t prev = -1;
+  for (uint32_t c = 0; c <= k; ++c) {  // c == k: trailing empty slots + the "" terminator
+    uint64_t cur[4] = {ra[0], ra[1], ra[2], ra[3]};
+    uint32_t mc = c < k ? ma : (16u << 8);
+    ra[0] = rb[0]; ra[1] = rb[1]; ra[2] = rb[2]; ra[3] = rb[3];
+    ma = mb;
+    if (c + 2 < k) {
+      const uint64_t* p2 = cr + 4 * (c + 2);
+      mb = cm[c + 2];
+      rb[0] = p2[0]; rb[1] = p2[1]; rb[2] = p2[2]; rb[3] = p2[3];
     }
+    int32_t nib = (int32_t)(mc >> 8);
+    for (int32_t e = prev + 1; e < nib; ++e) w.put1(0x80);  // empty slots
+    prev = nib;
+    if (c < k)
+      w.ref(cur, mc & 0xFF);
+    else
+      w.put1(0x80);  // terminator (secure tries never store a value in a branch)
     if (w.wi >= 17) w.drain();
   }
-  w.put1(0x80);
   T.br_len[j] = L;
   uint32_t ext = T.br_ext[j];
   uint32_t parent = T.br_parent[j];

@@ -74,31 +74,65 @@ class GpuBackend:
         torch.cuda.synchronize(self.device)
 
 
+A2A_CHUNK = 1 << 30  # bytes per peer per all-to-all round (keeps every count < 2^31)
+
+
+def a2a_bytes(out, inp, out_splits, in_splits, chunk=None):
+    """all_to_all_single of uint8 buffers with per-peer byte splits, in rounds of at
+    most `chunk` bytes per peer so no message count reaches 2^31 (RCCL / c10d take
+    int counts)."""
+    world = len(in_splits)
+    chunk = chunk or A2A_CHUNK
+    # every rank must run the same number of rounds: agree on the largest split
+    big = torch.tensor([max(list(out_splits) + list(in_splits) + [0])], dtype=torch.int64, device=inp.device)
+    dist.all_reduce(big, op=dist.ReduceOp.MAX)
+    rounds = int(-(-int(big.item()) // chunk))
+    if rounds <= 1:
+        dist.all_to_all_single(out, inp, list(out_splits), list(in_splits))
+        return
+    ioff = np.concatenate([[0], np.cumsum(in_splits)])
+    ooff = np.concatenate([[0], np.cumsum(out_splits)])
+    for r in range(rounds):
+        lo = r * chunk
+        isz = [int(max(0, min(chunk, in_splits[p] - lo))) for p in range(world)]
+        osz = [int(max(0, min(chunk, out_splits[p] - lo))) for p in range(world)]
+        send = torch.cat([inp[int(ioff[p]) + lo:int(ioff[p]) + lo + isz[p]] for p in range(world)])
+        recv = torch.empty(sum(osz), dtype=inp.dtype, device=inp.device)
+        dist.all_to_all_single(recv, send, osz, isz)
+        o = 0
+        for p in range(world):
+            out[int(ooff[p]) + lo:int(ooff[p]) + lo + osz[p]].copy_(recv[o:o + osz[p]])
+            o += osz[p]
+
+
 def exchange(be, pkeys, pvals, pvlen, counts, nbytes):
     """All-to-all of the partitioned records.  Returns (keys32, vals, voff, m) of the
     records this rank owns, ordered by source rank then source order."""
     world = dist.get_world_size()
     dev = pkeys.device
-    sc = torch.tensor(np.concatenate([counts, nbytes]).astype(np.int64), device=dev)
-    meta = torch.empty(2 * world, dtype=torch.int64, device=dev)
+    if world == 1:  # nothing to route
+        m = int(counts[0])
+        voff = torch.zeros(m + 1, dtype=torch.int64, device=dev)
+        if m:
+            torch.cumsum(pvlen[:m], 0, out=voff[1:])
+        return pkeys, pvals, voff, m
     # counts and byte counts in one all-to-all: rank p receives (counts[p], nbytes[p]) pairs
-    send = torch.stack([sc[:world], sc[world:]], 1).reshape(-1).contiguous()
+    send = torch.tensor(np.stack([counts, nbytes], 1).reshape(-1).astype(np.int64), device=dev)
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send, [2] * world, [2] * world)
     rr = recv.cpu().numpy().reshape(world, 2)
     rc, rb = rr[:, 0].astype(np.int64), rr[:, 1].astype(np.int64)
-    del meta
     m = int(rc.sum())
     tot_b = int(rb.sum())
     cl, bl = [int(x) for x in counts], [int(x) for x in nbytes]
-    n_send = sum(cl)
-    b_send = sum(bl)
+    n_send, b_send = sum(cl), sum(bl)
     rkeys = be.empty(m * 32 + 64)
-    dist.all_to_all_single(rkeys[:m * 32], pkeys[:n_send * 32], [int(c) * 32 for c in rc], [c * 32 for c in cl])
+    a2a_bytes(rkeys[:m * 32], pkeys[:n_send * 32], [int(c) * 32 for c in rc], [c * 32 for c in cl])
     rlen = be.empty(max(m, 1), torch.int64)
-    dist.all_to_all_single(rlen[:m], pvlen[:n_send], [int(c) for c in rc], cl)
+    a2a_bytes(rlen[:m].view(torch.uint8), pvlen[:n_send].view(torch.uint8), [int(c) * 8 for c in rc],
+              [c * 8 for c in cl])
     rvals = be.empty(tot_b + 64)
-    dist.all_to_all_single(rvals[:tot_b], pvals[:b_send], [int(b) for b in rb], bl)
+    a2a_bytes(rvals[:tot_b], pvals[:b_send], [int(b) for b in rb], bl)
     voff = torch.zeros(m + 1, dtype=torch.int64, device=dev)
     if m:
         torch.cumsum(rlen[:m], 0, out=voff[1:])

@@ -90,7 +90,9 @@ def _worker(rank, world, port, case, q):
     from khipu_amd import sharded
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        addrs, vals, prehashed = case
+        addrs, vals, prehashed = case[:3]
+        if len(case) > 3:
+            sharded.A2A_CHUNK = case[3]  # force multi-round exchanges
         n_all = len(addrs)
         lo, hi = n_all * rank // world, n_all * (rank + 1) // world
         mine_a, mine_v = addrs[lo:hi], vals[lo:hi]
@@ -152,3 +154,10 @@ def test_sharded_single_top_nibble_fallback(oracle):
     vals = [codec.storage_value_rlp(r.randrange(1, 1 << 30)) for _ in keys]
     root = _run((keys, vals, True))
     assert root == oracle.seq_root(keys, vals)
+
+
+def test_sharded_chunked_exchange(oracle):
+    """All-to-all split into rounds (the >2 GiB path), forced with a 100-byte chunk."""
+    addrs, vals = _records(4, 200)
+    root = _run((addrs, vals, False, 100), 3)
+    assert root == oracle.seq_root([oracle.kec256(a) for a in addrs], vals)
