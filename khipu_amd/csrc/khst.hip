@@ -144,6 +144,11 @@ __global__ void __launch_bounds__(BS) k_compact(const uint64_t* skey, const uint
   if (sseg) oseg[p] = sseg[i];
 }
 
+__global__ void __launch_bounds__(BS) k_val_gather(Topo T) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < T.m) op_val_gather(T, i);
+}
+
 __global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb) {
   uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (b < nb) op_lcp(T, b);
@@ -226,7 +231,7 @@ __global__ void __launch_bounds__(BS) k_level_scatter(Topo T, uint64_t B, const 
 }
 
 __global__ void __launch_bounds__(BS) k_leaf_emit(Topo T) {
-  __shared__ uint64_t lds[STREAM_WORDS * BS];
+  __shared__ uint64_t lds[LEAF_STREAM_WORDS * BS];
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (i < T.m) {
@@ -507,7 +512,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       nb1, nb1 / 32 + 1024,                   // u, pyramid
       nb1 * 4, nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1 * 4, nb1 * 4,  // psv nsv pse rep ord isrep grp
       nb1 * 4, nb1 * 4, nb1, nb1, nb1 * 4, nb1, nb1 * 4, nb1 * 8, nb1 * 4, nb1 * 4,  // branches
-      n * 4, n, n, n * 8, n * 4,              // leaves
+      n * 4, n, n, n * 8, n * 4, n * 8, n * 4,  // leaves, svoff, svlen
       A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
       nres * 32, nres * 4, nres * 32,         // results
       CTR_N * 8, 64 * 4, 64 * 4, 64 * 4, nb1 * 4,  // ctr hist level_base cursor order
@@ -548,6 +553,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.lf_pd = cv.take<int8_t>(n);
   T.lf_aoff = cv.take<uint64_t>(n);
   T.lf_len = cv.take<uint32_t>(n);
+  T.svoff = cv.take<uint64_t>(n);
+  T.svlen = cv.take<uint32_t>(n);
   T.lf_hash = A.emit ? cv.take<uint64_t>(n * 4) : nullptr;
   T.br_hash = A.emit ? cv.take<uint64_t>(nb1 * 4) : nullptr;
   T.ex_hash = A.emit ? cv.take<uint64_t>(nb1 * 4) : nullptr;
@@ -659,6 +666,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.skey = skey;
   T.sidx = sidx;
   T.sseg = sseg;
+  hipLaunchKernelGGL(k_val_gather, GRID(m, BS), dim3(BS), 0, st, T);
+  LAUNCH_CHECK();
   HIPCHK(hipEventRecord(c->ev[2], st));
 
   // ---- 3. topology

@@ -147,6 +147,8 @@ struct Topo {
   const uint32_t* sseg;   // [m] segment id (segmented only)
   const uint8_t* vals;    // input values
   const uint64_t* voff;   // [n+1]
+  uint64_t* svoff;        // [m] value offset of sorted key i (gathered once after the sort)
+  uint32_t* svlen;        // [m] value length of sorted key i
   uint8_t* u;             // [m-1] boundary values
   int32_t* psv;           // [m-1] previous strictly smaller boundary (-1: none)
   int32_t* nsv;           // [m-1] next strictly smaller boundary (-1: none)
@@ -393,10 +395,16 @@ KH_HD uint32_t branch_arena_bytes(const Topo& T, uint32_t j) {
 
 // ---- leaf geometry
 KH_HD void leaf_value(const Topo& T, uint64_t i, const uint8_t** p, uint64_t* len) {
+  *p = T.vals + T.svoff[i];
+  *len = T.svlen[i];
+}
+
+// gather the value span of sorted key i (random reads once, sequential reads after)
+KH_HD void op_val_gather(const Topo& T, uint64_t i) {
   uint32_t src = T.sidx[i];
   uint64_t o = T.voff[src];
-  *p = T.vals + o;
-  *len = T.voff[src + 1] - o;
+  T.svoff[i] = o;
+  T.svlen[i] = (uint32_t)(T.voff[src + 1] - o);
 }
 
 // encoded leaf length for path start nibble s
@@ -429,7 +437,8 @@ KH_HD void op_leaf_topo(const Topo& T, uint64_t i) {
 // Every 17 complete words (one 136-byte rate block) are absorbed and permuted, so
 // no node encoding ever needs to exist in HBM unless write-back emission asks for
 // it (`gdst` non-null: the same words are also stored to the arena).
-constexpr uint32_t STREAM_WORDS = 24;  // 17 + the <= 5 words one item can add + 2
+constexpr uint32_t STREAM_WORDS = 24;       // branch: 17 + the <= 6 words one child can add + 1
+constexpr uint32_t LEAF_STREAM_WORDS = 18;  // leaf: <= 17 words before each drain
 template <int NT>
 struct Stream {
   uint64_t* buf;   // buf[w * NT]

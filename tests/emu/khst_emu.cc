@@ -62,6 +62,11 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
   T.sseg = sseg.data();
   T.vals = vals;
   T.voff = voff;
+  std::vector<uint64_t> svoff(m);
+  std::vector<uint32_t> svlen(m);
+  T.svoff = svoff.data();
+  T.svlen = svlen.data();
+  for (uint64_t i = 0; i < m; ++i) op_val_gather(T, i);
   const uint64_t nbb = nb + 1;
   std::vector<uint8_t> u(nbb), ord(nbb), br_depth(nbb), br_ext(nbb), br_pord(nbb), lf_pord(m);
   std::vector<int32_t> psv(nbb), nsv(nbb), pse(nbb);
@@ -171,7 +176,7 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
   uint64_t perms = 0, hashes = 0, inl = 0;
   for (uint64_t i = 0; i < m; ++i) {
     uint32_t in1 = 0;
-    uint64_t lb[STREAM_WORDS];
+    uint64_t lb[LEAF_STREAM_WORDS];
     uint32_t p = op_leaf_emit<1>(T, i, lb, &in1);
     perms += p;
     hashes += p ? 1 : 0;
