@@ -3,13 +3,14 @@
 //
 // Pipeline of one build (all on one HIP stream; DESIGN.md has the roofline of each):
 //   1. keys      kec256 of raw keys (KH_HASH_KEYS)                       k_hash_keys
-//   2. sort      64-bit key-prefix LSD radix sort of (prefix, index)     prims.h
-//                + tie check; full 256-bit sort + dedup only on ties     k_tie/k_word_key/k_dup
+//   2. sort      32-bit prefix LSD radix sort of (segment|key prefix, index) prims.h
+//                + local full-key sort of equal-prefix runs, dedup        k_tie_fix/k_dup
+//                (full 256-bit sort only for runs > 64: adversarial keys)
 //   3. topology  adjacent LCP -> min pyramid -> nearest smaller values
 //                -> groups (branches), parents, child ordinals            k_lcp..k_leaf_topo
-//   4. leaves    RLP-encode into the node arena + Keccak-256              k_leaf_emit
-//   5. branches  one launch per depth, deepest first: gather child refs,
-//                RLP-encode branch (+ extension) + Keccak-256             k_branch_emit
+//   4. leaves    RLP-encode into the node arena, then Keccak-256          k_leaf_prep/hash
+//   5. branches  per depth, deepest first: gather child refs and RLP-encode,
+//                then Keccak-256 (+ extension)                            k_branch_prep/hash
 // Results: the top node of every segment (root / subtrie reference).
 #include <hip/hip_runtime.h>
 
@@ -85,10 +86,54 @@ __global__ void __launch_bounds__(BS) k_make_ck(const uint64_t* K, const uint32_
   idx[i] = (uint32_t)i;
 }
 
-__global__ void __launch_bounds__(BS) k_tie(const uint64_t* ck, uint64_t n, unsigned long long* flag) {
+// Runs of equal 32-bit sort prefixes (same segment, equal leading key bits) are
+// put in full-key order by the thread at the run's start: an insertion sort of
+// (key, index, segment) in place, stable, so among equal keys the input order
+// (later put last) is kept.  flags |= 2 if equal keys exist (dedup needed),
+// |= 1 if a run exceeds TIE_RUN_MAX (take the full-sort path instead).
+constexpr uint32_t TIE_RUN_MAX = 64;
+__device__ __forceinline__ bool key_less(const uint64_t* a, const uint64_t* b) {
+  for (int j = 0; j < 4; ++j) {
+    uint64_t x = bswap64(a[j]), y = bswap64(b[j]);
+    if (x != y) return x < y;
+  }
+  return false;
+}
+__global__ void __launch_bounds__(BS) k_tie_fix(const uint64_t* ck, uint64_t n, uint64_t* skey, uint32_t* sidx,
+                                                uint32_t* sseg, unsigned long long* flags) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  bool t = (i + 1 < n) && ck[i] == ck[i + 1];
-  if (__any(t) && __lane_id() == 0) atomicOr(flag, 1ULL);
+  if (i + 1 >= n) return;
+  uint32_t hi = (uint32_t)(ck[i] >> 32);
+  if ((uint32_t)(ck[i + 1] >> 32) != hi) return;   // no run starting or continuing here
+  if (i > 0 && (uint32_t)(ck[i - 1] >> 32) == hi) return;  // not the run's first element
+  uint64_t e = i + 1;
+  while (e < n && (uint32_t)(ck[e] >> 32) == hi && e - i <= TIE_RUN_MAX) ++e;
+  if (e - i > TIE_RUN_MAX) {
+    atomicOr(flags, 1ULL);
+    return;
+  }
+  for (uint64_t a = i + 1; a < e; ++a) {
+    uint64_t k[4] = {skey[4 * a], skey[4 * a + 1], skey[4 * a + 2], skey[4 * a + 3]};
+    uint32_t ix = sidx[a];
+    uint32_t sg = sseg ? sseg[a] : 0;
+    uint64_t b = a;
+    while (b > i && key_less(k, skey + 4 * (b - 1))) {
+      for (int j = 0; j < 4; ++j) skey[4 * b + j] = skey[4 * (b - 1) + j];
+      sidx[b] = sidx[b - 1];
+      if (sseg) sseg[b] = sseg[b - 1];
+      --b;
+    }
+    for (int j = 0; j < 4; ++j) skey[4 * b + j] = k[j];
+    sidx[b] = ix;
+    if (sseg) sseg[b] = sg;
+  }
+  bool dup = false;
+  for (uint64_t a = i + 1; a < e; ++a) {
+    const uint64_t* x = skey + 4 * (a - 1);
+    const uint64_t* y = skey + 4 * a;
+    dup |= x[0] == y[0] && x[1] == y[1] && x[2] == y[2] && x[3] == y[3];
+  }
+  if (dup) atomicOr(flags, 2ULL);
 }
 
 __global__ void __launch_bounds__(BS) k_gather(const uint64_t* K, const uint32_t* seg, const uint32_t* idx,
@@ -181,24 +226,36 @@ __global__ void __launch_bounds__(BS) k_group(Topo T, uint64_t nb) {
   atomicMax(&T.br_k[g], (uint32_t)T.ord[b] + 2u);
 }
 
-__global__ void __launch_bounds__(BS) k_branch_topo(Topo T, uint64_t nb) {
-  // depth histogram: LDS atomics per block, one global atomic per (block, depth)
-  __shared__ uint32_t h[64];
-  if (threadIdx.x < 64) h[threadIdx.x] = 0;
+// sum three per-thread counters over the block; one atomic per counter per block
+__device__ __forceinline__ void block_add3(unsigned long long* c0, unsigned long long v0, unsigned long long* c1,
+                                           unsigned long long v1, unsigned long long* c2, unsigned long long v2) {
+  __shared__ unsigned long long red[BS / 64][3];
+  v0 = wave_sum(v0);
+  v1 = wave_sum(v1);
+  v2 = wave_sum(v2);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[w][0] = v0;
+    red[w][1] = v1;
+    red[w][2] = v2;
+  }
   __syncthreads();
+  if (threadIdx.x < 3) {
+    unsigned long long t = 0;
+    for (int q = 0; q < BS / 64; ++q) t += red[q][threadIdx.x];
+    unsigned long long* dst = threadIdx.x == 0 ? c0 : threadIdx.x == 1 ? c1 : c2;
+    if (t && dst) atomicAdd(dst, t);
+  }
+}
+
+__global__ void __launch_bounds__(BS) k_branch_topo(Topo T, uint64_t nb) {
   uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long ext = 0;
   if (b < nb) {
     op_branch_topo(T, b);
-    if (T.u[b] != 0 && T.rep[b] == (uint32_t)b) {
-      uint32_t j = T.isrep_bid[b];
-      atomicAdd(&h[T.br_depth[j]], 1u);
-      ext = T.br_ext[j] ? 1 : 0;
-    }
+    if (T.u[b] != 0 && T.rep[b] == (uint32_t)b) ext = T.br_ext[T.isrep_bid[b]] ? 1 : 0;
   }
-  wave_atomic_add(&T.ctr[CTR_EXT], ext);
-  __syncthreads();
-  if (threadIdx.x < 64 && h[threadIdx.x]) atomicAdd(&T.depth_hist[threadIdx.x], h[threadIdx.x]);
+  block_add3(&T.ctr[CTR_EXT], ext, nullptr, 0, nullptr, 0);
 }
 
 __global__ void __launch_bounds__(BS) k_leaf_topo(Topo T) {
@@ -206,54 +263,75 @@ __global__ void __launch_bounds__(BS) k_leaf_topo(Topo T) {
   if (i < T.m) op_leaf_topo(T, i);
 }
 
-__global__ void __launch_bounds__(BS) k_branch_alen(Topo T, uint64_t B) {
+// arena bytes per branch id (0 past the last branch, so the scan can run over nb)
+__global__ void __launch_bounds__(BS) k_branch_alen(Topo T, uint64_t nb, const uint32_t* Bp) {
   uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (j < B) T.br_aoff[j] = branch_arena_bytes(T, (uint32_t)j);
+  if (j < nb) T.br_aoff[j] = j < *Bp ? branch_arena_bytes(T, (uint32_t)j) : 0;
 }
 
-__global__ void __launch_bounds__(BS) k_level_scatter(Topo T, uint64_t B, const uint32_t* level_base,
-                                                      uint32_t* cursor, uint32_t* order) {
-  // bucket branch ids by depth: rank inside the block via LDS atomics, one global
-  // atomic per (block, depth) for the block's base in that depth's bucket
-  __shared__ uint32_t cnt[64], base[64];
+// Level order (branch ids bucketed by depth) without contended global atomics:
+// per-block depth counts laid out [depth][block], one exclusive scan gives every
+// (depth, block) its base, a second pass ranks inside the block with LDS atomics.
+__global__ void __launch_bounds__(BS) k_level_count(Topo T, const uint32_t* Bp, uint32_t* bcnt, uint32_t nblk) {
+  __shared__ uint32_t h[64];
+  if (threadIdx.x < 64) h[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (j < *Bp) atomicAdd(&h[T.br_depth[j]], 1u);
+  __syncthreads();
+  if (threadIdx.x < 64) bcnt[(uint64_t)threadIdx.x * nblk + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(BS) k_level_scatter(Topo T, const uint32_t* Bp, const uint32_t* bbase,
+                                                      uint32_t nblk, uint32_t* order) {
+  __shared__ uint32_t cnt[64];
   if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
   __syncthreads();
   uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  uint32_t d = 0, r = 0;
-  if (j < B) {
-    d = T.br_depth[j];
-    r = atomicAdd(&cnt[d], 1u);
+  if (j < *Bp) {
+    uint32_t d = T.br_depth[j];
+    uint32_t r = atomicAdd(&cnt[d], 1u);
+    order[bbase[(uint64_t)d * nblk + blockIdx.x] + r] = (uint32_t)j;
   }
-  __syncthreads();
-  if (threadIdx.x < 64 && cnt[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]);
-  __syncthreads();
-  if (j < B) order[level_base[d] + base[d] + r] = (uint32_t)j;
 }
 
-__global__ void __launch_bounds__(BS) k_leaf_emit(Topo T) {
-  __shared__ uint64_t lds[LEAF_STREAM_WORDS * BS];
+// level bounds: lb[d] = first position of depth d in `order`, lb[64] = B
+__global__ void k_level_bounds(const uint32_t* bbase, uint32_t nblk, const uint32_t* Bp, uint32_t* lb) {
+  uint32_t d = threadIdx.x;
+  if (d < 64) lb[d] = bbase[(uint64_t)d * nblk];
+  if (d == 0) lb[64] = *Bp;
+}
+
+__global__ void __launch_bounds__(BS) k_leaf_prep(Topo T) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < T.m) op_leaf_prep(T, i);
+}
+
+__global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (i < T.m) {
     uint32_t in1 = 0;
-    perms = op_leaf_emit<BS>(T, i, lds + threadIdx.x, &in1);
+    perms = op_leaf_hash(T, i, &in1);
     hashes = perms ? 1 : 0;
     inl = in1;
   }
-  wave_atomic_add(&T.ctr[CTR_PERMS], perms);
-  wave_atomic_add(&T.ctr[CTR_HASHES], hashes);
-  wave_atomic_add(&T.ctr[CTR_INLINE], inl);
+  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
 }
 
-__global__ void __launch_bounds__(BS) k_branch_emit(Topo T, const uint32_t* order, uint64_t cnt) {
-  __shared__ uint64_t lds[STREAM_WORDS * BS];
+__global__ void __launch_bounds__(BS) k_branch_prep(Topo T, const uint32_t* order, uint64_t cnt) {
+  uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (t < cnt) op_branch_prep(T, order[t]);
+}
+
+__global__ void __launch_bounds__(BS) k_branch_hash(Topo T, const uint32_t* order, uint64_t cnt) {
   uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (t < cnt) {
     uint32_t j = order[t];
     uint32_t in1 = 0;
-    perms = op_branch_emit<BS>(T, j, lds + threadIdx.x, &in1);
-    // hashes: branch hashed if len >= 32 or top; extension likewise
+    perms = op_branch_hash(T, j, &in1);
+    // hashes: the branch if its encoding is >= 32 B or it is the top; its extension likewise
     uint32_t L = T.br_len[j];
     bool top = T.br_parent[j] == NONE;
     bool ext = T.br_ext[j] != 0;
@@ -261,9 +339,7 @@ __global__ void __launch_bounds__(BS) k_branch_emit(Topo T, const uint32_t* orde
     if (ext) hashes += (T.ex_len[j] >= 32 || top) ? 1 : 0;
     inl = in1;
   }
-  wave_atomic_add(&T.ctr[CTR_PERMS], perms);
-  wave_atomic_add(&T.ctr[CTR_HASHES], hashes);
-  wave_atomic_add(&T.ctr[CTR_INLINE], inl);
+  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
 }
 
 // write-back emission: node q in [0, m + 2B): leaf q, or branch / extension of branch (q-m)/2
@@ -515,7 +591,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       n * 4, n, n, n * 8, n * 4, n * 8, n * 4,  // leaves, svoff, svlen
       A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
       nres * 32, nres * 4, nres * 32,         // results
-      CTR_N * 8, 64 * 4, 64 * 4, 64 * 4, nb1 * 4,  // ctr hist level_base cursor order
+      CTR_N * 8, 64 * 4, 80 * 4, 64 * ((nb1 + BS - 1) / BS) * 4, nb1 * 4,  // ctr hist lb bcnt order
   };
   c->ws1.ensure(carve_size(sz));
   Carver cv{(char*)c->ws1.p, 0, c->ws1.cap};
@@ -563,8 +639,9 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.res_inl = cv.take<uint64_t>(nres * 4);
   T.ctr = cv.take<unsigned long long>(CTR_N);
   T.depth_hist = cv.take<uint32_t>(64);
-  uint32_t* level_base = cv.take<uint32_t>(64);
-  uint32_t* cursor = cv.take<uint32_t>(64);
+  uint32_t* lb = cv.take<uint32_t>(80);
+  const uint32_t nblk_max = (uint32_t)((nb1 + BS - 1) / BS);
+  uint32_t* bcnt = cv.take<uint32_t>((uint64_t)64 * nblk_max);
   uint32_t* order = cv.take<uint32_t>(nb1);
   T.depth0 = A.depth0;
   T.segmented = segmented ? 1 : 0;
@@ -573,7 +650,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
 
   HIPCHK(hipMemsetAsync(T.ctr, 0, CTR_N * 8, st));
   HIPCHK(hipMemsetAsync(T.depth_hist, 0, 64 * 4, st));
-  HIPCHK(hipMemsetAsync(cursor, 0, 64 * 4, st));
+  HIPCHK(hipMemsetAsync(lb, 0, 80 * 4, st));
   HIPCHK(hipMemsetAsync(T.res_len, 0, nres * 4, st));
   HIPCHK(hipMemsetAsync(T.res_hash, 0, nres * 32, st));
   HIPCHK(hipMemsetAsync(T.res_inl, 0, nres * 32, st));
@@ -586,33 +663,33 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   }
   HIPCHK(hipEventRecord(c->ev[1], st));
 
-  // ---- 2. sort on the 64-bit composite prefix
+  // ---- 2. sort: LSD radix on the top 32 bits of the composite (segment | key) prefix,
+  // then fix the rare runs of equal prefixes locally (k_tie_fix); a full 256-bit sort
+  // only if a run is longer than TIE_RUN_MAX (adversarial keys)
   hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, sb, n, ck0, idx0);
   LAUNCH_CHECK();
-  bool flip = radix_sort_pairs(ck0, idx0, ck1, idx1, n, 0, 64, rs_scratch, st);
+  bool flip = radix_sort_pairs(ck0, idx0, ck1, idx1, n, 32, 64, rs_scratch, st);
   uint64_t* cks = flip ? ck1 : ck0;
   uint32_t* idxs = flip ? idx1 : idx0;
-  uint32_t* idxo = flip ? idx0 : idx1;
-  uint64_t* cko = flip ? ck0 : ck1;
   LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_tie, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, n, T.ctr + CTR_TIE);
+  hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, (const uint32_t*)idxs, n,
+                     skey, sseg);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_tie_fix, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, n, skey, idxs, sseg,
+                     T.ctr + CTR_TIE);
   LAUNCH_CHECK();
   HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  bool ties = c->h_pinned[0] != 0;
+  const uint64_t tie_flags = c->h_pinned[0];
+  const bool fallback = tie_flags & 1, dups = tie_flags & 2;
   uint64_t m = n;
   uint32_t* sidx = idxs;
-  if (!ties) {
-    hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, (const uint32_t*)idxs,
-                       n, skey, sseg);
-    LAUNCH_CHECK();
-  } else {
-    // full 256-bit (+segment) LSD sort from the input order, then keep the last duplicate
+  if (fallback) {
+    // full 256-bit (+segment) LSD sort from the input order
     uint32_t* ia = idx0;
     uint32_t* ib = idx1;
     uint64_t* ka = ck0;
     uint64_t* kb = ck1;
-    std::vector<uint32_t> ident;  // identity via kernel: reuse k_make_ck to fill idx
     hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, 0u, n, ka, ia);
     LAUNCH_CHECK();
     auto pass = [&](int word, int bits) {
@@ -629,12 +706,15 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     };
     for (int w = 3; w >= 0; --w) pass(w, 64);
     if (segmented) pass(-1, ((sb + 7) / 8) * 8);
-    // gather in full order into skey (ib/kb are free now)
     hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, (const uint32_t*)ia, n,
                        skey, sseg);
     LAUNCH_CHECK();
-    uint32_t* keep = (uint32_t*)kb;  // n*8 bytes available
-    uint32_t* keep_pos = ib;
+    sidx = ia;
+  }
+  if (fallback || dups) {
+    // keep the LAST of equal keys (later puts win): flags, scan, compaction
+    uint32_t* keep = (uint32_t*)(sidx == idx0 ? ck1 : ck0);  // n*8 free bytes
+    uint32_t* keep_pos = sidx == idx0 ? idx1 : idx0;
     hipLaunchKernelGGL(k_dup, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)skey, (const uint32_t*)sseg, n, keep);
     LAUNCH_CHECK();
     uint32_t* mtot = (uint32_t*)(T.ctr + CTR_M);
@@ -643,25 +723,21 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     HIPCHK(hipStreamSynchronize(st));
     m = (uint32_t)c->h_pinned[0];
     if (m < n) {
-      // compact into a second key buffer carved from ws3
       c->ws3.ensure(carve_size({n * 32, n * 4, n * 4}));
       Carver c3{(char*)c->ws3.p, 0, c->ws3.cap};
       uint64_t* skey2 = c3.take<uint64_t>(n * 4);
       uint32_t* sidx2 = c3.take<uint32_t>(n);
       uint32_t* sseg2 = segmented ? c3.take<uint32_t>(n) : nullptr;
-      hipLaunchKernelGGL(k_compact, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)skey, (const uint32_t*)ia,
+      hipLaunchKernelGGL(k_compact, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)skey, (const uint32_t*)sidx,
                          (const uint32_t*)sseg, (const uint32_t*)keep_pos, (const uint32_t*)keep, n, skey2, sidx2,
                          sseg2);
       LAUNCH_CHECK();
       skey = skey2;
       sidx = sidx2;
       sseg = sseg2;
-    } else {
-      sidx = ia;
     }
-    (void)idxo;
-    (void)cko;
   }
+  const bool ties = fallback;
   T.m = m;
   T.skey = skey;
   T.sidx = sidx;
@@ -672,8 +748,9 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
 
   // ---- 3. topology
   const uint64_t nb = m - 1;
-  uint64_t B = 0;
-  std::vector<uint32_t> hist(64, 0);
+  unsigned long long* ctr = T.ctr;
+  uint32_t* Bp = (uint32_t*)(ctr + CTR_B);
+  HIPCHK(hipMemsetAsync(ctr + CTR_B, 0, 8 * 6, st));  // B, br bytes, lf bytes, C, E0, E1
   if (nb > 0) {
     hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
@@ -696,77 +773,71 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_chain, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
-    uint32_t* btot = (uint32_t*)(T.ctr + CTR_B);
-    scan_exclusive<uint32_t>(T.isrep_bid, T.isrep_bid, nb, btot, scan_scratch, st);
+    scan_exclusive<uint32_t>(T.isrep_bid, T.isrep_bid, nb, Bp, scan_scratch, st);
     HIPCHK(hipMemsetAsync(T.br_k, 0, nb * 4, st));
     hipLaunchKernelGGL(k_group, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_branch_topo, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
-    HIPCHK(hipMemcpyAsync(c->h_pinned, btot, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(c->h_pinned + 1, T.ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(c->h_pinned + 8, T.depth_hist, 64 * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    B = (uint32_t)c->h_pinned[0];
-    if (c->h_pinned[1]) throw KhError{KH_EINTERNAL, "topology invariant violated (group chain > 15)"};
-    memcpy(hist.data(), c->h_pinned + 8, 64 * 4);
+    // level order (grids sized by nb; threads past B exit)
+    const uint32_t nblk = (uint32_t)((nb + BS - 1) / BS);
+    hipLaunchKernelGGL(k_level_count, dim3(nblk), dim3(BS), 0, st, T, (const uint32_t*)Bp, bcnt, nblk);
+    LAUNCH_CHECK();
+    scan_exclusive<uint32_t>(bcnt, bcnt, (uint64_t)64 * nblk, (uint32_t*)nullptr, scan_scratch, st);
+    hipLaunchKernelGGL(k_level_scatter, dim3(nblk), dim3(BS), 0, st, T, (const uint32_t*)Bp,
+                       (const uint32_t*)bcnt, nblk, order);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_level_bounds, dim3(1), dim3(64), 0, st, (const uint32_t*)bcnt, nblk, (const uint32_t*)Bp,
+                       lb);
+    LAUNCH_CHECK();
+    // child record bases and branch arena offsets
+    scan_exclusive<uint32_t>(T.br_k, T.br_cbase, nb, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
+    hipLaunchKernelGGL(k_branch_alen, GRID(nb, BS), dim3(BS), 0, st, T, nb, (const uint32_t*)Bp);
+    LAUNCH_CHECK();
+    scan_exclusive<uint64_t>(T.br_aoff, T.br_aoff, nb, (uint64_t*)(ctr + CTR_BRBYTES), scan_scratch, st);
   }
   hipLaunchKernelGGL(k_leaf_topo, GRID(m, BS), dim3(BS), 0, st, T);
   LAUNCH_CHECK();
-  // ---- child bases and arena offsets
-  unsigned long long* ctr = T.ctr;
-  HIPCHK(hipMemsetAsync(ctr + CTR_BRBYTES, 0, 24, st));
-  if (B > 0) {
-    scan_exclusive<uint32_t>(T.br_k, T.br_cbase, B, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
-    if (A.emit) {  // node arena only for write-back emission
-      hipLaunchKernelGGL(k_branch_alen, GRID(B, BS), dim3(BS), 0, st, T, B);
-      LAUNCH_CHECK();
-      scan_exclusive<uint64_t>(T.br_aoff, T.br_aoff, B, (uint64_t*)(ctr + CTR_BRBYTES), scan_scratch, st);
-    }
-  }
-  if (A.emit) scan_exclusive<uint64_t>(T.lf_aoff, T.lf_aoff, m, (uint64_t*)(ctr + CTR_LFBYTES), scan_scratch, st);
-  HIPCHK(hipMemcpyAsync(c->h_pinned, ctr + CTR_BRBYTES, 24, hipMemcpyDeviceToHost, st));
+  scan_exclusive<uint64_t>(T.lf_aoff, T.lf_aoff, m, (uint64_t*)(ctr + CTR_LFBYTES), scan_scratch, st);
+  // one host sync for every size the second workspace needs
+  HIPCHK(hipMemcpyAsync(c->h_pinned, ctr + CTR_B, 8 * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(c->h_pinned + 4, ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(c->h_pinned + 8, lb, 65 * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  const uint64_t br_bytes = c->h_pinned[0];
-  const uint64_t lf_bytes = c->h_pinned[1];
-  const uint64_t C = (uint32_t)c->h_pinned[2];
+  const uint64_t B = (uint32_t)c->h_pinned[0];
+  const uint64_t br_bytes = c->h_pinned[1];
+  const uint64_t lf_bytes = c->h_pinned[2];
+  const uint64_t C = (uint32_t)c->h_pinned[3];
+  if (c->h_pinned[4]) throw KhError{KH_EINTERNAL, "topology invariant violated (group chain > 15)"};
+  std::vector<uint32_t> lbh(65, 0);
+  memcpy(lbh.data(), c->h_pinned + 8, 65 * 4);
+  if (nb == 0) std::fill(lbh.begin(), lbh.end(), 0u);
 
-  // ---- phase-2 workspace: child records (+ node arena for emission)
-  c->ws2.ensure(carve_size({C * 32, C * 2, A.emit ? lf_bytes + br_bytes + 64 : 0}));
+  // ---- phase-2 workspace: child records + node arena
+  c->ws2.ensure(carve_size({C * 32, C * 2, lf_bytes + br_bytes + 64}));
   Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
   T.cref = cv2.take<uint64_t>(C * 4);
   T.cmeta = cv2.take<uint16_t>(C);
-  T.arena = A.emit ? cv2.take<uint8_t>(lf_bytes + br_bytes + 64) : nullptr;
+  T.arena = cv2.take<uint8_t>(lf_bytes + br_bytes + 64);
   T.br_arena_base = lf_bytes;
-
-  // level order: branches grouped by depth, deepest first
-  std::vector<uint32_t> base(64, 0);
-  {
-    uint32_t run = 0;
-    for (int d = 0; d < 64; ++d) {
-      base[d] = run;
-      run += hist[d];
-    }
-  }
-  if (B > 0) {
-    HIPCHK(hipMemcpyAsync(level_base, base.data(), 64 * 4, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_level_scatter, GRID(B, BS), dim3(BS), 0, st, T, B, (const uint32_t*)level_base, cursor,
-                       order);
-    LAUNCH_CHECK();
-  }
   HIPCHK(hipEventRecord(c->ev[3], st));
 
-  // ---- 4. leaves
-  hipLaunchKernelGGL(k_leaf_emit, GRID(m, BS), dim3(BS), 0, st, T);
+  // ---- 4. leaves: encode into the arena, then hash
+  hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_leaf_hash, GRID(m, BS), dim3(BS), 0, st, T);
   LAUNCH_CHECK();
   HIPCHK(hipEventRecord(c->ev[4], st));
 
-  // ---- 5. branch levels, deepest first
+  // ---- 5. branch levels, deepest first: encode (gathers the children's refs), then hash
   uint32_t levels = 0;
   for (int d = 63; d >= 0; --d) {
-    if (!hist[d]) continue;
-    hipLaunchKernelGGL(k_branch_emit, GRID(hist[d], BS), dim3(BS), 0, st, T, (const uint32_t*)(order + base[d]),
-                       (uint64_t)hist[d]);
+    uint32_t cnt = lbh[d + 1] - lbh[d];
+    if (!cnt) continue;
+    const uint32_t* ord = order + lbh[d];
+    hipLaunchKernelGGL(k_branch_prep, GRID(cnt, BS), dim3(BS), 0, st, T, ord, (uint64_t)cnt);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_branch_hash, GRID(cnt, BS), dim3(BS), 0, st, T, ord, (uint64_t)cnt);
     LAUNCH_CHECK();
     ++levels;
   }
@@ -789,7 +860,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     stats->n_inline = c->h_pinned[CTR_INLINE];
     stats->n_extensions = c->h_pinned[CTR_EXT];
     stats->n_key_perms = (A.flags & KH_HASH_KEYS) ? n * (uint64_t)(A.klen / 136 + 1) : 0;
-    stats->arena_bytes = A.emit ? lf_bytes + br_bytes : 0;
+    stats->arena_bytes = lf_bytes + br_bytes;
     stats->n_levels = levels;
     stats->full_sort = ties ? 1 : 0;
     stats->t_keys_ms = ev_ms(c->ev[0], c->ev[1]);

@@ -430,125 +430,20 @@ KH_HD void op_leaf_topo(const Topo& T, uint64_t i) {
   T.lf_aoff[i] = (L + 7) & ~(uint64_t)7;
 }
 
-// ---- streaming Keccak absorber over a per-thread LDS word buffer
-// The node encoding is produced byte-stream style (RLP headers, HP path, key
-// suffix, value bytes, child references) into `buf` (this thread's words, stride
-// NT words apart so a wave's stores/loads are contiguous and bank-conflict free).
-// Every 17 complete words (one 136-byte rate block) are absorbed and permuted, so
-// no node encoding ever needs to exist in HBM unless write-back emission asks for
-// it (`gdst` non-null: the same words are also stored to the arena).
-constexpr uint32_t STREAM_WORDS = 24;       // branch: 17 + the <= 6 words one child can add + 1
-constexpr uint32_t LEAF_STREAM_WORDS = 18;  // leaf: <= 17 words before each drain
-template <int NT>
-struct Stream {
-  uint64_t* buf;   // buf[w * NT]
-  uint64_t* gdst;  // arena copy (nullable)
-  uint64_t acc;
-  uint32_t fill;   // bytes in acc
-  uint32_t wi;     // complete words in buf
-  uint32_t nblk;   // blocks absorbed
-  KState s;
-  KH_HD void init(uint64_t* b, uint64_t* g) {
-    buf = b;
-    gdst = g;
-    acc = 0;
-    fill = wi = nblk = 0;
-    s = KState{};
-  }
-  KH_HD void word(uint64_t w) {
-    buf[wi * NT] = w;
-    ++wi;
-    if (gdst) *gdst++ = w;
-  }
-  KH_HD void put(uint64_t w, uint32_t nb) {  // nb in [1, 8]; low nb bytes of w
-    w &= low_bytes_mask(nb);
-    uint64_t a = acc | (w << (8 * fill));
-    uint32_t nf = fill + nb;
-    if (nf >= 8) {
-      word(a);
-      acc = fill ? (w >> (8 * (8 - fill))) : 0;
-      nf -= 8;
-    } else {
-      acc = a;
-    }
-    fill = nf;
-  }
-  KH_HD void put1(uint32_t b) { put(b, 1); }
-  KH_HD void len_prefix(uint64_t len, uint32_t offset) {
-    if (len < 56) {
-      put1((uint32_t)(len + offset));
-    } else {
-      uint32_t nb = be_nbytes(len);
-      put1(nb + offset + 55);
-      for (int i = (int)nb - 1; i >= 0; --i) put1((uint32_t)(len >> (8 * i)) & 0xFF);
-    }
-  }
-  KH_HD void key_suffix(const Key4& k, uint32_t from) {
-    while (from < 32) {
-      uint32_t nb = 8 - (from & 7);
-      put(key_word(k, from >> 3) >> (8 * (from & 7)), nb);
-      from += nb;
-    }
-  }
-  KH_HD void ref(const uint64_t r[4], uint32_t len) {  // child reference: hash or inline bytes
-    if (len == 32) {
-      put1(0xA0);
-      put(r[0], 8);
-      put(r[1], 8);
-      put(r[2], 8);
-      put(r[3], 8);
-    } else {
-      for (int j = 0; j < 4 && len; ++j) {
-        uint32_t nb = len < 8 ? len : 8;
-        put(r[j], nb);
-        len -= nb;
-      }
-    }
-  }
-  // absorb every complete 136-byte block in the buffer (one call site per kernel)
-  KH_HD void drain() {
-    while (wi >= 17) {
-#pragma unroll
-      for (int i = 0; i < 17; ++i) kxor(s, i, buf[i * NT]);
-      keccakf(s);
-      for (uint32_t q = 17; q < wi; ++q) buf[(q - 17) * NT] = buf[q * NT];
-      wi -= 17;
-      ++nblk;
-    }
-  }
-  // the first 4 words of a message shorter than 32 bytes (before finish())
-  KH_HD void head(uint64_t w[4]) const {
-    for (int j = 0; j < 4; ++j) w[j] = (uint32_t)j < wi ? buf[j * NT] : ((uint32_t)j == wi ? acc : 0);
-  }
-  // pad and absorb the last block; returns kec256 in h, permutations spent
-  KH_HD uint32_t finish(uint64_t h[4]) {
-    if (gdst && fill) *gdst = acc;
-    uint64_t last = acc ^ (0x01ULL << (8 * fill));
-    buf[wi * NT] = last;
-    uint32_t nw = wi + 1;
-#pragma unroll
-    for (int i = 0; i < 17; ++i) {
-      uint64_t w = (uint32_t)i < nw ? buf[i * NT] : 0;
-      if (i == 16) w ^= 0x80ULL << 56;
-      kxor(s, i, w);
-    }
-    keccakf(s);
-    h[0] = lane(s, 0);
-    h[1] = lane(s, 1);
-    h[2] = lane(s, 2);
-    h[3] = lane(s, 3);
-    return nblk + 1;
-  }
-};
+// ---- node hashing is split in two kernels per node set:
+//   prep: RLP-encode the node into its arena slot (memory-bound, many waves in
+//         flight to hide the gathers of values / child references),
+//   hash: Keccak-256 of the arena bytes (aligned, independent loads; VALU-bound)
+// and the hash step publishes the node's reference into its parent's child record.
 
 // ---- publishing a finished node's reference into its parent's child record or
-// the segment result.  head: the encoding's first 4 words (used when L < 32).
+// the segment result.  enc: the node's encoding in the arena (used when L < 32).
 KH_HD void publish_ref(const Topo& T, uint32_t parent, uint32_t pord, uint32_t nib, uint64_t first_key,
-                       const uint64_t head[4], uint32_t L, const uint64_t h[4]) {
+                       const uint64_t* enc, uint32_t L, const uint64_t h[4]) {
   uint64_t w[4];
   for (int j = 0; j < 4; ++j) {
     uint32_t base = 8u * (uint32_t)j;
-    w[j] = L >= 32 ? h[j] : (base < L ? (head[j] & low_bytes_mask(L - base < 8 ? L - base : 8)) : 0);
+    w[j] = L >= 32 ? h[j] : (base < L ? (enc[j] & low_bytes_mask(L - base < 8 ? L - base : 8)) : 0);
   }
   if (parent == NONE) {
     uint32_t r = result_index(T, first_key);
@@ -564,10 +459,31 @@ KH_HD void publish_ref(const Topo& T, uint32_t parent, uint32_t pord, uint32_t n
   }
 }
 
-// ---- stage: leaf encode + hash (thread per leaf).  Returns permutations spent
-// (0 for an inline leaf: the reference never hashes a node it embeds).
-template <int NT>
-KH_HD uint32_t op_leaf_emit(const Topo& T, uint64_t i, uint64_t* lbuf, uint32_t* inl) {
+// Keccak-256 of an arena message, skipped for an inline (< 32 B) non-top node: the
+// reference never hashes a node it embeds.  Returns permutations spent.
+KH_HD uint32_t hash_node(const uint64_t* enc, uint32_t L, bool top, uint64_t h[4]) {
+  if (L < 32 && !top) {
+    h[0] = h[1] = h[2] = h[3] = 0;
+    return 0;
+  }
+  kec256_msg<true>((const uint8_t*)enc, L, h);
+  return perms_for_len(L);
+}
+
+KH_HD void bw_ref(BW& w, const uint64_t r[4], uint32_t len) {  // child reference: 0xa0+hash or inline bytes
+  if (len == 32) {
+    w.put1(0xA0);
+    w.put(r[0], 8);
+    w.put(r[1], 8);
+    w.put(r[2], 8);
+    w.put(r[3], 8);
+  } else {
+    w.words(r, len);
+  }
+}
+
+// ---- leaf prep: [HP(path, leaf), value] into the arena (thread per leaf)
+KH_HD void op_leaf_prep(const Topo& T, uint64_t i) {
   Key4 k = load_key(T.skey, i);
   int32_t pd = T.lf_pd[i];
   uint32_t s = (uint32_t)(pd + 1);
@@ -579,136 +495,97 @@ KH_HD uint32_t op_leaf_emit(const Topo& T, uint64_t i, uint64_t* lbuf, uint32_t*
   uint32_t hp0 = (p & 1) ? (0x30u | key_nibble(k, (int)s)) : 0x20u;
   uint64_t hpl = h == 1 ? 1 : 1 + h;
   uint64_t payload = hpl + rlp_str_len(vlen, v0);
-  uint32_t L = (uint32_t)(rlp_hdr_len(payload) + payload);
-  // issue every load of the value up front (one exposed memory latency, not one per word)
-  constexpr uint32_t NVW = 14;
-  const uint64_t* vq = (const uint64_t*)((uintptr_t)vp & ~(uintptr_t)7);
-  const uint32_t voffb = (uint32_t)((uintptr_t)vp & 7);
-  const uint64_t vwords = (voffb + vlen + 7) / 8;
-  uint64_t vw[NVW];
-#pragma unroll
-  for (uint32_t q = 0; q < NVW; ++q) vw[q] = q < vwords ? vq[q] : 0;
-  Stream<NT> w;
-  w.init(lbuf, T.arena ? (uint64_t*)(T.arena + T.lf_aoff[i]) : nullptr);
+  BW w{(uint64_t*)(T.arena + T.lf_aoff[i]), 0, 0};
   w.len_prefix(payload, 0xC0);
   if (h > 1) w.put1(0x80 + h);
   w.put1(hp0);
   w.key_suffix(k, (s + 1) / 2);
   if (!(vlen == 1 && v0 < 0x80)) w.len_prefix(vlen, 0x80);
-  if (L <= 135 && vwords <= NVW) {
-    // one-block leaf (every account leaf): straight from registers, no drain needed
-#pragma unroll
-    for (uint32_t q = 0; q + 1 < NVW; ++q) {
-      if (8 * q < vlen) {
-        uint64_t x = voffb ? ((vw[q] >> (8 * voffb)) | (vw[q + 1] << (64 - 8 * voffb))) : vw[q];
-        uint64_t rem = vlen - 8 * q;
-        w.put(x, rem < 8 ? (uint32_t)rem : 8);
-      }
-    }
-  } else {
-    // long value: stream it, absorbing each full block as it completes
-    while (vlen) {
-      uint32_t nb = vlen < 8 ? (uint32_t)vlen : 8;
-      w.put(load64u_n(vp, nb), nb);
-      vp += nb;
-      vlen -= nb;
-      if (w.wi >= 17) w.drain();
-    }
-  }
-  T.lf_len[i] = L;
-  bool top = T.lf_parent[i] == NONE;
-  uint64_t head[4], hh[4] = {0, 0, 0, 0};
-  w.head(head);
-  uint32_t perms = 0;
-  if (L >= 32 || top) perms = w.finish(hh);
+  w.bytes(vp, vlen);
+  w.flush();
+  T.lf_len[i] = (uint32_t)(rlp_hdr_len(payload) + payload);
+}
+
+// ---- leaf hash (thread per leaf).  Returns permutations spent.
+KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
+  const uint64_t* enc = (const uint64_t*)(T.arena + T.lf_aoff[i]);
+  uint32_t L = T.lf_len[i];
+  uint32_t parent = T.lf_parent[i];
+  bool top = parent == NONE;
+  uint64_t hh[4];
+  uint32_t perms = hash_node(enc, L, top, hh);
   if (T.lf_hash)
     for (int j = 0; j < 4; ++j) T.lf_hash[4 * i + j] = hh[j];
-  uint32_t nib = top ? 0 : key_nibble(k, pd);
-  publish_ref(T, T.lf_parent[i], T.lf_pord[i], nib, i, head, L, hh);
+  uint32_t nib = 0;
+  if (!top) {
+    uint32_t pd = (uint32_t)T.lf_pd[i];
+    uint32_t b = (uint32_t)(T.skey[4 * i + (pd >> 4)] >> (8 * ((pd >> 1) & 7))) & 0xFF;
+    nib = (pd & 1) ? (b & 0xF) : (b >> 4);
+  }
+  publish_ref(T, parent, T.lf_pord[i], nib, i, enc, L, hh);
   *inl = (L < 32 && !top) ? 1 : 0;
   return perms;
 }
 
-// ---- stage: branch (+ extension) encode + hash (thread per branch of one level)
-template <int NT>
-KH_HD uint32_t op_branch_emit(const Topo& T, uint32_t j, uint64_t* lbuf, uint32_t* inl) {
+// ---- branch prep: [ref_0 .. ref_15, ""] into the arena (thread per branch of one level)
+KH_HD void op_branch_prep(const Topo& T, uint32_t j) {
   uint32_t k = T.br_k[j];
   uint64_t cb = T.br_cbase[j];
+  const uint16_t* cm = T.cmeta + cb;
   uint32_t payload = 1 + (16 - k);  // terminator "" + empty slots
   for (uint32_t c = 0; c < k; ++c) {
-    uint32_t len = T.cmeta[cb + c] & 0xFF;
+    uint32_t len = cm[c] & 0xFF;
     payload += (len == 32) ? 33 : len;
   }
-  uint32_t L = rlp_hdr_len(payload) + payload;
-  uint64_t* garena = T.arena ? (uint64_t*)(T.arena + T.br_arena_base + T.br_aoff[j]) : nullptr;
-  Stream<NT> w;
-  w.init(lbuf, garena);
+  BW w{(uint64_t*)(T.arena + T.br_arena_base + T.br_aoff[j]), 0, 0};
   w.len_prefix(payload, 0xC0);
-  // walk the children in nibble order; each child's reference is loaded two
-  // children ahead so its memory latency overlaps the encoding/absorbing work
   const uint64_t* cr = T.cref + 4 * cb;
-  const uint16_t* cm = T.cmeta + cb;
-  uint64_t ra[4] = {0, 0, 0, 0}, rb[4] = {0, 0, 0, 0};
-  uint32_t ma = 0, mb = 0;
-  if (k > 0) {
-    ma = cm[0];
-    ra[0] = cr[0]; ra[1] = cr[1]; ra[2] = cr[2]; ra[3] = cr[3];
-  }
-  if (k > 1) {
-    mb = cm[1];
-    rb[0] = cr[4]; rb[1] = cr[5]; rb[2] = cr[6]; rb[3] = cr[7];
-  }
   int32_t prev = -1;
-  for (uint32_t c = 0; c <= k; ++c) {  // c == k: trailing empty slots + the "" terminator
-    uint64_t cur[4] = {ra[0], ra[1], ra[2], ra[3]};
-    uint32_t mc = c < k ? ma : (16u << 8);
-    ra[0] = rb[0]; ra[1] = rb[1]; ra[2] = rb[2]; ra[3] = rb[3];
-    ma = mb;
-    if (c + 2 < k) {
-      const uint64_t* p2 = cr + 4 * (c + 2);
-      mb = cm[c + 2];
-      rb[0] = p2[0]; rb[1] = p2[1]; rb[2] = p2[2]; rb[3] = p2[3];
-    }
+  for (uint32_t c = 0; c < k; ++c) {
+    uint32_t mc = cm[c];
     int32_t nib = (int32_t)(mc >> 8);
     for (int32_t e = prev + 1; e < nib; ++e) w.put1(0x80);  // empty slots
     prev = nib;
-    if (c < k)
-      w.ref(cur, mc & 0xFF);
-    else
-      w.put1(0x80);  // terminator (secure tries never store a value in a branch)
-    if (w.wi >= 17) w.drain();
+    uint64_t r[4] = {cr[4 * c], cr[4 * c + 1], cr[4 * c + 2], cr[4 * c + 3]};
+    bw_ref(w, r, mc & 0xFF);
   }
-  T.br_len[j] = L;
+  for (int32_t e = prev + 1; e < 16; ++e) w.put1(0x80);
+  w.put1(0x80);  // terminator (a secure trie never stores a value in a branch)
+  w.flush();
+  T.br_len[j] = rlp_hdr_len(payload) + payload;
+}
+
+// ---- branch hash (+ extension encode + hash) (thread per branch of one level)
+KH_HD uint32_t op_branch_hash(const Topo& T, uint32_t j, uint32_t* inl) {
+  uint32_t k = T.br_k[j];
+  const uint64_t* enc = (const uint64_t*)(T.arena + T.br_arena_base + T.br_aoff[j]);
+  uint32_t L = T.br_len[j];
   uint32_t ext = T.br_ext[j];
   uint32_t parent = T.br_parent[j];
   uint64_t first = T.br_first[j];
   uint32_t d = T.br_depth[j];
   int32_t pd = (int32_t)d - (int32_t)ext - 1;
   bool top = parent == NONE;
-  uint64_t bhead[4], hb[4] = {0, 0, 0, 0};
-  w.head(bhead);
-  uint32_t perms = 0;
-  bool hash_b = L >= 32 || (top && ext == 0);
-  if (hash_b) perms = w.finish(hb);
+  uint64_t hb[4];
+  uint32_t perms = hash_node(enc, L, top && ext == 0, hb);
   uint32_t ninl = (L < 32 && !(top && ext == 0)) ? 1 : 0;
   if (T.br_hash)
     for (int q = 0; q < 4; ++q) T.br_hash[4 * j + q] = hb[q];
   Key4 key = load_key(T.skey, first);
   uint32_t nib = top ? 0 : key_nibble(key, pd);
   if (ext == 0) {
-    publish_ref(T, parent, T.br_pord[j], nib, first, bhead, L, hb);
+    publish_ref(T, parent, T.br_pord[j], nib, first, enc, L, hb);
     *inl = ninl;
     return perms;
   }
-  // extension: [HP(nibbles pd+1 .. d-1, ext), ref(branch)] (<= 70 bytes: one block)
+  // extension: [HP(nibbles pd+1 .. d-1, ext), ref(branch)], written after the branch slot
+  uint64_t* xenc = (uint64_t*)((uint8_t*)enc + branch_bound(k));
   uint32_t s = (uint32_t)(pd + 1);
   uint32_t hl = ext / 2 + 1;  // HP bytes
   uint32_t refl = L >= 32 ? 33 : L;
   uint32_t hpl = hl == 1 ? 1 : 1 + hl;  // first HP byte 0x00 / 0x1_ < 0x80
   uint32_t xpay = hpl + refl;
-  uint32_t XL = rlp_hdr_len(xpay) + xpay;
-  Stream<NT> x;
-  x.init(lbuf, garena ? (uint64_t*)((uint8_t*)garena + branch_bound(k)) : nullptr);
+  BW x{xenc, 0, 0};
   x.len_prefix(xpay, 0xC0);
   if (hl > 1) x.put1(0x80 + hl);
   uint32_t q = s;
@@ -720,16 +597,17 @@ KH_HD uint32_t op_branch_emit(const Topo& T, uint32_t j, uint64_t* lbuf, uint32_
   }
   for (; q < d; q += 2) x.put1((key_nibble(key, (int)q) << 4) | key_nibble(key, (int)q + 1));
   uint64_t bref[4];
-  for (int t = 0; t < 4; ++t) bref[t] = L >= 32 ? hb[t] : bhead[t];
-  x.ref(bref, L >= 32 ? 32 : L);
+  for (int t = 0; t < 4; ++t) bref[t] = L >= 32 ? hb[t] : enc[t];
+  bw_ref(x, bref, L >= 32 ? 32 : L);
+  x.flush();
+  uint32_t XL = rlp_hdr_len(xpay) + xpay;
   T.ex_len[j] = XL;
-  uint64_t xhead[4], hx[4] = {0, 0, 0, 0};
-  x.head(xhead);
-  if (XL >= 32 || top) perms += x.finish(hx);
+  uint64_t hx[4];
+  perms += hash_node(xenc, XL, top, hx);
   if (T.ex_hash)
     for (int q2 = 0; q2 < 4; ++q2) T.ex_hash[4 * j + q2] = hx[q2];
   ninl += (XL < 32 && !top) ? 1 : 0;
-  publish_ref(T, parent, T.br_pord[j], nib, first, xhead, XL, hx);
+  publish_ref(T, parent, T.br_pord[j], nib, first, xenc, XL, hx);
   *inl = ninl;
   return perms;
 }

@@ -72,13 +72,17 @@ def all_cases(seed=11, big=True):
                                                                                            300, 1000])))
                                       for _ in ks]))
     cases.append(("empty_values", ks[:5], [b""] * 5))
-    # first 8 bytes equal -> 64-bit prefix ties -> full-key sort path
+    # first 8 bytes equal -> a run of 64 equal sort prefixes, fixed locally (k_tie_fix)
     pre = _rk(r)[:8]
     ks = [pre + _rk(r)[8:] for _ in range(64)] + [_rk(r) for _ in range(64)]
     cases.append(("prefix_ties", ks, [account_value(r) for _ in ks]))
     ks = [pre + _rk(r)[8:] for _ in range(10)]
     ks = ks + ks[:4]
     cases.append(("prefix_ties_dups", ks, [storage_value(r) for _ in ks]))
+    # a run longer than TIE_RUN_MAX (64) -> the full 256-bit sort path
+    ks = [pre[:4] + _rk(r)[4:] for _ in range(150)] + [_rk(r) for _ in range(30)]
+    ks = ks + ks[5:9]
+    cases.append(("prefix_ties_long", ks, [storage_value(r) for _ in ks]))
     return cases
 
 

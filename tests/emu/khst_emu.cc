@@ -174,25 +174,27 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
   T.arena = (uint8_t*)arena.data();
   T.br_arena_base = lfb;
   uint64_t perms = 0, hashes = 0, inl = 0;
+  for (uint64_t i = 0; i < m; ++i) op_leaf_prep(T, i);
   for (uint64_t i = 0; i < m; ++i) {
     uint32_t in1 = 0;
-    uint64_t lb[LEAF_STREAM_WORDS];
-    uint32_t p = op_leaf_emit<1>(T, i, lb, &in1);
+    uint32_t p = op_leaf_hash(T, i, &in1);
     perms += p;
     hashes += p ? 1 : 0;
     inl += in1;
   }
-  for (int d = 63; d >= 0; --d)
+  for (int d = 63; d >= 0; --d) {
+    for (uint64_t j = 0; j < B; ++j)
+      if (br_depth[j] == d) op_branch_prep(T, (uint32_t)j);
     for (uint64_t j = 0; j < B; ++j) {
       if (br_depth[j] != d) continue;
       uint32_t in1 = 0;
-      uint64_t lb[STREAM_WORDS];
-      perms += op_branch_emit<1>(T, (uint32_t)j, lb, &in1);
+      perms += op_branch_hash(T, (uint32_t)j, &in1);
       bool top = br_parent[j] == NONE, ext = br_ext[j] != 0;
       hashes += (br_len[j] >= 32 || (top && !ext)) ? 1 : 0;
       if (ext) hashes += (ex_len[j] >= 32 || top) ? 1 : 0;
       inl += in1;
     }
+  }
   memcpy(out_hash, res_hash.data(), nres * 32);
   memcpy(out_len, res_len.data(), nres * 4);
   memcpy(out_inl, res_inl.data(), nres * 32);

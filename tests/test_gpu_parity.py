@@ -43,8 +43,7 @@ def test_trie_root_vs_oracle(khst, oracle, case):
     st = khst.KhStats()
     got = khst.trie_root(keys, vals, stats=st)
     assert got == oracle.seq_root(keys, vals), name
-    if name.startswith("prefix_ties"):
-        assert st.full_sort == 1
+    assert st.full_sort == (1 if name == "prefix_ties_long" else 0), name
 
 
 def test_trie_root_hash_keys(khst, oracle):
@@ -79,7 +78,7 @@ def test_write_back_node_set(khst, oracle):
     """Emitted (hash -> RLP) == every node reachable from the oracle's root with
     encoding >= 32 B plus the root (MerklePatriciaTrie.scala:505-511)."""
     for name, keys, vals in C.all_cases(big=False):
-        if name in ("duplicates", "prefix_ties_dups"):
+        if name in ("duplicates", "prefix_ties_dups", "prefix_ties_long"):
             continue
         root, nodes = khst.trie_root_nodes(keys, vals)
         t = oracle.Trie()
