@@ -263,12 +263,6 @@ __global__ void __launch_bounds__(BS) k_leaf_topo(Topo T) {
   if (i < T.m) op_leaf_topo(T, i);
 }
 
-// arena bytes per branch id (0 past the last branch, so the scan can run over nb)
-__global__ void __launch_bounds__(BS) k_branch_alen(Topo T, uint64_t nb, const uint32_t* Bp) {
-  uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (j < nb) T.br_aoff[j] = j < *Bp ? branch_arena_bytes(T, (uint32_t)j) : 0;
-}
-
 // Level order (branch ids bucketed by depth) without contended global atomics:
 // per-block depth counts laid out [depth][block], one exclusive scan gives every
 // (depth, block) its base, a second pass ranks inside the block with LDS atomics.
@@ -319,18 +313,19 @@ __global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
   block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
 }
 
-__global__ void __launch_bounds__(BS) k_branch_prep(Topo T, const uint32_t* order, uint64_t cnt) {
+// one level: `first` = its first position in the level order, `cnt` = its size
+__global__ void __launch_bounds__(BS) k_branch_prep(Topo T, const uint32_t* order, uint64_t first, uint64_t cnt) {
   uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (t < cnt) op_branch_prep(T, order[t]);
+  if (t < cnt) op_branch_prep(T, order[first + t], first + t);
 }
 
-__global__ void __launch_bounds__(BS) k_branch_hash(Topo T, const uint32_t* order, uint64_t cnt) {
+__global__ void __launch_bounds__(BS) k_branch_hash(Topo T, const uint32_t* order, uint64_t first, uint64_t cnt) {
   uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (t < cnt) {
-    uint32_t j = order[t];
+    uint32_t j = order[first + t];
     uint32_t in1 = 0;
-    perms = op_branch_hash(T, j, &in1);
+    perms = op_branch_hash(T, j, first + t, &in1);
     // hashes: the branch if its encoding is >= 32 B or it is the top; its extension likewise
     uint32_t L = T.br_len[j];
     bool top = T.br_parent[j] == NONE;
@@ -342,13 +337,20 @@ __global__ void __launch_bounds__(BS) k_branch_hash(Topo T, const uint32_t* orde
   block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
 }
 
-// write-back emission: node q in [0, m + 2B): leaf q, or branch / extension of branch (q-m)/2
-__device__ __forceinline__ bool emit_node(const Topo& T, uint64_t B, uint64_t q, uint64_t* aoff, uint32_t* len,
-                                          const uint64_t** hash) {
+// write-back emission: node q in [0, m + 2B): leaf q, or branch / extension of branch (q-m)/2.
+// src/stride: the node's message words (stride m for one-block leaves, 1 otherwise).
+__device__ __forceinline__ bool emit_node(const Topo& T, uint64_t B, uint64_t q, const uint64_t** src,
+                                          uint64_t* stride, uint32_t* len, const uint64_t** hash) {
+  *stride = 1;
   if (q < T.m) {
     uint32_t L = T.lf_len[q];
     bool top = T.lf_parent[q] == NONE;
-    *aoff = T.lf_aoff[q];
+    if (L <= LEAF_SHORT_MAX) {
+      *src = T.lmsg + q;
+      *stride = T.lstride;
+    } else {
+      *src = (const uint64_t*)(T.arena + T.lf_aoff[q]);
+    }
     *len = L;
     *hash = T.lf_hash + 4 * q;
     return L >= 32 || top;
@@ -356,16 +358,18 @@ __device__ __forceinline__ bool emit_node(const Topo& T, uint64_t B, uint64_t q,
   uint64_t j = (q - T.m) >> 1;
   bool top = T.br_parent[j] == NONE;
   bool has_ext = T.br_ext[j] != 0;
-  if (((q - T.m) & 1) == 0) {
+  bool is_ext = ((q - T.m) & 1) != 0;
+  if (is_ext && !has_ext) return false;
+  Slot sl = branch_slot(T, T.br_aoff[j], T.br_depth[j], is_ext);
+  *src = sl.w;
+  *stride = sl.stride;
+  if (!is_ext) {
     uint32_t L = T.br_len[j];
-    *aoff = T.br_arena_base + T.br_aoff[j];
     *len = L;
     *hash = T.br_hash + 4 * j;
     return L >= 32 || (top && !has_ext);
   }
-  if (!has_ext) return false;
   uint32_t L = T.ex_len[j];
-  *aoff = T.br_arena_base + T.br_aoff[j] + branch_bound(T.br_k[j]);
   *len = L;
   *hash = T.ex_hash + 4 * j;
   return L >= 32 || top;
@@ -374,10 +378,11 @@ __device__ __forceinline__ bool emit_node(const Topo& T, uint64_t B, uint64_t q,
 __global__ void __launch_bounds__(BS) k_emit_sizes(Topo T, uint64_t B, uint32_t* flag, uint64_t* bytes) {
   uint64_t q = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (q >= T.m + 2 * B) return;
-  uint64_t aoff;
+  const uint64_t* src;
+  uint64_t stride;
   uint32_t len;
   const uint64_t* h;
-  bool e = emit_node(T, B, q, &aoff, &len, &h);
+  bool e = emit_node(T, B, q, &src, &stride, &len, &h);
   flag[q] = e ? 1 : 0;
   bytes[q] = e ? len : 0;
 }
@@ -386,16 +391,16 @@ __global__ void __launch_bounds__(BS) k_emit_copy(Topo T, uint64_t B, const uint
                                                   uint8_t* out_hash, uint8_t* out_rlp, uint64_t* out_off) {
   uint64_t q = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (q >= T.m + 2 * B) return;
-  uint64_t aoff;
+  const uint64_t* src;
+  uint64_t stride;
   uint32_t len;
   const uint64_t* h;
-  if (!emit_node(T, B, q, &aoff, &len, &h)) return;
+  if (!emit_node(T, B, q, &src, &stride, &len, &h)) return;
   uint64_t p = pos[q];
   uint64_t* oh = (uint64_t*)(out_hash + 32 * p);
   for (int j = 0; j < 4; ++j) oh[j] = h[j];
-  const uint8_t* src = T.arena + aoff;
   uint8_t* dst = out_rlp + boff[q];
-  for (uint32_t b = 0; b < len; ++b) dst[b] = src[b];
+  for (uint32_t b = 0; b < len; ++b) dst[b] = (uint8_t)(src[(b >> 3) * stride] >> (8 * (b & 7)));
   out_off[p] = boff[q];
 }
 
@@ -790,11 +795,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     hipLaunchKernelGGL(k_level_bounds, dim3(1), dim3(64), 0, st, (const uint32_t*)bcnt, nblk, (const uint32_t*)Bp,
                        lb);
     LAUNCH_CHECK();
-    // child record bases and branch arena offsets
+    // child record bases
     scan_exclusive<uint32_t>(T.br_k, T.br_cbase, nb, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
-    hipLaunchKernelGGL(k_branch_alen, GRID(nb, BS), dim3(BS), 0, st, T, nb, (const uint32_t*)Bp);
-    LAUNCH_CHECK();
-    scan_exclusive<uint64_t>(T.br_aoff, T.br_aoff, nb, (uint64_t*)(ctr + CTR_BRBYTES), scan_scratch, st);
   }
   hipLaunchKernelGGL(k_leaf_topo, GRID(m, BS), dim3(BS), 0, st, T);
   LAUNCH_CHECK();
@@ -805,7 +807,6 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   HIPCHK(hipMemcpyAsync(c->h_pinned + 8, lb, 65 * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const uint64_t B = (uint32_t)c->h_pinned[0];
-  const uint64_t br_bytes = c->h_pinned[1];
   const uint64_t lf_bytes = c->h_pinned[2];
   const uint64_t C = (uint32_t)c->h_pinned[3];
   if (c->h_pinned[4]) throw KhError{KH_EINTERNAL, "topology invariant violated (group chain > 15)"};
@@ -814,12 +815,17 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   if (nb == 0) std::fill(lbh.begin(), lbh.end(), 0u);
 
   // ---- phase-2 workspace: child records + node arena
-  c->ws2.ensure(carve_size({C * 32, C * 2, lf_bytes + br_bytes + 64}));
+  c->ws2.ensure(carve_size({C * 32, C * 2, (uint64_t)LEAF_WORDS * 8 * m, lf_bytes + 64, (uint64_t)BR_WORDS * 8 * B,
+                            (uint64_t)EXT_WORDS * 8 * B}));
   Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
   T.cref = cv2.take<uint64_t>(C * 4);
   T.cmeta = cv2.take<uint16_t>(C);
-  T.arena = cv2.take<uint8_t>(lf_bytes + br_bytes + 64);
-  T.br_arena_base = lf_bytes;
+  T.lmsg = cv2.take<uint64_t>((uint64_t)LEAF_WORDS * m);
+  T.lstride = m;
+  T.arena = cv2.take<uint8_t>(lf_bytes + 64);  // long leaves
+  T.bmsg = cv2.take<uint64_t>((uint64_t)BR_WORDS * B);
+  T.xmsg = cv2.take<uint64_t>((uint64_t)EXT_WORDS * B);
+  T.lb = lb;
   HIPCHK(hipEventRecord(c->ev[3], st));
 
   // ---- 4. leaves: encode into the arena, then hash
@@ -834,10 +840,11 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   for (int d = 63; d >= 0; --d) {
     uint32_t cnt = lbh[d + 1] - lbh[d];
     if (!cnt) continue;
-    const uint32_t* ord = order + lbh[d];
-    hipLaunchKernelGGL(k_branch_prep, GRID(cnt, BS), dim3(BS), 0, st, T, ord, (uint64_t)cnt);
+    hipLaunchKernelGGL(k_branch_prep, GRID(cnt, BS), dim3(BS), 0, st, T, (const uint32_t*)order, (uint64_t)lbh[d],
+                       (uint64_t)cnt);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_branch_hash, GRID(cnt, BS), dim3(BS), 0, st, T, ord, (uint64_t)cnt);
+    hipLaunchKernelGGL(k_branch_hash, GRID(cnt, BS), dim3(BS), 0, st, T, (const uint32_t*)order, (uint64_t)lbh[d],
+                       (uint64_t)cnt);
     LAUNCH_CHECK();
     ++levels;
   }
@@ -860,7 +867,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     stats->n_inline = c->h_pinned[CTR_INLINE];
     stats->n_extensions = c->h_pinned[CTR_EXT];
     stats->n_key_perms = (A.flags & KH_HASH_KEYS) ? n * (uint64_t)(A.klen / 136 + 1) : 0;
-    stats->arena_bytes = lf_bytes + br_bytes;
+    stats->arena_bytes = (uint64_t)LEAF_WORDS * 8 * m + lf_bytes + (uint64_t)(BR_WORDS + EXT_WORDS) * 8 * B;
     stats->n_levels = levels;
     stats->full_sort = ties ? 1 : 0;
     stats->t_keys_ms = ev_ms(c->ev[0], c->ev[1]);

@@ -79,17 +79,21 @@ KH_HD uint64_t rlp_str_len(uint64_t len, uint32_t b0) {
   return rlp_hdr_len(len) + len;
 }
 
-// ---- byte writer into an 8-byte-aligned buffer (whole-word stores)
+// ---- byte writer into an 8-byte-aligned buffer (whole-word stores); consecutive
+// words are `stride` words apart (1: packed; m: the transposed leaf layout)
 struct BW {
   uint64_t* dst;
   uint64_t acc;
   uint32_t fill;
+  uint64_t stride;
+  KH_HD BW(uint64_t* d, uint64_t s = 1) : dst(d), acc(0), fill(0), stride(s) {}
   KH_HD void put(uint64_t w, uint32_t nb) {  // nb in [1, 8]; low nb bytes of w
     w &= low_bytes_mask(nb);
     acc |= w << (8 * fill);
     uint32_t nf = fill + nb;
     if (nf >= 8) {
-      *dst++ = acc;
+      *dst = acc;
+      dst += stride;
       acc = fill ? (w >> (8 * (8 - fill))) : 0;
       nf -= 8;
     }
@@ -165,15 +169,17 @@ struct Topo {
   uint32_t* br_parent;    // parent branch id or NONE (top of a segment)
   uint8_t* br_pord;       // ordinal in parent
   uint32_t* br_first;     // first key index of the branch's range
-  uint64_t* br_aoff;      // arena bytes reserved, scanned in place into the arena offset
-                          // (the extension follows the branch at +branch_bound(k))
+  uint64_t* br_aoff;      // position of the branch in the level order (message slot)
   uint32_t* br_len;       // encoding length of the branch
   uint32_t* ex_len;       // encoding length of the extension
   // leaves
   uint32_t* lf_parent;
   uint8_t* lf_pord;
   int8_t* lf_pd;          // parent depth (depth0-1 for a top leaf)
-  uint64_t* lf_aoff;      // aligned length, scanned in place into the arena offset
+  uint64_t* lf_aoff;      // long leaves (> 135 B): aligned length, scanned into the
+                          // offset in the packed long-leaf region at `arena`
+  uint64_t* lmsg;         // one-block leaves: word q of leaf i at lmsg[q * lstride + i]
+  uint64_t lstride;       //   (transposed: a wave's store / load of word q is contiguous)
   uint32_t* lf_len;
   // child references: 32 B each + meta (len | nibble << 8); len 32 = hash
   uint64_t* cref;
@@ -182,9 +188,12 @@ struct Topo {
   uint64_t* lf_hash;
   uint64_t* br_hash;
   uint64_t* ex_hash;
-  // arena
-  uint8_t* arena;
-  uint64_t br_arena_base;  // branch region starts here
+  // message stores
+  uint8_t* arena;          // long leaves (> 135 B), packed
+  uint64_t* bmsg;          // branch messages: level d's t-th branch, word q at
+                           //   bmsg[BR_WORDS * lb[d] + q * cnt_d + t]  (transposed per level)
+  uint64_t* xmsg;          // extension messages, same scheme with EXT_WORDS
+  const uint32_t* lb;      // [65] first order position of each depth (lb[64] = B)
   // per-result outputs
   uint64_t* res_hash;  // [nres*4]
   uint32_t* res_len;   // [nres]
@@ -201,8 +210,24 @@ enum {
   CTR_N = 16
 };
 
+constexpr uint32_t LEAF_SHORT_MAX = 135;  // one Keccak block: the transposed leaf layout
+constexpr uint32_t LEAF_WORDS = 17;
+
 KH_HD uint32_t branch_bound(uint32_t k) { return 24 + 32 * k; }  // >= 3 + 33k + (16-k) + 1, 8-aligned
 constexpr uint32_t EXT_BOUND = 72;                               // >= 2 + 33 + 33
+constexpr uint32_t BR_WORDS = 67;                                // branch_bound(16) / 8
+constexpr uint32_t EXT_WORDS = EXT_BOUND / 8;
+
+// message slot of branch j (its position g in the level order): word-0 pointer + stride
+struct Slot {
+  uint64_t* w;
+  uint64_t stride;
+};
+KH_HD Slot branch_slot(const Topo& T, uint64_t g, uint32_t d, bool ext) {
+  uint64_t first = T.lb[d], cnt = T.lb[d + 1] - first;
+  uint64_t* base = ext ? T.xmsg + (uint64_t)EXT_WORDS * first : T.bmsg + (uint64_t)BR_WORDS * first;
+  return Slot{base + (g - first), cnt};
+}
 
 KH_HD uint32_t result_index(const Topo& T, uint64_t first_key) {
   if (T.segmented) return T.sseg[first_key];
@@ -227,38 +252,66 @@ struct Pyr {
   int nl;
 };
 
-// largest j < b with u[j] < t (strict) or <= t; -1 if none
-KH_HD int64_t ansv_left(const Pyr& P, uint64_t b, uint32_t t, bool strict) {
+// SWAR helpers: 8 boundary values (each <= 64 < 128) per 64-bit word.
+// lt_mask(x, t): bit 7 of byte i set iff byte i of x < t, exactly, for bytes <= 127
+// and t in [1, 128]: (x_i | 0x80) - t never borrows across bytes.
+KH_HD uint64_t lt_mask(uint64_t x, uint32_t t) {
+  const uint64_t ones = 0x0101010101010101ULL, highs = 0x8080808080808080ULL;
+  return ~((x | highs) - ones * t) & highs;
+}
+KH_HD int ctz64(uint64_t x) { return x ? __builtin_ctzll(x) : 64; }
+// bytes [lo, hi) of an 8-byte group as a byte-lane mask of bit 7s
+KH_HD uint64_t byte_range_mask(uint32_t lo, uint32_t hi) {
+  uint64_t m_hi = hi >= 8 ? ~0ULL : ((1ULL << (8 * hi)) - 1);
+  uint64_t m_lo = lo >= 8 ? ~0ULL : ((1ULL << (8 * lo)) - 1);
+  return (m_hi & ~m_lo) & 0x8080808080808080ULL;
+}
+// 8 values at level array a starting at 8-aligned index w8 (past the end reads as 127)
+KH_HD uint64_t load8(const uint8_t* a, uint64_t w8, uint64_t sz) {
+  if (w8 + 8 <= sz) return *(const uint64_t*)(a + w8);
+  uint64_t x = 0x7F7F7F7F7F7F7F7FULL;
+  for (uint64_t q = w8; q < sz; ++q) x = (x & ~(0xFFULL << (8 * (q - w8)))) | ((uint64_t)a[q] << (8 * (q - w8)));
+  return x;
+}
+// rightmost index in [lo, hi) of level array a with value < t, or -1
+KH_HD int64_t scan_left(const uint8_t* a, uint64_t sz, uint64_t lo, uint64_t hi, uint32_t t) {
+  while (hi > lo) {
+    uint64_t w8 = (hi - 1) & ~(uint64_t)7;
+    uint64_t from = w8 > lo ? w8 : lo;
+    uint64_t m = lt_mask(load8(a, w8, sz), t) & byte_range_mask((uint32_t)(from - w8), (uint32_t)(hi - w8));
+    if (m) return (int64_t)(w8 + ((63 - clz64(m)) >> 3));
+    hi = from;
+  }
+  return -1;
+}
+// leftmost index in [lo, hi) with value < t, or -1
+KH_HD int64_t scan_right(const uint8_t* a, uint64_t sz, uint64_t lo, uint64_t hi, uint32_t t) {
+  while (lo < hi) {
+    uint64_t w8 = lo & ~(uint64_t)7;
+    uint64_t to = w8 + 8 < hi ? w8 + 8 : hi;
+    uint64_t m = lt_mask(load8(a, w8, sz), t) & byte_range_mask((uint32_t)(lo - w8), (uint32_t)(to - w8));
+    if (m) return (int64_t)(w8 + (ctz64(m) >> 3));
+    lo = to;
+  }
+  return -1;
+}
+
+// largest j < b with u[j] < t; -1 if none (the 64-ary min pyramid bounds each level's
+// scan to one 64-entry block).  "<= t" is "< t+1".
+KH_HD int64_t ansv_left(const Pyr& P, uint64_t b, uint32_t t) {
   uint64_t pos = b;
   int L = 0;
   int64_t found = -1;
   for (; L < P.nl; ++L) {
-    const uint8_t* a = P.lv[L];
-    uint64_t start = pos & ~(uint64_t)63;
-    for (uint64_t j = pos; j > start;) {
-      --j;
-      uint32_t x = a[j];
-      if (strict ? x < t : x <= t) {
-        found = (int64_t)j;
-        break;
-      }
-    }
+    found = scan_left(P.lv[L], P.sz[L], pos & ~(uint64_t)63, pos, t);
     if (found >= 0) break;
     pos >>= 6;
   }
   if (found < 0) return -1;
   for (; L > 0; --L) {
-    const uint8_t* a = P.lv[L - 1];
     uint64_t lo = (uint64_t)found * 64;
-    uint64_t hi = lo + 63 < P.sz[L - 1] - 1 ? lo + 63 : P.sz[L - 1] - 1;
-    for (uint64_t j = hi + 1; j > lo;) {
-      --j;
-      uint32_t x = a[j];
-      if (strict ? x < t : x <= t) {
-        found = (int64_t)j;
-        break;
-      }
-    }
+    uint64_t hi = lo + 64 < P.sz[L - 1] ? lo + 64 : P.sz[L - 1];
+    found = scan_left(P.lv[L - 1], P.sz[L - 1], lo, hi, t);
   }
   return found;
 }
@@ -269,29 +322,17 @@ KH_HD int64_t ansv_right(const Pyr& P, uint64_t b, uint32_t t) {
   int L = 0;
   int64_t found = -1;
   for (; L < P.nl; ++L) {
-    const uint8_t* a = P.lv[L];
     uint64_t end = (pos | 63) + 1;
     if (end > P.sz[L]) end = P.sz[L];
-    for (uint64_t j = pos + 1; j < end; ++j) {
-      if (a[j] < t) {
-        found = (int64_t)j;
-        break;
-      }
-    }
+    found = scan_right(P.lv[L], P.sz[L], pos + 1, end, t);
     if (found >= 0) break;
     pos >>= 6;
   }
   if (found < 0) return -1;
   for (; L > 0; --L) {
-    const uint8_t* a = P.lv[L - 1];
     uint64_t lo = (uint64_t)found * 64;
-    uint64_t hi = lo + 63 < P.sz[L - 1] - 1 ? lo + 63 : P.sz[L - 1] - 1;
-    for (uint64_t j = lo; j <= hi; ++j) {
-      if (a[j] < t) {
-        found = (int64_t)j;
-        break;
-      }
-    }
+    uint64_t hi = lo + 64 < P.sz[L - 1] ? lo + 64 : P.sz[L - 1];
+    found = scan_right(P.lv[L - 1], P.sz[L - 1], lo, hi, t);
   }
   return found;
 }
@@ -309,8 +350,11 @@ KH_HD void op_ansv(const Topo& T, const Pyr& P, uint64_t b) {
     T.psv[b] = T.nsv[b] = T.pse[b] = -1;
     return;
   }
-  T.psv[b] = (int32_t)ansv_left(P, b, t, true);
-  T.pse[b] = (int32_t)ansv_left(P, b, t, false);
+  // previous smaller-or-equal first; it is also the previous strictly smaller one
+  // unless it carries the same value (then keep scanning left from it)
+  int64_t pse = ansv_left(P, b, t + 1);
+  T.pse[b] = (int32_t)pse;
+  T.psv[b] = (int32_t)((pse < 0 || T.u[pse] < t) ? pse : ansv_left(P, (uint64_t)pse, t));
   T.nsv[b] = (int32_t)ansv_right(P, b, t);
 }
 
@@ -389,9 +433,6 @@ KH_HD void op_branch_topo(const Topo& T, uint64_t b) {
   T.br_first[j] = (uint32_t)(a + 1);
 }
 
-KH_HD uint32_t branch_arena_bytes(const Topo& T, uint32_t j) {
-  return branch_bound(T.br_k[j]) + (T.br_ext[j] ? EXT_BOUND : 0);
-}
 
 // ---- leaf geometry
 KH_HD void leaf_value(const Topo& T, uint64_t i, const uint8_t** p, uint64_t* len) {
@@ -427,7 +468,7 @@ KH_HD void op_leaf_topo(const Topo& T, uint64_t i) {
   leaf_value(T, i, &vp, &vlen);
   uint32_t v0 = vlen ? (uint32_t)load64u_n(vp, 1) & 0xFF : 0;
   uint64_t L = leaf_enc_len((uint32_t)(P.pd + 1), vlen, v0);
-  T.lf_aoff[i] = (L + 7) & ~(uint64_t)7;
+  T.lf_aoff[i] = L > LEAF_SHORT_MAX ? (L + 7) & ~(uint64_t)7 : 0;
 }
 
 // ---- node hashing is split in two kernels per node set:
@@ -469,6 +510,18 @@ KH_HD uint32_t hash_node(const uint64_t* enc, uint32_t L, bool top, uint64_t h[4
   kec256_msg<true>((const uint8_t*)enc, L, h);
   return perms_for_len(L);
 }
+KH_HD void kec256_strided(const uint64_t* w, uint64_t stride, uint32_t len, uint64_t out[4]);
+KH_HD uint32_t hash_slot(const Slot& sl, uint32_t L, bool top, uint64_t h[4]) {
+  if (L < 32 && !top) {
+    h[0] = h[1] = h[2] = h[3] = 0;
+    return 0;
+  }
+  kec256_strided(sl.w, sl.stride, L, h);
+  return perms_for_len(L);
+}
+KH_HD void slot_head(const Slot& sl, uint32_t L, uint64_t head[4]) {
+  for (int q = 0; q < 4; ++q) head[q] = (8u * q < L) ? sl.w[q * sl.stride] : 0;
+}
 
 KH_HD void bw_ref(BW& w, const uint64_t r[4], uint32_t len) {  // child reference: 0xa0+hash or inline bytes
   if (len == 32) {
@@ -482,7 +535,7 @@ KH_HD void bw_ref(BW& w, const uint64_t r[4], uint32_t len) {  // child referenc
   }
 }
 
-// ---- leaf prep: [HP(path, leaf), value] into the arena (thread per leaf)
+// ---- leaf prep: [HP(path, leaf), value] into the message store (thread per leaf)
 KH_HD void op_leaf_prep(const Topo& T, uint64_t i) {
   Key4 k = load_key(T.skey, i);
   int32_t pd = T.lf_pd[i];
@@ -495,7 +548,8 @@ KH_HD void op_leaf_prep(const Topo& T, uint64_t i) {
   uint32_t hp0 = (p & 1) ? (0x30u | key_nibble(k, (int)s)) : 0x20u;
   uint64_t hpl = h == 1 ? 1 : 1 + h;
   uint64_t payload = hpl + rlp_str_len(vlen, v0);
-  BW w{(uint64_t*)(T.arena + T.lf_aoff[i]), 0, 0};
+  uint32_t L = (uint32_t)(rlp_hdr_len(payload) + payload);
+  BW w = L <= LEAF_SHORT_MAX ? BW(T.lmsg + i, T.lstride) : BW((uint64_t*)(T.arena + T.lf_aoff[i]), 1);
   w.len_prefix(payload, 0xC0);
   if (h > 1) w.put1(0x80 + h);
   w.put1(hp0);
@@ -503,17 +557,55 @@ KH_HD void op_leaf_prep(const Topo& T, uint64_t i) {
   if (!(vlen == 1 && v0 < 0x80)) w.len_prefix(vlen, 0x80);
   w.bytes(vp, vlen);
   w.flush();
-  T.lf_len[i] = (uint32_t)(rlp_hdr_len(payload) + payload);
+  T.lf_len[i] = L;
+}
+
+// Keccak-256 of a message whose words are `stride` words apart (any length)
+KH_HD void kec256_strided(const uint64_t* w, uint64_t stride, uint32_t len, uint64_t out[4]) {
+  KState s = {};
+  uint32_t nfull = len / 136;
+  for (uint32_t b = 0; b < nfull; ++b) {
+#pragma unroll
+    for (int q = 0; q < 17; ++q) kxor(s, q, w[q * stride]);
+    keccakf(s);
+    w += 17 * stride;
+  }
+  len -= nfull * 136;
+#pragma unroll
+  for (int q = 0; q < 17; ++q) {
+    uint64_t x = 0;
+    uint32_t base = 8u * (uint32_t)q;
+    if (base < len) x = w[q * stride] & low_bytes_mask(len - base < 8 ? len - base : 8);
+    if ((len >> 3) == (uint32_t)q) x ^= 0x01ULL << (8 * (len & 7));
+    if (q == 16) x ^= 0x80ULL << 56;
+    kxor(s, q, x);
+  }
+  keccakf(s);
+  out[0] = lane(s, 0);
+  out[1] = lane(s, 1);
+  out[2] = lane(s, 2);
+  out[3] = lane(s, 3);
 }
 
 // ---- leaf hash (thread per leaf).  Returns permutations spent.
 KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
-  const uint64_t* enc = (const uint64_t*)(T.arena + T.lf_aoff[i]);
   uint32_t L = T.lf_len[i];
   uint32_t parent = T.lf_parent[i];
   bool top = parent == NONE;
-  uint64_t hh[4];
-  uint32_t perms = hash_node(enc, L, top, hh);
+  uint64_t hh[4] = {0, 0, 0, 0}, head[4];
+  uint32_t perms = 0;
+  if (L <= LEAF_SHORT_MAX) {
+    const uint64_t* w = T.lmsg + i;
+    if (L >= 32 || top) {
+      kec256_strided(w, T.lstride, L, hh);
+      perms = 1;
+    }
+    for (int q = 0; q < 4; ++q) head[q] = (8u * q < L) ? w[q * T.lstride] : 0;
+  } else {
+    const uint64_t* enc = (const uint64_t*)(T.arena + T.lf_aoff[i]);
+    perms = hash_node(enc, L, top, hh);
+    for (int q = 0; q < 4; ++q) head[q] = enc[q];
+  }
   if (T.lf_hash)
     for (int j = 0; j < 4; ++j) T.lf_hash[4 * i + j] = hh[j];
   uint32_t nib = 0;
@@ -522,13 +614,14 @@ KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
     uint32_t b = (uint32_t)(T.skey[4 * i + (pd >> 4)] >> (8 * ((pd >> 1) & 7))) & 0xFF;
     nib = (pd & 1) ? (b & 0xF) : (b >> 4);
   }
-  publish_ref(T, parent, T.lf_pord[i], nib, i, enc, L, hh);
+  publish_ref(T, parent, T.lf_pord[i], nib, i, head, L, hh);
   *inl = (L < 32 && !top) ? 1 : 0;
   return perms;
 }
 
-// ---- branch prep: [ref_0 .. ref_15, ""] into the arena (thread per branch of one level)
-KH_HD void op_branch_prep(const Topo& T, uint32_t j) {
+// ---- branch prep: [ref_0 .. ref_15, ""] into its message slot (thread per branch of
+// one level; g = its position in the level order)
+KH_HD void op_branch_prep(const Topo& T, uint32_t j, uint64_t g) {
   uint32_t k = T.br_k[j];
   uint64_t cb = T.br_cbase[j];
   const uint16_t* cm = T.cmeta + cb;
@@ -537,7 +630,9 @@ KH_HD void op_branch_prep(const Topo& T, uint32_t j) {
     uint32_t len = cm[c] & 0xFF;
     payload += (len == 32) ? 33 : len;
   }
-  BW w{(uint64_t*)(T.arena + T.br_arena_base + T.br_aoff[j]), 0, 0};
+  Slot sl = branch_slot(T, g, T.br_depth[j], false);
+  T.br_aoff[j] = g;
+  BW w(sl.w, sl.stride);
   w.len_prefix(payload, 0xC0);
   const uint64_t* cr = T.cref + 4 * cb;
   int32_t prev = -1;
@@ -556,9 +651,7 @@ KH_HD void op_branch_prep(const Topo& T, uint32_t j) {
 }
 
 // ---- branch hash (+ extension encode + hash) (thread per branch of one level)
-KH_HD uint32_t op_branch_hash(const Topo& T, uint32_t j, uint32_t* inl) {
-  uint32_t k = T.br_k[j];
-  const uint64_t* enc = (const uint64_t*)(T.arena + T.br_arena_base + T.br_aoff[j]);
+KH_HD uint32_t op_branch_hash(const Topo& T, uint32_t j, uint64_t g, uint32_t* inl) {
   uint32_t L = T.br_len[j];
   uint32_t ext = T.br_ext[j];
   uint32_t parent = T.br_parent[j];
@@ -566,26 +659,28 @@ KH_HD uint32_t op_branch_hash(const Topo& T, uint32_t j, uint32_t* inl) {
   uint32_t d = T.br_depth[j];
   int32_t pd = (int32_t)d - (int32_t)ext - 1;
   bool top = parent == NONE;
-  uint64_t hb[4];
-  uint32_t perms = hash_node(enc, L, top && ext == 0, hb);
+  Slot sl = branch_slot(T, g, d, false);
+  uint64_t hb[4], bhead[4];
+  uint32_t perms = hash_slot(sl, L, top && ext == 0, hb);
+  slot_head(sl, L, bhead);
   uint32_t ninl = (L < 32 && !(top && ext == 0)) ? 1 : 0;
   if (T.br_hash)
     for (int q = 0; q < 4; ++q) T.br_hash[4 * j + q] = hb[q];
   Key4 key = load_key(T.skey, first);
   uint32_t nib = top ? 0 : key_nibble(key, pd);
   if (ext == 0) {
-    publish_ref(T, parent, T.br_pord[j], nib, first, enc, L, hb);
+    publish_ref(T, parent, T.br_pord[j], nib, first, bhead, L, hb);
     *inl = ninl;
     return perms;
   }
-  // extension: [HP(nibbles pd+1 .. d-1, ext), ref(branch)], written after the branch slot
-  uint64_t* xenc = (uint64_t*)((uint8_t*)enc + branch_bound(k));
+  // extension: [HP(nibbles pd+1 .. d-1, ext), ref(branch)] in its own slot
+  Slot xs = branch_slot(T, g, d, true);
   uint32_t s = (uint32_t)(pd + 1);
   uint32_t hl = ext / 2 + 1;  // HP bytes
   uint32_t refl = L >= 32 ? 33 : L;
   uint32_t hpl = hl == 1 ? 1 : 1 + hl;  // first HP byte 0x00 / 0x1_ < 0x80
   uint32_t xpay = hpl + refl;
-  BW x{xenc, 0, 0};
+  BW x(xs.w, xs.stride);
   x.len_prefix(xpay, 0xC0);
   if (hl > 1) x.put1(0x80 + hl);
   uint32_t q = s;
@@ -597,17 +692,18 @@ KH_HD uint32_t op_branch_hash(const Topo& T, uint32_t j, uint32_t* inl) {
   }
   for (; q < d; q += 2) x.put1((key_nibble(key, (int)q) << 4) | key_nibble(key, (int)q + 1));
   uint64_t bref[4];
-  for (int t = 0; t < 4; ++t) bref[t] = L >= 32 ? hb[t] : enc[t];
+  for (int t = 0; t < 4; ++t) bref[t] = L >= 32 ? hb[t] : bhead[t];
   bw_ref(x, bref, L >= 32 ? 32 : L);
   x.flush();
   uint32_t XL = rlp_hdr_len(xpay) + xpay;
   T.ex_len[j] = XL;
-  uint64_t hx[4];
-  perms += hash_node(xenc, XL, top, hx);
+  uint64_t hx[4], xhead[4];
+  perms += hash_slot(xs, XL, top, hx);
+  slot_head(xs, XL, xhead);
   if (T.ex_hash)
     for (int q2 = 0; q2 < 4; ++q2) T.ex_hash[4 * j + q2] = hx[q2];
   ninl += (XL < 32 && !top) ? 1 : 0;
-  publish_ref(T, parent, T.br_pord[j], nib, first, xenc, XL, hx);
+  publish_ref(T, parent, T.br_pord[j], nib, first, xhead, XL, hx);
   *inl = ninl;
   return perms;
 }
@@ -618,7 +714,7 @@ KH_HD uint32_t op_branch_hash(const Topo& T, uint32_t j, uint32_t* inl) {
 KH_HD uint32_t encode_branch16(const uint64_t* refs, const uint32_t* lens, uint8_t* out) {
   uint32_t payload = 1;
   for (int i = 0; i < 16; ++i) payload += lens[i] == 0 ? 1 : lens[i] == 32 ? 33 : lens[i];
-  BW w{(uint64_t*)out, 0, 0};
+  BW w((uint64_t*)out);
   w.len_prefix(payload, 0xC0);
   for (int i = 0; i < 16; ++i) {
     if (lens[i] == 0) {

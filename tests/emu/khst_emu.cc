@@ -155,24 +155,31 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
     br_cbase[j] = (uint32_t)C;
     C += br_k[j];
   }
-  uint64_t brb = 0;
-  for (uint64_t j = 0; j < B; ++j) {
-    uint64_t a = branch_arena_bytes(T, (uint32_t)j);
-    br_aoff[j] = brb;
-    brb += a;
-  }
   uint64_t lfb = 0;
   for (uint64_t i = 0; i < m; ++i) {
     uint64_t a = lf_aoff[i];
     lf_aoff[i] = lfb;
     lfb += a;
   }
-  std::vector<uint64_t> cref(4 * C + 4), arena((lfb + brb + 64) / 8 + 1);
+  std::vector<uint64_t> cref(4 * C + 4), arena((lfb + 64) / 8 + 1), lmsg(LEAF_WORDS * m + 1),
+      bmsg(BR_WORDS * B + 1), xmsg(EXT_WORDS * B + 1);
+  T.lmsg = lmsg.data();
+  T.lstride = m;
+  T.bmsg = bmsg.data();
+  T.xmsg = xmsg.data();
+  // level order: branch ids bucketed by depth (ascending id inside a level)
+  std::vector<uint32_t> lbv(65, 0), lorder;
+  for (int d = 0; d < 64; ++d) {
+    lbv[d] = (uint32_t)lorder.size();
+    for (uint64_t j = 0; j < B; ++j)
+      if (br_depth[j] == d) lorder.push_back((uint32_t)j);
+  }
+  lbv[64] = (uint32_t)lorder.size();
+  T.lb = lbv.data();
   std::vector<uint16_t> cmeta(C + 1);
   T.cref = cref.data();
   T.cmeta = cmeta.data();
   T.arena = (uint8_t*)arena.data();
-  T.br_arena_base = lfb;
   uint64_t perms = 0, hashes = 0, inl = 0;
   for (uint64_t i = 0; i < m; ++i) op_leaf_prep(T, i);
   for (uint64_t i = 0; i < m; ++i) {
@@ -183,12 +190,11 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
     inl += in1;
   }
   for (int d = 63; d >= 0; --d) {
-    for (uint64_t j = 0; j < B; ++j)
-      if (br_depth[j] == d) op_branch_prep(T, (uint32_t)j);
-    for (uint64_t j = 0; j < B; ++j) {
-      if (br_depth[j] != d) continue;
+    for (uint64_t g = lbv[d]; g < lbv[d + 1]; ++g) op_branch_prep(T, lorder[g], g);
+    for (uint64_t g = lbv[d]; g < lbv[d + 1]; ++g) {
+      uint32_t j = lorder[g];
       uint32_t in1 = 0;
-      perms += op_branch_hash(T, (uint32_t)j, &in1);
+      perms += op_branch_hash(T, j, g, &in1);
       bool top = br_parent[j] == NONE, ext = br_ext[j] != 0;
       hashes += (br_len[j] >= 32 || (top && !ext)) ? 1 : 0;
       if (ext) hashes += (ex_len[j] >= 32 || top) ? 1 : 0;
@@ -243,3 +249,54 @@ int emu_fold16(const uint8_t* hash32x16, const uint32_t* len16, const uint8_t* i
 }
 
 }  // extern "C"
+
+// Brute-force check of the pyramid + SWAR nearest-smaller-value searches (trie_ops.h)
+// against their naive definitions on random, shallow and almost-flat value arrays.
+// Returns 0 if every query agrees.
+#include <random>
+extern "C" int emu_ansv_check(uint64_t seed, int iters) {
+  std::mt19937_64 r(seed);
+  for (int it = 0; it < iters; ++it) {
+    uint64_t n = 1 + r() % 5000;
+    std::vector<uint8_t> u(n + 16);
+    int mode = it % 3;
+    for (uint64_t i = 0; i < n; ++i)
+      u[i] = mode == 0 ? r() % 65
+                       : (mode == 1 ? 1 + (r() % 4 == 0 ? r() % 3 : 5 + r() % 3) : (r() % 100 == 0 ? 0 : 6 + r() % 2));
+    std::vector<std::vector<uint8_t>> lv;
+    lv.reserve(8);
+    Pyr P{};
+    P.lv[0] = u.data();
+    P.sz[0] = n;
+    P.nl = 1;
+    while (P.sz[P.nl - 1] > 64) {
+      uint64_t nin = P.sz[P.nl - 1], nout = (nin + 63) / 64;
+      lv.emplace_back(nout + 16);
+      for (uint64_t i = 0; i < nout; ++i) op_min64(P.lv[P.nl - 1], nin, lv.back().data(), i);
+      P.lv[P.nl] = lv.back().data();
+      P.sz[P.nl] = nout;
+      P.nl++;
+    }
+    for (uint64_t b = 0; b < n; ++b) {
+      uint32_t t = u[b];
+      if (!t) continue;
+      for (uint32_t tt : {t, t + 1}) {
+        int64_t e = -1;
+        for (int64_t j = (int64_t)b - 1; j >= 0; --j)
+          if (u[j] < tt) {
+            e = j;
+            break;
+          }
+        if (ansv_left(P, b, tt) != e) return 1;
+      }
+      int64_t e = -1;
+      for (uint64_t j = b + 1; j < n; ++j)
+        if (u[j] < t) {
+          e = (int64_t)j;
+          break;
+        }
+      if (ansv_right(P, b, t) != e) return 2;
+    }
+  }
+  return 0;
+}

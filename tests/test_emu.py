@@ -85,3 +85,11 @@ def test_replay_synth_matches_codec(oracle):
     vals = [vb[int(off[i]):int(off[i + 1])].tobytes() for i in range(n)]
     res, _ = E.build(keys, vals)
     assert _root(res[0]) == oracle.seq_root(keys, vals)
+
+
+def test_nearest_smaller_value_searches():
+    """k_ansv's pyramid + SWAR scans == naive nearest-smaller-value definitions."""
+    import ctypes
+    L = E.lib()
+    L.emu_ansv_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    assert L.emu_ansv_check(7, 150) == 0
