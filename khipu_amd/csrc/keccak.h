@@ -145,9 +145,9 @@ KH_HD void kxor(KState& s, int i, uint64_t w) {
 // loads; only the aligned words holding bytes [p, p+nb) are read, so no access
 // leaves the 8-byte-aligned span of the message.  Bytes above nb are garbage.
 KH_HD uint64_t load64u_n(const uint8_t* p, uint32_t nb) {
-  uintptr_t a = (uintptr_t)p;
-  const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
-  uint32_t off = (uint32_t)(a & 7);
+  // pointer arithmetic, not an int round trip, so the address space survives (ds_read / global_load)
+  uint32_t off = (uint32_t)((uintptr_t)p & 7);
+  const uint64_t* q = (const uint64_t*)(p - off);
   uint64_t lo = q[0] >> (8 * off);
   if (off + nb > 8) lo |= q[1] << (64 - 8 * off);
   return lo;

@@ -214,18 +214,6 @@ __global__ void __launch_bounds__(BS) k_chain(Topo T, uint64_t nb) {
   if (b < nb) op_chain(T, b);
 }
 
-__global__ void __launch_bounds__(BS) k_group(Topo T, uint64_t nb) {
-  uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (b >= nb) return;
-  if (T.u[b] == 0) {
-    T.grp[b] = NONE;
-    return;
-  }
-  uint32_t g = T.isrep_bid[T.rep[b]];
-  T.grp[b] = g;
-  atomicMax(&T.br_k[g], (uint32_t)T.ord[b] + 2u);
-}
-
 // sum three per-thread counters over the block; one atomic per counter per block
 __device__ __forceinline__ void block_add3(unsigned long long* c0, unsigned long long v0, unsigned long long* c1,
                                            unsigned long long v1, unsigned long long* c2, unsigned long long v2) {
@@ -248,11 +236,11 @@ __device__ __forceinline__ void block_add3(unsigned long long* c0, unsigned long
   }
 }
 
-__global__ void __launch_bounds__(BS) k_branch_topo(Topo T, uint64_t nb) {
+__global__ void __launch_bounds__(BS) k_branch_topo(Topo T, Pyr P, uint64_t nb) {
   uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long ext = 0;
   if (b < nb) {
-    op_branch_topo(T, b);
+    op_branch_topo(T, P, nb, b);
     if (T.u[b] != 0 && T.rep[b] == (uint32_t)b) ext = T.br_ext[T.isrep_bid[b]] ? 1 : 0;
   }
   block_add3(&T.ctr[CTR_EXT], ext, nullptr, 0, nullptr, 0);
@@ -263,42 +251,92 @@ __global__ void __launch_bounds__(BS) k_leaf_topo(Topo T) {
   if (i < T.m) op_leaf_topo(T, i);
 }
 
-// Level order (branch ids bucketed by depth) without contended global atomics:
-// per-block depth counts laid out [depth][block], one exclusive scan gives every
-// (depth, block) its base, a second pass ranks inside the block with LDS atomics.
+// Level order without contended global atomics: branch ids bucketed by
+//   bucket = depth * 8 + has_extension * 4 + (3 - (blocks - 1))
+// (blocks = Keccak blocks of the branch if every child is hashed), so a level is
+// the contiguous range of its 8 buckets, heaviest branches first and extensions
+// grouped: the waves of a level run the same number of permutations.  Per-block
+// bucket counts are laid out [bucket][block]; one exclusive scan gives every
+// (bucket, block) its base; a second pass ranks inside the block with LDS atomics.
+constexpr uint32_t NBUCKET = 64 * 8;
+__device__ __forceinline__ uint32_t branch_bucket(const Topo& T, uint64_t j) {
+  uint32_t k = T.br_k[j];
+  uint32_t payload = 32 * k + 17;
+  uint32_t blocks = perms_for_len(rlp_hdr_len(payload) + payload);  // 1..4
+  return (uint32_t)T.br_depth[j] * 8 + (T.br_ext[j] ? 4 : 0) + (4 - blocks);
+}
 __global__ void __launch_bounds__(BS) k_level_count(Topo T, const uint32_t* Bp, uint32_t* bcnt, uint32_t nblk) {
-  __shared__ uint32_t h[64];
-  if (threadIdx.x < 64) h[threadIdx.x] = 0;
+  __shared__ uint32_t h[NBUCKET];
+  for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) h[q] = 0;
   __syncthreads();
   uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (j < *Bp) atomicAdd(&h[T.br_depth[j]], 1u);
+  if (j < *Bp) atomicAdd(&h[branch_bucket(T, j)], 1u);
   __syncthreads();
-  if (threadIdx.x < 64) bcnt[(uint64_t)threadIdx.x * nblk + blockIdx.x] = h[threadIdx.x];
+  for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) bcnt[(uint64_t)q * nblk + blockIdx.x] = h[q];
 }
 
 __global__ void __launch_bounds__(BS) k_level_scatter(Topo T, const uint32_t* Bp, const uint32_t* bbase,
                                                       uint32_t nblk, uint32_t* order) {
-  __shared__ uint32_t cnt[64];
-  if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+  __shared__ uint32_t cnt[NBUCKET];
+  for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) cnt[q] = 0;
   __syncthreads();
   uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (j < *Bp) {
-    uint32_t d = T.br_depth[j];
-    uint32_t r = atomicAdd(&cnt[d], 1u);
-    order[bbase[(uint64_t)d * nblk + blockIdx.x] + r] = (uint32_t)j;
+    uint32_t q = branch_bucket(T, j);
+    uint32_t r = atomicAdd(&cnt[q], 1u);
+    order[bbase[(uint64_t)q * nblk + blockIdx.x] + r] = (uint32_t)j;
   }
 }
 
 // level bounds: lb[d] = first position of depth d in `order`, lb[64] = B
 __global__ void k_level_bounds(const uint32_t* bbase, uint32_t nblk, const uint32_t* Bp, uint32_t* lb) {
   uint32_t d = threadIdx.x;
-  if (d < 64) lb[d] = bbase[(uint64_t)d * nblk];
+  if (d < 64) lb[d] = bbase[(uint64_t)d * 8 * nblk];
   if (d == 0) lb[64] = *Bp;
 }
 
+// Leaf encode.  The value spans are random in the input buffer; if every lane
+// walked its own span with 8-byte loads, the ~12 dependent loads per lane would be
+// spread over time and the lines re-fetched after L2 eviction (measured ~570 B of
+// fabric reads per 80 B value).  Instead each wave first copies the spans of its 64
+// leaves into LDS cooperatively (16 lanes per span, one coalesced 128 B request),
+// then every lane encodes its own leaf from LDS.  Spans wider than the stage are
+// read from global memory directly (long values; such leaves go to the arena).
+constexpr uint32_t STAGE_WORDS = 19;  // aligned 8-byte words per staged value span
+
 __global__ void __launch_bounds__(BS) k_leaf_prep(Topo T) {
+  __shared__ uint64_t stage[BS * STAGE_WORDS];
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i < T.m) op_leaf_prep(T, i);
+  const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u;
+  uint64_t off = 0;
+  uint32_t vlen = 0;
+  if (i < T.m) {
+    off = T.svoff[i];
+    vlen = T.svlen[i];
+  }
+  const uint32_t vmis = (uint32_t)((uintptr_t)T.vals & 7);  // vals base misalignment
+  typedef const __attribute__((address_space(1))) uint64_t gword;  // global (not flat) loads
+  gword* vw = (gword*)(T.vals - vmis);
+  const uint64_t a0 = (off + vmis) >> 3;                     // first aligned word of the span
+  const uint32_t nw = vlen ? (uint32_t)(((off + vmis + vlen + 7) >> 3) - a0) : 0;
+  const uint32_t g = ln >> 4, gl = ln & 15;
+  for (uint32_t it = 0; it < 16; ++it) {
+    uint32_t src = it * 4 + g;  // lane of the wave whose span this group copies
+    uint64_t sa = __shfl(a0, (int)src);
+    uint32_t sn = __shfl(nw, (int)src);
+    if (sn <= STAGE_WORDS) {
+      uint64_t* dst = stage + (wbase + src) * STAGE_WORDS;
+      if (gl < sn) dst[gl] = vw[sa + gl];
+      if (gl + 16 < sn) dst[gl + 16] = vw[sa + gl + 16];
+    }
+  }
+  __syncthreads();
+  if (i < T.m) {
+    if (nw <= STAGE_WORDS)  // two call sites so each keeps its address space (ds_read vs global_load)
+      op_leaf_prep(T, i, (const uint8_t*)(stage + threadIdx.x * STAGE_WORDS) + ((off + vmis) & 7), vlen);
+    else
+      op_leaf_prep(T, i, T.vals + off, vlen);
+  }
 }
 
 __global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
@@ -591,12 +629,12 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       n * 32, segmented ? n * 4 : 0,          // skey sseg
       radix_scratch_bytes(n), scan_scratch_bytes(n, 8),
       nb1, nb1 / 32 + 1024,                   // u, pyramid
-      nb1 * 4, nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1 * 4, nb1 * 4,  // psv nsv pse rep ord isrep grp
+      nb1 * 4, nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1 * 4,  // psv nsv pse rep ord isrep
       nb1 * 4, nb1 * 4, nb1, nb1, nb1 * 4, nb1, nb1 * 4, nb1 * 8, nb1 * 4, nb1 * 4,  // branches
       n * 4, n, n, n * 8, n * 4, n * 8, n * 4,  // leaves, svoff, svlen
       A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
       nres * 32, nres * 4, nres * 32,         // results
-      CTR_N * 8, 64 * 4, 80 * 4, 64 * ((nb1 + BS - 1) / BS) * 4, nb1 * 4,  // ctr hist lb bcnt order
+      CTR_N * 8, 64 * 4, 80 * 4, 512 * ((nb1 + BS - 1) / BS) * 4, nb1 * 4,  // ctr hist lb bcnt order
   };
   c->ws1.ensure(carve_size(sz));
   Carver cv{(char*)c->ws1.p, 0, c->ws1.cap};
@@ -618,7 +656,6 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.rep = cv.take<uint32_t>(nb1);
   T.ord = cv.take<uint8_t>(nb1);
   T.isrep_bid = cv.take<uint32_t>(nb1);
-  T.grp = cv.take<uint32_t>(nb1);
   T.br_k = cv.take<uint32_t>(nb1);
   T.br_cbase = cv.take<uint32_t>(nb1);
   T.br_depth = cv.take<uint8_t>(nb1);
@@ -646,7 +683,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.depth_hist = cv.take<uint32_t>(64);
   uint32_t* lb = cv.take<uint32_t>(80);
   const uint32_t nblk_max = (uint32_t)((nb1 + BS - 1) / BS);
-  uint32_t* bcnt = cv.take<uint32_t>((uint64_t)64 * nblk_max);
+  uint32_t* bcnt = cv.take<uint32_t>((uint64_t)NBUCKET * nblk_max);
   uint32_t* order = cv.take<uint32_t>(nb1);
   T.depth0 = A.depth0;
   T.segmented = segmented ? 1 : 0;
@@ -779,16 +816,14 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     hipLaunchKernelGGL(k_chain, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
     scan_exclusive<uint32_t>(T.isrep_bid, T.isrep_bid, nb, Bp, scan_scratch, st);
-    HIPCHK(hipMemsetAsync(T.br_k, 0, nb * 4, st));
-    hipLaunchKernelGGL(k_group, GRID(nb, BS), dim3(BS), 0, st, T, nb);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_branch_topo, GRID(nb, BS), dim3(BS), 0, st, T, nb);
+    HIPCHK(hipMemsetAsync(T.br_k, 0, nb * 4, st));  // entries past B must scan as 0
+    hipLaunchKernelGGL(k_branch_topo, GRID(nb, BS), dim3(BS), 0, st, T, P, nb);
     LAUNCH_CHECK();
     // level order (grids sized by nb; threads past B exit)
     const uint32_t nblk = (uint32_t)((nb + BS - 1) / BS);
     hipLaunchKernelGGL(k_level_count, dim3(nblk), dim3(BS), 0, st, T, (const uint32_t*)Bp, bcnt, nblk);
     LAUNCH_CHECK();
-    scan_exclusive<uint32_t>(bcnt, bcnt, (uint64_t)64 * nblk, (uint32_t*)nullptr, scan_scratch, st);
+    scan_exclusive<uint32_t>(bcnt, bcnt, (uint64_t)NBUCKET * nblk, (uint32_t*)nullptr, scan_scratch, st);
     hipLaunchKernelGGL(k_level_scatter, dim3(nblk), dim3(BS), 0, st, T, (const uint32_t*)Bp,
                        (const uint32_t*)bcnt, nblk, order);
     LAUNCH_CHECK();

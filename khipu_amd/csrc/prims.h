@@ -2,10 +2,11 @@
 // and a stable LSD radix sort of (uint64 key, uint32 value) pairs.
 //
 // Radix sort: 8-bit digits, one (histogram, scan, scatter) triple per pass.  A
-// tile is 256 threads x 16 items = 4096 keys; each 64-lane wave owns a
-// contiguous 1024-key slice of the tile and ranks its keys with a ballot-based
+// tile is 256 threads x 8 items = 2048 keys; each 64-lane wave owns a
+// contiguous 512-key slice of the tile and ranks its keys with a ballot-based
 // wave-level multisplit (8 ballots give the mask of lanes holding the same
-// digit), so the scatter is stable without an LDS sort.
+// digit), so the scatter is stable; the tile is then staged in LDS in digit
+// order and written out run by run (coalesced).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -132,10 +133,10 @@ void scan_exclusive(const T* in, T* out, uint64_t n, T* total, void* scratch, hi
 // Radix sort of (uint64 key, uint32 val) pairs on key bits [lo_bit, hi_bit).
 // ---------------------------------------------------------------------------
 constexpr int RS_THREADS = 256;
-constexpr int RS_ITEMS = 16;
-constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096
+constexpr int RS_ITEMS = 8;
+constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 2048 keys: 24 KiB of LDS staging
 constexpr int RS_WAVES = RS_THREADS / 64;
-constexpr int RS_WSLICE = RS_TILE / RS_WAVES;   // 1024 keys per wave
+constexpr int RS_WSLICE = RS_TILE / RS_WAVES;   // 512 keys per wave
 
 __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const uint64_t* keys, uint64_t n, int shift, uint32_t* counts,
                                                         uint32_t ntiles) {
@@ -158,14 +159,23 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const uint64_t* keys, ui
   }
 }
 
+// Scatter of one pass.  Keys are ranked per wave (ballot multisplit), placed in
+// LDS in digit order for the whole tile, then written out so that each digit's
+// run of the tile goes to consecutive global addresses (coalesced stores instead
+// of one scattered 8-byte store per key).
 __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const uint64_t* keys, const uint32_t* vals, uint64_t* okeys,
                                                            uint32_t* ovals, uint64_t n, int shift,
                                                            const uint32_t* offs, uint32_t ntiles) {
   __shared__ uint32_t wc[RS_WAVES][256];
+  __shared__ uint32_t tstart[256], gbase[256];
+  __shared__ uint32_t lw[RS_THREADS / 64];
+  __shared__ uint64_t sk[RS_TILE];
+  __shared__ uint32_t sv[RS_TILE];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&wc[0][0])[i] = 0;
   __syncthreads();
-  uint64_t base = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * RS_WSLICE;
+  const uint64_t tbase = (uint64_t)blockIdx.x * RS_TILE;
+  const uint64_t base = tbase + (uint64_t)w * RS_WSLICE;
   uint64_t k[RS_ITEMS];
   uint32_t v[RS_ITEMS];
   uint32_t r[RS_ITEMS];
@@ -192,14 +202,19 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const uint64_t* keys,
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
-  for (int d = threadIdx.x; d < 256; d += RS_THREADS) {
-    uint32_t run = offs[(uint64_t)d * ntiles + blockIdx.x];
+  // per digit: wave offsets inside the tile's digit run, tile-local run start, global base
+  {
+    const int d = threadIdx.x;  // RS_THREADS == 256 digits
+    uint32_t run = 0;
 #pragma unroll
     for (int q = 0; q < RS_WAVES; ++q) {
       uint32_t t = wc[q][d];
       wc[q][d] = run;
       run += t;
     }
+    uint32_t tot;
+    tstart[d] = block_exclusive_scan<uint32_t>(run, lw, &tot);
+    gbase[d] = offs[(uint64_t)d * ntiles + blockIdx.x];
   }
   __syncthreads();
 #pragma unroll
@@ -207,10 +222,19 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const uint64_t* keys,
     uint64_t i = base + (uint64_t)it * 64 + lane;
     if (i < n) {
       uint32_t d = (uint32_t)(k[it] >> shift) & 0xFF;
-      uint32_t pos = wc[w][d] + r[it];
-      okeys[pos] = k[it];
-      ovals[pos] = v[it];
+      uint32_t li = tstart[d] + wc[w][d] + r[it];
+      sk[li] = k[it];
+      sv[li] = v[it];
     }
+  }
+  __syncthreads();
+  const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)RS_TILE ? (n - tbase) : (uint64_t)RS_TILE);
+  for (uint32_t li = threadIdx.x; li < tn; li += RS_THREADS) {
+    uint64_t key = sk[li];
+    uint32_t d = (uint32_t)(key >> shift) & 0xFF;
+    uint32_t pos = gbase[d] + (li - tstart[d]);
+    okeys[pos] = key;
+    ovals[pos] = sv[li];
   }
 }
 

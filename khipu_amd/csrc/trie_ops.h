@@ -160,9 +160,8 @@ struct Topo {
   uint32_t* rep;          // [m-1] group representative of b
   uint8_t* ord;           // [m-1] ordinal of b within its group
   uint32_t* isrep_bid;    // [m-1] 1 if rep, then (after scan) branch id of rep
-  uint32_t* grp;          // [m-1] branch id of b's group
   // branches (B <= m-1)
-  uint32_t* br_k;         // child count (then scanned into br_cbase)
+  uint32_t* br_k;         // child count
   uint32_t* br_cbase;     // first child record
   uint8_t* br_depth;
   uint8_t* br_ext;        // extension nibbles above the branch (0: none)
@@ -383,17 +382,6 @@ KH_HD void op_chain(const Topo& T, uint64_t b) {
   T.isrep_bid[b] = (o == 0) ? 1u : 0u;
 }
 
-// after exclusive scan of isrep_bid (which now holds branch ids of reps)
-KH_HD uint32_t op_group(const Topo& T, uint64_t b) {  // returns k candidate (ord+2) or 0
-  if (T.u[b] == 0) {
-    T.grp[b] = NONE;
-    return 0;
-  }
-  uint32_t g = T.isrep_bid[T.rep[b]];
-  T.grp[b] = g;
-  return g;
-}
-
 // parent resolution for a node whose key range is [s, e]: boundaries s-1 and e
 struct Parent {
   uint32_t bid;  // NONE: top of its segment
@@ -408,31 +396,35 @@ KH_HD Parent resolve_parent(const Topo& T, int64_t a, int64_t c) {
     P.pd = (int32_t)T.depth0 - 1;
     P.pord = 0;
   } else if (va >= vc) {
-    P.bid = T.grp[a];
+    P.bid = T.isrep_bid[T.rep[a]];
     P.pd = (int32_t)va - 1;
     P.pord = T.ord[a] + 1u;
   } else {
-    P.bid = T.grp[c];
+    P.bid = T.isrep_bid[T.rep[c]];
     P.pd = (int32_t)vc - 1;
     P.pord = T.ord[c];
   }
   return P;
 }
 
-// ---- stage: branch records (thread per boundary; only reps act)
-KH_HD void op_branch_topo(const Topo& T, uint64_t b) {
+// ---- stage: branch records (thread per boundary; only reps act).  The child count
+// comes from the group's last member: the rightmost boundary <= t before the next
+// strictly smaller one (one more pyramid query), k = its ordinal + 2.
+KH_HD void op_branch_topo(const Topo& T, const Pyr& P, uint64_t nb, uint64_t b) {
   if (T.u[b] == 0 || T.rep[b] != (uint32_t)b) return;
   uint32_t j = T.isrep_bid[b];
-  uint32_t d = T.u[b] - 1u;
+  uint32_t t = T.u[b];
+  uint32_t d = t - 1u;
   int64_t a = T.psv[b], c = T.nsv[b];
-  Parent P = resolve_parent(T, a, c);
+  Parent Pp = resolve_parent(T, a, c);
+  int64_t last = ansv_left(P, c < 0 ? nb : (uint64_t)c, t + 1);
+  T.br_k[j] = (uint32_t)T.ord[last] + 2u;
   T.br_depth[j] = (uint8_t)d;
-  T.br_ext[j] = (uint8_t)((int32_t)d - P.pd - 1);
-  T.br_parent[j] = P.bid;
-  T.br_pord[j] = (uint8_t)P.pord;
+  T.br_ext[j] = (uint8_t)((int32_t)d - Pp.pd - 1);
+  T.br_parent[j] = Pp.bid;
+  T.br_pord[j] = (uint8_t)Pp.pord;
   T.br_first[j] = (uint32_t)(a + 1);
 }
-
 
 // ---- leaf geometry
 KH_HD void leaf_value(const Topo& T, uint64_t i, const uint8_t** p, uint64_t* len) {
@@ -536,13 +528,11 @@ KH_HD void bw_ref(BW& w, const uint64_t r[4], uint32_t len) {  // child referenc
 }
 
 // ---- leaf prep: [HP(path, leaf), value] into the message store (thread per leaf)
-KH_HD void op_leaf_prep(const Topo& T, uint64_t i) {
+// vp: the value bytes (global memory, or a staged copy in LDS on the device)
+KH_HD void op_leaf_prep(const Topo& T, uint64_t i, const uint8_t* vp, uint64_t vlen) {
   Key4 k = load_key(T.skey, i);
   int32_t pd = T.lf_pd[i];
   uint32_t s = (uint32_t)(pd + 1);
-  const uint8_t* vp;
-  uint64_t vlen;
-  leaf_value(T, i, &vp, &vlen);
   uint32_t v0 = vlen ? (uint32_t)load64u_n(vp, 1) & 0xFF : 0;
   uint32_t p = 64 - s, h = p / 2 + 1;
   uint32_t hp0 = (p & 1) ? (0x30u | key_nibble(k, (int)s)) : 0x20u;

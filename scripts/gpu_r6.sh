@@ -1,2 +1,4 @@
 #!/bin/bash
-bash scripts/gpu_round.sh r6 && bash scripts/gpu_pmc.sh pmc6
+# round + PMC passes
+TAG=${1:-r}
+bash scripts/gpu_round.sh $TAG && bash scripts/gpu_pmc.sh pmc_$TAG

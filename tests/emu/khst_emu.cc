@@ -70,7 +70,7 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
   const uint64_t nbb = nb + 1;
   std::vector<uint8_t> u(nbb), ord(nbb), br_depth(nbb), br_ext(nbb), br_pord(nbb), lf_pord(m);
   std::vector<int32_t> psv(nbb), nsv(nbb), pse(nbb);
-  std::vector<uint32_t> rep(nbb), isrep(nbb), grp(nbb), br_k(nbb, 0), br_cbase(nbb), br_parent(nbb), br_first(nbb),
+  std::vector<uint32_t> rep(nbb), isrep(nbb), br_k(nbb, 0), br_cbase(nbb), br_parent(nbb), br_first(nbb),
       br_len(nbb), ex_len(nbb), lf_parent(m), lf_len(m);
   std::vector<int8_t> lf_pd(m);
   std::vector<uint64_t> br_aoff(nbb), lf_aoff(m);
@@ -83,7 +83,6 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
   T.rep = rep.data();
   T.ord = ord.data();
   T.isrep_bid = isrep.data();
-  T.grp = grp.data();
   T.br_k = br_k.data();
   T.br_cbase = br_cbase.data();
   T.br_depth = br_depth.data();
@@ -132,16 +131,7 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
     }
     B = run;
     for (uint64_t b = 0; b < nb; ++b) {
-      if (u[b] == 0) {
-        grp[b] = NONE;
-        continue;
-      }
-      uint32_t g = isrep[rep[b]];
-      grp[b] = g;
-      br_k[g] = std::max(br_k[g], (uint32_t)ord[b] + 2u);
-    }
-    for (uint64_t b = 0; b < nb; ++b) {
-      op_branch_topo(T, b);
+      op_branch_topo(T, P, nb, b);
       if (u[b] != 0 && rep[b] == b) {
         uint32_t j = isrep[b];
         hist[br_depth[j]]++;
@@ -181,7 +171,7 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
   T.cmeta = cmeta.data();
   T.arena = (uint8_t*)arena.data();
   uint64_t perms = 0, hashes = 0, inl = 0;
-  for (uint64_t i = 0; i < m; ++i) op_leaf_prep(T, i);
+  for (uint64_t i = 0; i < m; ++i) op_leaf_prep(T, i, T.vals + T.svoff[i], T.svlen[i]);
   for (uint64_t i = 0; i < m; ++i) {
     uint32_t in1 = 0;
     uint32_t p = op_leaf_hash(T, i, &in1);
