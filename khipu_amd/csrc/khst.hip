@@ -136,17 +136,21 @@ __global__ void __launch_bounds__(BS) k_tie_fix(const uint64_t* ck, uint64_t n, 
   if (dup) atomicOr(flags, 2ULL);
 }
 
-__global__ void __launch_bounds__(BS) k_gather(const uint64_t* K, const uint32_t* seg, const uint32_t* idx,
-                                               uint64_t n, uint64_t* skey, uint32_t* sseg) {
+// 32-byte keys move as two 16-byte vectors, both loads issued before any store
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void copy_key(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst) {
+  u64x2 a = ((const u64x2*)src)[0], b = ((const u64x2*)src)[1];
+  ((u64x2*)dst)[0] = a;
+  ((u64x2*)dst)[1] = b;
+}
+
+__global__ void __launch_bounds__(BS) k_gather(const uint64_t* __restrict__ K, const uint32_t* __restrict__ seg,
+                                               const uint32_t* __restrict__ idx, uint64_t n,
+                                               uint64_t* __restrict__ skey, uint32_t* __restrict__ sseg) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
   uint32_t s = idx[i];
-  const uint64_t* p = K + 4 * (uint64_t)s;
-  uint64_t* q = skey + 4 * i;
-  q[0] = p[0];
-  q[1] = p[1];
-  q[2] = p[2];
-  q[3] = p[3];
+  copy_key(K + 4 * (uint64_t)s, skey + 4 * i);
   if (seg) sseg[i] = seg[s];
 }
 
@@ -184,7 +188,7 @@ __global__ void __launch_bounds__(BS) k_compact(const uint64_t* skey, const uint
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n || !keep[i]) return;
   uint64_t p = keep_pos[i];
-  for (int j = 0; j < 4; ++j) okey[4 * p + j] = skey[4 * i + j];
+  copy_key(skey + 4 * i, okey + 4 * p);
   oidx[p] = sidx[i];
   if (sseg) oseg[p] = sseg[i];
 }
@@ -623,8 +627,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
 
   // ---- phase-1 workspace (sized by n)
   const uint64_t nb1 = n;  // boundaries <= n-1; round up
+  // keys are moved as 16-byte vectors: caller keys that are not 16-byte aligned get copied
+  const bool own_keys = (A.flags & KH_HASH_KEYS) || ((uintptr_t)A.keys & 15);
   std::vector<size_t> sz = {
-      (A.flags & KH_HASH_KEYS) ? n * 32 : 0,  // K32
+      own_keys ? n * 32 : 0,                  // K32
       n * 8, n * 8, n * 4, n * 4,             // ck0 ck1 idx0 idx1
       n * 32, segmented ? n * 4 : 0,          // skey sseg
       radix_scratch_bytes(n), scan_scratch_bytes(n, 8),
@@ -638,7 +644,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   };
   c->ws1.ensure(carve_size(sz));
   Carver cv{(char*)c->ws1.p, 0, c->ws1.cap};
-  uint64_t* K32 = (A.flags & KH_HASH_KEYS) ? cv.take<uint64_t>(n * 4) : (uint64_t*)A.keys;
+  uint64_t* K32 = own_keys ? cv.take<uint64_t>(n * 4) : (uint64_t*)A.keys;
   uint64_t* ck0 = cv.take<uint64_t>(n);
   uint64_t* ck1 = cv.take<uint64_t>(n);
   uint32_t* idx0 = cv.take<uint32_t>(n);
@@ -702,6 +708,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   if (A.flags & KH_HASH_KEYS) {
     hipLaunchKernelGGL(k_hash_keys, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32);
     LAUNCH_CHECK();
+  } else if (own_keys) {
+    HIPCHK(hipMemcpyAsync(K32, A.keys, n * 32, hipMemcpyDeviceToDevice, st));
   }
   HIPCHK(hipEventRecord(c->ev[1], st));
 

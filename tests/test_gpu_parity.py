@@ -203,3 +203,25 @@ def test_sharded_driver_rccl_world1(khst, oracle):
         assert root == hh[0].tobytes()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("koff,voff_shift", [(8, 0), (1, 3), (0, 5)])
+def test_device_build_misaligned_buffers(khst, oracle, koff, voff_shift):
+    """Device keys / values at arbitrary byte offsets (the ABI takes plain pointers):
+    keys not 16-byte aligned are copied into the workspace; value spans are staged
+    by aligned words whatever the base alignment."""
+    import torch
+    from khipu_amd.device import Ctx
+    ctx = Ctx(0)
+    r = random.Random(17 + koff)
+    keys = [bytes(r.getrandbits(8) for _ in range(32)) for _ in range(3000)]
+    vals = [C.account_value(r) if i % 3 else C.storage_value(r) for i in range(len(keys))]
+    kb = torch.zeros(len(keys) * 32 + 64, dtype=torch.uint8)
+    kb[koff:koff + 32 * len(keys)] = torch.frombuffer(bytearray(b"".join(keys)), dtype=torch.uint8)
+    blob = b"".join(vals)
+    vb = torch.zeros(len(blob) + 64, dtype=torch.uint8)
+    vb[voff_shift:voff_shift + len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+    off = torch.tensor(np.concatenate([[0], np.cumsum([len(v) for v in vals])]), dtype=torch.int64)
+    dk, dv, do = kb.cuda()[koff:], vb.cuda()[voff_shift:], off.cuda()
+    hh, _, _, _ = ctx.build(dk, 32, dv, do, len(keys))
+    assert hh[0].tobytes() == oracle.seq_root(keys, vals)
