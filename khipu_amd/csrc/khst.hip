@@ -355,6 +355,83 @@ __global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
   block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
 }
 
+// Fused leaf encode + hash (the root-only build; the write-back build keeps the
+// encodings and uses k_leaf_prep/k_leaf_hash).  Each lane owns a 17-word LDS
+// message slot.  1) the wave copies the value bytes of its 64 leaves straight to
+// their message positions (16 lanes per leaf: one coalesced request per value,
+// funnel-shifted by the header length), 2) each lane writes its header bytes in
+// front (merging the shared word), Keccak's its slot and publishes the reference.
+// Leaves longer than one block take the arena path (k_leaf_prep's global writer).
+__global__ void __launch_bounds__(BS) k_leaf_fused(Topo T) {
+  __shared__ uint64_t msg[BS * LEAF_WORDS];
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u;
+  const bool valid = i < T.m;
+  uint64_t off = 0;
+  uint32_t vlen = 0, v0 = 0;
+  Key4 k{0, 0, 0, 0};
+  int32_t pd = 0;
+  if (valid) {
+    off = T.svoff[i];
+    vlen = T.svlen[i];
+    k = load_key(T.skey, i);
+    pd = T.lf_pd[i];
+    if (vlen == 1) v0 = T.vals[off];
+  }
+  LeafGeom g = leaf_geom(k, pd, vlen, v0);
+  const bool shortl = valid && g.L <= LEAF_SHORT_MAX;
+  typedef const __attribute__((address_space(1))) uint64_t gword;  // global (not flat) loads
+  const uint32_t vmis = (uint32_t)((uintptr_t)T.vals & 7);
+  gword* vw = (gword*)(T.vals - vmis);
+  // value span [vs, vs + vlen) in aligned-word coordinates; header length P = L - vlen
+  const uint64_t vs = off + vmis;
+  const uint32_t P = g.L - vlen;
+  const uint32_t qlo = P >> 3, nq = (shortl && vlen) ? ((g.L + 7) >> 3) - qlo : 0;
+  const uint32_t gi = ln >> 4, gl = ln & 15;
+  for (uint32_t it = 0; it < 16; ++it) {
+    const int src = (int)(it * 4 + gi);
+    const uint32_t snq = __shfl(nq, src);
+    if (snq == 0) continue;
+    const uint64_t svs = __shfl(vs, src);
+    const uint32_t sP = __shfl(P, src), sL = __shfl(g.L, src), sq = __shfl(qlo, src);
+    const uint64_t w_first = svs >> 3, w_last = (svs + (sL - sP) - 1) >> 3;
+    uint64_t* dst = msg + (wbase + src) * LEAF_WORDS;
+    for (uint32_t q = sq + gl; q < sq + snq; q += 16) {
+      // message byte 8q <-> value byte 8q - P <-> buffer byte svs + 8q - P (may precede the span)
+      const int64_t bp = (int64_t)svs + 8 * (int64_t)q - (int64_t)sP;
+      const int64_t wa = bp >> 3;  // arithmetic shift: floor
+      const uint32_t sh = (uint32_t)(bp & 7);
+      const uint64_t lo = (wa >= (int64_t)w_first && (uint64_t)wa <= w_last) ? vw[wa] : 0;
+      const uint64_t hi = (sh && wa + 1 >= (int64_t)w_first && (uint64_t)(wa + 1) <= w_last) ? vw[wa + 1] : 0;
+      uint64_t x = sh ? (lo >> (8 * sh)) | (hi << (64 - 8 * sh)) : lo;
+      // keep message bytes [P, L) of this word
+      const uint32_t b0 = 8 * q;
+      if (b0 < sP) x &= ~low_bytes_mask(sP - b0);
+      if (b0 + 8 > sL) x &= low_bytes_mask(sL - b0);
+      dst[q] = x;
+    }
+  }
+  __syncthreads();
+  unsigned long long perms = 0, hashes = 0, inl = 0;
+  if (valid) {
+    uint32_t in1 = 0;
+    if (shortl) {
+      uint64_t* my = msg + threadIdx.x * LEAF_WORDS;
+      BW w(my, 1);
+      leaf_header(w, k, g, vlen);
+      if (vlen) w.flush_or();
+      else w.flush();
+      perms = leaf_hash_at(T, i, my, 1, g.L, &in1);
+    } else {
+      op_leaf_prep(T, i, T.vals + off, vlen);  // arena
+      perms = leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, g.L, &in1);
+    }
+    hashes = perms ? 1 : 0;
+    inl = in1;
+  }
+  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
+}
+
 // one level: `first` = its first position in the level order, `cnt` = its size
 __global__ void __launch_bounds__(BS) k_branch_prep(Topo T, const uint32_t* order, uint64_t first, uint64_t cnt) {
   uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -858,12 +935,14 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   if (nb == 0) std::fill(lbh.begin(), lbh.end(), 0u);
 
   // ---- phase-2 workspace: child records + node arena
-  c->ws2.ensure(carve_size({C * 32, C * 2, (uint64_t)LEAF_WORDS * 8 * m, lf_bytes + 64, (uint64_t)BR_WORDS * 8 * B,
+  // leaf encodings are kept (transposed message slots) only when the node set is emitted
+  const uint64_t lmsg_words = A.emit ? (uint64_t)LEAF_WORDS * m : 0;
+  c->ws2.ensure(carve_size({C * 32, C * 2, lmsg_words * 8, lf_bytes + 64, (uint64_t)BR_WORDS * 8 * B,
                             (uint64_t)EXT_WORDS * 8 * B}));
   Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
   T.cref = cv2.take<uint64_t>(C * 4);
   T.cmeta = cv2.take<uint16_t>(C);
-  T.lmsg = cv2.take<uint64_t>((uint64_t)LEAF_WORDS * m);
+  T.lmsg = A.emit ? cv2.take<uint64_t>(lmsg_words) : nullptr;
   T.lstride = m;
   T.arena = cv2.take<uint8_t>(lf_bytes + 64);  // long leaves
   T.bmsg = cv2.take<uint64_t>((uint64_t)BR_WORDS * B);
@@ -871,11 +950,17 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.lb = lb;
   HIPCHK(hipEventRecord(c->ev[3], st));
 
-  // ---- 4. leaves: encode into the arena, then hash
-  hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T);
-  LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_leaf_hash, GRID(m, BS), dim3(BS), 0, st, T);
-  LAUNCH_CHECK();
+  // ---- 4. leaves: encode + hash in LDS (root only), or encode into message slots
+  //         that the node-set emitter reads back, then hash
+  if (A.emit) {
+    hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_leaf_hash, GRID(m, BS), dim3(BS), 0, st, T);
+    LAUNCH_CHECK();
+  } else {
+    hipLaunchKernelGGL(k_leaf_fused, GRID(m, BS), dim3(BS), 0, st, T);
+    LAUNCH_CHECK();
+  }
   HIPCHK(hipEventRecord(c->ev[4], st));
 
   // ---- 5. branch levels, deepest first: encode (gathers the children's refs), then hash

@@ -103,6 +103,9 @@ struct BW {
   KH_HD void flush() {
     if (fill) *dst = acc;
   }
+  KH_HD void flush_or() {  // the rest of the last word already holds bytes written elsewhere
+    if (fill) *dst = (*dst & ~low_bytes_mask(fill)) | acc;
+  }
   KH_HD void len_prefix(uint64_t len, uint32_t offset) {  // RLP.encodeLength
     if (len < 56) {
       put1((uint32_t)(len + offset));
@@ -458,7 +461,7 @@ KH_HD void op_leaf_topo(const Topo& T, uint64_t i) {
   const uint8_t* vp;
   uint64_t vlen;
   leaf_value(T, i, &vp, &vlen);
-  uint32_t v0 = vlen ? (uint32_t)load64u_n(vp, 1) & 0xFF : 0;
+  uint32_t v0 = vlen == 1 ? (uint32_t)*vp : 0;  // the first byte matters only for a 1-byte value
   uint64_t L = leaf_enc_len((uint32_t)(P.pd + 1), vlen, v0);
   T.lf_aoff[i] = L > LEAF_SHORT_MAX ? (L + 7) & ~(uint64_t)7 : 0;
 }
@@ -528,26 +531,47 @@ KH_HD void bw_ref(BW& w, const uint64_t r[4], uint32_t len) {  // child referenc
 }
 
 // ---- leaf prep: [HP(path, leaf), value] into the message store (thread per leaf)
+// Leaf encoding RLP[HP(path, leaf), value] (MerklePatriciaTrie.scala:565-583):
+// a header of P = L - vlen bytes (list prefix, HP prefix, key suffix, value prefix)
+// followed by the value bytes.
+struct LeafGeom {
+  uint32_t s;        // first path nibble (parent depth + 1)
+  uint32_t h;        // HP bytes
+  uint32_t hp0;      // first HP byte
+  uint64_t payload;  // list payload length
+  uint32_t L;        // encoding length
+  uint32_t v0;       // the value's first byte (only read for a 1-byte value)
+};
+KH_HD LeafGeom leaf_geom(const Key4& k, int32_t pd, uint64_t vlen, uint32_t v0) {
+  LeafGeom g;
+  g.s = (uint32_t)(pd + 1);
+  uint32_t p = 64 - g.s;
+  g.h = p / 2 + 1;
+  g.hp0 = (p & 1) ? (0x30u | key_nibble(k, (int)g.s)) : 0x20u;
+  uint64_t hpl = g.h == 1 ? 1 : 1 + g.h;
+  g.payload = hpl + rlp_str_len(vlen, v0);
+  g.L = (uint32_t)(rlp_hdr_len(g.payload) + g.payload);
+  g.v0 = v0;
+  return g;
+}
+KH_HD void leaf_header(BW& w, const Key4& k, const LeafGeom& g, uint64_t vlen) {
+  w.len_prefix(g.payload, 0xC0);
+  if (g.h > 1) w.put1(0x80 + g.h);
+  w.put1(g.hp0);
+  w.key_suffix(k, (g.s + 1) / 2);
+  if (!(vlen == 1 && g.v0 < 0x80)) w.len_prefix(vlen, 0x80);
+}
+
 // vp: the value bytes (global memory, or a staged copy in LDS on the device)
 KH_HD void op_leaf_prep(const Topo& T, uint64_t i, const uint8_t* vp, uint64_t vlen) {
   Key4 k = load_key(T.skey, i);
-  int32_t pd = T.lf_pd[i];
-  uint32_t s = (uint32_t)(pd + 1);
-  uint32_t v0 = vlen ? (uint32_t)load64u_n(vp, 1) & 0xFF : 0;
-  uint32_t p = 64 - s, h = p / 2 + 1;
-  uint32_t hp0 = (p & 1) ? (0x30u | key_nibble(k, (int)s)) : 0x20u;
-  uint64_t hpl = h == 1 ? 1 : 1 + h;
-  uint64_t payload = hpl + rlp_str_len(vlen, v0);
-  uint32_t L = (uint32_t)(rlp_hdr_len(payload) + payload);
-  BW w = L <= LEAF_SHORT_MAX ? BW(T.lmsg + i, T.lstride) : BW((uint64_t*)(T.arena + T.lf_aoff[i]), 1);
-  w.len_prefix(payload, 0xC0);
-  if (h > 1) w.put1(0x80 + h);
-  w.put1(hp0);
-  w.key_suffix(k, (s + 1) / 2);
-  if (!(vlen == 1 && v0 < 0x80)) w.len_prefix(vlen, 0x80);
+  uint32_t v0 = vlen == 1 ? (uint32_t)*vp : 0;  // the first byte matters only for a 1-byte value
+  LeafGeom g = leaf_geom(k, T.lf_pd[i], vlen, v0);
+  BW w = g.L <= LEAF_SHORT_MAX ? BW(T.lmsg + i, T.lstride) : BW((uint64_t*)(T.arena + T.lf_aoff[i]), 1);
+  leaf_header(w, k, g, vlen);
   w.bytes(vp, vlen);
   w.flush();
-  T.lf_len[i] = L;
+  T.lf_len[i] = g.L;
 }
 
 // Keccak-256 of a message whose words are `stride` words apart (any length)
@@ -578,23 +602,22 @@ KH_HD void kec256_strided(const uint64_t* w, uint64_t stride, uint32_t len, uint
 }
 
 // ---- leaf hash (thread per leaf).  Returns permutations spent.
-KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
-  uint32_t L = T.lf_len[i];
+// hash + publish of leaf i whose encoding (L bytes) sits at w, words `stride` apart
+KH_HD uint32_t leaf_hash_at(const Topo& T, uint64_t i, const uint64_t* w, uint64_t stride, uint32_t L,
+                            uint32_t* inl) {
   uint32_t parent = T.lf_parent[i];
   bool top = parent == NONE;
   uint64_t hh[4] = {0, 0, 0, 0}, head[4];
   uint32_t perms = 0;
   if (L <= LEAF_SHORT_MAX) {
-    const uint64_t* w = T.lmsg + i;
     if (L >= 32 || top) {
-      kec256_strided(w, T.lstride, L, hh);
+      kec256_strided(w, stride, L, hh);
       perms = 1;
     }
-    for (int q = 0; q < 4; ++q) head[q] = (8u * q < L) ? w[q * T.lstride] : 0;
+    for (int q = 0; q < 4; ++q) head[q] = (8u * q < L) ? w[q * stride] : 0;
   } else {
-    const uint64_t* enc = (const uint64_t*)(T.arena + T.lf_aoff[i]);
-    perms = hash_node(enc, L, top, hh);
-    for (int q = 0; q < 4; ++q) head[q] = enc[q];
+    perms = hash_node(w, L, top, hh);
+    for (int q = 0; q < 4; ++q) head[q] = w[q];
   }
   if (T.lf_hash)
     for (int j = 0; j < 4; ++j) T.lf_hash[4 * i + j] = hh[j];
@@ -607,6 +630,12 @@ KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
   publish_ref(T, parent, T.lf_pord[i], nib, i, head, L, hh);
   *inl = (L < 32 && !top) ? 1 : 0;
   return perms;
+}
+
+KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
+  uint32_t L = T.lf_len[i];
+  if (L <= LEAF_SHORT_MAX) return leaf_hash_at(T, i, T.lmsg + i, T.lstride, L, inl);
+  return leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, L, inl);
 }
 
 // ---- branch prep: [ref_0 .. ref_15, ""] into its message slot (thread per branch of
