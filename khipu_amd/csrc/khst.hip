@@ -389,11 +389,13 @@ __global__ void __launch_bounds__(BS) k_leaf_fused(Topo T) {
   const uint32_t qlo = P >> 3, nq = (shortl && vlen) ? ((g.L + 7) >> 3) - qlo : 0;
   const uint32_t gi = ln >> 4, gl = ln & 15;
   for (uint32_t it = 0; it < 16; ++it) {
-    const int src = (int)(it * 4 + gi);
+    const int src = (int)(it * 4 + gi);  // src is usually in another 16-lane group:
+    // every shuffle runs with the whole wave active (a lane masked off by an early
+    // `continue` would hand its neighbours undefined data)
     const uint32_t snq = __shfl(nq, src);
-    if (snq == 0) continue;
     const uint64_t svs = __shfl(vs, src);
     const uint32_t sP = __shfl(P, src), sL = __shfl(g.L, src), sq = __shfl(qlo, src);
+    if (snq == 0) continue;
     const uint64_t w_first = svs >> 3, w_last = (svs + (sL - sP) - 1) >> 3;
     uint64_t* dst = msg + (wbase + src) * LEAF_WORDS;
     for (uint32_t q = sq + gl; q < sq + snq; q += 16) {
