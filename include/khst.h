@@ -147,6 +147,32 @@ int kh_dev_partition(kh_ctx* ctx, const uint8_t* d_keys32, const uint8_t* d_vals
                      uint64_t n, uint32_t nparts, uint8_t* d_out_keys, uint8_t* d_out_vals, uint64_t* d_out_vlen,
                      uint64_t* h_counts, uint64_t* h_bytes);
 
+/* ---- resident trie: incremental commit ----
+ * A trie kept in HBM between commits: its sorted (key, value) set and the capped
+ * reference of every branch node.  Replaces the per-key fold of TrieAccounts.flush /
+ * TrieStorage.flush (TrieAccounts.scala:22-28, TrieStorage.scala:43-60) over
+ * MerklePatriciaTrie.put / remove (MerklePatriciaTrie.scala:157-281, 290-477): a commit
+ * merges the batch, rebuilds the topology, and re-hashes only the branches on the
+ * changed keys' paths (clean branches keep their references).  Device buffers; the
+ * handle owns its HBM and uses its context's stream (one thread at a time). */
+typedef struct kh_trie kh_trie;
+
+/* Build from n records (keys as in kh_dev_trie_build; duplicates: the later wins). */
+int kh_trie_open(kh_ctx* ctx, const uint8_t* d_keys, uint32_t klen, const uint8_t* d_vals, const uint64_t* d_voff,
+                 uint64_t n, uint32_t flags, uint8_t root32[32], kh_trie** out);
+
+/* One commit: nup upserts (keys, packed values with d_up_voff[nup+1]) and ndel deletes,
+ * klen-byte keys (32, or any with KH_HASH_KEYS).  The batch is applied as upserts then
+ * deletes with the last op on a key winning; deleting an absent key is a no-op
+ * (MerklePatriciaTrie.remove of a missing key leaves the trie unchanged).
+ * root32 receives the new root.  stats: n_node_hashes counts the re-hashed nodes only. */
+int kh_trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals, const uint64_t* d_up_voff,
+                  uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
+                  uint8_t root32[32], kh_stats* stats);
+
+int kh_trie_size(const kh_trie* h, uint64_t* n);
+int kh_trie_free(kh_trie* h);
+
 /* Synthetic account generator (pinned in khipu_amd/csrc/synth.h): writes
  * accounts [first, first+n) of config `cfg` — 20-byte addresses (d_addr, n*20 B) and RLP
  * account bodies packed at d_vals with d_voff[n+1] (offsets relative to d_vals; d_vals

@@ -26,6 +26,7 @@
 #include "prims.h"
 #include "synth.h"
 #include "trie_ops.h"
+#include "resident.h"
 
 using namespace khst;
 
@@ -366,7 +367,7 @@ __global__ void __launch_bounds__(BS) k_leaf_fused(Topo T) {
   __shared__ uint64_t msg[BS * LEAF_WORDS];
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u;
-  const bool valid = i < T.m;
+  const bool valid = i < T.m && !under_clean(T, T.lf_parent[i]);
   uint64_t off = 0;
   uint32_t vlen = 0, v0 = 0;
   Key4 k{0, 0, 0, 0};
@@ -536,6 +537,46 @@ __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uin
   for (; q < L; ++q) dst[q] = src[q];
 }
 
+// ---- resident trie: merge a sorted batch into the sorted (key, value) set (resident.h)
+__global__ void __launch_bounds__(BS) k_op_locate(Merge M) {
+  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o < M.nops) op_locate(M, o);
+}
+__global__ void __launch_bounds__(BS) k_op_mark(Merge M) {
+  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o < M.nops) op_mark(M, o, [](uint32_t* p) { atomicAdd(p, 1u); });
+}
+__global__ void __launch_bounds__(BS) k_place_resident(Merge M, const uint32_t* del_flag) {
+  uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (j < M.m) op_place_resident(M, del_flag, j);
+}
+__global__ void __launch_bounds__(BS) k_place_op(Merge M, const uint32_t* ins_flag, const uint32_t* eff_flag) {
+  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o < M.nops) op_place_op(M, ins_flag, eff_flag, o);
+}
+// value bytes of the merged set: from the resident buffer or the upsert buffer
+__global__ void __launch_bounds__(BS) k_merge_vals(const uint64_t* nsrc, const uint32_t* nlen, const uint64_t* noff,
+                                                  uint64_t m, const uint8_t* rval, const uint8_t* uval,
+                                                  uint8_t* nval) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= m) return;
+  uint64_t s = nsrc[i];
+  const uint8_t* src = (s & SRC_UPSERT) ? uval + (s & ~SRC_UPSERT) : rval + s;
+  copy_bytes(nval + noff[i], src, nlen[i]);
+}
+__global__ void __launch_bounds__(BS) k_u32_to_u64(const uint32_t* in, uint64_t* out, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < n) out[i] = in[i];
+}
+__global__ void __launch_bounds__(BS) k_br_dirty(Topo T, const uint64_t* dkey, uint64_t nd, const uint32_t* Bp) {
+  uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (j < *Bp) op_br_dirty(T, dkey, nd, (uint32_t)j);
+}
+__global__ void __launch_bounds__(BS) k_br_clean(Topo T, Prev V, const uint32_t* Bp) {
+  uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (j < *Bp) op_br_clean(T, V, (uint32_t)j);
+}
+
 // ---- multi-GPU routing: stable partition of records by top-nibble owner
 __device__ __forceinline__ uint32_t nibble_owner(uint64_t w0, uint32_t nparts) {
   return (((uint32_t)(w0 & 0xFF) >> 4) * nparts) >> 4;
@@ -663,6 +704,24 @@ struct BuildArgs {
   uint32_t depth0;
   uint32_t flags;
   bool emit;
+  bool presorted = false;       // keys sorted and unique (a resident trie's merged set)
+  struct IncArgs* inc = nullptr;  // resident-trie bookkeeping (nullable)
+};
+// resident-trie bookkeeping of one build (kh_trie_open / kh_trie_apply)
+struct IncArgs {
+  // in: the changed keys (nullptr: a first build, every branch dirty) and the
+  // previous version's tables
+  const uint64_t* dkey = nullptr;
+  uint64_t nd = 0;
+  Prev V{};
+  // out: this version's tables
+  DevBuf* ref = nullptr;   // [B*4] branch references
+  DevBuf* rlen = nullptr;  // [B]
+  DevBuf* u = nullptr;     // [nb] boundary values
+  DevBuf* pyr = nullptr;   // pyramid levels >= 1
+  DevBuf* bid = nullptr;   // [nb] scanned rep flags
+  Pyr P{};                 // rebased onto *u / *pyr
+  uint64_t nb = 0;
 };
 struct BuildOut {
   std::vector<uint64_t> res_hash;  // nres*4
@@ -680,6 +739,122 @@ static float ev_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0;
   if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
   return ms;
+}
+
+// Sort n 32-byte keys (with optional segment ids) and drop duplicates, keeping the
+// last of equal keys.  Outputs the sorted keys, the input index of each and m.
+struct SortIO {
+  const uint64_t* K32;
+  const uint32_t* seg;
+  uint32_t sb;
+  uint64_t n;
+  uint64_t *ck0, *ck1;
+  uint32_t *idx0, *idx1;
+  uint64_t* skey;
+  uint32_t* sseg;
+  void* rs_scratch;
+  void* scan_scratch;
+  unsigned long long* ctr;
+  // out
+  uint64_t m;
+  uint32_t* sidx;
+  bool fallback;
+};
+static void sort_dedup(kh_ctx* c, SortIO& S) {
+  hipStream_t st = c->st;
+  const uint64_t n = S.n;
+  const uint64_t* K32 = S.K32;
+  const uint32_t* seg = S.seg;
+  const uint32_t sb = S.sb;
+  const bool segmented = seg != nullptr;
+  uint64_t *ck0 = S.ck0, *ck1 = S.ck1;
+  uint32_t *idx0 = S.idx0, *idx1 = S.idx1;
+  uint64_t* skey = S.skey;
+  uint32_t* sseg = S.sseg;
+  void* rs_scratch = S.rs_scratch;
+  void* scan_scratch = S.scan_scratch;
+  struct {
+    unsigned long long* ctr;
+  } T{S.ctr};
+  // ---- 2. sort: LSD radix on the top 32 bits of the composite (segment | key) prefix,
+  // then fix the rare runs of equal prefixes locally (k_tie_fix); a full 256-bit sort
+  // only if a run is longer than TIE_RUN_MAX (adversarial keys)
+  hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, sb, n, ck0, idx0);
+  LAUNCH_CHECK();
+  bool flip = radix_sort_pairs(ck0, idx0, ck1, idx1, n, 32, 64, rs_scratch, st);
+  uint64_t* cks = flip ? ck1 : ck0;
+  uint32_t* idxs = flip ? idx1 : idx0;
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, (const uint32_t*)idxs, n,
+                     skey, sseg);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_tie_fix, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, n, skey, idxs, sseg,
+                     T.ctr + CTR_TIE);
+  LAUNCH_CHECK();
+  HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint64_t tie_flags = c->h_pinned[0];
+  const bool fallback = tie_flags & 1, dups = tie_flags & 2;
+  uint64_t m = n;
+  uint32_t* sidx = idxs;
+  if (fallback) {
+    // full 256-bit (+segment) LSD sort from the input order
+    uint32_t* ia = idx0;
+    uint32_t* ib = idx1;
+    uint64_t* ka = ck0;
+    uint64_t* kb = ck1;
+    hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, 0u, n, ka, ia);
+    LAUNCH_CHECK();
+    auto pass = [&](int word, int bits) {
+      if (word >= 0)
+        hipLaunchKernelGGL(k_word_key, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, (const uint32_t*)ia, word,
+                           n, ka);
+      else
+        hipLaunchKernelGGL(k_seg_key, GRID(n, BS), dim3(BS), 0, st, seg, (const uint32_t*)ia, n, ka);
+      LAUNCH_CHECK();
+      if (radix_sort_pairs(ka, ia, kb, ib, n, 0, bits, rs_scratch, st)) {
+        std::swap(ka, kb);
+        std::swap(ia, ib);
+      }
+    };
+    for (int w = 3; w >= 0; --w) pass(w, 64);
+    if (segmented) pass(-1, ((sb + 7) / 8) * 8);
+    hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, (const uint32_t*)ia, n,
+                       skey, sseg);
+    LAUNCH_CHECK();
+    sidx = ia;
+  }
+  if (fallback || dups) {
+    // keep the LAST of equal keys (later puts win): flags, scan, compaction
+    uint32_t* keep = (uint32_t*)(sidx == idx0 ? ck1 : ck0);  // n*8 free bytes
+    uint32_t* keep_pos = sidx == idx0 ? idx1 : idx0;
+    hipLaunchKernelGGL(k_dup, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)skey, (const uint32_t*)sseg, n, keep);
+    LAUNCH_CHECK();
+    uint32_t* mtot = (uint32_t*)(T.ctr + CTR_M);
+    scan_exclusive<uint32_t>(keep, keep_pos, n, mtot, scan_scratch, st);
+    HIPCHK(hipMemcpyAsync(c->h_pinned, mtot, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    m = (uint32_t)c->h_pinned[0];
+    if (m < n) {
+      c->ws3.ensure(carve_size({n * 32, n * 4, n * 4}));
+      Carver c3{(char*)c->ws3.p, 0, c->ws3.cap};
+      uint64_t* skey2 = c3.take<uint64_t>(n * 4);
+      uint32_t* sidx2 = c3.take<uint32_t>(n);
+      uint32_t* sseg2 = segmented ? c3.take<uint32_t>(n) : nullptr;
+      hipLaunchKernelGGL(k_compact, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)skey, (const uint32_t*)sidx,
+                         (const uint32_t*)sseg, (const uint32_t*)keep_pos, (const uint32_t*)keep, n, skey2, sidx2,
+                         sseg2);
+      LAUNCH_CHECK();
+      skey = skey2;
+      sidx = sidx2;
+      sseg = sseg2;
+    }
+  }
+  S.m = m;
+  S.sidx = sidx;
+  S.skey = skey;
+  S.sseg = sseg;
+  S.fallback = fallback;
 }
 
 static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats) {
@@ -707,7 +882,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // ---- phase-1 workspace (sized by n)
   const uint64_t nb1 = n;  // boundaries <= n-1; round up
   // keys are moved as 16-byte vectors: caller keys that are not 16-byte aligned get copied
-  const bool own_keys = (A.flags & KH_HASH_KEYS) || ((uintptr_t)A.keys & 15);
+  const bool own_keys = !A.presorted && ((A.flags & KH_HASH_KEYS) || ((uintptr_t)A.keys & 15));
   std::vector<size_t> sz = {
       own_keys ? n * 32 : 0,                  // K32
       n * 8, n * 8, n * 4, n * 4,             // ck0 ck1 idx0 idx1
@@ -792,79 +967,20 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   }
   HIPCHK(hipEventRecord(c->ev[1], st));
 
-  // ---- 2. sort: LSD radix on the top 32 bits of the composite (segment | key) prefix,
-  // then fix the rare runs of equal prefixes locally (k_tie_fix); a full 256-bit sort
-  // only if a run is longer than TIE_RUN_MAX (adversarial keys)
-  hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, sb, n, ck0, idx0);
-  LAUNCH_CHECK();
-  bool flip = radix_sort_pairs(ck0, idx0, ck1, idx1, n, 32, 64, rs_scratch, st);
-  uint64_t* cks = flip ? ck1 : ck0;
-  uint32_t* idxs = flip ? idx1 : idx0;
-  LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, (const uint32_t*)idxs, n,
-                     skey, sseg);
-  LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_tie_fix, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, n, skey, idxs, sseg,
-                     T.ctr + CTR_TIE);
-  LAUNCH_CHECK();
-  HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  const uint64_t tie_flags = c->h_pinned[0];
-  const bool fallback = tie_flags & 1, dups = tie_flags & 2;
+  // ---- 2. sort + dedup
   uint64_t m = n;
-  uint32_t* sidx = idxs;
-  if (fallback) {
-    // full 256-bit (+segment) LSD sort from the input order
-    uint32_t* ia = idx0;
-    uint32_t* ib = idx1;
-    uint64_t* ka = ck0;
-    uint64_t* kb = ck1;
-    hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, 0u, n, ka, ia);
-    LAUNCH_CHECK();
-    auto pass = [&](int word, int bits) {
-      if (word >= 0)
-        hipLaunchKernelGGL(k_word_key, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, (const uint32_t*)ia, word,
-                           n, ka);
-      else
-        hipLaunchKernelGGL(k_seg_key, GRID(n, BS), dim3(BS), 0, st, A.seg, (const uint32_t*)ia, n, ka);
-      LAUNCH_CHECK();
-      if (radix_sort_pairs(ka, ia, kb, ib, n, 0, bits, rs_scratch, st)) {
-        std::swap(ka, kb);
-        std::swap(ia, ib);
-      }
-    };
-    for (int w = 3; w >= 0; --w) pass(w, 64);
-    if (segmented) pass(-1, ((sb + 7) / 8) * 8);
-    hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, A.seg, (const uint32_t*)ia, n,
-                       skey, sseg);
-    LAUNCH_CHECK();
-    sidx = ia;
-  }
-  if (fallback || dups) {
-    // keep the LAST of equal keys (later puts win): flags, scan, compaction
-    uint32_t* keep = (uint32_t*)(sidx == idx0 ? ck1 : ck0);  // n*8 free bytes
-    uint32_t* keep_pos = sidx == idx0 ? idx1 : idx0;
-    hipLaunchKernelGGL(k_dup, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)skey, (const uint32_t*)sseg, n, keep);
-    LAUNCH_CHECK();
-    uint32_t* mtot = (uint32_t*)(T.ctr + CTR_M);
-    scan_exclusive<uint32_t>(keep, keep_pos, n, mtot, scan_scratch, st);
-    HIPCHK(hipMemcpyAsync(c->h_pinned, mtot, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    m = (uint32_t)c->h_pinned[0];
-    if (m < n) {
-      c->ws3.ensure(carve_size({n * 32, n * 4, n * 4}));
-      Carver c3{(char*)c->ws3.p, 0, c->ws3.cap};
-      uint64_t* skey2 = c3.take<uint64_t>(n * 4);
-      uint32_t* sidx2 = c3.take<uint32_t>(n);
-      uint32_t* sseg2 = segmented ? c3.take<uint32_t>(n) : nullptr;
-      hipLaunchKernelGGL(k_compact, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)skey, (const uint32_t*)sidx,
-                         (const uint32_t*)sseg, (const uint32_t*)keep_pos, (const uint32_t*)keep, n, skey2, sidx2,
-                         sseg2);
-      LAUNCH_CHECK();
-      skey = skey2;
-      sidx = sidx2;
-      sseg = sseg2;
-    }
+  uint32_t* sidx = nullptr;
+  bool fallback = false;
+  if (A.presorted) {
+    skey = (uint64_t*)A.keys;  // sorted, unique (the merged set of a resident trie)
+  } else {
+    SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr};
+    sort_dedup(c, S);
+    m = S.m;
+    sidx = S.sidx;
+    skey = S.skey;
+    sseg = S.sseg;
+    fallback = S.fallback;
   }
   const bool ties = fallback;
   T.m = m;
@@ -880,10 +996,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   unsigned long long* ctr = T.ctr;
   uint32_t* Bp = (uint32_t*)(ctr + CTR_B);
   HIPCHK(hipMemsetAsync(ctr + CTR_B, 0, 8 * 6, st));  // B, br bytes, lf bytes, C, E0, E1
+  Pyr P{};
   if (nb > 0) {
     hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
-    Pyr P{};
     P.lv[0] = T.u;
     P.sz[0] = nb;
     P.nl = 1;
@@ -939,8 +1055,9 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // ---- phase-2 workspace: child records + node arena
   // leaf encodings are kept (transposed message slots) only when the node set is emitted
   const uint64_t lmsg_words = A.emit ? (uint64_t)LEAF_WORDS * m : 0;
+  const bool inc_dirty = A.inc && A.inc->dkey;
   c->ws2.ensure(carve_size({C * 32, C * 2, lmsg_words * 8, lf_bytes + 64, (uint64_t)BR_WORDS * 8 * B,
-                            (uint64_t)EXT_WORDS * 8 * B}));
+                            (uint64_t)EXT_WORDS * 8 * B, inc_dirty ? B : 0}));
   Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
   T.cref = cv2.take<uint64_t>(C * 4);
   T.cmeta = cv2.take<uint16_t>(C);
@@ -950,6 +1067,21 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.bmsg = cv2.take<uint64_t>((uint64_t)BR_WORDS * B);
   T.xmsg = cv2.take<uint64_t>((uint64_t)EXT_WORDS * B);
   T.lb = lb;
+  if (A.inc) {
+    IncArgs& I = *A.inc;
+    I.ref->ensure(B * 32 + 64);
+    I.rlen->ensure(B * 4 + 64);
+    T.br_ref = (uint64_t*)I.ref->p;
+    T.br_rlen = (uint32_t*)I.rlen->p;
+    if (inc_dirty && B) {
+      // dirty = prefix of a changed key; clean branches take the previous reference
+      T.br_dirty = cv2.take<uint8_t>(B);
+      hipLaunchKernelGGL(k_br_dirty, GRID(B, BS), dim3(BS), 0, st, T, I.dkey, I.nd, (const uint32_t*)Bp);
+      LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_br_clean, GRID(B, BS), dim3(BS), 0, st, T, I.V, (const uint32_t*)Bp);
+      LAUNCH_CHECK();
+    }
+  }
   HIPCHK(hipEventRecord(c->ev[3], st));
 
   // ---- 4. leaves: encode + hash in LDS (root only), or encode into message slots
@@ -986,6 +1118,24 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   HIPCHK(hipMemcpyAsync(O.res_inl.data(), T.res_inl, nres * 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_pinned, ctr, CTR_N * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (c->h_pinned[CTR_ERR]) throw KhError{KH_EINTERNAL, "incremental commit: clean branch not found in the previous version"};
+  if (A.inc) {  // keep this version's tables for the next commit
+    IncArgs& I = *A.inc;
+    I.nb = nb;
+    I.P = Pyr{};
+    if (nb > 0) {
+      uint64_t pyr_bytes = (uint64_t)(P.lv[P.nl - 1] - pyr) + P.sz[P.nl - 1];
+      I.u->ensure(nb + 64);
+      I.bid->ensure(nb * 4 + 64);
+      I.pyr->ensure(pyr_bytes + 64);
+      HIPCHK(hipMemcpyAsync(I.u->p, T.u, nb, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(I.bid->p, T.isrep_bid, nb * 4, hipMemcpyDeviceToDevice, st));
+      if (P.nl > 1) HIPCHK(hipMemcpyAsync(I.pyr->p, pyr, pyr_bytes, hipMemcpyDeviceToDevice, st));
+      I.P = P;
+      I.P.lv[0] = (const uint8_t*)I.u->p;
+      for (int L = 1; L < P.nl; ++L) I.P.lv[L] = (const uint8_t*)I.pyr->p + (P.lv[L] - pyr);
+    }
+  }
   c->T = T;
   c->last_B = B;
   c->last_nres = nres;
@@ -1092,6 +1242,237 @@ static void copy_root(const BuildOut& O, uint64_t r, uint8_t* out32) {
     memcpy(out32, EMPTY_TRIE_HASH, 32);
   else
     memcpy(out32, &O.res_hash[4 * r], 32);
+}
+
+// ---------------------------------------------------------------------------
+// resident trie: sorted (key, value) set + branch references in HBM
+// ---------------------------------------------------------------------------
+struct kh_trie {
+  kh_ctx* c = nullptr;
+  uint64_t m = 0;  // keys
+  int cur = 0;     // current half of the double buffers
+  DevBuf key[2], val[2], off[2], ref[2], rlen[2];
+  DevBuf u, pyr, bid;  // the current version's topology tables
+  Pyr P{};
+  uint64_t nb = 0;
+  DevBuf mws;  // merge scratch
+  uint8_t root[32] = {};
+};
+
+// keep the sorted set of the build just run (c->T): keys, then the value spans
+// compacted in key order
+static void save_sorted(kh_trie* h, int half, uint64_t m, const uint8_t* vals) {
+  kh_ctx* c = h->c;
+  hipStream_t st = c->st;
+  const Topo& T = c->T;
+  h->key[half].ensure(m * 32 + 64);
+  h->off[half].ensure((m + 1) * 8 + 64);
+  uint64_t* off = (uint64_t*)h->off[half].p;
+  HIPCHK(hipMemsetAsync(off, 0, (m + 1) * 8, st));
+  if (m == 0) return;
+  HIPCHK(hipMemcpyAsync(h->key[half].p, T.skey, m * 32, hipMemcpyDeviceToDevice, st));
+  h->mws.ensure(carve_size({m * 8, scan_scratch_bytes(m, 8), 64}));
+  Carver cv{(char*)h->mws.p, 0, h->mws.cap};
+  uint64_t* len64 = cv.take<uint64_t>(m);
+  void* scr = cv.take<char>(scan_scratch_bytes(m, 8));
+  uint64_t* tot = cv.take<uint64_t>(8);
+  hipLaunchKernelGGL(k_u32_to_u64, GRID(m, BS), dim3(BS), 0, st, (const uint32_t*)T.svlen, len64, m);
+  LAUNCH_CHECK();
+  scan_exclusive<uint64_t>(len64, off, m, tot, scr, st);
+  HIPCHK(hipMemcpyAsync(off + m, tot, 8, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync(c->h_pinned, tot, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  uint64_t vbytes = c->h_pinned[0];
+  h->val[half].ensure(vbytes + 64);
+  hipLaunchKernelGGL(k_merge_vals, GRID(m, BS), dim3(BS), 0, st, (const uint64_t*)T.svoff, (const uint32_t*)T.svlen,
+                     (const uint64_t*)off, m, vals, (const uint8_t*)nullptr, (uint8_t*)h->val[half].p);
+  LAUNCH_CHECK();
+  HIPCHK(hipStreamSynchronize(st));
+}
+
+static IncArgs inc_out(kh_trie* h, int half) {
+  IncArgs I;
+  I.ref = &h->ref[half];
+  I.rlen = &h->rlen[half];
+  I.u = &h->u;
+  I.pyr = &h->pyr;
+  I.bid = &h->bid;
+  return I;
+}
+
+static void trie_open(kh_trie* h, const uint8_t* d_keys, uint32_t klen, const uint8_t* d_vals, const uint64_t* d_voff,
+                      uint64_t n, uint32_t flags, kh_stats* stats) {
+  IncArgs I = inc_out(h, 0);
+  BuildArgs A{d_keys, klen, d_vals, d_voff, n, nullptr, 1, 0, flags, false};
+  A.inc = &I;
+  BuildOut O;
+  run_build(h->c, A, O, stats);
+  uint64_t m = n ? h->c->T.m : 0;
+  save_sorted(h, 0, m, d_vals);
+  h->m = m;
+  h->cur = 0;
+  h->P = I.P;
+  h->nb = I.nb;
+  copy_root(O, 0, h->root);
+}
+
+// One commit: upserts (d_up_*) then deletes, the last op on a key winning.
+static void trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals, const uint64_t* d_up_voff,
+                       uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
+                       kh_stats* stats) {
+  kh_ctx* c = h->c;
+  hipStream_t st = c->st;
+  if (stats) memset(stats, 0, sizeof(*stats));
+  const uint64_t nops = nup + ndel, m = h->m;
+  if (nops == 0) return;
+  if (nops >= (1ULL << 31) || m + nops >= (1ULL << 31)) throw KhError{KH_EINVAL, "batch too large"};
+  if (!(flags & KH_HASH_KEYS) && klen != 32) throw KhError{KH_EINVAL, "keys must be 32 bytes unless KH_HASH_KEYS"};
+  const int cur = h->cur, nxt = 1 - cur;
+  const uint64_t mx = m + nops;  // merged size bound
+  // ---- scratch
+  std::vector<size_t> sz = {
+      nops * 32,                                   // K (op keys)
+      nops * 8, nops * 8, nops * 4, nops * 4,      // ck0 ck1 idx0 idx1
+      nops * 32, radix_scratch_bytes(nops),        // sorted op keys, radix scratch
+      scan_scratch_bytes(mx + 1, 8), CTR_N * 8,    // scan scratch, counters
+      nops * 4, nops, nops * 4, nops * 4, nops * 4, nops * 4,  // o_lb o_kind o_insf o_ins o_efff o_eff
+      (m + 1) * 4, (m + 1) * 4, (m + 1) * 4, (m + 1) * 4, m * 4 + 4,  // pos_cnt pos_ins del_flag pos_del pos_upd
+      mx * 4, mx * 8, mx * 4, mx * 8, nops * 32,   // nlen nsrc oldpos len64 dkey
+  };
+  h->mws.ensure(carve_size(sz));
+  Carver cv{(char*)h->mws.p, 0, h->mws.cap};
+  uint64_t* K = cv.take<uint64_t>(nops * 4);
+  SortIO S{};
+  S.K32 = K;
+  S.n = nops;
+  S.ck0 = cv.take<uint64_t>(nops);
+  S.ck1 = cv.take<uint64_t>(nops);
+  S.idx0 = cv.take<uint32_t>(nops);
+  S.idx1 = cv.take<uint32_t>(nops);
+  S.skey = cv.take<uint64_t>(nops * 4);
+  S.rs_scratch = cv.take<char>(radix_scratch_bytes(nops));
+  S.scan_scratch = cv.take<char>(scan_scratch_bytes(mx + 1, 8));
+  S.ctr = cv.take<unsigned long long>(CTR_N);
+  Merge M{};
+  M.o_lb = cv.take<uint32_t>(nops);
+  M.o_kind = cv.take<uint8_t>(nops);
+  uint32_t* o_insf = cv.take<uint32_t>(nops);
+  M.o_ins = cv.take<uint32_t>(nops);
+  uint32_t* o_efff = cv.take<uint32_t>(nops);
+  M.o_eff = cv.take<uint32_t>(nops);
+  M.pos_cnt = cv.take<uint32_t>(m + 1);
+  M.pos_ins = cv.take<uint32_t>(m + 1);
+  uint32_t* del_flag = cv.take<uint32_t>(m + 1);
+  M.pos_del = cv.take<uint32_t>(m + 1);
+  M.pos_upd = cv.take<uint32_t>(m + 1);
+  M.nlen = cv.take<uint32_t>(mx);
+  M.nsrc = cv.take<uint64_t>(mx);
+  M.oldpos = cv.take<uint32_t>(mx);
+  uint64_t* len64 = cv.take<uint64_t>(mx);
+  M.dkey = cv.take<uint64_t>(nops * 4);
+  HIPCHK(hipMemsetAsync(S.ctr, 0, CTR_N * 8, st));
+  HIPCHK(hipEventRecord(c->ev[6], st));
+
+  // ---- 1. op keys (hashed or copied), sorted, last op per key kept
+  if (flags & KH_HASH_KEYS) {
+    if (nup) hipLaunchKernelGGL(k_hash_keys, GRID(nup, BS), dim3(BS), 0, st, d_up_keys, klen, nup, K);
+    if (ndel) hipLaunchKernelGGL(k_hash_keys, GRID(ndel, BS), dim3(BS), 0, st, d_del_keys, klen, ndel, K + 4 * nup);
+    LAUNCH_CHECK();
+  } else {
+    if (nup) HIPCHK(hipMemcpyAsync(K, d_up_keys, nup * 32, hipMemcpyDeviceToDevice, st));
+    if (ndel) HIPCHK(hipMemcpyAsync(K + 4 * nup, d_del_keys, ndel * 32, hipMemcpyDeviceToDevice, st));
+  }
+  sort_dedup(c, S);
+  const uint64_t nsorted = S.m;
+
+  // ---- 2. merge into the other half of the double buffers
+  M.rkey = (const uint64_t*)h->key[cur].p;
+  M.roff = (const uint64_t*)h->off[cur].p;
+  M.m = m;
+  M.okey = S.skey;
+  M.oidx = S.sidx;
+  M.nops = nsorted;
+  M.nup = nup;
+  M.uoff = d_up_voff;
+  h->key[nxt].ensure(mx * 32 + 64);
+  M.nkey = (uint64_t*)h->key[nxt].p;
+  HIPCHK(hipMemsetAsync(M.pos_cnt, 0, (m + 1) * 4, st));
+  HIPCHK(hipMemsetAsync(del_flag, 0, (m + 1) * 4, st));
+  HIPCHK(hipMemsetAsync(M.pos_upd, 0xFF, (m + 1) * 4, st));
+  hipLaunchKernelGGL(k_op_locate, GRID(nsorted, BS), dim3(BS), 0, st, M);
+  LAUNCH_CHECK();
+  HIPCHK(hipMemcpyAsync(o_insf, M.o_ins, nsorted * 4, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync(o_efff, M.o_eff, nsorted * 4, hipMemcpyDeviceToDevice, st));
+  Merge Mk = M;
+  Mk.pos_del = del_flag;  // op_mark writes the raw flags
+  hipLaunchKernelGGL(k_op_mark, GRID(nsorted, BS), dim3(BS), 0, st, Mk);
+  LAUNCH_CHECK();
+  unsigned long long* tot = S.ctr + 12;  // inserts, deletes, dirty keys, value bytes (slots the sort left free)
+  scan_exclusive<uint32_t>(M.pos_cnt, M.pos_ins, m + 1, (uint32_t*)(tot + 0), S.scan_scratch, st);
+  scan_exclusive<uint32_t>(del_flag, M.pos_del, m + 1, (uint32_t*)(tot + 1), S.scan_scratch, st);
+  scan_exclusive<uint32_t>(o_insf, M.o_ins, nsorted, (uint32_t*)nullptr, S.scan_scratch, st);
+  scan_exclusive<uint32_t>(o_efff, M.o_eff, nsorted, (uint32_t*)(tot + 2), S.scan_scratch, st);
+  HIPCHK(hipMemcpyAsync(c->h_pinned, tot, 3 * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint64_t n_ins = (uint32_t)c->h_pinned[0], n_del = (uint32_t)c->h_pinned[1], nd = (uint32_t)c->h_pinned[2];
+  const uint64_t m2 = m + n_ins - n_del;
+  if (stats) {
+    stats->n_inputs = nops;
+    stats->n_leaves = m2;
+  }
+  if (nd == 0) return;  // nothing changes: same root
+  hipLaunchKernelGGL(k_place_resident, GRID(m, BS), dim3(BS), 0, st, M, (const uint32_t*)del_flag);
+  hipLaunchKernelGGL(k_place_op, GRID(nsorted, BS), dim3(BS), 0, st, M, (const uint32_t*)o_insf,
+                     (const uint32_t*)o_efff);
+  LAUNCH_CHECK();
+  h->off[nxt].ensure((m2 + 1) * 8 + 64);
+  uint64_t* noff = (uint64_t*)h->off[nxt].p;
+  HIPCHK(hipMemsetAsync(noff, 0, (m2 + 1) * 8, st));
+  if (m2) {
+    hipLaunchKernelGGL(k_u32_to_u64, GRID(m2, BS), dim3(BS), 0, st, (const uint32_t*)M.nlen, len64, m2);
+    LAUNCH_CHECK();
+    scan_exclusive<uint64_t>(len64, noff, m2, (uint64_t*)(tot + 3), S.scan_scratch, st);
+    HIPCHK(hipMemcpyAsync(noff + m2, tot + 3, 8, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned, tot + 3, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    h->val[nxt].ensure(c->h_pinned[0] + 64);
+    hipLaunchKernelGGL(k_merge_vals, GRID(m2, BS), dim3(BS), 0, st, (const uint64_t*)M.nsrc, (const uint32_t*)M.nlen,
+                       (const uint64_t*)noff, m2, (const uint8_t*)h->val[cur].p, d_up_vals,
+                       (uint8_t*)h->val[nxt].p);
+    LAUNCH_CHECK();
+  } else {
+    h->val[nxt].ensure(64);
+  }
+  HIPCHK(hipEventRecord(c->ev[7], st));
+
+  // ---- 3. topology of the merged set + hashing of the dirty branches
+  IncArgs I = inc_out(h, nxt);
+  I.dkey = M.dkey;
+  I.nd = nd;
+  I.V.P = h->P;
+  I.V.bid = (const uint32_t*)h->bid.p;
+  I.V.ref = (const uint64_t*)h->ref[cur].p;
+  I.V.rlen = (const uint32_t*)h->rlen[cur].p;
+  I.V.nb = h->nb;
+  I.V.oldpos = M.oldpos;
+  BuildArgs A{(const uint8_t*)h->key[nxt].p, 32, (const uint8_t*)h->val[nxt].p, noff, m2, nullptr, 1, 0, 0, false};
+  A.presorted = true;
+  A.inc = &I;
+  BuildOut O;
+  kh_stats bst{};
+  run_build(c, A, O, &bst);
+  float merge_ms = ev_ms(c->ev[6], c->ev[7]);
+  if (stats) {
+    *stats = bst;
+    stats->n_inputs = nops;
+    stats->t_sort_ms = merge_ms;  // batch sort + merge
+    stats->t_total_ms += merge_ms;
+  }
+  h->cur = nxt;
+  h->m = m2;
+  h->P = I.P;
+  h->nb = I.nb;
+  copy_root(O, 0, h->root);
 }
 
 // ---------------------------------------------------------------------------
@@ -1402,6 +1783,55 @@ int kh_dev_synth_accounts(kh_ctx* c, uint32_t cfg, uint64_t first, uint64_t n, u
                        d_vals);
     LAUNCH_CHECK();
     HIPCHK(hipStreamSynchronize(st));
+  })
+}
+
+int kh_trie_open(kh_ctx* c, const uint8_t* d_keys, uint32_t klen, const uint8_t* d_vals, const uint64_t* d_voff,
+                 uint64_t n, uint32_t flags, uint8_t root32[32], kh_trie** out) {
+  if (!c || !out) return set_err(KH_EINVAL, "null context or handle");
+  kh_trie* h = nullptr;
+  API_TRY({
+    HIPCHK(hipSetDevice(c->dev));
+    h = new kh_trie();
+    h->c = c;
+    try {
+      trie_open(h, d_keys, klen, d_vals, d_voff, n, flags, nullptr);
+    } catch (...) {
+      kh_trie_free(h);
+      h = nullptr;
+      throw;
+    }
+    if (root32) memcpy(root32, h->root, 32);
+    *out = h;
+  })
+}
+
+int kh_trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals, const uint64_t* d_up_voff,
+                  uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
+                  uint8_t root32[32], kh_stats* stats) {
+  if (!h) return set_err(KH_EINVAL, "null handle");
+  API_TRY({
+    HIPCHK(hipSetDevice(h->c->dev));
+    trie_apply(h, d_up_keys, d_up_vals, d_up_voff, nup, d_del_keys, ndel, klen, flags, stats);
+    if (root32) memcpy(root32, h->root, 32);
+  })
+}
+
+int kh_trie_size(const kh_trie* h, uint64_t* n) {
+  if (!h || !n) return set_err(KH_EINVAL, "null handle");
+  *n = h->m;
+  return KH_OK;
+}
+
+int kh_trie_free(kh_trie* h) {
+  if (!h) return KH_OK;
+  API_TRY({
+    (void)hipSetDevice(h->c->dev);
+    (void)hipStreamSynchronize(h->c->st);
+    for (int q = 0; q < 2; ++q)
+      for (DevBuf* b : {&h->key[q], &h->val[q], &h->off[q], &h->ref[q], &h->rlen[q]}) b->release();
+    for (DevBuf* b : {&h->u, &h->pyr, &h->bid, &h->mws}) b->release();
+    delete h;
   })
 }
 

@@ -196,6 +196,10 @@ struct Topo {
                            //   bmsg[BR_WORDS * lb[d] + q * cnt_d + t]  (transposed per level)
   uint64_t* xmsg;          // extension messages, same scheme with EXT_WORDS
   const uint32_t* lb;      // [65] first order position of each depth (lb[64] = B)
+  // incremental commit (resident.h; all nullable)
+  uint8_t* br_dirty;   // [B] 1: re-encode and re-hash; 0: reference from the previous version
+  uint64_t* br_ref;    // [B*4] capped reference of each branch node (saved for the next commit)
+  uint32_t* br_rlen;   // [B] its encoding length
   // per-result outputs
   uint64_t* res_hash;  // [nres*4]
   uint32_t* res_len;   // [nres]
@@ -437,7 +441,7 @@ KH_HD void leaf_value(const Topo& T, uint64_t i, const uint8_t** p, uint64_t* le
 
 // gather the value span of sorted key i (random reads once, sequential reads after)
 KH_HD void op_val_gather(const Topo& T, uint64_t i) {
-  uint32_t src = T.sidx[i];
+  uint32_t src = T.sidx ? T.sidx[i] : (uint32_t)i;  // presorted input: identity
   uint64_t o = T.voff[src];
   T.svoff[i] = o;
   T.svlen[i] = (uint32_t)(T.voff[src + 1] - o);
@@ -602,6 +606,11 @@ KH_HD void kec256_strided(const uint64_t* w, uint64_t stride, uint32_t len, uint
 }
 
 // ---- leaf hash (thread per leaf).  Returns permutations spent.
+// incremental commit: a node under a clean branch is neither hashed nor published
+KH_HD bool under_clean(const Topo& T, uint32_t parent) {
+  return T.br_dirty && parent != NONE && !T.br_dirty[parent];
+}
+
 // hash + publish of leaf i whose encoding (L bytes) sits at w, words `stride` apart
 KH_HD uint32_t leaf_hash_at(const Topo& T, uint64_t i, const uint64_t* w, uint64_t stride, uint32_t L,
                             uint32_t* inl) {
@@ -633,6 +642,8 @@ KH_HD uint32_t leaf_hash_at(const Topo& T, uint64_t i, const uint64_t* w, uint64
 }
 
 KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
+  *inl = 0;
+  if (under_clean(T, T.lf_parent[i])) return 0;
   uint32_t L = T.lf_len[i];
   if (L <= LEAF_SHORT_MAX) return leaf_hash_at(T, i, T.lmsg + i, T.lstride, L, inl);
   return leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, L, inl);
@@ -641,6 +652,7 @@ KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
 // ---- branch prep: [ref_0 .. ref_15, ""] into its message slot (thread per branch of
 // one level; g = its position in the level order)
 KH_HD void op_branch_prep(const Topo& T, uint32_t j, uint64_t g) {
+  if (T.br_dirty && !T.br_dirty[j]) return;  // clean: reference from the previous version
   uint32_t k = T.br_k[j];
   uint64_t cb = T.br_cbase[j];
   const uint16_t* cm = T.cmeta + cb;
@@ -671,20 +683,38 @@ KH_HD void op_branch_prep(const Topo& T, uint32_t j, uint64_t g) {
 
 // ---- branch hash (+ extension encode + hash) (thread per branch of one level)
 KH_HD uint32_t op_branch_hash(const Topo& T, uint32_t j, uint64_t g, uint32_t* inl) {
-  uint32_t L = T.br_len[j];
   uint32_t ext = T.br_ext[j];
   uint32_t parent = T.br_parent[j];
   uint64_t first = T.br_first[j];
   uint32_t d = T.br_depth[j];
   int32_t pd = (int32_t)d - (int32_t)ext - 1;
   bool top = parent == NONE;
-  Slot sl = branch_slot(T, g, d, false);
+  *inl = 0;
   uint64_t hb[4], bhead[4];
-  uint32_t perms = hash_slot(sl, L, top && ext == 0, hb);
-  slot_head(sl, L, bhead);
-  uint32_t ninl = (L < 32 && !(top && ext == 0)) ? 1 : 0;
-  if (T.br_hash)
-    for (int q = 0; q < 4; ++q) T.br_hash[4 * j + q] = hb[q];
+  uint32_t L, perms = 0, ninl = 0;
+  if (T.br_dirty && !T.br_dirty[j]) {
+    // clean: the node is unchanged; only its reference (and extension) is needed,
+    // and only by a dirty parent
+    if (under_clean(T, parent)) return 0;
+    L = T.br_rlen[j];
+    for (int q = 0; q < 4; ++q) bhead[q] = hb[q] = T.br_ref[4 * j + q];
+  } else {
+    L = T.br_len[j];
+    Slot sl = branch_slot(T, g, d, false);
+    perms = hash_slot(sl, L, top && ext == 0, hb);
+    slot_head(sl, L, bhead);
+    ninl = (L < 32 && !(top && ext == 0)) ? 1 : 0;
+    if (T.br_hash)
+      for (int q = 0; q < 4; ++q) T.br_hash[4 * j + q] = hb[q];
+    if (T.br_ref) {  // capped reference, for the next incremental commit
+      for (int q = 0; q < 4; ++q) {
+        uint32_t base = 8u * (uint32_t)q;
+        T.br_ref[4 * j + q] =
+            L >= 32 ? hb[q] : (base < L ? bhead[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0);
+      }
+      T.br_rlen[j] = L;
+    }
+  }
   Key4 key = load_key(T.skey, first);
   uint32_t nib = top ? 0 : key_nibble(key, pd);
   if (ext == 0) {

@@ -83,3 +83,83 @@ def fold_root16(hash32x16, len16, inline32x16):
     out = np.zeros(32, np.uint8)
     check(lib().kh_fold_root16(hh.ctypes.data, ll.ctypes.data, ii.ctypes.data, out.ctypes.data))
     return out.tobytes()
+
+
+def _pack_dev(items, device):
+    """bytes list -> (uint8 data, int64 offsets[n+1]) tensors on the device."""
+    import torch
+    blob = b"".join(items)
+    data = torch.zeros(len(blob) + 64, dtype=torch.uint8)
+    if blob:
+        data[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+    off = torch.tensor(np.concatenate([[0], np.cumsum([len(x) for x in items], dtype=np.int64)]).astype(np.int64))
+    return data.to(device), off.to(device)
+
+
+class ResidentTrie:
+    """A trie kept in HBM between commits (kh_trie_open / kh_trie_apply).
+
+    commit(upserts, deletes) folds a block's dirty set the way TrieAccounts.flush /
+    TrieStorage.flush fold their logs into MerklePatriciaTrie.put / remove
+    (TrieAccounts.scala:22-28, TrieStorage.scala:43-60), re-hashing only the changed
+    paths.  Keys are 32-byte trie keys, or raw (address / slot) bytes with hash_keys.
+    """
+
+    def __init__(self, ctx, keys=(), vals=(), hash_keys=False):
+        self.ctx = ctx
+        self.dev = f"cuda:{ctx.device}"
+        self.h = None
+        klen = len(keys[0]) if keys else 32
+        kd, _ = _pack_dev(list(keys), self.dev)
+        vd, vo = _pack_dev(list(vals), self.dev)
+        self._open(kd, klen, vd, vo, len(keys), hash_keys)
+
+    def _open(self, kd, klen, vd, vo, n, hash_keys):
+        h = ctypes.c_void_p()
+        root = np.zeros(32, np.uint8)
+        flags = _lib.KH_HASH_KEYS if hash_keys else 0
+        self.ctx._sync()
+        check(lib().kh_trie_open(self.ctx.h, _ptr(kd), klen, _ptr(vd), _ptr(vo), n, flags, root.ctypes.data,
+                                 ctypes.byref(h)))
+        self.h = h
+        self.root = root.tobytes()
+
+    def commit(self, upserts=(), deletes=(), hash_keys=False, stats=None):
+        """Apply {key: value} upserts, then deletes; returns the new root."""
+        ups = list(upserts.items()) if isinstance(upserts, dict) else list(upserts)
+        dels = list(deletes)
+        klen = len(ups[0][0]) if ups else (len(dels[0]) if dels else 32)
+        uk, _ = _pack_dev([k for k, _ in ups], self.dev)
+        uv, uo = _pack_dev([v for _, v in ups], self.dev)
+        dk, _ = _pack_dev(dels, self.dev)
+        return self.commit_dev(uk, uv, uo, len(ups), dk, len(dels), klen, hash_keys, stats)
+
+    def commit_dev(self, up_keys, up_vals, up_voff, nup, del_keys, ndel, klen=32, hash_keys=False, stats=None):
+        root = np.zeros(32, np.uint8)
+        st = stats if stats is not None else KhStats()
+        flags = _lib.KH_HASH_KEYS if hash_keys else 0
+        self.ctx._sync()
+        check(lib().kh_trie_apply(self.h, _ptr(up_keys), _ptr(up_vals), _ptr(up_voff), nup, _ptr(del_keys), ndel,
+                                  klen, flags, root.ctypes.data, ctypes.byref(st)))
+        self.root = root.tobytes()
+        return self.root
+
+    @property
+    def root_hash(self):
+        return self.root
+
+    def __len__(self):
+        n = ctypes.c_uint64()
+        check(lib().kh_trie_size(self.h, ctypes.byref(n)))
+        return int(n.value)
+
+    def close(self):
+        if self.h:
+            lib().kh_trie_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -99,3 +99,83 @@ def segmented_case(seed=5, nseg=40):
     if tries[5][0] and tries[6][0]:
         tries[6][0][0] = tries[5][0][0]
     return tries
+
+
+def commit_scenarios(seed=21):
+    """Resident-trie commit sequences: (name, init_keys, init_vals, batches),
+    batch = (upserts [(key, value)], deletes [key]).  The expected root after each batch
+    is the oracle trie after put(upserts...) then remove(deletes...) in order."""
+    r = random.Random(seed)
+    out = []
+
+    def acct():
+        return account_value(r)
+
+    # accounts: updates, inserts, deletes (incl. absent keys), mixed, delete + re-insert
+    ks = [_rk(r) for _ in range(2000)]
+    vs = [acct() for _ in ks]
+    live = list(ks)
+    b = []
+    b.append(([(k, acct()) for k in r.sample(live, 50)], []))
+    new = [_rk(r) for _ in range(30)]
+    b.append(([(k, acct()) for k in new], []))
+    live += new
+    gone = r.sample(live, 30)
+    b.append(([], gone + [_rk(r) for _ in range(5)]))
+    live = [k for k in live if k not in set(gone)]
+    mix_up = [(k, acct()) for k in r.sample(live, 40)] + [(_rk(r), acct()) for _ in range(40)]
+    mix_del = r.sample(live, 20)
+    b.append((mix_up, mix_del))
+    b.append(([(gone[0], acct()), (gone[1], acct())], []))  # re-insert deleted keys
+    b.append(([(live[5], vs[0])], []))                      # one update
+    out.append(("accounts", ks, vs, b))
+
+    # storage tries: 1-byte values -> inline leaves / inline branches; deletes collapse
+    ks = [_rk(r) for _ in range(300)]
+    vs = [storage_value(r) for _ in ks]
+    b = [([(k, storage_value(r)) for k in r.sample(ks, 20)], r.sample(ks, 40)),
+         ([(_rk(r), b"\x01") for _ in range(30)], []),
+         ([], r.sample(ks, 100))]
+    out.append(("storage", ks, vs, b))
+
+    # deep keys: long shared prefixes (extensions), deletes that merge extensions
+    ks = deep_keys(r, 120)
+    vs = [codec.storage_value_rlp(i + 1) for i in range(len(ks))]
+    b = [([], ks[:60:2]), ([(k, b"\x05") for k in deep_keys(r, 10, base=ks[0])], ks[1:20:3]),
+         ([], ks[60:110])]
+    out.append(("deep", ks, vs, b))
+
+    # to empty and back; from empty; single key
+    ks = [_rk(r) for _ in range(40)]
+    vs = [acct() for _ in ks]
+    out.append(("to_empty", ks, vs, [([], ks[:20]), ([], ks[20:]), ([(ks[3], acct())], []), ([(k, acct()) for k in ks[:10]], [])]))
+    out.append(("from_empty", [], [], [([(k, acct()) for k in ks[:1]], []), ([(k, acct()) for k in ks[1:2]], []),
+                                       ([(k, acct()) for k in ks[2:30]], []), ([], ks[:29])]))
+    k1, k2 = _rk(r), _rk(r)
+    out.append(("single", [k1], [acct()], [([(k1, acct())], []), ([(k2, acct())], []), ([], [k1]), ([], [k2])]))
+    # the same key twice in one batch: later upsert wins; upsert + delete -> deleted
+    ks = [_rk(r) for _ in range(100)]
+    vs = [acct() for _ in ks]
+    out.append(("same_key_batch", ks, vs, [([(ks[0], acct()), (ks[0], acct())], []), ([(ks[1], acct())], [ks[1]]),
+                                          ([(ks[1], acct()), (ks[2], acct())], [ks[2], ks[2]])]))
+    # a large batch relative to the trie
+    ks = [_rk(r) for _ in range(2000)]
+    vs = [acct() for _ in ks]
+    out.append(("large_batch", ks, vs, [([(k, acct()) for k in r.sample(ks, 700)] + [(_rk(r), acct()) for _ in range(300)],
+                                         r.sample(ks, 500))]))
+    return out
+
+
+def oracle_commits(oracle, init_keys, init_vals, batches):
+    """Expected roots: the oracle trie folded put-by-put, remove-by-remove."""
+    t = oracle.Trie()
+    for k, v in zip(init_keys, init_vals):
+        t.put(k, v)
+    roots = [t.root_hash()]
+    for ups, dels in batches:
+        for k, v in ups:
+            t.put(k, v)
+        for k in dels:
+            t.remove(k)
+        roots.append(t.root_hash())
+    return roots

@@ -1,0 +1,83 @@
+"""GPU parity of the resident trie's incremental commit (kh_trie_open / kh_trie_apply,
+SURVEY §8 f1) against the oracle trie folded put-by-put / remove-by-remove, and at
+1M accounts against a from-scratch device build of the same final set."""
+import random
+
+import numpy as np
+import pytest
+
+from tests import cases as C
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("sc", C.commit_scenarios(), ids=lambda s: s[0])
+def test_commits_vs_oracle(khst, oracle, sc):
+    from khipu_amd.device import Ctx, ResidentTrie
+    name, ks, vs, batches = sc
+    want = C.oracle_commits(oracle, ks, vs, batches)
+    t = ResidentTrie(Ctx(0), ks, vs)
+    assert t.root == want[0], name
+    for i, (ups, dels) in enumerate(batches):
+        assert t.commit(ups, dels) == want[i + 1], (name, i)
+    t.close()
+
+
+def test_commit_hash_keys(khst, oracle):
+    """Addresses hashed on the device (KH_HASH_KEYS), as TrieAccounts keys them."""
+    from khipu_amd.device import Ctx, ResidentTrie
+    r = random.Random(8)
+    addrs = [bytes(r.getrandbits(8) for _ in range(20)) for _ in range(500)]
+    vals = [C.account_value(r) for _ in addrs]
+    t = ResidentTrie(Ctx(0), addrs, vals, hash_keys=True)
+    ups = [(a, C.account_value(r)) for a in r.sample(addrs, 40)] + [
+        (bytes(r.getrandbits(8) for _ in range(20)), C.account_value(r)) for _ in range(10)]
+    dels = r.sample(addrs, 15)
+    got = t.commit(ups, dels, hash_keys=True)
+    hk = [oracle.kec256(a) for a in addrs]
+    want = C.oracle_commits(oracle, hk, vals, [([(oracle.kec256(a), v) for a, v in ups],
+                                                [oracle.kec256(a) for a in dels])])
+    assert t.root_hash == got
+    assert got == want[1]
+
+
+def test_commit_1m_vs_full_build(khst):
+    """configs[2]-style commit at 1M accounts: 20k dirty (90% updates, 5% inserts, 5%
+    deletes) -> the root of a from-scratch build of the final set; only the changed
+    paths are re-hashed."""
+    import torch
+    from khipu_amd.device import Ctx, ResidentTrie, _pack_dev
+    ctx = Ctx(0)
+    n = 1_000_000
+    addr, vals, voff = ctx.synth_accounts(3, 0, n)
+    keys = torch.empty(n * 32 + 64, dtype=torch.uint8, device="cuda:0")
+    from khipu_amd._lib import check, lib
+    from khipu_amd.device import _ptr
+    torch.cuda.synchronize()
+    check(lib().kh_dev_hash_keys(ctx.h, _ptr(addr), 20, n, _ptr(keys)))
+    torch.cuda.synchronize()
+    t = ResidentTrie.__new__(ResidentTrie)
+    t.ctx, t.dev, t.h = ctx, "cuda:0", None
+    t._open(keys, 32, vals, voff, n, False)
+    r = random.Random(3)
+    kh = keys[:32 * n].cpu().numpy().reshape(n, 32)
+    vo = voff.cpu().numpy()
+    vb = vals.cpu().numpy()
+    state = {kh[i].tobytes(): vb[vo[i]:vo[i + 1]].tobytes() for i in range(n)}
+    idx = r.sample(range(n), 19_000)
+    ups = [(kh[i].tobytes(), C.account_value(r)) for i in idx[:18_000]]
+    ups += [(bytes(r.getrandbits(8) for _ in range(32)), C.account_value(r)) for _ in range(1_000)]
+    dels = [kh[i].tobytes() for i in idx[18_000:]]
+    st = khst.KhStats()
+    got = t.commit(ups, dels, stats=st)
+    for k, v in ups:
+        state[k] = v
+    for k in dels:
+        state.pop(k, None)
+    fk = list(state.keys())
+    kd, _ = _pack_dev(fk, "cuda:0")
+    vd, od = _pack_dev([state[k] for k in fk], "cuda:0")
+    hh, _, _, full = ctx.build(kd, 32, vd, od, len(fk))
+    assert got == hh[0].tobytes()
+    assert st.n_node_hashes < full.n_node_hashes // 5, (st.n_node_hashes, full.n_node_hashes)
+    t.close()
