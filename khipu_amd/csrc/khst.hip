@@ -253,7 +253,8 @@ __global__ void __launch_bounds__(BS) k_branch_topo(Topo T, Pyr P, uint64_t nb) 
 
 __global__ void __launch_bounds__(BS) k_leaf_topo(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i < T.m) op_leaf_topo(T, i);
+  if (i < T.m)
+    op_leaf_topo(T, i, [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); });
 }
 
 // Level order without contended global atomics: branch ids bucketed by
@@ -270,26 +271,26 @@ __device__ __forceinline__ uint32_t branch_bucket(const Topo& T, uint64_t j) {
   uint32_t blocks = perms_for_len(rlp_hdr_len(payload) + payload);  // 1..4
   return (uint32_t)T.br_depth[j] * 8 + (T.br_ext[j] ? 4 : 0) + (4 - blocks);
 }
+constexpr uint32_t LV_TILE = BS * 16;  // branch ids per block: few blocks -> a short [bucket][block] table
 __global__ void __launch_bounds__(BS) k_level_count(Topo T, const uint32_t* Bp, uint32_t* bcnt, uint32_t nblk) {
   __shared__ uint32_t h[NBUCKET];
   for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) h[q] = 0;
   __syncthreads();
-  uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (j < *Bp) atomicAdd(&h[branch_bucket(T, j)], 1u);
+  const uint64_t B = *Bp, j0 = (uint64_t)blockIdx.x * LV_TILE;
+  for (uint64_t j = j0 + threadIdx.x; j < j0 + LV_TILE && j < B; j += BS) atomicAdd(&h[branch_bucket(T, j)], 1u);
   __syncthreads();
   for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) bcnt[(uint64_t)q * nblk + blockIdx.x] = h[q];
 }
 
 __global__ void __launch_bounds__(BS) k_level_scatter(Topo T, const uint32_t* Bp, const uint32_t* bbase,
                                                       uint32_t nblk, uint32_t* order) {
-  __shared__ uint32_t cnt[NBUCKET];
-  for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) cnt[q] = 0;
+  __shared__ uint32_t base[NBUCKET];
+  for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) base[q] = bbase[(uint64_t)q * nblk + blockIdx.x];
   __syncthreads();
-  uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (j < *Bp) {
-    uint32_t q = branch_bucket(T, j);
-    uint32_t r = atomicAdd(&cnt[q], 1u);
-    order[bbase[(uint64_t)q * nblk + blockIdx.x] + r] = (uint32_t)j;
+  const uint64_t B = *Bp, j0 = (uint64_t)blockIdx.x * LV_TILE;
+  for (uint64_t j = j0 + threadIdx.x; j < j0 + LV_TILE && j < B; j += BS) {
+    uint32_t r = atomicAdd(&base[branch_bucket(T, j)], 1u);
+    order[r] = (uint32_t)j;
   }
 }
 
@@ -894,7 +895,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       n * 4, n, n, n * 8, n * 4, n * 8, n * 4,  // leaves, svoff, svlen
       A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
       nres * 32, nres * 4, nres * 32,         // results
-      CTR_N * 8, 64 * 4, 80 * 4, 512 * ((nb1 + BS - 1) / BS) * 4, nb1 * 4,  // ctr hist lb bcnt order
+      CTR_N * 8, 64 * 4, 80 * 4, 512 * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
   };
   c->ws1.ensure(carve_size(sz));
   Carver cv{(char*)c->ws1.p, 0, c->ws1.cap};
@@ -942,7 +943,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.ctr = cv.take<unsigned long long>(CTR_N);
   T.depth_hist = cv.take<uint32_t>(64);
   uint32_t* lb = cv.take<uint32_t>(80);
-  const uint32_t nblk_max = (uint32_t)((nb1 + BS - 1) / BS);
+  const uint32_t nblk_max = (uint32_t)((nb1 + LV_TILE - 1) / LV_TILE);
   uint32_t* bcnt = cv.take<uint32_t>((uint64_t)NBUCKET * nblk_max);
   uint32_t* order = cv.take<uint32_t>(nb1);
   T.depth0 = A.depth0;
@@ -1023,7 +1024,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     hipLaunchKernelGGL(k_branch_topo, GRID(nb, BS), dim3(BS), 0, st, T, P, nb);
     LAUNCH_CHECK();
     // level order (grids sized by nb; threads past B exit)
-    const uint32_t nblk = (uint32_t)((nb + BS - 1) / BS);
+    const uint32_t nblk = (uint32_t)((nb + LV_TILE - 1) / LV_TILE);
     hipLaunchKernelGGL(k_level_count, dim3(nblk), dim3(BS), 0, st, T, (const uint32_t*)Bp, bcnt, nblk);
     LAUNCH_CHECK();
     scan_exclusive<uint32_t>(bcnt, bcnt, (uint64_t)NBUCKET * nblk, (uint32_t*)nullptr, scan_scratch, st);
@@ -1038,7 +1039,6 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   }
   hipLaunchKernelGGL(k_leaf_topo, GRID(m, BS), dim3(BS), 0, st, T);
   LAUNCH_CHECK();
-  scan_exclusive<uint64_t>(T.lf_aoff, T.lf_aoff, m, (uint64_t*)(ctr + CTR_LFBYTES), scan_scratch, st);
   // one host sync for every size the second workspace needs
   HIPCHK(hipMemcpyAsync(c->h_pinned, ctr + CTR_B, 8 * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_pinned + 4, ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
@@ -1416,6 +1416,8 @@ static void trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up
   HIPCHK(hipStreamSynchronize(st));
   const uint64_t n_ins = (uint32_t)c->h_pinned[0], n_del = (uint32_t)c->h_pinned[1], nd = (uint32_t)c->h_pinned[2];
   const uint64_t m2 = m + n_ins - n_del;
+  if (n_ins > nsorted || n_del > m || nd > nsorted || m2 > mx)
+    throw KhError{KH_EINTERNAL, "merge: inconsistent batch counts"};
   if (stats) {
     stats->n_inputs = nops;
     stats->n_leaves = m2;
@@ -1434,7 +1436,13 @@ static void trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up
     scan_exclusive<uint64_t>(len64, noff, m2, (uint64_t*)(tot + 3), S.scan_scratch, st);
     HIPCHK(hipMemcpyAsync(noff + m2, tot + 3, 8, hipMemcpyDeviceToDevice, st));
     HIPCHK(hipMemcpyAsync(c->h_pinned, tot + 3, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned + 1, M.roff + m, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned + 2, d_up_voff ? d_up_voff + nup : M.roff, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (c->h_pinned[0] > c->h_pinned[1] + (nup ? c->h_pinned[2] : 0))
+      throw KhError{KH_EINTERNAL, "merge: value bytes exceed resident + upserts (" + std::to_string(c->h_pinned[0]) +
+                                      " > " + std::to_string(c->h_pinned[1]) + " + " +
+                                      std::to_string(nup ? c->h_pinned[2] : 0) + ")"};
     h->val[nxt].ensure(c->h_pinned[0] + 64);
     hipLaunchKernelGGL(k_merge_vals, GRID(m2, BS), dim3(BS), 0, st, (const uint64_t*)M.nsrc, (const uint32_t*)M.nlen,
                        (const uint64_t*)noff, m2, (const uint8_t*)h->val[cur].p, d_up_vals,

@@ -456,7 +456,10 @@ KH_HD uint64_t leaf_enc_len(uint32_t s, uint64_t vlen, uint32_t v0) {
   return rlp_hdr_len(payload) + payload;
 }
 
-KH_HD void op_leaf_topo(const Topo& T, uint64_t i) {
+// alloc(bytes) -> offset in the long-leaf region (device: an atomic bump on
+// CTR_LFBYTES; long leaves are rare, so there is no contention)
+template <typename AllocFn>
+KH_HD void op_leaf_topo(const Topo& T, uint64_t i, AllocFn alloc) {
   int64_t a = (int64_t)i - 1, c = (i + 1 < T.m) ? (int64_t)i : -1;
   Parent P = resolve_parent(T, a, c);
   T.lf_parent[i] = P.bid;
@@ -467,7 +470,7 @@ KH_HD void op_leaf_topo(const Topo& T, uint64_t i) {
   leaf_value(T, i, &vp, &vlen);
   uint32_t v0 = vlen == 1 ? (uint32_t)*vp : 0;  // the first byte matters only for a 1-byte value
   uint64_t L = leaf_enc_len((uint32_t)(P.pd + 1), vlen, v0);
-  T.lf_aoff[i] = L > LEAF_SHORT_MAX ? (L + 7) & ~(uint64_t)7 : 0;
+  T.lf_aoff[i] = L > LEAF_SHORT_MAX ? alloc((L + 7) & ~(uint64_t)7) : 0;
 }
 
 // ---- node hashing is split in two kernels per node set:

@@ -169,17 +169,16 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       }
     }
   }
-  for (uint64_t i = 0; i < m; ++i) op_leaf_topo(T, i);
+  uint64_t lfb = 0;
+  for (uint64_t i = 0; i < m; ++i) op_leaf_topo(T, i, [&](uint64_t b) {
+      uint64_t o = lfb;
+      lfb += b;
+      return o;
+    });
   uint64_t C = 0;
   for (uint64_t j = 0; j < B; ++j) {
     br_cbase[j] = (uint32_t)C;
     C += br_k[j];
-  }
-  uint64_t lfb = 0;
-  for (uint64_t i = 0; i < m; ++i) {
-    uint64_t a = lf_aoff[i];
-    lf_aoff[i] = lfb;
-    lfb += a;
   }
   std::vector<uint64_t> cref(4 * C + 4), arena((lfb + 64) / 8 + 1), lmsg(LEAF_WORDS * m + 1),
       bmsg(BR_WORDS * B + 1), xmsg(EXT_WORDS * B + 1);
