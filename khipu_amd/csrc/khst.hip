@@ -45,9 +45,11 @@ struct KhError {
 #define HIPCHK(x)                                                                                  \
   do {                                                                                             \
     hipError_t e_ = (x);                                                                           \
-    if (e_ != hipSuccess)                                                                          \
+    if (e_ != hipSuccess) {                                                                        \
+      (void)hipGetLastError(); /* clear it, or the next launch check reports it again */           \
       throw KhError{e_ == hipErrorOutOfMemory ? KH_ENOMEM : KH_EDEVICE,                            \
                     std::string(#x) + ": " + hipGetErrorString(e_)};                               \
+    }                                                                                              \
   } while (0)
 #define LAUNCH_CHECK() HIPCHK(hipGetLastError())
 
@@ -1124,7 +1126,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     I.nb = nb;
     I.P = Pyr{};
     if (nb > 0) {
-      uint64_t pyr_bytes = (uint64_t)(P.lv[P.nl - 1] - pyr) + P.sz[P.nl - 1];
+      // levels >= 1 live in `pyr` (level 0 is T.u); a one-level pyramid has none
+      uint64_t pyr_bytes = P.nl > 1 ? (uint64_t)(P.lv[P.nl - 1] - pyr) + P.sz[P.nl - 1] : 0;
       I.u->ensure(nb + 64);
       I.bid->ensure(nb * 4 + 64);
       I.pyr->ensure(pyr_bytes + 64);

@@ -75,7 +75,11 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
                     (!segmented || seg[order[i]] == seg[order[i + 1]]);
     if (!dup_next) sidx.push_back(order[i]);
   }
-  if (presorted && sidx.size() != n) return -1;  // presorted input must be unique
+  if (presorted) {  // the merged set must already be sorted and unique (the device does not sort it)
+    if (sidx.size() != n) return -1;
+    for (uint64_t i = 0; i < n; ++i)
+      if (sidx[i] != i) return -2;
+  }
   const uint64_t m = sidx.size(), nb = m - 1;
   std::vector<uint64_t> skey(4 * m);
   std::vector<uint32_t> sseg(m);
