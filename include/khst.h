@@ -147,6 +147,26 @@ int kh_dev_partition(kh_ctx* ctx, const uint8_t* d_keys32, const uint8_t* d_vals
                      uint64_t n, uint32_t nparts, uint8_t* d_out_keys, uint8_t* d_out_vals, uint64_t* d_out_vlen,
                      uint64_t* h_counts, uint64_t* h_bytes);
 
+/* ---- fast-sync NodeData verification ----
+ * NodeDatasRequest.processResponse (sync/package.scala:81-125) over a batch of peer
+ * values: kec256 each value (data packed, off[n+1]), match it against the nreq
+ * requested hashes (req32, req_kind[r]: 0 state trie node, 1 storage root, 2 contract
+ * storage node, 3 EVM code; a duplicate hash takes the last request's kind), and
+ * decode a matched trie node with PV63's MptNode rules (PV63.scala:96-127) to list the
+ * children still to fetch: getStateNodeChildren / getContractMptNodeChildren
+ * (sync/package.scala:127-165) — branch / extension child hashes, and for a state
+ * leaf the account's codeHash (kind 3) then stateRoot (kind 1) unless empty.
+ * Per value i (host buffers; any output may be NULL):
+ *   hash32[32i..)          kec256(value)
+ *   match[i]               matched request index, -1 if none (then nothing is decoded)
+ *   status[i]              0 ok, 1 not a trie node ("Cannot decode NodeData"),
+ *                          2 bad child ("unexpected value in node"), 3 bad account
+ *                          ("Cannot decode Account"), 4 malformed RLP
+ *   nchild[i], child32[512i..), child_kind[16i..)   children in the reference's order */
+int kh_verify_nodes(const uint8_t* data, const uint64_t* off, uint64_t n, const uint8_t* req32, const uint8_t* req_kind,
+                    uint64_t nreq, uint8_t* hash32, int64_t* match, uint8_t* status, uint8_t* nchild, uint8_t* child32,
+                    uint8_t* child_kind);
+
 /* ---- resident trie: incremental commit ----
  * A trie kept in HBM between commits: its sorted (key, value) set and the capped
  * reference of every branch node.  Replaces the per-key fold of TrieAccounts.flush /

@@ -25,6 +25,7 @@ EXPORTS = (
     "kh_trie_roots_segmented", "kh_trie_root_nodes", "kh_ctx_create", "kh_ctx_destroy", "kh_ctx_set_stream",
     "kh_dev_kec256_batch", "kh_dev_trie_build", "kh_fold_root16", "kh_dev_synth_accounts", "kh_dev_hash_keys",
     "kh_dev_partition", "kh_trie_open", "kh_trie_apply", "kh_trie_size", "kh_trie_free",
+    "kh_verify_nodes",
 )
 
 
@@ -102,6 +103,7 @@ def lib():
     L.kh_trie_apply.argtypes = [vp, vp, vp, vp, u64, vp, u64, u32, u32, vp, vp]
     L.kh_trie_size.argtypes = [vp, ctypes.POINTER(u64)]
     L.kh_trie_free.argtypes = [vp]
+    L.kh_verify_nodes.argtypes = [vp, vp, u64, vp, vp, u64, vp, vp, vp, vp, vp, vp]
     for name in EXPORTS:
         fn = getattr(L, name)
         if fn.restype is ctypes.c_int or name not in ("kh_last_error", "kh_version"):

@@ -27,6 +27,7 @@
 #include "synth.h"
 #include "trie_ops.h"
 #include "resident.h"
+#include "nodedata.h"
 
 using namespace khst;
 
@@ -67,6 +68,32 @@ __global__ void __launch_bounds__(BS) k_kec_batch(const uint8_t* data, const uin
   uint64_t o = off[i];
   kec256_msg<false>(data + o, (uint32_t)(off[i + 1] - o), h);
   for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
+}
+
+// fast-sync NodeData verification (nodedata.h): hash, match against the sorted
+// requested hashes (the last of equal requests wins, as Map construction does), decode
+__global__ void __launch_bounds__(BS) k_verify_nodes(const uint8_t* data, const uint64_t* off, uint64_t n,
+                                                     const uint64_t* req, const uint8_t* req_kind,
+                                                     const uint32_t* req_idx, uint64_t nreq, uint64_t* hash_out,
+                                                     int64_t* match, uint8_t* status, uint8_t* nchild,
+                                                     uint8_t* child32, uint8_t* child_kind) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t o = off[i];
+  const uint32_t len = (uint32_t)(off[i + 1] - o);
+  uint64_t h[4];
+  kec256_msg<false>(data + o, len, h);
+  for (int j = 0; j < 4; ++j) hash_out[4 * i + j] = h[j];
+  uint64_t p = key_lower_bound(req, nreq, h);
+  int64_t mi = -1;
+  uint8_t kind = NK_NONE;
+  if (p < nreq && key_cmp(req + 4 * p, h) == 0) {
+    while (p + 1 < nreq && key_cmp(req + 4 * (p + 1), h) == 0) ++p;
+    mi = req_idx[p];
+    kind = req_kind[p];
+  }
+  match[i] = mi;
+  status[i] = op_node_children(data + o, len, kind, child32 + 512 * i, child_kind + 16 * i, nchild + i);
 }
 
 __global__ void __launch_bounds__(BS) k_hash_keys(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out) {
@@ -1426,7 +1453,7 @@ static void trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up
     stats->n_leaves = m2;
   }
   if (nd == 0) return;  // nothing changes: same root
-  hipLaunchKernelGGL(k_place_resident, GRID(m, BS), dim3(BS), 0, st, M, (const uint32_t*)del_flag);
+  if (m) hipLaunchKernelGGL(k_place_resident, GRID(m, BS), dim3(BS), 0, st, M, (const uint32_t*)del_flag);
   hipLaunchKernelGGL(k_place_op, GRID(nsorted, BS), dim3(BS), 0, st, M, (const uint32_t*)o_insf,
                      (const uint32_t*)o_efff);
   LAUNCH_CHECK();
@@ -1793,6 +1820,65 @@ int kh_dev_synth_accounts(kh_ctx* c, uint32_t cfg, uint64_t first, uint64_t n, u
     hipLaunchKernelGGL(k_synth_write, GRID(n, BS), dim3(BS), 0, st, cfg, first, n, (const uint64_t*)d_voff, d_addr,
                        d_vals);
     LAUNCH_CHECK();
+    HIPCHK(hipStreamSynchronize(st));
+  })
+}
+
+int kh_verify_nodes(const uint8_t* data, const uint64_t* off, uint64_t n, const uint8_t* req32, const uint8_t* req_kind,
+                    uint64_t nreq, uint8_t* hash32, int64_t* match, uint8_t* status, uint8_t* nchild, uint8_t* child32,
+                    uint8_t* child_kind) {
+  API_TRY({
+    if (n == 0) return KH_OK;
+    if (!data || !off || (nreq && (!req32 || !req_kind))) throw KhError{KH_EINVAL, "null buffer"};
+    kh_ctx* c = shared_ctx(current_device());
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->dev));
+    hipStream_t st = c->st;
+    // requests sorted by hash on the host (stable: the last duplicate ends last)
+    std::vector<uint32_t> ord(nreq);
+    for (uint64_t r = 0; r < nreq; ++r) ord[r] = (uint32_t)r;
+    std::stable_sort(ord.begin(), ord.end(),
+                     [&](uint32_t a, uint32_t b) { return memcmp(req32 + 32ull * a, req32 + 32ull * b, 32) < 0; });
+    std::vector<uint8_t> rs(32 * nreq + 32), rk(nreq + 1);
+    for (uint64_t r = 0; r < nreq; ++r) {
+      memcpy(&rs[32 * r], req32 + 32ull * ord[r], 32);
+      rk[r] = req_kind[ord[r]];
+    }
+    uint64_t v0 = off[0], vbytes = off[n] - v0;
+    std::vector<uint64_t> rel(off, off + n + 1);
+    for (auto& x : rel) x -= v0;
+    c->in_vals.ensure(vbytes + 64);
+    c->in_voff.ensure((n + 1) * 8 + 64);
+    c->in_keys.ensure(carve_size({32 * nreq + 32, nreq + 1, 4 * nreq + 4}));
+    c->out_emit.ensure(carve_size({32 * n, 8 * n, n, n, 512 * n, 16 * n}));
+    Carver ci{(char*)c->in_keys.p, 0, c->in_keys.cap};
+    uint64_t* dreq = ci.take<uint64_t>(4 * nreq + 4);
+    uint8_t* dkind = ci.take<uint8_t>(nreq + 1);
+    uint32_t* didx = ci.take<uint32_t>(nreq + 1);
+    Carver co{(char*)c->out_emit.p, 0, c->out_emit.cap};
+    uint64_t* dh = co.take<uint64_t>(4 * n);
+    int64_t* dm = co.take<int64_t>(n);
+    uint8_t* ds = co.take<uint8_t>(n);
+    uint8_t* dn = co.take<uint8_t>(n);
+    uint8_t* dc = co.take<uint8_t>(512 * n);
+    uint8_t* dk = co.take<uint8_t>(16 * n);
+    if (vbytes) HIPCHK(hipMemcpyAsync(c->in_vals.p, data + v0, vbytes, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->in_voff.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    if (nreq) {
+      HIPCHK(hipMemcpyAsync(dreq, rs.data(), 32 * nreq, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(dkind, rk.data(), nreq, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(didx, ord.data(), 4 * nreq, hipMemcpyHostToDevice, st));
+    }
+    hipLaunchKernelGGL(k_verify_nodes, GRID(n, BS), dim3(BS), 0, st, (const uint8_t*)c->in_vals.p,
+                       (const uint64_t*)c->in_voff.p, n, (const uint64_t*)dreq, (const uint8_t*)dkind,
+                       (const uint32_t*)didx, nreq, dh, dm, ds, dn, dc, dk);
+    LAUNCH_CHECK();
+    if (hash32) HIPCHK(hipMemcpyAsync(hash32, dh, 32 * n, hipMemcpyDeviceToHost, st));
+    if (match) HIPCHK(hipMemcpyAsync(match, dm, 8 * n, hipMemcpyDeviceToHost, st));
+    if (status) HIPCHK(hipMemcpyAsync(status, ds, n, hipMemcpyDeviceToHost, st));
+    if (nchild) HIPCHK(hipMemcpyAsync(nchild, dn, n, hipMemcpyDeviceToHost, st));
+    if (child32) HIPCHK(hipMemcpyAsync(child32, dc, 512 * n, hipMemcpyDeviceToHost, st));
+    if (child_kind) HIPCHK(hipMemcpyAsync(child_kind, dk, 16 * n, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
   })
 }

@@ -745,6 +745,144 @@ struct or_trie {
   or_trie() : st(&own), mpt(&own, EMPTY_TRIE_HASH) {}
 };
 
+// ---------------------------------------------------------------------------
+// Fast-sync NodeData decode: PV63.MptNode decoding
+// (network/p2p/messages/PV63.scala:96-127) and the child-hash lists of
+// NodeDatasRequest (blockchain/sync/package.scala:127-165).  RLP items are decoded
+// strictly: a truncated item is an error here (the reference's copyOfRange would
+// zero-pad it), reported with the status codes of include/khst.h kh_verify_nodes.
+// ---------------------------------------------------------------------------
+struct NodeErr {
+  int status;
+};
+struct SItem {  // strictly decoded RLP item
+  bool isList = false;
+  Bytes bytes;
+  std::vector<SItem> items;
+};
+static SItem sdecode(const Bytes& d, size_t pos, size_t end, size_t* next) {
+  if (pos >= end) throw NodeErr{4};
+  const uint8_t* u = (const uint8_t*)d.data();
+  unsigned p = u[pos];
+  size_t off, len;
+  bool list;
+  if (p < 0x80) {
+    off = pos, len = 1, list = false;
+  } else if (p <= 0xb7) {
+    off = pos + 1, len = p - 0x80, list = false;
+  } else if (p <= 0xbf || p >= 0xf8) {
+    size_t ll = p <= 0xbf ? p - 0xb7 : p - 0xf7;
+    if (ll > 4 || pos + 1 + ll > end) throw NodeErr{4};
+    len = 0;
+    for (size_t i = 0; i < ll; ++i) len = (len << 8) | u[pos + 1 + i];
+    off = pos + 1 + ll, list = p >= 0xc0;
+  } else {
+    off = pos + 1, len = p - 0xc0, list = true;
+  }
+  if (off + len > end) throw NodeErr{4};
+  SItem it;
+  it.isList = list;
+  if (!list) {
+    it.bytes = d.substr(off, len);
+  } else {
+    size_t q = off;
+    while (q < off + len) {
+      size_t nx;
+      it.items.push_back(sdecode(d, q, off + len, &nx));
+      q = nx;
+    }
+  }
+  *next = off + len;
+  return it;
+}
+static Bytes sencode(const SItem& it) {  // rlp.encode (canonical)
+  if (!it.isList) return rlpStr(it.bytes);
+  Bytes pl;
+  for (auto& c : it.items) pl += sencode(c);
+  return rlpList(pl);
+}
+static void mptNodeCheck(const SItem& it);
+// decodeChild (PV63.scala:113-125): true = Left(MptHash), false = Right(node)
+static bool decodeChild(const SItem& c) {
+  if (!c.isList && (c.bytes.size() == 32 || c.bytes.empty())) return true;
+  size_t enc = sencode(c).size();
+  if (c.isList && (c.items.size() == 2 || c.items.size() == 17) && enc <= 31) {
+    mptNodeCheck(c);
+    return false;
+  }
+  throw NodeErr{2};
+}
+// toMptNode (PV63.scala:99-111), for its exceptions only
+static void mptNodeCheck(const SItem& it) {
+  if (it.isList && it.items.size() == 17) {
+    for (int i = 0; i < 16; ++i) decodeChild(it.items[i]);
+    if (it.items[16].isList) throw NodeErr{4};
+    return;
+  }
+  if (it.isList && it.items.size() == 2) {
+    if (it.items[0].isList || it.items[0].bytes.empty()) throw NodeErr{4};
+    bool leaf = (((uint8_t)it.items[0].bytes[0] >> 4) & 2) != 0;
+    if (leaf) {
+      if (it.items[1].isList) throw NodeErr{4};
+    } else {
+      decodeChild(it.items[1]);
+    }
+    return;
+  }
+  throw NodeErr{1};
+}
+// kind: 0 state node, 1 storage root, 2 contract storage node, 3 evm code
+static int nodeChildren(const Bytes& v, int kind, std::vector<std::pair<Bytes, int>>& out) {
+  if (kind == 3) return 0;
+  try {
+    size_t nx;
+    SItem it = sdecode(v, 0, v.size(), &nx);
+    const int ck = kind == 0 ? 0 : 2;  // StateMptNodeHash / ContractStorageMptNodeHash
+    if (it.isList && it.items.size() == 17) {  // MptBranch: Left hashes, nonEmpty
+      std::vector<std::pair<Bytes, int>> kids;
+      for (int i = 0; i < 16; ++i)
+        if (decodeChild(it.items[i]) && !it.items[i].bytes.empty()) kids.push_back({it.items[i].bytes, ck});
+      if (it.items[16].isList) throw NodeErr{4};
+      out = kids;
+      return 0;
+    }
+    if (it.isList && it.items.size() == 2) {
+      if (it.items[0].isList || it.items[0].bytes.empty()) throw NodeErr{4};
+      bool leaf = (((uint8_t)it.items[0].bytes[0] >> 4) & 2) != 0;
+      if (leaf) {
+        if (it.items[1].isList) throw NodeErr{4};
+        if (kind != 0) return 0;  // getContractMptNodeChildren: a leaf has none
+        // getAccount: rawDecode(value) = RLPList(nonce, balance, stateRoot, codeHash)
+        const Bytes& val = it.items[1].bytes;
+        SItem a;
+        try {
+          size_t n2;
+          a = sdecode(val, 0, val.size(), &n2);
+        } catch (NodeErr&) {
+          throw NodeErr{3};
+        }
+        if (!a.isList || a.items.size() != 4) throw NodeErr{3};
+        for (auto& f : a.items)
+          if (f.isList) throw NodeErr{3};
+        if (a.items[0].bytes.size() > 32 || a.items[1].bytes.size() > 32) throw NodeErr{3};  // DataWord
+        if (a.items[2].bytes.size() != 32 || a.items[3].bytes.size() != 32) throw NodeErr{3};
+        static const Bytes EMPTY_CODE = kec256(Bytes());
+        if (a.items[3].bytes != EMPTY_CODE) out.push_back({a.items[3].bytes, 3});       // EvmcodeHash
+        if (a.items[2].bytes != EMPTY_TRIE_HASH) out.push_back({a.items[2].bytes, 1});  // StorageRootHash
+        return 0;
+      }
+      // MptExtension: Left(hash) -> the hash; Right(node) -> none
+      if (decodeChild(it.items[1]) && !it.items[1].bytes.empty()) out.push_back({it.items[1].bytes, ck});
+      return 0;
+    }
+    if (!it.isList) throw NodeErr{1};
+    throw NodeErr{1};
+  } catch (NodeErr& e) {
+    out.clear();
+    return e.status;
+  }
+}
+
 static thread_local std::string g_err;
 
 extern "C" {
@@ -912,6 +1050,19 @@ int or_seq_root(const uint8_t* keys, uint64_t klen, const uint8_t* vals, const u
     g_err = e.what();
     return -1;
   }
+}
+
+// fast-sync decode of one value: status (kh_verify_nodes codes); children into
+// out32 (16 x 32 B) and kinds, count into *n
+int or_node_children(const uint8_t* v, uint64_t len, int kind, uint8_t* out32, uint8_t* kinds, uint32_t* n) {
+  std::vector<std::pair<Bytes, int>> ch;
+  int st = nodeChildren(Bytes((const char*)v, len), kind, ch);
+  *n = (uint32_t)ch.size();
+  for (size_t i = 0; i < ch.size() && i < 16; ++i) {
+    memcpy(out32 + 32 * i, ch[i].first.data(), 32);
+    kinds[i] = (uint8_t)ch[i].second;
+  }
+  return st;
 }
 
 }  // extern "C"

@@ -52,6 +52,9 @@ def lib():
         L.or_trie_reachable.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                         ctypes.c_uint64, ctypes.c_void_p]
         L.or_trie_reachable.restype = ctypes.c_int64
+        L.or_node_children.argtypes = [u8p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p]
+        L.or_node_children.restype = ctypes.c_int
         L.or_seq_root.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
         _lib = L
@@ -204,3 +207,13 @@ def perm_count() -> int:
 
 def perm_reset():
     lib().or_perm_reset()
+
+
+def node_children(value: bytes, kind: int):
+    """PV63 decode + NodeDatasRequest child lists of one NodeData value
+    (blockchain/sync/package.scala:127-165): (status, [(hash32, kind), ...])."""
+    out = ctypes.create_string_buffer(512)
+    kinds = ctypes.create_string_buffer(16)
+    n = ctypes.c_uint32()
+    st = lib().or_node_children(value, len(value), kind, out, kinds, ctypes.byref(n))
+    return st, [(out.raw[32 * i:32 * i + 32], kinds.raw[i]) for i in range(n.value)]

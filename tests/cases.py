@@ -179,3 +179,45 @@ def oracle_commits(oracle, init_keys, init_vals, batches):
             t.remove(k)
         roots.append(t.root_hash())
     return roots
+
+
+def sync_node_sets(oracle, seed=31):
+    """Trie nodes as a fast-sync peer returns them: (name, kind,
+    {hash: encoding}) for a state trie with contract accounts and for storage tries
+    whose nodes embed inline (< 32 B) children."""
+    r = random.Random(seed)
+    out = []
+    t = oracle.Trie()
+    for i in range(300):
+        k = _rk(r)
+        if i % 3 == 0:  # contract: non-empty storage root and code hash
+            v = codec.account_rlp(r.randrange(100), r.randrange(10 ** 20), state_root=_rk(r), code_hash=_rk(r))
+        elif i % 7 == 0:
+            v = codec.account_rlp(0, 1, code_hash=_rk(r))
+        else:
+            v = account_value(r)
+        t.put(k, v)
+    out.append(("state", 0, t.reachable()))
+    for name, keys in (("storage_deep", deep_keys(r, 120)), ("storage", [_rk(r) for _ in range(200)])):
+        t = oracle.Trie()
+        for i, k in enumerate(keys):
+            t.put(k, codec.storage_value_rlp(r.choice([1, 5, 0x7f, 0x80, i + 1, r.randrange(1, 2 ** 64)])))
+        out.append((name, 2, t.reachable()))
+    return out
+
+
+def mutate(r, b):
+    """One random byte-level corruption of an encoding (truncate, flip, insert, delete)."""
+    b = bytearray(b)
+    op = r.randrange(5)
+    if op == 0 and len(b) > 1:
+        del b[r.randrange(1, len(b)):]
+    elif op == 1 and b:
+        b[r.randrange(len(b))] ^= 1 << r.randrange(8)
+    elif op == 2:
+        b.insert(r.randrange(len(b) + 1), r.randrange(256))
+    elif op == 3 and len(b) > 1:
+        del b[r.randrange(len(b))]
+    elif b:
+        b[r.randrange(min(len(b), 4))] = r.randrange(256)  # header bytes
+    return bytes(b)

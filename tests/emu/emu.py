@@ -25,6 +25,7 @@ def lib():
         L.emu_trie_open.restype = vp
         L.emu_trie_apply.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp, vp]
         L.emu_trie_free.argtypes = [vp]
+        L.emu_node_children.argtypes = [vp, ctypes.c_uint64, ctypes.c_int, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -105,3 +106,12 @@ class ResidentTrie:
         if getattr(self, "h", None):
             lib().emu_trie_free(self.h)
             self.h = None
+
+
+def node_children(value: bytes, kind: int):
+    out = np.zeros(512, np.uint8)
+    kinds = np.zeros(16, np.uint8)
+    n = np.zeros(1, np.uint32)
+    buf = _buf(value + b"\0" * 16)
+    st = lib().emu_node_children(buf.ctypes.data, len(value), kind, out.ctypes.data, kinds.ctypes.data, n.ctypes.data)
+    return st, [(out[32 * i:32 * i + 32].tobytes(), int(kinds[i])) for i in range(int(n[0]))]

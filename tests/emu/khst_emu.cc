@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "../../khipu_amd/csrc/nodedata.h"
 #include "../../khipu_amd/csrc/resident.h"
 #include "../../khipu_amd/csrc/synth.h"
 
@@ -440,6 +441,13 @@ int emu_trie_apply(void* handle, const uint8_t* up_keys, const uint8_t* up_vals,
 }
 
 void emu_trie_free(void* handle) { delete (EmuTrie*)handle; }
+
+int emu_node_children(const uint8_t* v, uint64_t len, int kind, uint8_t* out32, uint8_t* kinds, uint32_t* n) {
+  uint8_t nc = 0;
+  int st = op_node_children(v, (uint32_t)len, (uint8_t)kind, out32, kinds, &nc);
+  *n = nc;
+  return st;
+}
 
 void emu_kec256(const uint8_t* p, uint64_t len, uint8_t* out) {
   uint64_t h[4];
