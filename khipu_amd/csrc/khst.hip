@@ -397,7 +397,12 @@ __global__ void __launch_bounds__(BS) k_leaf_fused(Topo T) {
   __shared__ uint64_t msg[BS * LEAF_WORDS];
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u;
-  const bool valid = i < T.m && !under_clean(T, T.lf_parent[i]);
+  const int cstate = i < T.m ? leaf_cache_state(T, i) : 2;  // 0: encode + hash here
+  const bool valid = i < T.m && cstate == 0;
+  if (i < T.m && cstate && T.lf_oldpos) {
+    uint32_t in0;
+    leaf_reuse(T, i, cstate, &in0);
+  }
   uint64_t off = 0;
   uint32_t vlen = 0, v0 = 0;
   Key4 k{0, 0, 0, 0};
@@ -750,6 +755,9 @@ struct IncArgs {
   DevBuf* u = nullptr;     // [nb] boundary values
   DevBuf* pyr = nullptr;   // pyramid levels >= 1
   DevBuf* bid = nullptr;   // [nb] scanned rep flags
+  DevBuf* lref = nullptr;  // [m*4] leaf references
+  DevBuf* lrlen = nullptr; // [m]
+  DevBuf* lpd = nullptr;   // [m] leaf parent depths
   Pyr P{};                 // rebased onto *u / *pyr
   uint64_t nb = 0;
 };
@@ -1102,6 +1110,17 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     I.rlen->ensure(B * 4 + 64);
     T.br_ref = (uint64_t*)I.ref->p;
     T.br_rlen = (uint32_t*)I.rlen->p;
+    I.lref->ensure(m * 32 + 64);
+    I.lrlen->ensure(m * 4 + 64);
+    T.lf_ref = (uint64_t*)I.lref->p;
+    T.lf_rlen = (uint32_t*)I.lrlen->p;
+    if (inc_dirty) {  // leaves: reuse the previous reference of an unchanged leaf
+      T.lf_oldpos = I.V.oldpos;
+      T.lf_upd = I.V.upd;
+      T.lf_opd = I.V.lpd;
+      T.lf_oref = I.V.lref;
+      T.lf_orlen = I.V.lrlen;
+    }
     if (inc_dirty && B) {
       // dirty = prefix of a changed key; clean branches take the previous reference
       T.br_dirty = cv2.take<uint8_t>(B);
@@ -1150,6 +1169,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   if (c->h_pinned[CTR_ERR]) throw KhError{KH_EINTERNAL, "incremental commit: clean branch not found in the previous version"};
   if (A.inc) {  // keep this version's tables for the next commit
     IncArgs& I = *A.inc;
+    I.lpd->ensure(m + 64);
+    HIPCHK(hipMemcpyAsync(I.lpd->p, T.lf_pd, m, hipMemcpyDeviceToDevice, st));
     I.nb = nb;
     I.P = Pyr{};
     if (nb > 0) {
@@ -1281,8 +1302,8 @@ struct kh_trie {
   kh_ctx* c = nullptr;
   uint64_t m = 0;  // keys
   int cur = 0;     // current half of the double buffers
-  DevBuf key[2], val[2], off[2], ref[2], rlen[2];
-  DevBuf u, pyr, bid;  // the current version's topology tables
+  DevBuf key[2], val[2], off[2], ref[2], rlen[2], lref[2], lrlen[2];
+  DevBuf u, pyr, bid, lpd;  // the current version's topology tables
   Pyr P{};
   uint64_t nb = 0;
   DevBuf mws;  // merge scratch
@@ -1324,6 +1345,9 @@ static IncArgs inc_out(kh_trie* h, int half) {
   IncArgs I;
   I.ref = &h->ref[half];
   I.rlen = &h->rlen[half];
+  I.lref = &h->lref[half];
+  I.lrlen = &h->lrlen[half];
+  I.lpd = &h->lpd;
   I.u = &h->u;
   I.pyr = &h->pyr;
   I.bid = &h->bid;
@@ -1367,7 +1391,7 @@ static void trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up
       scan_scratch_bytes(mx + 1, 8), CTR_N * 8,    // scan scratch, counters
       nops * 4, nops, nops * 4, nops * 4, nops * 4, nops * 4,  // o_lb o_kind o_insf o_ins o_efff o_eff
       (m + 1) * 4, (m + 1) * 4, (m + 1) * 4, (m + 1) * 4, m * 4 + 4,  // pos_cnt pos_ins del_flag pos_del pos_upd
-      mx * 4, mx * 8, mx * 4, mx * 8, nops * 32,   // nlen nsrc oldpos len64 dkey
+      mx * 4, mx * 8, mx * 4, mx * 8, nops * 32, mx,  // nlen nsrc oldpos len64 dkey nupd
   };
   h->mws.ensure(carve_size(sz));
   Carver cv{(char*)h->mws.p, 0, h->mws.cap};
@@ -1400,6 +1424,7 @@ static void trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up
   M.oldpos = cv.take<uint32_t>(mx);
   uint64_t* len64 = cv.take<uint64_t>(mx);
   M.dkey = cv.take<uint64_t>(nops * 4);
+  M.nupd = cv.take<uint8_t>(mx);
   HIPCHK(hipMemsetAsync(S.ctr, 0, CTR_N * 8, st));
   HIPCHK(hipEventRecord(c->ev[6], st));
 
@@ -1493,6 +1518,10 @@ static void trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up
   I.V.rlen = (const uint32_t*)h->rlen[cur].p;
   I.V.nb = h->nb;
   I.V.oldpos = M.oldpos;
+  I.V.upd = M.nupd;
+  I.V.lpd = (const int8_t*)h->lpd.p;
+  I.V.lref = (const uint64_t*)h->lref[cur].p;
+  I.V.lrlen = (const uint32_t*)h->lrlen[cur].p;
   BuildArgs A{(const uint8_t*)h->key[nxt].p, 32, (const uint8_t*)h->val[nxt].p, noff, m2, nullptr, 1, 0, 0, false};
   A.presorted = true;
   A.inc = &I;
@@ -1926,8 +1955,9 @@ int kh_trie_free(kh_trie* h) {
     (void)hipSetDevice(h->c->dev);
     (void)hipStreamSynchronize(h->c->st);
     for (int q = 0; q < 2; ++q)
-      for (DevBuf* b : {&h->key[q], &h->val[q], &h->off[q], &h->ref[q], &h->rlen[q]}) b->release();
-    for (DevBuf* b : {&h->u, &h->pyr, &h->bid, &h->mws}) b->release();
+      for (DevBuf* b : {&h->key[q], &h->val[q], &h->off[q], &h->ref[q], &h->rlen[q], &h->lref[q], &h->lrlen[q]})
+        b->release();
+    for (DevBuf* b : {&h->u, &h->pyr, &h->bid, &h->lpd, &h->mws}) b->release();
     delete h;
   })
 }

@@ -13,8 +13,9 @@
 //      prefix of some changed key (updated, inserted or deleted) — exactly the
 //      nodes the reference's put/remove paths touch.  A clean branch covers the same
 //      key set as before, so its reference is looked up in the previous version's
-//      tables (by its first key and depth) instead of being recomputed; leaves are
-//      hashed only when their parent is dirty.
+//      tables (by its first key and depth) instead of being recomputed.  A leaf is
+//      re-encoded only if it was inserted or upserted or its path changed (parent
+//      depth); otherwise its previous reference is carried over.
 // Per-element ops (KH_HD): the HIP kernels and the host replay share them.
 #pragma once
 #include "trie_ops.h"
@@ -70,6 +71,7 @@ struct Merge {
   uint32_t* nlen;    // [m'] value length
   uint64_t* nsrc;    // [m'] value source offset; bit 63: the upsert buffer
   uint32_t* oldpos;  // [m'] resident position of the key, NONE if inserted
+  uint8_t* nupd;     // [m'] 1 if the value comes from the batch (updated or inserted)
   uint64_t* dkey;    // [ndirty*4] changed keys, sorted
 };
 
@@ -117,6 +119,7 @@ KH_HD void op_place_resident(const Merge& M, const uint32_t* del_flag, uint64_t 
     M.nlen[np] = (uint32_t)(M.roff[j + 1] - M.roff[j]);
   }
   M.oldpos[np] = (uint32_t)j;
+  M.nupd[np] = u != NONE ? 1 : 0;
 }
 
 // 3b. place inserted op o (o_ins scanned to the insert rank) and record the dirty
@@ -134,6 +137,7 @@ KH_HD void op_place_op(const Merge& M, const uint32_t* ins_flag, const uint32_t*
   M.nsrc[np] = SRC_UPSERT | M.uoff[src];
   M.nlen[np] = (uint32_t)(M.uoff[src + 1] - M.uoff[src]);
   M.oldpos[np] = NONE;
+  M.nupd[np] = 1;
 }
 
 // ---- dirty marking and clean-branch lookup (after the topology of the merged set)
@@ -146,6 +150,10 @@ struct Prev {
   const uint32_t* rlen;   // [B] its encoding length
   uint64_t nb;            // boundaries (m - 1)
   const uint32_t* oldpos; // merged position -> previous position
+  const uint8_t* upd;     // merged position -> value upserted
+  const int8_t* lpd;      // previous leaves' parent depths
+  const uint64_t* lref;   // previous leaves' capped references
+  const uint32_t* lrlen;
 };
 
 // branch j is dirty iff some changed key starts with its d-nibble prefix

@@ -200,6 +200,14 @@ struct Topo {
   uint8_t* br_dirty;   // [B] 1: re-encode and re-hash; 0: reference from the previous version
   uint64_t* br_ref;    // [B*4] capped reference of each branch node (saved for the next commit)
   uint32_t* br_rlen;   // [B] its encoding length
+  uint64_t* lf_ref;    // [m*4] capped reference of each leaf (saved for the next commit)
+  uint32_t* lf_rlen;   // [m]
+  // the previous version, seen from the merged set (nullable)
+  const uint32_t* lf_oldpos;  // [m] previous position of leaf i, NONE if inserted
+  const uint8_t* lf_upd;      // [m] 1 if the value was upserted
+  const int8_t* lf_opd;       // previous parent depth per previous position
+  const uint64_t* lf_oref;    // previous leaf references
+  const uint32_t* lf_orlen;
   // per-result outputs
   uint64_t* res_hash;  // [nres*4]
   uint32_t* res_len;   // [nres]
@@ -614,6 +622,38 @@ KH_HD bool under_clean(const Topo& T, uint32_t parent) {
   return T.br_dirty && parent != NONE && !T.br_dirty[parent];
 }
 
+// Incremental commit, per leaf: 0 = encode and hash, 1 = unchanged under a dirty
+// parent (publish the previous reference), 2 = unchanged under a clean parent (keep
+// the previous reference).  A leaf is unchanged when it was neither inserted nor
+// upserted and its parent depth (hence its path) is the same.
+KH_HD int leaf_cache_state(const Topo& T, uint64_t i) {
+  if (!T.lf_oldpos) return under_clean(T, T.lf_parent[i]) ? 2 : 0;
+  if (T.lf_parent[i] == NONE) return 0;  // a lone leaf is the root: always hashed
+  uint32_t o = T.lf_oldpos[i];
+  if (o == NONE || T.lf_upd[i] || T.lf_opd[o] != T.lf_pd[i]) return 0;
+  return under_clean(T, T.lf_parent[i]) ? 2 : 1;
+}
+KH_HD uint32_t leaf_nibble(const Topo& T, uint64_t i) {
+  uint32_t pd = (uint32_t)T.lf_pd[i];
+  uint32_t b = (uint32_t)(T.skey[4 * i + (pd >> 4)] >> (8 * ((pd >> 1) & 7))) & 0xFF;
+  return (pd & 1) ? (b & 0xF) : (b >> 4);
+}
+// states 1 and 2: carry the previous reference over (and publish it for state 1)
+KH_HD void leaf_reuse(const Topo& T, uint64_t i, int state, uint32_t* inl) {
+  uint32_t o = T.lf_oldpos[i];
+  uint64_t r[4];
+  for (int q = 0; q < 4; ++q) r[q] = T.lf_oref[4ull * o + q];
+  uint32_t L = T.lf_orlen[o];
+  if (T.lf_ref) {
+    for (int q = 0; q < 4; ++q) T.lf_ref[4 * i + q] = r[q];
+    T.lf_rlen[i] = L;
+  }
+  *inl = 0;
+  if (state != 1) return;
+  uint32_t parent = T.lf_parent[i];
+  publish_ref(T, parent, T.lf_pord[i], leaf_nibble(T, i), i, r, L, r);
+}
+
 // hash + publish of leaf i whose encoding (L bytes) sits at w, words `stride` apart
 KH_HD uint32_t leaf_hash_at(const Topo& T, uint64_t i, const uint64_t* w, uint64_t stride, uint32_t L,
                             uint32_t* inl) {
@@ -633,12 +673,15 @@ KH_HD uint32_t leaf_hash_at(const Topo& T, uint64_t i, const uint64_t* w, uint64
   }
   if (T.lf_hash)
     for (int j = 0; j < 4; ++j) T.lf_hash[4 * i + j] = hh[j];
-  uint32_t nib = 0;
-  if (!top) {
-    uint32_t pd = (uint32_t)T.lf_pd[i];
-    uint32_t b = (uint32_t)(T.skey[4 * i + (pd >> 4)] >> (8 * ((pd >> 1) & 7))) & 0xFF;
-    nib = (pd & 1) ? (b & 0xF) : (b >> 4);
+  if (T.lf_ref) {  // capped reference, for the next incremental commit
+    for (int q = 0; q < 4; ++q) {
+      uint32_t base = 8u * (uint32_t)q;
+      T.lf_ref[4 * i + q] =
+          L >= 32 ? hh[q] : (base < L ? head[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0);
+    }
+    T.lf_rlen[i] = L;
   }
+  uint32_t nib = top ? 0 : leaf_nibble(T, i);
   publish_ref(T, parent, T.lf_pord[i], nib, i, head, L, hh);
   *inl = (L < 32 && !top) ? 1 : 0;
   return perms;
@@ -646,7 +689,11 @@ KH_HD uint32_t leaf_hash_at(const Topo& T, uint64_t i, const uint64_t* w, uint64
 
 KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
   *inl = 0;
-  if (under_clean(T, T.lf_parent[i])) return 0;
+  int cs = leaf_cache_state(T, i);
+  if (cs) {
+    if (T.lf_oldpos) leaf_reuse(T, i, cs, inl);
+    return 0;
+  }
   uint32_t L = T.lf_len[i];
   if (L <= LEAF_SHORT_MAX) return leaf_hash_at(T, i, T.lmsg + i, T.lstride, L, inl);
   return leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, L, inl);

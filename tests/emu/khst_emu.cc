@@ -21,8 +21,9 @@ using namespace khst;
 
 // host mirror of IncArgs (khst.hip): the resident trie's tables
 struct EmuTables {
-  std::vector<uint64_t> ref;
-  std::vector<uint32_t> rlen;
+  std::vector<uint64_t> ref, lref;
+  std::vector<uint32_t> rlen, lrlen;
+  std::vector<int8_t> lpd;
   std::vector<uint8_t> u;
   std::vector<std::vector<uint8_t>> pyr;
   std::vector<uint32_t> bid;
@@ -206,7 +207,16 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
     inc->out->rlen.assign(B + 1, 0);
     T.br_ref = inc->out->ref.data();
     T.br_rlen = inc->out->rlen.data();
+    inc->out->lref.assign(4 * m + 4, 0);
+    inc->out->lrlen.assign(m + 1, 0);
+    T.lf_ref = inc->out->lref.data();
+    T.lf_rlen = inc->out->lrlen.data();
     if (inc->dkey) {
+      T.lf_oldpos = inc->V.oldpos;
+      T.lf_upd = inc->V.upd;
+      T.lf_opd = inc->V.lpd;
+      T.lf_oref = inc->V.lref;
+      T.lf_orlen = inc->V.lrlen;
       T.br_dirty = br_dirty.data();
       for (uint64_t j = 0; j < B; ++j) op_br_dirty(T, inc->dkey, inc->nd, (uint32_t)j);
       for (uint64_t j = 0; j < B; ++j) op_br_clean(T, inc->V, (uint32_t)j);
@@ -246,6 +256,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
     o.u.assign(u.begin(), u.begin() + nb);
     o.bid.assign(isrep.begin(), isrep.begin() + nb);
     o.pyr = pyr;
+    o.lpd.assign(lf_pd.begin(), lf_pd.end());
   }
   if (skey_out) *skey_out = skey;
   if (svoff_out) *svoff_out = svoff;
@@ -389,10 +400,12 @@ int emu_trie_apply(void* handle, const uint8_t* up_keys, const uint8_t* up_vals,
   }
   std::vector<uint64_t> nkey(4 * m2 + 4), nsrc(m2 + 1), dkey(4 * nd + 4);
   std::vector<uint32_t> nlen(m2 + 1), oldpos(m2 + 1);
+  std::vector<uint8_t> nupd(m2 + 1);
   M.nkey = nkey.data();
   M.nlen = nlen.data();
   M.nsrc = nsrc.data();
   M.oldpos = oldpos.data();
+  M.nupd = nupd.data();
   M.dkey = dkey.data();
   for (uint64_t j = 0; j < m; ++j) op_place_resident(M, del_flag.data(), j);
   for (uint64_t o = 0; o < ns; ++o) op_place_op(M, o_insf.data(), o_efff.data(), o);
@@ -417,6 +430,10 @@ int emu_trie_apply(void* handle, const uint8_t* up_keys, const uint8_t* up_vals,
   I.V.rlen = t->tab.rlen.data();
   I.V.nb = t->tab.nb;
   I.V.oldpos = oldpos.data();
+  I.V.upd = nupd.data();
+  I.V.lpd = t->tab.lpd.data();
+  I.V.lref = t->tab.lref.data();
+  I.V.lrlen = t->tab.lrlen.data();
   I.out = &tab;
   uint8_t hh[32], inl[32];
   uint32_t len = 0;

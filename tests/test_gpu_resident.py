@@ -79,5 +79,6 @@ def test_commit_1m_vs_full_build(khst):
     vd, od = _pack_dev([state[k] for k in fk], "cuda:0")
     hh, _, _, full = ctx.build(kd, 32, vd, od, len(fk))
     assert got == hh[0].tobytes()
-    assert st.n_node_hashes < full.n_node_hashes // 5, (st.n_node_hashes, full.n_node_hashes)
+    # ~19k changed leaves + the ~23k branches on their paths, not the 1.36M of a full build
+    assert st.n_node_hashes < full.n_node_hashes // 20, (st.n_node_hashes, full.n_node_hashes)
     t.close()
