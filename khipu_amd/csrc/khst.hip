@@ -483,12 +483,7 @@ __global__ void __launch_bounds__(BS) k_branch_hash(Topo T, const uint32_t* orde
     uint32_t j = order[first + t];
     uint32_t in1 = 0;
     perms = op_branch_hash(T, j, first + t, &in1);
-    // hashes: the branch if its encoding is >= 32 B or it is the top; its extension likewise
-    uint32_t L = T.br_len[j];
-    bool top = T.br_parent[j] == NONE;
-    bool ext = T.br_ext[j] != 0;
-    hashes = (L >= 32 || (top && !ext)) ? 1 : 0;
-    if (ext) hashes += (T.ex_len[j] >= 32 || top) ? 1 : 0;
+    hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
   }
   block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);

@@ -807,6 +807,17 @@ KH_HD uint32_t op_branch_hash(const Topo& T, uint32_t j, uint64_t g, uint32_t* i
   return perms;
 }
 
+// node hashes op_branch_hash(T, j, ...) spent `perms` on: the branch if it was
+// re-encoded and its encoding is >= 32 B or it is the top; its extension likewise
+// (an extension is re-encoded only when perms were spent on it or its branch)
+KH_HD uint32_t branch_hash_count(const Topo& T, uint32_t j, uint32_t perms) {
+  const bool top = T.br_parent[j] == NONE, ext = T.br_ext[j] != 0;
+  const bool hashed_branch = !T.br_dirty || T.br_dirty[j];
+  uint32_t h = (hashed_branch && (T.br_len[j] >= 32 || (top && !ext))) ? 1 : 0;
+  if (ext && perms) h += (T.ex_len[j] >= 32 || top) ? 1 : 0;
+  return h;
+}
+
 // Root branch over 16 capped references (the host fold of the sharded path).
 // refs: 16 x 4 words, lens: 0 = empty, 32 = hash, else inline length.
 // Writes the encoding into out (>= 600 B, 8-aligned); returns its length.

@@ -243,10 +243,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       uint32_t in1 = 0;
       uint32_t p = op_branch_hash(T, j, g, &in1);
       perms += p;
-      bool top = br_parent[j] == NONE, ext = br_ext[j] != 0;
-      bool hashed_branch = !T.br_dirty || T.br_dirty[j];
-      if (hashed_branch) hashes += (br_len[j] >= 32 || (top && !ext)) ? 1 : 0;
-      if (ext && p) hashes += (ex_len[j] >= 32 || top) ? 1 : 0;
+      hashes += branch_hash_count(T, j, p);
       inl += in1;
     }
   }
