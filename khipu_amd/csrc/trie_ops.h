@@ -208,6 +208,10 @@ struct Topo {
   const int8_t* lf_opd;       // previous parent depth per previous position
   const uint64_t* lf_oref;    // previous leaf references
   const uint32_t* lf_orlen;
+  // early leaves (plain root builds; nullable): capped reference and its length
+  // (32 = hash, EMETA_LONG = not hashed yet: longer than one Keccak block)
+  uint64_t* lf_eref;   // [m*4]
+  uint8_t* lf_emeta;   // [m]
   // per-result outputs
   uint64_t* res_hash;  // [nres*4]
   uint32_t* res_len;   // [nres]
@@ -218,7 +222,7 @@ struct Topo {
 };
 
 enum {
-  CTR_HASHES = 0, CTR_PERMS = 1, CTR_INLINE = 2, CTR_ARENA = 3, CTR_ERR = 4, CTR_EXT = 5,
+  CTR_HASHES = 0, CTR_PERMS = 1, CTR_INLINE = 2, CTR_ARENA = 3, CTR_ERR = 4, CTR_EXT = 5, CTR_LONGB = 6,
   // scratch slots for device-side totals read back by the host
   CTR_TIE = 8, CTR_M = 9, CTR_B = 10, CTR_BRBYTES = 11, CTR_LFBYTES = 12, CTR_C = 13, CTR_E0 = 14, CTR_E1 = 15,
   CTR_N = 16
@@ -697,6 +701,14 @@ KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
   uint32_t L = T.lf_len[i];
   if (L <= LEAF_SHORT_MAX) return leaf_hash_at(T, i, T.lmsg + i, T.lstride, L, inl);
   return leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, L, inl);
+}
+
+// ---- early leaves: parent depth from the two adjacent boundaries (= resolve_parent's pd)
+constexpr uint8_t EMETA_LONG = 0xFF;
+KH_HD int32_t leaf_pd_early(const Topo& T, uint64_t i) {
+  uint32_t va = i > 0 ? T.u[i - 1] : 0, vc = i + 1 < T.m ? T.u[i] : 0;
+  uint32_t v = va > vc ? va : vc;
+  return v == 0 ? (int32_t)T.depth0 - 1 : (int32_t)v - 1;
 }
 
 // ---- branch prep: [ref_0 .. ref_15, ""] into its message slot (thread per branch of

@@ -1,13 +1,18 @@
 #!/bin/bash
-# PMC passes (each counter group in its own run, --kernel-trace only; MI355X_MICROARCH.md §rocprofv3).
+# PMC passes over one bench step (1 warmup + 1 timed build), one rocprofv3 run per
+# counter group (rocprofv3 does not split counters over passes; FETCH_SIZE uses 3 TCC
+# slots and WRITE_SIZE 2, so they take separate passes).  Summarise with
+#   python scripts/pmc_summary.py <tag> [--json profiles/<tag>_pmc_traffic.json]
+# Every pass has its own time limit; the first failing pass ends the script.
 export TMPDIR=/tmp
 TAG=${1:-pmc}
-N=${PMC_ACCOUNTS:-10000000}
-rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
-i=0
-for PMC in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES" "GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY"; do
-  i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $PMC --kernel-trace --output-format csv -d gpurun_out/${TAG}_p$i -o pmc -- python bench.py --accounts $N --steps 1 --warmup 1 --no-cpu > gpurun_out/${TAG}_p$i.log 2>&1
-  rc=$?; echo "PMC pass $i ($PMC) rc=$rc"
-  if [ $rc -ne 0 ]; then tail -5 gpurun_out/${TAG}_p$i.log; exit $rc; fi
-done
+N=${PMC_ACCOUNTS:-100000000}
+run() {
+  local p=$1; shift
+  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d gpurun_out/${TAG}_$p -o pmc \
+    -- python3 bench.py --accounts $N --steps 1 --warmup 1 --no-cpu > gpurun_out/${TAG}_$p.log 2>&1
+  local rc=$?; echo "PMC_${p}_RC=$rc"; [ $rc -eq 0 ] || exit $rc
+}
+run p1 FETCH_SIZE
+run p2 WRITE_SIZE
+run p3 SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_WAVES

@@ -1,26 +1,57 @@
-"""Summarise rocprofv3 PMC passes (scripts/gpu_pmc.sh output) per kernel, per call."""
+"""Summarise the rocprofv3 PMC passes of scripts/gpu_pmc.sh per kernel.
+
+usage: python scripts/pmc_summary.py <tag> [builds] [--json out.json]
+
+Counters are summed over every dispatch of a kernel and divided by the number of
+builds the profiled command ran (bench.py --steps 1 --warmup 1 -> 2 builds), so each
+row is per build; `calls` is dispatches per build.  HBM bytes follow
+MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts 64 B per fabric read request and
+reports half the bytes of a wide coalesced read, so the corrected read bytes are
+2 x FETCH_SIZE(kB) x 1e3; WRITE_SIZE is taken as is.
+"""
 import collections
 import csv
 import glob
+import json
 import sys
 
-tag = sys.argv[1] if len(sys.argv) > 1 else "pmc6"
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+tag = args[0] if args else "pmc"
+builds = int(args[1]) if len(args) > 1 else 2
+out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
+if out_json in args:
+    args.remove(out_json)
+
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
-for f in sorted(glob.glob(f"gpurun_out/{tag}_p*/pmc_counter_collection.csv")):
+for f in sorted(glob.glob(f"gpurun_out/{tag}_p*/**/pmc_counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         agg[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]] += float(r["Counter_Value"])
-tr = list(csv.DictReader(open(f"gpurun_out/{tag}_p3/pmc_kernel_trace.csv")))
 dur = collections.defaultdict(float)
 calls = collections.defaultdict(int)
 vg = {}
-for r in tr:
-    k = r["Kernel_Name"].split("(")[0]
-    dur[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-    calls[k] += 1
-    vg[k] = (r["VGPR_Count"], r["LDS_Block_Size"])
-ncall = 2  # warmup + 1 step
-print(f"{'kernel':24s} {'ms':>7s} {'FETCH MB':>9s} {'WRITE MB':>9s} {'VALU M':>8s} {'wait%':>5s}  vgpr/lds")
-for k in sorted(dur, key=lambda x: -dur[x])[:int(sys.argv[2]) if len(sys.argv) > 2 else 20]:
+for f in sorted(glob.glob(f"gpurun_out/{tag}_p1/**/pmc_kernel_trace.csv", recursive=True)):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].split("(")[0]
+        dur[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        calls[k] += 1
+        vg[k] = (r.get("VGPR_Count") or r.get("Arch_VGPR_Count"), r.get("LDS_Block_Size"))
+
+rows = {}
+print(f"{'kernel':26s} {'calls':>5s} {'ms':>8s} {'read MB':>9s} {'write MB':>9s} {'GB/s':>7s} {'VALU M':>8s} "
+      f"{'valu%':>5s} {'wait%':>5s}  vgpr/lds")
+for k in sorted(dur, key=lambda x: -dur[x]):
     a = agg[k]
-    print(f"{k[:24]:24s} {dur[k] / ncall:7.3f} {a['FETCH_SIZE'] / ncall / 1e3:9.1f} {a['WRITE_SIZE'] / ncall / 1e3:9.1f} "
-          f"{a['SQ_INSTS_VALU'] / ncall / 1e6:8.1f} {100 * a['SQ_WAIT_ANY'] / max(a['SQ_WAVE_CYCLES'], 1):5.0f}  {vg[k]}")
+    ms = dur[k] / builds
+    rd = 2 * a["FETCH_SIZE"] * 1e3 / builds
+    wr = a["WRITE_SIZE"] * 1e3 / builds
+    cyc = max(a["SQ_WAVE_CYCLES"], 1)
+    rows[k] = {"calls_per_build": calls[k] / builds, "ms_per_build": ms, "read_bytes": rd, "write_bytes": wr,
+               "hbm_bytes": rd + wr, "valu_insts": a["SQ_INSTS_VALU"] / builds,
+               "valu_active_frac": a["SQ_ACTIVE_INST_VALU"] / cyc, "wait_frac": a["SQ_WAIT_ANY"] / cyc}
+    print(f"{k[:26]:26s} {calls[k] / builds:5.0f} {ms:8.3f} {rd / 1e6:9.1f} {wr / 1e6:9.1f} "
+          f"{(rd + wr) / max(ms, 1e-9) / 1e6:7.0f} {a['SQ_INSTS_VALU'] / builds / 1e6:8.1f} "
+          f"{100 * a['SQ_ACTIVE_INST_VALU'] / cyc:5.0f} {100 * a['SQ_WAIT_ANY'] / cyc:5.0f}  {vg.get(k)}")
+if out_json:
+    with open(out_json, "w") as f:
+        json.dump({"tag": tag, "builds": builds, "hbm_correction": "read = 2 x FETCH_SIZE, write = WRITE_SIZE",
+                   "kernels": rows}, f, indent=1)
