@@ -393,13 +393,18 @@ __global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
 // funnel-shifted by the header length), 2) each lane writes its header bytes in
 // front (merging the shared word), Keccak's its slot and publishes the reference.
 // Leaves longer than one block take the arena path (k_leaf_prep's global writer).
+// EARLY (plain root builds, trie_ops.h "early leaves"): launched on the second
+// stream right after k_lcp; the parent depth comes from the two boundaries, the
+// reference is stashed for k_leaf_topo_early, and long leaves are only counted
+// (their arena bytes) for k_leaf_long.
+template <bool EARLY>
 __global__ void __launch_bounds__(BS) k_leaf_fused(Topo T) {
   __shared__ uint64_t msg[BS * LEAF_WORDS];
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u;
-  const int cstate = i < T.m ? leaf_cache_state(T, i) : 2;  // 0: encode + hash here
+  const int cstate = EARLY ? 0 : (i < T.m ? leaf_cache_state(T, i) : 2);  // 0: encode + hash here
   const bool valid = i < T.m && cstate == 0;
-  if (i < T.m && cstate && T.lf_oldpos) {
+  if (!EARLY && i < T.m && cstate && T.lf_oldpos) {
     uint32_t in0;
     leaf_reuse(T, i, cstate, &in0);
   }
@@ -411,7 +416,7 @@ __global__ void __launch_bounds__(BS) k_leaf_fused(Topo T) {
     off = T.svoff[i];
     vlen = T.svlen[i];
     k = load_key(T.skey, i);
-    pd = T.lf_pd[i];
+    pd = EARLY ? leaf_pd_early(T, i) : T.lf_pd[i];
     if (vlen == 1) v0 = T.vals[off];
   }
   LeafGeom g = leaf_geom(k, pd, vlen, v0);
@@ -450,7 +455,7 @@ __global__ void __launch_bounds__(BS) k_leaf_fused(Topo T) {
     }
   }
   __syncthreads();
-  unsigned long long perms = 0, hashes = 0, inl = 0;
+  unsigned long long perms = 0, hashes = 0, inl = 0, longb = 0;
   if (valid) {
     uint32_t in1 = 0;
     if (shortl) {
@@ -459,11 +464,40 @@ __global__ void __launch_bounds__(BS) k_leaf_fused(Topo T) {
       leaf_header(w, k, g, vlen);
       if (vlen) w.flush_or();
       else w.flush();
-      perms = leaf_hash_at(T, i, my, 1, g.L, &in1);
+      perms = EARLY ? leaf_hash_early(T, i, pd == (int32_t)T.depth0 - 1, my, 1, g.L, &in1)
+                    : leaf_hash_at(T, i, my, 1, g.L, &in1);
+    } else if (EARLY) {
+      T.lf_emeta[i] = EMETA_LONG;  // encoded + hashed by k_leaf_long into its arena slot
+      longb = (g.L + 7) & ~7u;
     } else {
       op_leaf_prep(T, i, T.vals + off, vlen);  // arena
       perms = leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, g.L, &in1);
     }
+    hashes = perms ? 1 : 0;
+    inl = in1;
+  }
+  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
+  if (EARLY) {
+    __syncthreads();  // block_add3's LDS slots are reused
+    block_add3(&T.ctr[CTR_LONGB], longb, nullptr, 0, nullptr, 0);
+  }
+}
+
+// after the branch topology (plain root builds): stashed leaf references into the
+// parents' child records, arena slots for long leaves
+__global__ void __launch_bounds__(BS) k_leaf_topo_early(Topo T) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < T.m)
+    op_leaf_topo_early(T, i,
+                       [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); });
+}
+
+__global__ void __launch_bounds__(BS) k_leaf_long(Topo T) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  unsigned long long perms = 0, hashes = 0, inl = 0;
+  if (i < T.m) {
+    uint32_t in1 = 0;
+    perms = op_leaf_long(T, i, &in1);
     hashes = perms ? 1 : 0;
     inl = in1;
   }
@@ -710,9 +744,10 @@ struct kh_ctx {
   int dev = 0;
   hipStream_t own = nullptr;
   hipStream_t st = nullptr;
+  hipStream_t st2 = nullptr;  // leaf hashing, concurrent with the branch topology
   std::mutex mu;
   DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, out_emit;
-  hipEvent_t ev[8] = {};
+  hipEvent_t ev[11] = {};  // [8] boundaries ready (st), [9] / [10] leaf kernel start / end (st2)
   unsigned long long* h_pinned = nullptr;  // small pinned staging for syncs
   // last build (for emission)
   Topo T{};
@@ -902,6 +937,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   if (A.klen == 0 || A.klen > 4096) throw KhError{KH_EINVAL, "bad key length"};
   const uint32_t sb = segmented ? bits_for(A.nseg) : 0;
   if (sb > 32) throw KhError{KH_EINVAL, "too many segments"};
+  // plain root builds hash their leaves on c->st2 while c->st computes the branch
+  // topology (trie_ops.h "early leaves"); write-back and incremental builds keep
+  // the leaf stage after the topology (they need the parents / dirty marks first)
+  const bool early = !A.emit && !A.inc;
 
   O.res_hash.assign(nres * 4, 0);
   O.res_len.assign(nres, 0);
@@ -928,6 +967,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
       nres * 32, nres * 4, nres * 32,         // results
       CTR_N * 8, 64 * 4, 80 * 4, 512 * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
+      early ? n * 32 : 0, early ? n : 0,      // early leaves: stashed references, meta
   };
   c->ws1.ensure(carve_size(sz));
   Carver cv{(char*)c->ws1.p, 0, c->ws1.cap};
@@ -978,6 +1018,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   const uint32_t nblk_max = (uint32_t)((nb1 + LV_TILE - 1) / LV_TILE);
   uint32_t* bcnt = cv.take<uint32_t>((uint64_t)NBUCKET * nblk_max);
   uint32_t* order = cv.take<uint32_t>(nb1);
+  T.lf_eref = early ? cv.take<uint64_t>(n * 4) : nullptr;
+  T.lf_emeta = early ? cv.take<uint8_t>(n) : nullptr;
   T.depth0 = A.depth0;
   T.segmented = segmented ? 1 : 0;
   T.vals = A.vals;
@@ -1033,6 +1075,16 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   if (nb > 0) {
     hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
+  }
+  if (early) {  // leaves need only the boundaries: hash them beside the topology
+    HIPCHK(hipEventRecord(c->ev[8], st));
+    HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
+    HIPCHK(hipEventRecord(c->ev[9], c->st2));
+    hipLaunchKernelGGL(k_leaf_fused<true>, GRID(m, BS), dim3(BS), 0, c->st2, T);
+    LAUNCH_CHECK();
+    HIPCHK(hipEventRecord(c->ev[10], c->st2));
+  }
+  if (nb > 0) {
     P.lv[0] = T.u;
     P.sz[0] = nb;
     P.nl = 1;
@@ -1069,15 +1121,21 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     // child record bases
     scan_exclusive<uint32_t>(T.br_k, T.br_cbase, nb, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
   }
-  hipLaunchKernelGGL(k_leaf_topo, GRID(m, BS), dim3(BS), 0, st, T);
-  LAUNCH_CHECK();
+  if (early) {
+    HIPCHK(hipEventRecord(c->ev[3], st));      // topology done (the leaves may still run)
+    HIPCHK(hipStreamWaitEvent(st, c->ev[10], 0));  // ... and the leaves: their long-leaf bytes
+  } else {
+    hipLaunchKernelGGL(k_leaf_topo, GRID(m, BS), dim3(BS), 0, st, T);
+    LAUNCH_CHECK();
+  }
   // one host sync for every size the second workspace needs
+  HIPCHK(hipMemcpyAsync(c->h_pinned + 5, ctr + CTR_LONGB, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_pinned, ctr + CTR_B, 8 * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_pinned + 4, ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_pinned + 8, lb, 65 * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const uint64_t B = (uint32_t)c->h_pinned[0];
-  const uint64_t lf_bytes = c->h_pinned[2];
+  const uint64_t lf_bytes = early ? c->h_pinned[5] : c->h_pinned[2];
   const uint64_t C = (uint32_t)c->h_pinned[3];
   if (c->h_pinned[4]) throw KhError{KH_EINTERNAL, "topology invariant violated (group chain > 15)"};
   std::vector<uint32_t> lbh(65, 0);
@@ -1125,17 +1183,24 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       LAUNCH_CHECK();
     }
   }
-  HIPCHK(hipEventRecord(c->ev[3], st));
+  if (!early) HIPCHK(hipEventRecord(c->ev[3], st));
 
   // ---- 4. leaves: encode + hash in LDS (root only), or encode into message slots
   //         that the node-set emitter reads back, then hash
-  if (A.emit) {
+  if (early) {  // hashed already: publish into the child records; long leaves now
+    hipLaunchKernelGGL(k_leaf_topo_early, GRID(m, BS), dim3(BS), 0, st, T);
+    LAUNCH_CHECK();
+    if (lf_bytes) {
+      hipLaunchKernelGGL(k_leaf_long, GRID(m, BS), dim3(BS), 0, st, T);
+      LAUNCH_CHECK();
+    }
+  } else if (A.emit) {
     hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_leaf_hash, GRID(m, BS), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
   } else {
-    hipLaunchKernelGGL(k_leaf_fused, GRID(m, BS), dim3(BS), 0, st, T);
+    hipLaunchKernelGGL(k_leaf_fused<false>, GRID(m, BS), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
   }
   HIPCHK(hipEventRecord(c->ev[4], st));
@@ -1199,7 +1264,9 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     stats->t_keys_ms = ev_ms(c->ev[0], c->ev[1]);
     stats->t_sort_ms = ev_ms(c->ev[1], c->ev[2]);
     stats->t_topo_ms = ev_ms(c->ev[2], c->ev[3]);
-    stats->t_leaf_ms = ev_ms(c->ev[3], c->ev[4]);
+    // early: the leaf kernel's own span on st2, where it overlaps the topology (the
+    // publish of its references runs on st after both; t_total_ms holds it)
+    stats->t_leaf_ms = early ? ev_ms(c->ev[9], c->ev[10]) : ev_ms(c->ev[3], c->ev[4]);
     stats->t_branch_ms = ev_ms(c->ev[4], c->ev[5]);
     stats->t_total_ms = ev_ms(c->ev[0], c->ev[5]);
   }
@@ -1219,6 +1286,7 @@ static kh_ctx* ctx_new(int dev) {
   kh_ctx* c = new kh_ctx();
   c->dev = dev;
   HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
   c->st = c->own;
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipHostMalloc((void**)&c->h_pinned, 4096, hipHostMallocDefault));
@@ -1563,6 +1631,7 @@ int kh_ctx_destroy(kh_ctx* c) {
       if (e) (void)hipEventDestroy(e);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->own) (void)hipStreamDestroy(c->own);
+    if (c->st2) (void)hipStreamDestroy(c->st2);
     delete c;
   })
 }

@@ -710,6 +710,60 @@ KH_HD int32_t leaf_pd_early(const Topo& T, uint64_t i) {
   uint32_t v = va > vc ? va : vc;
   return v == 0 ? (int32_t)T.depth0 - 1 : (int32_t)v - 1;
 }
+// Plain root builds hash leaves right after op_lcp, on a second stream, while the
+// branch topology is computed; the reference is stashed per leaf and
+// op_leaf_topo_early moves it into the parent's child record.  A top leaf (both
+// boundaries 0) publishes its result here.  One-block leaf at w, L bytes:
+KH_HD uint32_t leaf_hash_early(const Topo& T, uint64_t i, bool top, const uint64_t* w, uint64_t stride, uint32_t L,
+                               uint32_t* inl) {
+  uint64_t hh[4] = {0, 0, 0, 0}, head[4];
+  uint32_t perms = 0;
+  if (L >= 32 || top) {
+    kec256_strided(w, stride, L, hh);
+    perms = 1;
+  }
+  for (int q = 0; q < 4; ++q) head[q] = (8u * q < L) ? w[q * stride] : 0;
+  *inl = 0;
+  if (top) {
+    publish_ref(T, NONE, 0, 0, i, head, L, hh);
+    return perms;
+  }
+  for (int q = 0; q < 4; ++q) {
+    uint32_t base = 8u * (uint32_t)q;
+    T.lf_eref[4 * i + q] = L >= 32 ? hh[q] : (base < L ? head[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0);
+  }
+  T.lf_emeta[i] = (uint8_t)(L >= 32 ? 32 : L);
+  *inl = L < 32 ? 1 : 0;
+  return perms;
+}
+// after the branch topology: the stashed reference goes to the parent's child
+// record; a long leaf gets its arena slot (as in op_leaf_topo) for op_leaf_long
+template <typename AllocFn>
+KH_HD void op_leaf_topo_early(const Topo& T, uint64_t i, AllocFn alloc) {
+  int64_t a = (int64_t)i - 1, c = (i + 1 < T.m) ? (int64_t)i : -1;
+  const uint8_t em = T.lf_emeta[i];
+  Parent P = resolve_parent(T, a, c);
+  if (em == EMETA_LONG) {
+    T.lf_parent[i] = P.bid;
+    T.lf_pord[i] = (uint8_t)P.pord;
+    T.lf_pd[i] = (int8_t)P.pd;
+    uint64_t L = leaf_enc_len((uint32_t)(P.pd + 1), T.svlen[i], 0);  // a long value has > 1 byte
+    T.lf_aoff[i] = alloc((L + 7) & ~(uint64_t)7);
+    return;
+  }
+  if (P.bid == NONE) return;  // a top leaf: its result is already published
+  Key4 k = load_key(T.skey, i);
+  uint64_t slot = (uint64_t)T.br_cbase[P.bid] + P.pord;
+  for (int q = 0; q < 4; ++q) T.cref[4 * slot + q] = T.lf_eref[4 * i + q];
+  T.cmeta[slot] = (uint16_t)(em | (key_nibble(k, P.pd) << 8));
+}
+// a long leaf (> one Keccak block): encode into its arena slot, hash, publish
+KH_HD uint32_t op_leaf_long(const Topo& T, uint64_t i, uint32_t* inl) {
+  *inl = 0;
+  if (T.lf_emeta[i] != EMETA_LONG) return 0;
+  op_leaf_prep(T, i, T.vals + T.svoff[i], T.svlen[i]);
+  return leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, T.lf_len[i], inl);
+}
 
 // ---- branch prep: [ref_0 .. ref_15, ""] into its message slot (thread per branch of
 // one level; g = its position in the level order)

@@ -175,19 +175,62 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       }
     }
   }
-  uint64_t lfb = 0;
-  for (uint64_t i = 0; i < m; ++i) op_leaf_topo(T, i, [&](uint64_t b) {
-      uint64_t o = lfb;
-      lfb += b;
-      return o;
-    });
+  // plain builds replay the device's early-leaf path (k_leaf_fused<true>: hashed from
+  // the boundaries alone, references stashed, published after the topology)
+  const bool early = inc == nullptr;
+  std::vector<uint64_t> eref(early ? 4 * m + 4 : 0);
+  std::vector<uint8_t> emeta(early ? m + 1 : 0);
+  uint64_t perms = 0, hashes = 0, inl = 0, longb = 0;
+  if (early) {
+    T.lf_eref = eref.data();
+    T.lf_emeta = emeta.data();
+    for (uint64_t i = 0; i < m; ++i) {
+      Key4 k = load_key(T.skey, i);
+      const uint8_t* vp = T.vals + T.svoff[i];
+      uint32_t vlen = T.svlen[i];
+      int32_t pd = leaf_pd_early(T, i);
+      LeafGeom g = leaf_geom(k, pd, vlen, vlen == 1 ? *vp : 0);
+      if (g.L > LEAF_SHORT_MAX) {
+        emeta[i] = EMETA_LONG;
+        longb += (g.L + 7) & ~7u;
+        continue;
+      }
+      uint64_t buf[LEAF_WORDS + 1] = {};
+      BW w(buf, 1);
+      leaf_header(w, k, g, vlen);
+      w.bytes(vp, vlen);
+      w.flush();
+      uint32_t in1 = 0;
+      uint32_t p = leaf_hash_early(T, i, pd == (int32_t)depth0 - 1, buf, 1, g.L, &in1);
+      perms += p;
+      hashes += p ? 1 : 0;
+      inl += in1;
+    }
+  }
   uint64_t C = 0;
   for (uint64_t j = 0; j < B; ++j) {
     br_cbase[j] = (uint32_t)C;
     C += br_k[j];
   }
-  std::vector<uint64_t> cref(4 * C + 4), arena((lfb + 64) / 8 + 1), lmsg(LEAF_WORDS * m + 1),
-      bmsg(BR_WORDS * B + 1), xmsg(EXT_WORDS * B + 1);
+  uint64_t lfb = 0;
+  std::vector<uint64_t> cref(4 * C + 4);
+  std::vector<uint16_t> cmeta(C + 1);
+  T.cref = cref.data();
+  T.cmeta = cmeta.data();
+  auto bump = [&](uint64_t b) {
+    uint64_t o = lfb;
+    lfb += b;
+    return o;
+  };
+  for (uint64_t i = 0; i < m; ++i) {
+    if (early)
+      op_leaf_topo_early(T, i, bump);
+    else
+      op_leaf_topo(T, i, bump);
+  }
+  if (early && lfb != longb) return -7;  // the arena is sized by the early count
+  std::vector<uint64_t> arena((lfb + 64) / 8 + 1), lmsg(LEAF_WORDS * m + 1), bmsg(BR_WORDS * B + 1),
+      xmsg(EXT_WORDS * B + 1);
   T.lmsg = lmsg.data();
   T.lstride = m;
   T.bmsg = bmsg.data();
@@ -223,15 +266,12 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       if (ctr[CTR_ERR]) return -6;
     }
   }
-  std::vector<uint16_t> cmeta(C + 1);
-  T.cref = cref.data();
-  T.cmeta = cmeta.data();
   T.arena = (uint8_t*)arena.data();
-  uint64_t perms = 0, hashes = 0, inl = 0;
-  for (uint64_t i = 0; i < m; ++i) op_leaf_prep(T, i, T.vals + T.svoff[i], T.svlen[i]);
+  if (!early)
+    for (uint64_t i = 0; i < m; ++i) op_leaf_prep(T, i, T.vals + T.svoff[i], T.svlen[i]);
   for (uint64_t i = 0; i < m; ++i) {
     uint32_t in1 = 0;
-    uint32_t p = op_leaf_hash(T, i, &in1);
+    uint32_t p = early ? op_leaf_long(T, i, &in1) : op_leaf_hash(T, i, &in1);
     perms += p;
     hashes += p ? 1 : 0;
     inl += in1;
