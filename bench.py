@@ -82,6 +82,21 @@ def cpu_baseline(ctx, cfg, n_sample):
             "seconds": dt, "state_root_s_extrapolated_100M": dt / n_sample * 1e8}
 
 
+def pmc_traffic(kernel, n):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this
+    workload size (profiles/*_pmc_traffic_<n>.json, written by scripts/pmc_summary.py
+    from scripts/gpu_pmc.sh: read = 2 x FETCH_SIZE, write = WRITE_SIZE per
+    MI355X_MICROARCH.md), or None when no pass was collected for it."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_traffic_{n}.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        with open(f) as fh:
+            row = json.load(fh)["kernels"].get(kernel)
+        if row and row.get("calls_per_build"):
+            return row["hbm_bytes"] / row["calls_per_build"]
+    return None
+
+
 def single(args):
     import torch
     from khipu_amd.device import Ctx
@@ -102,18 +117,18 @@ def single(args):
     root = hh[0].tobytes().hex()
     s = stats[-1]
     ms_dev = float(np.mean([x["t_total_ms"] for x in stats]))
-    # dominant kernel: the stage with the largest device time
-    stages = {"k_hash_keys": "t_keys_ms", "k_leaf_emit": "t_leaf_ms", "k_branch_emit": "t_branch_ms",
+    # stage times (HIP events on the stream each stage runs on; k_leaf_fused runs on
+    # the library's second stream, overlapped with the topology stage)
+    stages = {"k_hash_keys": "t_keys_ms", "k_leaf_fused": "t_leaf_ms", "branch_levels": "t_branch_ms",
               "sort": "t_sort_ms", "topology": "t_topo_ms"}
     avg = {k: float(np.mean([x[v] for x in stats])) for k, v in stages.items()}
-    dom = max(avg, key=avg.get)
-    perms = {"k_hash_keys": s["n_key_perms"], "k_leaf_emit": s["n_leaves"]}.get(dom)
-    roof = None
-    if perms:
-        achieved = perms * OPS_PER_PERM / (avg[dom] * 1e-3)
-        roof = {"kernel": dom, "bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
-                "unit": "T int32-lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS, "traffic": None,
-                "avg_ms": avg[dom], "perms_per_launch": perms}
+    # dominant single kernel: the larger of the two one-launch hash kernels
+    dom = max(("k_hash_keys", "k_leaf_fused"), key=avg.get)
+    perms = {"k_hash_keys": s["n_key_perms"], "k_leaf_fused": s["n_leaves"]}[dom]
+    achieved = perms * OPS_PER_PERM / (avg[dom] * 1e-3)
+    roof = {"kernel": dom, "bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
+            "unit": "T int32-lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS,
+            "traffic": pmc_traffic(dom, n), "avg_ms": avg[dom], "perms_per_launch": perms}
     out = {
         "metric": "node-hashes/sec (full state root, 100M-account trie)",
         "value": s["n_node_hashes"] / dt,

@@ -1285,8 +1285,12 @@ static kh_ctx* ctx_new(int dev) {
   HIPCHK(hipSetDevice(dev));
   kh_ctx* c = new kh_ctx();
   c->dev = dev;
-  HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
+  // the latency-bound topology kernels (own stream) get the dispatcher's priority
+  // over the VALU-bound leaf kernel they overlap with (st2)
+  int prio_lo = 0, prio_hi = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  HIPCHK(hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, prio_hi));
+  HIPCHK(hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, prio_lo));
   c->st = c->own;
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipHostMalloc((void**)&c->h_pinned, 4096, hipHostMallocDefault));

@@ -3,7 +3,7 @@
 # Every GPU step has its own time limit; the first failing step ends the round.
 export TMPDIR=/tmp
 TAG=${1:-r}
-step() { local name=$1; shift; "$@"; local rc=$?; echo "${name}_RC=$rc"; [ $rc -eq 0 ] || exit $rc; }
+step() { local name=$1; shift; "$@"; local rc=$?; echo "${name}_RC=$rc" >&2; [ $rc -eq 0 ] || exit $rc; }
 step SMOKE timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke_$TAG.log 2>&1
 step PYTEST timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread -o log_cli=false --junitxml=gpurun_out/pytest_$TAG.xml > gpurun_out/pytest_$TAG.log 2>&1
 tail -3 gpurun_out/pytest_$TAG.log

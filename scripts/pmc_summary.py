@@ -22,16 +22,21 @@ out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else N
 if out_json in args:
     args.remove(out_json)
 
+def kname(full):
+    """'void khst::k_scan_tiles<unsigned int>(...)' -> 'k_scan_tiles' (template instances merge)"""
+    return full.split("(")[0].replace("void ", "").split("<")[0].replace("khst::", "").strip()
+
+
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in sorted(glob.glob(f"gpurun_out/{tag}_p*/**/pmc_counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
-        agg[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]] += float(r["Counter_Value"])
+        agg[kname(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
 dur = collections.defaultdict(float)
 calls = collections.defaultdict(int)
 vg = {}
 for f in sorted(glob.glob(f"gpurun_out/{tag}_p1/**/pmc_kernel_trace.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0]
+        k = kname(r["Kernel_Name"])
         dur[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
         calls[k] += 1
         vg[k] = (r.get("VGPR_Count") or r.get("Arch_VGPR_Count"), r.get("LDS_Block_Size"))
