@@ -311,16 +311,39 @@ __global__ void __launch_bounds__(BS) k_level_count(Topo T, const uint32_t* Bp, 
   for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) bcnt[(uint64_t)q * nblk + blockIdx.x] = h[q];
 }
 
+// pos[j] = position of branch j (numbered in key order by the rep scan) in the
+// level order; the branch tables are then permuted to that order (k_branch_permute)
+// so a level reads its branches' fields, child records and message slots contiguously
 __global__ void __launch_bounds__(BS) k_level_scatter(Topo T, const uint32_t* Bp, const uint32_t* bbase,
-                                                      uint32_t nblk, uint32_t* order) {
+                                                      uint32_t nblk, uint32_t* pos) {
   __shared__ uint32_t base[NBUCKET];
   for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) base[q] = bbase[(uint64_t)q * nblk + blockIdx.x];
   __syncthreads();
   const uint64_t B = *Bp, j0 = (uint64_t)blockIdx.x * LV_TILE;
-  for (uint64_t j = j0 + threadIdx.x; j < j0 + LV_TILE && j < B; j += BS) {
-    uint32_t r = atomicAdd(&base[branch_bucket(T, j)], 1u);
-    order[r] = (uint32_t)j;
-  }
+  for (uint64_t j = j0 + threadIdx.x; j < j0 + LV_TILE && j < B; j += BS)
+    pos[j] = atomicAdd(&base[branch_bucket(T, j)], 1u);
+}
+
+// the branch tables k_branch_topo wrote in key-order ids (J), moved to level order
+struct BrTab {
+  uint32_t *k, *parent, *first;
+  uint8_t *depth, *ext, *pord;
+};
+__global__ void __launch_bounds__(BS) k_branch_permute(Topo T, BrTab J, const uint32_t* pos, const uint32_t* Bp) {
+  const uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (j >= *Bp) return;
+  const uint32_t g = pos[j], p = J.parent[j];
+  T.br_k[g] = J.k[j];
+  T.br_depth[g] = J.depth[j];
+  T.br_ext[g] = J.ext[j];
+  T.br_pord[g] = J.pord[j];
+  T.br_first[g] = J.first[j];
+  T.br_parent[g] = p == NONE ? NONE : pos[p];  // parents of neighbouring branches are neighbours
+}
+// group reps carry level-order branch ids from here on (leaf parents, resident tables)
+__global__ void __launch_bounds__(BS) k_bid_remap(Topo T, const uint32_t* pos, uint64_t nb) {
+  const uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (b < nb && T.u[b] != 0 && T.rep[b] == (uint32_t)b) T.isrep_bid[b] = pos[T.isrep_bid[b]];
 }
 
 // level bounds: lb[d] = first position of depth d in `order`, lb[64] = B
@@ -504,17 +527,18 @@ __global__ void __launch_bounds__(BS) k_leaf_long(Topo T) {
   block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
 }
 
-// one level: `first` = its first position in the level order, `cnt` = its size
-__global__ void __launch_bounds__(BS) k_branch_prep(Topo T, const uint32_t* order, uint64_t first, uint64_t cnt) {
+// one level: `first` = its first position in the level order, `cnt` = its size;
+// branch ids are level positions (k_branch_permute)
+__global__ void __launch_bounds__(BS) k_branch_prep(Topo T, uint64_t first, uint64_t cnt) {
   uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (t < cnt) op_branch_prep(T, order[first + t], first + t);
+  if (t < cnt) op_branch_prep(T, (uint32_t)(first + t), first + t);
 }
 
-__global__ void __launch_bounds__(BS) k_branch_hash(Topo T, const uint32_t* order, uint64_t first, uint64_t cnt) {
+__global__ void __launch_bounds__(BS) k_branch_hash(Topo T, uint64_t first, uint64_t cnt) {
   uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (t < cnt) {
-    uint32_t j = order[first + t];
+    uint32_t j = (uint32_t)(first + t);
     uint32_t in1 = 0;
     perms = op_branch_hash(T, j, first + t, &in1);
     hashes = branch_hash_count(T, j, (uint32_t)perms);
@@ -968,6 +992,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       nres * 32, nres * 4, nres * 32,         // results
       CTR_N * 8, 64 * 4, 80 * 4, 512 * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
       early ? n * 32 : 0, early ? n : 0,      // early leaves: stashed references, meta
+      nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1, nb1,  // branch tables in key-order ids (BrTab J)
   };
   c->ws1.ensure(carve_size(sz));
   Carver cv{(char*)c->ws1.p, 0, c->ws1.cap};
@@ -1020,6 +1045,13 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint32_t* order = cv.take<uint32_t>(nb1);
   T.lf_eref = early ? cv.take<uint64_t>(n * 4) : nullptr;
   T.lf_emeta = early ? cv.take<uint8_t>(n) : nullptr;
+  BrTab J{};
+  J.k = cv.take<uint32_t>(nb1);
+  J.parent = cv.take<uint32_t>(nb1);
+  J.first = cv.take<uint32_t>(nb1);
+  J.depth = cv.take<uint8_t>(nb1);
+  J.ext = cv.take<uint8_t>(nb1);
+  J.pord = cv.take<uint8_t>(nb1);
   T.depth0 = A.depth0;
   T.segmented = segmented ? 1 : 0;
   T.vals = A.vals;
@@ -1104,19 +1136,33 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     hipLaunchKernelGGL(k_chain, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
     scan_exclusive<uint32_t>(T.isrep_bid, T.isrep_bid, nb, Bp, scan_scratch, st);
-    HIPCHK(hipMemsetAsync(T.br_k, 0, nb * 4, st));  // entries past B must scan as 0
-    hipLaunchKernelGGL(k_branch_topo, GRID(nb, BS), dim3(BS), 0, st, T, P, nb);
+    // branch tables in key-order ids first (k_branch_topo writes them, thread per boundary)
+    Topo TJ = T;
+    TJ.br_k = J.k;
+    TJ.br_parent = J.parent;
+    TJ.br_first = J.first;
+    TJ.br_depth = J.depth;
+    TJ.br_ext = J.ext;
+    TJ.br_pord = J.pord;
+    hipLaunchKernelGGL(k_branch_topo, GRID(nb, BS), dim3(BS), 0, st, TJ, P, nb);
     LAUNCH_CHECK();
-    // level order (grids sized by nb; threads past B exit)
+    // level order (grids sized by nb; threads past B exit), then every branch id
+    // becomes its level position
     const uint32_t nblk = (uint32_t)((nb + LV_TILE - 1) / LV_TILE);
-    hipLaunchKernelGGL(k_level_count, dim3(nblk), dim3(BS), 0, st, T, (const uint32_t*)Bp, bcnt, nblk);
+    hipLaunchKernelGGL(k_level_count, dim3(nblk), dim3(BS), 0, st, TJ, (const uint32_t*)Bp, bcnt, nblk);
     LAUNCH_CHECK();
     scan_exclusive<uint32_t>(bcnt, bcnt, (uint64_t)NBUCKET * nblk, (uint32_t*)nullptr, scan_scratch, st);
-    hipLaunchKernelGGL(k_level_scatter, dim3(nblk), dim3(BS), 0, st, T, (const uint32_t*)Bp,
+    hipLaunchKernelGGL(k_level_scatter, dim3(nblk), dim3(BS), 0, st, TJ, (const uint32_t*)Bp,
                        (const uint32_t*)bcnt, nblk, order);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_level_bounds, dim3(1), dim3(64), 0, st, (const uint32_t*)bcnt, nblk, (const uint32_t*)Bp,
                        lb);
+    LAUNCH_CHECK();
+    HIPCHK(hipMemsetAsync(T.br_k, 0, nb * 4, st));  // entries past B must scan as 0
+    hipLaunchKernelGGL(k_branch_permute, GRID(nb, BS), dim3(BS), 0, st, T, J, (const uint32_t*)order,
+                       (const uint32_t*)Bp);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_bid_remap, GRID(nb, BS), dim3(BS), 0, st, T, (const uint32_t*)order, nb);
     LAUNCH_CHECK();
     // child record bases
     scan_exclusive<uint32_t>(T.br_k, T.br_cbase, nb, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
@@ -1210,11 +1256,9 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   for (int d = 63; d >= 0; --d) {
     uint32_t cnt = lbh[d + 1] - lbh[d];
     if (!cnt) continue;
-    hipLaunchKernelGGL(k_branch_prep, GRID(cnt, BS), dim3(BS), 0, st, T, (const uint32_t*)order, (uint64_t)lbh[d],
-                       (uint64_t)cnt);
+    hipLaunchKernelGGL(k_branch_prep, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_branch_hash, GRID(cnt, BS), dim3(BS), 0, st, T, (const uint32_t*)order, (uint64_t)lbh[d],
-                       (uint64_t)cnt);
+    hipLaunchKernelGGL(k_branch_hash, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     LAUNCH_CHECK();
     ++levels;
   }
