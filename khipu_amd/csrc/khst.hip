@@ -452,17 +452,27 @@ __global__ void __launch_bounds__(BS) k_leaf_fused(Topo T) {
   const uint32_t P = g.L - vlen;
   const uint32_t qlo = P >> 3, nq = (shortl && vlen) ? ((g.L + 7) >> 3) - qlo : 0;
   const uint32_t gi = ln >> 4, gl = ln & 15;
+  // the staging parameters of the wave's 64 leaves go through LDS (one broadcast
+  // read per group instead of five shuffles), and the copy loop is fully unrolled
+  // with two predicated word steps, so every group's loads are independent and issue
+  // back to back (the random value reads are latency-bound)
+  __shared__ uint64_t s_vs[BS];
+  __shared__ uint32_t s_pq[BS];
+  s_vs[threadIdx.x] = vs;
+  s_pq[threadIdx.x] = P | ((g.L & 0xFFu) << 8) | (qlo << 16) | (nq << 24);  // nq > 0 only for one-block leaves
+  __syncthreads();
+#pragma unroll
   for (uint32_t it = 0; it < 16; ++it) {
-    const int src = (int)(it * 4 + gi);  // src is usually in another 16-lane group:
-    // every shuffle runs with the whole wave active (a lane masked off by an early
-    // `continue` would hand its neighbours undefined data)
-    const uint32_t snq = __shfl(nq, src);
-    const uint64_t svs = __shfl(vs, src);
-    const uint32_t sP = __shfl(P, src), sL = __shfl(g.L, src), sq = __shfl(qlo, src);
-    if (snq == 0) continue;
+    const uint32_t src = it * 4 + gi;
+    const uint32_t pq = s_pq[wbase + src];
+    const uint32_t snq = pq >> 24, sP = pq & 0xFF, sL = (pq >> 8) & 0xFF, sq = (pq >> 16) & 0xFF;
+    const uint64_t svs = s_vs[wbase + src];
     const uint64_t w_first = svs >> 3, w_last = (svs + (sL - sP) - 1) >> 3;
     uint64_t* dst = msg + (wbase + src) * LEAF_WORDS;
-    for (uint32_t q = sq + gl; q < sq + snq; q += 16) {
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+      const uint32_t q = sq + gl + 16 * h;
+      if (q >= sq + snq) continue;
       // message byte 8q <-> value byte 8q - P <-> buffer byte svs + 8q - P (may precede the span)
       const int64_t bp = (int64_t)svs + 8 * (int64_t)q - (int64_t)sP;
       const int64_t wa = bp >> 3;  // arithmetic shift: floor
