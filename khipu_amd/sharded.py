@@ -162,15 +162,33 @@ def gather_refs(be, hh, ll, ii):
     return H, L, I
 
 
-def sharded_root(be, addr, vals, voff, n, klen=20, keys_prehashed=False):
+def sharded_root(be, addr, vals, voff, n, klen=20, keys_prehashed=False, phases=None):
     """One sharded state-root step.  Every rank calls it with its slice of the records;
-    every rank returns the root (bytes) and the number of node hashes it computed."""
+    every rank returns the root (bytes) and the number of node hashes it computed.
+    phases: optional dict that receives each phase's wall time in ms (synchronising
+    the device after every phase: a diagnostic run, not the timed one)."""
+    import time
     world = dist.get_world_size()
+    t = [time.perf_counter()]
+
+    def mark():
+        if phases is not None:
+            be.sync()
+            t.append(time.perf_counter())
+
     keys32 = addr if keys_prehashed else be.hash_keys(addr, n, klen)
+    mark()
     pk, pv, pl, cnt, nb = be.partition(keys32, vals, voff, n, world)
+    mark()
     rk, rv, ro, m = exchange(be, pk, pv, pl, cnt, nb)
+    mark()
     hh, ll, ii = be.build(rk, rv, ro, m, depth0=1)
+    mark()
     H, L, I = gather_refs(be, hh, ll, ii)
+    mark()
+    if phases is not None:
+        for name, a, b in zip(("hash_keys", "partition", "exchange", "build", "gather"), t, t[1:]):
+            phases[name] = (b - a) * 1e3
     occupied = [q for q in range(16) if L[q] > 0]
     if len(occupied) >= 2:
         return be.fold(H, L, I)
@@ -226,6 +244,12 @@ def bench_main(args):
     dist.all_reduce(hashes)
     dt = float(dt.item())
     node_hashes = int(hashes[0].item()) + 1  # + the folded root branch
+    # one more (untimed) step with a device sync after every phase: where the time goes
+    phases = {}
+    sharded_root(be, addr, vals, voff, n, phases=phases)
+    ph = torch.tensor([phases[k] for k in sorted(phases)], dtype=torch.float64, device=f"cuda:{local}")
+    dist.all_reduce(ph, op=dist.ReduceOp.MAX)
+    phases = {k: round(float(v), 3) for k, v in zip(sorted(phases), ph.tolist())}
     if rank == 0:
         out = {
             "metric": "node-hashes/sec (full state root, 100M-account trie)",
@@ -238,6 +262,8 @@ def bench_main(args):
             "state_root": root.hex(),
             "topology": {"n_leaves": int(hashes[1].item()), "n_branches": int(hashes[2].item()) + 1,
                          "n_node_hashes": node_hashes},
+            "phase_ms_max_over_ranks": phases,
+            "per_rank_build_ms": st.t_total_ms,
             "roofline": None,
             "cpu_baseline": None,
         }
