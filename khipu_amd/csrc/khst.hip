@@ -625,14 +625,23 @@ __global__ void __launch_bounds__(BS) k_emit_copy(Topo T, uint64_t B, const uint
 }
 
 
-// copy L bytes between arbitrary byte addresses: word loads (load64u_n), then
-// whole-word stores where the destination is aligned, bytes at the unaligned ends
-__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint64_t L) {
-  uint64_t q = 0;
-  uint32_t head = (uint32_t)((8 - ((uintptr_t)dst & 7)) & 7);
-  for (; q < L && q < head; ++q) dst[q] = src[q];
-  for (; q + 8 <= L; q += 8) *(uint64_t*)(dst + q) = load64u_n(src + q, 8);
-  for (; q < L; ++q) dst[q] = src[q];
+// Copy L bytes between arbitrary byte addresses with a group of CG consecutive lanes
+// (lane = 0..CG-1): word loads (load64u_n), whole-word stores where the destination is
+// aligned, bytes at the unaligned ends.  The group's word stores are adjacent, so a
+// wave writes 64/CG spans as contiguous runs instead of 64 scattered words.  Span
+// gathers (resident merge, multi-GPU partition) are HBM-bound; one thread per span
+// left them at <1 TB/s.
+constexpr uint32_t CG = 8;
+constexpr uint64_t PART_BLOCKS = 256 * 16;  // k_part_copy: 16 blocks per CU
+__device__ __forceinline__ void copy_bytes_group(uint8_t* dst, const uint8_t* src, uint64_t L, uint32_t lane) {
+  uint64_t hb = (8 - ((uintptr_t)dst & 7)) & 7;
+  if (hb > L) hb = L;
+  if (lane < hb) dst[lane] = src[lane];
+  const uint64_t nw = (L - hb) >> 3;
+  for (uint64_t w = lane; w < nw; w += CG)
+    *(uint64_t*)(dst + hb + 8 * w) = load64u_n(src + hb + 8 * w, 8);
+  const uint64_t t0 = hb + 8 * nw;
+  if (t0 + lane < L) dst[t0 + lane] = src[t0 + lane];
 }
 
 // ---- resident trie: merge a sorted batch into the sorted (key, value) set (resident.h)
@@ -656,11 +665,11 @@ __global__ void __launch_bounds__(BS) k_place_op(Merge M, const uint32_t* ins_fl
 __global__ void __launch_bounds__(BS) k_merge_vals(const uint64_t* nsrc, const uint32_t* nlen, const uint64_t* noff,
                                                   uint64_t m, const uint8_t* rval, const uint8_t* uval,
                                                   uint8_t* nval) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  uint64_t i = ((uint64_t)blockIdx.x * BS + threadIdx.x) / CG;
   if (i >= m) return;
   uint64_t s = nsrc[i];
   const uint8_t* src = (s & SRC_UPSERT) ? uval + (s & ~SRC_UPSERT) : rval + s;
-  copy_bytes(nval + noff[i], src, nlen[i]);
+  copy_bytes_group(nval + noff[i], src, nlen[i], threadIdx.x % CG);
 }
 __global__ void __launch_bounds__(BS) k_u32_to_u64(const uint32_t* in, uint64_t* out, uint64_t n) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -700,15 +709,19 @@ __global__ void __launch_bounds__(BS) k_part_copy(const uint64_t* K, const uint8
   __shared__ unsigned long long c[16], b[16];
   if (threadIdx.x < 16) c[threadIdx.x] = b[threadIdx.x] = 0;
   __syncthreads();
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i < n) {
+  // grid-stride over records (PART_BLOCKS blocks): the per-block owner counters are
+  // flushed with 2 global atomics per owner, so the block count must stay small
+  const uint32_t lane = threadIdx.x % CG;
+  for (uint64_t i = ((uint64_t)blockIdx.x * BS + threadIdx.x) / CG; i < n; i += (uint64_t)gridDim.x * (BS / CG)) {
     uint32_t s = idx[i];
-    for (int j = 0; j < 4; ++j) okeys[4 * i + j] = K[4 * (uint64_t)s + j];
+    if (lane < 4) okeys[4 * i + lane] = K[4 * (uint64_t)s + lane];
     uint64_t o = voff[s], L = voff[s + 1] - o;
-    copy_bytes(ovals + ooff[i], vals + o, L);
-    uint32_t p = (uint32_t)ck[i];
-    atomicAdd(&c[p], 1ULL);
-    atomicAdd(&b[p], (unsigned long long)L);
+    copy_bytes_group(ovals + ooff[i], vals + o, L, lane);
+    if (lane == 0) {
+      uint32_t p = (uint32_t)ck[i];
+      atomicAdd(&c[p], 1ULL);
+      atomicAdd(&b[p], (unsigned long long)L);
+    }
   }
   __syncthreads();
   if (threadIdx.x < 16 && c[threadIdx.x]) {
@@ -1456,7 +1469,7 @@ static void save_sorted(kh_trie* h, int half, uint64_t m, const uint8_t* vals) {
   HIPCHK(hipStreamSynchronize(st));
   uint64_t vbytes = c->h_pinned[0];
   h->val[half].ensure(vbytes + 64);
-  hipLaunchKernelGGL(k_merge_vals, GRID(m, BS), dim3(BS), 0, st, (const uint64_t*)T.svoff, (const uint32_t*)T.svlen,
+  hipLaunchKernelGGL(k_merge_vals, GRID(m * CG, BS), dim3(BS), 0, st, (const uint64_t*)T.svoff, (const uint32_t*)T.svlen,
                      (const uint64_t*)off, m, vals, (const uint8_t*)nullptr, (uint8_t*)h->val[half].p);
   LAUNCH_CHECK();
   HIPCHK(hipStreamSynchronize(st));
@@ -1620,7 +1633,7 @@ static void trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up
                                       " > " + std::to_string(c->h_pinned[1]) + " + " +
                                       std::to_string(nup ? c->h_pinned[2] : 0) + ")"};
     h->val[nxt].ensure(c->h_pinned[0] + 64);
-    hipLaunchKernelGGL(k_merge_vals, GRID(m2, BS), dim3(BS), 0, st, (const uint64_t*)M.nsrc, (const uint32_t*)M.nlen,
+    hipLaunchKernelGGL(k_merge_vals, GRID(m2 * CG, BS), dim3(BS), 0, st, (const uint64_t*)M.nsrc, (const uint32_t*)M.nlen,
                        (const uint64_t*)noff, m2, (const uint8_t*)h->val[cur].p, d_up_vals,
                        (uint8_t*)h->val[nxt].p);
     LAUNCH_CHECK();
@@ -1930,7 +1943,8 @@ int kh_dev_partition(kh_ctx* c, const uint8_t* d_keys32, const uint8_t* d_vals, 
     LAUNCH_CHECK();
     scan_exclusive<uint64_t>(d_out_vlen, ooff, n, (uint64_t*)nullptr, sc, st);
     HIPCHK(hipMemsetAsync(tot, 0, 256, st));
-    hipLaunchKernelGGL(k_part_copy, GRID(n, BS), dim3(BS), 0, st, K, d_vals, d_voff, (const uint32_t*)i0,
+    const unsigned pgrid = (unsigned)std::min<uint64_t>(PART_BLOCKS, (n * CG + BS - 1) / BS);
+    hipLaunchKernelGGL(k_part_copy, dim3(pgrid), dim3(BS), 0, st, K, d_vals, d_voff, (const uint32_t*)i0,
                        (const uint64_t*)ooff, n, (const uint64_t*)ck0, (uint64_t*)d_out_keys, d_out_vals, tot,
                        tot + 16);
     LAUNCH_CHECK();

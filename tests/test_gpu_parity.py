@@ -225,3 +225,35 @@ def test_device_build_misaligned_buffers(khst, oracle, koff, voff_shift):
     dk, dv, do = kb.cuda()[koff:], vb.cuda()[voff_shift:], off.cuda()
     hh, _, _, _ = ctx.build(dk, 32, dv, do, len(keys))
     assert hh[0].tobytes() == oracle.seq_root(keys, vals)
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 3, 8, 16])
+def test_partition_vs_host(khst, nparts):
+    """kh_dev_partition (grouped span copy) == a stable numpy partition by top-nibble owner:
+    keys, value bytes, value lengths, per-owner counts and bytes; ragged 0..300-byte values
+    at unaligned offsets, plus the empty batch."""
+    import torch
+    from khipu_amd import sharded
+    rng = np.random.default_rng(nparts)
+    be = sharded.GpuBackend(0)
+    for n in (0, 1, 777, 100_003):
+        lens = rng.integers(0, 301, n).astype(np.int64)
+        short = rng.random(n) < 0.5
+        lens[short] = rng.integers(0, 12, int(short.sum()))
+        vo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        v = rng.integers(0, 256, int(vo[-1]) + 64, dtype=np.uint8)
+        k = rng.integers(0, 256, n * 32 + 64, dtype=np.uint8)
+        kd, vd, od = (torch.from_numpy(x).to("cuda:0") for x in (k, v, vo))
+        pk, pv, pl, cnt, nb = be.partition(kd, vd, od, n, nparts)
+        torch.cuda.synchronize()
+        kk = k[:n * 32].reshape(n, 32)
+        owner = ((kk[:, 0] >> 4).astype(np.int64) * nparts) >> 4
+        order = np.argsort(owner, kind="stable")
+        assert np.array_equal(cnt, np.bincount(owner, minlength=nparts)[:nparts])
+        assert np.array_equal(nb, np.bincount(owner, weights=lens, minlength=nparts)[:nparts].astype(np.int64))
+        if n == 0:
+            continue
+        assert np.array_equal(pk[:n * 32].cpu().numpy(), kk[order].reshape(-1))
+        assert np.array_equal(pl[:n].cpu().numpy(), lens[order])
+        want = np.concatenate([v[vo[i]:vo[i + 1]] for i in order])
+        assert np.array_equal(pv[:len(want)].cpu().numpy(), want)
