@@ -190,6 +190,15 @@ int kh_trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals
                   uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
                   uint8_t root32[32], kh_stats* stats);
 
+/* Storage write-back hand-off for a resident trie: the node set of the
+ * current version — every node reachable from the committed root whose encoding is
+ * >= 32 B, plus the root node — what persist()/changes hand to NodeStorage.update
+ * (MerklePatriciaTrie.scala:491-516,544-554; BlockWorldState.scala:312-330).  Same layout
+ * and KH_ENOSPC size negotiation as kh_trie_root_nodes; host outputs.  The current version
+ * is re-encoded from its sorted set (no sort), and its root is checked against the commit's. */
+int kh_trie_emit_nodes(kh_trie* h, uint8_t* hashes32, uint64_t node_cap, uint8_t* rlp, uint64_t rlp_cap,
+                       uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len);
+
 int kh_trie_size(const kh_trie* h, uint64_t* n);
 int kh_trie_free(kh_trie* h);
 

@@ -24,7 +24,7 @@ EXPORTS = (
     "kh_last_error", "kh_version", "kh_device_count", "kh_kec256_batch", "kh_trie_root",
     "kh_trie_roots_segmented", "kh_trie_root_nodes", "kh_ctx_create", "kh_ctx_destroy", "kh_ctx_set_stream",
     "kh_dev_kec256_batch", "kh_dev_trie_build", "kh_fold_root16", "kh_dev_synth_accounts", "kh_dev_hash_keys",
-    "kh_dev_partition", "kh_trie_open", "kh_trie_apply", "kh_trie_size", "kh_trie_free",
+    "kh_dev_partition", "kh_trie_open", "kh_trie_apply", "kh_trie_emit_nodes", "kh_trie_size", "kh_trie_free",
     "kh_verify_nodes",
 )
 
@@ -101,6 +101,7 @@ def lib():
     L.kh_dev_partition.argtypes = [vp, vp, vp, vp, u64, u32, vp, vp, vp, vp, vp]
     L.kh_trie_open.argtypes = [vp, vp, u32, vp, vp, u64, u32, vp, ctypes.POINTER(vp)]
     L.kh_trie_apply.argtypes = [vp, vp, vp, vp, u64, vp, u64, u32, u32, vp, vp]
+    L.kh_trie_emit_nodes.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp]
     L.kh_trie_size.argtypes = [vp, ctypes.POINTER(u64)]
     L.kh_trie_free.argtypes = [vp]
     L.kh_verify_nodes.argtypes = [vp, vp, u64, vp, vp, u64, vp, vp, vp, vp, vp, vp]

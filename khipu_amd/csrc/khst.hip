@@ -1794,6 +1794,57 @@ int kh_trie_roots_segmented(const uint8_t* keys, uint32_t klen, const uint8_t* v
   })
 }
 
+// Emission of the node set of the build just run on c (c->T): every node reachable from
+// the root whose encoding is >= 32 B, plus the root node (MerklePatriciaTrie.scala:505-511).
+// Host outputs; KH_ENOSPC with the needed sizes in *n_nodes / *rlp_len.
+static int emit_node_set(kh_ctx* c, uint8_t* hashes32, uint64_t node_cap, uint8_t* rlp, uint64_t rlp_cap,
+                         uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len) {
+  Topo& T = c->T;
+  uint64_t B = c->last_B;
+  uint64_t Q = T.m + 2 * B;
+  c->ws3.ensure(carve_size({Q * 4, Q * 8, Q * 8 + 64}));
+  Carver c3{(char*)c->ws3.p, 0, c->ws3.cap};
+  uint32_t* flag = c3.take<uint32_t>(Q);
+  uint64_t* bytes = c3.take<uint64_t>(Q);
+  char* sscr = c3.take<char>(scan_scratch_bytes(Q, 8));
+  (void)sscr;
+  hipStream_t st = c->st;
+  hipLaunchKernelGGL(k_emit_sizes, GRID(Q, BS), dim3(BS), 0, st, T, B, flag, bytes);
+  LAUNCH_CHECK();
+  // totals: reuse the build's counter block
+  uint64_t* totb = (uint64_t*)(T.ctr + CTR_E0);
+  uint32_t* totn = (uint32_t*)(T.ctr + CTR_E1);
+  HIPCHK(hipMemsetAsync(T.ctr + CTR_E0, 0, 16, st));
+  // scan scratch: ws1's scan scratch may be too small for Q; use a dedicated buffer
+  c->out_emit.ensure(scan_scratch_bytes(Q, 8) + 256);
+  scan_exclusive<uint64_t>(bytes, bytes, Q, totb, c->out_emit.p, st);
+  scan_exclusive<uint32_t>(flag, flag, Q, totn, c->out_emit.p, st);
+  HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_E0, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  uint64_t tb = c->h_pinned[0];
+  uint64_t tn = (uint32_t)c->h_pinned[1];
+  *n_nodes = tn;
+  *rlp_len = tb;
+  if (tn > node_cap || tb > rlp_cap || !hashes32 || !rlp || !off) return set_err(KH_ENOSPC, "output too small");
+  // device output: hashes | rlp | off
+  DevBuf outb;
+  outb.ensure(tn * 32 + tb + (tn + 1) * 8 + 1024);
+  uint8_t* oh = (uint8_t*)outb.p;
+  uint8_t* orlp = oh + ((tn * 32 + 255) & ~255ULL);
+  uint64_t* ooff = (uint64_t*)(orlp + ((tb + 255) & ~255ULL));
+  // re-derive flags (scan overwrote them with positions; emission re-tests each node)
+  hipLaunchKernelGGL(k_emit_copy, GRID(Q, BS), dim3(BS), 0, st, T, B, (const uint32_t*)flag,
+                     (const uint64_t*)bytes, oh, orlp, ooff);
+  LAUNCH_CHECK();
+  HIPCHK(hipMemcpyAsync(hashes32, oh, tn * 32, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(rlp, orlp, tb, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(off, ooff, tn * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  off[tn] = tb;
+  outb.release();
+  return KH_OK;
+}
+
 int kh_trie_root_nodes(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const uint64_t* voff, uint64_t n,
                        uint32_t flags, uint8_t root32[32], uint8_t* hashes32, uint64_t node_cap, uint8_t* rlp,
                        uint64_t rlp_cap, uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len, kh_stats* stats) {
@@ -1814,50 +1865,7 @@ int kh_trie_root_nodes(const uint8_t* keys, uint32_t klen, const uint8_t* vals, 
     BuildOut O;
     run_build(c, A, O, stats);
     copy_root(O, 0, root32);
-    // emission
-    Topo& T = c->T;
-    uint64_t B = c->last_B;
-    uint64_t Q = T.m + 2 * B;
-    c->ws3.ensure(carve_size({Q * 4, Q * 8, Q * 8 + 64}));
-    Carver c3{(char*)c->ws3.p, 0, c->ws3.cap};
-    uint32_t* flag = c3.take<uint32_t>(Q);
-    uint64_t* bytes = c3.take<uint64_t>(Q);
-    char* sscr = c3.take<char>(scan_scratch_bytes(Q, 8));
-    (void)sscr;
-    hipStream_t st = c->st;
-    hipLaunchKernelGGL(k_emit_sizes, GRID(Q, BS), dim3(BS), 0, st, T, B, flag, bytes);
-    LAUNCH_CHECK();
-    // totals: reuse the build's counter block
-    uint64_t* totb = (uint64_t*)(T.ctr + CTR_E0);
-    uint32_t* totn = (uint32_t*)(T.ctr + CTR_E1);
-    HIPCHK(hipMemsetAsync(T.ctr + CTR_E0, 0, 16, st));
-    // scan scratch: ws1's scan scratch may be too small for Q; use a dedicated buffer
-    c->out_emit.ensure(scan_scratch_bytes(Q, 8) + 256);
-    scan_exclusive<uint64_t>(bytes, bytes, Q, totb, c->out_emit.p, st);
-    scan_exclusive<uint32_t>(flag, flag, Q, totn, c->out_emit.p, st);
-    HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_E0, 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    uint64_t tb = c->h_pinned[0];
-    uint64_t tn = (uint32_t)c->h_pinned[1];
-    *n_nodes = tn;
-    *rlp_len = tb;
-    if (tn > node_cap || tb > rlp_cap || !hashes32 || !rlp || !off) return set_err(KH_ENOSPC, "output too small");
-    // device output: hashes | rlp | off
-    DevBuf outb;
-    outb.ensure(tn * 32 + tb + (tn + 1) * 8 + 1024);
-    uint8_t* oh = (uint8_t*)outb.p;
-    uint8_t* orlp = oh + ((tn * 32 + 255) & ~255ULL);
-    uint64_t* ooff = (uint64_t*)(orlp + ((tb + 255) & ~255ULL));
-    // re-derive flags (scan overwrote them with positions; emission re-tests each node)
-    hipLaunchKernelGGL(k_emit_copy, GRID(Q, BS), dim3(BS), 0, st, T, B, (const uint32_t*)flag,
-                       (const uint64_t*)bytes, oh, orlp, ooff);
-    LAUNCH_CHECK();
-    HIPCHK(hipMemcpyAsync(hashes32, oh, tn * 32, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(rlp, orlp, tb, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(off, ooff, tn * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    off[tn] = tb;
-    outb.release();
+    return emit_node_set(c, hashes32, node_cap, rlp, rlp_cap, off, n_nodes, rlp_len);
   })
 }
 
@@ -2076,6 +2084,31 @@ int kh_trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals
     HIPCHK(hipSetDevice(h->c->dev));
     trie_apply(h, d_up_keys, d_up_vals, d_up_voff, nup, d_del_keys, ndel, klen, flags, stats);
     if (root32) memcpy(root32, h->root, 32);
+  })
+}
+
+int kh_trie_emit_nodes(kh_trie* h, uint8_t* hashes32, uint64_t node_cap, uint8_t* rlp, uint64_t rlp_cap,
+                       uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len) {
+  if (!h || !n_nodes || !rlp_len) return set_err(KH_EINVAL, "null handle or size outputs");
+  API_TRY({
+    *n_nodes = 0;
+    *rlp_len = 0;
+    if (h->m == 0) {
+      if (off && node_cap + 1 > 0) off[0] = 0;
+      return KH_OK;
+    }
+    kh_ctx* c = h->c;
+    HIPCHK(hipSetDevice(c->dev));
+    // re-encode the current version from its sorted set (no sort), keeping the encodings
+    BuildArgs A{(const uint8_t*)h->key[h->cur].p, 32, (const uint8_t*)h->val[h->cur].p,
+                (const uint64_t*)h->off[h->cur].p, h->m, nullptr, 1, 0, 0, true};
+    A.presorted = true;
+    BuildOut O;
+    run_build(c, A, O, nullptr);
+    uint8_t r[32];
+    copy_root(O, 0, r);
+    if (memcmp(r, h->root, 32) != 0) throw KhError{KH_EINTERNAL, "emit: re-encoded root differs from the committed root"};
+    return emit_node_set(c, hashes32, node_cap, rlp, rlp_cap, off, n_nodes, rlp_len);
   })
 }
 

@@ -144,6 +144,25 @@ class ResidentTrie:
         self.root = root.tobytes()
         return self.root
 
+    def nodes(self):
+        """{hash: encoding} of the current version for storage write-back (kh_trie_emit_nodes):
+        every node reachable from the root with an encoding >= 32 B, plus the root node."""
+        nn, nl = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        cap_n, cap_b = 0, 0
+        for _ in range(2):
+            hs = np.zeros(32 * max(cap_n, 1), np.uint8)
+            rl = np.zeros(max(cap_b, 1), np.uint8)
+            of = np.zeros(cap_n + 1, np.uint64)
+            self.ctx._sync()
+            rc = lib().kh_trie_emit_nodes(self.h, hs.ctypes.data, cap_n, rl.ctypes.data, cap_b, of.ctypes.data,
+                                          ctypes.byref(nn), ctypes.byref(nl))
+            if rc == _lib.KH_ENOSPC:
+                cap_n, cap_b = nn.value, nl.value
+                continue
+            check(rc)
+            return {hs[32 * i:32 * i + 32].tobytes(): rl[of[i]:of[i + 1]].tobytes() for i in range(nn.value)}
+        raise RuntimeError("kh_trie_emit_nodes: size negotiation failed")
+
     @property
     def root_hash(self):
         return self.root

@@ -82,3 +82,35 @@ def test_commit_1m_vs_full_build(khst):
     # ~19k changed leaves + the ~23k branches on their paths, not the 1.36M of a full build
     assert st.n_node_hashes < full.n_node_hashes // 20, (st.n_node_hashes, full.n_node_hashes)
     t.close()
+
+
+@pytest.mark.parametrize("sc", C.commit_scenarios(), ids=lambda s: s[0])
+def test_emit_nodes_after_commits(khst, oracle, sc):
+    """kh_trie_emit_nodes after every commit == the oracle's reachable node
+    set, and the nodes new in this version (absent from the previous one) are Updated
+    entries of the faithful log of that block's puts/removes (MerklePatriciaTrie.scala:491-516)."""
+    from khipu_amd.device import Ctx, ResidentTrie
+    name, ks, vs, batches = sc
+    o = oracle.Trie()
+    for k, v in zip(ks, vs):
+        o.put(k, v)
+    t = ResidentTrie(Ctx(0), ks, vs)
+    prev = t.nodes()
+    assert prev == (o.reachable() if ks else {}), name
+    o.persist().reopen()
+    for i, (ups, dels) in enumerate(batches):
+        for k, v in ups:
+            o.put(k, v)
+        for k in dels:
+            o.remove(k)
+        t.commit(ups, dels)
+        cur = t.nodes()
+        assert t.root == o.root_hash(), (name, i)
+        want = o.reachable() if len(t) else {}
+        assert cur == want, (name, i)
+        upd = o.updated()
+        new = {h: e for h, e in cur.items() if h not in prev}
+        assert all(h in upd and upd[h] == e for h, e in new.items()), (name, i)
+        o.persist().reopen()
+        prev = cur
+    t.close()
