@@ -15,10 +15,10 @@ import glob
 import json
 import sys
 
-args = [a for a in sys.argv[1:] if not a.startswith("--")]
+out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
+args = [a for a in sys.argv[1:] if not a.startswith("--") and a != out_json]
 tag = args[0] if args else "pmc"
 builds = int(args[1]) if len(args) > 1 else 2
-out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
 if out_json in args:
     args.remove(out_json)
 
