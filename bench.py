@@ -88,7 +88,7 @@ def pmc_traffic(kernel, n):
     from scripts/gpu_pmc.sh: read = 2 x FETCH_SIZE, write = WRITE_SIZE per
     MI355X_MICROARCH.md), or None when no pass was collected for it."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_traffic_{n}.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_traffic_{n}.json")))  # tags sort by round: newest last
     for f in reversed(files):
         with open(f) as fh:
             row = json.load(fh)["kernels"].get(kernel)
