@@ -11,14 +11,28 @@ N > 1: (torch.distributed.run, one rank per GPU, RCCL) the same 100M trie with
 each rank holding 1/N of the accounts: keys are routed to their top-nibble
 owner with one all-to-all, each rank builds its 16/N subtries, the 16
 references are all-gathered and folded into the root (khipu_amd/sharded.py).
-Total work is fixed as N grows: "scaling": "strong".
+Total work is fixed as N grows: "scaling": "strong".  `python bench.py --gpus N`
+without a launcher re-launches itself under torch.distributed.run (before any GPU
+call) and exits with its status.
+
+CPU legs (rank 0, N = 1, after the timed region):
+  cpu_baseline       the khipu-faithful sequential trie (oracle/khipu_oracle.cc, 1 core)
+                     on the first 20k/50k/100k accounts of the same workload; every
+                     sample's root is asserted equal to the GPU root of the same prefix;
+                     the 100M state-root time is extrapolated from the fitted per-put cost
+  cpu_batch_allcore  the independent batch builder (oracle/batch_root.cc) on ALL cores
+                     over the full workload; its root is asserted equal to the GPU root
 
 Prints ONE JSON line (rank 0).
 """
 import argparse
 import json
+import math
 import os
 import platform
+import re
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,6 +47,7 @@ sys.path.insert(0, ROOT)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 HBM_PEAK = 8.0e12
 OPS_PER_PERM = 5760  # 24 rounds x 240 int32 ops
+SEQ_SAMPLES = (20_000, 50_000, 100_000)
 
 
 def parse():
@@ -42,8 +57,11 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--accounts", type=int, default=100_000_000)
     p.add_argument("--cfg", type=int, default=5, help="synthetic config id (SURVEY §8d seed)")
-    p.add_argument("--cpu-sample", type=int, default=150_000, help="accounts in the CPU-baseline sample")
+    p.add_argument("--seq-samples", type=str, default=",".join(map(str, SEQ_SAMPLES)),
+                   help="account counts timed on the sequential CPU trie (comma separated)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="threads of the CPU batch builder (0: the box's share)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-cpu-batch", action="store_true", help="skip the all-core full-size CPU root")
     p.add_argument("--sharded", action="store_true", help="force the nibble-sharded RCCL path (any N)")
     return p.parse_args()
 
@@ -59,27 +77,86 @@ def cpu_model():
     return platform.processor()
 
 
-def cpu_baseline(ctx, cfg, n_sample):
-    """khipu-faithful sequential trie (oracle, 1 core) on the first n_sample accounts of
-    the same synthetic workload, key hashing included; unit: node-hashes/s."""
+def cpu_threads(req=0):
+    """The box's CPU share: OMP_NUM_THREADS (16 per GPU on the pool), capped by affinity."""
+    if req:
+        return req
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+
+
+def fit_put_cost(samples):
+    """Least-squares fit of us/put = a + b * log16(n) over (n, seconds) samples (the
+    sequential put descends ~log16(n) levels)."""
+    xs = np.array([math.log(n, 16) for n, _ in samples])
+    ys = np.array([t / n * 1e6 for n, t in samples])
+    if len(samples) < 2:
+        return float(ys[0]), 0.0
+    A = np.stack([np.ones_like(xs), xs], 1)
+    (a, b), *_ = np.linalg.lstsq(A, ys, rcond=None)
+    return float(a), float(b)
+
+
+def host_inputs(addr, vals, voff, n):
+    a = addr[:20 * n].cpu().numpy()
+    vo = voff[:n + 1].cpu().numpy().astype(np.uint64)
+    vb = vals[:int(vo[n])].cpu().numpy()
+    return a, vb, vo
+
+
+def cpu_baseline(ctx, cfg, addr, vals, voff, samples):
+    """khipu-faithful sequential trie (oracle, 1 core) on prefixes of the same synthetic
+    workload, key hashing included; unit: node-hashes/s.  Asserts GPU == CPU per sample."""
     from oracle import oracle
-    addr, vals, voff = ctx.synth_accounts(cfg, 0, n_sample)
-    a = addr[:20 * n_sample].cpu().numpy().reshape(n_sample, 20)
-    vo = voff.cpu().numpy().astype(np.uint64)
-    vb = vals[:int(vo[n_sample])].cpu().numpy()
-    # the same sample on the GPU gives the algorithmic node-hash count
-    _, _, _, st = ctx.build(addr, 20, vals, voff, n_sample, hash_keys=True)
-    t0 = time.perf_counter()
-    keys = np.frombuffer(b"".join(oracle.kec256(x.tobytes()) for x in a), np.uint8)
-    root = oracle.seq_root_packed(keys, 32, vb, vo, n_sample)
-    dt = time.perf_counter() - t0
-    hh, _, _, _ = ctx.build(addr, 20, vals, voff, n_sample, hash_keys=True)
-    assert hh[0].tobytes() == root, "GPU/CPU root mismatch on the baseline sample"
-    return {"value": st.n_node_hashes / dt, "unit": "node-hashes/s", "cores": 1, "kind": "port",
-            "sample": f"first {n_sample} accounts of the same synthetic workload, sequential put per account "
+    rows = []
+    for s in samples:
+        _, _, _, st = ctx.build(addr, 20, vals, voff, s, hash_keys=True)  # algorithmic node-hash count
+        hh, _, _, _ = ctx.build(addr, 20, vals, voff, s, hash_keys=True)
+        a, vb, vo = host_inputs(addr, vals, voff, s)
+        t0 = time.perf_counter()
+        keys = np.frombuffer(b"".join(oracle.kec256(a[20 * i:20 * i + 20].tobytes()) for i in range(s)), np.uint8)
+        root = oracle.seq_root_packed(keys, 32, vb, vo, s)
+        dt = time.perf_counter() - t0
+        assert hh[0].tobytes() == root, f"GPU/CPU root mismatch on the {s}-account sample"
+        rows.append({"accounts": s, "seconds": round(dt, 3), "us_per_put": round(dt / s * 1e6, 3),
+                     "node_hashes": int(st.n_node_hashes)})
+    a, b = fit_put_cost([(r["accounts"], r["seconds"]) for r in rows])
+    big = rows[-1]
+    est = 1e8 * (a + b * math.log(1e8, 16)) * 1e-6
+    return {"value": big["node_hashes"] / big["seconds"], "unit": "node-hashes/s", "cores": 1, "kind": "port",
+            "sample": f"first {big['accounts']} accounts of the same synthetic workload, sequential put per account "
                       f"(MerklePatriciaTrie.scala:157-281 as driven by TrieAccounts.flush), key hashing included; "
-                      f"{dt:.2f} s, {dt / n_sample * 1e6:.2f} us/account, CPU: {cpu_model()}",
-            "seconds": dt, "state_root_s_extrapolated_100M": dt / n_sample * 1e8}
+                      f"{big['seconds']:.2f} s; GPU root asserted equal on every sample; CPU: {cpu_model()}",
+            "samples": rows, "fit_us_per_put": {"a": round(a, 4), "b_per_log16n": round(b, 4)},
+            "state_root_s_extrapolated_100M": round(est, 1),
+            "extrapolation": "100M x (a + b log16 100M) us from the fitted samples (not run)"}
+
+
+def cpu_batch(addr, vals, voff, n, gpu_root, threads):
+    """Independent batch builder (oracle/batch_root.cc) on all of the box's cores over the
+    full workload; asserts its root equals the GPU's."""
+    from oracle import oracle
+    a, vb, vo = host_inputs(addr, vals, voff, n)
+    t0 = time.perf_counter()
+    roots, st = oracle.batch_roots(a, (vb, vo), klen=20, hash_keys=True, nthreads=threads)
+    dt = time.perf_counter() - t0
+    ok = roots[0] == gpu_root
+    del a, vb, vo
+    assert ok, f"GPU root {gpu_root.hex()} != CPU batch root {roots[0].hex()} at {n} accounts"
+    return {"value": st["node_hashes"] / dt, "unit": "node-hashes/s", "cores": threads, "kind": "port",
+            "seconds": round(dt, 3), "state_root_match": True, "node_hashes": st["node_hashes"],
+            "node_perms": st["node_perms"], "key_perms": st["key_perms"],
+            "sample": f"all {n} accounts (the full workload), sort + bottom-up hash on {threads} threads, "
+                      f"key hashing included; CPU: {cpu_model()}"}
+
+
+def round_key(path):
+    """profiles/r<round><letters>_... -> (round, letters): r10a sorts after r2b."""
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    return (int(m.group(1)), m.group(2)) if m else (-1, "")
 
 
 def pmc_traffic(kernel, n):
@@ -88,13 +165,28 @@ def pmc_traffic(kernel, n):
     from scripts/gpu_pmc.sh: read = 2 x FETCH_SIZE, write = WRITE_SIZE per
     MI355X_MICROARCH.md), or None when no pass was collected for it."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_traffic_{n}.json")))  # tags sort by round: newest last
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_traffic_{n}.json")), key=round_key)
     for f in reversed(files):
         with open(f) as fh:
             row = json.load(fh)["kernels"].get(kernel)
         if row and row.get("calls_per_build"):
             return row["hbm_bytes"] / row["calls_per_build"]
     return None
+
+
+def roofline(stats, n):
+    """Dominant single kernel of the step (the larger of the two one-launch hash kernels),
+    from the HIP events the library records on the stream each kernel runs on."""
+    stages = {"k_hash_keys": "t_keys_ms", "k_leaf_fused": "t_leaf_ms", "branch_levels": "t_branch_ms",
+              "sort": "t_sort_ms", "topology": "t_topo_ms"}
+    avg = {k: float(np.mean([x[v] for x in stats])) for k, v in stages.items()}
+    s = stats[-1]
+    dom = max(("k_hash_keys", "k_leaf_fused"), key=avg.get)
+    perms = {"k_hash_keys": s["n_key_perms"], "k_leaf_fused": s["n_leaves"]}[dom]
+    achieved = perms * OPS_PER_PERM / (avg[dom] * 1e-3)
+    return avg, {"kernel": dom, "bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
+                 "unit": "T int32-lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS,
+                 "traffic": pmc_traffic(dom, n), "avg_ms": avg[dom], "perms_per_launch": perms}
 
 
 def single(args):
@@ -114,21 +206,10 @@ def single(args):
         stats.append(st.as_dict())
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
-    root = hh[0].tobytes().hex()
+    root = hh[0].tobytes()
     s = stats[-1]
     ms_dev = float(np.mean([x["t_total_ms"] for x in stats]))
-    # stage times (HIP events on the stream each stage runs on; k_leaf_fused runs on
-    # the library's second stream, overlapped with the topology stage)
-    stages = {"k_hash_keys": "t_keys_ms", "k_leaf_fused": "t_leaf_ms", "branch_levels": "t_branch_ms",
-              "sort": "t_sort_ms", "topology": "t_topo_ms"}
-    avg = {k: float(np.mean([x[v] for x in stats])) for k, v in stages.items()}
-    # dominant single kernel: the larger of the two one-launch hash kernels
-    dom = max(("k_hash_keys", "k_leaf_fused"), key=avg.get)
-    perms = {"k_hash_keys": s["n_key_perms"], "k_leaf_fused": s["n_leaves"]}[dom]
-    achieved = perms * OPS_PER_PERM / (avg[dom] * 1e-3)
-    roof = {"kernel": dom, "bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
-            "unit": "T int32-lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS,
-            "traffic": pmc_traffic(dom, n), "avg_ms": avg[dom], "perms_per_launch": perms}
+    avg, roof = roofline(stats, n)
     out = {
         "metric": "node-hashes/sec (full state root, 100M-account trie)",
         "value": s["n_node_hashes"] / dt,
@@ -139,7 +220,7 @@ def single(args):
         "dtype": "u64", "data": "synthetic (counter-based accounts, SURVEY §8d, csrc/synth.h)",
         "config": {"workload": f"{n} synthetic accounts -> state root (keys hashed on GPU)", "accounts": n,
                    "parallelism": "single GPU"},
-        "state_root": root,
+        "state_root": root.hex(),
         "device_ms_per_step": ms_dev,
         "stage_ms": avg,
         "topology": {k: s[k] for k in ("n_leaves", "n_branches", "n_extensions", "n_inline", "n_node_hashes",
@@ -147,12 +228,33 @@ def single(args):
         "roofline": roof,
     }
     if not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(ctx, args.cfg, args.cpu_sample)
+        samples = [int(x) for x in args.seq_samples.split(",") if x and int(x) <= n]
+        if samples:
+            out["cpu_baseline"] = cpu_baseline(ctx, args.cfg, addr, vals, voff, samples)
+        if not args.no_cpu_batch:
+            out["cpu_batch_allcore"] = cpu_batch(addr, vals, voff, n, root, cpu_threads(args.cpu_threads))
+            out["parity"] = {"full_size_root_vs_cpu_batch": "equal"}
     print(json.dumps(out), flush=True)
+
+
+def relaunch(args):
+    """`bench.py --gpus N` without a launcher: start torch.distributed.run as a child (no
+    GPU call has been made in this process) and exit with its status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 or args.gpus > 1 or args.sharded:
         from khipu_amd import sharded

@@ -751,6 +751,10 @@ __global__ void __launch_bounds__(BS) k_synth_write(uint32_t cfg, uint64_t first
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }  // a throw between ensure() and release() does not leak HBM
   void ensure(size_t bytes) {
     if (bytes <= cap) return;
     if (p) HIPCHK(hipFree(p));
@@ -1802,6 +1806,8 @@ static int emit_node_set(kh_ctx* c, uint8_t* hashes32, uint64_t node_cap, uint8_
   Topo& T = c->T;
   uint64_t B = c->last_B;
   uint64_t Q = T.m + 2 * B;
+  // node counts and positions are scanned as uint32
+  if (Q >= (1ULL << 32)) throw KhError{KH_EINVAL, "node set too large to emit in one call (>= 2^32 candidates)"};
   c->ws3.ensure(carve_size({Q * 4, Q * 8, Q * 8 + 64}));
   Carver c3{(char*)c->ws3.p, 0, c->ws3.cap};
   uint32_t* flag = c3.take<uint32_t>(Q);

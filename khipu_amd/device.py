@@ -109,6 +109,7 @@ class ResidentTrie:
         self.ctx = ctx
         self.dev = f"cuda:{ctx.device}"
         self.h = None
+        self.hash_keys = bool(hash_keys)  # every commit hashes its keys the same way
         klen = len(keys[0]) if keys else 32
         kd, _ = _pack_dev(list(keys), self.dev)
         vd, vo = _pack_dev(list(vals), self.dev)
@@ -124,7 +125,17 @@ class ResidentTrie:
         self.h = h
         self.root = root.tobytes()
 
-    def commit(self, upserts=(), deletes=(), hash_keys=False, stats=None):
+    def _flag(self, hash_keys):
+        """The trie's key encoder is fixed at open (as the reference's implicit
+        ByteArrayEncoder[K] is per trie type): None means that one; a different value raises."""
+        if hash_keys is None:
+            return self.hash_keys
+        if bool(hash_keys) != self.hash_keys:
+            raise _lib.MPTException(_lib.KH_EINVAL, f"trie opened with hash_keys={self.hash_keys}, commit asked "
+                                                    f"for hash_keys={bool(hash_keys)}")
+        return self.hash_keys
+
+    def commit(self, upserts=(), deletes=(), hash_keys=None, stats=None):
         """Apply {key: value} upserts, then deletes; returns the new root."""
         ups = list(upserts.items()) if isinstance(upserts, dict) else list(upserts)
         dels = list(deletes)
@@ -134,10 +145,10 @@ class ResidentTrie:
         dk, _ = _pack_dev(dels, self.dev)
         return self.commit_dev(uk, uv, uo, len(ups), dk, len(dels), klen, hash_keys, stats)
 
-    def commit_dev(self, up_keys, up_vals, up_voff, nup, del_keys, ndel, klen=32, hash_keys=False, stats=None):
+    def commit_dev(self, up_keys, up_vals, up_voff, nup, del_keys, ndel, klen=32, hash_keys=None, stats=None):
         root = np.zeros(32, np.uint8)
         st = stats if stats is not None else KhStats()
-        flags = _lib.KH_HASH_KEYS if hash_keys else 0
+        flags = _lib.KH_HASH_KEYS if self._flag(hash_keys) else 0
         self.ctx._sync()
         check(lib().kh_trie_apply(self.h, _ptr(up_keys), _ptr(up_vals), _ptr(up_voff), nup, _ptr(del_keys), ndel,
                                   klen, flags, root.ctypes.data, ctypes.byref(st)))

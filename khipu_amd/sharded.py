@@ -244,6 +244,18 @@ def bench_main(args):
     dist.all_reduce(hashes)
     dt = float(dt.item())
     node_hashes = int(hashes[0].item()) + 1  # + the folded root branch
+    # roofline of the dominant kernel (k_leaf_fused, one launch per rank per step), on the
+    # slowest rank: its HIP-event time on the library's stream
+    leaf = torch.tensor([st.t_leaf_ms, float(st.n_leaves)], dtype=torch.float64, device=f"cuda:{local}")
+    leaf_all = [torch.zeros_like(leaf) for _ in range(world)]
+    dist.all_gather(leaf_all, leaf)
+    leaf_all = [x.tolist() for x in leaf_all]
+    slow = max(leaf_all, key=lambda x: x[0])
+    VALU_PEAK, OPS = 256 * 4 * 32 * 2.4e9, 5760
+    achieved = slow[1] * OPS / max(slow[0] * 1e-3, 1e-12)
+    roof = {"kernel": "k_leaf_fused", "bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK / 1e12,
+            "unit": "T int32-lane-ops/s", "frac": achieved / VALU_PEAK, "traffic": None, "avg_ms": slow[0],
+            "perms_per_launch": int(slow[1]), "rank": "slowest of the ranks"}
     # one more (untimed) step with a device sync after every phase: where the time goes
     phases = {}
     sharded_root(be, addr, vals, voff, n, phases=phases)
@@ -264,9 +276,17 @@ def bench_main(args):
                          "n_node_hashes": node_hashes},
             "phase_ms_max_over_ranks": phases,
             "per_rank_build_ms": st.t_total_ms,
-            "roofline": None,
-            "cpu_baseline": None,
+            "roofline": roof,
         }
+        if not getattr(args, "no_cpu", False):
+            # the khipu-faithful sequential CPU trie on prefixes of rank 0's slice (its first
+            # accounts are the workload's first accounts), asserted against this GPU's root of
+            # the same prefix; the full-size all-core CPU root check runs in the N = 1 line
+            import bench
+            samples = [int(x) for x in str(getattr(args, "seq_samples", "20000,50000")).split(",")
+                       if x and int(x) <= min(n, 50_000)]
+            if samples:
+                out["cpu_baseline"] = bench.cpu_baseline(be.ctx, args.cfg, addr, vals, voff, samples)
         print(json.dumps(out), flush=True)
     dist.barrier()
     dist.destroy_process_group()

@@ -22,8 +22,9 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
-                os.path.join(_HERE, "khipu_oracle.cc")):
+        srcs = [os.path.join(_HERE, f) for f in ("khipu_oracle.cc", "batch_root.cc")]
+        if not os.path.exists(_LIB_PATH) or any(os.path.exists(s) and os.path.getmtime(_LIB_PATH) < os.path.getmtime(s)
+                                                for s in srcs):
             build()
         L = ctypes.CDLL(_LIB_PATH)
         u8p = ctypes.c_char_p
@@ -57,6 +58,10 @@ def lib():
         L.or_node_children.restype = ctypes.c_int
         L.or_seq_root.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+        vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+        L.or_batch_roots.argtypes = [vp, vp, u64, vp, vp, u64, vp, u64, ctypes.c_int, ctypes.c_int, vp, vp]
+        L.or_batch_last_error.restype = ctypes.c_char_p
+        L.or_batch_kec256.argtypes = [u8p, u64, vp]
         _lib = L
     return _lib
 
@@ -198,6 +203,68 @@ def seq_root_packed(keys_u8, klen, vals_u8, voff_u64, n, mode=0) -> bytes:
     rc = lib().or_seq_root(keys_u8.ctypes.data, klen, vals_u8.ctypes.data, voff_u64.ctypes.data, None, n, mode, out)
     if rc != 0:
         raise OracleError(lib().or_last_error().decode())
+    return out.raw
+
+
+BATCH_STATS = ("leaves", "branches", "extensions", "node_hashes", "node_perms", "key_perms", "inline", "distinct")
+
+
+def _np_u8(x):
+    import numpy as np
+    if isinstance(x, (bytes, bytearray)):
+        return np.frombuffer(bytes(x) + b"\0" * 8, np.uint8)
+    return np.ascontiguousarray(x, dtype=np.uint8).reshape(-1)
+
+
+def batch_roots(keys, vals, klen=None, seg_off=None, hash_keys=False, nthreads=None):
+    """Independent multi-threaded batch builder (oracle/batch_root.cc): roots of the
+    tries holding put(keys[i], vals[i]) in order (later puts win).
+
+    keys: list of bytes (any lengths: list tries), or a uint8 array of n*klen;
+    vals: list of bytes, or (uint8 array, uint64 offsets[n+1]);
+    seg_off: None (one trie) or offsets[nseg+1] from 0 to n (many independent tries).
+    Returns (list of 32-byte roots, stats dict)."""
+    import numpy as np
+    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    koff = None
+    if isinstance(keys, np.ndarray):
+        kb = _np_u8(keys)
+        n = kb.size // klen
+    else:
+        keys = list(keys)
+        n = len(keys)
+        kb = _np_u8(b"".join(keys))
+        lens = {len(k) for k in keys}
+        if len(lens) > 1 or klen is None:
+            koff = np.zeros(n + 1, np.uint64)
+            koff[1:] = np.cumsum([len(k) for k in keys])
+            klen = 0
+    if isinstance(vals, tuple):
+        vb, voff = _np_u8(vals[0]), np.ascontiguousarray(vals[1], dtype=np.uint64)
+    else:
+        vals = list(vals)
+        vb = _np_u8(b"".join(vals))
+        voff = np.zeros(len(vals) + 1, np.uint64)
+        voff[1:] = np.cumsum([len(v) for v in vals])
+    so = None if seg_off is None else np.ascontiguousarray(seg_off, dtype=np.uint64)
+    nseg = 1 if so is None else len(so) - 1
+    roots = np.zeros(32 * max(nseg, 1), np.uint8)
+    st = np.zeros(8, np.uint64)
+    rc = lib().or_batch_roots(kb.ctypes.data, None if koff is None else koff.ctypes.data, klen or 0, vb.ctypes.data,
+                              voff.ctypes.data, n, None if so is None else so.ctypes.data, nseg,
+                              1 if hash_keys else 0, nthreads, roots.ctypes.data, st.ctypes.data)
+    if rc != 0:
+        raise OracleError(lib().or_batch_last_error().decode())
+    return [roots[32 * i:32 * i + 32].tobytes() for i in range(nseg)], dict(zip(BATCH_STATS, map(int, st)))
+
+
+def batch_root(keys, vals, **kw) -> bytes:
+    return batch_roots(keys, vals, **kw)[0][0]
+
+
+def batch_kec256(data: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().or_batch_kec256(data, len(data), out)
     return out.raw
 
 

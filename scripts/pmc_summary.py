@@ -19,8 +19,6 @@ out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else N
 args = [a for a in sys.argv[1:] if not a.startswith("--") and a != out_json]
 tag = args[0] if args else "pmc"
 builds = int(args[1]) if len(args) > 1 else 2
-if out_json in args:
-    args.remove(out_json)
 
 def kname(full):
     """'void khst::k_scan_tiles<unsigned int>(...)' -> 'k_scan_tiles' (template instances merge)"""

@@ -221,3 +221,38 @@ def mutate(r, b):
     elif b:
         b[r.randrange(min(len(b), 4))] = r.randrange(256)  # header bytes
     return bytes(b)
+
+
+def list_key(i):
+    """MptListValidator.intByteArraySerializable.toBytes: rlp.encode(i: Int)
+    (MptListValidator.scala:15-18, RLPImplicits.scala:40-41, RLP.scala:238-276): 0 -> 0x80."""
+    return codec.storage_value_rlp(i)
+
+
+def list_cases(seed=41):
+    """List tries (transactions / receipts roots): keys rlp(0..n-1) of
+    1-3 bytes (the 127/128 and 255/256 index boundaries), item bytes from 1 to 300 B so
+    short items give inline leaves."""
+    r = random.Random(seed)
+    out = []
+    for n in [1, 2, 3, 16, 17, 127, 128, 129, 200, 256, 257, 1000]:
+        vals = [bytes(r.getrandbits(8) for _ in range(r.choice([1, 2, 20, 60, 110, 200, 300]))) for _ in range(n)]
+        out.append((f"list{n}", [list_key(i) for i in range(n)], vals))
+    return out
+
+
+def prefix_key_cases(seed=43):
+    """Arbitrary-length keys where one key is a prefix of another: the shorter key's value
+    sits in the branch's 17th slot (Node.scala:31-40, MerklePatriciaTrie.scala:207-214,263-267)."""
+    r = random.Random(seed)
+    out = []
+    base = bytes(r.getrandbits(8) for _ in range(6))
+    ks = [base[:2], base[:4], base[:4] + b"\x01", base[:4] + b"\x10", base, base[:3], b"\x00", b"\xff\xfe"]
+    out.append(("prefix_small", ks, [bytes([i + 1]) * (i * 9 + 1) for i in range(len(ks))]))
+    ks = []
+    for _ in range(300):
+        L = r.choice([1, 2, 3, 4, 8])
+        ks.append(base[:r.randrange(0, 3)] + bytes(r.getrandbits(8) & 0x11 for _ in range(L)))
+    ks = [k for k in dict.fromkeys(ks) if k]
+    out.append(("prefix_random", ks, [storage_value(r) for _ in ks]))
+    return out

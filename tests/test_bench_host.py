@@ -29,3 +29,23 @@ def test_pmc_summary_json_arg(tmp_path):
     r = subprocess.run([sys.executable, "scripts/pmc_summary.py", "no_such_tag", "--json", str(out)],
                        cwd=ROOT, capture_output=True, text=True, timeout=60)
     assert "invalid literal" not in r.stderr
+    assert r.returncode == 0, r.stderr
+    with open(out) as fh:
+        assert "kernels" in json.load(fh)
+
+
+def test_pmc_round_order():
+    """Newest summary by round number, not by file-name string order (r10a after r2a)."""
+    names = ["profiles/r1l_pmc_traffic_5.json", "profiles/r10a_pmc_traffic_5.json", "profiles/r2b_pmc_traffic_5.json",
+             "profiles/r2a_pmc_traffic_5.json"]
+    assert sorted(names, key=bench.round_key)[-1].endswith("r10a_pmc_traffic_5.json")
+    assert sorted(names, key=bench.round_key)[0].endswith("r1l_pmc_traffic_5.json")
+
+
+def test_extrapolation_fit():
+    """us/put = a + b*log16(n) through exact samples recovers a and b."""
+    import math
+    a, b = 3.0, 4.0
+    samples = [(n, n * (a + b * math.log(n, 16)) * 1e-6) for n in (20000, 50000, 100000)]
+    fa, fb = bench.fit_put_cost(samples)
+    assert abs(fa - a) < 1e-6 and abs(fb - b) < 1e-6

@@ -1,0 +1,56 @@
+"""BASELINE.json configs at their configured shapes on the GPU, checked against the
+independent CPU batch builder (oracle/batch_root.cc) for every root and against the
+khipu-faithful sequential oracle on sampled tries."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def storage_tries(rng, ntries, lo=1, hi=10_000):
+    """configs[3]: ntries contract storage tries, slot counts log-uniform in [lo, hi]; slot
+    key = kec256(32-byte big-endian slot index) (hashDataWordSerializable,
+    trie/package.scala:34-36) -> raw 32-byte keys hashed on the device; value =
+    RLP(trimmed 1-32 random bytes) (rlpDataWordSerializer, trie/package.scala:28-32), so
+    1-byte values < 0x80 (inline leaves) occur."""
+    cnt = np.exp(rng.uniform(np.log(lo), np.log(hi + 1), ntries)).astype(np.int64).clip(lo, hi)
+    seg_off = np.zeros(ntries + 1, np.uint64)
+    seg_off[1:] = np.cumsum(cnt)
+    n = int(seg_off[-1])
+    keys = np.zeros((n, 32), np.uint8)
+    keys[:, 24:] = rng.integers(0, 1 << 20, n, dtype=np.uint64).astype(">u8").view(np.uint8).reshape(n, 8)
+    vlen = rng.integers(1, 33, n)
+    first = rng.integers(1, 256, n).astype(np.uint8)  # trimmed: no leading zero byte
+    raw1 = (vlen == 1) & (first < 0x80)
+    enc_len = np.where(raw1, 1, vlen + 1)
+    voff = np.zeros(n + 1, np.uint64)
+    voff[1:] = np.cumsum(enc_len)
+    vb = rng.integers(0, 256, int(voff[-1]) + 8, dtype=np.uint8)
+    st = voff[:-1].astype(np.int64)
+    vb[st[~raw1]] = (0x80 + vlen[~raw1]).astype(np.uint8)
+    vb[st[~raw1] + 1] = first[~raw1]
+    vb[st[raw1]] = first[raw1]
+    return keys.reshape(-1), vb, voff, seg_off
+
+
+def test_config3_100k_storage_tries(khst, oracle):
+    import torch
+    from khipu_amd.device import Ctx
+    rng = np.random.default_rng(3)
+    ntries = 100_000
+    keys, vb, voff, seg_off = storage_tries(rng, ntries)
+    n = int(seg_off[-1])
+    seg = np.repeat(np.arange(ntries, dtype=np.uint32), np.diff(seg_off).astype(np.int64))
+    ctx = Ctx(0)
+    dk, dv, do, ds = (torch.from_numpy(x).to("cuda:0") for x in (keys, vb, voff.astype(np.int64), seg))
+    hh, ll, ii, st = ctx.build(dk, 32, dv, do, n, seg=ds, nseg=ntries, hash_keys=True)
+    gpu = [hh[s].tobytes() if ll[s] else khst.EMPTY_TRIE_HASH for s in range(ntries)]
+    cpu, cst = oracle.batch_roots(keys, (vb, voff), klen=32, seg_off=seg_off, hash_keys=True)
+    assert gpu == cpu
+    assert st.n_leaves == cst["distinct"] and st.n_node_hashes == cst["node_hashes"]
+    # 17-bit segment prefix in the sort key; sampled tries against the sequential oracle
+    for s in rng.choice(ntries, 12, replace=False):
+        a, b = int(seg_off[s]), int(seg_off[s + 1])
+        ks = [oracle.kec256(keys[32 * i:32 * i + 32].tobytes()) for i in range(a, b)]
+        vs = [vb[int(voff[i]):int(voff[i + 1])].tobytes() for i in range(a, b)]
+        assert gpu[s] == oracle.seq_root(ks, vs), s

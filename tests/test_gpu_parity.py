@@ -169,6 +169,10 @@ def test_full_size_1m(khst, oracle):
     vo = voff.cpu().numpy().astype(np.uint64)
     vb = vals[:int(vo[n])].cpu().numpy()
     assert root == oracle.seq_root_packed(keys, 32, vb, vo, n)
+    # the independent all-core batch builder (the full-size check bench.py uses at 100M)
+    roots, bst = oracle.batch_roots(a.reshape(-1), (vb, vo), klen=20, hash_keys=True)
+    assert roots[0] == root
+    assert (bst["leaves"], bst["node_hashes"], bst["node_perms"]) == (st.n_leaves, st.n_node_hashes, st.n_node_perms)
     # input-order invariance: the same puts in reverse order give the same root
     lens = np.diff(vo)[::-1].astype(np.int64)
     new_off = np.zeros(n + 1, np.uint64)
