@@ -109,13 +109,13 @@ class ResidentTrie:
         self.ctx = ctx
         self.dev = f"cuda:{ctx.device}"
         self.h = None
-        self.hash_keys = bool(hash_keys)  # every commit hashes its keys the same way
         klen = len(keys[0]) if keys else 32
         kd, _ = _pack_dev(list(keys), self.dev)
         vd, vo = _pack_dev(list(vals), self.dev)
         self._open(kd, klen, vd, vo, len(keys), hash_keys)
 
     def _open(self, kd, klen, vd, vo, n, hash_keys):
+        self.hash_keys = bool(hash_keys)  # every commit hashes its keys the same way
         h = ctypes.c_void_p()
         root = np.zeros(32, np.uint8)
         flags = _lib.KH_HASH_KEYS if hash_keys else 0

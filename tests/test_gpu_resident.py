@@ -41,6 +41,27 @@ def test_commit_hash_keys(khst, oracle):
     assert got == want[1]
 
 
+def test_commit_uses_open_hash_keys(khst, oracle):
+    """A storage trie opened with hash_keys=True hashes 32-byte slot keys on every commit
+    without repeating the flag (the flag used to default to False); asking for
+    the other encoder raises."""
+    from khipu_amd.device import Ctx, ResidentTrie
+    from khipu_amd._lib import MPTException
+    r = random.Random(12)
+    slots = [bytes(r.getrandbits(8) for _ in range(32)) for _ in range(300)]
+    vals = [C.storage_value(r) for _ in slots]
+    t = ResidentTrie(Ctx(0), slots, vals, hash_keys=True)
+    ups = [(s, C.storage_value(r)) for s in r.sample(slots, 30)] + [
+        (bytes(r.getrandbits(8) for _ in range(32)), b"\x07") for _ in range(5)]
+    dels = r.sample(slots, 10)
+    got = t.commit(ups, dels)
+    want = C.oracle_commits(oracle, [oracle.kec256(s) for s in slots], vals,
+                            [([(oracle.kec256(s), v) for s, v in ups], [oracle.kec256(s) for s in dels])])
+    assert got == want[1]
+    with pytest.raises(MPTException):
+        t.commit(ups[:1], [], hash_keys=False)
+
+
 def test_commit_1m_vs_full_build(khst):
     """configs[2]-style commit at 1M accounts: 20k dirty (90% updates, 5% inserts, 5%
     deletes) -> the root of a from-scratch build of the final set; only the changed
