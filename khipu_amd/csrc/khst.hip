@@ -557,6 +557,26 @@ __global__ void __launch_bounds__(BS) k_branch_hash(Topo T, uint64_t first, uint
   block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
 }
 
+// Fused per-level branch kernel (root-only and incremental builds; row N1): each thread
+// streams its branch's encoding block by block through its own 17-word LDS slot into
+// the Keccak state (op_branch_fused), so no branch RLP is written to or read back from
+// HBM: the level reads its contiguous child records once and writes one 34-byte
+// reference per node.  Slot layout [thread][word]: a wave's 8-byte slot accesses are
+// bank-conflict-free within each 16-lane group (stride 34 dwords).
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8))) k_branch_fused(Topo T, uint64_t first, uint64_t cnt) {
+  __shared__ uint64_t slots[BS * LEAF_WORDS];
+  uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  unsigned long long perms = 0, hashes = 0, inl = 0;
+  if (t < cnt) {
+    uint32_t j = (uint32_t)(first + t);
+    uint32_t in1 = 0;
+    perms = op_branch_fused(T, j, slots + threadIdx.x * LEAF_WORDS, 1, &in1);
+    hashes = branch_hash_count(T, j, (uint32_t)perms);
+    inl = in1;
+  }
+  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
+}
+
 // write-back emission: node q in [0, m + 2B): leaf q, or branch / extension of branch (q-m)/2.
 // src/stride: the node's message words (stride m for one-block leaves, 1 otherwise).
 __device__ __forceinline__ bool emit_node(const Topo& T, uint64_t B, uint64_t q, const uint64_t** src,
@@ -1219,16 +1239,17 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // leaf encodings are kept (transposed message slots) only when the node set is emitted
   const uint64_t lmsg_words = A.emit ? (uint64_t)LEAF_WORDS * m : 0;
   const bool inc_dirty = A.inc && A.inc->dkey;
-  c->ws2.ensure(carve_size({C * 32, C * 2, lmsg_words * 8, lf_bytes + 64, (uint64_t)BR_WORDS * 8 * B,
-                            (uint64_t)EXT_WORDS * 8 * B, inc_dirty ? B : 0}));
+  const uint64_t bmsg_words = A.emit ? (uint64_t)BR_WORDS * B : 0, xmsg_words = A.emit ? (uint64_t)EXT_WORDS * B : 0;
+  c->ws2.ensure(carve_size({C * 32, C * 2, lmsg_words * 8, lf_bytes + 64, bmsg_words * 8, xmsg_words * 8,
+                            inc_dirty ? B : 0}));
   Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
   T.cref = cv2.take<uint64_t>(C * 4);
   T.cmeta = cv2.take<uint16_t>(C);
   T.lmsg = A.emit ? cv2.take<uint64_t>(lmsg_words) : nullptr;
   T.lstride = m;
   T.arena = cv2.take<uint8_t>(lf_bytes + 64);  // long leaves
-  T.bmsg = cv2.take<uint64_t>((uint64_t)BR_WORDS * B);
-  T.xmsg = cv2.take<uint64_t>((uint64_t)EXT_WORDS * B);
+  T.bmsg = A.emit ? cv2.take<uint64_t>(bmsg_words) : nullptr;
+  T.xmsg = A.emit ? cv2.take<uint64_t>(xmsg_words) : nullptr;
   T.lb = lb;
   if (A.inc) {
     IncArgs& I = *A.inc;
@@ -1283,9 +1304,13 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   for (int d = 63; d >= 0; --d) {
     uint32_t cnt = lbh[d + 1] - lbh[d];
     if (!cnt) continue;
-    hipLaunchKernelGGL(k_branch_prep, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_branch_hash, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+    if (A.emit) {  // the write-back build keeps every encoding in its message slot for emission
+      hipLaunchKernelGGL(k_branch_prep, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+      LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_branch_hash, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+    } else {
+      hipLaunchKernelGGL(k_branch_fused, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+    }
     LAUNCH_CHECK();
     ++levels;
   }
@@ -1329,7 +1354,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     stats->n_inline = c->h_pinned[CTR_INLINE];
     stats->n_extensions = c->h_pinned[CTR_EXT];
     stats->n_key_perms = (A.flags & KH_HASH_KEYS) ? n * (uint64_t)(A.klen / 136 + 1) : 0;
-    stats->arena_bytes = (uint64_t)LEAF_WORDS * 8 * m + lf_bytes + (uint64_t)(BR_WORDS + EXT_WORDS) * 8 * B;
+    stats->arena_bytes = lmsg_words * 8 + lf_bytes + (bmsg_words + xmsg_words) * 8;  // node RLP kept in HBM
     stats->n_levels = levels;
     stats->full_sort = ties ? 1 : 0;
     stats->t_keys_ms = ev_ms(c->ev[0], c->ev[1]);

@@ -537,7 +537,8 @@ KH_HD void slot_head(const Slot& sl, uint32_t L, uint64_t head[4]) {
   for (int q = 0; q < 4; ++q) head[q] = (8u * q < L) ? sl.w[q * sl.stride] : 0;
 }
 
-KH_HD void bw_ref(BW& w, const uint64_t r[4], uint32_t len) {  // child reference: 0xa0+hash or inline bytes
+template <typename W>
+KH_HD void bw_ref(W& w, const uint64_t r[4], uint32_t len) {  // child reference: 0xa0+hash or inline bytes
   if (len == 32) {
     w.put1(0xA0);
     w.put(r[0], 8);
@@ -658,23 +659,12 @@ KH_HD void leaf_reuse(const Topo& T, uint64_t i, int state, uint32_t* inl) {
   publish_ref(T, parent, T.lf_pord[i], leaf_nibble(T, i), i, r, L, r);
 }
 
-// hash + publish of leaf i whose encoding (L bytes) sits at w, words `stride` apart
-KH_HD uint32_t leaf_hash_at(const Topo& T, uint64_t i, const uint64_t* w, uint64_t stride, uint32_t L,
-                            uint32_t* inl) {
+// publish of leaf i after hashing: hh = its hash (zero if not hashed: L < 32 and not the
+// top), head = its first 4 message words (the inline reference when L < 32)
+KH_HD void leaf_publish_at(const Topo& T, uint64_t i, uint32_t L, const uint64_t hh[4], const uint64_t head[4],
+                           uint32_t* inl) {
   uint32_t parent = T.lf_parent[i];
   bool top = parent == NONE;
-  uint64_t hh[4] = {0, 0, 0, 0}, head[4];
-  uint32_t perms = 0;
-  if (L <= LEAF_SHORT_MAX) {
-    if (L >= 32 || top) {
-      kec256_strided(w, stride, L, hh);
-      perms = 1;
-    }
-    for (int q = 0; q < 4; ++q) head[q] = (8u * q < L) ? w[q * stride] : 0;
-  } else {
-    perms = hash_node(w, L, top, hh);
-    for (int q = 0; q < 4; ++q) head[q] = w[q];
-  }
   if (T.lf_hash)
     for (int j = 0; j < 4; ++j) T.lf_hash[4 * i + j] = hh[j];
   if (T.lf_ref) {  // capped reference, for the next incremental commit
@@ -688,6 +678,25 @@ KH_HD uint32_t leaf_hash_at(const Topo& T, uint64_t i, const uint64_t* w, uint64
   uint32_t nib = top ? 0 : leaf_nibble(T, i);
   publish_ref(T, parent, T.lf_pord[i], nib, i, head, L, hh);
   *inl = (L < 32 && !top) ? 1 : 0;
+}
+
+// hash + publish of leaf i whose encoding (L bytes) sits at w, words `stride` apart
+KH_HD uint32_t leaf_hash_at(const Topo& T, uint64_t i, const uint64_t* w, uint64_t stride, uint32_t L,
+                            uint32_t* inl) {
+  bool top = T.lf_parent[i] == NONE;
+  uint64_t hh[4] = {0, 0, 0, 0}, head[4];
+  uint32_t perms = 0;
+  if (L <= LEAF_SHORT_MAX) {
+    if (L >= 32 || top) {
+      kec256_strided(w, stride, L, hh);
+      perms = 1;
+    }
+    for (int q = 0; q < 4; ++q) head[q] = (8u * q < L) ? w[q * stride] : 0;
+  } else {
+    perms = hash_node(w, L, top, hh);
+    for (int q = 0; q < 4; ++q) head[q] = w[q];
+  }
+  leaf_publish_at(T, i, L, hh, head, inl);
   return perms;
 }
 
@@ -714,6 +723,20 @@ KH_HD int32_t leaf_pd_early(const Topo& T, uint64_t i) {
 // branch topology is computed; the reference is stashed per leaf and
 // op_leaf_topo_early moves it into the parent's child record.  A top leaf (both
 // boundaries 0) publishes its result here.  One-block leaf at w, L bytes:
+KH_HD void leaf_publish_early(const Topo& T, uint64_t i, bool top, uint32_t L, const uint64_t hh[4],
+                              const uint64_t head[4], uint32_t* inl) {
+  *inl = 0;
+  if (top) {
+    publish_ref(T, NONE, 0, 0, i, head, L, hh);
+    return;
+  }
+  for (int q = 0; q < 4; ++q) {
+    uint32_t base = 8u * (uint32_t)q;
+    T.lf_eref[4 * i + q] = L >= 32 ? hh[q] : (base < L ? head[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0);
+  }
+  T.lf_emeta[i] = (uint8_t)(L >= 32 ? 32 : L);
+  *inl = L < 32 ? 1 : 0;
+}
 KH_HD uint32_t leaf_hash_early(const Topo& T, uint64_t i, bool top, const uint64_t* w, uint64_t stride, uint32_t L,
                                uint32_t* inl) {
   uint64_t hh[4] = {0, 0, 0, 0}, head[4];
@@ -723,17 +746,7 @@ KH_HD uint32_t leaf_hash_early(const Topo& T, uint64_t i, bool top, const uint64
     perms = 1;
   }
   for (int q = 0; q < 4; ++q) head[q] = (8u * q < L) ? w[q * stride] : 0;
-  *inl = 0;
-  if (top) {
-    publish_ref(T, NONE, 0, 0, i, head, L, hh);
-    return perms;
-  }
-  for (int q = 0; q < 4; ++q) {
-    uint32_t base = 8u * (uint32_t)q;
-    T.lf_eref[4 * i + q] = L >= 32 ? hh[q] : (base < L ? head[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0);
-  }
-  T.lf_emeta[i] = (uint8_t)(L >= 32 ? 32 : L);
-  *inl = L < 32 ? 1 : 0;
+  leaf_publish_early(T, i, top, L, hh, head, inl);
   return perms;
 }
 // after the branch topology: the stashed reference goes to the parent's child
@@ -765,21 +778,24 @@ KH_HD uint32_t op_leaf_long(const Topo& T, uint64_t i, uint32_t* inl) {
   return leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, T.lf_len[i], inl);
 }
 
-// ---- branch prep: [ref_0 .. ref_15, ""] into its message slot (thread per branch of
-// one level; g = its position in the level order)
-KH_HD void op_branch_prep(const Topo& T, uint32_t j, uint64_t g) {
-  if (T.br_dirty && !T.br_dirty[j]) return;  // clean: reference from the previous version
+// ---- branch encoding [ref_0 .. ref_15, ""] (Node.scala:31-40): payload length from the
+// child records' meta, then the byte stream into any writer (BW: a whole message
+// slot; WinBW: one 136-byte Keccak block of it)
+KH_HD uint32_t branch_payload(const Topo& T, uint32_t j) {
   uint32_t k = T.br_k[j];
-  uint64_t cb = T.br_cbase[j];
-  const uint16_t* cm = T.cmeta + cb;
+  const uint16_t* cm = T.cmeta + T.br_cbase[j];
   uint32_t payload = 1 + (16 - k);  // terminator "" + empty slots
   for (uint32_t c = 0; c < k; ++c) {
     uint32_t len = cm[c] & 0xFF;
     payload += (len == 32) ? 33 : len;
   }
-  Slot sl = branch_slot(T, g, T.br_depth[j], false);
-  T.br_aoff[j] = g;
-  BW w(sl.w, sl.stride);
+  return payload;
+}
+template <typename W>
+KH_HD void branch_stream(const Topo& T, uint32_t j, W& w, uint32_t payload) {
+  uint32_t k = T.br_k[j];
+  uint64_t cb = T.br_cbase[j];
+  const uint16_t* cm = T.cmeta + cb;
   w.len_prefix(payload, 0xC0);
   const uint64_t* cr = T.cref + 4 * cb;
   int32_t prev = -1;
@@ -793,53 +809,78 @@ KH_HD void op_branch_prep(const Topo& T, uint32_t j, uint64_t g) {
   }
   for (int32_t e = prev + 1; e < 16; ++e) w.put1(0x80);
   w.put1(0x80);  // terminator (a secure trie never stores a value in a branch)
+}
+
+// ---- branch prep: the whole encoding into its message slot (thread per branch of one
+// level; g = its position in the level order).  The write-back build keeps it there.
+KH_HD void op_branch_prep(const Topo& T, uint32_t j, uint64_t g) {
+  if (T.br_dirty && !T.br_dirty[j]) return;  // clean: reference from the previous version
+  uint32_t payload = branch_payload(T, j);
+  Slot sl = branch_slot(T, g, T.br_depth[j], false);
+  T.br_aoff[j] = g;
+  BW w(sl.w, sl.stride);
+  branch_stream(T, j, w, payload);
   w.flush();
   T.br_len[j] = rlp_hdr_len(payload) + payload;
 }
 
-// ---- branch hash (+ extension encode + hash) (thread per branch of one level)
-KH_HD uint32_t op_branch_hash(const Topo& T, uint32_t j, uint64_t g, uint32_t* inl) {
+// Windowed writer: of a byte stream written from position 0, only bytes [w0, w0 + 136)
+// (one Keccak block; w0 is a multiple of 136, so 8-aligned) land in the 17-word slot.
+struct WinBW {
+  BW w;
+  uint32_t pos, w0;  // branch encodings are < 600 B
+  KH_HD WinBW(uint64_t* d, uint64_t s, uint32_t win0) : w(d, s), pos(0), w0(win0) {}
+  KH_HD void put(uint64_t x, uint32_t nb) {
+    const uint32_t e = pos + nb;
+    if (e > w0 && pos < w0 + 136) {
+      if (pos < w0) {
+        const uint32_t d = (uint32_t)(w0 - pos);
+        x >>= 8 * d;
+        nb -= d;
+        pos = w0;
+      }
+      if (pos + nb > w0 + 136) nb = (uint32_t)(w0 + 136 - pos);
+      w.put(x, nb);
+    }
+    pos = e;
+  }
+  KH_HD void put1(uint32_t b) { put(b, 1); }
+  KH_HD void flush() { w.flush(); }
+  KH_HD void len_prefix(uint64_t len, uint32_t offset) {
+    if (len < 56) {
+      put1((uint32_t)(len + offset));
+    } else {
+      uint32_t nb = be_nbytes(len);
+      put1(nb + offset + 55);
+      for (int i = (int)nb - 1; i >= 0; --i) put1((uint32_t)(len >> (8 * i)) & 0xFF);
+    }
+  }
+  KH_HD void words(const uint64_t* wd, uint32_t n) {
+    for (int j = 0; j < 4 && n; ++j) {
+      uint32_t nb = n < 8 ? n : 8;
+      put(wd[j], nb);
+      n -= nb;
+    }
+  }
+};
+
+// ---- extension (if any) + publish of branch j whose reference is (L, hb, bhead): an
+// extension [HP(nibbles pd+1 .. d-1, ext), ref(branch)] is encoded into xs and hashed.
+// Returns the permutations spent on the extension; *ninl counts inline nodes.
+KH_HD uint32_t branch_publish(const Topo& T, uint32_t j, uint32_t L, const uint64_t hb[4], const uint64_t bhead[4],
+                              Slot xs, uint32_t* ninl) {
   uint32_t ext = T.br_ext[j];
   uint32_t parent = T.br_parent[j];
   uint64_t first = T.br_first[j];
   uint32_t d = T.br_depth[j];
   int32_t pd = (int32_t)d - (int32_t)ext - 1;
   bool top = parent == NONE;
-  *inl = 0;
-  uint64_t hb[4], bhead[4];
-  uint32_t L, perms = 0, ninl = 0;
-  if (T.br_dirty && !T.br_dirty[j]) {
-    // clean: the node is unchanged; only its reference (and extension) is needed,
-    // and only by a dirty parent
-    if (under_clean(T, parent)) return 0;
-    L = T.br_rlen[j];
-    for (int q = 0; q < 4; ++q) bhead[q] = hb[q] = T.br_ref[4 * j + q];
-  } else {
-    L = T.br_len[j];
-    Slot sl = branch_slot(T, g, d, false);
-    perms = hash_slot(sl, L, top && ext == 0, hb);
-    slot_head(sl, L, bhead);
-    ninl = (L < 32 && !(top && ext == 0)) ? 1 : 0;
-    if (T.br_hash)
-      for (int q = 0; q < 4; ++q) T.br_hash[4 * j + q] = hb[q];
-    if (T.br_ref) {  // capped reference, for the next incremental commit
-      for (int q = 0; q < 4; ++q) {
-        uint32_t base = 8u * (uint32_t)q;
-        T.br_ref[4 * j + q] =
-            L >= 32 ? hb[q] : (base < L ? bhead[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0);
-      }
-      T.br_rlen[j] = L;
-    }
-  }
   Key4 key = load_key(T.skey, first);
   uint32_t nib = top ? 0 : key_nibble(key, pd);
   if (ext == 0) {
     publish_ref(T, parent, T.br_pord[j], nib, first, bhead, L, hb);
-    *inl = ninl;
-    return perms;
+    return 0;
   }
-  // extension: [HP(nibbles pd+1 .. d-1, ext), ref(branch)] in its own slot
-  Slot xs = branch_slot(T, g, d, true);
   uint32_t s = (uint32_t)(pd + 1);
   uint32_t hl = ext / 2 + 1;  // HP bytes
   uint32_t refl = L >= 32 ? 33 : L;
@@ -863,12 +904,111 @@ KH_HD uint32_t op_branch_hash(const Topo& T, uint32_t j, uint64_t g, uint32_t* i
   uint32_t XL = rlp_hdr_len(xpay) + xpay;
   T.ex_len[j] = XL;
   uint64_t hx[4], xhead[4];
-  perms += hash_slot(xs, XL, top, hx);
+  uint32_t perms = hash_slot(xs, XL, top, hx);
   slot_head(xs, XL, xhead);
   if (T.ex_hash)
     for (int q2 = 0; q2 < 4; ++q2) T.ex_hash[4 * j + q2] = hx[q2];
-  ninl += (XL < 32 && !top) ? 1 : 0;
+  *ninl += (XL < 32 && !top) ? 1 : 0;
   publish_ref(T, parent, T.br_pord[j], nib, first, xhead, XL, hx);
+  return perms;
+}
+
+// a clean branch (incremental commit): its reference from the previous version.
+// Returns false when it is not needed (its parent is clean too).
+KH_HD bool branch_clean_ref(const Topo& T, uint32_t j, uint32_t* L, uint64_t hb[4], uint64_t bhead[4]) {
+  if (under_clean(T, T.br_parent[j])) return false;
+  *L = T.br_rlen[j];
+  for (int q = 0; q < 4; ++q) bhead[q] = hb[q] = T.br_ref[4 * j + q];
+  return true;
+}
+// after hashing a dirty branch: per-node hash (write-back) and capped reference (next commit)
+KH_HD void branch_keep(const Topo& T, uint32_t j, uint32_t L, const uint64_t hb[4], const uint64_t bhead[4]) {
+  if (T.br_hash)
+    for (int q = 0; q < 4; ++q) T.br_hash[4 * j + q] = hb[q];
+  if (T.br_ref) {
+    for (int q = 0; q < 4; ++q) {
+      uint32_t base = 8u * (uint32_t)q;
+      T.br_ref[4 * j + q] = L >= 32 ? hb[q] : (base < L ? bhead[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0);
+    }
+    T.br_rlen[j] = L;
+  }
+}
+
+// ---- branch hash (+ extension encode + hash) of a message prepared by op_branch_prep
+// (thread per branch of one level; the write-back build)
+KH_HD uint32_t op_branch_hash(const Topo& T, uint32_t j, uint64_t g, uint32_t* inl) {
+  uint32_t ext = T.br_ext[j];
+  uint32_t d = T.br_depth[j];
+  bool top = T.br_parent[j] == NONE;
+  *inl = 0;
+  uint64_t hb[4], bhead[4];
+  uint32_t L, perms = 0, ninl = 0;
+  if (T.br_dirty && !T.br_dirty[j]) {
+    if (!branch_clean_ref(T, j, &L, hb, bhead)) return 0;
+  } else {
+    L = T.br_len[j];
+    Slot sl = branch_slot(T, g, d, false);
+    perms = hash_slot(sl, L, top && ext == 0, hb);
+    slot_head(sl, L, bhead);
+    ninl = (L < 32 && !(top && ext == 0)) ? 1 : 0;
+    branch_keep(T, j, L, hb, bhead);
+  }
+  perms += branch_publish(T, j, L, hb, bhead, branch_slot(T, g, d, true), &ninl);
+  *inl = ninl;
+  return perms;
+}
+
+// ---- fused branch encode + hash (row N1: no node RLP in HBM).  The encoding is streamed
+// one 136-byte Keccak block at a time through `slot` (17 words, stride apart: an LDS
+// slot of the thread on the device) and absorbed into the state registers as each block
+// completes; the child references are read from the contiguous child records.  The
+// extension (if any) is encoded into the same slot afterwards.
+KH_HD uint32_t op_branch_fused(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl) {
+  uint32_t ext = T.br_ext[j];
+  bool top = T.br_parent[j] == NONE;
+  *inl = 0;
+  uint64_t hb[4] = {0, 0, 0, 0}, bhead[4] = {0, 0, 0, 0};
+  uint32_t L, perms = 0, ninl = 0;
+  if (T.br_dirty && !T.br_dirty[j]) {
+    if (!branch_clean_ref(T, j, &L, hb, bhead)) return 0;
+  } else {
+    const uint32_t payload = branch_payload(T, j);
+    L = rlp_hdr_len(payload) + payload;
+    T.br_len[j] = L;
+    const bool hashit = L >= 32 || (top && ext == 0);
+    const uint32_t nfull = L / 136;
+    KState S = {};
+    for (uint32_t b = 0; b <= nfull; ++b) {
+      WinBW w(slot, stride, 136u * b);
+      branch_stream(T, j, w, payload);
+      w.flush();
+      const uint32_t rem = b < nfull ? 136 : L - 136 * nfull;
+      if (!hashit) break;  // embedded in its parent: never hashed (Node.scala:114)
+#pragma unroll
+      for (int q = 0; q < 17; ++q) {
+        const uint32_t base = 8u * (uint32_t)q;
+        uint64_t x = base < rem ? slot[q * stride] & low_bytes_mask(rem - base < 8 ? rem - base : 8) : 0;
+        if (b == nfull) {
+          if ((rem >> 3) == (uint32_t)q) x ^= 0x01ULL << (8 * (rem & 7));
+          if (q == 16) x ^= 0x80ULL << 56;
+        }
+        kxor(S, q, x);
+      }
+      keccakf(S);
+    }
+    if (hashit) {
+      for (int q = 0; q < 4; ++q) hb[q] = lane(S, q);
+      perms = nfull + 1;
+    }
+    if (L < 32)  // one window: the slot still holds the whole encoding (the inline reference)
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t base = 8u * (uint32_t)q;
+        bhead[q] = base < L ? slot[q * stride] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0;
+      }
+    ninl = hashit ? 0 : 1;
+    branch_keep(T, j, L, hb, bhead);
+  }
+  perms += branch_publish(T, j, L, hb, bhead, Slot{slot, stride}, &ninl);
   *inl = ninl;
   return perms;
 }

@@ -276,12 +276,14 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
     hashes += p ? 1 : 0;
     inl += in1;
   }
+  // branch levels as the device runs them for root-only and incremental builds
+  // (k_branch_fused: every encoding streamed block by block through a 17-word slot)
   for (int d = 63; d >= 0; --d) {
-    for (uint64_t g = lbv[d]; g < lbv[d + 1]; ++g) op_branch_prep(T, lorder[g], g);
     for (uint64_t g = lbv[d]; g < lbv[d + 1]; ++g) {
       uint32_t j = lorder[g];
       uint32_t in1 = 0;
-      uint32_t p = op_branch_hash(T, j, g, &in1);
+      uint64_t slot[LEAF_WORDS + 1];
+      uint32_t p = op_branch_fused(T, j, slot, 1, &in1);
       perms += p;
       hashes += branch_hash_count(T, j, p);
       inl += in1;
