@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -573,6 +574,180 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8)))
     perms = op_branch_fused(T, j, slots + threadIdx.x * LEAF_WORDS, 1, &in1);
     hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
+  }
+  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
+}
+
+// LDS ordering between lanes of ONE wave (the wave's LDS operations execute in
+// order; the fences stop the compiler from moving them across): no block barrier
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 16-lane inclusive prefix sum inside each DPP row (row_shr:1,2,4,8; lanes shifted in
+// from outside the row read 0)
+__device__ __forceinline__ uint32_t row16_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    uint32_t w = (uint32_t)__shfl_xor((int)v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
+// Wave-cooperative variant of k_branch_fused (row N1, measured against it: see
+// DESIGN.md §5).  Each thread still owns one branch and its Keccak state, but the
+// encoding window of block b is assembled by a 16-lane group (one DPP row) per branch:
+// lane c takes child record c (one coalesced 32-byte load per lane; the level's records
+// are contiguous), its byte offset in the encoding is hdr + nibble + the row's exclusive
+// DPP prefix sum of (item length - 1), and it XORs its bytes (^ 0x80) into the window,
+// which the row first fills with 0x80 (every empty slot and the terminator are 0x80).
+// The 4 rows of a wave assemble the 64 windows in 16 steps; then every lane absorbs its
+// own window and the permutation runs on all 64 lanes.
+__global__ void __launch_bounds__(BS) k_branch_coop(Topo T, uint64_t first, uint64_t cnt) {
+  __shared__ uint64_t win[BS * LEAF_WORDS];
+  __shared__ uint32_t s_L[BS], s_cb[BS], s_kh[BS];  // per owner: length, child base, k | hdr << 8 | nblk << 16
+  const uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u, c = ln & 15, row = ln >> 4;
+  const uint32_t j = (uint32_t)(first + t);
+  const bool valid = t < cnt;
+  const bool clean = valid && T.br_dirty && !T.br_dirty[j];
+  const bool top = valid && T.br_parent[j] == NONE;
+  const uint32_t ext = valid ? T.br_ext[j] : 0;
+  uint32_t L = 0, payload = 0, k = 0, nblk = 0;
+  bool hashit = false;
+  if (valid && !clean) {
+    payload = branch_payload(T, j);
+    L = rlp_hdr_len(payload) + payload;
+    k = T.br_k[j];
+    hashit = L >= 32 || (top && ext == 0);
+    nblk = hashit ? L / 136 + 1 : 1;
+    T.br_len[j] = L;
+  }
+  s_L[threadIdx.x] = L;
+  s_cb[threadIdx.x] = valid ? T.br_cbase[j] : 0;
+  s_kh[threadIdx.x] = k | (rlp_hdr_len(payload) << 8) | (nblk << 16);
+  const uint32_t nb_wave = wave_max_u32(nblk);
+  wave_lds_sync();
+  KState S = {};
+  for (uint32_t b = 0; b < nb_wave; ++b) {
+    for (uint32_t sidx = 0; sidx < 16; ++sidx) {
+      const uint32_t o = wbase + row * 16 + sidx;  // the owner whose window this row builds
+      const uint32_t kh = s_kh[o], kk = kh & 0xFF, hh = (kh >> 8) & 0xFF, onb = kh >> 16;
+      if (b >= onb) continue;  // row-uniform
+      const uint32_t LL = s_L[o], w0 = 136u * b;
+      uint64_t* wb = win + (uint64_t)o * LEAF_WORDS;
+      // 1. 0x80 fill of the window's message bytes (lane c: word c; lane 0 also word 16)
+      for (uint32_t w = c; w < 17; w += 16) {
+        const uint32_t a = w0 + 8 * w;
+        const uint32_t n80 = LL > a ? (LL - a < 8 ? LL - a : 8) : 0;
+        wb[w] = low_bytes_mask(n80) & 0x8080808080808080ULL;
+      }
+      // 2. child c: its item bytes (0xa0 + hash, or the inline encoding) at its offset
+      uint32_t len = 0, nib = 0;
+      uint64_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+      const uint64_t rec = (uint64_t)s_cb[o] + c;
+      if (c < kk) {
+        const uint32_t mc = T.cmeta[rec];
+        len = mc & 0xFF;
+        nib = mc >> 8;
+        r0 = T.cref[4 * rec];
+        r1 = T.cref[4 * rec + 1];
+        r2 = T.cref[4 * rec + 2];
+        r3 = T.cref[4 * rec + 3];
+      }
+      const uint32_t ilen = len == 32 ? 33 : len;
+      const uint32_t incl = row16_scan(ilen ? ilen - 1 : 0);
+      const uint32_t off = hh + nib + incl - (ilen ? ilen - 1 : 0);
+      wave_lds_sync();  // the fill lands before any XOR
+      if (ilen && off < w0 + 136 && off + ilen > w0) {
+        uint64_t I[5];
+        if (len == 32) {
+          I[0] = 0xA0 | (r0 << 8);
+          I[1] = (r0 >> 56) | (r1 << 8);
+          I[2] = (r1 >> 56) | (r2 << 8);
+          I[3] = (r2 >> 56) | (r3 << 8);
+          I[4] = r3 >> 56;
+        } else {
+          I[0] = r0; I[1] = r1; I[2] = r2; I[3] = r3; I[4] = 0;  // zero beyond len (capped refs)
+        }
+        const uint32_t sh = off & 7, wfirst = off >> 3;
+#pragma unroll
+        for (uint32_t q = 0; q < 6; ++q) {
+          const uint64_t cur = q < 5 ? I[q] : 0, prv = q ? I[q - 1] : 0;
+          const uint64_t y = sh ? (cur << (8 * sh)) | (prv >> (64 - 8 * sh)) : cur;
+          const uint32_t W = wfirst + q;  // absolute word
+          // item bytes of this word: [max(off, 8W), min(off + ilen, 8W + 8)) relative to 8W
+          const int32_t lo = (int32_t)off - 8 * (int32_t)W, hi = (int32_t)(off + ilen) - 8 * (int32_t)W;
+          const uint32_t blo = lo > 0 ? (uint32_t)lo : 0, bhi = hi < 8 ? (hi > 0 ? (uint32_t)hi : 0) : 8;
+          if (bhi <= blo || W < w0 / 8 || W >= w0 / 8 + 17) continue;
+          const uint64_t m = low_bytes_mask(bhi) & ~low_bytes_mask(blo);
+          atomicXor((unsigned long long*)(wb + (W - w0 / 8)), (unsigned long long)((y ^ 0x8080808080808080ULL) & m));
+        }
+      }
+      // 3. the list header (window 0), lane 0
+      if (c == 0 && b == 0) {
+        const uint32_t pl = LL - hh;
+        uint64_t hdr = hh == 1 ? (0xC0 + pl) : hh == 2 ? (0xF8 | ((uint64_t)pl << 8))
+                                                        : (0xF9 | ((uint64_t)(pl >> 8) << 8) | ((uint64_t)(pl & 0xFF) << 16));
+        atomicXor((unsigned long long*)wb, (unsigned long long)((hdr ^ 0x8080808080808080ULL) & low_bytes_mask(hh)));
+      }
+      wave_lds_sync();
+    }
+    // absorb my window (one Keccak block) and permute
+    if (b < nblk && hashit) {
+      const uint32_t nfull = L / 136, rem = b < nfull ? 136 : L - 136 * nfull;
+      const uint64_t* my = win + (uint64_t)threadIdx.x * LEAF_WORDS;
+#pragma unroll
+      for (int q = 0; q < 17; ++q) {
+        const uint32_t base = 8u * (uint32_t)q;
+        uint64_t x = base < rem ? my[q] & low_bytes_mask(rem - base < 8 ? rem - base : 8) : 0;
+        if (b == nfull) {
+          if ((rem >> 3) == (uint32_t)q) x ^= 0x01ULL << (8 * (rem & 7));
+          if (q == 16) x ^= 0x80ULL << 56;
+        }
+        kxor(S, q, x);
+      }
+      keccakf(S);
+    }
+    wave_lds_sync();  // the next window reuses the slots
+  }
+  unsigned long long perms = 0, hashes = 0, inl = 0;
+  if (valid) {
+    uint64_t hb[4] = {0, 0, 0, 0}, bhead[4] = {0, 0, 0, 0};
+    uint32_t ninl = 0, p = 0;
+    bool go = true;
+    if (clean) {
+      go = branch_clean_ref(T, j, &L, hb, bhead);
+    } else {
+      if (hashit) {
+        for (int q = 0; q < 4; ++q) hb[q] = lane(S, q);
+        p = L / 136 + 1;
+      }
+      if (L < 32) {  // one window, still in the slot
+        const uint64_t* my = win + (uint64_t)threadIdx.x * LEAF_WORDS;
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t base = 8u * (uint32_t)q;
+          bhead[q] = base < L ? my[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0;
+        }
+      }
+      ninl = hashit ? 0 : 1;
+      branch_keep(T, j, L, hb, bhead);
+    }
+    if (go) {
+      p += branch_publish(T, j, L, hb, bhead, Slot{win + (uint64_t)threadIdx.x * LEAF_WORDS, 1}, &ninl);
+      perms = p;
+      hashes = branch_hash_count(T, j, p);
+      inl = ninl;
+    }
   }
   block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
 }
@@ -1301,6 +1476,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
 
   // ---- 5. branch levels, deepest first: encode (gathers the children's refs), then hash
   uint32_t levels = 0;
+  // N1 variant: one thread per branch assembling its own window (default) or the
+  // wave-cooperative DPP assembly (KHST_BRANCH=coop; DESIGN.md §5 has the measurement)
+  const char* bv = getenv("KHST_BRANCH");
+  const bool coop = bv && strcmp(bv, "coop") == 0;
   for (int d = 63; d >= 0; --d) {
     uint32_t cnt = lbh[d + 1] - lbh[d];
     if (!cnt) continue;
@@ -1308,6 +1487,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       hipLaunchKernelGGL(k_branch_prep, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
       LAUNCH_CHECK();
       hipLaunchKernelGGL(k_branch_hash, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+    } else if (coop) {
+      hipLaunchKernelGGL(k_branch_coop, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     } else {
       hipLaunchKernelGGL(k_branch_fused, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     }

@@ -261,3 +261,23 @@ def test_partition_vs_host(khst, nparts):
         assert np.array_equal(pl[:n].cpu().numpy(), lens[order])
         want = np.concatenate([v[vo[i]:vo[i + 1]] for i in order])
         assert np.array_equal(pv[:len(want)].cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("variant", ["lane", "coop"])
+def test_branch_variants_vs_oracle(khst, oracle, variant, monkeypatch):
+    """Both N1 branch kernels (KHST_BRANCH: one thread per branch, or the wave-cooperative
+    DPP assembly) give the oracle's roots on every edge case, storage tries with inline
+    children and segmented builds."""
+    monkeypatch.setenv("KHST_BRANCH", variant)
+    for name, keys, vals in C.all_cases(big=False):
+        assert khst.trie_root(keys, vals) == oracle.seq_root(keys, vals), (variant, name)
+    tries = C.segmented_case()
+    for (ks, vs), g in zip(tries, khst.trie_roots(tries)):
+        assert g == (oracle.seq_root(ks, vs) if ks else khst.EMPTY_TRIE_HASH), variant
+    from khipu_amd.device import Ctx
+    ctx = Ctx(0)
+    (hh, _, _, st), (addr, vals, voff) = _device_synth_root(ctx, 200_000)
+    a = addr[:20 * 200_000].cpu().numpy()
+    vo = voff.cpu().numpy().astype(np.uint64)
+    roots, bst = oracle.batch_roots(a, (vals[:int(vo[-1])].cpu().numpy(), vo), klen=20, hash_keys=True)
+    assert hh[0].tobytes() == roots[0] and st.n_node_perms == bst["node_perms"], variant
