@@ -57,6 +57,8 @@ extern "C" {
 
 /* flags */
 #define KH_HASH_KEYS 0x1u   /* trie key = kec256(input key) */
+#define KH_EMIT_NODES 0x2u  /* resident tries: keep each commit's write-back set (kh_trie_emit_nodes) */
+#define KH_NO_TRIE 0xFFFFFFFFu  /* kh_block_commit: an account upsert without a storage trie */
 
 typedef struct kh_stats {
   uint64_t n_inputs;       /* puts received */
@@ -167,38 +169,71 @@ int kh_verify_nodes(const uint8_t* data, const uint64_t* off, uint64_t n, const 
                     uint64_t nreq, uint8_t* hash32, int64_t* match, uint8_t* status, uint8_t* nchild, uint8_t* child32,
                     uint8_t* child_kind);
 
-/* ---- resident trie: incremental commit ----
- * A trie kept in HBM between commits: its sorted (key, value) set and the capped
- * reference of every branch node.  Replaces the per-key fold of TrieAccounts.flush /
- * TrieStorage.flush (TrieAccounts.scala:22-28, TrieStorage.scala:43-60) over
- * MerklePatriciaTrie.put / remove (MerklePatriciaTrie.scala:157-281, 290-477): a commit
- * merges the batch, rebuilds the topology, and re-hashes only the branches on the
- * changed keys' paths (clean branches keep their references).  Device buffers; the
- * handle owns its HBM and uses its context's stream (one thread at a time). */
+/* ---- resident tries and forests: incremental commit ----
+ * A trie kept in HBM between commits as node records found by their anchor (trie id,
+ * depth, key prefix): khipu_amd/csrc/forest.h.  Replaces the per-key fold of
+ * TrieAccounts.flush / TrieStorage.flush (TrieAccounts.scala:22-28, TrieStorage.scala:43-60)
+ * over MerklePatriciaTrie.put / remove (MerklePatriciaTrie.scala:157-281, 290-477): a commit
+ * opens only the nodes on the changed keys' paths and rebuilds them (with the canonical
+ * `fix` collapse of :430-477), O(dirty keys x depth) work.  A FOREST holds many tries
+ * (contract storage tries, BlockWorldState.scala:243-252) in one handle, each op tagged
+ * with its trie id; one commit re-roots every trie the block touched.  Device-buffer
+ * entry points use the handle's context stream (one thread at a time per handle); the
+ * _host variants take host buffers (what the JNI shim binds).
+ * Semantics of a commit: nup upserts then ndel deletes, the last op on a key winning;
+ * deleting an absent key is a no-op; keys are klen bytes (32, or any with KH_HASH_KEYS,
+ * which must match the flag the trie was opened with). */
 typedef struct kh_trie kh_trie;
 
-/* Build from n records (keys as in kh_dev_trie_build; duplicates: the later wins). */
+/* Open a trie from n records (duplicates: the later wins).  flags: KH_HASH_KEYS, KH_EMIT_NODES. */
 int kh_trie_open(kh_ctx* ctx, const uint8_t* d_keys, uint32_t klen, const uint8_t* d_vals, const uint64_t* d_voff,
                  uint64_t n, uint32_t flags, uint8_t root32[32], kh_trie** out);
+int kh_trie_open_host(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const uint64_t* voff, uint64_t n,
+                      uint32_t flags, uint8_t root32[32], kh_trie** out);
 
-/* One commit: nup upserts (keys, packed values with d_up_voff[nup+1]) and ndel deletes,
- * klen-byte keys (32, or any with KH_HASH_KEYS).  The batch is applied as upserts then
- * deletes with the last op on a key winning; deleting an absent key is a no-op
- * (MerklePatriciaTrie.remove of a missing key leaves the trie unchanged).
- * root32 receives the new root.  stats: n_node_hashes counts the re-hashed nodes only. */
+/* One commit; root32 receives the new root.  stats: n_node_hashes counts the nodes re-hashed. */
 int kh_trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals, const uint64_t* d_up_voff,
                   uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
                   uint8_t root32[32], kh_stats* stats);
+int kh_trie_apply_host(kh_trie* h, const uint8_t* up_keys, const uint8_t* up_vals, const uint64_t* up_voff,
+                       uint64_t nup, const uint8_t* del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
+                       uint8_t root32[32], kh_stats* stats);
 
-/* Storage write-back hand-off for a resident trie: the node set of the
- * current version — every node reachable from the committed root whose encoding is
- * >= 32 B, plus the root node — what persist()/changes hand to NodeStorage.update
+/* A forest of tries (empty).  Each op names its trie (any uint32 id).  After a commit,
+ * h_tries / h_roots32 receive the touched tries (ascending ids) and their new roots
+ * (EMPTY_TRIE_HASH for a trie left empty); KH_ENOSPC with *n_tries when cap is short. */
+int kh_forest_open(kh_ctx* ctx, uint32_t flags, kh_trie** out);
+int kh_forest_apply(kh_trie* f, const uint32_t* d_up_trie, const uint8_t* d_up_keys, const uint8_t* d_up_vals,
+                    const uint64_t* d_up_voff, uint64_t nup, const uint32_t* d_del_trie, const uint8_t* d_del_keys,
+                    uint64_t ndel, uint32_t klen, uint32_t* h_tries, uint8_t* h_roots32, uint64_t cap,
+                    uint64_t* n_tries, kh_stats* stats);
+int kh_forest_apply_host(kh_trie* f, const uint32_t* up_trie, const uint8_t* up_keys, const uint8_t* up_vals,
+                         const uint64_t* up_voff, uint64_t nup, const uint32_t* del_trie, const uint8_t* del_keys,
+                         uint64_t ndel, uint32_t klen, uint32_t* h_tries, uint8_t* h_roots32, uint64_t cap,
+                         uint64_t* n_tries, kh_stats* stats);
+
+/* One block (BlockWorldState.flush, BlockWorldState.scala:243-252 then TrieAccounts.flush):
+ * the storage ops into the forest, each touched trie's new root written into the stateRoot
+ * field of the account upserts that name it (d_a_up_trie[i], KH_NO_TRIE for none; the body
+ * RLP[nonce, balance, stateRoot, codeHash] of PV63.scala:46-51 is patched in place in
+ * d_a_up_vals), then the account ops into the state trie.  One call per block. */
+int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_trie, const uint8_t* d_s_up_keys,
+                    const uint8_t* d_s_up_vals, const uint64_t* d_s_up_voff, uint64_t ns_up,
+                    const uint32_t* d_s_del_trie, const uint8_t* d_s_del_keys, uint64_t ns_del, uint32_t s_klen,
+                    const uint8_t* d_a_up_keys, uint8_t* d_a_up_vals, const uint64_t* d_a_up_voff,
+                    const uint32_t* d_a_up_trie, uint64_t na_up, const uint8_t* d_a_del_keys, uint64_t na_del,
+                    uint32_t a_klen, uint8_t state_root32[32], kh_stats* stats);
+
+/* Storage write-back hand-off of the LAST commit (open or apply) of a
+ * trie opened with KH_EMIT_NODES: exactly the nodes that commit created -- every node
+ * reachable from a new root whose encoding is >= 32 B and that the previous version did
+ * not hold, plus a changed root node -- what persist()/changes hand to NodeStorage.update
  * (MerklePatriciaTrie.scala:491-516,544-554; BlockWorldState.scala:312-330).  Same layout
- * and KH_ENOSPC size negotiation as kh_trie_root_nodes; host outputs.  The current version
- * is re-encoded from its sorted set (no sort), and its root is checked against the commit's. */
+ * and KH_ENOSPC size negotiation as kh_trie_root_nodes (no re-encoding on the retry). */
 int kh_trie_emit_nodes(kh_trie* h, uint8_t* hashes32, uint64_t node_cap, uint8_t* rlp, uint64_t rlp_cap,
                        uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len);
 
+/* Leaves of a trie (of all tries of a forest). */
 int kh_trie_size(const kh_trie* h, uint64_t* n);
 int kh_trie_free(kh_trie* h);
 

@@ -18,6 +18,8 @@ KH_ENODE = -4
 KH_EINTERNAL = -5
 KH_ENOSPC = -6
 KH_HASH_KEYS = 0x1
+KH_EMIT_NODES = 0x2
+KH_NO_TRIE = 0xFFFFFFFF
 
 # every symbol include/khst.h declares
 EXPORTS = (
@@ -25,7 +27,8 @@ EXPORTS = (
     "kh_trie_roots_segmented", "kh_trie_root_nodes", "kh_ctx_create", "kh_ctx_destroy", "kh_ctx_set_stream",
     "kh_dev_kec256_batch", "kh_dev_trie_build", "kh_fold_root16", "kh_dev_synth_accounts", "kh_dev_hash_keys",
     "kh_dev_partition", "kh_trie_open", "kh_trie_apply", "kh_trie_emit_nodes", "kh_trie_size", "kh_trie_free",
-    "kh_verify_nodes",
+    "kh_verify_nodes", "kh_trie_open_host", "kh_trie_apply_host", "kh_forest_open", "kh_forest_apply",
+    "kh_forest_apply_host", "kh_block_commit",
 )
 
 
@@ -105,6 +108,13 @@ def lib():
     L.kh_trie_size.argtypes = [vp, ctypes.POINTER(u64)]
     L.kh_trie_free.argtypes = [vp]
     L.kh_verify_nodes.argtypes = [vp, vp, u64, vp, vp, u64, vp, vp, vp, vp, vp, vp]
+    L.kh_trie_open_host.argtypes = [vp, u32, vp, vp, u64, u32, vp, ctypes.POINTER(vp)]
+    L.kh_trie_apply_host.argtypes = [vp, vp, vp, vp, u64, vp, u64, u32, u32, vp, vp]
+    L.kh_forest_open.argtypes = [vp, u32, ctypes.POINTER(vp)]
+    L.kh_forest_apply.argtypes = [vp, vp, vp, vp, vp, u64, vp, vp, u64, u32, vp, vp, u64, vp, vp]
+    L.kh_forest_apply_host.argtypes = [vp, vp, vp, vp, vp, u64, vp, vp, u64, u32, vp, vp, u64, vp, vp]
+    L.kh_block_commit.argtypes = [vp, vp, vp, vp, vp, vp, u64, vp, vp, u64, u32, vp, vp, vp, vp, u64, vp, u64, u32,
+                                  vp, vp]
     for name in EXPORTS:
         fn = getattr(L, name)
         if fn.restype is ctypes.c_int or name not in ("kh_last_error", "kh_version"):

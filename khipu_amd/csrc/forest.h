@@ -1,0 +1,229 @@
+// Resident forest: the nodes of one or many tries kept in HBM between commits
+// (SURVEY §8 rows f1 incremental commit, f2 per-block write-back, a12 many storage
+// tries per block, a10 open from a node store).
+//
+// The reference keeps a trie as immutable node objects found by hash through
+// NodeStorage (MerklePatriciaTrie.scala:520-542) and re-hashes the root path of every
+// put / remove (:157-477), one key at a time, from TrieAccounts.flush /
+// TrieStorage.flush (TrieAccounts.scala:22-28, TrieStorage.scala:43-60).  Here every
+// node of the current version is a RECORD found by its ANCHOR: (trie id, the depth d
+// in nibbles at which the node hangs, the key's first d nibbles).  A leaf's record holds
+// its key and the value's place in a value heap; a branch's record (with the extension
+// above it, if any: anchor d < branch depth db) holds a key under it, db, its child
+// nibble mask and two capped references (the branch's, and the one its parent sees).
+// The anchor -> record map is an open-addressing table (64-bit tags, linear probing,
+// tombstones; the record is checked on every tag match).
+//
+// A commit (a block's dirty set, all tries at once):
+//   1. descend: every op walks down from its trie's root by anchor lookups; every
+//      branch it passes into is OPENED, the leaf it ends at is TOUCHED
+//      (MerklePatriciaTrie.put/remove's search path);
+//   2. gather ELEMENTS: the untouched children of opened branches (unchanged subtrees:
+//      a leaf, or a branch kept as one opaque element with its cached reference), the
+//      touched leaves no op replaced or deleted, and every upsert;
+//   3. an element build (run_build): sort, topology, and hashing of exactly the nodes
+//      on the dirty paths -- the canonical shape put / fix converge to (:183-477) -- with
+//      subtree elements referenced, or re-wrapped in a new extension when their anchor
+//      moved;
+//   4. the new nodes replace the opened ones in the map; the nodes whose encodings
+//      changed are the block's write-back set.
+// Work per commit is O(dirty keys x depth x 16), not O(resident keys).
+#pragma once
+#include "resident.h"
+
+namespace khst {
+
+KH_HD uint64_t fmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+// word q of a key restricted to its first d nibbles (the rest zero)
+KH_HD uint64_t prefix_word(const uint64_t* key, uint32_t d, int q) {
+  const uint32_t nib0 = 16u * (uint32_t)q;
+  if (d <= nib0) return 0;
+  uint64_t w = key[q];
+  if (d >= nib0 + 16) return w;
+  uint64_t be = bswap64(w);
+  be &= ~0ULL << (64 - 4 * (d - nib0));
+  return bswap64(be);
+}
+KH_HD bool prefix_eq(const uint64_t* a, const uint64_t* b, uint32_t d) {
+  for (int q = 0; q < 4; ++q)
+    if (prefix_word(a, d, q) != prefix_word(b, d, q)) return false;
+  return true;
+}
+KH_HD uint64_t anchor_tag(uint32_t t, uint32_t d, const uint64_t* key) {
+  uint64_t h = fmix64(((uint64_t)t << 8) ^ d ^ 0x9E3779B97F4A7C15ULL);
+  for (int q = 0; q < 4; ++q) h = fmix64(h ^ prefix_word(key, d, q) ^ (0x632BE59BD9B4E019ULL * (q + 1)));
+  return h | 2;  // 0 = empty slot, 1 = tombstone
+}
+// the key with nibble i set to v
+KH_HD void set_nibble(uint64_t* key, uint32_t i, uint32_t v) {
+  const int q = (int)(i >> 4);
+  const uint32_t byte = (i >> 1) & 7, sh = 8 * byte + ((i & 1) ? 0 : 4);
+  key[q] = (key[q] & ~(0xFULL << sh)) | ((uint64_t)v << sh);
+}
+
+constexpr uint8_t REC_DEAD = 0, REC_LIVE = 1;
+
+// node records (structure of arrays)
+struct Recs {
+  uint64_t* rk;    // [cap*4] a key under the node (a leaf: its key)
+  uint32_t* rt;    // trie id
+  uint8_t* rd;     // anchor depth
+  uint8_t* rdb;    // EL_LEAF, or the branch depth
+  uint64_t* rvo;   // leaf: value offset in the heap
+  uint32_t* rvl;   // leaf: value length
+  uint64_t* rref;  // [cap*4] capped reference the parent holds (the extension's, if any)
+  uint8_t* rrl;    //   its length (32 = hash)
+  uint64_t* rbref; // [cap*4] branch: the branch's own capped reference
+  uint8_t* rbrl;
+  uint16_t* rmask; // branch: child nibbles
+  uint8_t* rlive;
+};
+
+struct AMap {
+  unsigned long long* tag;  // [cap] 0 empty, 1 tombstone
+  uint32_t* rec;
+  uint64_t mask;            // cap - 1 (cap a power of two, load <= 1/2 incl. tombstones)
+};
+
+KH_HD uint32_t map_find(const AMap& M, const Recs& R, uint32_t t, uint32_t d, const uint64_t* key) {
+  const uint64_t h = anchor_tag(t, d, key);
+  for (uint64_t s = h & M.mask, n = 0; n <= M.mask; s = (s + 1) & M.mask, ++n) {
+    const uint64_t g = M.tag[s];
+    if (g == 0) return NONE;
+    if (g == h) {
+      const uint32_t r = M.rec[s];
+      if (R.rt[r] == t && R.rd[r] == d && prefix_eq(R.rk + 4ull * r, key, d)) return r;
+    }
+  }
+  return NONE;
+}
+// slot of record r at its current anchor (NONE if absent)
+KH_HD uint64_t map_slot_of(const AMap& M, const Recs& R, uint32_t r) {
+  const uint64_t h = anchor_tag(R.rt[r], R.rd[r], R.rk + 4ull * r);
+  for (uint64_t s = h & M.mask, n = 0; n <= M.mask; s = (s + 1) & M.mask, ++n) {
+    const uint64_t g = M.tag[s];
+    if (g == 0) return ~0ULL;
+    if (g == h && M.rec[s] == r) return s;
+  }
+  return ~0ULL;
+}
+
+// ---- the batch of ops, sorted by (trie, key), one op per key (the last one wins)
+enum : uint8_t { FOP_UPSERT = 1, FOP_DELETE = 2 };
+enum : uint8_t { TERM_MISSING = 0, TERM_LEAF = 1, TERM_DIVERGE = 2 };
+struct FOps {
+  const uint64_t* key;  // [n*4]
+  const uint32_t* trie; // [n]
+  const uint8_t* kind;  // [n]
+  uint64_t n;
+};
+
+// 1. descent of op o; marks opened branches and touched leaves (idempotent byte writes)
+KH_HD void op_descend(const FOps& O, const AMap& M, const Recs& R, uint8_t* touched, uint8_t* replaced, uint64_t o,
+                      unsigned long long* err) {
+  const uint64_t* K = O.key + 4 * o;
+  const uint32_t t = O.trie[o];
+  uint32_t d = 0;
+  for (int step = 0; step < 70; ++step) {
+    const uint32_t r = map_find(M, R, t, d, K);
+    if (r == NONE) return;  // TERM_MISSING: the upsert becomes a leaf element
+    const uint32_t db = R.rdb[r];
+    if (db == EL_LEAF) {
+      touched[r] = 1;
+      const uint64_t* L = R.rk + 4ull * r;
+      if (L[0] == K[0] && L[1] == K[1] && L[2] == K[2] && L[3] == K[3]) replaced[r] = 1;
+      return;
+    }
+    Key4 a{K[0], K[1], K[2], K[3]};
+    Key4 b = load_key(R.rk, r);
+    if (lcp_nibbles(a, b) < (int)db) return;  // diverges inside the extension: the branch stays whole
+    touched[r] = 1;                             // opened
+    d = db + 1;
+  }
+  *err = 3;  // deeper than a 32-byte key allows: corrupt map
+}
+
+// elements of an element build
+struct Elems {
+  uint64_t* key;    // [cap*4]
+  uint32_t* seg;    // compact trie index of the build (segment id)
+  uint8_t* db;      // EL_LEAF or branch depth
+  uint64_t* bref;   // [cap*4]
+  uint8_t* brl;
+  uint64_t* vo;     // value offset in the heap (leaves)
+  uint32_t* vl;
+  uint32_t* src;    // source record, NONE for an upsert
+  uint8_t* oldd;    // the source record's anchor depth
+  unsigned long long* n;  // counter
+  uint64_t cap;
+};
+
+KH_HD uint32_t seg_of(const uint32_t* tries, uint32_t nt, uint32_t t) {
+  uint32_t lo = 0, hi = nt;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (tries[mid] < t) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+template <typename PushFn>
+KH_HD void elem_from_record(const Recs& R, uint32_t r, uint32_t seg, const Elems& E, PushFn push) {
+  const uint64_t e = push();
+  if (e >= E.cap) return;  // the host sized the buffer; overflow flagged by the counter
+  for (int q = 0; q < 4; ++q) E.key[4 * e + q] = R.rk[4ull * r + q];
+  E.seg[e] = seg;
+  E.db[e] = R.rdb[r];
+  for (int q = 0; q < 4; ++q) E.bref[4 * e + q] = R.rbref[4ull * r + q];
+  E.brl[e] = R.rbrl[r];
+  E.vo[e] = R.rvo[r];
+  E.vl[e] = R.rdb[r] == EL_LEAF ? R.rvl[r] : 0;
+  E.src[e] = r;
+  E.oldd[e] = R.rd[r];
+}
+
+// 2a. record r (any live record): if it is an opened branch, its untouched children
+// become elements; if it is a touched leaf nobody replaced, it is an element itself
+template <typename PushFn>
+KH_HD void op_gather_record(const AMap& M, const Recs& R, const uint8_t* touched, const uint8_t* replaced,
+                            const uint32_t* tries, uint32_t nt, const Elems& E, uint32_t r, PushFn push,
+                            unsigned long long* err) {
+  if (!touched[r] || R.rlive[r] != REC_LIVE) return;
+  const uint32_t t = R.rt[r], seg = seg_of(tries, nt, t);
+  const uint32_t db = R.rdb[r];
+  if (db == EL_LEAF) {
+    if (!replaced[r]) elem_from_record(R, r, seg, E, push);
+    return;
+  }
+  const uint32_t mask = R.rmask[r];
+  uint64_t ck[4] = {R.rk[4ull * r], R.rk[4ull * r + 1], R.rk[4ull * r + 2], R.rk[4ull * r + 3]};
+  for (uint32_t v = 0; v < 16; ++v) {
+    if (!((mask >> v) & 1)) continue;
+    set_nibble(ck, db, v);
+    const uint32_t c = map_find(M, R, t, db + 1, ck);
+    if (c == NONE) {
+      *err = 4;  // a child the branch records is missing: corrupt map
+      continue;
+    }
+    if (touched[c]) continue;  // opened further down, or a touched leaf
+    elem_from_record(R, c, seg, E, push);
+  }
+}
+
+// 2b. the root of a touched trie that no op passed into (every op diverged inside its
+// extension): one subtree element
+template <typename PushFn>
+KH_HD void op_gather_root(const AMap& M, const Recs& R, const uint8_t* touched, const uint32_t* tries, uint32_t nt,
+                          const Elems& E, uint32_t s, PushFn push) {
+  const uint64_t zero[4] = {0, 0, 0, 0};
+  const uint32_t r = map_find(M, R, tries[s], 0, zero);
+  if (r == NONE || touched[r]) return;
+  elem_from_record(R, r, s, E, push);
+}
+
+}  // namespace khst

@@ -28,6 +28,7 @@
 #include "synth.h"
 #include "trie_ops.h"
 #include "resident.h"
+#include "forest.h"
 #include "nodedata.h"
 
 using namespace khst;
@@ -227,6 +228,18 @@ __global__ void __launch_bounds__(BS) k_compact(const uint64_t* skey, const uint
 __global__ void __launch_bounds__(BS) k_val_gather(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i < T.m) op_val_gather(T, i);
+}
+
+// element builds: the element properties in sorted order
+__global__ void __launch_bounds__(BS) k_el_gather(const uint32_t* sidx, uint64_t m, const uint8_t* db,
+                                                  const uint64_t* bref, const uint8_t* brl, uint8_t* odb,
+                                                  uint64_t* obref, uint8_t* obrl) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= m) return;
+  const uint32_t s = sidx[i];
+  odb[i] = db[s];
+  for (int q = 0; q < 4; ++q) obref[4 * i + q] = bref[4ull * s + q];
+  obrl[i] = brl[s];
 }
 
 __global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb) {
@@ -798,6 +811,7 @@ __global__ void __launch_bounds__(BS) k_emit_sizes(Topo T, uint64_t B, uint32_t*
   uint32_t len;
   const uint64_t* h;
   bool e = emit_node(T, B, q, &src, &stride, &len, &h);
+  if (T.emit_sel) e = e && T.emit_sel[q];
   flag[q] = e ? 1 : 0;
   bytes[q] = e ? len : 0;
 }
@@ -811,6 +825,7 @@ __global__ void __launch_bounds__(BS) k_emit_copy(Topo T, uint64_t B, const uint
   uint32_t len;
   const uint64_t* h;
   if (!emit_node(T, B, q, &src, &stride, &len, &h)) return;
+  if (T.emit_sel && !T.emit_sel[q]) return;
   uint64_t p = pos[q];
   uint64_t* oh = (uint64_t*)(out_hash + 32 * p);
   for (int j = 0; j < 4; ++j) oh[j] = h[j];
@@ -992,7 +1007,7 @@ struct kh_ctx {
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // leaf hashing, concurrent with the branch topology
   std::mutex mu;
-  DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, out_emit;
+  DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, out_emit, emit_dev;
   hipEvent_t ev[11] = {};  // [8] boundaries ready (st), [9] / [10] leaf kernel start / end (st2)
   unsigned long long* h_pinned = nullptr;  // small pinned staging for syncs
   // last build (for emission)
@@ -1008,34 +1023,23 @@ struct BuildArgs {
   const uint8_t* keys;
   uint32_t klen;
   const uint8_t* vals;
-  const uint64_t* voff;
+  const uint64_t* voff;  // [n+1] offsets, or with vlen: [n] offsets of spans anywhere in vals
   uint64_t n;
   const uint32_t* seg;  // nullable
   uint64_t nseg;
   uint32_t depth0;
   uint32_t flags;
   bool emit;
-  bool presorted = false;       // keys sorted and unique (a resident trie's merged set)
-  struct IncArgs* inc = nullptr;  // resident-trie bookkeeping (nullable)
+  const uint32_t* vlen = nullptr;  // per-input value lengths (element builds: spans in a value heap)
+  struct ElemArgs* el = nullptr;   // element build of a resident forest commit (forest.h; nullable)
 };
-// resident-trie bookkeeping of one build (kh_trie_open / kh_trie_apply)
-struct IncArgs {
-  // in: the changed keys (nullptr: a first build, every branch dirty) and the
-  // previous version's tables
-  const uint64_t* dkey = nullptr;
-  uint64_t nd = 0;
-  Prev V{};
-  // out: this version's tables
-  DevBuf* ref = nullptr;   // [B*4] branch references
-  DevBuf* rlen = nullptr;  // [B]
-  DevBuf* u = nullptr;     // [nb] boundary values
-  DevBuf* pyr = nullptr;   // pyramid levels >= 1
-  DevBuf* bid = nullptr;   // [nb] scanned rep flags
-  DevBuf* lref = nullptr;  // [m*4] leaf references
-  DevBuf* lrlen = nullptr; // [m]
-  DevBuf* lpd = nullptr;   // [m] leaf parent depths
-  Pyr P{};                 // rebased onto *u / *pyr
-  uint64_t nb = 0;
+// element build (forest.h): inputs are leaves and subtree elements; the capped reference
+// of every element node, branch and extension is kept for the forest's records
+struct ElemArgs {
+  const uint8_t* db;     // [n] EL_LEAF or subtree branch depth (input order)
+  const uint64_t* bref;  // [n*4]
+  const uint8_t* brl;    // [n]
+  DevBuf* out;           // sorted el_db / el_bref / el_brl, lf_ref / lf_rlen, br_ref / br_rlen, ex_ref / ex_rlen
 };
 struct BuildOut {
   std::vector<uint64_t> res_hash;  // nres*4
@@ -1186,7 +1190,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // plain root builds hash their leaves on c->st2 while c->st computes the branch
   // topology (trie_ops.h "early leaves"); write-back and incremental builds keep
   // the leaf stage after the topology (they need the parents / dirty marks first)
-  const bool early = !A.emit && !A.inc;
+  const bool early = !A.emit && !A.el;
 
   O.res_hash.assign(nres * 4, 0);
   O.res_len.assign(nres, 0);
@@ -1200,7 +1204,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // ---- phase-1 workspace (sized by n)
   const uint64_t nb1 = n;  // boundaries <= n-1; round up
   // keys are moved as 16-byte vectors: caller keys that are not 16-byte aligned get copied
-  const bool own_keys = !A.presorted && ((A.flags & KH_HASH_KEYS) || ((uintptr_t)A.keys & 15));
+  const bool own_keys = (A.flags & KH_HASH_KEYS) || ((uintptr_t)A.keys & 15);
   std::vector<size_t> sz = {
       own_keys ? n * 32 : 0,                  // K32
       n * 8, n * 8, n * 4, n * 4,             // ck0 ck1 idx0 idx1
@@ -1278,6 +1282,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.segmented = segmented ? 1 : 0;
   T.vals = A.vals;
   T.voff = A.voff;
+  T.vlen_in = A.vlen;
 
   HIPCHK(hipMemsetAsync(T.ctr, 0, CTR_N * 8, st));
   HIPCHK(hipMemsetAsync(T.depth_hist, 0, 64 * 4, st));
@@ -1300,9 +1305,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint64_t m = n;
   uint32_t* sidx = nullptr;
   bool fallback = false;
-  if (A.presorted) {
-    skey = (uint64_t*)A.keys;  // sorted, unique (the merged set of a resident trie)
-  } else {
+  {
     SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr};
     sort_dedup(c, S);
     m = S.m;
@@ -1413,10 +1416,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // ---- phase-2 workspace: child records + node arena
   // leaf encodings are kept (transposed message slots) only when the node set is emitted
   const uint64_t lmsg_words = A.emit ? (uint64_t)LEAF_WORDS * m : 0;
-  const bool inc_dirty = A.inc && A.inc->dkey;
   const uint64_t bmsg_words = A.emit ? (uint64_t)BR_WORDS * B : 0, xmsg_words = A.emit ? (uint64_t)EXT_WORDS * B : 0;
-  c->ws2.ensure(carve_size({C * 32, C * 2, lmsg_words * 8, lf_bytes + 64, bmsg_words * 8, xmsg_words * 8,
-                            inc_dirty ? B : 0}));
+  c->ws2.ensure(carve_size({C * 32, C * 2, lmsg_words * 8, lf_bytes + 64, bmsg_words * 8, xmsg_words * 8}));
   Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
   T.cref = cv2.take<uint64_t>(C * 4);
   T.cmeta = cv2.take<uint16_t>(C);
@@ -1426,31 +1427,26 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.bmsg = A.emit ? cv2.take<uint64_t>(bmsg_words) : nullptr;
   T.xmsg = A.emit ? cv2.take<uint64_t>(xmsg_words) : nullptr;
   T.lb = lb;
-  if (A.inc) {
-    IncArgs& I = *A.inc;
-    I.ref->ensure(B * 32 + 64);
-    I.rlen->ensure(B * 4 + 64);
-    T.br_ref = (uint64_t*)I.ref->p;
-    T.br_rlen = (uint32_t*)I.rlen->p;
-    I.lref->ensure(m * 32 + 64);
-    I.lrlen->ensure(m * 4 + 64);
-    T.lf_ref = (uint64_t*)I.lref->p;
-    T.lf_rlen = (uint32_t*)I.lrlen->p;
-    if (inc_dirty) {  // leaves: reuse the previous reference of an unchanged leaf
-      T.lf_oldpos = I.V.oldpos;
-      T.lf_upd = I.V.upd;
-      T.lf_opd = I.V.lpd;
-      T.lf_oref = I.V.lref;
-      T.lf_orlen = I.V.lrlen;
-    }
-    if (inc_dirty && B) {
-      // dirty = prefix of a changed key; clean branches take the previous reference
-      T.br_dirty = cv2.take<uint8_t>(B);
-      hipLaunchKernelGGL(k_br_dirty, GRID(B, BS), dim3(BS), 0, st, T, I.dkey, I.nd, (const uint32_t*)Bp);
-      LAUNCH_CHECK();
-      hipLaunchKernelGGL(k_br_clean, GRID(B, BS), dim3(BS), 0, st, T, I.V, (const uint32_t*)Bp);
-      LAUNCH_CHECK();
-    }
+  if (A.el) {  // element build: sorted element properties, and every capped reference kept
+    ElemArgs& E = *A.el;
+    E.out->ensure(carve_size({m, m * 32, m, m * 32, m * 4, B * 32, B * 4, B * 32, B * 4, m + 2 * B}));
+    Carver ce{(char*)E.out->p, 0, E.out->cap};
+    uint8_t* edb = ce.take<uint8_t>(m);
+    uint64_t* ebref = ce.take<uint64_t>(m * 4);
+    uint8_t* ebrl = ce.take<uint8_t>(m);
+    T.lf_ref = ce.take<uint64_t>(m * 4);
+    T.lf_rlen = ce.take<uint32_t>(m);
+    T.br_ref = ce.take<uint64_t>(B * 4);
+    T.br_rlen = ce.take<uint32_t>(B);
+    T.ex_ref = ce.take<uint64_t>(B * 4);
+    T.ex_rlen = ce.take<uint32_t>(B);
+    T.emit_sel = nullptr;  // the forest sets its write-back selection after the build
+    hipLaunchKernelGGL(k_el_gather, GRID(m, BS), dim3(BS), 0, st, (const uint32_t*)T.sidx, m, E.db, E.bref, E.brl,
+                       edb, ebref, ebrl);
+    LAUNCH_CHECK();
+    T.el_db = edb;
+    T.el_bref = ebref;
+    T.el_brl = ebrl;
   }
   if (!early) HIPCHK(hipEventRecord(c->ev[3], st));
 
@@ -1503,27 +1499,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   HIPCHK(hipMemcpyAsync(O.res_inl.data(), T.res_inl, nres * 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_pinned, ctr, CTR_N * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  if (c->h_pinned[CTR_ERR]) throw KhError{KH_EINTERNAL, "incremental commit: clean branch not found in the previous version"};
-  if (A.inc) {  // keep this version's tables for the next commit
-    IncArgs& I = *A.inc;
-    I.lpd->ensure(m + 64);
-    HIPCHK(hipMemcpyAsync(I.lpd->p, T.lf_pd, m, hipMemcpyDeviceToDevice, st));
-    I.nb = nb;
-    I.P = Pyr{};
-    if (nb > 0) {
-      // levels >= 1 live in `pyr` (level 0 is T.u); a one-level pyramid has none
-      uint64_t pyr_bytes = P.nl > 1 ? (uint64_t)(P.lv[P.nl - 1] - pyr) + P.sz[P.nl - 1] : 0;
-      I.u->ensure(nb + 64);
-      I.bid->ensure(nb * 4 + 64);
-      I.pyr->ensure(pyr_bytes + 64);
-      HIPCHK(hipMemcpyAsync(I.u->p, T.u, nb, hipMemcpyDeviceToDevice, st));
-      HIPCHK(hipMemcpyAsync(I.bid->p, T.isrep_bid, nb * 4, hipMemcpyDeviceToDevice, st));
-      if (P.nl > 1) HIPCHK(hipMemcpyAsync(I.pyr->p, pyr, pyr_bytes, hipMemcpyDeviceToDevice, st));
-      I.P = P;
-      I.P.lv[0] = (const uint8_t*)I.u->p;
-      for (int L = 1; L < P.nl; ++L) I.P.lv[L] = (const uint8_t*)I.pyr->p + (P.lv[L] - pyr);
-    }
-  }
+  if (c->h_pinned[CTR_ERR]) throw KhError{KH_EINTERNAL, "build: device invariant violated"};
   c->T = T;
   c->last_B = B;
   c->last_nres = nres;
@@ -1640,106 +1616,412 @@ static void copy_root(const BuildOut& O, uint64_t r, uint8_t* out32) {
 }
 
 // ---------------------------------------------------------------------------
-// resident trie: sorted (key, value) set + branch references in HBM
+// resident forest (forest.h): node records + anchor map +
+// value heap in HBM; a commit rebuilds only the nodes on its dirty paths
 // ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32_t* touched, uint8_t* replaced,
+                                                  uint32_t* tlist, unsigned long long* ctr) {
+  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o >= O.n) return;
+  // ctr[0] touched list size, [1] replaced leaves, [2] error
+  auto mark = [&](uint32_t r) {
+    if (atomicExch(&touched[r], 1u) == 0u) tlist[atomicAdd(&ctr[0], 1ULL)] = r;
+  };
+  const uint64_t* K = O.key + 4 * o;
+  const uint32_t t = O.trie[o];
+  uint32_t d = 0;
+  for (int step = 0; step < 70; ++step) {
+    const uint32_t r = map_find(M, R, t, d, K);
+    if (r == NONE) return;
+    const uint32_t db = R.rdb[r];
+    if (db == EL_LEAF) {
+      mark(r);
+      const uint64_t* L = R.rk + 4ull * r;
+      if (L[0] == K[0] && L[1] == K[1] && L[2] == K[2] && L[3] == K[3]) {
+        replaced[r] = 1;  // keys are unique in the batch: one op per leaf
+        atomicAdd(&ctr[1], 1ULL);
+      }
+      return;
+    }
+    if (lcp_nibbles(load_key(K, 0), load_key(R.rk, r)) < (int)db) return;  // diverges in the extension
+    mark(r);
+    d = db + 1;
+  }
+  ctr[2] = 3;
+}
+
+// upsert op o (its rank among the batch's upserts = ur[o]) -> leaf element; value into the heap
+__global__ void __launch_bounds__(BS) k_f_upsert_elems(FOps O, const uint32_t* tries, uint32_t nt, const uint32_t* ur,
+                                                       const uint64_t* uoff, Elems E, uint64_t heap_base) {
+  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o >= O.n || O.kind[o] != FOP_UPSERT) return;
+  const uint64_t e = ur[o];
+  for (int q = 0; q < 4; ++q) E.key[4 * e + q] = O.key[4 * o + q];
+  E.seg[e] = seg_of(tries, nt, O.trie[o]);
+  E.db[e] = EL_LEAF;
+  for (int q = 0; q < 4; ++q) E.bref[4 * e + q] = 0;
+  E.brl[e] = 0;
+  E.vo[e] = heap_base + uoff[e];
+  E.vl[e] = (uint32_t)(uoff[e + 1] - uoff[e]);
+  E.src[e] = NONE;
+  E.oldd[e] = 0;
+}
+// op o's value: (batch offset, length) -> for the heap copy
+__global__ void __launch_bounds__(BS) k_f_upsert_len(FOps O, const uint32_t* sidx, const uint64_t* voff,
+                                                     uint64_t* ulen, uint32_t* isup) {
+  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o >= O.n) return;
+  const bool up = O.kind[o] == FOP_UPSERT;
+  isup[o] = up ? 1u : 0u;
+  ulen[o] = up ? voff[sidx[o] + 1] - voff[sidx[o]] : 0;
+}
+__global__ void __launch_bounds__(BS) k_f_rank_scatter(FOps O, const uint32_t* ur, const uint64_t* uoff, uint64_t* uo,
+                                                       uint64_t nups, uint64_t total) {
+  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o == 0) uo[nups] = total;
+  if (o < O.n && O.kind[o] == FOP_UPSERT) uo[ur[o]] = uoff[o];
+}
+__global__ void __launch_bounds__(BS) k_f_heap_copy(FOps O, const uint32_t* sidx, const uint32_t* ur,
+                                                    const uint8_t* vals, const uint64_t* voff, const uint64_t* uoff,
+                                                    uint8_t* heap, uint64_t heap_base) {
+  uint64_t o = ((uint64_t)blockIdx.x * BS + threadIdx.x) / CG;
+  if (o >= O.n || O.kind[o] != FOP_UPSERT) return;
+  const uint64_t e = ur[o], s = sidx[o];
+  copy_bytes_group(heap + heap_base + uoff[e], vals + voff[s], voff[s + 1] - voff[s], threadIdx.x % CG);
+}
+__global__ void __launch_bounds__(BS) k_f_kinds(const uint32_t* sidx, uint64_t n, uint64_t nup, uint8_t* kind) {
+  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o < n) kind[o] = sidx[o] < nup ? FOP_UPSERT : FOP_DELETE;
+}
+__global__ void __launch_bounds__(BS) k_f_trie_flags(const uint32_t* trie, uint64_t n, uint32_t* flag) {
+  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o < n) flag[o] = (o == 0 || trie[o] != trie[o - 1]) ? 1u : 0u;
+}
+__global__ void __launch_bounds__(BS) k_f_trie_list(const uint32_t* trie, const uint32_t* flag, const uint32_t* pos,
+                                                    uint64_t n, uint32_t* tries) {
+  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o < n && flag[o]) tries[pos[o]] = trie[o];
+}
+__global__ void __launch_bounds__(BS) k_f_gather(AMap M, Recs R, const uint32_t* touched, const uint8_t* replaced,
+                                                 const uint32_t* tlist, uint64_t ntl, const uint32_t* tries,
+                                                 uint32_t nt, Elems E, unsigned long long* ctr) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= ntl) return;
+  auto push = [&]() { return (uint64_t)atomicAdd(E.n, 1ULL); };
+  // touched is u32 here; forest.h's gather reads it as a flag
+  const uint32_t r = tlist[i];
+  if (R.rlive[r] != REC_LIVE) return;
+  const uint32_t t = R.rt[r], seg = seg_of(tries, nt, t), db = R.rdb[r];
+  if (db == EL_LEAF) {
+    if (!replaced[r]) elem_from_record(R, r, seg, E, push);
+    return;
+  }
+  const uint32_t mask = R.rmask[r];
+  uint64_t ck[4] = {R.rk[4ull * r], R.rk[4ull * r + 1], R.rk[4ull * r + 2], R.rk[4ull * r + 3]};
+  for (uint32_t v = 0; v < 16; ++v) {
+    if (!((mask >> v) & 1)) continue;
+    set_nibble(ck, db, v);
+    const uint32_t cr = map_find(M, R, t, db + 1, ck);
+    if (cr == NONE) {
+      ctr[2] = 4;
+      continue;
+    }
+    if (touched[cr]) continue;
+    elem_from_record(R, cr, seg, E, push);
+  }
+}
+__global__ void k_f_gather_roots(AMap M, Recs R, const uint32_t* touched, const uint32_t* tries, uint32_t nt, Elems E) {
+  uint64_t s = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (s >= nt) return;
+  auto push = [&]() { return (uint64_t)atomicAdd(E.n, 1ULL); };
+  const uint64_t zero[4] = {0, 0, 0, 0};
+  const uint32_t r = map_find(M, R, tries[s], 0, zero);
+  if (r == NONE || touched[r]) return;
+  elem_from_record(R, r, (uint32_t)s, E, push);
+}
+
+// after the element build (c->T): one new record per branch (+ extension) at base + j,
+// and the write-back selection of branch / extension j (node m + 2j, m + 2j + 1): a node
+// identical to the one the old version holds at the same anchor is not written back
+__global__ void __launch_bounds__(BS) k_f_branch_recs(Topo T, const uint32_t* Bp, const uint32_t* tries, AMap M,
+                                                      Recs R, uint64_t base, uint8_t* sel) {
+  const uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (j >= *Bp) return;
+  const uint64_t f = T.br_first[j], r = base + j;
+  const uint32_t t = tries[T.sseg ? T.sseg[f] : 0];
+  const uint32_t db = T.br_depth[j], ext = T.br_ext[j], d = db - ext;
+  const uint64_t* K = T.skey + 4 * f;
+  for (int q = 0; q < 4; ++q) R.rk[4 * r + q] = K[q];
+  R.rt[r] = t;
+  R.rd[r] = (uint8_t)d;
+  R.rdb[r] = (uint8_t)db;
+  R.rvo[r] = 0;
+  R.rvl[r] = 0;
+  const uint32_t brl = T.br_rlen[j] >= 32 ? 32 : T.br_rlen[j];
+  const uint32_t xrl = ext ? (T.ex_rlen[j] >= 32 ? 32 : T.ex_rlen[j]) : brl;
+  const uint64_t* xr = ext ? T.ex_ref + 4 * j : T.br_ref + 4 * j;
+  for (int q = 0; q < 4; ++q) {
+    R.rbref[4 * r + q] = T.br_ref[4 * j + q];
+    R.rref[4 * r + q] = xr[q];
+  }
+  R.rbrl[r] = (uint8_t)brl;
+  R.rrl[r] = (uint8_t)xrl;
+  uint32_t mask = 0;
+  for (uint32_t c = 0; c < T.br_k[j]; ++c) mask |= 1u << (T.cmeta[T.br_cbase[j] + c] >> 8);
+  R.rmask[r] = (uint16_t)mask;
+  R.rlive[r] = REC_LIVE;
+  const uint32_t old = map_find(M, R, t, d, K);
+  bool same_b = false, same_x = false;
+  if (old != NONE && R.rdb[old] == db && R.rbrl[old] == brl) {
+    same_b = true;
+    for (int q = 0; q < 4; ++q) same_b = same_b && R.rbref[4ull * old + q] == T.br_ref[4 * j + q];
+    same_x = same_b && R.rrl[old] == xrl;
+    for (int q = 0; q < 4; ++q) same_x = same_x && R.rref[4ull * old + q] == xr[q];
+  }
+  sel[T.m + 2 * j] = same_b ? 0 : 1;
+  sel[T.m + 2 * j + 1] = same_x ? 0 : 1;
+}
+// elements (sorted position i): flag of a new record (an upsert) for the scan of their ids
+__global__ void __launch_bounds__(BS) k_f_elem_new(Topo T, Elems E, uint32_t* isnew) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < T.m) isnew[i] = E.src[T.sidx[i]] == NONE ? 1u : 0u;
+}
+// write-back selection of element i: an upsert's leaf, a leaf whose anchor moved, and a
+// subtree's new extension (a subtree hanging at its own depth has no node of its own)
+__global__ void __launch_bounds__(BS) k_f_elem_sel(Topo T, Elems E, uint8_t* sel) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= T.m) return;
+  const uint32_t s = T.sidx[i], a = (uint32_t)(T.lf_pd[i] + 1);
+  const bool moved = E.src[s] == NONE || E.oldd[s] != a;
+  const bool sub = T.el_db[i] != EL_LEAF;
+  sel[i] = (moved && !(sub && T.el_db[i] == a)) ? 1 : 0;
+}
+// element records: an upsert's new record (id base + rank), or its source record re-anchored
+__global__ void __launch_bounds__(BS) k_f_elem_recs(Topo T, Elems E, const uint32_t* tries, const uint32_t* newrank,
+                                                    Recs R, uint64_t base, uint32_t* eid) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= T.m) return;
+  const uint32_t s = T.sidx[i];
+  const uint64_t r = E.src[s] == NONE ? base + newrank[i] : E.src[s];
+  eid[i] = (uint32_t)r;
+  for (int q = 0; q < 4; ++q) R.rk[4 * r + q] = T.skey[4 * i + q];
+  R.rt[r] = tries[T.sseg ? T.sseg[i] : 0];
+  R.rd[r] = (uint8_t)(T.lf_pd[i] + 1);
+  R.rdb[r] = T.el_db[i];
+  R.rvo[r] = E.vo[s];
+  R.rvl[r] = E.vl[s];
+  const uint32_t L = T.lf_rlen[i];
+  for (int q = 0; q < 4; ++q) {
+    R.rref[4 * r + q] = T.lf_ref[4 * i + q];
+    R.rbref[4 * r + q] = T.el_bref[4 * i + q];
+  }
+  R.rrl[r] = (uint8_t)(L >= 32 ? 32 : L);
+  R.rbrl[r] = T.el_brl[i];
+  R.rlive[r] = REC_LIVE;
+}
+__global__ void __launch_bounds__(BS) k_f_elem_src(Topo T, Elems E, uint32_t* src) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < T.m) src[i] = E.src[T.sidx[i]];
+}
+// map maintenance: delete records' current anchors, mark dead, insert
+__global__ void __launch_bounds__(BS) k_map_delete(AMap M, Recs R, const uint32_t* list, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n || list[i] == NONE) return;
+  const uint64_t sl = map_slot_of(M, R, list[i]);
+  if (sl != ~0ULL) M.tag[sl] = 1;  // tombstone
+}
+__global__ void __launch_bounds__(BS) k_rec_dead(Recs R, const uint32_t* list, uint64_t n, uint32_t* touched,
+                                                 uint8_t* replaced) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = list[i];
+  R.rlive[r] = REC_DEAD;
+  touched[r] = 0;
+  replaced[r] = 0;
+}
+// insert records list[i] (or base + i when list is null) at their anchors
+__global__ void __launch_bounds__(BS) k_map_insert(AMap M, Recs R, const uint32_t* list, uint64_t base, uint64_t n,
+                                                   unsigned long long* err) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = list ? list[i] : (uint32_t)(base + i);
+  if (R.rlive[r] != REC_LIVE) return;
+  const unsigned long long h = anchor_tag(R.rt[r], R.rd[r], R.rk + 4ull * r);
+  for (uint64_t s = h & M.mask, k = 0; k <= M.mask; s = (s + 1) & M.mask, ++k) {
+    unsigned long long g = M.tag[s];
+    if (g > 1) continue;
+    if (atomicCAS(&M.tag[s], g, h) == g) {
+      M.rec[s] = r;
+      return;
+    }
+  }
+  *err = 5;  // full table
+}
+// per touched trie: its new root (segment result), EMPTY when no element remained
+__global__ void k_f_roots(const uint64_t* res_hash, const uint32_t* res_len, uint32_t nt, uint64_t* roots) {
+  const uint32_t s = blockIdx.x * BS + threadIdx.x;
+  if (s >= nt) return;
+  const uint64_t E[4] = {0xa655cc1b171fe856ULL, 0x6ef8c092e64583ffULL, 0xc0ad6c991be0485bULL, 0x21b463e3b52f6201ULL};
+  for (int q = 0; q < 4; ++q) roots[4 * s + q] = res_len && res_len[s] ? res_hash[4 * s + q] : E[q];
+}
+// block commit: the new storage root of account upsert i's trie into bytes [len-65, len-33)
+// of its body (RLP[nonce, balance, stateRoot, codeHash], PV63.scala:46-51)
+__global__ void __launch_bounds__(BS) k_inject_roots(uint8_t* vals, const uint64_t* voff, const uint32_t* acct_trie,
+                                                     uint64_t n, const uint32_t* tries, uint32_t nt,
+                                                     const uint64_t* roots, unsigned long long* err) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n || acct_trie[i] == 0xFFFFFFFFu) return;
+  const uint32_t s = seg_of(tries, nt, acct_trie[i]);
+  if (s >= nt || tries[s] != acct_trie[i]) return;  // storage unchanged this block
+  const uint64_t e = voff[i + 1];
+  if (e - voff[i] < 66 || vals[e - 66] != 0xA0 || vals[e - 33] != 0xA0) {
+    *err = 6;  // not an account body
+    return;
+  }
+  const uint8_t* rb = (const uint8_t*)(roots + 4 * s);
+  for (int q = 0; q < 32; ++q) vals[e - 65 + q] = rb[q];
+}
+
 struct kh_trie {
   kh_ctx* c = nullptr;
-  uint64_t m = 0;  // keys
-  int cur = 0;     // current half of the double buffers
-  DevBuf key[2], val[2], off[2], ref[2], rlen[2], lref[2], lrlen[2];
-  DevBuf u, pyr, bid, lpd;  // the current version's topology tables
-  Pyr P{};
-  uint64_t nb = 0;
-  DevBuf mws;  // merge scratch
+  uint32_t flags = 0;  // KH_HASH_KEYS: the trie's key encoder; KH_EMIT_NODES: keep each commit's write-back set
+  bool forest = false;
+  DevBuf rk, rt, rd, rdb, rvo, rvl, rref, rrl, rbref, rbrl, rmask, rlive, touched, replaced;
+  uint64_t rcap = 0, rn = 0, rdead = 0;
+  DevBuf mtag, mrec;
+  uint64_t mcap = 0, mused = 0;
+  DevBuf heap;
+  uint64_t heap_n = 0;
+  uint64_t nleaves = 0;
   uint8_t root[32] = {};
+  DevBuf ws, elout, em;  // commit scratch, element-build outputs, last write-back set
+  DevBuf tlb, ebuf, tbuf, ubuf, selb, merr;  // touched list, elements, trie ids + roots, upsert offsets, selections
+  uint64_t em_n = 0, em_bytes = 0;
+  bool em_valid = false;
+  std::vector<uint32_t> tries;  // last commit: touched tries and their roots
+  std::vector<uint8_t> roots;
 };
 
-// keep the sorted set of the build just run (c->T): keys, then the value spans
-// compacted in key order
-static void save_sorted(kh_trie* h, int half, uint64_t m, const uint8_t* vals) {
-  kh_ctx* c = h->c;
-  hipStream_t st = c->st;
-  const Topo& T = c->T;
-  h->key[half].ensure(m * 32 + 64);
-  h->off[half].ensure((m + 1) * 8 + 64);
-  uint64_t* off = (uint64_t*)h->off[half].p;
-  HIPCHK(hipMemsetAsync(off, 0, (m + 1) * 8, st));
-  if (m == 0) return;
-  HIPCHK(hipMemcpyAsync(h->key[half].p, T.skey, m * 32, hipMemcpyDeviceToDevice, st));
-  h->mws.ensure(carve_size({m * 8, scan_scratch_bytes(m, 8), 64}));
-  Carver cv{(char*)h->mws.p, 0, h->mws.cap};
-  uint64_t* len64 = cv.take<uint64_t>(m);
-  void* scr = cv.take<char>(scan_scratch_bytes(m, 8));
-  uint64_t* tot = cv.take<uint64_t>(8);
-  hipLaunchKernelGGL(k_u32_to_u64, GRID(m, BS), dim3(BS), 0, st, (const uint32_t*)T.svlen, len64, m);
-  LAUNCH_CHECK();
-  scan_exclusive<uint64_t>(len64, off, m, tot, scr, st);
-  HIPCHK(hipMemcpyAsync(off + m, tot, 8, hipMemcpyDeviceToDevice, st));
-  HIPCHK(hipMemcpyAsync(c->h_pinned, tot, 8, hipMemcpyDeviceToHost, st));
+static Recs recs_of(kh_trie* h) {
+  return Recs{(uint64_t*)h->rk.p,   (uint32_t*)h->rt.p,   (uint8_t*)h->rd.p,   (uint8_t*)h->rdb.p,
+              (uint64_t*)h->rvo.p,  (uint32_t*)h->rvl.p,  (uint64_t*)h->rref.p, (uint8_t*)h->rrl.p,
+              (uint64_t*)h->rbref.p, (uint8_t*)h->rbrl.p, (uint16_t*)h->rmask.p, (uint8_t*)h->rlive.p};
+}
+static AMap map_of(kh_trie* h) { return AMap{(unsigned long long*)h->mtag.p, (uint32_t*)h->mrec.p, h->mcap - 1}; }
+
+// grow a device array, keeping its first `keep` bytes
+static void regrow(DevBuf& b, size_t keep, size_t bytes, hipStream_t st) {
+  if (bytes <= b.cap) return;
+  DevBuf nb;
+  nb.ensure(bytes);
+  if (keep) HIPCHK(hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipStreamSynchronize(st));
-  uint64_t vbytes = c->h_pinned[0];
-  h->val[half].ensure(vbytes + 64);
-  hipLaunchKernelGGL(k_merge_vals, GRID(m * CG, BS), dim3(BS), 0, st, (const uint64_t*)T.svoff, (const uint32_t*)T.svlen,
-                     (const uint64_t*)off, m, vals, (const uint8_t*)nullptr, (uint8_t*)h->val[half].p);
+  b.release();
+  b.p = nb.p;
+  b.cap = nb.cap;
+  nb.p = nullptr;
+  nb.cap = 0;
+}
+static void recs_reserve(kh_trie* h, uint64_t need) {
+  if (need <= h->rcap) return;
+  hipStream_t st = h->c->st;
+  const uint64_t cap = std::max<uint64_t>(need + need / 2, 4096), n = h->rn;
+  regrow(h->rk, n * 32, cap * 32, st);
+  regrow(h->rt, n * 4, cap * 4, st);
+  regrow(h->rd, n, cap, st);
+  regrow(h->rdb, n, cap, st);
+  regrow(h->rvo, n * 8, cap * 8, st);
+  regrow(h->rvl, n * 4, cap * 4, st);
+  regrow(h->rref, n * 32, cap * 32, st);
+  regrow(h->rrl, n, cap, st);
+  regrow(h->rbref, n * 32, cap * 32, st);
+  regrow(h->rbrl, n, cap, st);
+  regrow(h->rmask, n * 2, cap * 2, st);
+  regrow(h->rlive, n, cap, st);
+  regrow(h->touched, n * 4, cap * 4, st);
+  regrow(h->replaced, n, cap, st);
+  // the new tail: not live, not touched
+  HIPCHK(hipMemsetAsync((uint8_t*)h->rlive.p + n, 0, h->rlive.cap - n, st));
+  HIPCHK(hipMemsetAsync((uint8_t*)h->touched.p + 4 * n, 0, h->touched.cap - 4 * n, st));
+  HIPCHK(hipMemsetAsync((uint8_t*)h->replaced.p + n, 0, h->replaced.cap - n, st));
+  h->rcap = std::min({h->rk.cap / 32, h->rt.cap / 4, h->rd.cap, h->rdb.cap, h->rvo.cap / 8, h->rvl.cap / 4,
+                      h->rref.cap / 32, h->rrl.cap, h->rbref.cap / 32, h->rbrl.cap, h->rmask.cap / 2, h->rlive.cap,
+                      h->touched.cap / 4, h->replaced.cap});
+}
+__global__ void __launch_bounds__(BS) k_rec_count_live(const uint8_t* live, uint64_t n, unsigned long long* cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  unsigned long long v = (i < n && live[i] == REC_LIVE) ? 1 : 0;
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(cnt, v);
+}
+// (re)build the anchor map with capacity >= 2 * (records + headroom), inserting every live record
+static void map_rebuild(kh_trie* h, uint64_t headroom) {
+  hipStream_t st = h->c->st;
+  uint64_t cap = 1024;
+  while (cap < 2 * (h->rn + headroom) + 1024) cap <<= 1;
+  h->mtag.ensure(cap * 8);
+  h->mrec.ensure(cap * 4);
+  h->mcap = cap;
+  HIPCHK(hipMemsetAsync(h->mtag.p, 0, cap * 8, st));
+  h->merr.ensure(64);
+  unsigned long long* err = (unsigned long long*)h->merr.p;
+  HIPCHK(hipMemsetAsync(err, 0, 16, st));
+  if (h->rn) {
+    hipLaunchKernelGGL(k_map_insert, GRID(h->rn, BS), dim3(BS), 0, st, map_of(h), recs_of(h), (const uint32_t*)nullptr,
+                       (uint64_t)0, h->rn, err);
+    hipLaunchKernelGGL(k_rec_count_live, GRID(h->rn, BS), dim3(BS), 0, st, (const uint8_t*)h->rlive.p, h->rn, err + 1);
+  }
   LAUNCH_CHECK();
+  HIPCHK(hipMemcpyAsync(h->c->h_pinned, err, 16, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (h->c->h_pinned[0]) throw KhError{KH_EINTERNAL, "anchor map rebuild failed"};
+  h->mused = h->c->h_pinned[1];
+  h->rdead = h->rn - h->mused;
 }
 
-static IncArgs inc_out(kh_trie* h, int half) {
-  IncArgs I;
-  I.ref = &h->ref[half];
-  I.rlen = &h->rlen[half];
-  I.lref = &h->lref[half];
-  I.lrlen = &h->lrlen[half];
-  I.lpd = &h->lpd;
-  I.u = &h->u;
-  I.pyr = &h->pyr;
-  I.bid = &h->bid;
-  return I;
+struct FCommit {  // one commit's inputs (device buffers)
+  const uint32_t* up_trie = nullptr;  // nullable: trie 0
+  const uint8_t* up_keys = nullptr;
+  const uint8_t* up_vals = nullptr;
+  const uint64_t* up_voff = nullptr;
+  uint64_t nup = 0;
+  const uint32_t* del_trie = nullptr;
+  const uint8_t* del_keys = nullptr;
+  uint64_t ndel = 0;
+  uint32_t klen = 32;
+};
+
+__global__ void __launch_bounds__(BS) k_u32_fill(uint32_t* out, uint64_t n, uint32_t v) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < n) out[i] = v;
 }
 
-static void trie_open(kh_trie* h, const uint8_t* d_keys, uint32_t klen, const uint8_t* d_vals, const uint64_t* d_voff,
-                      uint64_t n, uint32_t flags, kh_stats* stats) {
-  IncArgs I = inc_out(h, 0);
-  BuildArgs A{d_keys, klen, d_vals, d_voff, n, nullptr, 1, 0, flags, false};
-  A.inc = &I;
-  BuildOut O;
-  run_build(h->c, A, O, stats);
-  uint64_t m = n ? h->c->T.m : 0;
-  save_sorted(h, 0, m, d_vals);
-  h->m = m;
-  h->cur = 0;
-  h->P = I.P;
-  h->nb = I.nb;
-  copy_root(O, 0, h->root);
-}
+static int emit_nodes_dev(kh_ctx* c, DevBuf& out, uint64_t* n_nodes, uint64_t* rlp_len);
 
-// One commit: upserts (d_up_*) then deletes, the last op on a key winning.
-static void trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals, const uint64_t* d_up_voff,
-                       uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
-                       kh_stats* stats) {
+// One commit of a block's ops into the forest: upserts then deletes, the last op on a
+// key winning; deleting an absent key is a no-op.  Fills h->tries / h->roots.
+static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   kh_ctx* c = h->c;
   hipStream_t st = c->st;
   if (stats) memset(stats, 0, sizeof(*stats));
-  const uint64_t nops = nup + ndel, m = h->m;
+  h->tries.clear();
+  h->roots.clear();
+  h->em_valid = false;
+  const uint64_t nops = F.nup + F.ndel;
   if (nops == 0) return;
-  if (nops >= (1ULL << 31) || m + nops >= (1ULL << 31)) throw KhError{KH_EINVAL, "batch too large"};
-  if (!(flags & KH_HASH_KEYS) && klen != 32) throw KhError{KH_EINVAL, "keys must be 32 bytes unless KH_HASH_KEYS"};
-  const int cur = h->cur, nxt = 1 - cur;
-  const uint64_t mx = m + nops;  // merged size bound
-  // ---- scratch
-  std::vector<size_t> sz = {
-      nops * 32,                                   // K (op keys)
-      nops * 8, nops * 8, nops * 4, nops * 4,      // ck0 ck1 idx0 idx1
-      nops * 32, radix_scratch_bytes(nops),        // sorted op keys, radix scratch
-      scan_scratch_bytes(mx + 1, 8), CTR_N * 8,    // scan scratch, counters
-      nops * 4, nops, nops * 4, nops * 4, nops * 4, nops * 4,  // o_lb o_kind o_insf o_ins o_efff o_eff
-      (m + 1) * 4, (m + 1) * 4, (m + 1) * 4, (m + 1) * 4, m * 4 + 4,  // pos_cnt pos_ins del_flag pos_del pos_upd
-      mx * 4, mx * 8, mx * 4, mx * 8, nops * 32, mx,  // nlen nsrc oldpos len64 dkey nupd
-  };
-  h->mws.ensure(carve_size(sz));
-  Carver cv{(char*)h->mws.p, 0, h->mws.cap};
+  if (nops >= (1ULL << 30)) throw KhError{KH_EINVAL, "batch too large"};
+  if (!(h->flags & KH_HASH_KEYS) && F.klen != 32) throw KhError{KH_EINVAL, "keys must be 32 bytes unless KH_HASH_KEYS"};
+  if (F.klen == 0 || F.klen > 4096) throw KhError{KH_EINVAL, "bad key length"};
+  HIPCHK(hipEventRecord(c->ev[6], st));
+  // ---- 1. op keys (the trie's key encoder), trie ids, sort by (trie, key), last op wins
+  const bool segd = h->forest;
+  std::vector<size_t> sz = {nops * 32, nops * 4, nops * 8, nops * 8, nops * 4, nops * 4, nops * 32, nops * 4,
+                            radix_scratch_bytes(nops), scan_scratch_bytes(nops + 1, 8), CTR_N * 8,
+                            nops, nops * 4, nops * 4, nops * 4, (nops + 1) * 8, nops * 8, nops * 4};
+  h->ws.ensure(carve_size(sz));
+  Carver cv{(char*)h->ws.p, 0, h->ws.cap};
   uint64_t* K = cv.take<uint64_t>(nops * 4);
+  uint32_t* Tid = cv.take<uint32_t>(nops);
   SortIO S{};
   S.K32 = K;
   S.n = nops;
@@ -1748,142 +2030,248 @@ static void trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up
   S.idx0 = cv.take<uint32_t>(nops);
   S.idx1 = cv.take<uint32_t>(nops);
   S.skey = cv.take<uint64_t>(nops * 4);
+  uint32_t* sseg = cv.take<uint32_t>(nops);
+  S.sseg = segd ? sseg : nullptr;
+  S.seg = segd ? Tid : nullptr;
+  S.sb = segd ? 32 : 0;
   S.rs_scratch = cv.take<char>(radix_scratch_bytes(nops));
-  S.scan_scratch = cv.take<char>(scan_scratch_bytes(mx + 1, 8));
+  S.scan_scratch = cv.take<char>(scan_scratch_bytes(nops + 1, 8));
   S.ctr = cv.take<unsigned long long>(CTR_N);
-  Merge M{};
-  M.o_lb = cv.take<uint32_t>(nops);
-  M.o_kind = cv.take<uint8_t>(nops);
-  uint32_t* o_insf = cv.take<uint32_t>(nops);
-  M.o_ins = cv.take<uint32_t>(nops);
-  uint32_t* o_efff = cv.take<uint32_t>(nops);
-  M.o_eff = cv.take<uint32_t>(nops);
-  M.pos_cnt = cv.take<uint32_t>(m + 1);
-  M.pos_ins = cv.take<uint32_t>(m + 1);
-  uint32_t* del_flag = cv.take<uint32_t>(m + 1);
-  M.pos_del = cv.take<uint32_t>(m + 1);
-  M.pos_upd = cv.take<uint32_t>(m + 1);
-  M.nlen = cv.take<uint32_t>(mx);
-  M.nsrc = cv.take<uint64_t>(mx);
-  M.oldpos = cv.take<uint32_t>(mx);
-  uint64_t* len64 = cv.take<uint64_t>(mx);
-  M.dkey = cv.take<uint64_t>(nops * 4);
-  M.nupd = cv.take<uint8_t>(mx);
+  uint8_t* kind = cv.take<uint8_t>(nops);
+  uint32_t* tflag = cv.take<uint32_t>(nops);
+  uint32_t* tpos = cv.take<uint32_t>(nops);
+  uint32_t* isup = cv.take<uint32_t>(nops);
+  uint64_t* uoff = cv.take<uint64_t>(nops + 1);
+  uint64_t* ulen = cv.take<uint64_t>(nops);
+  uint32_t* ur = cv.take<uint32_t>(nops);
   HIPCHK(hipMemsetAsync(S.ctr, 0, CTR_N * 8, st));
-  HIPCHK(hipEventRecord(c->ev[6], st));
-
-  // ---- 1. op keys (hashed or copied), sorted, last op per key kept
-  if (flags & KH_HASH_KEYS) {
-    if (nup) hipLaunchKernelGGL(k_hash_keys, GRID(nup, BS), dim3(BS), 0, st, d_up_keys, klen, nup, K);
-    if (ndel) hipLaunchKernelGGL(k_hash_keys, GRID(ndel, BS), dim3(BS), 0, st, d_del_keys, klen, ndel, K + 4 * nup);
+  if (h->flags & KH_HASH_KEYS) {
+    if (F.nup) hipLaunchKernelGGL(k_hash_keys, GRID(F.nup, BS), dim3(BS), 0, st, F.up_keys, F.klen, F.nup, K);
+    if (F.ndel)
+      hipLaunchKernelGGL(k_hash_keys, GRID(F.ndel, BS), dim3(BS), 0, st, F.del_keys, F.klen, F.ndel, K + 4 * F.nup);
     LAUNCH_CHECK();
   } else {
-    if (nup) HIPCHK(hipMemcpyAsync(K, d_up_keys, nup * 32, hipMemcpyDeviceToDevice, st));
-    if (ndel) HIPCHK(hipMemcpyAsync(K + 4 * nup, d_del_keys, ndel * 32, hipMemcpyDeviceToDevice, st));
+    if (F.nup) HIPCHK(hipMemcpyAsync(K, F.up_keys, F.nup * 32, hipMemcpyDeviceToDevice, st));
+    if (F.ndel) HIPCHK(hipMemcpyAsync(K + 4 * F.nup, F.del_keys, F.ndel * 32, hipMemcpyDeviceToDevice, st));
+  }
+  if (segd) {
+    if (F.nup) {
+      if (!F.up_trie) throw KhError{KH_EINVAL, "forest ops need trie ids"};
+      HIPCHK(hipMemcpyAsync(Tid, F.up_trie, F.nup * 4, hipMemcpyDeviceToDevice, st));
+    }
+    if (F.ndel) {
+      if (!F.del_trie) throw KhError{KH_EINVAL, "forest ops need trie ids"};
+      HIPCHK(hipMemcpyAsync(Tid + F.nup, F.del_trie, F.ndel * 4, hipMemcpyDeviceToDevice, st));
+    }
   }
   sort_dedup(c, S);
-  const uint64_t nsorted = S.m;
-
-  // ---- 2. merge into the other half of the double buffers
-  M.rkey = (const uint64_t*)h->key[cur].p;
-  M.roff = (const uint64_t*)h->off[cur].p;
-  M.m = m;
-  M.okey = S.skey;
-  M.oidx = S.sidx;
-  M.nops = nsorted;
-  M.nup = nup;
-  M.uoff = d_up_voff;
-  h->key[nxt].ensure(mx * 32 + 64);
-  M.nkey = (uint64_t*)h->key[nxt].p;
-  HIPCHK(hipMemsetAsync(M.pos_cnt, 0, (m + 1) * 4, st));
-  HIPCHK(hipMemsetAsync(del_flag, 0, (m + 1) * 4, st));
-  HIPCHK(hipMemsetAsync(M.pos_upd, 0xFF, (m + 1) * 4, st));
-  hipLaunchKernelGGL(k_op_locate, GRID(nsorted, BS), dim3(BS), 0, st, M);
-  LAUNCH_CHECK();
-  HIPCHK(hipMemcpyAsync(o_insf, M.o_ins, nsorted * 4, hipMemcpyDeviceToDevice, st));
-  HIPCHK(hipMemcpyAsync(o_efff, M.o_eff, nsorted * 4, hipMemcpyDeviceToDevice, st));
-  Merge Mk = M;
-  Mk.pos_del = del_flag;  // op_mark writes the raw flags
-  hipLaunchKernelGGL(k_op_mark, GRID(nsorted, BS), dim3(BS), 0, st, Mk);
-  LAUNCH_CHECK();
-  unsigned long long* tot = S.ctr + 12;  // inserts, deletes, dirty keys, value bytes (slots the sort left free)
-  scan_exclusive<uint32_t>(M.pos_cnt, M.pos_ins, m + 1, (uint32_t*)(tot + 0), S.scan_scratch, st);
-  scan_exclusive<uint32_t>(del_flag, M.pos_del, m + 1, (uint32_t*)(tot + 1), S.scan_scratch, st);
-  scan_exclusive<uint32_t>(o_insf, M.o_ins, nsorted, (uint32_t*)nullptr, S.scan_scratch, st);
-  scan_exclusive<uint32_t>(o_efff, M.o_eff, nsorted, (uint32_t*)(tot + 2), S.scan_scratch, st);
-  HIPCHK(hipMemcpyAsync(c->h_pinned, tot, 3 * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  const uint64_t n_ins = (uint32_t)c->h_pinned[0], n_del = (uint32_t)c->h_pinned[1], nd = (uint32_t)c->h_pinned[2];
-  const uint64_t m2 = m + n_ins - n_del;
-  if (n_ins > nsorted || n_del > m || nd > nsorted || m2 > mx)
-    throw KhError{KH_EINTERNAL, "merge: inconsistent batch counts"};
-  if (stats) {
-    stats->n_inputs = nops;
-    stats->n_leaves = m2;
-  }
-  if (nd == 0) return;  // nothing changes: same root
-  if (m) hipLaunchKernelGGL(k_place_resident, GRID(m, BS), dim3(BS), 0, st, M, (const uint32_t*)del_flag);
-  hipLaunchKernelGGL(k_place_op, GRID(nsorted, BS), dim3(BS), 0, st, M, (const uint32_t*)o_insf,
-                     (const uint32_t*)o_efff);
-  LAUNCH_CHECK();
-  h->off[nxt].ensure((m2 + 1) * 8 + 64);
-  uint64_t* noff = (uint64_t*)h->off[nxt].p;
-  HIPCHK(hipMemsetAsync(noff, 0, (m2 + 1) * 8, st));
-  if (m2) {
-    hipLaunchKernelGGL(k_u32_to_u64, GRID(m2, BS), dim3(BS), 0, st, (const uint32_t*)M.nlen, len64, m2);
+  const uint64_t nd = S.m;
+  uint32_t* otrie = sseg;
+  if (!segd) {
+    hipLaunchKernelGGL(k_u32_fill, GRID(nd, BS), dim3(BS), 0, st, otrie, nd, 0u);
     LAUNCH_CHECK();
-    scan_exclusive<uint64_t>(len64, noff, m2, (uint64_t*)(tot + 3), S.scan_scratch, st);
-    HIPCHK(hipMemcpyAsync(noff + m2, tot + 3, 8, hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->h_pinned, tot + 3, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(c->h_pinned + 1, M.roff + m, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(c->h_pinned + 2, d_up_voff ? d_up_voff + nup : M.roff, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (c->h_pinned[0] > c->h_pinned[1] + (nup ? c->h_pinned[2] : 0))
-      throw KhError{KH_EINTERNAL, "merge: value bytes exceed resident + upserts (" + std::to_string(c->h_pinned[0]) +
-                                      " > " + std::to_string(c->h_pinned[1]) + " + " +
-                                      std::to_string(nup ? c->h_pinned[2] : 0) + ")"};
-    h->val[nxt].ensure(c->h_pinned[0] + 64);
-    hipLaunchKernelGGL(k_merge_vals, GRID(m2 * CG, BS), dim3(BS), 0, st, (const uint64_t*)M.nsrc, (const uint32_t*)M.nlen,
-                       (const uint64_t*)noff, m2, (const uint8_t*)h->val[cur].p, d_up_vals,
-                       (uint8_t*)h->val[nxt].p);
+  }
+  hipLaunchKernelGGL(k_f_kinds, GRID(nd, BS), dim3(BS), 0, st, (const uint32_t*)S.sidx, nd, F.nup, kind);
+  LAUNCH_CHECK();
+  FOps O{(const uint64_t*)S.skey, (const uint32_t*)otrie, (const uint8_t*)kind, nd};
+  // distinct tries of the batch (sorted): the segments of the element build
+  hipLaunchKernelGGL(k_f_trie_flags, GRID(nd, BS), dim3(BS), 0, st, (const uint32_t*)otrie, nd, tflag);
+  LAUNCH_CHECK();
+  uint32_t* ntp = (uint32_t*)(S.ctr + 12);
+  scan_exclusive<uint32_t>(tflag, tpos, nd, ntp, S.scan_scratch, st);
+  // upserts: ranks and value offsets (their values go to the heap)
+  hipLaunchKernelGGL(k_f_upsert_len, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)S.sidx, F.up_voff, ulen, isup);
+  LAUNCH_CHECK();
+  uint32_t* nupp = (uint32_t*)(S.ctr + 13);
+  scan_exclusive<uint32_t>(isup, ur, nd, nupp, S.scan_scratch, st);
+  scan_exclusive<uint64_t>(ulen, uoff, nd, (uint64_t*)(S.ctr + 14), S.scan_scratch, st);
+  HIPCHK(hipMemcpyAsync(c->h_pinned, S.ctr + 12, 3 * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint32_t nt = (uint32_t)c->h_pinned[0], nups = (uint32_t)c->h_pinned[1];
+  const uint64_t ubytes = c->h_pinned[2];
+  // ---- trie list
+  h->tbuf.ensure(carve_size({(uint64_t)nt * 4, (uint64_t)nt * 32}));
+  Carver ct{(char*)h->tbuf.p, 0, h->tbuf.cap};
+  uint32_t* tries = ct.take<uint32_t>(nt);
+  uint64_t* roots = ct.take<uint64_t>((uint64_t)nt * 4);
+  hipLaunchKernelGGL(k_f_trie_list, GRID(nd, BS), dim3(BS), 0, st, (const uint32_t*)otrie, (const uint32_t*)tflag,
+                     (const uint32_t*)tpos, nd, tries);
+  LAUNCH_CHECK();
+  // ---- 2. descent: opened branches and touched leaves
+  recs_reserve(h, h->rn + 16);
+  if (h->mcap == 0) map_rebuild(h, nops + 1024);
+  h->tlb.ensure(carve_size({nd * 70 * 4 + 64, 64}));
+  Carver c3{(char*)h->tlb.p, 0, h->tlb.cap};
+  uint32_t* tlist = c3.take<uint32_t>(nd * 70 + 16);
+  unsigned long long* fctr = c3.take<unsigned long long>(8);
+  HIPCHK(hipMemsetAsync(fctr, 0, 64, st));
+  hipLaunchKernelGGL(k_f_descend, GRID(nd, BS), dim3(BS), 0, st, O, map_of(h), recs_of(h), (uint32_t*)h->touched.p,
+                     (uint8_t*)h->replaced.p, tlist, fctr);
+  LAUNCH_CHECK();
+  HIPCHK(hipMemcpyAsync(c->h_pinned, fctr, 24, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint64_t ntl = c->h_pinned[0], nrep = c->h_pinned[1];
+  if (c->h_pinned[2]) throw KhError{KH_EINTERNAL, "forest descent: corrupt anchor map"};
+  // ---- 3. elements: upserts (values appended to the heap), untouched children, kept leaves, roots
+  const uint64_t ecap = (uint64_t)nups + 16 * ntl + nt + 16;
+  regrow(h->heap, h->heap_n, h->heap_n + ubytes + 64, st);
+  const uint64_t hb = h->heap_n;
+  h->ebuf.ensure(carve_size({ecap * 32, ecap * 4, ecap, ecap * 32, ecap, ecap * 8, ecap * 4, ecap * 4, ecap, 64}));
+  Carver ce{(char*)h->ebuf.p, 0, h->ebuf.cap};
+  Elems E{};
+  E.key = ce.take<uint64_t>(ecap * 4);
+  E.seg = ce.take<uint32_t>(ecap);
+  E.db = ce.take<uint8_t>(ecap);
+  E.bref = ce.take<uint64_t>(ecap * 4);
+  E.brl = ce.take<uint8_t>(ecap);
+  E.vo = ce.take<uint64_t>(ecap);
+  E.vl = ce.take<uint32_t>(ecap);
+  E.src = ce.take<uint32_t>(ecap);
+  E.oldd = ce.take<uint8_t>(ecap);
+  E.n = ce.take<unsigned long long>(8);
+  E.cap = ecap;
+  // upsert values: uoff is the exclusive scan of their lengths over the sorted ops;
+  // uo = the same offsets indexed by upsert rank (uo[nups] = total)
+  h->ubuf.ensure(((uint64_t)nups + 1) * 8 + 64);
+  uint64_t* uo = (uint64_t*)h->ubuf.p;
+  hipLaunchKernelGGL(k_f_rank_scatter, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)ur, (const uint64_t*)uoff,
+                     uo, (uint64_t)nups, ubytes);
+  LAUNCH_CHECK();
+  if (ubytes)
+    hipLaunchKernelGGL(k_f_heap_copy, GRID(nd * CG, BS), dim3(BS), 0, st, O, (const uint32_t*)S.sidx,
+                       (const uint32_t*)ur, F.up_vals, F.up_voff, (const uint64_t*)uo, (uint8_t*)h->heap.p, hb);
+  LAUNCH_CHECK();
+  c->h_pinned[8] = nups;  // the record elements are pushed after the upserts
+  HIPCHK(hipMemcpyAsync(E.n, c->h_pinned + 8, 8, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_f_upsert_elems, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)tries, nt,
+                     (const uint32_t*)ur, (const uint64_t*)uo, E, hb);
+  LAUNCH_CHECK();
+  if (ntl)
+    hipLaunchKernelGGL(k_f_gather, GRID(ntl, BS), dim3(BS), 0, st, map_of(h), recs_of(h),
+                       (const uint32_t*)h->touched.p, (const uint8_t*)h->replaced.p, (const uint32_t*)tlist, ntl,
+                       (const uint32_t*)tries, nt, E, fctr);
+  hipLaunchKernelGGL(k_f_gather_roots, GRID(nt, BS), dim3(BS), 0, st, map_of(h), recs_of(h),
+                     (const uint32_t*)h->touched.p, (const uint32_t*)tries, nt, E);
+  LAUNCH_CHECK();
+  HIPCHK(hipMemcpyAsync(c->h_pinned, E.n, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(c->h_pinned + 1, fctr + 2, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint64_t ne = c->h_pinned[0];
+  if (c->h_pinned[1]) throw KhError{KH_EINTERNAL, "forest gather: corrupt anchor map"};
+  if (ne > ecap) throw KhError{KH_EINTERNAL, "forest gather: element overflow"};
+  h->heap_n = hb + ubytes;
+  HIPCHK(hipEventRecord(c->ev[7], st));
+  // ---- 4. element build (every touched trie a segment), or all tries emptied
+  BuildOut O2;
+  kh_stats bst{};
+  uint64_t B = 0, m = 0;
+  const bool keep_em = h->flags & KH_EMIT_NODES;
+  if (ne) {
+    ElemArgs EA{E.db, E.bref, E.brl, &h->elout};
+    BuildArgs A{(const uint8_t*)E.key, 32, (const uint8_t*)h->heap.p, (const uint64_t*)E.vo, ne,
+                nt > 1 ? (const uint32_t*)E.seg : nullptr, nt, 0, 0, true};
+    A.vlen = E.vl;
+    A.el = &EA;
+    run_build(c, A, O2, &bst);
+    B = c->last_B;
+    m = c->T.m;
+    if (m != ne) throw KhError{KH_EINTERNAL, "forest: duplicate elements"};
+  }
+  // ---- 5. records: new branches, re-anchored / new elements; the anchor map follows
+  const uint64_t nnew = nups;  // every upsert is a new leaf record
+  recs_reserve(h, h->rn + B + nnew + 16);
+  const uint64_t base_b = h->rn, base_e = h->rn + B;
+  Recs R = recs_of(h);
+  AMap M = map_of(h);
+  uint32_t *isnew = nullptr, *nrank = nullptr, *eid = nullptr, *esrc = nullptr;
+  uint8_t* sel = nullptr;
+  if (ne) {
+    h->selb.ensure(carve_size({m + 2 * B, m * 4, m * 4, m * 4, m * 4, scan_scratch_bytes(m + 1, 4), 64}));
+    Carver cs{(char*)h->selb.p, 0, h->selb.cap};
+    sel = cs.take<uint8_t>(m + 2 * B);
+    isnew = cs.take<uint32_t>(m);
+    nrank = cs.take<uint32_t>(m);
+    eid = cs.take<uint32_t>(m);
+    esrc = cs.take<uint32_t>(m);
+    void* sscr = cs.take<char>(scan_scratch_bytes(m + 1, 4));
+    uint32_t* tot = cs.take<uint32_t>(8);
+    Topo T = c->T;
+    if (B)
+      hipLaunchKernelGGL(k_f_branch_recs, GRID(B, BS), dim3(BS), 0, st, T, (const uint32_t*)(T.ctr + CTR_B),
+                         (const uint32_t*)tries, M, R, base_b, sel);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_f_elem_sel, GRID(m, BS), dim3(BS), 0, st, T, E, sel);
+    hipLaunchKernelGGL(k_f_elem_new, GRID(m, BS), dim3(BS), 0, st, T, E, isnew);
+    hipLaunchKernelGGL(k_f_elem_src, GRID(m, BS), dim3(BS), 0, st, T, E, esrc);
+    LAUNCH_CHECK();
+    scan_exclusive<uint32_t>(isnew, nrank, m, tot, sscr, st);
+    // old anchors out of the map (touched records, element sources), then touched records die
+    if (ntl) hipLaunchKernelGGL(k_map_delete, GRID(ntl, BS), dim3(BS), 0, st, M, R, (const uint32_t*)tlist, ntl);
+    hipLaunchKernelGGL(k_map_delete, GRID(m, BS), dim3(BS), 0, st, M, R, (const uint32_t*)esrc, m);
+    LAUNCH_CHECK();
+    if (ntl)
+      hipLaunchKernelGGL(k_rec_dead, GRID(ntl, BS), dim3(BS), 0, st, R, (const uint32_t*)tlist, ntl,
+                         (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_f_elem_recs, GRID(m, BS), dim3(BS), 0, st, T, E, (const uint32_t*)tries,
+                       (const uint32_t*)nrank, R, base_e, eid);
+    LAUNCH_CHECK();
+    // map capacity: rebuild when live + tombstones would pass half the table
+    h->rn = base_e + nnew;
+    if (2 * (h->mused + B + m + 1024) > h->mcap) {
+      map_rebuild(h, B + m);
+    } else {
+      unsigned long long* err = fctr + 3;
+      if (B)
+        hipLaunchKernelGGL(k_map_insert, GRID(B, BS), dim3(BS), 0, st, M, R, (const uint32_t*)nullptr, base_b, B, err);
+      hipLaunchKernelGGL(k_map_insert, GRID(m, BS), dim3(BS), 0, st, M, R, (const uint32_t*)eid, (uint64_t)0, m, err);
+      LAUNCH_CHECK();
+      h->mused += B + m;
+    }
+    hipLaunchKernelGGL(k_f_roots, GRID(nt, BS), dim3(BS), 0, st, (const uint64_t*)T.res_hash,
+                       (const uint32_t*)T.res_len, nt, roots);
     LAUNCH_CHECK();
   } else {
-    h->val[nxt].ensure(64);
+    if (ntl) hipLaunchKernelGGL(k_map_delete, GRID(ntl, BS), dim3(BS), 0, st, M, R, (const uint32_t*)tlist, ntl);
+    if (ntl)
+      hipLaunchKernelGGL(k_rec_dead, GRID(ntl, BS), dim3(BS), 0, st, R, (const uint32_t*)tlist, ntl,
+                         (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p);
+    hipLaunchKernelGGL(k_f_roots, GRID(nt, BS), dim3(BS), 0, st, (const uint64_t*)nullptr, (const uint32_t*)nullptr,
+                       nt, roots);
+    LAUNCH_CHECK();
   }
-  HIPCHK(hipEventRecord(c->ev[7], st));
-
-  // ---- 3. topology of the merged set + hashing of the dirty branches
-  IncArgs I = inc_out(h, nxt);
-  I.dkey = M.dkey;
-  I.nd = nd;
-  I.V.P = h->P;
-  I.V.bid = (const uint32_t*)h->bid.p;
-  I.V.ref = (const uint64_t*)h->ref[cur].p;
-  I.V.rlen = (const uint32_t*)h->rlen[cur].p;
-  I.V.nb = h->nb;
-  I.V.oldpos = M.oldpos;
-  I.V.upd = M.nupd;
-  I.V.lpd = (const int8_t*)h->lpd.p;
-  I.V.lref = (const uint64_t*)h->lref[cur].p;
-  I.V.lrlen = (const uint32_t*)h->lrlen[cur].p;
-  BuildArgs A{(const uint8_t*)h->key[nxt].p, 32, (const uint8_t*)h->val[nxt].p, noff, m2, nullptr, 1, 0, 0, false};
-  A.presorted = true;
-  A.inc = &I;
-  BuildOut O;
-  kh_stats bst{};
-  run_build(c, A, O, &bst);
+  h->rn = base_e + nnew;
+  h->nleaves = h->nleaves + nups - nrep;
+  // ---- 6. this commit's write-back set (kept on the device for kh_trie_emit_nodes)
+  if (keep_em && ne) {
+    c->T.emit_sel = sel;
+    uint64_t en = 0, eb2 = 0;
+    emit_nodes_dev(c, h->em, &en, &eb2);
+    c->T.emit_sel = nullptr;
+    h->em_n = en;
+    h->em_bytes = eb2;
+    h->em_valid = true;
+  } else if (keep_em) {
+    h->em_n = h->em_bytes = 0;
+    h->em_valid = true;
+  }
+  // ---- roots to the host
+  h->tries.resize(nt);
+  h->roots.resize((uint64_t)nt * 32);
+  HIPCHK(hipMemcpyAsync(h->tries.data(), tries, (uint64_t)nt * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(h->roots.data(), roots, (uint64_t)nt * 32, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(c->h_pinned, fctr + 3, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (c->h_pinned[0]) throw KhError{KH_EINTERNAL, "anchor map insert failed"};
+  if (!h->forest) memcpy(h->root, nt ? h->roots.data() : h->root, 32);
   float merge_ms = ev_ms(c->ev[6], c->ev[7]);
   if (stats) {
     *stats = bst;
     stats->n_inputs = nops;
-    stats->t_sort_ms = merge_ms;  // batch sort + merge
+    stats->n_leaves = h->nleaves;
+    stats->t_sort_ms = merge_ms;  // batch sort + descent + element gather
     stats->t_total_ms += merge_ms;
   }
-  h->cur = nxt;
-  h->m = m2;
-  h->P = I.P;
-  h->nb = I.nb;
-  copy_root(O, 0, h->root);
 }
 
 // ---------------------------------------------------------------------------
@@ -1906,7 +2294,8 @@ int kh_ctx_destroy(kh_ctx* c) {
   API_TRY({
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->st);
-    for (DevBuf* b : {&c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->out_emit})
+    for (DevBuf* b : {&c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->out_emit,
+                      &c->emit_dev})
       b->release();
     for (auto& e : c->ev)
       if (e) (void)hipEventDestroy(e);
@@ -2005,10 +2394,20 @@ int kh_trie_roots_segmented(const uint8_t* keys, uint32_t klen, const uint8_t* v
 }
 
 // Emission of the node set of the build just run on c (c->T): every node reachable from
-// the root whose encoding is >= 32 B, plus the root node (MerklePatriciaTrie.scala:505-511).
-// Host outputs; KH_ENOSPC with the needed sizes in *n_nodes / *rlp_len.
-static int emit_node_set(kh_ctx* c, uint8_t* hashes32, uint64_t node_cap, uint8_t* rlp, uint64_t rlp_cap,
-                         uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len) {
+// the root whose encoding is >= 32 B, plus the root node (MerklePatriciaTrie.scala:505-511),
+// restricted to T.emit_sel when set.  Device output in `out`: hashes | rlp | off.
+struct EmitLayout {
+  uint8_t* hashes;
+  uint8_t* rlp;
+  uint64_t* off;
+};
+static EmitLayout emit_layout(DevBuf& out, uint64_t tn, uint64_t tb) {
+  uint8_t* oh = (uint8_t*)out.p;
+  uint8_t* orlp = oh + ((tn * 32 + 255) & ~255ULL);
+  uint64_t* ooff = (uint64_t*)(orlp + ((tb + 255) & ~255ULL));
+  return EmitLayout{oh, orlp, ooff};
+}
+static int emit_nodes_dev(kh_ctx* c, DevBuf& out, uint64_t* n_nodes, uint64_t* rlp_len) {
   Topo& T = c->T;
   uint64_t B = c->last_B;
   uint64_t Q = T.m + 2 * B;
@@ -2018,42 +2417,45 @@ static int emit_node_set(kh_ctx* c, uint8_t* hashes32, uint64_t node_cap, uint8_
   Carver c3{(char*)c->ws3.p, 0, c->ws3.cap};
   uint32_t* flag = c3.take<uint32_t>(Q);
   uint64_t* bytes = c3.take<uint64_t>(Q);
-  char* sscr = c3.take<char>(scan_scratch_bytes(Q, 8));
-  (void)sscr;
   hipStream_t st = c->st;
   hipLaunchKernelGGL(k_emit_sizes, GRID(Q, BS), dim3(BS), 0, st, T, B, flag, bytes);
   LAUNCH_CHECK();
-  // totals: reuse the build's counter block
   uint64_t* totb = (uint64_t*)(T.ctr + CTR_E0);
   uint32_t* totn = (uint32_t*)(T.ctr + CTR_E1);
   HIPCHK(hipMemsetAsync(T.ctr + CTR_E0, 0, 16, st));
-  // scan scratch: ws1's scan scratch may be too small for Q; use a dedicated buffer
   c->out_emit.ensure(scan_scratch_bytes(Q, 8) + 256);
   scan_exclusive<uint64_t>(bytes, bytes, Q, totb, c->out_emit.p, st);
   scan_exclusive<uint32_t>(flag, flag, Q, totn, c->out_emit.p, st);
   HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_E0, 16, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  uint64_t tb = c->h_pinned[0];
-  uint64_t tn = (uint32_t)c->h_pinned[1];
+  const uint64_t tb = c->h_pinned[0], tn = (uint32_t)c->h_pinned[1];
+  out.ensure(tn * 32 + tb + (tn + 1) * 8 + 1024);
+  EmitLayout Lo = emit_layout(out, tn, tb);
+  hipLaunchKernelGGL(k_emit_copy, GRID(Q, BS), dim3(BS), 0, st, T, B, (const uint32_t*)flag, (const uint64_t*)bytes,
+                     Lo.hashes, Lo.rlp, Lo.off);
+  LAUNCH_CHECK();
+  c->h_pinned[2] = tb;
+  HIPCHK(hipMemcpyAsync(Lo.off + tn, c->h_pinned + 2, 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));
   *n_nodes = tn;
   *rlp_len = tb;
-  if (tn > node_cap || tb > rlp_cap || !hashes32 || !rlp || !off) return set_err(KH_ENOSPC, "output too small");
-  // device output: hashes | rlp | off
-  DevBuf outb;
-  outb.ensure(tn * 32 + tb + (tn + 1) * 8 + 1024);
-  uint8_t* oh = (uint8_t*)outb.p;
-  uint8_t* orlp = oh + ((tn * 32 + 255) & ~255ULL);
-  uint64_t* ooff = (uint64_t*)(orlp + ((tb + 255) & ~255ULL));
-  // re-derive flags (scan overwrote them with positions; emission re-tests each node)
-  hipLaunchKernelGGL(k_emit_copy, GRID(Q, BS), dim3(BS), 0, st, T, B, (const uint32_t*)flag,
-                     (const uint64_t*)bytes, oh, orlp, ooff);
-  LAUNCH_CHECK();
-  HIPCHK(hipMemcpyAsync(hashes32, oh, tn * 32, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(rlp, orlp, tb, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(off, ooff, tn * 8, hipMemcpyDeviceToHost, st));
+  return KH_OK;
+}
+// host copy of an emitted node set; KH_ENOSPC with the sizes when the caller's buffers are short
+static int emit_to_host(kh_ctx* c, DevBuf& src, uint64_t tn, uint64_t tb, uint8_t* hashes32, uint64_t node_cap,
+                        uint8_t* rlp, uint64_t rlp_cap, uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len) {
+  *n_nodes = tn;
+  *rlp_len = tb;
+  if (tn > node_cap || tb > rlp_cap || !hashes32 || !rlp || !off) {
+    if (tn == 0 && off) off[0] = 0;
+    return (tn == 0) ? KH_OK : set_err(KH_ENOSPC, "output too small");
+  }
+  EmitLayout Lo = emit_layout(src, tn, tb);
+  hipStream_t st = c->st;
+  if (tn) HIPCHK(hipMemcpyAsync(hashes32, Lo.hashes, tn * 32, hipMemcpyDeviceToHost, st));
+  if (tb) HIPCHK(hipMemcpyAsync(rlp, Lo.rlp, tb, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(off, Lo.off, (tn + 1) * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  off[tn] = tb;
-  outb.release();
   return KH_OK;
 }
 
@@ -2077,7 +2479,9 @@ int kh_trie_root_nodes(const uint8_t* keys, uint32_t klen, const uint8_t* vals, 
     BuildOut O;
     run_build(c, A, O, stats);
     copy_root(O, 0, root32);
-    return emit_node_set(c, hashes32, node_cap, rlp, rlp_cap, off, n_nodes, rlp_len);
+    uint64_t tn = 0, tb = 0;
+    emit_nodes_dev(c, c->emit_dev, &tn, &tb);
+    return emit_to_host(c, c->emit_dev, tn, tb, hashes32, node_cap, rlp, rlp_cap, off, n_nodes, rlp_len);
   })
 }
 
@@ -2268,18 +2672,36 @@ int kh_verify_nodes(const uint8_t* data, const uint64_t* off, uint64_t n, const 
   })
 }
 
+static kh_trie* trie_new(kh_ctx* c, uint32_t flags, bool forest) {
+  kh_trie* h = new kh_trie();
+  h->c = c;
+  h->flags = flags;
+  h->forest = forest;
+  memcpy(h->root, EMPTY_TRIE_HASH, 32);
+  return h;
+}
+static void check_flags(const kh_trie* h, uint32_t flags) {
+  if ((flags & KH_HASH_KEYS) != (h->flags & KH_HASH_KEYS))
+    throw KhError{KH_EINVAL, "KH_HASH_KEYS differs from the flag the trie was opened with"};
+}
+
 int kh_trie_open(kh_ctx* c, const uint8_t* d_keys, uint32_t klen, const uint8_t* d_vals, const uint64_t* d_voff,
                  uint64_t n, uint32_t flags, uint8_t root32[32], kh_trie** out) {
   if (!c || !out) return set_err(KH_EINVAL, "null context or handle");
   kh_trie* h = nullptr;
   API_TRY({
     HIPCHK(hipSetDevice(c->dev));
-    h = new kh_trie();
-    h->c = c;
+    h = trie_new(c, flags, false);
     try {
-      trie_open(h, d_keys, klen, d_vals, d_voff, n, flags, nullptr);
+      FCommit F;
+      F.up_keys = d_keys;
+      F.up_vals = d_vals;
+      F.up_voff = d_voff;
+      F.nup = n;
+      F.klen = klen;
+      forest_commit(h, F, nullptr);
     } catch (...) {
-      kh_trie_free(h);
+      delete h;
       h = nullptr;
       throw;
     }
@@ -2288,14 +2710,211 @@ int kh_trie_open(kh_ctx* c, const uint8_t* d_keys, uint32_t klen, const uint8_t*
   })
 }
 
+int kh_trie_open_host(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const uint64_t* voff, uint64_t n,
+                      uint32_t flags, uint8_t root32[32], kh_trie** out) {
+  if (!out || (n && (!keys || !voff))) return set_err(KH_EINVAL, "null input");
+  API_TRY({
+    kh_ctx* c = shared_ctx(current_device());
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->dev));
+    Staged S = stage_inputs(c, keys, klen, vals, voff, n, nullptr);
+    int rc = kh_trie_open(c, S.keys, klen, S.vals, S.voff, n, flags, root32, out);
+    if (rc != KH_OK) return rc;
+  })
+}
+
 int kh_trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals, const uint64_t* d_up_voff,
                   uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
                   uint8_t root32[32], kh_stats* stats) {
-  if (!h) return set_err(KH_EINVAL, "null handle");
+  if (!h || h->forest) return set_err(KH_EINVAL, "null handle or a forest (use kh_forest_apply)");
   API_TRY({
     HIPCHK(hipSetDevice(h->c->dev));
-    trie_apply(h, d_up_keys, d_up_vals, d_up_voff, nup, d_del_keys, ndel, klen, flags, stats);
+    check_flags(h, flags);
+    FCommit F;
+    F.up_keys = d_up_keys;
+    F.up_vals = d_up_vals;
+    F.up_voff = d_up_voff;
+    F.nup = nup;
+    F.del_keys = d_del_keys;
+    F.ndel = ndel;
+    F.klen = klen;
+    forest_commit(h, F, stats);
     if (root32) memcpy(root32, h->root, 32);
+  })
+}
+
+// host batch -> the context's staging buffers (keys of both kinds share in_keys)
+static FCommit stage_commit(kh_ctx* c, const uint32_t* up_trie, const uint8_t* up_keys, const uint8_t* up_vals,
+                            const uint64_t* up_voff, uint64_t nup, const uint32_t* del_trie, const uint8_t* del_keys,
+                            uint64_t ndel, uint32_t klen) {
+  hipStream_t st = c->st;
+  const uint64_t v0 = nup ? up_voff[0] : 0, vb = nup ? up_voff[nup] - v0 : 0;
+  c->in_keys.ensure(carve_size({nup * klen, ndel * klen}));
+  c->in_vals.ensure(vb + 64);
+  c->in_voff.ensure((nup + 1) * 8 + 64);
+  c->in_seg.ensure(carve_size({nup * 4, ndel * 4}));
+  Carver ck{(char*)c->in_keys.p, 0, c->in_keys.cap};
+  uint8_t* uk = ck.take<uint8_t>(nup * klen);
+  uint8_t* dk = ck.take<uint8_t>(ndel * klen);
+  Carver cs{(char*)c->in_seg.p, 0, c->in_seg.cap};
+  uint32_t* ut = cs.take<uint32_t>(nup);
+  uint32_t* dt = cs.take<uint32_t>(ndel);
+  std::vector<uint64_t> rel(nup + 1, 0);
+  for (uint64_t i = 0; i <= nup && nup; ++i) rel[i] = up_voff[i] - v0;
+  if (nup) {
+    HIPCHK(hipMemcpyAsync(uk, up_keys, nup * klen, hipMemcpyHostToDevice, st));
+    if (vb) HIPCHK(hipMemcpyAsync(c->in_vals.p, up_vals + v0, vb, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->in_voff.p, rel.data(), (nup + 1) * 8, hipMemcpyHostToDevice, st));
+    if (up_trie) HIPCHK(hipMemcpyAsync(ut, up_trie, nup * 4, hipMemcpyHostToDevice, st));
+  }
+  if (ndel) {
+    HIPCHK(hipMemcpyAsync(dk, del_keys, ndel * klen, hipMemcpyHostToDevice, st));
+    if (del_trie) HIPCHK(hipMemcpyAsync(dt, del_trie, ndel * 4, hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));  // `rel` is a host temporary
+  FCommit F;
+  F.up_trie = up_trie ? ut : nullptr;
+  F.up_keys = uk;
+  F.up_vals = (const uint8_t*)c->in_vals.p;
+  F.up_voff = (const uint64_t*)c->in_voff.p;
+  F.nup = nup;
+  F.del_trie = del_trie ? dt : nullptr;
+  F.del_keys = dk;
+  F.ndel = ndel;
+  F.klen = klen;
+  return F;
+}
+
+int kh_trie_apply_host(kh_trie* h, const uint8_t* up_keys, const uint8_t* up_vals, const uint64_t* up_voff,
+                       uint64_t nup, const uint8_t* del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
+                       uint8_t root32[32], kh_stats* stats) {
+  if (!h || h->forest) return set_err(KH_EINVAL, "null handle or a forest (use kh_forest_apply_host)");
+  API_TRY({
+    std::lock_guard<std::mutex> g(h->c->mu);
+    HIPCHK(hipSetDevice(h->c->dev));
+    check_flags(h, flags);
+    FCommit F = stage_commit(h->c, nullptr, up_keys, up_vals, up_voff, nup, nullptr, del_keys, ndel, klen);
+    forest_commit(h, F, stats);
+    if (root32) memcpy(root32, h->root, 32);
+  })
+}
+
+int kh_forest_open(kh_ctx* c, uint32_t flags, kh_trie** out) {
+  if (!c || !out) return set_err(KH_EINVAL, "null context or handle");
+  API_TRY({ *out = trie_new(c, flags, true); })
+}
+
+static int forest_out(kh_trie* f, uint32_t* h_tries, uint8_t* h_roots32, uint64_t cap, uint64_t* n_tries) {
+  const uint64_t nt = f->tries.size();
+  if (n_tries) *n_tries = nt;
+  if (nt > cap || (nt && (!h_tries || !h_roots32))) return set_err(KH_ENOSPC, "trie output too small");
+  if (nt) {
+    memcpy(h_tries, f->tries.data(), nt * 4);
+    memcpy(h_roots32, f->roots.data(), nt * 32);
+  }
+  return KH_OK;
+}
+
+int kh_forest_apply(kh_trie* f, const uint32_t* d_up_trie, const uint8_t* d_up_keys, const uint8_t* d_up_vals,
+                    const uint64_t* d_up_voff, uint64_t nup, const uint32_t* d_del_trie, const uint8_t* d_del_keys,
+                    uint64_t ndel, uint32_t klen, uint32_t* h_tries, uint8_t* h_roots32, uint64_t cap,
+                    uint64_t* n_tries, kh_stats* stats) {
+  if (!f || !f->forest) return set_err(KH_EINVAL, "null handle or not a forest");
+  API_TRY({
+    HIPCHK(hipSetDevice(f->c->dev));
+    FCommit F;
+    F.up_trie = d_up_trie;
+    F.up_keys = d_up_keys;
+    F.up_vals = d_up_vals;
+    F.up_voff = d_up_voff;
+    F.nup = nup;
+    F.del_trie = d_del_trie;
+    F.del_keys = d_del_keys;
+    F.ndel = ndel;
+    F.klen = klen;
+    forest_commit(f, F, stats);
+    return forest_out(f, h_tries, h_roots32, cap, n_tries);
+  })
+}
+
+int kh_forest_apply_host(kh_trie* f, const uint32_t* up_trie, const uint8_t* up_keys, const uint8_t* up_vals,
+                         const uint64_t* up_voff, uint64_t nup, const uint32_t* del_trie, const uint8_t* del_keys,
+                         uint64_t ndel, uint32_t klen, uint32_t* h_tries, uint8_t* h_roots32, uint64_t cap,
+                         uint64_t* n_tries, kh_stats* stats) {
+  if (!f || !f->forest) return set_err(KH_EINVAL, "null handle or not a forest");
+  if ((nup && !up_trie) || (ndel && !del_trie)) return set_err(KH_EINVAL, "forest ops need trie ids");
+  API_TRY({
+    std::lock_guard<std::mutex> g(f->c->mu);
+    HIPCHK(hipSetDevice(f->c->dev));
+    FCommit F = stage_commit(f->c, up_trie, up_keys, up_vals, up_voff, nup, del_trie, del_keys, ndel, klen);
+    forest_commit(f, F, stats);
+    return forest_out(f, h_tries, h_roots32, cap, n_tries);
+  })
+}
+
+int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_trie, const uint8_t* d_s_up_keys,
+                    const uint8_t* d_s_up_vals, const uint64_t* d_s_up_voff, uint64_t ns_up,
+                    const uint32_t* d_s_del_trie, const uint8_t* d_s_del_keys, uint64_t ns_del, uint32_t s_klen,
+                    const uint8_t* d_a_up_keys, uint8_t* d_a_up_vals, const uint64_t* d_a_up_voff,
+                    const uint32_t* d_a_up_trie, uint64_t na_up, const uint8_t* d_a_del_keys, uint64_t na_del,
+                    uint32_t a_klen, uint8_t state_root32[32], kh_stats* stats) {
+  if (!state || state->forest || !storage || !storage->forest) return set_err(KH_EINVAL, "need a state trie and a forest");
+  if (state->c != storage->c) return set_err(KH_EINVAL, "state trie and forest on different contexts");
+  API_TRY({
+    kh_ctx* c = state->c;
+    HIPCHK(hipSetDevice(c->dev));
+    hipStream_t st = c->st;
+    kh_stats sst{}, ast{};
+    // 1. every storage trie of the block (BlockWorldState.scala:243-252 -> TrieStorage.flush)
+    FCommit S;
+    S.up_trie = d_s_up_trie;
+    S.up_keys = d_s_up_keys;
+    S.up_vals = d_s_up_vals;
+    S.up_voff = d_s_up_voff;
+    S.nup = ns_up;
+    S.del_trie = d_s_del_trie;
+    S.del_keys = d_s_del_keys;
+    S.ndel = ns_del;
+    S.klen = s_klen;
+    forest_commit(storage, S, &sst);
+    // 2. account.withStateRoot: the new storage roots into the account bodies
+    const uint32_t nt = (uint32_t)storage->tries.size();
+    if (nt && na_up && d_a_up_trie) {
+      c->ws3.ensure(carve_size({(uint64_t)nt * 4, (uint64_t)nt * 32, 64}));
+      Carver cw{(char*)c->ws3.p, 0, c->ws3.cap};
+      uint32_t* tr = cw.take<uint32_t>(nt);
+      uint64_t* ro = cw.take<uint64_t>((uint64_t)nt * 4);
+      unsigned long long* err = cw.take<unsigned long long>(8);
+      HIPCHK(hipMemcpyAsync(tr, storage->tries.data(), (uint64_t)nt * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(ro, storage->roots.data(), (uint64_t)nt * 32, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemsetAsync(err, 0, 8, st));
+      hipLaunchKernelGGL(k_inject_roots, GRID(na_up, BS), dim3(BS), 0, st, d_a_up_vals, d_a_up_voff, d_a_up_trie,
+                         na_up, (const uint32_t*)tr, nt, (const uint64_t*)ro, err);
+      LAUNCH_CHECK();
+      HIPCHK(hipMemcpyAsync(c->h_pinned, err, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (c->h_pinned[0]) throw KhError{KH_EINVAL, "an account upsert with a storage trie is not an account body"};
+    }
+    // 3. the accounts (TrieAccounts.flush, TrieAccounts.scala:22-28)
+    FCommit A;
+    A.up_keys = d_a_up_keys;
+    A.up_vals = d_a_up_vals;
+    A.up_voff = d_a_up_voff;
+    A.nup = na_up;
+    A.del_keys = d_a_del_keys;
+    A.ndel = na_del;
+    A.klen = a_klen;
+    forest_commit(state, A, &ast);
+    memcpy(state_root32, state->root, 32);
+    if (stats) {
+      *stats = ast;
+      stats->n_inputs = ast.n_inputs + sst.n_inputs;
+      stats->n_node_hashes = ast.n_node_hashes + sst.n_node_hashes;
+      stats->n_node_perms = ast.n_node_perms + sst.n_node_perms;
+      stats->n_key_perms = ast.n_key_perms + sst.n_key_perms;
+      stats->n_branches = ast.n_branches + sst.n_branches;
+      stats->t_total_ms = ast.t_total_ms + sst.t_total_ms;
+    }
   })
 }
 
@@ -2303,30 +2922,20 @@ int kh_trie_emit_nodes(kh_trie* h, uint8_t* hashes32, uint64_t node_cap, uint8_t
                        uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len) {
   if (!h || !n_nodes || !rlp_len) return set_err(KH_EINVAL, "null handle or size outputs");
   API_TRY({
-    *n_nodes = 0;
-    *rlp_len = 0;
-    if (h->m == 0) {
-      if (off && node_cap + 1 > 0) off[0] = 0;
+    if (!(h->flags & KH_EMIT_NODES)) throw KhError{KH_EINVAL, "trie opened without KH_EMIT_NODES"};
+    HIPCHK(hipSetDevice(h->c->dev));
+    if (!h->em_valid) {
+      *n_nodes = *rlp_len = 0;
+      if (off) off[0] = 0;
       return KH_OK;
     }
-    kh_ctx* c = h->c;
-    HIPCHK(hipSetDevice(c->dev));
-    // re-encode the current version from its sorted set (no sort), keeping the encodings
-    BuildArgs A{(const uint8_t*)h->key[h->cur].p, 32, (const uint8_t*)h->val[h->cur].p,
-                (const uint64_t*)h->off[h->cur].p, h->m, nullptr, 1, 0, 0, true};
-    A.presorted = true;
-    BuildOut O;
-    run_build(c, A, O, nullptr);
-    uint8_t r[32];
-    copy_root(O, 0, r);
-    if (memcmp(r, h->root, 32) != 0) throw KhError{KH_EINTERNAL, "emit: re-encoded root differs from the committed root"};
-    return emit_node_set(c, hashes32, node_cap, rlp, rlp_cap, off, n_nodes, rlp_len);
+    return emit_to_host(h->c, h->em, h->em_n, h->em_bytes, hashes32, node_cap, rlp, rlp_cap, off, n_nodes, rlp_len);
   })
 }
 
 int kh_trie_size(const kh_trie* h, uint64_t* n) {
   if (!h || !n) return set_err(KH_EINVAL, "null handle");
-  *n = h->m;
+  *n = h->nleaves;
   return KH_OK;
 }
 
@@ -2335,11 +2944,7 @@ int kh_trie_free(kh_trie* h) {
   API_TRY({
     (void)hipSetDevice(h->c->dev);
     (void)hipStreamSynchronize(h->c->st);
-    for (int q = 0; q < 2; ++q)
-      for (DevBuf* b : {&h->key[q], &h->val[q], &h->off[q], &h->ref[q], &h->rlen[q], &h->lref[q], &h->lrlen[q]})
-        b->release();
-    for (DevBuf* b : {&h->u, &h->pyr, &h->bid, &h->lpd, &h->mws}) b->release();
-    delete h;
+    delete h;  // every DevBuf releases its HBM
   })
 }
 

@@ -153,7 +153,8 @@ struct Topo {
   const uint32_t* sidx;   // [m] input index of sorted key i
   const uint32_t* sseg;   // [m] segment id (segmented only)
   const uint8_t* vals;    // input values
-  const uint64_t* voff;   // [n+1]
+  const uint64_t* voff;   // [n+1] (or [n] offsets with vlen_in)
+  const uint32_t* vlen_in; // [n] value lengths (nullable: voff[i+1] - voff[i])
   uint64_t* svoff;        // [m] value offset of sorted key i (gathered once after the sort)
   uint32_t* svlen;        // [m] value length of sorted key i
   uint8_t* u;             // [m-1] boundary values
@@ -212,6 +213,15 @@ struct Topo {
   // (32 = hash, EMETA_LONG = not hashed yet: longer than one Keccak block)
   uint64_t* lf_eref;   // [m*4]
   uint8_t* lf_emeta;   // [m]
+  // element builds (resident commits, forest.h; all nullable): an element is a leaf, or
+  // a SUBTREE standing for an unchanged branch at depth el_db[i] whose capped reference
+  // is el_bref / el_brl (its keys all share key i's first el_db nibbles)
+  const uint8_t* el_db;     // [m] EL_LEAF or the subtree's branch depth
+  const uint64_t* el_bref;  // [m*4]
+  const uint8_t* el_brl;    // [m]
+  uint64_t* ex_ref;         // [B*4] capped reference of each extension (nullable)
+  uint32_t* ex_rlen;        // [B]
+  const uint8_t* emit_sel;  // [m + 2B] node q is emitted iff set (nullable: every node >= 32 B + tops)
   // per-result outputs
   uint64_t* res_hash;  // [nres*4]
   uint32_t* res_len;   // [nres]
@@ -251,6 +261,19 @@ KH_HD uint32_t result_index(const Topo& T, uint64_t first_key) {
   if (T.segmented) return T.sseg[first_key];
   if (T.depth0 == 1) return (uint32_t)(T.skey[4 * first_key] & 0xFF) >> 4;
   return 0;
+}
+
+// ---- element builds: subtree elements
+constexpr uint8_t EL_LEAF = 0xFF;
+KH_HD bool el_subtree(const Topo& T, uint64_t i) { return T.el_db && T.el_db[i] != EL_LEAF; }
+// encoding length of a subtree element hanging at anchor depth a: 0 extension nibbles ->
+// no node of its own (the parent embeds / references the branch: returns its capped
+// length); else the extension [HP(nibbles a .. db-1, ext), ref(branch)]
+KH_HD uint32_t el_ext_nibbles(const Topo& T, uint64_t i, uint32_t a) { return (uint32_t)T.el_db[i] - a; }
+KH_HD uint32_t ext_enc_len(uint32_t e, uint32_t brl) {
+  uint32_t hl = e / 2 + 1;
+  uint32_t xpay = (hl == 1 ? 1 : 1 + hl) + (brl >= 32 ? 33 : brl);
+  return rlp_hdr_len(xpay) + xpay;
 }
 
 // ---- stage: boundary values
@@ -456,7 +479,7 @@ KH_HD void op_val_gather(const Topo& T, uint64_t i) {
   uint32_t src = T.sidx ? T.sidx[i] : (uint32_t)i;  // presorted input: identity
   uint64_t o = T.voff[src];
   T.svoff[i] = o;
-  T.svlen[i] = (uint32_t)(T.voff[src + 1] - o);
+  T.svlen[i] = T.vlen_in ? T.vlen_in[src] : (uint32_t)(T.voff[src + 1] - o);
 }
 
 // encoded leaf length for path start nibble s
@@ -477,6 +500,12 @@ KH_HD void op_leaf_topo(const Topo& T, uint64_t i, AllocFn alloc) {
   T.lf_parent[i] = P.bid;
   T.lf_pord[i] = (uint8_t)P.pord;
   T.lf_pd[i] = (int8_t)P.pd;
+  if (el_subtree(T, i)) {
+    const uint32_t e = el_ext_nibbles(T, i, (uint32_t)(P.pd + 1));
+    T.lf_aoff[i] = 0;
+    T.lf_len[i] = e ? ext_enc_len(e, T.el_brl[i]) : T.el_brl[i];
+    return;
+  }
   const uint8_t* vp;
   uint64_t vlen;
   leaf_value(T, i, &vp, &vlen);
@@ -585,6 +614,26 @@ KH_HD void leaf_header(BW& w, const Key4& k, const LeafGeom& g, uint64_t vlen) {
 // vp: the value bytes (global memory, or a staged copy in LDS on the device)
 KH_HD void op_leaf_prep(const Topo& T, uint64_t i, const uint8_t* vp, uint64_t vlen) {
   Key4 k = load_key(T.skey, i);
+  if (el_subtree(T, i)) {  // extension over the unchanged branch (nothing when it hangs at its own depth)
+    const uint32_t a = (uint32_t)(T.lf_pd[i] + 1), e = el_ext_nibbles(T, i, a);
+    if (!e) return;
+    const uint32_t brl = T.el_brl[i], hl = e / 2 + 1;
+    const uint32_t xpay = (hl == 1 ? 1 : 1 + hl) + (brl >= 32 ? 33 : brl);
+    BW x(T.lmsg + i, T.lstride);
+    x.len_prefix(xpay, 0xC0);
+    if (hl > 1) x.put1(0x80 + hl);
+    uint32_t q = a;
+    if (e & 1) {
+      x.put1(0x10u | key_nibble(k, (int)q));
+      ++q;
+    } else {
+      x.put1(0x00);
+    }
+    for (; q < T.el_db[i]; q += 2) x.put1((key_nibble(k, (int)q) << 4) | key_nibble(k, (int)q + 1));
+    bw_ref(x, T.el_bref + 4 * i, brl >= 32 ? 32 : brl);
+    x.flush();
+    return;
+  }
   uint32_t v0 = vlen == 1 ? (uint32_t)*vp : 0;  // the first byte matters only for a 1-byte value
   LeafGeom g = leaf_geom(k, T.lf_pd[i], vlen, v0);
   BW w = g.L <= LEAF_SHORT_MAX ? BW(T.lmsg + i, T.lstride) : BW((uint64_t*)(T.arena + T.lf_aoff[i]), 1);
@@ -708,6 +757,20 @@ KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
     return 0;
   }
   uint32_t L = T.lf_len[i];
+  if (el_subtree(T, i) && el_ext_nibbles(T, i, (uint32_t)(T.lf_pd[i] + 1)) == 0) {
+    // the branch itself hangs here: its capped reference goes to the parent; as a top
+    // node (the root) it is always hashed, also when its encoding (then held inline) is < 32 B
+    const uint64_t* r = T.el_bref + 4 * i;
+    uint64_t hh[4] = {r[0], r[1], r[2], r[3]}, head[4] = {r[0], r[1], r[2], r[3]};
+    uint32_t perms = 0;
+    if (L < 32 && T.lf_parent[i] == NONE) {
+      kec256_msg<false>((const uint8_t*)head, L, hh);
+      perms = 1;
+    }
+    leaf_publish_at(T, i, L, hh, head, inl);
+    *inl = 0;  // embedded or referenced, it is not a node of this build
+    return perms;
+  }
   if (L <= LEAF_SHORT_MAX) return leaf_hash_at(T, i, T.lmsg + i, T.lstride, L, inl);
   return leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, L, inl);
 }
@@ -908,6 +971,14 @@ KH_HD uint32_t branch_publish(const Topo& T, uint32_t j, uint32_t L, const uint6
   slot_head(xs, XL, xhead);
   if (T.ex_hash)
     for (int q2 = 0; q2 < 4; ++q2) T.ex_hash[4 * j + q2] = hx[q2];
+  if (T.ex_ref) {
+    for (int q2 = 0; q2 < 4; ++q2) {
+      uint32_t base = 8u * (uint32_t)q2;
+      T.ex_ref[4 * j + q2] =
+          XL >= 32 ? hx[q2] : (base < XL ? xhead[q2] & low_bytes_mask(XL - base < 8 ? XL - base : 8) : 0);
+    }
+    T.ex_rlen[j] = XL;
+  }
   *ninl += (XL < 32 && !top) ? 1 : 0;
   publish_ref(T, parent, T.br_pord[j], nib, first, xhead, XL, hx);
   return perms;

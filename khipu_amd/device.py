@@ -97,28 +97,30 @@ def _pack_dev(items, device):
 
 
 class ResidentTrie:
-    """A trie kept in HBM between commits (kh_trie_open / kh_trie_apply; SURVEY §8 f1).
+    """A trie kept in HBM between commits (kh_trie_open / kh_trie_apply; SURVEY §8 f1, f2).
 
     commit(upserts, deletes) folds a block's dirty set the way TrieAccounts.flush /
     TrieStorage.flush fold their logs into MerklePatriciaTrie.put / remove
-    (TrieAccounts.scala:22-28, TrieStorage.scala:43-60), re-hashing only the changed
-    paths.  Keys are 32-byte trie keys, or raw (address / slot) bytes with hash_keys.
+    (TrieAccounts.scala:22-28, TrieStorage.scala:43-60), rebuilding only the nodes on the
+    changed paths (csrc/forest.h).  Keys are 32-byte trie keys, or raw (address / slot)
+    bytes with hash_keys.  With emit=True, nodes() returns the write-back set of the last
+    commit (the nodes it created).
     """
 
-    def __init__(self, ctx, keys=(), vals=(), hash_keys=False):
+    def __init__(self, ctx, keys=(), vals=(), hash_keys=False, emit=True):
         self.ctx = ctx
         self.dev = f"cuda:{ctx.device}"
         self.h = None
         klen = len(keys[0]) if keys else 32
         kd, _ = _pack_dev(list(keys), self.dev)
         vd, vo = _pack_dev(list(vals), self.dev)
-        self._open(kd, klen, vd, vo, len(keys), hash_keys)
+        self._open(kd, klen, vd, vo, len(keys), hash_keys, emit)
 
-    def _open(self, kd, klen, vd, vo, n, hash_keys):
+    def _open(self, kd, klen, vd, vo, n, hash_keys, emit=True):
         self.hash_keys = bool(hash_keys)  # every commit hashes its keys the same way
         h = ctypes.c_void_p()
         root = np.zeros(32, np.uint8)
-        flags = _lib.KH_HASH_KEYS if hash_keys else 0
+        flags = (_lib.KH_HASH_KEYS if hash_keys else 0) | (_lib.KH_EMIT_NODES if emit else 0)
         self.ctx._sync()
         check(lib().kh_trie_open(self.ctx.h, _ptr(kd), klen, _ptr(vd), _ptr(vo), n, flags, root.ctypes.data,
                                  ctypes.byref(h)))
@@ -156,27 +158,84 @@ class ResidentTrie:
         return self.root
 
     def nodes(self):
-        """{hash: encoding} of the current version for storage write-back (kh_trie_emit_nodes):
-        every node reachable from the root with an encoding >= 32 B, plus the root node."""
-        nn, nl = ctypes.c_uint64(0), ctypes.c_uint64(0)
-        cap_n, cap_b = 0, 0
-        for _ in range(2):
-            hs = np.zeros(32 * max(cap_n, 1), np.uint8)
-            rl = np.zeros(max(cap_b, 1), np.uint8)
-            of = np.zeros(cap_n + 1, np.uint64)
-            self.ctx._sync()
-            rc = lib().kh_trie_emit_nodes(self.h, hs.ctypes.data, cap_n, rl.ctypes.data, cap_b, of.ctypes.data,
-                                          ctypes.byref(nn), ctypes.byref(nl))
-            if rc == _lib.KH_ENOSPC:
-                cap_n, cap_b = nn.value, nl.value
-                continue
-            check(rc)
-            return {hs[32 * i:32 * i + 32].tobytes(): rl[of[i]:of[i + 1]].tobytes() for i in range(nn.value)}
-        raise RuntimeError("kh_trie_emit_nodes: size negotiation failed")
+        """{hash: encoding} written back by the last commit (kh_trie_emit_nodes): the nodes it
+        created, every one reachable from the new root with an encoding >= 32 B, plus a changed root."""
+        return emitted_nodes(lambda *a: lib().kh_trie_emit_nodes(self.h, *a))
 
     @property
     def root_hash(self):
         return self.root
+
+    def __len__(self):
+        n = ctypes.c_uint64()
+        check(lib().kh_trie_size(self.h, ctypes.byref(n)))
+        return int(n.value)
+
+    def close(self):
+        if self.h:
+            lib().kh_trie_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def emitted_nodes(call):
+    """Size negotiation of kh_trie_emit_nodes (KH_ENOSPC reports the sizes; no re-encoding)."""
+    nn, nl = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    cap_n, cap_b = 0, 0
+    for _ in range(2):
+        hs = np.zeros(32 * max(cap_n, 1), np.uint8)
+        rl = np.zeros(max(cap_b, 1), np.uint8)
+        of = np.zeros(cap_n + 1, np.uint64)
+        rc = call(hs.ctypes.data, cap_n, rl.ctypes.data, cap_b, of.ctypes.data, ctypes.byref(nn), ctypes.byref(nl))
+        if rc == _lib.KH_ENOSPC:
+            cap_n, cap_b = nn.value, nl.value
+            continue
+        check(rc)
+        return {hs[32 * i:32 * i + 32].tobytes(): rl[of[i]:of[i + 1]].tobytes() for i in range(nn.value)}
+    raise RuntimeError("kh_trie_emit_nodes: size negotiation failed")
+
+
+class ResidentForest:
+    """Many tries in one handle (contract storage tries; kh_forest_open / kh_forest_apply,
+    SURVEY §8 a12): each op names its trie id; one commit re-roots every touched trie."""
+
+    def __init__(self, ctx, hash_keys=False, emit=False):
+        self.ctx = ctx
+        self.dev = f"cuda:{ctx.device}"
+        self.hash_keys = bool(hash_keys)
+        h = ctypes.c_void_p()
+        flags = (_lib.KH_HASH_KEYS if hash_keys else 0) | (_lib.KH_EMIT_NODES if emit else 0)
+        check(lib().kh_forest_open(ctx.h, flags, ctypes.byref(h)))
+        self.h = h
+
+    def commit(self, upserts=(), deletes=(), stats=None):
+        """upserts: [(trie_id, key, value)], deletes: [(trie_id, key)] -> {trie_id: new root}."""
+        import torch
+        ups, dels = list(upserts), list(deletes)
+        klen = len(ups[0][1]) if ups else (len(dels[0][1]) if dels else 32)
+        uk, _ = _pack_dev([k for _, k, _ in ups], self.dev)
+        uv, uo = _pack_dev([v for _, _, v in ups], self.dev)
+        dk, _ = _pack_dev([k for _, k in dels], self.dev)
+        ut = torch.tensor([t for t, _, _ in ups] + [0], dtype=torch.int64).to(torch.int32).to(self.dev)
+        dt = torch.tensor([t for t, _ in dels] + [0], dtype=torch.int64).to(torch.int32).to(self.dev)
+        cap = len(ups) + len(dels) + 1
+        tries = np.zeros(cap, np.uint32)
+        roots = np.zeros(32 * cap, np.uint8)
+        nt = ctypes.c_uint64()
+        st = stats if stats is not None else KhStats()
+        self.ctx._sync()
+        check(lib().kh_forest_apply(self.h, _ptr(ut), _ptr(uk), _ptr(uv), _ptr(uo), len(ups), _ptr(dt), _ptr(dk),
+                                    len(dels), klen, tries.ctypes.data, roots.ctypes.data, cap, ctypes.byref(nt),
+                                    ctypes.byref(st)))
+        return {int(tries[i]): roots[32 * i:32 * i + 32].tobytes() for i in range(nt.value)}
+
+    def nodes(self):
+        return emitted_nodes(lambda *a: lib().kh_trie_emit_nodes(self.h, *a))
 
     def __len__(self):
         n = ctypes.c_uint64()

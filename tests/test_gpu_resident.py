@@ -107,17 +107,19 @@ def test_commit_1m_vs_full_build(khst):
 
 @pytest.mark.parametrize("sc", C.commit_scenarios(), ids=lambda s: s[0])
 def test_emit_nodes_after_commits(khst, oracle, sc):
-    """kh_trie_emit_nodes after every commit == the oracle's reachable node
-    set, and the nodes new in this version (absent from the previous one) are Updated
-    entries of the faithful log of that block's puts/removes (MerklePatriciaTrie.scala:491-516)."""
+    """kh_trie_emit_nodes is each commit's write-back DELTA: after open it is
+    the oracle's reachable node set; after a block, (1) every emitted pair is an Updated entry
+    of the faithful log of that block's puts/removes (MerklePatriciaTrie.scala:491-516), (2)
+    every emitted node is reachable from the new root, and (3) every reachable node the store
+    did not hold is emitted -- so the store after the hand-off holds the whole new trie."""
     from khipu_amd.device import Ctx, ResidentTrie
     name, ks, vs, batches = sc
     o = oracle.Trie()
     for k, v in zip(ks, vs):
         o.put(k, v)
     t = ResidentTrie(Ctx(0), ks, vs)
-    prev = t.nodes()
-    assert prev == (o.reachable() if ks else {}), name
+    store = dict(t.nodes())
+    assert store == (o.reachable() if ks else {}), name
     o.persist().reopen()
     for i, (ups, dels) in enumerate(batches):
         for k, v in ups:
@@ -125,13 +127,59 @@ def test_emit_nodes_after_commits(khst, oracle, sc):
         for k in dels:
             o.remove(k)
         t.commit(ups, dels)
-        cur = t.nodes()
+        delta = t.nodes()
         assert t.root == o.root_hash(), (name, i)
         want = o.reachable() if len(t) else {}
-        assert cur == want, (name, i)
         upd = o.updated()
-        new = {h: e for h, e in cur.items() if h not in prev}
-        assert all(h in upd and upd[h] == e for h, e in new.items()), (name, i)
+        assert all(h in upd and upd[h] == e for h, e in delta.items()), (name, i)
+        assert all(h in want and want[h] == e for h, e in delta.items()), (name, i)
+        missing = {h for h in want if h not in store and h not in delta}
+        assert not missing, (name, i, len(missing))
+        store.update(delta)
         o.persist().reopen()
-        prev = cur
     t.close()
+
+
+def test_forest_vs_oracle(khst, oracle):
+    """A forest (kh_forest_apply): storage tries of many contracts in one
+    handle, blocks touching some of them; every touched trie's root equals the oracle's
+    trie of that contract folded put-by-put / remove-by-remove; a trie deleted to empty has
+    EMPTY_TRIE_HASH; identical keys in different tries stay apart."""
+    from khipu_amd.device import Ctx, ResidentForest
+    r = random.Random(77)
+    f = ResidentForest(Ctx(0), hash_keys=True, emit=True)
+    tries = {}
+    ids = [r.randrange(1 << 32) for _ in range(60)]
+    for blk in range(6):
+        ups, dels = [], []
+        for t in r.sample(ids, 25):
+            o = tries.setdefault(t, oracle.Trie())
+            live = getattr(o, "_live", [])
+            for _ in range(r.choice([1, 3, 10, 40])):
+                slot = bytes(r.getrandbits(8) for _ in range(32)) if not live or r.random() < 0.6 else r.choice(live)
+                ups.append((t, slot, C.storage_value(r)))
+            if live and r.random() < 0.5:
+                for slot in r.sample(live, min(len(live), r.choice([1, 5, len(live)]))):
+                    dels.append((t, slot))
+        if blk == 2:  # the same slot in two tries
+            ups.append((ids[0], b"\x11" * 32, b"\x01"))
+            ups.append((ids[1], b"\x11" * 32, b"\x02"))
+        got = f.commit(ups, dels)
+        for t, slot, v in ups:
+            o = tries.setdefault(t, oracle.Trie())
+            o.put(oracle.kec256(slot), v)
+            o._live = list(dict.fromkeys(getattr(o, "_live", []) + [slot]))
+        for t, slot in dels:
+            tries[t].remove(oracle.kec256(slot))
+            tries[t]._live = [s for s in tries[t]._live if s != slot]
+        touched = {t for t, _, _ in ups} | {t for t, _ in dels}
+        assert set(got) == touched, blk
+        for t in touched:
+            assert got[t] == tries[t].root_hash(), (blk, t)
+        delta = f.nodes()
+        for t in touched:
+            want = tries[t].reachable() if tries[t]._live else {}
+            for h, e in delta.items():
+                if h in want:
+                    assert want[h] == e
+    f.close()
