@@ -1039,7 +1039,8 @@ struct ElemArgs {
   const uint8_t* db;     // [n] EL_LEAF or subtree branch depth (input order)
   const uint64_t* bref;  // [n*4]
   const uint8_t* brl;    // [n]
-  DevBuf* out;           // sorted el_db / el_bref / el_brl, lf_ref / lf_rlen, br_ref / br_rlen, ex_ref / ex_rlen
+  DevBuf* out;           // sorted el_db / el_bref / el_brl and lf_ref / lf_rlen (sized by m)
+  DevBuf* outb;          // br_ref / br_rlen, ex_ref / ex_rlen (sized by B)
 };
 struct BuildOut {
   std::vector<uint64_t> res_hash;  // nres*4
@@ -1321,6 +1322,22 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.sseg = sseg;
   hipLaunchKernelGGL(k_val_gather, GRID(m, BS), dim3(BS), 0, st, T);
   LAUNCH_CHECK();
+  if (A.el) {  // element build: the element properties in sorted order (the leaf topology reads them)
+    ElemArgs& E = *A.el;
+    E.out->ensure(carve_size({m, m * 32, m, m * 32, m * 4}));
+    Carver ce{(char*)E.out->p, 0, E.out->cap};
+    uint8_t* edb = ce.take<uint8_t>(m);
+    uint64_t* ebref = ce.take<uint64_t>(m * 4);
+    uint8_t* ebrl = ce.take<uint8_t>(m);
+    T.lf_ref = ce.take<uint64_t>(m * 4);
+    T.lf_rlen = ce.take<uint32_t>(m);
+    hipLaunchKernelGGL(k_el_gather, GRID(m, BS), dim3(BS), 0, st, (const uint32_t*)T.sidx, m, E.db, E.bref, E.brl,
+                       edb, ebref, ebrl);
+    LAUNCH_CHECK();
+    T.el_db = edb;
+    T.el_bref = ebref;
+    T.el_brl = ebrl;
+  }
   HIPCHK(hipEventRecord(c->ev[2], st));
 
   // ---- 3. topology
@@ -1427,26 +1444,15 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.bmsg = A.emit ? cv2.take<uint64_t>(bmsg_words) : nullptr;
   T.xmsg = A.emit ? cv2.take<uint64_t>(xmsg_words) : nullptr;
   T.lb = lb;
-  if (A.el) {  // element build: sorted element properties, and every capped reference kept
+  if (A.el) {  // element build: every capped reference kept for the forest's records
     ElemArgs& E = *A.el;
-    E.out->ensure(carve_size({m, m * 32, m, m * 32, m * 4, B * 32, B * 4, B * 32, B * 4, m + 2 * B}));
-    Carver ce{(char*)E.out->p, 0, E.out->cap};
-    uint8_t* edb = ce.take<uint8_t>(m);
-    uint64_t* ebref = ce.take<uint64_t>(m * 4);
-    uint8_t* ebrl = ce.take<uint8_t>(m);
-    T.lf_ref = ce.take<uint64_t>(m * 4);
-    T.lf_rlen = ce.take<uint32_t>(m);
+    E.outb->ensure(carve_size({B * 32, B * 4, B * 32, B * 4}));
+    Carver ce{(char*)E.outb->p, 0, E.outb->cap};
     T.br_ref = ce.take<uint64_t>(B * 4);
     T.br_rlen = ce.take<uint32_t>(B);
     T.ex_ref = ce.take<uint64_t>(B * 4);
     T.ex_rlen = ce.take<uint32_t>(B);
     T.emit_sel = nullptr;  // the forest sets its write-back selection after the build
-    hipLaunchKernelGGL(k_el_gather, GRID(m, BS), dim3(BS), 0, st, (const uint32_t*)T.sidx, m, E.db, E.bref, E.brl,
-                       edb, ebref, ebrl);
-    LAUNCH_CHECK();
-    T.el_db = edb;
-    T.el_bref = ebref;
-    T.el_brl = ebrl;
   }
   if (!early) HIPCHK(hipEventRecord(c->ev[3], st));
 
@@ -1894,7 +1900,7 @@ struct kh_trie {
   uint64_t heap_n = 0;
   uint64_t nleaves = 0;
   uint8_t root[32] = {};
-  DevBuf ws, elout, em;  // commit scratch, element-build outputs, last write-back set
+  DevBuf ws, elout, eloutb, em;  // commit scratch, element-build outputs, last write-back set
   DevBuf tlb, ebuf, tbuf, ubuf, selb, merr;  // touched list, elements, trie ids + roots, upsert offsets, selections
   uint64_t em_n = 0, em_bytes = 0;
   bool em_valid = false;
@@ -2167,7 +2173,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   uint64_t B = 0, m = 0;
   const bool keep_em = h->flags & KH_EMIT_NODES;
   if (ne) {
-    ElemArgs EA{E.db, E.bref, E.brl, &h->elout};
+    ElemArgs EA{E.db, E.bref, E.brl, &h->elout, &h->eloutb};
     BuildArgs A{(const uint8_t*)E.key, 32, (const uint8_t*)h->heap.p, (const uint64_t*)E.vo, ne,
                 nt > 1 ? (const uint32_t*)E.seg : nullptr, nt, 0, 0, true};
     A.vlen = E.vl;

@@ -269,7 +269,13 @@ KH_HD bool el_subtree(const Topo& T, uint64_t i) { return T.el_db && T.el_db[i] 
 // encoding length of a subtree element hanging at anchor depth a: 0 extension nibbles ->
 // no node of its own (the parent embeds / references the branch: returns its capped
 // length); else the extension [HP(nibbles a .. db-1, ext), ref(branch)]
-KH_HD uint32_t el_ext_nibbles(const Topo& T, uint64_t i, uint32_t a) { return (uint32_t)T.el_db[i] - a; }
+KH_HD uint32_t el_ext_nibbles(const Topo& T, uint64_t i, uint32_t a) {
+  if (a > T.el_db[i]) {  // cannot happen (a subtree's neighbours diverge above its branch): flag it
+    T.ctr[CTR_ERR] = 7;
+    return 0;
+  }
+  return (uint32_t)T.el_db[i] - a;
+}
 KH_HD uint32_t ext_enc_len(uint32_t e, uint32_t brl) {
   uint32_t hl = e / 2 + 1;
   uint32_t xpay = (hl == 1 ? 1 : 1 + hl) + (brl >= 32 ? 33 : brl);
