@@ -115,38 +115,12 @@ KH_HD uint64_t map_slot_of(const AMap& M, const Recs& R, uint32_t r) {
 
 // ---- the batch of ops, sorted by (trie, key), one op per key (the last one wins)
 enum : uint8_t { FOP_UPSERT = 1, FOP_DELETE = 2 };
-enum : uint8_t { TERM_MISSING = 0, TERM_LEAF = 1, TERM_DIVERGE = 2 };
 struct FOps {
   const uint64_t* key;  // [n*4]
   const uint32_t* trie; // [n]
   const uint8_t* kind;  // [n]
   uint64_t n;
 };
-
-// 1. descent of op o; marks opened branches and touched leaves (idempotent byte writes)
-KH_HD void op_descend(const FOps& O, const AMap& M, const Recs& R, uint8_t* touched, uint8_t* replaced, uint64_t o,
-                      unsigned long long* err) {
-  const uint64_t* K = O.key + 4 * o;
-  const uint32_t t = O.trie[o];
-  uint32_t d = 0;
-  for (int step = 0; step < 70; ++step) {
-    const uint32_t r = map_find(M, R, t, d, K);
-    if (r == NONE) return;  // TERM_MISSING: the upsert becomes a leaf element
-    const uint32_t db = R.rdb[r];
-    if (db == EL_LEAF) {
-      touched[r] = 1;
-      const uint64_t* L = R.rk + 4ull * r;
-      if (L[0] == K[0] && L[1] == K[1] && L[2] == K[2] && L[3] == K[3]) replaced[r] = 1;
-      return;
-    }
-    Key4 a{K[0], K[1], K[2], K[3]};
-    Key4 b = load_key(R.rk, r);
-    if (lcp_nibbles(a, b) < (int)db) return;  // diverges inside the extension: the branch stays whole
-    touched[r] = 1;                             // opened
-    d = db + 1;
-  }
-  *err = 3;  // deeper than a 32-byte key allows: corrupt map
-}
 
 // elements of an element build
 struct Elems {
@@ -158,7 +132,9 @@ struct Elems {
   uint64_t* vo;     // value offset in the heap (leaves)
   uint32_t* vl;
   uint32_t* src;    // source record, NONE for an upsert
-  uint8_t* oldd;    // the source record's anchor depth
+  uint8_t* oldd;    // the source record's anchor depth (EL_NEW for an upsert)
+  uint64_t* cref;   // [cap*4] the source record's capped reference (rref)
+  uint8_t* crl;
   unsigned long long* n;  // counter
   uint64_t cap;
 };
@@ -185,45 +161,8 @@ KH_HD void elem_from_record(const Recs& R, uint32_t r, uint32_t seg, const Elems
   E.vl[e] = R.rdb[r] == EL_LEAF ? R.rvl[r] : 0;
   E.src[e] = r;
   E.oldd[e] = R.rd[r];
-}
-
-// 2a. record r (any live record): if it is an opened branch, its untouched children
-// become elements; if it is a touched leaf nobody replaced, it is an element itself
-template <typename PushFn>
-KH_HD void op_gather_record(const AMap& M, const Recs& R, const uint8_t* touched, const uint8_t* replaced,
-                            const uint32_t* tries, uint32_t nt, const Elems& E, uint32_t r, PushFn push,
-                            unsigned long long* err) {
-  if (!touched[r] || R.rlive[r] != REC_LIVE) return;
-  const uint32_t t = R.rt[r], seg = seg_of(tries, nt, t);
-  const uint32_t db = R.rdb[r];
-  if (db == EL_LEAF) {
-    if (!replaced[r]) elem_from_record(R, r, seg, E, push);
-    return;
-  }
-  const uint32_t mask = R.rmask[r];
-  uint64_t ck[4] = {R.rk[4ull * r], R.rk[4ull * r + 1], R.rk[4ull * r + 2], R.rk[4ull * r + 3]};
-  for (uint32_t v = 0; v < 16; ++v) {
-    if (!((mask >> v) & 1)) continue;
-    set_nibble(ck, db, v);
-    const uint32_t c = map_find(M, R, t, db + 1, ck);
-    if (c == NONE) {
-      *err = 4;  // a child the branch records is missing: corrupt map
-      continue;
-    }
-    if (touched[c]) continue;  // opened further down, or a touched leaf
-    elem_from_record(R, c, seg, E, push);
-  }
-}
-
-// 2b. the root of a touched trie that no op passed into (every op diverged inside its
-// extension): one subtree element
-template <typename PushFn>
-KH_HD void op_gather_root(const AMap& M, const Recs& R, const uint8_t* touched, const uint32_t* tries, uint32_t nt,
-                          const Elems& E, uint32_t s, PushFn push) {
-  const uint64_t zero[4] = {0, 0, 0, 0};
-  const uint32_t r = map_find(M, R, tries[s], 0, zero);
-  if (r == NONE || touched[r]) return;
-  elem_from_record(R, r, s, E, push);
+  for (int q = 0; q < 4; ++q) E.cref[4 * e + q] = R.rref[4ull * r + q];
+  E.crl[e] = R.rrl[r];
 }
 
 }  // namespace khst

@@ -1039,6 +1039,9 @@ struct ElemArgs {
   const uint8_t* db;     // [n] EL_LEAF or subtree branch depth (input order)
   const uint64_t* bref;  // [n*4]
   const uint8_t* brl;    // [n]
+  const uint8_t* oldd;   // [n] previous anchor depth (EL_NEW: none)
+  const uint64_t* cref;  // [n*4] previous capped reference
+  const uint8_t* crl;    // [n]
   DevBuf* out;           // sorted el_db / el_bref / el_brl and lf_ref / lf_rlen (sized by m)
   DevBuf* outb;          // br_ref / br_rlen, ex_ref / ex_rlen (sized by B)
 };
@@ -1324,19 +1327,27 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   LAUNCH_CHECK();
   if (A.el) {  // element build: the element properties in sorted order (the leaf topology reads them)
     ElemArgs& E = *A.el;
-    E.out->ensure(carve_size({m, m * 32, m, m * 32, m * 4}));
+    E.out->ensure(carve_size({m, m * 32, m, m, m * 32, m, m * 32, m * 4}));
     Carver ce{(char*)E.out->p, 0, E.out->cap};
     uint8_t* edb = ce.take<uint8_t>(m);
     uint64_t* ebref = ce.take<uint64_t>(m * 4);
     uint8_t* ebrl = ce.take<uint8_t>(m);
+    uint8_t* eoldd = ce.take<uint8_t>(m);
+    uint64_t* ecref = ce.take<uint64_t>(m * 4);
+    uint8_t* ecrl = ce.take<uint8_t>(m);
     T.lf_ref = ce.take<uint64_t>(m * 4);
     T.lf_rlen = ce.take<uint32_t>(m);
     hipLaunchKernelGGL(k_el_gather, GRID(m, BS), dim3(BS), 0, st, (const uint32_t*)T.sidx, m, E.db, E.bref, E.brl,
                        edb, ebref, ebrl);
+    hipLaunchKernelGGL(k_el_gather, GRID(m, BS), dim3(BS), 0, st, (const uint32_t*)T.sidx, m, E.oldd, E.cref, E.crl,
+                       eoldd, ecref, ecrl);
     LAUNCH_CHECK();
     T.el_db = edb;
     T.el_bref = ebref;
     T.el_brl = ebrl;
+    T.el_oldd = eoldd;
+    T.el_cref = ecref;
+    T.el_crl = ecrl;
   }
   HIPCHK(hipEventRecord(c->ev[2], st));
 
@@ -1670,7 +1681,9 @@ __global__ void __launch_bounds__(BS) k_f_upsert_elems(FOps O, const uint32_t* t
   E.vo[e] = heap_base + uoff[e];
   E.vl[e] = (uint32_t)(uoff[e + 1] - uoff[e]);
   E.src[e] = NONE;
-  E.oldd[e] = 0;
+  E.oldd[e] = EL_NEW;
+  for (int q = 0; q < 4; ++q) E.cref[4 * e + q] = 0;
+  E.crl[e] = 0;
 }
 // op o's value: (batch offset, length) -> for the heap copy
 __global__ void __launch_bounds__(BS) k_f_upsert_len(FOps O, const uint32_t* sidx, const uint64_t* voff,
@@ -2122,7 +2135,8 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   const uint64_t ecap = (uint64_t)nups + 16 * ntl + nt + 16;
   regrow(h->heap, h->heap_n, h->heap_n + ubytes + 64, st);
   const uint64_t hb = h->heap_n;
-  h->ebuf.ensure(carve_size({ecap * 32, ecap * 4, ecap, ecap * 32, ecap, ecap * 8, ecap * 4, ecap * 4, ecap, 64}));
+  h->ebuf.ensure(
+      carve_size({ecap * 32, ecap * 4, ecap, ecap * 32, ecap, ecap * 8, ecap * 4, ecap * 4, ecap, ecap * 32, ecap, 64}));
   Carver ce{(char*)h->ebuf.p, 0, h->ebuf.cap};
   Elems E{};
   E.key = ce.take<uint64_t>(ecap * 4);
@@ -2134,6 +2148,8 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   E.vl = ce.take<uint32_t>(ecap);
   E.src = ce.take<uint32_t>(ecap);
   E.oldd = ce.take<uint8_t>(ecap);
+  E.cref = ce.take<uint64_t>(ecap * 4);
+  E.crl = ce.take<uint8_t>(ecap);
   E.n = ce.take<unsigned long long>(8);
   E.cap = ecap;
   // upsert values: uoff is the exclusive scan of their lengths over the sorted ops;
@@ -2173,7 +2189,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   uint64_t B = 0, m = 0;
   const bool keep_em = h->flags & KH_EMIT_NODES;
   if (ne) {
-    ElemArgs EA{E.db, E.bref, E.brl, &h->elout, &h->eloutb};
+    ElemArgs EA{E.db, E.bref, E.brl, E.oldd, E.cref, E.crl, &h->elout, &h->eloutb};
     BuildArgs A{(const uint8_t*)E.key, 32, (const uint8_t*)h->heap.p, (const uint64_t*)E.vo, ne,
                 nt > 1 ? (const uint32_t*)E.seg : nullptr, nt, 0, 0, true};
     A.vlen = E.vl;

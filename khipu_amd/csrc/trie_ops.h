@@ -219,6 +219,9 @@ struct Topo {
   const uint8_t* el_db;     // [m] EL_LEAF or the subtree's branch depth
   const uint64_t* el_bref;  // [m*4]
   const uint8_t* el_brl;    // [m]
+  const uint8_t* el_oldd;   // [m] anchor depth of the element's node in the previous version (EL_NEW: none)
+  const uint64_t* el_cref;  // [m*4] that node's capped reference (the parent's view)
+  const uint8_t* el_crl;    // [m]
   uint64_t* ex_ref;         // [B*4] capped reference of each extension (nullable)
   uint32_t* ex_rlen;        // [B]
   const uint8_t* emit_sel;  // [m + 2B] node q is emitted iff set (nullable: every node >= 32 B + tops)
@@ -264,8 +267,11 @@ KH_HD uint32_t result_index(const Topo& T, uint64_t first_key) {
 }
 
 // ---- element builds: subtree elements
-constexpr uint8_t EL_LEAF = 0xFF;
+constexpr uint8_t EL_LEAF = 0xFF, EL_NEW = 0xFF;
 KH_HD bool el_subtree(const Topo& T, uint64_t i) { return T.el_db && T.el_db[i] != EL_LEAF; }
+// an unchanged node still hanging at its old anchor: its encoding is what it was, so its
+// cached reference is published as is (no re-encoding, no hash, nothing written back)
+KH_HD bool el_cached(const Topo& T, uint64_t i, uint32_t a) { return T.el_oldd && T.el_oldd[i] == a; }
 // encoding length of a subtree element hanging at anchor depth a: 0 extension nibbles ->
 // no node of its own (the parent embeds / references the branch: returns its capped
 // length); else the extension [HP(nibbles a .. db-1, ext), ref(branch)]
@@ -506,6 +512,11 @@ KH_HD void op_leaf_topo(const Topo& T, uint64_t i, AllocFn alloc) {
   T.lf_parent[i] = P.bid;
   T.lf_pord[i] = (uint8_t)P.pord;
   T.lf_pd[i] = (int8_t)P.pd;
+  if (el_cached(T, i, (uint32_t)(P.pd + 1))) {
+    T.lf_aoff[i] = 0;
+    T.lf_len[i] = T.el_crl[i];
+    return;
+  }
   if (el_subtree(T, i)) {
     const uint32_t e = el_ext_nibbles(T, i, (uint32_t)(P.pd + 1));
     T.lf_aoff[i] = 0;
@@ -620,6 +631,7 @@ KH_HD void leaf_header(BW& w, const Key4& k, const LeafGeom& g, uint64_t vlen) {
 // vp: the value bytes (global memory, or a staged copy in LDS on the device)
 KH_HD void op_leaf_prep(const Topo& T, uint64_t i, const uint8_t* vp, uint64_t vlen) {
   Key4 k = load_key(T.skey, i);
+  if (el_cached(T, i, (uint32_t)(T.lf_pd[i] + 1))) return;
   if (el_subtree(T, i)) {  // extension over the unchanged branch (nothing when it hangs at its own depth)
     const uint32_t a = (uint32_t)(T.lf_pd[i] + 1), e = el_ext_nibbles(T, i, a);
     if (!e) return;
@@ -763,10 +775,13 @@ KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
     return 0;
   }
   uint32_t L = T.lf_len[i];
-  if (el_subtree(T, i) && el_ext_nibbles(T, i, (uint32_t)(T.lf_pd[i] + 1)) == 0) {
-    // the branch itself hangs here: its capped reference goes to the parent; as a top
-    // node (the root) it is always hashed, also when its encoding (then held inline) is < 32 B
-    const uint64_t* r = T.el_bref + 4 * i;
+  const uint32_t a = (uint32_t)(T.lf_pd[i] + 1);
+  const bool cached = el_cached(T, i, a);
+  if (cached || (el_subtree(T, i) && el_ext_nibbles(T, i, a) == 0)) {
+    // an unchanged node at its old anchor, or a branch hanging at its own depth: its capped
+    // reference goes to the parent; as a top node (the root) it is always hashed, also when
+    // its encoding (then held inline) is < 32 B
+    const uint64_t* r = cached ? T.el_cref + 4 * i : T.el_bref + 4 * i;
     uint64_t hh[4] = {r[0], r[1], r[2], r[3]}, head[4] = {r[0], r[1], r[2], r[3]};
     uint32_t perms = 0;
     if (L < 32 && T.lf_parent[i] == NONE) {
