@@ -2085,7 +2085,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   }
   sort_dedup(c, S);
   const uint64_t nd = S.m;
-  uint32_t* otrie = sseg;
+  uint32_t* otrie = segd ? S.sseg : sseg;  // the compaction of duplicates moves the sorted ids
   if (!segd) {
     hipLaunchKernelGGL(k_u32_fill, GRID(nd, BS), dim3(BS), 0, st, otrie, nd, 0u);
     LAUNCH_CHECK();
