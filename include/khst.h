@@ -212,6 +212,9 @@ int kh_forest_apply_host(kh_trie* f, const uint32_t* up_trie, const uint8_t* up_
                          uint64_t ndel, uint32_t klen, uint32_t* h_tries, uint8_t* h_roots32, uint64_t cap,
                          uint64_t* n_tries, kh_stats* stats);
 
+/* The touched tries and roots of a forest's last commit (also after kh_block_commit). */
+int kh_forest_last_roots(kh_trie* f, uint32_t* h_tries, uint8_t* h_roots32, uint64_t cap, uint64_t* n_tries);
+
 /* One block (BlockWorldState.flush, BlockWorldState.scala:243-252 then TrieAccounts.flush):
  * the storage ops into the forest, each touched trie's new root written into the stateRoot
  * field of the account upserts that name it (d_a_up_trie[i], KH_NO_TRIE for none; the body

@@ -29,7 +29,7 @@
 //      changed are the block's write-back set.
 // Work per commit is O(dirty keys x depth x 16), not O(resident keys).
 #pragma once
-#include "resident.h"
+#include "keyorder.h"
 
 namespace khst {
 

@@ -27,7 +27,7 @@
 #include "prims.h"
 #include "synth.h"
 #include "trie_ops.h"
-#include "resident.h"
+#include "keyorder.h"
 #include "forest.h"
 #include "nodedata.h"
 
@@ -430,21 +430,16 @@ __global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
 // funnel-shifted by the header length), 2) each lane writes its header bytes in
 // front (merging the shared word), Keccak's its slot and publishes the reference.
 // Leaves longer than one block take the arena path (k_leaf_prep's global writer).
-// EARLY (plain root builds, trie_ops.h "early leaves"): launched on the second
-// stream right after k_lcp; the parent depth comes from the two boundaries, the
-// reference is stashed for k_leaf_topo_early, and long leaves are only counted
-// (their arena bytes) for k_leaf_long.
-template <bool EARLY>
+// Plain root builds (trie_ops.h "early leaves"): launched on the second stream right
+// after k_lcp; the parent depth comes from the two boundaries, the reference is
+// stashed for k_leaf_topo_early, and long leaves are only counted (their arena bytes)
+// for k_leaf_long.
 __global__ void __launch_bounds__(BS) k_leaf_fused(Topo T) {
+  constexpr bool EARLY = true;
   __shared__ uint64_t msg[BS * LEAF_WORDS];
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u;
-  const int cstate = EARLY ? 0 : (i < T.m ? leaf_cache_state(T, i) : 2);  // 0: encode + hash here
-  const bool valid = i < T.m && cstate == 0;
-  if (!EARLY && i < T.m && cstate && T.lf_oldpos) {
-    uint32_t in0;
-    leaf_reuse(T, i, cstate, &in0);
-  }
+  const bool valid = i < T.m;
   uint64_t off = 0;
   uint32_t vlen = 0, v0 = 0;
   Key4 k{0, 0, 0, 0};
@@ -632,12 +627,11 @@ __global__ void __launch_bounds__(BS) k_branch_coop(Topo T, uint64_t first, uint
   const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u, c = ln & 15, row = ln >> 4;
   const uint32_t j = (uint32_t)(first + t);
   const bool valid = t < cnt;
-  const bool clean = valid && T.br_dirty && !T.br_dirty[j];
   const bool top = valid && T.br_parent[j] == NONE;
   const uint32_t ext = valid ? T.br_ext[j] : 0;
   uint32_t L = 0, payload = 0, k = 0, nblk = 0;
   bool hashit = false;
-  if (valid && !clean) {
+  if (valid) {
     payload = branch_payload(T, j);
     L = rlp_hdr_len(payload) + payload;
     k = T.br_k[j];
@@ -737,10 +731,7 @@ __global__ void __launch_bounds__(BS) k_branch_coop(Topo T, uint64_t first, uint
   if (valid) {
     uint64_t hb[4] = {0, 0, 0, 0}, bhead[4] = {0, 0, 0, 0};
     uint32_t ninl = 0, p = 0;
-    bool go = true;
-    if (clean) {
-      go = branch_clean_ref(T, j, &L, hb, bhead);
-    } else {
+    {
       if (hashit) {
         for (int q = 0; q < 4; ++q) hb[q] = lane(S, q);
         p = L / 136 + 1;
@@ -755,12 +746,10 @@ __global__ void __launch_bounds__(BS) k_branch_coop(Topo T, uint64_t first, uint
       ninl = hashit ? 0 : 1;
       branch_keep(T, j, L, hb, bhead);
     }
-    if (go) {
-      p += branch_publish(T, j, L, hb, bhead, Slot{win + (uint64_t)threadIdx.x * LEAF_WORDS, 1}, &ninl);
-      perms = p;
-      hashes = branch_hash_count(T, j, p);
-      inl = ninl;
-    }
+    p += branch_publish(T, j, L, hb, bhead, Slot{win + (uint64_t)threadIdx.x * LEAF_WORDS, 1}, &ninl);
+    perms = p;
+    hashes = branch_hash_count(T, j, p);
+    inl = ninl;
   }
   block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
 }
@@ -852,46 +841,6 @@ __device__ __forceinline__ void copy_bytes_group(uint8_t* dst, const uint8_t* sr
     *(uint64_t*)(dst + hb + 8 * w) = load64u_n(src + hb + 8 * w, 8);
   const uint64_t t0 = hb + 8 * nw;
   if (t0 + lane < L) dst[t0 + lane] = src[t0 + lane];
-}
-
-// ---- resident trie: merge a sorted batch into the sorted (key, value) set (resident.h)
-__global__ void __launch_bounds__(BS) k_op_locate(Merge M) {
-  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (o < M.nops) op_locate(M, o);
-}
-__global__ void __launch_bounds__(BS) k_op_mark(Merge M) {
-  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (o < M.nops) op_mark(M, o, [](uint32_t* p) { atomicAdd(p, 1u); });
-}
-__global__ void __launch_bounds__(BS) k_place_resident(Merge M, const uint32_t* del_flag) {
-  uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (j < M.m) op_place_resident(M, del_flag, j);
-}
-__global__ void __launch_bounds__(BS) k_place_op(Merge M, const uint32_t* ins_flag, const uint32_t* eff_flag) {
-  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (o < M.nops) op_place_op(M, ins_flag, eff_flag, o);
-}
-// value bytes of the merged set: from the resident buffer or the upsert buffer
-__global__ void __launch_bounds__(BS) k_merge_vals(const uint64_t* nsrc, const uint32_t* nlen, const uint64_t* noff,
-                                                  uint64_t m, const uint8_t* rval, const uint8_t* uval,
-                                                  uint8_t* nval) {
-  uint64_t i = ((uint64_t)blockIdx.x * BS + threadIdx.x) / CG;
-  if (i >= m) return;
-  uint64_t s = nsrc[i];
-  const uint8_t* src = (s & SRC_UPSERT) ? uval + (s & ~SRC_UPSERT) : rval + s;
-  copy_bytes_group(nval + noff[i], src, nlen[i], threadIdx.x % CG);
-}
-__global__ void __launch_bounds__(BS) k_u32_to_u64(const uint32_t* in, uint64_t* out, uint64_t n) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i < n) out[i] = in[i];
-}
-__global__ void __launch_bounds__(BS) k_br_dirty(Topo T, const uint64_t* dkey, uint64_t nd, const uint32_t* Bp) {
-  uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (j < *Bp) op_br_dirty(T, dkey, nd, (uint32_t)j);
-}
-__global__ void __launch_bounds__(BS) k_br_clean(Topo T, Prev V, const uint32_t* Bp) {
-  uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (j < *Bp) op_br_clean(T, V, (uint32_t)j);
 }
 
 // ---- multi-GPU routing: stable partition of records by top-nibble owner
@@ -1365,7 +1314,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     HIPCHK(hipEventRecord(c->ev[8], st));
     HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
     HIPCHK(hipEventRecord(c->ev[9], c->st2));
-    hipLaunchKernelGGL(k_leaf_fused<true>, GRID(m, BS), dim3(BS), 0, c->st2, T);
+    hipLaunchKernelGGL(k_leaf_fused, GRID(m, BS), dim3(BS), 0, c->st2, T);
     LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[10], c->st2));
   }
@@ -1476,13 +1425,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       hipLaunchKernelGGL(k_leaf_long, GRID(m, BS), dim3(BS), 0, st, T);
       LAUNCH_CHECK();
     }
-  } else if (A.emit) {
+  } else {  // write-back and element builds: encodings kept in message slots, then hashed
     hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_leaf_hash, GRID(m, BS), dim3(BS), 0, st, T);
-    LAUNCH_CHECK();
-  } else {
-    hipLaunchKernelGGL(k_leaf_fused<false>, GRID(m, BS), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
   }
   HIPCHK(hipEventRecord(c->ev[4], st));
@@ -2872,6 +2818,11 @@ int kh_forest_apply_host(kh_trie* f, const uint32_t* up_trie, const uint8_t* up_
     forest_commit(f, F, stats);
     return forest_out(f, h_tries, h_roots32, cap, n_tries);
   })
+}
+
+int kh_forest_last_roots(kh_trie* f, uint32_t* h_tries, uint8_t* h_roots32, uint64_t cap, uint64_t* n_tries) {
+  if (!f) return set_err(KH_EINVAL, "null handle");
+  API_TRY({ return forest_out(f, h_tries, h_roots32, cap, n_tries); })
 }
 
 int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_trie, const uint8_t* d_s_up_keys,

@@ -197,18 +197,11 @@ struct Topo {
                            //   bmsg[BR_WORDS * lb[d] + q * cnt_d + t]  (transposed per level)
   uint64_t* xmsg;          // extension messages, same scheme with EXT_WORDS
   const uint32_t* lb;      // [65] first order position of each depth (lb[64] = B)
-  // incremental commit (resident.h; all nullable)
-  uint8_t* br_dirty;   // [B] 1: re-encode and re-hash; 0: reference from the previous version
-  uint64_t* br_ref;    // [B*4] capped reference of each branch node (saved for the next commit)
+  // capped references kept for a resident forest's records (element builds; nullable)
+  uint64_t* br_ref;    // [B*4] capped reference of each branch node
   uint32_t* br_rlen;   // [B] its encoding length
-  uint64_t* lf_ref;    // [m*4] capped reference of each leaf (saved for the next commit)
+  uint64_t* lf_ref;    // [m*4] capped reference of each element node (leaf or extension)
   uint32_t* lf_rlen;   // [m]
-  // the previous version, seen from the merged set (nullable)
-  const uint32_t* lf_oldpos;  // [m] previous position of leaf i, NONE if inserted
-  const uint8_t* lf_upd;      // [m] 1 if the value was upserted
-  const int8_t* lf_opd;       // previous parent depth per previous position
-  const uint64_t* lf_oref;    // previous leaf references
-  const uint32_t* lf_orlen;
   // early leaves (plain root builds; nullable): capped reference and its length
   // (32 = hash, EMETA_LONG = not hashed yet: longer than one Keccak block)
   uint64_t* lf_eref;   // [m*4]
@@ -689,43 +682,11 @@ KH_HD void kec256_strided(const uint64_t* w, uint64_t stride, uint32_t len, uint
 }
 
 // ---- leaf hash (thread per leaf).  Returns permutations spent.
-// incremental commit: a node under a clean branch is neither hashed nor published
-KH_HD bool under_clean(const Topo& T, uint32_t parent) {
-  return T.br_dirty && parent != NONE && !T.br_dirty[parent];
-}
-
-// Incremental commit, per leaf: 0 = encode and hash, 1 = unchanged under a dirty
-// parent (publish the previous reference), 2 = unchanged under a clean parent (keep
-// the previous reference).  A leaf is unchanged when it was neither inserted nor
-// upserted and its parent depth (hence its path) is the same.
-KH_HD int leaf_cache_state(const Topo& T, uint64_t i) {
-  if (!T.lf_oldpos) return under_clean(T, T.lf_parent[i]) ? 2 : 0;
-  if (T.lf_parent[i] == NONE) return 0;  // a lone leaf is the root: always hashed
-  uint32_t o = T.lf_oldpos[i];
-  if (o == NONE || T.lf_upd[i] || T.lf_opd[o] != T.lf_pd[i]) return 0;
-  return under_clean(T, T.lf_parent[i]) ? 2 : 1;
-}
 KH_HD uint32_t leaf_nibble(const Topo& T, uint64_t i) {
   uint32_t pd = (uint32_t)T.lf_pd[i];
   uint32_t b = (uint32_t)(T.skey[4 * i + (pd >> 4)] >> (8 * ((pd >> 1) & 7))) & 0xFF;
   return (pd & 1) ? (b & 0xF) : (b >> 4);
 }
-// states 1 and 2: carry the previous reference over (and publish it for state 1)
-KH_HD void leaf_reuse(const Topo& T, uint64_t i, int state, uint32_t* inl) {
-  uint32_t o = T.lf_oldpos[i];
-  uint64_t r[4];
-  for (int q = 0; q < 4; ++q) r[q] = T.lf_oref[4ull * o + q];
-  uint32_t L = T.lf_orlen[o];
-  if (T.lf_ref) {
-    for (int q = 0; q < 4; ++q) T.lf_ref[4 * i + q] = r[q];
-    T.lf_rlen[i] = L;
-  }
-  *inl = 0;
-  if (state != 1) return;
-  uint32_t parent = T.lf_parent[i];
-  publish_ref(T, parent, T.lf_pord[i], leaf_nibble(T, i), i, r, L, r);
-}
-
 // publish of leaf i after hashing: hh = its hash (zero if not hashed: L < 32 and not the
 // top), head = its first 4 message words (the inline reference when L < 32)
 KH_HD void leaf_publish_at(const Topo& T, uint64_t i, uint32_t L, const uint64_t hh[4], const uint64_t head[4],
@@ -769,11 +730,6 @@ KH_HD uint32_t leaf_hash_at(const Topo& T, uint64_t i, const uint64_t* w, uint64
 
 KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
   *inl = 0;
-  int cs = leaf_cache_state(T, i);
-  if (cs) {
-    if (T.lf_oldpos) leaf_reuse(T, i, cs, inl);
-    return 0;
-  }
   uint32_t L = T.lf_len[i];
   const uint32_t a = (uint32_t)(T.lf_pd[i] + 1);
   const bool cached = el_cached(T, i, a);
@@ -898,7 +854,6 @@ KH_HD void branch_stream(const Topo& T, uint32_t j, W& w, uint32_t payload) {
 // ---- branch prep: the whole encoding into its message slot (thread per branch of one
 // level; g = its position in the level order).  The write-back build keeps it there.
 KH_HD void op_branch_prep(const Topo& T, uint32_t j, uint64_t g) {
-  if (T.br_dirty && !T.br_dirty[j]) return;  // clean: reference from the previous version
   uint32_t payload = branch_payload(T, j);
   Slot sl = branch_slot(T, g, T.br_depth[j], false);
   T.br_aoff[j] = g;
@@ -1005,15 +960,7 @@ KH_HD uint32_t branch_publish(const Topo& T, uint32_t j, uint32_t L, const uint6
   return perms;
 }
 
-// a clean branch (incremental commit): its reference from the previous version.
-// Returns false when it is not needed (its parent is clean too).
-KH_HD bool branch_clean_ref(const Topo& T, uint32_t j, uint32_t* L, uint64_t hb[4], uint64_t bhead[4]) {
-  if (under_clean(T, T.br_parent[j])) return false;
-  *L = T.br_rlen[j];
-  for (int q = 0; q < 4; ++q) bhead[q] = hb[q] = T.br_ref[4 * j + q];
-  return true;
-}
-// after hashing a dirty branch: per-node hash (write-back) and capped reference (next commit)
+// after hashing a branch: per-node hash (write-back) and capped reference (forest records)
 KH_HD void branch_keep(const Topo& T, uint32_t j, uint32_t L, const uint64_t hb[4], const uint64_t bhead[4]) {
   if (T.br_hash)
     for (int q = 0; q < 4; ++q) T.br_hash[4 * j + q] = hb[q];
@@ -1034,17 +981,12 @@ KH_HD uint32_t op_branch_hash(const Topo& T, uint32_t j, uint64_t g, uint32_t* i
   bool top = T.br_parent[j] == NONE;
   *inl = 0;
   uint64_t hb[4], bhead[4];
-  uint32_t L, perms = 0, ninl = 0;
-  if (T.br_dirty && !T.br_dirty[j]) {
-    if (!branch_clean_ref(T, j, &L, hb, bhead)) return 0;
-  } else {
-    L = T.br_len[j];
-    Slot sl = branch_slot(T, g, d, false);
-    perms = hash_slot(sl, L, top && ext == 0, hb);
-    slot_head(sl, L, bhead);
-    ninl = (L < 32 && !(top && ext == 0)) ? 1 : 0;
-    branch_keep(T, j, L, hb, bhead);
-  }
+  const uint32_t L = T.br_len[j];
+  Slot sl = branch_slot(T, g, d, false);
+  uint32_t perms = hash_slot(sl, L, top && ext == 0, hb);
+  slot_head(sl, L, bhead);
+  uint32_t ninl = (L < 32 && !(top && ext == 0)) ? 1 : 0;
+  branch_keep(T, j, L, hb, bhead);
   perms += branch_publish(T, j, L, hb, bhead, branch_slot(T, g, d, true), &ninl);
   *inl = ninl;
   return perms;
@@ -1061,9 +1003,7 @@ KH_HD uint32_t op_branch_fused(const Topo& T, uint32_t j, uint64_t* slot, uint64
   *inl = 0;
   uint64_t hb[4] = {0, 0, 0, 0}, bhead[4] = {0, 0, 0, 0};
   uint32_t L, perms = 0, ninl = 0;
-  if (T.br_dirty && !T.br_dirty[j]) {
-    if (!branch_clean_ref(T, j, &L, hb, bhead)) return 0;
-  } else {
+  {
     const uint32_t payload = branch_payload(T, j);
     L = rlp_hdr_len(payload) + payload;
     T.br_len[j] = L;
@@ -1110,8 +1050,7 @@ KH_HD uint32_t op_branch_fused(const Topo& T, uint32_t j, uint64_t* slot, uint64
 // (an extension is re-encoded only when perms were spent on it or its branch)
 KH_HD uint32_t branch_hash_count(const Topo& T, uint32_t j, uint32_t perms) {
   const bool top = T.br_parent[j] == NONE, ext = T.br_ext[j] != 0;
-  const bool hashed_branch = !T.br_dirty || T.br_dirty[j];
-  uint32_t h = (hashed_branch && (T.br_len[j] >= 32 || (top && !ext))) ? 1 : 0;
+  uint32_t h = (T.br_len[j] >= 32 || (top && !ext)) ? 1 : 0;
   if (ext && perms) h += (T.ex_len[j] >= 32 || top) ? 1 : 0;
   return h;
 }

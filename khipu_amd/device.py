@@ -237,6 +237,18 @@ class ResidentForest:
     def nodes(self):
         return emitted_nodes(lambda *a: lib().kh_trie_emit_nodes(self.h, *a))
 
+    def last_roots(self):
+        """{trie_id: root} of the last commit (kh_forest_last_roots; also after block_commit)."""
+        n = ctypes.c_uint64()
+        rc = lib().kh_forest_last_roots(self.h, None, None, 0, ctypes.byref(n))
+        if rc not in (_lib.KH_OK, _lib.KH_ENOSPC):
+            check(rc)
+        cap = n.value
+        tries = np.zeros(max(cap, 1), np.uint32)
+        roots = np.zeros(32 * max(cap, 1), np.uint8)
+        check(lib().kh_forest_last_roots(self.h, tries.ctypes.data, roots.ctypes.data, cap, ctypes.byref(n)))
+        return {int(tries[i]): roots[32 * i:32 * i + 32].tobytes() for i in range(n.value)}
+
     def __len__(self):
         n = ctypes.c_uint64()
         check(lib().kh_trie_size(self.h, ctypes.byref(n)))
@@ -252,3 +264,21 @@ class ResidentForest:
             self.close()
         except Exception:
             pass
+
+
+def block_commit(state, forest, s_up_trie, s_up_keys, s_up_vals, s_up_voff, ns_up, s_del_trie, s_del_keys, ns_del,
+                 a_up_keys, a_up_vals, a_up_voff, a_up_trie, na_up, a_del_keys, na_del, s_klen=32, a_klen=32,
+                 stats=None):
+    """One block through kh_block_commit (device tensors): the storage ops into the forest,
+    the touched tries' new roots written into the stateRoot of the account upserts that name
+    them (a_up_trie, KH_NO_TRIE for none; a_up_vals is patched in place), then the account
+    ops into the state trie.  Returns the new state root."""
+    root = np.zeros(32, np.uint8)
+    st = stats if stats is not None else KhStats()
+    state.ctx._sync()
+    check(lib().kh_block_commit(state.h, forest.h, _ptr(s_up_trie), _ptr(s_up_keys), _ptr(s_up_vals), _ptr(s_up_voff),
+                                ns_up, _ptr(s_del_trie), _ptr(s_del_keys), ns_del, s_klen, _ptr(a_up_keys),
+                                _ptr(a_up_vals), _ptr(a_up_voff), _ptr(a_up_trie), na_up, _ptr(a_del_keys), na_del,
+                                a_klen, root.ctypes.data, ctypes.byref(st)))
+    state.root = root.tobytes()
+    return state.root

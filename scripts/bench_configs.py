@@ -1,19 +1,19 @@
 """Secondary workloads of BASELINE.json `configs` on one MI355X (bench.py measures configs[4]).
 
   --cfg 2  configs[1]: 1M synthetic accounts, full build + root (keys hashed on the GPU).
-  --cfg 3  configs[2]: incremental block commit over a resident trie:
-           open N_RES accounts (default 50M) with kh_trie_open, then per block 20k dirty
-           accounts (90% balance/nonce updates, 5% inserts, 5% deletes) through kh_trie_apply;
-           the block's storage side is 2,000 contracts x 1k slots re-rooted as one
-           segmented build (kh_dev_trie_build, d_seg), and 50 of them also as resident
-           tries with 10 dirty slots each (per-trie kh_trie_apply latency).
+  --cfg 3  configs[2]: block commits over a resident state: N_RES
+           accounts (default 50M) plus 2,000 resident 1k-slot storage tries; per block 20k
+           dirty accounts (90% updates, 5% inserts, 5% deletes) and 10 dirty slots per
+           contract, storage roots injected into the accounts, one kh_block_commit
+           (tests/blocks.py).
   --cfg 4  configs[3]: 100k storage tries, slot counts log-uniform in [1, 1e4], slot key =
            kec256(32-byte BE slot index) (KH_HASH_KEYS), value = RLP(trimmed 1-32 random
            bytes), one segmented build; 4 segments re-built alone must give the same roots.
 
 Inputs are generated on the device before the timed region.  Prints one JSON line per
-config.  Parity of these paths is tests/test_gpu_resident.py and test_gpu_parity.py;
-here every root is also cross-checked against a from-scratch device build.
+config.  Parity of these paths is tests/test_gpu_configs.py, test_gpu_resident.py and
+test_gpu_parity.py; here every root is also cross-checked against a from-scratch device
+build of the same final set.
 """
 import argparse
 import json
@@ -28,9 +28,8 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-from khipu_amd import _lib  # noqa: E402
-from khipu_amd._lib import KhStats, check, lib  # noqa: E402
-from khipu_amd.device import Ctx, ResidentTrie, _ptr  # noqa: E402
+from khipu_amd._lib import check, lib  # noqa: E402
+from khipu_amd.device import Ctx, _ptr  # noqa: E402
 
 DEV = "cuda:0"
 
@@ -93,88 +92,35 @@ def cfg2(args):
 
 
 def cfg3(args):
+    """configs[2] at its configured size: tests/blocks.py's workload over a 50M-account
+    resident state trie with 2,000 resident 1k-slot storage tries; one kh_block_commit per
+    block.  The final state root and every storage root are checked against from-scratch
+    GPU builds of the final sets (parity of the same path at 1M against the CPU batch
+    builder and the oracle: tests/test_gpu_configs.py::test_config2_block_commits)."""
+    from tests.blocks import BlockWorkload
     ctx = Ctx(0)
-    n = args.resident
-    g = torch.Generator(device=DEV)
-    g.manual_seed(3)
-    addr, vals, voff = ctx.synth_accounts(3, 0, n)
-    keys = hash_keys(ctx, addr, 20, n)
-    del addr
-    t = ResidentTrie.__new__(ResidentTrie)
-    t.ctx, t.dev, t.h = ctx, DEV, None
+    nb = args.warmup + args.steps
     t0 = time.perf_counter()
-    t._open(keys, 32, vals, voff, n, False)
+    w = BlockWorkload(ctx, args.resident, nb)
     open_s = time.perf_counter() - t0
-    del vals, voff
-    nupd, nins, ndel = 18_000, 1_000, 1_000
-    blocks = []
-    for blk in range(args.warmup + args.steps):
-        # dirty set: updates/deletes of resident accounts, inserts of fresh addresses
-        pick = torch.randperm(n, generator=g, device=DEV)[:nupd + ndel]
-        kk = keys[:32 * n].view(n, 32)
-        up_old = kk[pick[:nupd]].reshape(-1)
-        dels = kk[pick[nupd:]].reshape(-1).clone()
-        a2, v2, o2 = ctx.synth_accounts(3, 10**9 + blk * 100_000, nupd + nins)
-        new_keys = hash_keys(ctx, a2, 20, nins)[:32 * nins]
-        up_keys = torch.cat([up_old, new_keys]).contiguous()
-        torch.cuda.synchronize()
-        st = KhStats()
-        t0 = time.perf_counter()
-        root = t.commit_dev(up_keys, v2, o2, nupd + nins, dels, ndel, 32, False, st)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        # later blocks may pick a key deleted earlier: updating it re-inserts it, which
-        # is a valid put (the block's dirty set stays 20k records)
-        if blk >= args.warmup:
-            blocks.append((dt * 1e3, st.t_total_ms, st.n_node_hashes, st.n_leaves))
-    live = len(t)
-    ms = np.array([b[0] for b in blocks])
-    out = {"config": f"configs[2]: 20k dirty accounts per block over a {n // 10**6}M-account resident trie",
-           "open_s": open_s, "commit_ms_median": float(np.median(ms)), "commit_ms_all": ms.tolist(),
-           "commit_device_ms_median": float(np.median([b[1] for b in blocks])),
-           "rehashed_nodes_median": int(np.median([b[2] for b in blocks])), "resident_accounts_after": live,
-           "root_after": root.hex()}
-    t.close()
-    del keys
-    torch.cuda.empty_cache()
-
-    # storage side of the block: 2,000 contracts x 1k slots, 10 dirty slots each
-    nc, ns = 2000, 1000
-    idx = torch.arange(ns, device=DEV, dtype=torch.int64).repeat(nc)
-    seg = torch.arange(nc, device=DEV, dtype=torch.int32).repeat_interleave(ns)
-    sk = slot_keys(idx)
-    sv, so = storage_values(g, nc * ns)
-    hh, st = seg_build(ctx, sk, sv, so, seg, nc, nc * ns)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        hh, st = seg_build(ctx, sk, sv, so, seg, nc, nc * ns)
-    torch.cuda.synchronize()
-    out["storage_segmented_ms"] = (time.perf_counter() - t0) / args.steps * 1e3
-    out["storage_segmented"] = f"{nc} storage tries x {ns} slots re-rooted in one segmented build"
-    # resident per-contract commits: 10 dirty slots (10% zero = delete) on 50 tries
-    lat = []
-    skh = sk.view(nc * ns, 32)
-    for c in range(50):
-        lo, hi = c * ns, (c + 1) * ns
-        kc = hash_keys(ctx, skh[lo:hi].reshape(-1).contiguous(), 32, ns)
-        vc = sv[int(so[lo]):int(so[hi])].contiguous()
-        oc = (so[lo:hi + 1] - so[lo]).contiguous()
-        rt = ResidentTrie.__new__(ResidentTrie)
-        rt.ctx, rt.dev, rt.h = ctx, DEV, None
-        rt._open(kc, 32, vc, oc, ns, False)
-        assert rt.root == hh[c].tobytes(), "resident storage root != segmented root"
-        kcv = kc[:32 * ns].view(ns, 32)
-        up = kcv[0:9].reshape(-1).contiguous()
-        uv, uo = storage_values(g, 9)
-        dl = kcv[9:10].reshape(-1).contiguous()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        rt.commit_dev(up, uv, uo, 9, dl, 1, 32, False)
-        lat.append((time.perf_counter() - t0) * 1e3)
-        rt.close()
-    out["storage_resident_commit_ms_median"] = float(np.median(lat))
-    return out
+    for b in range(nb):
+        root = w.block(b)
+    blocks = w.t_commit[args.warmup:]
+    ms = np.array([x[0] for x in blocks])
+    K, V, O, N = w.final_accounts()
+    hf, _, _, _ = ctx.build(K, 32, V, O, N)
+    assert hf[0].tobytes() == root, "block-commit state root != full build of the final state"
+    del K, V, O
+    K, V, O, T, N = w.final_storage()
+    hh, _, _, _ = ctx.build(K, 32, V, O, N, seg=T, nseg=w.nc, hash_keys=True)
+    bad = [c for c in range(w.nc) if hh[c].tobytes() != w.roots[c]]
+    assert not bad, f"storage roots differ from full builds: {bad[:5]}"
+    return {"config": f"configs[2]: 20k dirty accounts + 2,000 storage tries x 10 dirty slots per block over a "
+                      f"{args.resident // 10**6}M-account resident trie (kh_block_commit)",
+            "open_s": open_s, "block_ms_median": float(np.median(ms)), "block_ms_all": ms.tolist(),
+            "rehashed_nodes_median": int(np.median([x[1] for x in blocks])),
+            "ops_per_block": int(blocks[0][2]), "resident_accounts_after": len(w.state),
+            "state_root_after": root.hex(), "checked": "state root and all 2,000 storage roots == full GPU builds"}
 
 
 def cfg4(args):

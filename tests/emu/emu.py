@@ -21,10 +21,6 @@ def lib():
         L.emu_kec256.argtypes = [vp, ctypes.c_uint64, vp]
         L.emu_synth.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp]
         L.emu_fold16.argtypes = [vp, vp, vp, vp]
-        L.emu_trie_open.argtypes = [vp, vp, vp, ctypes.c_uint64, vp]
-        L.emu_trie_open.restype = vp
-        L.emu_trie_apply.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp, vp]
-        L.emu_trie_free.argtypes = [vp]
         L.emu_node_children.argtypes = [vp, ctypes.c_uint64, ctypes.c_int, vp, vp, vp]
         _lib = L
     return _lib
@@ -75,37 +71,6 @@ def synth(cfg, first, n):
     off = np.zeros(n + 1, np.uint64)
     lib().emu_synth(cfg, first, n, addr.ctypes.data, vals.ctypes.data, off.ctypes.data)
     return addr[:20 * n].reshape(n, 20), vals[:int(off[n])], off
-
-
-class ResidentTrie:
-    """Host replay of the resident trie (kh_trie_open / kh_trie_apply)."""
-
-    def __init__(self, keys32=(), vals=()):
-        kb = _buf(b"".join(keys32) + b"\0" * 16)
-        vb, off = pack(list(vals))
-        root = np.zeros(32, np.uint8)
-        self.h = lib().emu_trie_open(kb.ctypes.data, vb.ctypes.data, off.ctypes.data, len(keys32), root.ctypes.data)
-        assert self.h
-        self.root = root.tobytes()
-
-    def commit(self, upserts=(), deletes=()):
-        ups = list(upserts.items()) if isinstance(upserts, dict) else list(upserts)
-        uk = _buf(b"".join(k for k, _ in ups) + b"\0" * 16)
-        uv, uo = pack([v for _, v in ups])
-        dk = _buf(b"".join(deletes) + b"\0" * 16)
-        root = np.zeros(32, np.uint8)
-        st = np.zeros(4, np.uint64)
-        rc = lib().emu_trie_apply(self.h, uk.ctypes.data, uv.ctypes.data, uo.ctypes.data, len(ups), dk.ctypes.data,
-                                  len(deletes), root.ctypes.data, st.ctypes.data)
-        assert rc == 0, rc
-        self.root = root.tobytes()
-        self.stats = st
-        return self.root
-
-    def __del__(self):
-        if getattr(self, "h", None):
-            lib().emu_trie_free(self.h)
-            self.h = None
 
 
 def node_children(value: bytes, kind: int):

@@ -54,3 +54,48 @@ def test_config3_100k_storage_tries(khst, oracle):
         ks = [oracle.kec256(keys[32 * i:32 * i + 32].tobytes()) for i in range(a, b)]
         vs = [vb[int(voff[i]):int(voff[i + 1])].tobytes() for i in range(a, b)]
         assert gpu[s] == oracle.seq_root(ks, vs), s
+
+
+def test_config2_block_commits(khst, oracle):
+    """configs[2] shape at 1M resident accounts (tests/blocks.py): 3 blocks of 20k dirty
+    accounts (90% updates, 5% inserts, 5% deletes) and 2,000 resident 1k-slot storage tries
+    with 10 dirty slots each (10% deletes), storage roots injected into the account bodies,
+    one kh_block_commit per block.  Checks: every storage root against a from-scratch
+    segmented GPU build and the CPU batch builder; sampled storage tries against the
+    sequential oracle; the final state root against the CPU batch builder over the whole
+    final state and a from-scratch GPU build."""
+    import torch
+    from khipu_amd.device import Ctx
+    from tests.blocks import BlockWorkload
+    ctx = Ctx(0)
+    nb = 3
+    w = BlockWorkload(ctx, 1_000_000, nb)
+    for b in range(nb):
+        root = w.block(b)
+    # storage tries
+    K, V, O, T, N = w.final_storage()
+    hh, ll, _, _ = ctx.build(K, 32, V, O, N, seg=T, nseg=w.nc, hash_keys=True)
+    so = O.cpu().numpy().astype(np.uint64)
+    tid = T.cpu().numpy()
+    seg_off = np.searchsorted(tid, np.arange(w.nc + 1)).astype(np.uint64)
+    kb = K.cpu().numpy()
+    vb = V[:int(so[-1])].cpu().numpy()
+    cpu, _ = oracle.batch_roots(kb, (vb, so), klen=32, seg_off=seg_off, hash_keys=True)
+    for c in range(w.nc):
+        assert w.roots[c] == hh[c].tobytes() == cpu[c], c
+    for c in (0, 777, w.nc - 1):
+        a, e = int(seg_off[c]), int(seg_off[c + 1])
+        t = oracle.Trie()
+        for i in range(a, e):
+            t.put(oracle.kec256(kb[32 * i:32 * i + 32].tobytes()), vb[int(so[i]):int(so[i + 1])].tobytes())
+        assert t.root_hash() == w.roots[c], c
+    # state trie
+    K, V, O, N = w.final_accounts()
+    hf, _, _, _ = ctx.build(K, 32, V, O, N)
+    assert hf[0].tobytes() == root
+    vo = O.cpu().numpy().astype(np.uint64)
+    cpu, cst = oracle.batch_roots(K.cpu().numpy(), (V[:int(vo[-1])].cpu().numpy(), vo), klen=32)
+    assert cpu[0] == root
+    assert len(w.state) == cst["distinct"]
+    # O(dirty) work: a block re-hashes a small fraction of the 1.36M nodes of a full build
+    assert max(x[1] for x in w.t_commit) < 400_000, w.t_commit
