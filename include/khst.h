@@ -191,6 +191,17 @@ int kh_trie_open(kh_ctx* ctx, const uint8_t* d_keys, uint32_t klen, const uint8_
 int kh_trie_open_host(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const uint64_t* voff, uint64_t n,
                       uint32_t flags, uint8_t root32[32], kh_trie** out);
 
+/* Open a trie from its root hash and a node store: MerklePatriciaTrie.apply(
+ * rootHash, source) with getNode (MerklePatriciaTrie.scala:60-66,520-542).  The store holds
+ * n node encodings enc[off[i] .. off[i+1]), keyed by their kec256 (content addressed, as
+ * NodeStorage is); the nodes reachable from root32 are decoded on the device.  A node
+ * missing from the store returns KH_ENODE with its hash in missing32
+ * (MPTNodeMissingException); EMPTY_TRIE_HASH opens an empty trie. */
+int kh_trie_open_nodes(kh_ctx* ctx, const uint8_t root32[32], const uint8_t* d_enc, const uint64_t* d_off, uint64_t n,
+                       uint32_t flags, uint8_t missing32[32], kh_trie** out);
+int kh_trie_open_nodes_host(const uint8_t root32[32], const uint8_t* enc, const uint64_t* off, uint64_t n,
+                            uint32_t flags, uint8_t missing32[32], kh_trie** out);
+
 /* One commit; root32 receives the new root.  stats: n_node_hashes counts the nodes re-hashed. */
 int kh_trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals, const uint64_t* d_up_voff,
                   uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,

@@ -28,7 +28,8 @@ EXPORTS = (
     "kh_dev_kec256_batch", "kh_dev_trie_build", "kh_fold_root16", "kh_dev_synth_accounts", "kh_dev_hash_keys",
     "kh_dev_partition", "kh_trie_open", "kh_trie_apply", "kh_trie_emit_nodes", "kh_trie_size", "kh_trie_free",
     "kh_verify_nodes", "kh_trie_open_host", "kh_trie_apply_host", "kh_forest_open", "kh_forest_apply",
-    "kh_forest_apply_host", "kh_block_commit", "kh_forest_last_roots",
+    "kh_forest_apply_host", "kh_block_commit", "kh_forest_last_roots", "kh_trie_open_nodes",
+    "kh_trie_open_nodes_host",
 )
 
 
@@ -114,6 +115,8 @@ def lib():
     L.kh_forest_apply.argtypes = [vp, vp, vp, vp, vp, u64, vp, vp, u64, u32, vp, vp, u64, vp, vp]
     L.kh_forest_apply_host.argtypes = [vp, vp, vp, vp, vp, u64, vp, vp, u64, u32, vp, vp, u64, vp, vp]
     L.kh_forest_last_roots.argtypes = [vp, vp, vp, u64, vp]
+    L.kh_trie_open_nodes.argtypes = [vp, vp, vp, vp, u64, u32, vp, ctypes.POINTER(vp)]
+    L.kh_trie_open_nodes_host.argtypes = [vp, vp, vp, u64, u32, vp, ctypes.POINTER(vp)]
     L.kh_block_commit.argtypes = [vp, vp, vp, vp, vp, vp, u64, vp, vp, u64, u32, vp, vp, vp, vp, u64, vp, u64, u32,
                                   vp, vp]
     for name in EXPORTS:

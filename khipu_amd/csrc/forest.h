@@ -30,6 +30,7 @@
 // Work per commit is O(dirty keys x depth x 16), not O(resident keys).
 #pragma once
 #include "keyorder.h"
+#include "nodedata.h"
 
 namespace khst {
 
@@ -163,6 +164,50 @@ KH_HD void elem_from_record(const Recs& R, uint32_t r, uint32_t seg, const Elems
   E.oldd[e] = R.rd[r];
   for (int q = 0; q < 4; ++q) E.cref[4 * e + q] = R.rref[4ull * r + q];
   E.crl[e] = R.rrl[r];
+}
+
+
+// ---- open a resident trie from (root hash, node store):
+// MerklePatriciaTrie.apply(rootHash, source) + getNode (MerklePatriciaTrie.scala:60-66,
+// 520-542; Node.nodeDec, Node.scala:46-102): the nodes reachable from the root are
+// decoded level by level on the device into records.  A frontier item is one node to
+// decode: referenced by hash (looked up in the store) or embedded (its < 32-byte
+// encoding carried in the item).
+struct OItems {
+  uint64_t* pre;   // [cap*4] key prefix: nibbles [0, d) of every key below
+  uint8_t* a;      // anchor depth of the record the node belongs to
+  uint8_t* d;      // depth at which the node starts (> a: the child of an extension)
+  uint64_t* ref;   // [cap*4] hash, or the embedded encoding
+  uint8_t* rl;     // 32 = hash, else the embedded length
+  uint64_t* pref;  // [cap*4] the capped reference the record's parent holds
+  uint8_t* prl;
+  unsigned long long* n;
+  uint64_t cap;
+};
+struct NStore {
+  const uint64_t* hash;  // [m*4] sorted node hashes
+  const uint32_t* idx;   // [m] node index of sorted hash i
+  uint64_t m;
+  const uint8_t* enc;
+  const uint64_t* off;   // [n+1]
+};
+enum : unsigned long long { OPEN_OK = 0, OPEN_MISSING = 1, OPEN_BAD = 2, OPEN_VALUE = 3 };
+
+KH_HD void hp_nibbles(const uint8_t* b, uint32_t len, uint32_t* n, bool* leaf, uint8_t* out) {
+  // HexPrefix.decode (HexPrefix.scala:30-40): flag nibble, optional pad nibble
+  const uint32_t f = b[0] >> 4;
+  *leaf = (f & 2) != 0;
+  uint32_t k = 0;
+  if (f & 1) out[k++] = b[0] & 0xF;
+  for (uint32_t i = 1; i < len && k < 64; ++i) {
+    out[k++] = b[i] >> 4;
+    if (k < 64) out[k++] = b[i] & 0xF;
+  }
+  *n = k;
+}
+KH_HD void words_of(const uint8_t* p, uint32_t len, uint64_t w[4]) {  // <= 32 bytes, zero padded
+  for (int q = 0; q < 4; ++q) w[q] = 0;
+  for (uint32_t i = 0; i < len && i < 32; ++i) w[i >> 3] |= (uint64_t)p[i] << (8 * (i & 7));
 }
 
 }  // namespace khst

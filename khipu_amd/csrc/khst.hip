@@ -1944,6 +1944,136 @@ static void map_rebuild(kh_trie* h, uint64_t headroom) {
   h->rdead = h->rn - h->mused;
 }
 
+// one level of the open-from-store walk: decode every frontier node into a record (a
+// leaf, or a branch with the extension above it) and push its children to the next level
+__global__ void __launch_bounds__(BS) k_open_level(OItems I, uint64_t ni, OItems N, NStore S, Recs R,
+                                                   unsigned long long* rcount, uint64_t rbase, uint32_t trie,
+                                                   uint8_t* heap, unsigned long long* heap_n,
+                                                   unsigned long long* leaves, unsigned long long* err,
+                                                   uint8_t* missing) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= ni) return;
+  const uint64_t* h = I.ref + 4 * i;
+  const uint8_t* e;
+  uint32_t L;
+  if (I.rl[i] == 32) {
+    const uint64_t p = key_lower_bound(S.hash, S.m, h);
+    if (p >= S.m || key_cmp(S.hash + 4 * p, h) != 0) {  // MPTNodeMissingException (MerklePatriciaTrie.scala:534-537)
+      if (atomicCAS(err, OPEN_OK, OPEN_MISSING) == OPEN_OK)
+        for (int q = 0; q < 32; ++q) missing[q] = (uint8_t)(h[q >> 3] >> (8 * (q & 7)));
+      return;
+    }
+    const uint32_t j = S.idx[p];
+    e = S.enc + S.off[j];
+    L = (uint32_t)(S.off[j + 1] - S.off[j]);
+  } else {
+    e = (const uint8_t*)h;
+    L = I.rl[i];
+  }
+  auto bad = [&](unsigned long long code) { atomicCAS(err, OPEN_OK, code); };
+  RItem top;
+  if (!rlp_valid(e, L, 0, 0) || !rlp_at(e, L, 0, top) || !top.list) return bad(OPEN_BAD);
+  RItem it[18];
+  const int k = rlp_items(e, L, top, it, 18);
+  const uint32_t a = I.a[i], d = I.d[i];
+  uint64_t own[4];  // the node's capped reference (Node.capped, Node.scala:114)
+  uint32_t ownl;
+  if (L >= 32) {
+    for (int q = 0; q < 4; ++q) own[q] = h[q];  // referenced by hash (a root < 32 B: its bytes below)
+    ownl = 32;
+  } else {
+    words_of(e, L, own);
+    ownl = L;
+  }
+  if (L >= 32 && I.rl[i] != 32) return bad(OPEN_BAD);  // an embedded node must be < 32 B
+  const uint64_t* pre = I.pre + 4 * i;
+  auto push = [&](const uint64_t* np, uint32_t na, uint32_t nd, const uint8_t* cref, uint32_t crl, bool is_hash,
+                  const uint64_t* pr, uint32_t prl) {
+    const unsigned long long t = atomicAdd(N.n, 1ULL);
+    if (t >= N.cap) return bad(OPEN_BAD);
+    for (int q = 0; q < 4; ++q) N.pre[4 * t + q] = np[q];
+    N.a[t] = (uint8_t)na;
+    N.d[t] = (uint8_t)nd;
+    uint64_t w[4];
+    words_of(cref, crl, w);
+    for (int q = 0; q < 4; ++q) N.ref[4 * t + q] = w[q];
+    N.rl[t] = (uint8_t)(is_hash ? 32 : crl);
+    for (int q = 0; q < 4; ++q) N.pref[4 * t + q] = pr ? pr[q] : w[q];
+    N.prl[t] = (uint8_t)(pr ? prl : (is_hash ? 32 : crl));
+  };
+  if (k == 17) {  // branch [ref_0 .. ref_15, value]
+    if (it[16].list || it[16].len) return bad(OPEN_VALUE);  // a secure trie never stores a branch value
+    uint32_t mask = 0;
+    for (int c = 0; c < 16; ++c) {
+      if (!it[c].list && it[c].len == 0) continue;
+      if (!it[c].list && it[c].len != 32) return bad(OPEN_BAD);
+      uint64_t np[4] = {pre[0], pre[1], pre[2], pre[3]};
+      set_nibble(np, d, (uint32_t)c);
+      if (!it[c].list) {
+        push(np, d + 1, d + 1, e + it[c].off, 32, true, nullptr, 0);
+      } else {
+        const uint32_t st = c ? it[c - 1].next : top.off;
+        push(np, d + 1, d + 1, e + st, it[c].next - st, false, nullptr, 0);
+      }
+      mask |= 1u << c;
+    }
+    const uint64_t r = rbase + atomicAdd(rcount, 1ULL);
+    for (int q = 0; q < 4; ++q) {
+      R.rk[4 * r + q] = pre[q];
+      R.rbref[4 * r + q] = own[q];
+      R.rref[4 * r + q] = I.pref[4 * i + q];
+    }
+    R.rt[r] = trie;
+    R.rd[r] = (uint8_t)a;
+    R.rdb[r] = (uint8_t)d;
+    R.rvo[r] = 0;
+    R.rvl[r] = 0;
+    R.rbrl[r] = (uint8_t)ownl;
+    R.rrl[r] = I.prl[i];
+    R.rmask[r] = (uint16_t)mask;
+    R.rlive[r] = REC_LIVE;
+    return;
+  }
+  if (k != 2 || it[0].list || it[0].len == 0 || d != a) return bad(OPEN_BAD);  // a leaf / extension hangs where it starts
+  uint8_t nib[64];
+  uint32_t np = 0;
+  bool leaf = false;
+  hp_nibbles(e + it[0].off, it[0].len, &np, &leaf, nib);
+  uint64_t key[4] = {pre[0], pre[1], pre[2], pre[3]};
+  if (d + np > 64) return bad(OPEN_BAD);
+  for (uint32_t q = 0; q < np; ++q) set_nibble(key, d + q, nib[q]);
+  if (leaf) {  // [HP(path, leaf), value]: the key is complete (32-byte keys)
+    if (d + np != 64 || it[1].list) return bad(OPEN_BAD);
+    const uint64_t vo = atomicAdd(heap_n, (unsigned long long)it[1].len);
+    for (uint32_t q = 0; q < it[1].len; ++q) heap[vo + q] = e[it[1].off + q];
+    const uint64_t r = rbase + atomicAdd(rcount, 1ULL);
+    for (int q = 0; q < 4; ++q) {
+      R.rk[4 * r + q] = key[q];
+      R.rbref[4 * r + q] = 0;
+      R.rref[4 * r + q] = I.pref[4 * i + q];
+    }
+    R.rt[r] = trie;
+    R.rd[r] = (uint8_t)a;
+    R.rdb[r] = EL_LEAF;
+    R.rvo[r] = vo;
+    R.rvl[r] = it[1].len;
+    R.rbrl[r] = 0;
+    R.rrl[r] = I.prl[i];
+    R.rmask[r] = 0;
+    R.rlive[r] = REC_LIVE;
+    atomicAdd(leaves, 1ULL);
+    return;
+  }
+  // extension [HP(shared, ext), ref]: its branch child gets the extension's record (anchor a)
+  if (np == 0) return bad(OPEN_BAD);
+  if (!it[1].list) {
+    if (it[1].len != 32) return bad(OPEN_BAD);
+    push(key, a, d + np, e + it[1].off, 32, true, I.pref + 4 * i, I.prl[i]);
+  } else {
+    push(key, a, d + np, e + it[0].next, it[1].next - it[0].next, false, I.pref + 4 * i, I.prl[i]);
+  }
+}
+
 struct FCommit {  // one commit's inputs (device buffers)
   const uint32_t* up_trie = nullptr;  // nullable: trie 0
   const uint8_t* up_keys = nullptr;
@@ -2640,6 +2770,114 @@ int kh_verify_nodes(const uint8_t* data, const uint64_t* off, uint64_t n, const 
   })
 }
 
+static OItems oitems_carve(DevBuf& b, uint64_t cap) {
+  b.ensure(carve_size({cap * 32, cap, cap, cap * 32, cap, cap * 32, cap, 64}));
+  Carver cv{(char*)b.p, 0, b.cap};
+  OItems I{};
+  I.pre = cv.take<uint64_t>(cap * 4);
+  I.a = cv.take<uint8_t>(cap);
+  I.d = cv.take<uint8_t>(cap);
+  I.ref = cv.take<uint64_t>(cap * 4);
+  I.rl = cv.take<uint8_t>(cap);
+  I.pref = cv.take<uint64_t>(cap * 4);
+  I.prl = cv.take<uint8_t>(cap);
+  I.n = cv.take<unsigned long long>(8);
+  I.cap = cap;
+  return I;
+}
+
+// open an (empty) trie from root32 and n stored node encodings (device buffers)
+static void trie_open_nodes(kh_trie* h, const uint8_t* root32, const uint8_t* d_enc, const uint64_t* d_off,
+                            uint64_t n, uint8_t* missing32) {
+  kh_ctx* c = h->c;
+  hipStream_t st = c->st;
+  memcpy(h->root, root32, 32);
+  if (memcmp(root32, EMPTY_TRIE_HASH, 32) == 0) return;  // MerklePatriciaTrie.scala:60-66
+  if (n >= (1ULL << 31)) throw KhError{KH_EINVAL, "node store too large"};
+  // the store, keyed by kec256 of each encoding (content addressed)
+  std::vector<size_t> sz = {n * 32 + 32, n * 8, n * 8, n * 4, n * 4, n * 32 + 32, radix_scratch_bytes(n + 1),
+                            scan_scratch_bytes(n + 1, 8), CTR_N * 8, 64, 64};
+  h->ws.ensure(carve_size(sz));
+  Carver cv{(char*)h->ws.p, 0, h->ws.cap};
+  uint64_t* hs = cv.take<uint64_t>(n * 4 + 4);
+  SortIO S{};
+  S.K32 = hs;
+  S.n = n;
+  S.ck0 = cv.take<uint64_t>(n);
+  S.ck1 = cv.take<uint64_t>(n);
+  S.idx0 = cv.take<uint32_t>(n);
+  S.idx1 = cv.take<uint32_t>(n);
+  S.skey = cv.take<uint64_t>(n * 4 + 4);
+  S.rs_scratch = cv.take<char>(radix_scratch_bytes(n + 1));
+  S.scan_scratch = cv.take<char>(scan_scratch_bytes(n + 1, 8));
+  S.ctr = cv.take<unsigned long long>(CTR_N);
+  unsigned long long* oc = cv.take<unsigned long long>(8);  // records, heap bytes, leaves, error
+  uint8_t* dmiss = cv.take<uint8_t>(64);
+  HIPCHK(hipMemsetAsync(S.ctr, 0, CTR_N * 8, st));
+  HIPCHK(hipMemsetAsync(oc, 0, 64, st));
+  uint64_t total = 0;
+  NStore NS{nullptr, nullptr, 0, d_enc, d_off};
+  if (n) {
+    hipLaunchKernelGGL(k_kec_batch, GRID(n, BS), dim3(BS), 0, st, d_enc, d_off, n, hs);
+    LAUNCH_CHECK();
+    sort_dedup(c, S);
+    NS.hash = S.skey;
+    NS.idx = S.sidx;
+    NS.m = S.m;
+    HIPCHK(hipMemcpyAsync(c->h_pinned, d_off, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned + 1, d_off + n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    total = c->h_pinned[1] - c->h_pinned[0];
+  }
+  // leaf values land in the heap: at most the store's bytes
+  regrow(h->heap, h->heap_n, h->heap_n + total + 64, st);
+  c->h_pinned[0] = h->heap_n;
+  HIPCHK(hipMemcpyAsync(oc + 1, c->h_pinned, 8, hipMemcpyHostToDevice, st));
+  DevBuf fa, fb;
+  OItems cur = oitems_carve(fa, 1);
+  {  // the root: referenced by its hash, at anchor 0
+    uint64_t w[4];
+    memcpy(w, root32, 32);
+    c->h_pinned[1] = 1;
+    HIPCHK(hipMemsetAsync(cur.pre, 0, 32, st));
+    HIPCHK(hipMemsetAsync(cur.a, 0, 1, st));
+    HIPCHK(hipMemsetAsync(cur.d, 0, 1, st));
+    HIPCHK(hipMemcpyAsync(cur.ref, w, 32, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(cur.pref, w, 32, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(cur.rl, 32, 1, st));
+    HIPCHK(hipMemsetAsync(cur.prl, 32, 1, st));
+    HIPCHK(hipStreamSynchronize(st));  // w is a host temporary
+  }
+  uint64_t ni = 1, nrec = 0;
+  for (int level = 0; ni && level < 80; ++level) {
+    recs_reserve(h, h->rn + nrec + ni + 16);
+    OItems nxt = oitems_carve(level & 1 ? fa : fb, 16 * ni);
+    HIPCHK(hipMemsetAsync(nxt.n, 0, 8, st));
+    hipLaunchKernelGGL(k_open_level, GRID(ni, BS), dim3(BS), 0, st, cur, ni, nxt, NS, recs_of(h), oc, h->rn,
+                       0u, (uint8_t*)h->heap.p, oc + 1, oc + 2, oc + 3, dmiss);
+    LAUNCH_CHECK();
+    HIPCHK(hipMemcpyAsync(c->h_pinned, nxt.n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned + 1, oc, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned + 8, dmiss, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint64_t code = c->h_pinned[4];
+    if (code == OPEN_MISSING) {
+      if (missing32) memcpy(missing32, c->h_pinned + 8, 32);
+      throw KhError{KH_ENODE, "node missing from the store (MPTNodeMissingException)"};
+    }
+    if (code == OPEN_VALUE) throw KhError{KH_EINVAL, "a branch with a value: not a secure trie"};
+    if (code) throw KhError{KH_EINVAL, "the store holds a node that is not a canonical secure-trie node"};
+    nrec = c->h_pinned[1];
+    ni = c->h_pinned[0];
+    cur = nxt;
+  }
+  if (ni) throw KhError{KH_EINVAL, "node store deeper than a 32-byte key allows"};
+  h->rn += nrec;
+  h->heap_n = c->h_pinned[2];
+  h->nleaves += c->h_pinned[3];
+  map_rebuild(h, 1024);
+}
+
 static kh_trie* trie_new(kh_ctx* c, uint32_t flags, bool forest) {
   kh_trie* h = new kh_trie();
   h->c = c;
@@ -2675,6 +2913,45 @@ int kh_trie_open(kh_ctx* c, const uint8_t* d_keys, uint32_t klen, const uint8_t*
     }
     if (root32) memcpy(root32, h->root, 32);
     *out = h;
+  })
+}
+
+int kh_trie_open_nodes(kh_ctx* c, const uint8_t root32[32], const uint8_t* d_enc, const uint64_t* d_off, uint64_t n,
+                       uint32_t flags, uint8_t missing32[32], kh_trie** out) {
+  if (!c || !out || !root32) return set_err(KH_EINVAL, "null context, root or handle");
+  kh_trie* h = nullptr;
+  API_TRY({
+    HIPCHK(hipSetDevice(c->dev));
+    h = trie_new(c, flags, false);
+    try {
+      trie_open_nodes(h, root32, d_enc, d_off, n, missing32);
+    } catch (...) {
+      delete h;
+      h = nullptr;
+      throw;
+    }
+    *out = h;
+  })
+}
+
+int kh_trie_open_nodes_host(const uint8_t root32[32], const uint8_t* enc, const uint64_t* off, uint64_t n,
+                            uint32_t flags, uint8_t missing32[32], kh_trie** out) {
+  if (!out || !root32 || (n && (!enc || !off))) return set_err(KH_EINVAL, "null input");
+  API_TRY({
+    kh_ctx* c = shared_ctx(current_device());
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->dev));
+    const uint64_t o0 = n ? off[0] : 0, bytes = n ? off[n] - o0 : 0;
+    c->in_vals.ensure(bytes + 64);
+    c->in_voff.ensure((n + 1) * 8 + 64);
+    std::vector<uint64_t> rel(n + 1, 0);
+    for (uint64_t i = 0; i <= n && n; ++i) rel[i] = off[i] - o0;
+    if (bytes) HIPCHK(hipMemcpyAsync(c->in_vals.p, enc + o0, bytes, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(c->in_voff.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    int rc = kh_trie_open_nodes(c, root32, (const uint8_t*)c->in_vals.p, (const uint64_t*)c->in_voff.p, n, flags,
+                                missing32, out);
+    if (rc != KH_OK) return rc;
   })
 }
 

@@ -127,6 +127,32 @@ class ResidentTrie:
         self.h = h
         self.root = root.tobytes()
 
+    @classmethod
+    def from_nodes(cls, ctx, root, nodes, hash_keys=False, emit=True):
+        """Open from a root hash and a node store {hash: encoding} (kh_trie_open_nodes;
+        MerklePatriciaTrie.apply(rootHash, source)).  A missing node raises
+        MPTNodeMissingException with the missing hash in .missing."""
+        t = cls.__new__(cls)
+        t.ctx, t.dev, t.h = ctx, f"cuda:{ctx.device}", None
+        t.hash_keys = bool(hash_keys)
+        encs = list(nodes.values())
+        ed, eo = _pack_dev(encs, t.dev)
+        h = ctypes.c_void_p()
+        miss = np.zeros(32, np.uint8)
+        flags = (_lib.KH_HASH_KEYS if hash_keys else 0) | (_lib.KH_EMIT_NODES if emit else 0)
+        rb = np.frombuffer(bytes(root), np.uint8).copy()
+        ctx._sync()
+        rc = lib().kh_trie_open_nodes(ctx.h, rb.ctypes.data, _ptr(ed), _ptr(eo), len(encs), flags, miss.ctypes.data,
+                                      ctypes.byref(h))
+        if rc == _lib.KH_ENODE:
+            e = _lib.MPTNodeMissingException(rc, lib().kh_last_error().decode())
+            e.missing = miss.tobytes()
+            raise e
+        check(rc)
+        t.h = h
+        t.root = bytes(root)
+        return t
+
     def _flag(self, hash_keys):
         """The trie's key encoder is fixed at open (as the reference's implicit
         ByteArrayEncoder[K] is per trie type): None means that one; a different value raises."""

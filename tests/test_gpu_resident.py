@@ -183,3 +183,60 @@ def test_forest_vs_oracle(khst, oracle):
                 if h in want:
                     assert want[h] == e
     f.close()
+
+
+@pytest.mark.parametrize("sc", C.commit_scenarios()[:4], ids=lambda s: s[0])
+def test_open_from_node_store(khst, oracle, sc):
+    """kh_trie_open_nodes: a trie opened from its root hash and the
+    oracle's persisted node store (MerklePatriciaTrie.apply(rootHash, source),
+    MerklePatriciaTrie.scala:60-66,520-542) commits exactly like the oracle; a store
+    missing a reachable node raises MPTNodeMissingException with that node's hash."""
+    from khipu_amd.device import Ctx, ResidentTrie
+    from khipu_amd._lib import MPTNodeMissingException
+    name, ks, vs, batches = sc
+    o = oracle.Trie()
+    for k, v in zip(ks, vs):
+        o.put(k, v)
+    store = o.reachable() if ks else {}
+    root = o.root_hash()
+    t = ResidentTrie.from_nodes(Ctx(0), root, store)
+    assert t.root == root and len(t) == len(set(ks)), name
+    for i, (ups, dels) in enumerate(batches):
+        for k, v in ups:
+            o.put(k, v)
+        for k in dels:
+            o.remove(k)
+        assert t.commit(ups, dels) == o.root_hash(), (name, i)
+    t.close()
+    if len(store) > 2:
+        victim = sorted(store)[len(store) // 2]
+        partial = {h: e for h, e in store.items() if h != victim}
+        with pytest.raises(MPTNodeMissingException) as ei:
+            ResidentTrie.from_nodes(Ctx(0), root, partial)
+        assert ei.value.missing == victim
+
+
+def test_open_from_node_store_1m(khst):
+    """At 1M accounts: the node set a resident trie writes back at open, opened again from
+    the root alone, gives the same roots through the same commits."""
+    import torch
+    from khipu_amd.device import Ctx, ResidentTrie
+    ctx = Ctx(0)
+    n = 1_000_000
+    addr, vals, voff = ctx.synth_accounts(9, 0, n)
+    a = ResidentTrie.__new__(ResidentTrie)
+    a.ctx, a.dev, a.h = ctx, "cuda:0", None
+    a._open(addr, 20, vals, voff, n, True)
+    store = a.nodes()
+    b = ResidentTrie.from_nodes(ctx, a.root, store, hash_keys=True)
+    assert b.root == a.root and len(b) == n
+    r = random.Random(5)
+    for _ in range(3):
+        ups = [(bytes(r.getrandbits(8) for _ in range(20)), C.account_value(r)) for _ in range(2000)]
+        idx = r.sample(range(n), 500)
+        ah = addr[:20 * n].view(n, 20).cpu().numpy()
+        ups += [(ah[i].tobytes(), C.account_value(r)) for i in idx[:400]]
+        dels = [ah[i].tobytes() for i in idx[400:]]
+        assert a.commit(ups, dels) == b.commit(ups, dels)
+    a.close()
+    b.close()
