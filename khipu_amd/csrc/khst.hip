@@ -2849,11 +2849,13 @@ static void trie_open_nodes(kh_trie* h, const uint8_t* root32, const uint8_t* d_
     HIPCHK(hipStreamSynchronize(st));  // w is a host temporary
   }
   uint64_t ni = 1, nrec = 0;
+  const uint64_t rn0 = h->rn;
   for (int level = 0; ni && level < 80; ++level) {
-    recs_reserve(h, h->rn + nrec + ni + 16);
+    h->rn = rn0 + nrec;  // a regrow keeps the records of the earlier levels
+    recs_reserve(h, h->rn + ni + 16);
     OItems nxt = oitems_carve(level & 1 ? fa : fb, 16 * ni);
     HIPCHK(hipMemsetAsync(nxt.n, 0, 8, st));
-    hipLaunchKernelGGL(k_open_level, GRID(ni, BS), dim3(BS), 0, st, cur, ni, nxt, NS, recs_of(h), oc, h->rn,
+    hipLaunchKernelGGL(k_open_level, GRID(ni, BS), dim3(BS), 0, st, cur, ni, nxt, NS, recs_of(h), oc, rn0,
                        0u, (uint8_t*)h->heap.p, oc + 1, oc + 2, oc + 3, dmiss);
     LAUNCH_CHECK();
     HIPCHK(hipMemcpyAsync(c->h_pinned, nxt.n, 8, hipMemcpyDeviceToHost, st));
@@ -2872,7 +2874,7 @@ static void trie_open_nodes(kh_trie* h, const uint8_t* root32, const uint8_t* d_
     cur = nxt;
   }
   if (ni) throw KhError{KH_EINVAL, "node store deeper than a 32-byte key allows"};
-  h->rn += nrec;
+  h->rn = rn0 + nrec;
   h->heap_n = c->h_pinned[2];
   h->nleaves += c->h_pinned[3];
   map_rebuild(h, 1024);
