@@ -19,6 +19,8 @@
  *   kh_trie_root_nodes      rootHash + the write-back node set of MerklePatriciaTrie.changes/persist
  *                           (MerklePatriciaTrie.scala:491-516,544-554 -> NodeStorage.update,
  *                           khipu-eth/.../storage/NodeStorage.scala:16-19)
+ *   kh_trie_roots_varkeys   generic unhashed keys of any length <= 32 B, branch values
+ *   kh_list_roots           transactions / receipts roots (MptListValidator.scala:15-46)
  *   kh_trie_root_sharded    the same root computed from per-GPU top-nibble shards
  *
  * Semantics shared by every trie entry point:
@@ -95,6 +97,21 @@ int kh_trie_root(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const 
 int kh_trie_roots_segmented(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const uint64_t* voff,
                             const uint64_t* seg_off, uint64_t nseg, uint32_t flags, uint8_t* roots32,
                             kh_stats* stats);
+
+/* Tries over variable-length unhashed keys of 0..32 bytes (key i = keys[koff[i] ..
+ * koff[i+1])): a key that is a prefix of other keys is the value of the branch where it
+ * ends (the branch's 17th item, Node.scala:31-40).  nseg tries as in
+ * kh_trie_roots_segmented (koff / voff indexed like the inputs).  The generic key path
+ * of MerklePatriciaTrie.put with an identity key serializer (trie/package.scala:28-36). */
+int kh_trie_roots_varkeys(const uint8_t* keys, const uint64_t* koff, const uint8_t* vals, const uint64_t* voff,
+                          const uint64_t* seg_off, uint64_t nseg, uint8_t* roots32, kh_stats* stats);
+
+/* List tries (transactions / receipts / ommers roots): item i of trie s, i.e. input
+ * seg_off[s] + i, is put under key rlp(i) (MptListValidator.isValid,
+ * khipu-eth/.../validators/MptListValidator.scala:15-46; BlockGenerator.scala:157-163);
+ * items[off[j] .. off[j+1]) is the serialized item.  Keys are made on the device. */
+int kh_list_roots(const uint8_t* items, const uint64_t* off, const uint64_t* seg_off, uint64_t nseg,
+                  uint8_t* roots32, kh_stats* stats);
 
 /* Root plus every node a fresh node store needs: each node reachable from the root
  * whose encoding is >= 32 B, plus the root node (MerklePatriciaTrie.scala:505-511).

@@ -29,7 +29,7 @@ EXPORTS = (
     "kh_dev_partition", "kh_trie_open", "kh_trie_apply", "kh_trie_emit_nodes", "kh_trie_size", "kh_trie_free",
     "kh_verify_nodes", "kh_trie_open_host", "kh_trie_apply_host", "kh_forest_open", "kh_forest_apply",
     "kh_forest_apply_host", "kh_block_commit", "kh_forest_last_roots", "kh_trie_open_nodes",
-    "kh_trie_open_nodes_host",
+    "kh_trie_open_nodes_host", "kh_trie_roots_varkeys", "kh_list_roots",
 )
 
 
@@ -119,6 +119,8 @@ def lib():
     L.kh_trie_open_nodes_host.argtypes = [vp, vp, vp, u64, u32, vp, ctypes.POINTER(vp)]
     L.kh_block_commit.argtypes = [vp, vp, vp, vp, vp, vp, u64, vp, vp, u64, u32, vp, vp, vp, vp, u64, vp, u64, u32,
                                   vp, vp]
+    L.kh_trie_roots_varkeys.argtypes = [vp, vp, vp, vp, vp, u64, vp, vp]
+    L.kh_list_roots.argtypes = [vp, vp, vp, u64, vp, vp]
     for name in EXPORTS:
         fn = getattr(L, name)
         if fn.restype is ctypes.c_int or name not in ("kh_last_error", "kh_version"):

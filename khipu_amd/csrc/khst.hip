@@ -124,15 +124,17 @@ __global__ void __launch_bounds__(BS) k_make_ck(const uint64_t* K, const uint32_
 // (later put last) is kept.  flags |= 2 if equal keys exist (dedup needed),
 // |= 1 if a run exceeds TIE_RUN_MAX (take the full-sort path instead).
 constexpr uint32_t TIE_RUN_MAX = 64;
-__device__ __forceinline__ bool key_less(const uint64_t* a, const uint64_t* b) {
+// variable-length keys (zero padded, kn nibbles): a key sorts before the longer keys it
+// prefixes, i.e. (padded key, length) order
+__device__ __forceinline__ bool key_less(const uint64_t* a, const uint64_t* b, uint32_t kna = 0, uint32_t knb = 0) {
   for (int j = 0; j < 4; ++j) {
     uint64_t x = bswap64(a[j]), y = bswap64(b[j]);
     if (x != y) return x < y;
   }
-  return false;
+  return kna < knb;
 }
 __global__ void __launch_bounds__(BS) k_tie_fix(const uint64_t* ck, uint64_t n, uint64_t* skey, uint32_t* sidx,
-                                                uint32_t* sseg, unsigned long long* flags) {
+                                                uint32_t* sseg, const uint8_t* kn, unsigned long long* flags) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i + 1 >= n) return;
   uint32_t hi = (uint32_t)(ck[i] >> 32);
@@ -149,7 +151,8 @@ __global__ void __launch_bounds__(BS) k_tie_fix(const uint64_t* ck, uint64_t n, 
     uint32_t ix = sidx[a];
     uint32_t sg = sseg ? sseg[a] : 0;
     uint64_t b = a;
-    while (b > i && key_less(k, skey + 4 * (b - 1))) {
+    const uint32_t kk = kn ? kn[ix] : 0;
+    while (b > i && key_less(k, skey + 4 * (b - 1), kk, kn ? kn[sidx[b - 1]] : 0)) {
       for (int j = 0; j < 4; ++j) skey[4 * b + j] = skey[4 * (b - 1) + j];
       sidx[b] = sidx[b - 1];
       if (sseg) sseg[b] = sseg[b - 1];
@@ -163,7 +166,7 @@ __global__ void __launch_bounds__(BS) k_tie_fix(const uint64_t* ck, uint64_t n, 
   for (uint64_t a = i + 1; a < e; ++a) {
     const uint64_t* x = skey + 4 * (a - 1);
     const uint64_t* y = skey + 4 * a;
-    dup |= x[0] == y[0] && x[1] == y[1] && x[2] == y[2] && x[3] == y[3];
+    dup |= x[0] == y[0] && x[1] == y[1] && x[2] == y[2] && x[3] == y[3] && (!kn || kn[sidx[a - 1]] == kn[sidx[a]]);
   }
   if (dup) atomicOr(flags, 2ULL);
 }
@@ -193,6 +196,16 @@ __global__ void __launch_bounds__(BS) k_word_key(const uint64_t* K, const uint32
   ck[i] = bswap64(K[4 * (uint64_t)idx[i] + word]);
 }
 
+__global__ void __launch_bounds__(BS) k_kn_key(const uint8_t* kn, const uint32_t* idx, uint64_t n, uint64_t* ck) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  ck[i] = kn[idx[i]];
+}
+__global__ void __launch_bounds__(BS) k_kn_gather(const uint8_t* kn, const uint32_t* idx, uint64_t n, uint8_t* out) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < n) out[i] = kn[idx[i]];
+}
+
 __global__ void __launch_bounds__(BS) k_seg_key(const uint32_t* seg, const uint32_t* idx, uint64_t n, uint64_t* ck) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
@@ -200,7 +213,8 @@ __global__ void __launch_bounds__(BS) k_seg_key(const uint32_t* seg, const uint3
 }
 
 // keep the LAST of equal keys (later puts win, TrieAccounts.scala:23-27)
-__global__ void __launch_bounds__(BS) k_dup(const uint64_t* skey, const uint32_t* sseg, uint64_t n, uint32_t* keep) {
+__global__ void __launch_bounds__(BS) k_dup(const uint64_t* skey, const uint32_t* sseg, const uint32_t* sidx,
+                                            const uint8_t* kn, uint64_t n, uint32_t* keep) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
   uint32_t k = 1;
@@ -209,6 +223,7 @@ __global__ void __launch_bounds__(BS) k_dup(const uint64_t* skey, const uint32_t
     const uint64_t* b = a + 4;
     bool eq = a[0] == b[0] && a[1] == b[1] && a[2] == b[2] && a[3] == b[3];
     if (sseg && sseg[i] != sseg[i + 1]) eq = false;
+    if (kn && kn[sidx[i]] != kn[sidx[i + 1]]) eq = false;
     k = eq ? 0 : 1;
   }
   keep[i] = k;
@@ -956,7 +971,7 @@ struct kh_ctx {
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // leaf hashing, concurrent with the branch topology
   std::mutex mu;
-  DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, out_emit, emit_dev;
+  DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, in_kn, in_aux, out_emit, emit_dev;
   hipEvent_t ev[11] = {};  // [8] boundaries ready (st), [9] / [10] leaf kernel start / end (st2)
   unsigned long long* h_pinned = nullptr;  // small pinned staging for syncs
   // last build (for emission)
@@ -980,6 +995,7 @@ struct BuildArgs {
   uint32_t flags;
   bool emit;
   const uint32_t* vlen = nullptr;  // per-input value lengths (element builds: spans in a value heap)
+  const uint8_t* kn = nullptr;     // variable-length keys (zero-padded to 32 B): nibble counts (list tries)
   struct ElemArgs* el = nullptr;   // element build of a resident forest commit (forest.h; nullable)
 };
 // element build (forest.h): inputs are leaves and subtree elements; the capped reference
@@ -1026,6 +1042,7 @@ struct SortIO {
   void* rs_scratch;
   void* scan_scratch;
   unsigned long long* ctr;
+  const uint8_t* kn;  // variable-length keys: nibble counts (input order; nullable)
   // out
   uint64_t m;
   uint32_t* sidx;
@@ -1059,7 +1076,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
   hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, (const uint32_t*)idxs, n,
                      skey, sseg);
   LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_tie_fix, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, n, skey, idxs, sseg,
+  hipLaunchKernelGGL(k_tie_fix, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, n, skey, idxs, sseg, S.kn,
                      T.ctr + CTR_TIE);
   LAUNCH_CHECK();
   HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
@@ -1080,6 +1097,8 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
       if (word >= 0)
         hipLaunchKernelGGL(k_word_key, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, (const uint32_t*)ia, word,
                            n, ka);
+      else if (word == -2)
+        hipLaunchKernelGGL(k_kn_key, GRID(n, BS), dim3(BS), 0, st, S.kn, (const uint32_t*)ia, n, ka);
       else
         hipLaunchKernelGGL(k_seg_key, GRID(n, BS), dim3(BS), 0, st, seg, (const uint32_t*)ia, n, ka);
       LAUNCH_CHECK();
@@ -1088,6 +1107,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
         std::swap(ia, ib);
       }
     };
+    if (S.kn) pass(-2, 8);  // least significant: the length
     for (int w = 3; w >= 0; --w) pass(w, 64);
     if (segmented) pass(-1, ((sb + 7) / 8) * 8);
     hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, (const uint32_t*)ia, n,
@@ -1099,7 +1119,8 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
     // keep the LAST of equal keys (later puts win): flags, scan, compaction
     uint32_t* keep = (uint32_t*)(sidx == idx0 ? ck1 : ck0);  // n*8 free bytes
     uint32_t* keep_pos = sidx == idx0 ? idx1 : idx0;
-    hipLaunchKernelGGL(k_dup, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)skey, (const uint32_t*)sseg, n, keep);
+    hipLaunchKernelGGL(k_dup, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)skey, (const uint32_t*)sseg,
+                       (const uint32_t*)sidx, S.kn, n, keep);
     LAUNCH_CHECK();
     uint32_t* mtot = (uint32_t*)(T.ctr + CTR_M);
     scan_exclusive<uint32_t>(keep, keep_pos, n, mtot, scan_scratch, st);
@@ -1143,7 +1164,9 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // plain root builds hash their leaves on c->st2 while c->st computes the branch
   // topology (trie_ops.h "early leaves"); write-back and incremental builds keep
   // the leaf stage after the topology (they need the parents / dirty marks first)
-  const bool early = !A.emit && !A.el;
+  const bool early = !A.emit && !A.el && !A.kn;
+  if (A.kn && (A.emit || A.el || (A.flags & KH_HASH_KEYS)))
+    throw KhError{KH_EINVAL, "variable-length keys: root-only builds of unhashed keys"};
 
   O.res_hash.assign(nres * 4, 0);
   O.res_len.assign(nres, 0);
@@ -1171,6 +1194,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       nres * 32, nres * 4, nres * 32,         // results
       CTR_N * 8, 64 * 4, 80 * 4, 512 * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
       early ? n * 32 : 0, early ? n : 0,      // early leaves: stashed references, meta
+      A.kn ? n : 0,                           // sorted key lengths
       nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1, nb1,  // branch tables in key-order ids (BrTab J)
   };
   c->ws1.ensure(carve_size(sz));
@@ -1224,6 +1248,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint32_t* order = cv.take<uint32_t>(nb1);
   T.lf_eref = early ? cv.take<uint64_t>(n * 4) : nullptr;
   T.lf_emeta = early ? cv.take<uint8_t>(n) : nullptr;
+  uint8_t* skn = A.kn ? cv.take<uint8_t>(n) : nullptr;
   BrTab J{};
   J.k = cv.take<uint32_t>(nb1);
   J.parent = cv.take<uint32_t>(nb1);
@@ -1259,7 +1284,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint32_t* sidx = nullptr;
   bool fallback = false;
   {
-    SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr};
+    SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr,
+             A.kn};
     sort_dedup(c, S);
     m = S.m;
     sidx = S.sidx;
@@ -1274,6 +1300,11 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.sseg = sseg;
   hipLaunchKernelGGL(k_val_gather, GRID(m, BS), dim3(BS), 0, st, T);
   LAUNCH_CHECK();
+  if (A.kn) {
+    hipLaunchKernelGGL(k_kn_gather, GRID(m, BS), dim3(BS), 0, st, A.kn, (const uint32_t*)sidx, m, skn);
+    LAUNCH_CHECK();
+    T.kn = skn;
+  }
   if (A.el) {  // element build: the element properties in sorted order (the leaf topology reads them)
     ElemArgs& E = *A.el;
     E.out->ensure(carve_size({m, m * 32, m, m, m * 32, m, m * 32, m * 4}));
@@ -1391,14 +1422,16 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   if (nb == 0) std::fill(lbh.begin(), lbh.end(), 0u);
 
   // ---- phase-2 workspace: child records + node arena
-  // leaf encodings are kept (transposed message slots) only when the node set is emitted
-  const uint64_t lmsg_words = A.emit ? (uint64_t)LEAF_WORDS * m : 0;
+  // leaf encodings are kept (transposed message slots) for the write-back, element and
+  // variable-key builds (the plain root build hashed its leaves in LDS)
+  const bool lmsgs = A.emit || A.kn;
+  const uint64_t lmsg_words = lmsgs ? (uint64_t)LEAF_WORDS * m : 0;
   const uint64_t bmsg_words = A.emit ? (uint64_t)BR_WORDS * B : 0, xmsg_words = A.emit ? (uint64_t)EXT_WORDS * B : 0;
   c->ws2.ensure(carve_size({C * 32, C * 2, lmsg_words * 8, lf_bytes + 64, bmsg_words * 8, xmsg_words * 8}));
   Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
   T.cref = cv2.take<uint64_t>(C * 4);
   T.cmeta = cv2.take<uint16_t>(C);
-  T.lmsg = A.emit ? cv2.take<uint64_t>(lmsg_words) : nullptr;
+  T.lmsg = lmsgs ? cv2.take<uint64_t>(lmsg_words) : nullptr;
   T.lstride = m;
   T.arena = cv2.take<uint8_t>(lf_bytes + 64);  // long leaves
   T.bmsg = A.emit ? cv2.take<uint64_t>(bmsg_words) : nullptr;
@@ -1438,7 +1471,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // N1 variant: one thread per branch assembling its own window (default) or the
   // wave-cooperative DPP assembly (KHST_BRANCH=coop; DESIGN.md §5 has the measurement)
   const char* bv = getenv("KHST_BRANCH");
-  const bool coop = bv && strcmp(bv, "coop") == 0;
+  const bool coop = bv && strcmp(bv, "coop") == 0 && !A.kn;  // (the coop assembly has no branch values)
   for (int d = 63; d >= 0; --d) {
     uint32_t cnt = lbh[d + 1] - lbh[d];
     if (!cnt) continue;
@@ -1554,7 +1587,7 @@ static Staged stage_inputs(kh_ctx* c, const uint8_t* keys, uint32_t klen, const 
   std::vector<uint64_t> rel(voff, voff + n + 1);
   for (auto& x : rel) x -= v0;
   hipStream_t st = c->st;
-  if (n) HIPCHK(hipMemcpyAsync(c->in_keys.p, keys, n * klen, hipMemcpyHostToDevice, st));
+  if (n && klen) HIPCHK(hipMemcpyAsync(c->in_keys.p, keys, n * klen, hipMemcpyHostToDevice, st));
   if (vbytes) HIPCHK(hipMemcpyAsync(c->in_vals.p, vals + v0, vbytes, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(c->in_voff.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
   const uint32_t* dseg = nullptr;
@@ -1565,6 +1598,45 @@ static Staged stage_inputs(kh_ctx* c, const uint8_t* keys, uint32_t klen, const 
   }
   HIPCHK(hipStreamSynchronize(st));  // `rel` and `seg` are host temporaries
   return Staged{(const uint8_t*)c->in_keys.p, (const uint8_t*)c->in_vals.p, (const uint64_t*)c->in_voff.p, dseg};
+}
+
+// list-trie keys: key of item i of its trie = RLP of the integer index
+// (MptListValidator.scala:15-46, BlockGenerator.scala:157-163; RLP.scala integer
+// encoding: 0 -> 0x80, 1..127 -> the byte, else 0x80 + n and n big-endian bytes),
+// zero-padded to 32 bytes, with its length in nibbles
+__global__ void __launch_bounds__(BS) k_list_keys(const uint32_t* seg, const uint64_t* seg_off, uint64_t n,
+                                                  uint64_t* K32, uint8_t* kn) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t idx = i - (seg_off[seg[i]] - seg_off[0]);
+  uint64_t w = 0;
+  uint32_t nb;
+  if (idx == 0) {
+    w = 0x80;
+    nb = 1;
+  } else if (idx < 0x80) {
+    w = idx;
+    nb = 1;
+  } else {
+    uint32_t L = 0;
+    for (uint64_t x = idx; x; x >>= 8) ++L;
+    w = 0x80 + L;
+    for (uint32_t b = 0; b < L; ++b) w |= ((idx >> (8 * (L - 1 - b))) & 0xFF) << (8 * (b + 1));
+    nb = L + 1;
+  }
+  K32[4 * i] = w;
+  K32[4 * i + 1] = K32[4 * i + 2] = K32[4 * i + 3] = 0;
+  kn[i] = (uint8_t)(2 * nb);
+}
+
+static std::vector<uint32_t> seg_ids(const uint64_t* seg_off, uint64_t nseg) {
+  const uint64_t n = seg_off[nseg] - seg_off[0];
+  std::vector<uint32_t> seg(n);
+  for (uint64_t s = 0; s < nseg; ++s) {
+    if (seg_off[s + 1] < seg_off[s]) throw KhError{KH_EINVAL, "seg_off not monotone"};
+    for (uint64_t i = seg_off[s]; i < seg_off[s + 1]; ++i) seg[i - seg_off[0]] = (uint32_t)s;
+  }
+  return seg;
 }
 
 static const uint8_t EMPTY_TRIE_HASH[32] = {0x56, 0xe8, 0x1f, 0x17, 0x1b, 0xcc, 0x55, 0xa6, 0xff, 0x83, 0x45,
@@ -2392,7 +2464,7 @@ int kh_ctx_destroy(kh_ctx* c) {
   API_TRY({
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->st);
-    for (DevBuf* b : {&c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->out_emit,
+    for (DevBuf* b : {&c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->in_kn, &c->in_aux, &c->out_emit,
                       &c->emit_dev})
       b->release();
     for (auto& e : c->ev)
@@ -2485,6 +2557,73 @@ int kh_trie_roots_segmented(const uint8_t* keys, uint32_t klen, const uint8_t* v
     const uint64_t* vo = voff + seg_off[0];
     Staged S = stage_inputs(c, keys + seg_off[0] * klen, klen, vals, vo, n, &seg);
     BuildArgs A{S.keys, klen, S.vals, S.voff, n, S.seg, nseg, 0, flags, false};
+    BuildOut O;
+    run_build(c, A, O, stats);
+    for (uint64_t s = 0; s < nseg; ++s) copy_root(O, s, roots32 + 32 * s);
+  })
+}
+
+// Variable-length keys (list tries and any unhashed keys of <= 32 bytes): the keys are
+// zero-padded on the host to 32 bytes and carry their nibble counts; a key that is a
+// prefix of others is the value of the branch at its end (the 17th slot)
+int kh_trie_roots_varkeys(const uint8_t* keys, const uint64_t* koff, const uint8_t* vals, const uint64_t* voff,
+                          const uint64_t* seg_off, uint64_t nseg, uint8_t* roots32, kh_stats* stats) {
+  API_TRY({
+    if (nseg == 0) return KH_OK;
+    std::vector<uint32_t> seg = seg_ids(seg_off, nseg);
+    const uint64_t n = seg.size(), i0 = seg_off[0];
+    if (stats) memset(stats, 0, sizeof(*stats));
+    if (n == 0) {
+      for (uint64_t s = 0; s < nseg; ++s) memcpy(roots32 + 32 * s, EMPTY_TRIE_HASH, 32);
+      return KH_OK;
+    }
+    std::vector<uint8_t> pk(n * 32, 0), kn(n);
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint64_t a = koff[i0 + i], b = koff[i0 + i + 1];
+      if (b < a || b - a > 32) throw KhError{KH_EINVAL, "variable-length keys must be 0..32 bytes"};
+      memcpy(&pk[32 * i], keys + a, b - a);
+      kn[i] = (uint8_t)(2 * (b - a));
+    }
+    kh_ctx* c = shared_ctx(current_device());
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->dev));
+    c->in_kn.ensure(n + 64);
+    HIPCHK(hipMemcpyAsync(c->in_kn.p, kn.data(), n, hipMemcpyHostToDevice, c->st));
+    Staged S = stage_inputs(c, pk.data(), 32, vals, voff + i0, n, nseg > 1 ? &seg : nullptr);
+    BuildArgs A{S.keys, 32, S.vals, S.voff, n, S.seg, nseg, 0, 0, false};
+    A.kn = (const uint8_t*)c->in_kn.p;
+    BuildOut O;
+    run_build(c, A, O, stats);
+    for (uint64_t s = 0; s < nseg; ++s) copy_root(O, s, roots32 + 32 * s);
+  })
+}
+
+// List tries (transactions / receipts roots): item i of trie s is keyed by rlp(i), the
+// keys generated on the device
+int kh_list_roots(const uint8_t* items, const uint64_t* off, const uint64_t* seg_off, uint64_t nseg, uint8_t* roots32,
+                  kh_stats* stats) {
+  API_TRY({
+    if (nseg == 0) return KH_OK;
+    std::vector<uint32_t> seg = seg_ids(seg_off, nseg);
+    const uint64_t n = seg.size(), i0 = seg_off[0];
+    if (stats) memset(stats, 0, sizeof(*stats));
+    if (n == 0) {
+      for (uint64_t s = 0; s < nseg; ++s) memcpy(roots32 + 32 * s, EMPTY_TRIE_HASH, 32);
+      return KH_OK;
+    }
+    kh_ctx* c = shared_ctx(current_device());
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(hipSetDevice(c->dev));
+    c->in_aux.ensure((nseg + 1) * 8 + 64);
+    HIPCHK(hipMemcpyAsync(c->in_aux.p, seg_off, (nseg + 1) * 8, hipMemcpyHostToDevice, c->st));
+    c->in_kn.ensure(n + 64);
+    Staged S = stage_inputs(c, nullptr, 0, items, off + i0, n, &seg);  // keys made below
+    c->in_keys.ensure(n * 32 + 64);
+    hipLaunchKernelGGL(k_list_keys, GRID(n, BS), dim3(BS), 0, c->st, S.seg, (const uint64_t*)c->in_aux.p, n,
+                       (uint64_t*)c->in_keys.p, (uint8_t*)c->in_kn.p);
+    LAUNCH_CHECK();
+    BuildArgs A{(const uint8_t*)c->in_keys.p, 32, S.vals, S.voff, n, nseg > 1 ? S.seg : nullptr, nseg, 0, 0, false};
+    A.kn = (const uint8_t*)c->in_kn.p;
     BuildOut O;
     run_build(c, A, O, stats);
     for (uint64_t s = 0; s < nseg; ++s) copy_root(O, s, roots32 + 32 * s);

@@ -115,10 +115,11 @@ struct BW {
       for (int i = (int)nb - 1; i >= 0; --i) put1((uint32_t)(len >> (8 * i)) & 0xFF);
     }
   }
-  // copy key bytes [from, 32)
-  KH_HD void key_suffix(const Key4& k, uint32_t from) {
-    while (from < 32) {
+  // copy key bytes [from, to)
+  KH_HD void key_suffix(const Key4& k, uint32_t from, uint32_t to = 32) {
+    while (from < to) {
       uint32_t nb = 8 - (from & 7);
+      if (nb > to - from) nb = to - from;
       put(key_word(k, from >> 3) >> (8 * (from & 7)), nb);
       from += nb;
     }
@@ -152,6 +153,7 @@ struct Topo {
   const uint64_t* skey;   // [m*4] sorted keys
   const uint32_t* sidx;   // [m] input index of sorted key i
   const uint32_t* sseg;   // [m] segment id (segmented only)
+  const uint8_t* kn;      // [m] key length in nibbles (variable-length key builds; nullable: 64)
   const uint8_t* vals;    // input values
   const uint64_t* voff;   // [n+1] (or [n] offsets with vlen_in)
   const uint32_t* vlen_in; // [n] value lengths (nullable: voff[i+1] - voff[i])
@@ -259,6 +261,15 @@ KH_HD uint32_t result_index(const Topo& T, uint64_t first_key) {
   return 0;
 }
 
+// ---- variable-length keys (list tries): key i has kn[i] nibbles; a key
+// that is a prefix of the next ones is the VALUE of the branch at its own depth (the
+// 17th slot, Node.scala:31-40), published to the parent as a value marker
+constexpr uint16_t VAL_META = 0xFFFF;
+KH_HD uint32_t key_nibs(const Topo& T, uint64_t i) { return T.kn ? T.kn[i] : 64; }
+KH_HD bool is_branch_value(const Topo& T, uint64_t i) {
+  return T.kn && T.lf_parent[i] != NONE && (int32_t)T.kn[i] == T.lf_pd[i];
+}
+
 // ---- element builds: subtree elements
 constexpr uint8_t EL_LEAF = 0xFF, EL_NEW = 0xFF;
 KH_HD bool el_subtree(const Topo& T, uint64_t i) { return T.el_db && T.el_db[i] != EL_LEAF; }
@@ -285,6 +296,10 @@ KH_HD uint32_t ext_enc_len(uint32_t e, uint32_t brl) {
 KH_HD void op_lcp(const Topo& T, uint64_t b) {
   Key4 a = load_key(T.skey, b), c = load_key(T.skey, b + 1);
   int l = lcp_nibbles(a, c);
+  if (T.kn) {  // padded keys: the common prefix ends with the shorter key
+    if (l > (int)T.kn[b]) l = T.kn[b];
+    if (l > (int)T.kn[b + 1]) l = T.kn[b + 1];
+  }
   uint8_t v = (uint8_t)(l + 1);
   if (l < (int)T.depth0 || l > 63) v = 0;  // 64 cannot occur after dedup
   if (T.segmented && T.sseg[b] != T.sseg[b + 1]) v = 0;
@@ -487,9 +502,9 @@ KH_HD void op_val_gather(const Topo& T, uint64_t i) {
   T.svlen[i] = T.vlen_in ? T.vlen_in[src] : (uint32_t)(T.voff[src + 1] - o);
 }
 
-// encoded leaf length for path start nibble s
-KH_HD uint64_t leaf_enc_len(uint32_t s, uint64_t vlen, uint32_t v0) {
-  uint32_t p = 64 - s;
+// encoded leaf length for path start nibble s (a key of kn nibbles)
+KH_HD uint64_t leaf_enc_len(uint32_t s, uint64_t vlen, uint32_t v0, uint32_t kn = 64) {
+  uint32_t p = kn - s;
   uint32_t h = p / 2 + 1;                   // HP bytes; first byte 0x2_/0x3_ < 0x80
   uint64_t hp = h == 1 ? 1 : 1 + h;         // h <= 33 < 56
   uint64_t payload = hp + rlp_str_len(vlen, v0);
@@ -516,11 +531,16 @@ KH_HD void op_leaf_topo(const Topo& T, uint64_t i, AllocFn alloc) {
     T.lf_len[i] = e ? ext_enc_len(e, T.el_brl[i]) : T.el_brl[i];
     return;
   }
+  if (is_branch_value(T, i)) {  // no node: the parent branch holds the value
+    T.lf_aoff[i] = 0;
+    T.lf_len[i] = 0;
+    return;
+  }
   const uint8_t* vp;
   uint64_t vlen;
   leaf_value(T, i, &vp, &vlen);
   uint32_t v0 = vlen == 1 ? (uint32_t)*vp : 0;  // the first byte matters only for a 1-byte value
-  uint64_t L = leaf_enc_len((uint32_t)(P.pd + 1), vlen, v0);
+  uint64_t L = leaf_enc_len((uint32_t)(P.pd + 1), vlen, v0, key_nibs(T, i));
   T.lf_aoff[i] = L > LEAF_SHORT_MAX ? alloc((L + 7) & ~(uint64_t)7) : 0;
 }
 
@@ -600,11 +620,13 @@ struct LeafGeom {
   uint64_t payload;  // list payload length
   uint32_t L;        // encoding length
   uint32_t v0;       // the value's first byte (only read for a 1-byte value)
+  uint32_t kb;       // key bytes (32; fewer for variable-length keys)
 };
-KH_HD LeafGeom leaf_geom(const Key4& k, int32_t pd, uint64_t vlen, uint32_t v0) {
+KH_HD LeafGeom leaf_geom(const Key4& k, int32_t pd, uint64_t vlen, uint32_t v0, uint32_t kn = 64) {
   LeafGeom g;
   g.s = (uint32_t)(pd + 1);
-  uint32_t p = 64 - g.s;
+  g.kb = kn / 2;
+  uint32_t p = kn - g.s;
   g.h = p / 2 + 1;
   g.hp0 = (p & 1) ? (0x30u | key_nibble(k, (int)g.s)) : 0x20u;
   uint64_t hpl = g.h == 1 ? 1 : 1 + g.h;
@@ -617,7 +639,7 @@ KH_HD void leaf_header(BW& w, const Key4& k, const LeafGeom& g, uint64_t vlen) {
   w.len_prefix(g.payload, 0xC0);
   if (g.h > 1) w.put1(0x80 + g.h);
   w.put1(g.hp0);
-  w.key_suffix(k, (g.s + 1) / 2);
+  w.key_suffix(k, (g.s + 1) / 2, g.kb);
   if (!(vlen == 1 && g.v0 < 0x80)) w.len_prefix(vlen, 0x80);
 }
 
@@ -645,8 +667,9 @@ KH_HD void op_leaf_prep(const Topo& T, uint64_t i, const uint8_t* vp, uint64_t v
     x.flush();
     return;
   }
+  if (is_branch_value(T, i)) return;
   uint32_t v0 = vlen == 1 ? (uint32_t)*vp : 0;  // the first byte matters only for a 1-byte value
-  LeafGeom g = leaf_geom(k, T.lf_pd[i], vlen, v0);
+  LeafGeom g = leaf_geom(k, T.lf_pd[i], vlen, v0, key_nibs(T, i));
   BW w = g.L <= LEAF_SHORT_MAX ? BW(T.lmsg + i, T.lstride) : BW((uint64_t*)(T.arena + T.lf_aoff[i]), 1);
   leaf_header(w, k, g, vlen);
   w.bytes(vp, vlen);
@@ -730,6 +753,14 @@ KH_HD uint32_t leaf_hash_at(const Topo& T, uint64_t i, const uint64_t* w, uint64
 
 KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
   *inl = 0;
+  if (is_branch_value(T, i)) {  // the value's place in the parent's child records
+    const uint64_t slot = (uint64_t)T.br_cbase[T.lf_parent[i]] + T.lf_pord[i];
+    T.cref[4 * slot] = T.svoff[i];
+    T.cref[4 * slot + 1] = T.svlen[i];
+    T.cref[4 * slot + 2] = T.cref[4 * slot + 3] = 0;
+    T.cmeta[slot] = VAL_META;
+    return 0;
+  }
   uint32_t L = T.lf_len[i];
   const uint32_t a = (uint32_t)(T.lf_pd[i] + 1);
   const bool cached = el_cached(T, i, a);
@@ -823,9 +854,16 @@ KH_HD uint32_t op_leaf_long(const Topo& T, uint64_t i, uint32_t* inl) {
 // slot; WinBW: one 136-byte Keccak block of it)
 KH_HD uint32_t branch_payload(const Topo& T, uint32_t j) {
   uint32_t k = T.br_k[j];
-  const uint16_t* cm = T.cmeta + T.br_cbase[j];
-  uint32_t payload = 1 + (16 - k);  // terminator "" + empty slots
-  for (uint32_t c = 0; c < k; ++c) {
+  const uint64_t cb = T.br_cbase[j];
+  const uint16_t* cm = T.cmeta + cb;
+  uint32_t c0 = 0, term = 1;  // terminator "" (a secure trie never stores a value in a branch)
+  if (k && cm[0] == VAL_META) {  // variable-length keys: a key ending here is the 17th item
+    const uint64_t vo = T.cref[4 * cb], vl = T.cref[4 * cb + 1];
+    term = (uint32_t)rlp_str_len(vl, vl == 1 ? T.vals[vo] : 0);
+    c0 = 1;
+  }
+  uint32_t payload = term + (16 - (k - c0));  // + empty slots
+  for (uint32_t c = c0; c < k; ++c) {
     uint32_t len = cm[c] & 0xFF;
     payload += (len == 32) ? 33 : len;
   }
@@ -838,8 +876,9 @@ KH_HD void branch_stream(const Topo& T, uint32_t j, W& w, uint32_t payload) {
   const uint16_t* cm = T.cmeta + cb;
   w.len_prefix(payload, 0xC0);
   const uint64_t* cr = T.cref + 4 * cb;
+  const uint32_t c0 = (k && cm[0] == VAL_META) ? 1 : 0;
   int32_t prev = -1;
-  for (uint32_t c = 0; c < k; ++c) {
+  for (uint32_t c = c0; c < k; ++c) {
     uint32_t mc = cm[c];
     int32_t nib = (int32_t)(mc >> 8);
     for (int32_t e = prev + 1; e < nib; ++e) w.put1(0x80);  // empty slots
@@ -848,7 +887,14 @@ KH_HD void branch_stream(const Topo& T, uint32_t j, W& w, uint32_t payload) {
     bw_ref(w, r, mc & 0xFF);
   }
   for (int32_t e = prev + 1; e < 16; ++e) w.put1(0x80);
-  w.put1(0x80);  // terminator (a secure trie never stores a value in a branch)
+  if (c0) {  // the value as an RLP string (RLP.scala:141-150)
+    const uint64_t vo = cr[0], vl = cr[1];
+    const uint8_t* vp = T.vals + vo;
+    if (!(vl == 1 && vp[0] < 0x80)) w.len_prefix(vl, 0x80);
+    for (uint64_t q = 0; q < vl; ++q) w.put1(vp[q]);
+  } else {
+    w.put1(0x80);  // terminator (a secure trie never stores a value in a branch)
+  }
 }
 
 // ---- branch prep: the whole encoding into its message slot (thread per branch of one

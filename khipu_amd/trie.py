@@ -11,6 +11,9 @@ and node encoding is computed by the HIP kernels of libkhst.so:
 * ``trie_root`` / ``trie_roots``  — the batch commit that TrieAccounts.flush /
   TrieStorage.flush perform (ledger/TrieAccounts.scala:22-28,
   ledger/TrieStorage.scala:52-60) as one device call.
+* ``trie_roots_varkeys`` — tries over unhashed keys of any length <= 32 B (branch values).
+* ``list_roots`` / ``MptListValidator`` — transactions / receipts roots over rlp(i) keys
+  (validators/MptListValidator.scala:15-46, mining/BlockGenerator.scala:157-163).
 
 The mirror keeps the trie's leaf set (key -> value bytes) on the host and
 rebuilds the root on the device when it is asked for; the resulting root and
@@ -114,6 +117,52 @@ def trie_roots(tries, hash_keys=False, stats=None):
     return [out[32 * i:32 * i + 32].tobytes() for i in range(nseg)]
 
 
+def trie_roots_varkeys(tries, stats=None):
+    """Roots of tries over variable-length unhashed keys (0..32 bytes each; a key that
+    prefixes others is a branch value).  tries: list of (keys, vals)."""
+    keys, vals, seg_off = [], [], [0]
+    for ks, vs in tries:
+        if len(ks) != len(vs):
+            raise MPTException(_lib.KH_EINVAL, "keys/values length mismatch")
+        keys += [bytes(k) for k in ks]
+        vals += list(vs)
+        seg_off.append(len(keys))
+    kb, koff = _pack(keys)
+    vb, off = _pack(vals)
+    so = np.asarray(seg_off, dtype=np.uint64)
+    nseg = len(tries)
+    out = np.zeros(32 * max(nseg, 1), dtype=np.uint8)
+    st = stats if stats is not None else KhStats()
+    check(lib().kh_trie_roots_varkeys(kb.ctypes.data, koff.ctypes.data, vb.ctypes.data, off.ctypes.data,
+                                      so.ctypes.data, nseg, out.ctypes.data, ctypes.byref(st)))
+    return [out[32 * i:32 * i + 32].tobytes() for i in range(nseg)]
+
+
+def list_roots(lists, stats=None):
+    """Roots of list tries: list j's item i is put under rlp(i) (keys made on the device).
+    lists: list of lists of serialized items."""
+    items, seg_off = [], [0]
+    for it in lists:
+        items += list(it)
+        seg_off.append(len(items))
+    ib, off = _pack(items)
+    so = np.asarray(seg_off, dtype=np.uint64)
+    nseg = len(lists)
+    out = np.zeros(32 * max(nseg, 1), dtype=np.uint8)
+    st = stats if stats is not None else KhStats()
+    check(lib().kh_list_roots(ib.ctypes.data, off.ctypes.data, so.ctypes.data, nseg, out.ctypes.data,
+                              ctypes.byref(st)))
+    return [out[32 * i:32 * i + 32].tobytes() for i in range(nseg)]
+
+
+class MptListValidator:
+    """validators/MptListValidator.scala:15-46: a block body's list matches its header root."""
+
+    @staticmethod
+    def is_valid(hash_, to_validate):
+        return list_roots([list(to_validate)])[0] == bytes(hash_)
+
+
 def trie_root_nodes(keys, vals, hash_keys=False, stats=None):
     """(root, {hash: encoding}) — the root plus every node a fresh node store needs."""
     klen = 32 if not keys else len(keys[0])
@@ -189,7 +238,11 @@ class MerklePatriciaTrie:
                 self._root = EMPTY_TRIE_HASH
             else:
                 ks = list(self._leaves.keys())
-                self._root = trie_root(ks, [self._leaves[k] for k in ks])
+                vs = [self._leaves[k] for k in ks]
+                if all(len(k) == 32 for k in ks):
+                    self._root = trie_root(ks, vs)
+                else:  # unhashed keys of other lengths (branch values possible)
+                    self._root = trie_roots_varkeys([(ks, vs)])[0]
         return self._root
 
     def changes(self):
