@@ -113,6 +113,17 @@ int kh_trie_roots_varkeys(const uint8_t* keys, const uint64_t* koff, const uint8
 int kh_list_roots(const uint8_t* items, const uint64_t* off, const uint64_t* seg_off, uint64_t nseg,
                   uint8_t* roots32, kh_stats* stats);
 
+/* The kh_trie_root result computed on ngpus GPUs of this process: the
+ * puts are split into ngpus contiguous slices, slice g staged to devices[g], keys hashed
+ * there, records routed to the owner of their top key nibble (q * ngpus >> 4) over RCCL
+ * point-to-point (xGMI), every owner builds its subtries from nibble 1, and the 16
+ * references are folded into the root branch.  Devices must be distinct for the RCCL
+ * exchange; a list that repeats a device runs several shards on it (device copies).
+ * stats: sums over the shards; t_keys_ms / t_sort_ms / t_total_ms are the host wall
+ * times of stage+hash+partition / exchange / the whole call.  Host buffers. */
+int kh_trie_root_sharded(const int* devices, int ngpus, const uint8_t* keys, uint32_t klen, const uint8_t* vals,
+                         const uint64_t* voff, uint64_t n, uint32_t flags, uint8_t root32[32], kh_stats* stats);
+
 /* Root plus every node a fresh node store needs: each node reachable from the root
  * whose encoding is >= 32 B, plus the root node (MerklePatriciaTrie.scala:505-511).
  * Node j: hash hashes32[32j..), encoding rlp[off[j] .. off[j+1]) (off has n_nodes+1

@@ -3340,3 +3340,6 @@ int kh_trie_free(kh_trie* h) {
 }
 
 }  // extern "C"
+
+// multi-GPU root over RCCL in one process (kh_trie_root_sharded)
+#include "sharded.h"

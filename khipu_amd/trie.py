@@ -92,6 +92,24 @@ def trie_root(keys, vals, hash_keys=False, klen=None, stats=None):
     return out.tobytes()
 
 
+def trie_root_sharded(keys, vals, devices, hash_keys=False, klen=None, stats=None):
+    """trie_root on several GPUs of this process (kh_trie_root_sharded: nibble shards,
+    RCCL point-to-point exchange, host fold of the 16 subtrie references)."""
+    if klen is None:
+        klen = 32 if isinstance(keys, np.ndarray) or not keys else len(keys[0])
+    kb, n = _keys_buf(keys, klen)
+    vb, off = vals if isinstance(vals, tuple) else _pack(list(vals))
+    vb = _u8(vb)
+    dv = np.asarray(list(devices), dtype=np.int32)
+    out = np.zeros(32, dtype=np.uint8)
+    st = stats if stats is not None else KhStats()
+    flags = _lib.KH_HASH_KEYS if hash_keys else 0
+    check(lib().kh_trie_root_sharded(dv.ctypes.data, len(dv), kb.ctypes.data, klen, vb.ctypes.data,
+                                     np.ascontiguousarray(off, np.uint64).ctypes.data, n, flags, out.ctypes.data,
+                                     ctypes.byref(st)))
+    return out.tobytes()
+
+
 def trie_roots(tries, hash_keys=False, stats=None):
     """Roots of many independent tries in one device call.  tries: list of (keys, vals)."""
     keys, vals, seg_off = [], [], [0]
