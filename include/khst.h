@@ -265,6 +265,13 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
                     const uint8_t* d_a_up_keys, uint8_t* d_a_up_vals, const uint64_t* d_a_up_voff,
                     const uint32_t* d_a_up_trie, uint64_t na_up, const uint8_t* d_a_del_keys, uint64_t na_del,
                     uint32_t a_klen, uint8_t state_root32[32], kh_stats* stats);
+/* kh_block_commit from host arrays (staged in one device buffer; for a JVM caller). */
+int kh_block_commit_host(kh_trie* state, kh_trie* storage, const uint32_t* s_up_trie, const uint8_t* s_up_keys,
+                         const uint8_t* s_up_vals, const uint64_t* s_up_voff, uint64_t ns_up,
+                         const uint32_t* s_del_trie, const uint8_t* s_del_keys, uint64_t ns_del, uint32_t s_klen,
+                         const uint8_t* a_up_keys, const uint8_t* a_up_vals, const uint64_t* a_up_voff,
+                         const uint32_t* a_up_trie, uint64_t na_up, const uint8_t* a_del_keys, uint64_t na_del,
+                         uint32_t a_klen, uint8_t state_root32[32], kh_stats* stats);
 
 /* Storage write-back hand-off of the LAST commit (open or apply) of a
  * trie opened with KH_EMIT_NODES: exactly the nodes that commit created -- every node

@@ -971,7 +971,7 @@ struct kh_ctx {
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // leaf hashing, concurrent with the branch topology
   std::mutex mu;
-  DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, in_kn, in_aux, out_emit, emit_dev;
+  DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, in_kn, in_aux, in_block, out_emit, emit_dev;
   hipEvent_t ev[11] = {};  // [8] boundaries ready (st), [9] / [10] leaf kernel start / end (st2)
   unsigned long long* h_pinned = nullptr;  // small pinned staging for syncs
   // last build (for emission)
@@ -2464,7 +2464,7 @@ int kh_ctx_destroy(kh_ctx* c) {
   API_TRY({
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->st);
-    for (DevBuf* b : {&c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->in_kn, &c->in_aux, &c->out_emit,
+    for (DevBuf* b : {&c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->in_kn, &c->in_aux, &c->in_block, &c->out_emit,
                       &c->emit_dev})
       b->release();
     for (auto& e : c->ev)
@@ -3307,6 +3307,67 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
       stats->t_total_ms = ast.t_total_ms + sst.t_total_ms;
     }
   })
+}
+
+// kh_block_commit from host arrays (the JVM caller): the block's whole dirty set staged
+// in one buffer, then the device variant
+int kh_block_commit_host(kh_trie* state, kh_trie* storage, const uint32_t* s_up_trie, const uint8_t* s_up_keys,
+                         const uint8_t* s_up_vals, const uint64_t* s_up_voff, uint64_t ns_up,
+                         const uint32_t* s_del_trie, const uint8_t* s_del_keys, uint64_t ns_del, uint32_t s_klen,
+                         const uint8_t* a_up_keys, const uint8_t* a_up_vals, const uint64_t* a_up_voff,
+                         const uint32_t* a_up_trie, uint64_t na_up, const uint8_t* a_del_keys, uint64_t na_del,
+                         uint32_t a_klen, uint8_t state_root32[32], kh_stats* stats) {
+  if (!state || !storage) return set_err(KH_EINVAL, "need a state trie and a forest");
+  if ((ns_up && (!s_up_trie || !s_up_voff)) || (ns_del && !s_del_trie) || (na_up && !a_up_voff))
+    return set_err(KH_EINVAL, "null input");
+  kh_ctx* c = state->c;
+  std::lock_guard<std::mutex> g(c->mu);
+  int rc = KH_OK;
+  try {
+    HIPCHK(hipSetDevice(c->dev));
+    const uint64_t sv0 = ns_up ? s_up_voff[0] : 0, svb = ns_up ? s_up_voff[ns_up] - sv0 : 0;
+    const uint64_t av0 = na_up ? a_up_voff[0] : 0, avb = na_up ? a_up_voff[na_up] - av0 : 0;
+    c->in_block.ensure(carve_size({ns_up * 4, ns_up * s_klen, svb + 64, (ns_up + 1) * 8, ns_del * 4, ns_del * s_klen,
+                                   na_up * a_klen, avb + 64, (na_up + 1) * 8, na_up * 4, na_del * a_klen}));
+    Carver cb{(char*)c->in_block.p, 0, c->in_block.cap};
+    uint32_t* st_ = cb.take<uint32_t>(ns_up);
+    uint8_t* sk = cb.take<uint8_t>(ns_up * s_klen);
+    uint8_t* sv = cb.take<uint8_t>(svb + 64);
+    uint64_t* so = cb.take<uint64_t>(ns_up + 1);
+    uint32_t* sdt = cb.take<uint32_t>(ns_del);
+    uint8_t* sdk = cb.take<uint8_t>(ns_del * s_klen);
+    uint8_t* ak = cb.take<uint8_t>(na_up * a_klen);
+    uint8_t* av = cb.take<uint8_t>(avb + 64);
+    uint64_t* ao = cb.take<uint64_t>(na_up + 1);
+    uint32_t* at = cb.take<uint32_t>(na_up);
+    uint8_t* adk = cb.take<uint8_t>(na_del * a_klen);
+    std::vector<uint64_t> srel(ns_up + 1, 0), arel(na_up + 1, 0);
+    for (uint64_t i = 0; ns_up && i <= ns_up; ++i) srel[i] = s_up_voff[i] - sv0;
+    for (uint64_t i = 0; na_up && i <= na_up; ++i) arel[i] = a_up_voff[i] - av0;
+    hipStream_t st = c->st;
+    auto up = [&](void* d, const void* h, uint64_t bytes) {
+      if (bytes) HIPCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
+    };
+    up(st_, s_up_trie, ns_up * 4);
+    up(sk, s_up_keys, ns_up * s_klen);
+    up(sv, s_up_vals ? s_up_vals + sv0 : nullptr, svb);
+    up(so, srel.data(), ns_up ? (ns_up + 1) * 8 : 0);
+    up(sdt, s_del_trie, ns_del * 4);
+    up(sdk, s_del_keys, ns_del * s_klen);
+    up(ak, a_up_keys, na_up * a_klen);
+    up(av, a_up_vals ? a_up_vals + av0 : nullptr, avb);
+    up(ao, arel.data(), na_up ? (na_up + 1) * 8 : 0);
+    up(at, a_up_trie, a_up_trie ? na_up * 4 : 0);
+    up(adk, a_del_keys, na_del * a_klen);
+    HIPCHK(hipStreamSynchronize(st));  // srel / arel are host temporaries
+    rc = kh_block_commit(state, storage, st_, sk, sv, so, ns_up, sdt, sdk, ns_del, s_klen, ak, av, ao,
+                         a_up_trie ? at : nullptr, na_up, adk, na_del, a_klen, state_root32, stats);
+  } catch (KhError& e) {
+    return set_err(e.code, e.msg);
+  } catch (std::exception& e) {
+    return set_err(KH_EINTERNAL, e.what());
+  }
+  return rc;
 }
 
 int kh_trie_emit_nodes(kh_trie* h, uint8_t* hashes32, uint64_t node_cap, uint8_t* rlp, uint64_t rlp_cap,

@@ -308,3 +308,30 @@ def block_commit(state, forest, s_up_trie, s_up_keys, s_up_vals, s_up_voff, ns_u
                                 a_klen, root.ctypes.data, ctypes.byref(st)))
     state.root = root.tobytes()
     return state.root
+
+
+def block_commit_host(state, forest, s_up_trie, s_up_keys, s_up_vals, s_up_voff, s_del_trie, s_del_keys,
+                      a_up_keys, a_up_vals, a_up_voff, a_up_trie, a_del_keys, s_klen=32, a_klen=32, stats=None):
+    """kh_block_commit_host: the same block from host (numpy) arrays; counts from the shapes."""
+    keep = []  # contiguous copies stay alive through the call
+
+    def p(a):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a)
+        keep.append(a)
+        return a.ctypes.data
+    ns_up = 0 if s_up_trie is None else len(s_up_trie)
+    ns_del = 0 if s_del_trie is None else len(s_del_trie)
+    na_up = len(a_up_voff) - 1
+    na_del = 0 if a_del_keys is None else len(a_del_keys) // a_klen
+    root = np.zeros(32, np.uint8)
+    st = stats if stats is not None else KhStats()
+    state.ctx._sync()
+    check(lib().kh_block_commit_host(state.h, forest.h, p(s_up_trie), p(s_up_keys), p(s_up_vals), p(s_up_voff), ns_up,
+                                     p(s_del_trie), p(s_del_keys), ns_del, s_klen, p(a_up_keys), p(a_up_vals),
+                                     p(a_up_voff), p(a_up_trie), na_up, p(a_del_keys), na_del, a_klen,
+                                     root.ctypes.data, ctypes.byref(st)))
+    del keep
+    state.root = root.tobytes()
+    return state.root

@@ -249,3 +249,41 @@ def test_open_from_node_store_1m(khst, oracle):
         assert (ra == want, rb == want) == (True, True), blk
     a.close()
     b.close()
+
+
+def test_block_commit_host_matches_device(khst):
+    """kh_block_commit_host (host arrays, the JVM entry) against kh_block_commit (device
+    tensors): a twin state trie + storage forest fed the same blocks gives the same state
+    roots and the same storage roots."""
+    import numpy as np
+    from khipu_amd.device import Ctx, ResidentForest, ResidentTrie, block_commit_host
+    from tests.blocks import BlockWorkload
+
+    class Twin(BlockWorkload):
+        def _commit(self, s_tid, s_keys, s_vals, s_voff, d_tid, d_keys, a_keys, a_vals, a_voff, a_tid, a_del,
+                    timed=True):
+            if not hasattr(self, "twin"):
+                st = ResidentTrie.__new__(ResidentTrie)
+                st.ctx, st.dev, st.h = self.ctx, self.dev, None
+                st._open(self.keys, 32, self.vals, self.voff, self.n, False, emit=False)
+                self.twin = (st, ResidentForest(self.ctx, hash_keys=True))
+                self.twin_roots = []
+            h = lambda t: None if t is None else t.cpu().numpy()  # noqa: E731
+            args = [h(t) for t in (s_tid, s_keys, s_vals, s_voff, d_tid, d_keys, a_keys, a_vals, a_voff, a_tid,
+                                   a_del)]
+            root = super()._commit(s_tid, s_keys, s_vals, s_voff, d_tid, d_keys, a_keys, a_vals, a_voff, a_tid, a_del,
+                                   timed)
+            s_tid_h, s_keys_h, s_vals_h, s_voff_h, d_tid_h, d_keys_h, a_keys_h, a_vals_h, a_voff_h, a_tid_h, a_del_h = args
+            n_s = len(s_tid_h)
+            r2 = block_commit_host(self.twin[0], self.twin[1], s_tid_h.astype(np.uint32), s_keys_h, s_vals_h,
+                                   s_voff_h[:n_s + 1].astype(np.uint64), None if d_tid_h is None else
+                                   d_tid_h.astype(np.uint32), d_keys_h, a_keys_h, a_vals_h,
+                                   a_voff_h[:len(a_tid_h) + 1].astype(np.uint64), a_tid_h.astype(np.uint32), a_del_h)
+            assert r2 == root
+            assert self.twin[1].last_roots() == self.forest.last_roots()
+            return root
+
+    ctx = Ctx(0)
+    w = Twin(ctx, 30_000, 2, nc=40, ns=100, dirty=2_000)
+    for b in range(2):
+        w.block(b)
