@@ -454,7 +454,7 @@ int or_batch_roots(const uint8_t* keys, const uint64_t* koff, uint64_t klen, con
       } else {
         x.k = koff ? keys + koff[i] : keys + i * klen;
         size_t kl = koff ? koff[i + 1] - koff[i] : klen;
-        if (kl == 0 || kl > (1u << 20)) throw std::runtime_error("key length must be in [1, 2^20]");
+        if (kl > (1u << 20)) throw std::runtime_error("key length must be at most 2^20");
         x.knib = (uint32_t)(2 * kl);
       }
       x.v = vals + voff[i];

@@ -247,7 +247,7 @@ def prefix_key_cases(seed=43):
     r = random.Random(seed)
     out = []
     base = bytes(r.getrandbits(8) for _ in range(6))
-    ks = [base[:2], base[:4], base[:4] + b"\x01", base[:4] + b"\x10", base, base[:3], b"\x00", b"\xff\xfe"]
+    ks = [base[:2], base[:4], base[:4] + b"\x01", base[:4] + b"\x10", base, base[:3], b"\x00", b"\xff\xfe", b""]
     out.append(("prefix_small", ks, [bytes([i + 1]) * (i * 9 + 1) for i in range(len(ks))]))
     ks = []
     for _ in range(300):
