@@ -75,3 +75,60 @@ def test_evmcode_and_unknown_are_not_decoded(oracle, kind):
     assert emu.node_children(b"\x60\x00", 3) == (0, [])
     assert oracle.node_children(b"\x60\x00", 3) == (0, [])
     assert emu.node_children(b"\xc0", kind) == oracle.node_children(b"\xc0", kind)
+
+
+def _ref_decode(d, pos=0):
+    """RLP.decodeWithPos / getItemBounds / slice as the reference runs them
+    (rlp/RLP.scala:179-230): `slice` is Arrays.copyOfRange, which ZERO-PADS a range past
+    the end, and reading a prefix byte past the end throws (ArrayIndexOutOfBounds ->
+    IndexError here)."""
+    def sl(a, b):
+        return bytes(d[a:b]) + b"\0" * max(0, b - max(a, len(d)))
+    p = d[pos]
+    if p == 0x80:
+        return b"", pos + 1
+    if p < 0x80:
+        return bytes([p]), pos + 1
+    if p <= 0xB7:
+        n = p - 0x80
+        return sl(pos + 1, pos + 1 + n), pos + 1 + n
+    if p < 0xC0:
+        ll = p - 0xB7
+        n = int.from_bytes(sl(pos + 1, pos + 1 + ll), "big")
+        b = pos + 1 + ll
+        return sl(b, b + n), b + n
+    if p <= 0xF7:
+        b, n = pos + 1, p - 0xC0
+    else:
+        ll = p - 0xF7
+        n = int.from_bytes(sl(pos + 1, pos + 1 + ll), "big")
+        b = pos + 1 + ll
+    items, q = [], b
+    while q < b + n:
+        it, q = _ref_decode(d, q)
+        items.append(it)
+    return items, b + n
+
+
+def test_truncated_items_reference_behaviour(oracle):
+    """What the reference does with a TRUNCATED node value, and why kh_verify_nodes may
+    reject it instead (status 4, strict decode).  The reference zero-pads a string item that
+    runs past the end (copyOfRange) or throws ArrayIndexOutOfBounds when a list item's
+    prefix lies past the end; either way the value is not a node encoding.  A NodeData
+    value reaches the decoder only after its kec256 matched a REQUESTED hash
+    (sync/package.scala:88-95), i.e. it is a preimage of a hash some valid trie node
+    produced, and every valid node is well-formed RLP -- so truncated values are
+    unreachable in the reference's flow and the two decoders agree on every reachable
+    input (test_node_children_real_nodes)."""
+    from tests.emu import emu
+    leaf = bytes.fromhex("e1a0") + bytes(range(32))  # [HP path (32 B string)]: one item
+    trunc_string = leaf[:-5]  # the string runs 5 bytes past the end
+    items, _ = _ref_decode(trunc_string)
+    assert items == [bytes(range(27)) + b"\0" * 5]  # the reference zero-pads
+    trunc_list = bytes([0xC4, 0x82, 0x01])  # the list claims 4 bytes, 2 present
+    with pytest.raises(IndexError):  # the reference throws reading the next prefix
+        _ref_decode(trunc_list)
+    for v in (trunc_string, trunc_list):
+        for kind in (0, 2):
+            st_o = oracle.node_children(v, kind)[0]
+            assert st_o != 0 and emu.node_children(v, kind)[0] == st_o
