@@ -177,12 +177,12 @@ def pmc_traffic(kernel, n):
 def roofline(stats, n):
     """Dominant single kernel of the step (the larger of the two one-launch hash kernels),
     from the HIP events the library records on the stream each kernel runs on."""
-    stages = {"k_hash_keys": "t_keys_ms", "k_leaf_fused": "t_leaf_ms", "branch_levels": "t_branch_ms",
+    stages = {"k_hash_keys_ck": "t_keys_ms", "k_leaf_in": "t_leaf_ms", "branch_levels": "t_branch_ms",
               "sort": "t_sort_ms", "topology": "t_topo_ms"}
     avg = {k: float(np.mean([x[v] for x in stats])) for k, v in stages.items()}
     s = stats[-1]
-    dom = max(("k_hash_keys", "k_leaf_fused"), key=avg.get)
-    perms = {"k_hash_keys": s["n_key_perms"], "k_leaf_fused": s["n_leaves"]}[dom]
+    dom = max(("k_hash_keys_ck", "k_leaf_in"), key=avg.get)
+    perms = {"k_hash_keys_ck": s["n_key_perms"], "k_leaf_in": s["n_leaves"]}[dom]
     achieved = perms * OPS_PER_PERM / (avg[dom] * 1e-3)
     return avg, {"kernel": dom, "bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
                  "unit": "T int32-lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS,

@@ -106,6 +106,19 @@ __global__ void __launch_bounds__(BS) k_hash_keys(const uint8_t* keys, uint32_t 
   for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
 }
 
+// ... and the unsegmented sort key (the key's leading 64 bits, big-endian) with the
+// identity index in the same pass (saves k_make_ck's re-read of the keys)
+__global__ void __launch_bounds__(BS) k_hash_keys_ck(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out,
+                                                     uint64_t* ck, uint32_t* idx) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h[4];
+  kec256_msg<false>(keys + i * klen, klen, h);
+  for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
+  ck[i] = bswap64(h[0]);
+  idx[i] = (uint32_t)i;
+}
+
 // composite sort key: segment id in the top sb bits, then the key's leading bits (big-endian)
 __global__ void __launch_bounds__(BS) k_make_ck(const uint64_t* K, const uint32_t* seg, uint32_t sb, uint64_t n,
                                                 uint64_t* ck, uint32_t* idx) {
@@ -438,106 +451,32 @@ __global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
   block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
 }
 
-// Fused leaf encode + hash (the root-only build; the write-back build keeps the
-// encodings and uses k_leaf_prep/k_leaf_hash).  Each lane owns a 17-word LDS
-// message slot.  1) the wave copies the value bytes of its 64 leaves straight to
-// their message positions (16 lanes per leaf: one coalesced request per value,
-// funnel-shifted by the header length), 2) each lane writes its header bytes in
-// front (merging the shared word), Keccak's its slot and publishes the reference.
-// Leaves longer than one block take the arena path (k_leaf_prep's global writer).
-// Plain root builds (trie_ops.h "early leaves"): launched on the second stream right
-// after k_lcp; the parent depth comes from the two boundaries, the reference is
-// stashed for k_leaf_topo_early, and long leaves are only counted (their arena bytes)
-// for k_leaf_long.
-__global__ void __launch_bounds__(BS) k_leaf_fused(Topo T) {
-  constexpr bool EARLY = true;
-  __shared__ uint64_t msg[BS * LEAF_WORDS];
-  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u;
-  const bool valid = i < T.m;
-  uint64_t off = 0;
-  uint32_t vlen = 0, v0 = 0;
-  Key4 k{0, 0, 0, 0};
-  int32_t pd = 0;
-  if (valid) {
-    off = T.svoff[i];
-    vlen = T.svlen[i];
-    k = load_key(T.skey, i);
-    pd = EARLY ? leaf_pd_early(T, i) : T.lf_pd[i];
-    if (vlen == 1) v0 = T.vals[off];
-  }
-  LeafGeom g = leaf_geom(k, pd, vlen, v0);
-  const bool shortl = valid && g.L <= LEAF_SHORT_MAX;
+// Early leaves (plain root builds; trie_ops.h op_leaf_in): one thread per INPUT,
+// launched on the second stream right after op_pd_scatter, beside the branch topology.
+// The keys and packed values are read in input order (sequential), the message is
+// assembled in registers straight into the Keccak state; only the <= 37-byte header goes
+// through a 5-word LDS slot per lane ([word][lane]: conflict-free).
+constexpr uint32_t HDR_WORDS = 5;
+__global__ void __launch_bounds__(BS) k_pd_scatter(Topo T) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < T.m) op_pd_scatter(T, i);
+}
+__global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
+  __shared__ uint64_t hdr[HDR_WORDS * BS];
+  const uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
   typedef const __attribute__((address_space(1))) uint64_t gword;  // global (not flat) loads
   const uint32_t vmis = (uint32_t)((uintptr_t)T.vals & 7);
   gword* vw = (gword*)(T.vals - vmis);
-  // value span [vs, vs + vlen) in aligned-word coordinates; header length P = L - vlen
-  const uint64_t vs = off + vmis;
-  const uint32_t P = g.L - vlen;
-  const uint32_t qlo = P >> 3, nq = (shortl && vlen) ? ((g.L + 7) >> 3) - qlo : 0;
-  const uint32_t gi = ln >> 4, gl = ln & 15;
-  // the staging parameters of the wave's 64 leaves go through LDS (one broadcast
-  // read per group instead of five shuffles), and the copy loop is fully unrolled
-  // with two predicated word steps, so every group's loads are independent and issue
-  // back to back (the random value reads are latency-bound)
-  __shared__ uint64_t s_vs[BS];
-  __shared__ uint32_t s_pq[BS];
-  s_vs[threadIdx.x] = vs;
-  s_pq[threadIdx.x] = P | ((g.L & 0xFFu) << 8) | (qlo << 16) | (nq << 24);  // nq > 0 only for one-block leaves
-  __syncthreads();
-#pragma unroll
-  for (uint32_t it = 0; it < 16; ++it) {
-    const uint32_t src = it * 4 + gi;
-    const uint32_t pq = s_pq[wbase + src];
-    const uint32_t snq = pq >> 24, sP = pq & 0xFF, sL = (pq >> 8) & 0xFF, sq = (pq >> 16) & 0xFF;
-    const uint64_t svs = s_vs[wbase + src];
-    const uint64_t w_first = svs >> 3, w_last = (svs + (sL - sP) - 1) >> 3;
-    uint64_t* dst = msg + (wbase + src) * LEAF_WORDS;
-#pragma unroll
-    for (uint32_t h = 0; h < 2; ++h) {
-      const uint32_t q = sq + gl + 16 * h;
-      if (q >= sq + snq) continue;
-      // message byte 8q <-> value byte 8q - P <-> buffer byte svs + 8q - P (may precede the span)
-      const int64_t bp = (int64_t)svs + 8 * (int64_t)q - (int64_t)sP;
-      const int64_t wa = bp >> 3;  // arithmetic shift: floor
-      const uint32_t sh = (uint32_t)(bp & 7);
-      const uint64_t lo = (wa >= (int64_t)w_first && (uint64_t)wa <= w_last) ? vw[wa] : 0;
-      const uint64_t hi = (sh && wa + 1 >= (int64_t)w_first && (uint64_t)(wa + 1) <= w_last) ? vw[wa + 1] : 0;
-      uint64_t x = sh ? (lo >> (8 * sh)) | (hi << (64 - 8 * sh)) : lo;
-      // keep message bytes [P, L) of this word
-      const uint32_t b0 = 8 * q;
-      if (b0 < sP) x &= ~low_bytes_mask(sP - b0);
-      if (b0 + 8 > sL) x &= low_bytes_mask(sL - b0);
-      dst[q] = x;
-    }
-  }
-  __syncthreads();
-  unsigned long long perms = 0, hashes = 0, inl = 0, longb = 0;
-  if (valid) {
-    uint32_t in1 = 0;
-    if (shortl) {
-      uint64_t* my = msg + threadIdx.x * LEAF_WORDS;
-      BW w(my, 1);
-      leaf_header(w, k, g, vlen);
-      if (vlen) w.flush_or();
-      else w.flush();
-      perms = EARLY ? leaf_hash_early(T, i, pd == (int32_t)T.depth0 - 1, my, 1, g.L, &in1)
-                    : leaf_hash_at(T, i, my, 1, g.L, &in1);
-    } else if (EARLY) {
-      T.lf_emeta[i] = EMETA_LONG;  // encoded + hashed by k_leaf_long into its arena slot
-      longb = (g.L + 7) & ~7u;
-    } else {
-      op_leaf_prep(T, i, T.vals + off, vlen);  // arena
-      perms = leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, g.L, &in1);
-    }
-    hashes = perms ? 1 : 0;
+  unsigned long long perms = 0, inl = 0, longb = 0;
+  if (j < n) {
+    uint32_t in1 = 0, lb = 0;
+    perms = op_leaf_in(T, j, vw, vmis, hdr + threadIdx.x, BS, &in1, &lb);
     inl = in1;
+    longb = lb;
   }
-  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
-  if (EARLY) {
-    __syncthreads();  // block_add3's LDS slots are reused
-    block_add3(&T.ctr[CTR_LONGB], longb, nullptr, 0, nullptr, 0);
-  }
+  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], perms, &T.ctr[CTR_INLINE], inl);
+  __syncthreads();  // block_add3's LDS slots are reused
+  block_add3(&T.ctr[CTR_LONGB], longb, nullptr, 0, nullptr, 0);
 }
 
 // after the branch topology (plain root builds): stashed leaf references into the
@@ -1043,6 +982,7 @@ struct SortIO {
   void* scan_scratch;
   unsigned long long* ctr;
   const uint8_t* kn;  // variable-length keys: nibble counts (input order; nullable)
+  bool ck_ready = false;  // ck0/idx0 already hold the unsegmented sort keys (k_hash_keys_ck)
   // out
   uint64_t m;
   uint32_t* sidx;
@@ -1067,8 +1007,10 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
   // ---- 2. sort: LSD radix on the top 32 bits of the composite (segment | key) prefix,
   // then fix the rare runs of equal prefixes locally (k_tie_fix); a full 256-bit sort
   // only if a run is longer than TIE_RUN_MAX (adversarial keys)
-  hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, sb, n, ck0, idx0);
-  LAUNCH_CHECK();
+  if (!S.ck_ready) {
+    hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, sb, n, ck0, idx0);
+    LAUNCH_CHECK();
+  }
   bool flip = radix_sort_pairs(ck0, idx0, ck1, idx1, n, 32, 64, rs_scratch, st);
   uint64_t* cks = flip ? ck1 : ck0;
   uint32_t* idxs = flip ? idx1 : idx0;
@@ -1187,13 +1129,13 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       n * 32, segmented ? n * 4 : 0,          // skey sseg
       radix_scratch_bytes(n), scan_scratch_bytes(n, 8),
       nb1, nb1 / 32 + 1024,                   // u, pyramid
-      nb1 * 4, nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1 * 4,  // psv nsv pse rep ord isrep
+      nb1 * 4, nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1 * 4, nb1, nb1,  // psv nsv pse rep ord isrep glast gk
       nb1 * 4, nb1 * 4, nb1, nb1, nb1 * 4, nb1, nb1 * 4, nb1 * 8, nb1 * 4, nb1 * 4,  // branches
       n * 4, n, n, n * 8, n * 4, n * 8, n * 4,  // leaves, svoff, svlen
       A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
       nres * 32, nres * 4, nres * 32,         // results
       CTR_N * 8, 64 * 4, 80 * 4, 512 * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
-      early ? n * 32 : 0, early ? n : 0,      // early leaves: stashed references, meta
+      early ? n * 32 : 0, early ? n : 0, early ? n * 8 : 0,  // early leaves: stashed references, meta, pd|position
       A.kn ? n : 0,                           // sorted key lengths
       nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1, nb1,  // branch tables in key-order ids (BrTab J)
   };
@@ -1217,6 +1159,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.rep = cv.take<uint32_t>(nb1);
   T.ord = cv.take<uint8_t>(nb1);
   T.isrep_bid = cv.take<uint32_t>(nb1);
+  T.glast = cv.take<uint8_t>(nb1);
+  T.gk = cv.take<uint8_t>(nb1);
   T.br_k = cv.take<uint32_t>(nb1);
   T.br_cbase = cv.take<uint32_t>(nb1);
   T.br_depth = cv.take<uint8_t>(nb1);
@@ -1248,6 +1192,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint32_t* order = cv.take<uint32_t>(nb1);
   T.lf_eref = early ? cv.take<uint64_t>(n * 4) : nullptr;
   T.lf_emeta = early ? cv.take<uint8_t>(n) : nullptr;
+  T.pdinv = early ? cv.take<uint64_t>(n) : nullptr;
+  T.kin = K32;
   uint8_t* skn = A.kn ? cv.take<uint8_t>(n) : nullptr;
   BrTab J{};
   J.k = cv.take<uint32_t>(nb1);
@@ -1271,7 +1217,11 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
 
   HIPCHK(hipEventRecord(c->ev[0], st));
   // ---- 1. keys
-  if (A.flags & KH_HASH_KEYS) {
+  const bool ck_ready = (A.flags & KH_HASH_KEYS) && !segmented;
+  if (ck_ready) {
+    hipLaunchKernelGGL(k_hash_keys_ck, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, ck0, idx0);
+    LAUNCH_CHECK();
+  } else if (A.flags & KH_HASH_KEYS) {
     hipLaunchKernelGGL(k_hash_keys, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32);
     LAUNCH_CHECK();
   } else if (own_keys) {
@@ -1285,7 +1235,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   bool fallback = false;
   {
     SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr,
-             A.kn};
+             A.kn, ck_ready};
     sort_dedup(c, S);
     m = S.m;
     sidx = S.sidx;
@@ -1298,8 +1248,13 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.skey = skey;
   T.sidx = sidx;
   T.sseg = sseg;
-  hipLaunchKernelGGL(k_val_gather, GRID(m, BS), dim3(BS), 0, st, T);
-  LAUNCH_CHECK();
+  if (early) {  // the leaves read their spans in input order; long ones through sidx
+    T.svoff = nullptr;
+    T.svlen = nullptr;
+  } else {
+    hipLaunchKernelGGL(k_val_gather, GRID(m, BS), dim3(BS), 0, st, T);
+    LAUNCH_CHECK();
+  }
   if (A.kn) {
     hipLaunchKernelGGL(k_kn_gather, GRID(m, BS), dim3(BS), 0, st, A.kn, (const uint32_t*)sidx, m, skn);
     LAUNCH_CHECK();
@@ -1341,11 +1296,14 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
   }
-  if (early) {  // leaves need only the boundaries: hash them beside the topology
+  if (early) {  // leaves need only the boundaries: hash them (input order) beside the topology
+    if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, st));  // dropped duplicates: PDINV_SKIP
+    hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, st, T);
+    LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[8], st));
     HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
     HIPCHK(hipEventRecord(c->ev[9], c->st2));
-    hipLaunchKernelGGL(k_leaf_fused, GRID(m, BS), dim3(BS), 0, c->st2, T);
+    hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, c->st2, T, n);
     LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[10], c->st2));
   }
@@ -1364,6 +1322,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       P.nl++;
       pp += (nout + 255) & ~(uint64_t)255;
     }
+    HIPCHK(hipMemsetAsync(T.glast, 1, nb, st));
     hipLaunchKernelGGL(k_ansv, GRID(nb, BS), dim3(BS), 0, st, T, P, nb);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_chain, GRID(nb, BS), dim3(BS), 0, st, T, nb);
@@ -1538,8 +1497,10 @@ static kh_ctx* ctx_new(int dev) {
   // over the VALU-bound leaf kernel they overlap with (st2)
   int prio_lo = 0, prio_hi = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  HIPCHK(hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, prio_hi));
-  HIPCHK(hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, prio_lo));
+  const char* lp = getenv("KHST_LEAF_PRIO");  // measurement switch: "hi" gives the leaf stream priority
+  const bool leaf_hi = lp && strcmp(lp, "hi") == 0;
+  HIPCHK(hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, leaf_hi ? prio_lo : prio_hi));
+  HIPCHK(hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, leaf_hi ? prio_hi : prio_lo));
   c->st = c->own;
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipHostMalloc((void**)&c->h_pinned, 4096, hipHostMallocDefault));

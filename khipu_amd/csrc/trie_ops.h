@@ -165,7 +165,9 @@ struct Topo {
   int32_t* pse;           // [m-1] previous smaller-or-equal boundary (-1: none)
   uint32_t* rep;          // [m-1] group representative of b
   uint8_t* ord;           // [m-1] ordinal of b within its group
-  uint32_t* isrep_bid;    // [m-1] 1 if rep, then (after scan) branch id of rep
+  uint32_t* isrep_bid;     // [m-1] 1 if rep, then (after scan) branch id of rep
+  uint8_t* glast;         // [nb] 1 unless a later boundary of the same group exists (preset 1)
+  uint8_t* gk;            // [nb] at a group's representative: its branch's child count
   // branches (B <= m-1)
   uint32_t* br_k;         // child count
   uint32_t* br_cbase;     // first child record
@@ -208,6 +210,9 @@ struct Topo {
   // (32 = hash, EMETA_LONG = not hashed yet: longer than one Keccak block)
   uint64_t* lf_eref;   // [m*4]
   uint8_t* lf_emeta;   // [m]
+  const uint64_t* kin; // [n*4] the keys in input order (the early leaf kernel reads them sequentially)
+  uint64_t* pdinv;     // [n] per INPUT position: parent depth << 32 | sorted position; PDINV_SKIP for
+                       //     a dropped duplicate
   // element builds (resident commits, forest.h; all nullable): an element is a leaf, or
   // a SUBTREE standing for an unchanged branch at depth el_db[i] whose capped reference
   // is el_bref / el_brl (its keys all share key i's first el_db nibbles)
@@ -405,17 +410,23 @@ KH_HD void op_min64(const uint8_t* in, uint64_t nin, uint8_t* out, uint64_t i) {
   out[i] = (uint8_t)mn;
 }
 
+// Previous smaller-or-equal boundary for every b.  If it carries the same value it is b's
+// predecessor in its group (b is not the group's first, and it is not the last); else b
+// is its group's representative, and only reps need their strictly-smaller neighbours
+// (the range of the branch): psv = pse, nsv one more query.  glast must be preset to 1.
 KH_HD void op_ansv(const Topo& T, const Pyr& P, uint64_t b) {
   uint32_t t = T.u[b];
   if (t == 0) {
     T.psv[b] = T.nsv[b] = T.pse[b] = -1;
     return;
   }
-  // previous smaller-or-equal first; it is also the previous strictly smaller one
-  // unless it carries the same value (then keep scanning left from it)
   int64_t pse = ansv_left(P, b, t + 1);
   T.pse[b] = (int32_t)pse;
-  T.psv[b] = (int32_t)((pse < 0 || T.u[pse] < t) ? pse : ansv_left(P, (uint64_t)pse, t));
+  if (pse >= 0 && T.u[pse] == t) {
+    T.glast[pse] = 0;  // the predecessor has a later member
+    return;
+  }
+  T.psv[b] = (int32_t)pse;
   T.nsv[b] = (int32_t)ansv_right(P, b, t);
 }
 
@@ -442,6 +453,7 @@ KH_HD void op_chain(const Topo& T, uint64_t b) {
   T.rep[b] = (uint32_t)j;
   T.ord[b] = (uint8_t)o;
   T.isrep_bid[b] = (o == 0) ? 1u : 0u;
+  if (T.glast[b]) T.gk[j] = (uint8_t)(o + 2);  // the group's last member: the branch has o + 2 children
 }
 
 // parent resolution for a node whose key range is [s, e]: boundaries s-1 and e
@@ -470,8 +482,7 @@ KH_HD Parent resolve_parent(const Topo& T, int64_t a, int64_t c) {
 }
 
 // ---- stage: branch records (thread per boundary; only reps act).  The child count
-// comes from the group's last member: the rightmost boundary <= t before the next
-// strictly smaller one (one more pyramid query), k = its ordinal + 2.
+// was left by the group's last member (op_chain): its ordinal + 2.
 KH_HD void op_branch_topo(const Topo& T, const Pyr& P, uint64_t nb, uint64_t b) {
   if (T.u[b] == 0 || T.rep[b] != (uint32_t)b) return;
   uint32_t j = T.isrep_bid[b];
@@ -479,8 +490,7 @@ KH_HD void op_branch_topo(const Topo& T, const Pyr& P, uint64_t nb, uint64_t b) 
   uint32_t d = t - 1u;
   int64_t a = T.psv[b], c = T.nsv[b];
   Parent Pp = resolve_parent(T, a, c);
-  int64_t last = ansv_left(P, c < 0 ? nb : (uint64_t)c, t + 1);
-  T.br_k[j] = (uint32_t)T.ord[last] + 2u;
+  T.br_k[j] = T.gk[b];
   T.br_depth[j] = (uint8_t)d;
   T.br_ext[j] = (uint8_t)((int32_t)d - Pp.pd - 1);
   T.br_parent[j] = Pp.bid;
@@ -785,40 +795,108 @@ KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
 
 // ---- early leaves: parent depth from the two adjacent boundaries (= resolve_parent's pd)
 constexpr uint8_t EMETA_LONG = 0xFF;
+constexpr uint64_t PDINV_SKIP = ~0ULL;
 KH_HD int32_t leaf_pd_early(const Topo& T, uint64_t i) {
   uint32_t va = i > 0 ? T.u[i - 1] : 0, vc = i + 1 < T.m ? T.u[i] : 0;
   uint32_t v = va > vc ? va : vc;
   return v == 0 ? (int32_t)T.depth0 - 1 : (int32_t)v - 1;
 }
-// Plain root builds hash leaves right after op_lcp, on a second stream, while the
-// branch topology is computed; the reference is stashed per leaf and
-// op_leaf_topo_early moves it into the parent's child record.  A top leaf (both
-// boundaries 0) publishes its result here.  One-block leaf at w, L bytes:
-KH_HD void leaf_publish_early(const Topo& T, uint64_t i, bool top, uint32_t L, const uint64_t hh[4],
-                              const uint64_t head[4], uint32_t* inl) {
+// Plain root builds hash their leaves in INPUT order right after op_lcp, on a second
+// stream, while the branch topology is computed.  Input order reads the keys and the
+// packed values sequentially (the sorted order would gather every value span at random:
+// ~2.5x the algorithmic bytes through 128-byte lines).  op_pd_scatter hands each kept
+// input its parent depth (from its sorted neighbours' boundaries) and its sorted
+// position, where the leaf kernel stashes the reference (one scattered 33-byte write,
+// fire-and-forget); op_leaf_topo_early then moves it into the parent's child record.
+KH_HD void op_pd_scatter(const Topo& T, uint64_t i) {
+  const uint32_t pd = (uint32_t)(uint8_t)(int8_t)leaf_pd_early(T, i);
+  T.pdinv[T.sidx ? T.sidx[i] : i] = ((uint64_t)pd << 32) | i;
+}
+// One input j.  The message (<= 135 B) is assembled in registers straight into the
+// Keccak state: the header bytes [0, P) come from `hdr` (5 words, stride hstride: a
+// per-lane LDS slot on the device), the value bytes [P, L) from the aligned words of the
+// value buffer `vw` (vals - vmis) funnel-shifted into place.  Returns permutations;
+// *inl / *longb count inline leaves and long-leaf arena bytes.
+template <typename WP>
+KH_HD uint32_t op_leaf_in(const Topo& T, uint64_t j, WP vw, uint32_t vmis, uint64_t* hdr, uint64_t hstride,
+                          uint32_t* inl, uint32_t* longb) {
   *inl = 0;
-  if (top) {
-    publish_ref(T, NONE, 0, 0, i, head, L, hh);
+  *longb = 0;
+  const uint64_t pv = T.pdinv[j];
+  if (pv == PDINV_SKIP) return 0;  // an earlier put of a key put again later
+  const int32_t pd = (int8_t)(uint8_t)(pv >> 32);
+  const uint64_t si = (uint32_t)pv;  // sorted position: where the reference is stashed
+  const Key4 k = load_key(T.kin, j);
+  const uint64_t off = T.voff[j];
+  const uint32_t vlen = (uint32_t)(T.voff[j + 1] - off);
+  const uint32_t v0 = vlen == 1 ? (uint32_t)T.vals[off] : 0;
+  const LeafGeom g = leaf_geom(k, pd, vlen, v0);
+  if (g.L > LEAF_SHORT_MAX) {  // encoded + hashed by op_leaf_long into its arena slot
+    T.lf_emeta[si] = EMETA_LONG;
+    *longb = (g.L + 7) & ~7u;
+    return 0;
+  }
+  const bool top = pd == (int32_t)T.depth0 - 1;
+  {
+    BW w(hdr, hstride);
+    leaf_header(w, k, g, vlen);
+    w.flush();
+  }
+  const uint32_t L = g.L, P = L - vlen;
+  const int64_t base = (int64_t)(off + vmis) - (int64_t)P;  // buffer byte of message byte 0
+  const int64_t a0 = base >> 3;                             // floor
+  const uint32_t sh = (uint32_t)(base & 7);
+  const int64_t wf = (int64_t)((off + vmis) >> 3), wl = vlen ? (int64_t)((off + vmis + vlen - 1) >> 3) : wf - 1;
+  KState S = {};
+  uint64_t head[4] = {0, 0, 0, 0};
+  uint64_t prev = (a0 >= wf && a0 <= wl) ? vw[a0] : 0;
+#pragma unroll
+  for (int q = 0; q < 17; ++q) {
+    const int64_t a = a0 + q + 1;
+    const uint64_t cur = (a >= wf && a <= wl) ? vw[a] : 0;
+    uint64_t x = sh ? (prev >> (8 * sh)) | (cur << (64 - 8 * sh)) : prev;
+    prev = cur;
+    const uint32_t b0 = 8u * (uint32_t)q;
+    if (b0 + 8 <= P || b0 >= L) x = 0;  // header-only or past the end
+    else {
+      if (b0 < P) x &= ~low_bytes_mask(P - b0);
+      if (b0 + 8 > L) x &= low_bytes_mask(L - b0);
+    }
+    if (q < 5 && b0 < P) x |= hdr[q * hstride];
+    if (q < 4) head[q] = x;
+    if ((L >> 3) == (uint32_t)q) x ^= 0x01ULL << (8 * (L & 7));
+    if (q == 16) x ^= 0x80ULL << 56;
+    S.lo[q] = (uint32_t)x;
+    S.hi[q] = (uint32_t)(x >> 32);
+  }
+  uint64_t* r = T.lf_eref + 4 * si;
+  uint32_t perms = 0;
+  if (L >= 32 || top) {  // a leaf embedded in its parent is never hashed (Node.scala:114)
+    keccakf(S);
+    for (int q = 0; q < 4; ++q) r[q] = lane(S, q);
+    perms = 1;
+  } else {
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t b = 8u * (uint32_t)q;
+      r[q] = b < L ? head[q] & low_bytes_mask(L - b < 8 ? L - b : 8) : 0;
+    }
+    *inl = 1;
+  }
+  // a top leaf is >= 35 B (its path is >= 63 nibbles: an HP of >= 33 B), so its stash is
+  // always the hash
+  T.lf_emeta[si] = (uint8_t)(L >= 32 ? 32 : L);
+  return perms;
+}
+// value span of sorted leaf i (early builds gather no spans: through the input index)
+KH_HD void leaf_span_early(const Topo& T, uint64_t i, uint64_t* off, uint32_t* len) {
+  if (T.svoff) {
+    *off = T.svoff[i];
+    *len = T.svlen[i];
     return;
   }
-  for (int q = 0; q < 4; ++q) {
-    uint32_t base = 8u * (uint32_t)q;
-    T.lf_eref[4 * i + q] = L >= 32 ? hh[q] : (base < L ? head[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0);
-  }
-  T.lf_emeta[i] = (uint8_t)(L >= 32 ? 32 : L);
-  *inl = L < 32 ? 1 : 0;
-}
-KH_HD uint32_t leaf_hash_early(const Topo& T, uint64_t i, bool top, const uint64_t* w, uint64_t stride, uint32_t L,
-                               uint32_t* inl) {
-  uint64_t hh[4] = {0, 0, 0, 0}, head[4];
-  uint32_t perms = 0;
-  if (L >= 32 || top) {
-    kec256_strided(w, stride, L, hh);
-    perms = 1;
-  }
-  for (int q = 0; q < 4; ++q) head[q] = (8u * q < L) ? w[q * stride] : 0;
-  leaf_publish_early(T, i, top, L, hh, head, inl);
-  return perms;
+  const uint32_t j = T.sidx ? T.sidx[i] : (uint32_t)i;
+  *off = T.voff[j];
+  *len = (uint32_t)(T.voff[j + 1] - *off);
 }
 // after the branch topology: the stashed reference goes to the parent's child
 // record; a long leaf gets its arena slot (as in op_leaf_topo) for op_leaf_long
@@ -831,21 +909,31 @@ KH_HD void op_leaf_topo_early(const Topo& T, uint64_t i, AllocFn alloc) {
     T.lf_parent[i] = P.bid;
     T.lf_pord[i] = (uint8_t)P.pord;
     T.lf_pd[i] = (int8_t)P.pd;
-    uint64_t L = leaf_enc_len((uint32_t)(P.pd + 1), T.svlen[i], 0);  // a long value has > 1 byte
+    uint64_t off;
+    uint32_t vlen;
+    leaf_span_early(T, i, &off, &vlen);
+    uint64_t L = leaf_enc_len((uint32_t)(P.pd + 1), vlen, 0);  // a long value has > 1 byte
     T.lf_aoff[i] = alloc((L + 7) & ~(uint64_t)7);
     return;
   }
-  if (P.bid == NONE) return;  // a top leaf: its result is already published
+  const uint64_t* r = T.lf_eref + 4 * i;
+  if (P.bid == NONE) {  // a top leaf: always hashed, its stash is the hash
+    publish_ref(T, NONE, 0, 0, i, r, 32, r);
+    return;
+  }
   Key4 k = load_key(T.skey, i);
   uint64_t slot = (uint64_t)T.br_cbase[P.bid] + P.pord;
-  for (int q = 0; q < 4; ++q) T.cref[4 * slot + q] = T.lf_eref[4 * i + q];
+  for (int q = 0; q < 4; ++q) T.cref[4 * slot + q] = r[q];
   T.cmeta[slot] = (uint16_t)(em | (key_nibble(k, P.pd) << 8));
 }
 // a long leaf (> one Keccak block): encode into its arena slot, hash, publish
 KH_HD uint32_t op_leaf_long(const Topo& T, uint64_t i, uint32_t* inl) {
   *inl = 0;
   if (T.lf_emeta[i] != EMETA_LONG) return 0;
-  op_leaf_prep(T, i, T.vals + T.svoff[i], T.svlen[i]);
+  uint64_t off;
+  uint32_t vlen;
+  leaf_span_early(T, i, &off, &vlen);
+  op_leaf_prep(T, i, T.vals + off, vlen);
   return leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, T.lf_len[i], inl);
 }
 

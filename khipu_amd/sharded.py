@@ -244,7 +244,7 @@ def bench_main(args):
     dist.all_reduce(hashes)
     dt = float(dt.item())
     node_hashes = int(hashes[0].item()) + 1  # + the folded root branch
-    # roofline of the dominant kernel (k_leaf_fused, one launch per rank per step), on the
+    # roofline of the dominant kernel (k_leaf_in, one launch per rank per step), on the
     # slowest rank: its HIP-event time on the library's stream
     leaf = torch.tensor([st.t_leaf_ms, float(st.n_leaves)], dtype=torch.float64, device=f"cuda:{local}")
     leaf_all = [torch.zeros_like(leaf) for _ in range(world)]
@@ -253,7 +253,7 @@ def bench_main(args):
     slow = max(leaf_all, key=lambda x: x[0])
     VALU_PEAK, OPS = 256 * 4 * 32 * 2.4e9, 5760
     achieved = slow[1] * OPS / max(slow[0] * 1e-3, 1e-12)
-    roof = {"kernel": "k_leaf_fused", "bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK / 1e12,
+    roof = {"kernel": "k_leaf_in", "bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK / 1e12,
             "unit": "T int32-lane-ops/s", "frac": achieved / VALU_PEAK, "traffic": None, "avg_ms": slow[0],
             "perms_per_launch": int(slow[1]), "rank": "slowest of the ranks"}
     # one more (untimed) step with a device sync after every phase: where the time goes

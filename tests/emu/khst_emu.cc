@@ -69,6 +69,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.svlen = svlen.data();
   for (uint64_t i = 0; i < m; ++i) op_val_gather(T, i);
   const uint64_t nbb = nb + 1;
+  std::vector<uint8_t> glast(nbb, 1), gk(nbb, 0);
   std::vector<uint8_t> u(nbb), ord(nbb), br_depth(nbb), br_ext(nbb), br_pord(nbb), lf_pord(m);
   std::vector<int32_t> psv(nbb), nsv(nbb), pse(nbb);
   std::vector<uint32_t> rep(nbb), isrep(nbb), br_k(nbb, 0), br_cbase(nbb), br_parent(nbb), br_first(nbb),
@@ -84,6 +85,8 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.rep = rep.data();
   T.ord = ord.data();
   T.isrep_bid = isrep.data();
+  T.glast = glast.data();
+  T.gk = gk.data();
   T.br_k = br_k.data();
   T.br_cbase = br_cbase.data();
   T.br_depth = br_depth.data();
@@ -140,36 +143,38 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       }
     }
   }
-  // plain builds replay the device's early-leaf path (k_leaf_fused: hashed from
-  // the boundaries alone, references stashed, published after the topology)
-  const bool early = true;  // plain builds: the device's early-leaf path
-  std::vector<uint64_t> eref(early ? 4 * m + 4 : 0);
-  std::vector<uint8_t> emeta(early ? m + 1 : 0);
+  // plain builds replay the device's early-leaf path: parent depths scattered to input
+  // order (k_pd_scatter), leaves hashed in input order (k_leaf_in), references stashed
+  // per input and published after the topology (k_leaf_topo_early)
+  const bool early = true;
+  std::vector<uint64_t> eref(4 * m + 4), kin(4 * n + 4);
+  std::vector<uint8_t> emeta(m + 1);
+  std::vector<uint64_t> pdinv(n + 1, PDINV_SKIP);
+  std::vector<uint64_t> hdr(8);
   uint64_t perms = 0, hashes = 0, inl = 0, longb = 0;
-  if (early) {
-    T.lf_eref = eref.data();
-    T.lf_emeta = emeta.data();
-    for (uint64_t i = 0; i < m; ++i) {
-      Key4 k = load_key(T.skey, i);
-      const uint8_t* vp = T.vals + T.svoff[i];
-      uint32_t vlen = T.svlen[i];
-      int32_t pd = leaf_pd_early(T, i);
-      LeafGeom g = leaf_geom(k, pd, vlen, vlen == 1 ? *vp : 0);
-      if (g.L > LEAF_SHORT_MAX) {
-        emeta[i] = EMETA_LONG;
-        longb += (g.L + 7) & ~7u;
-        continue;
-      }
-      uint64_t buf[LEAF_WORDS + 1] = {};
-      BW w(buf, 1);
-      leaf_header(w, k, g, vlen);
-      w.bytes(vp, vlen);
-      w.flush();
-      uint32_t in1 = 0;
-      uint32_t p = leaf_hash_early(T, i, pd == (int32_t)depth0 - 1, buf, 1, g.L, &in1);
+  memcpy(kin.data(), keys, 32 * n);
+  T.lf_eref = eref.data();
+  T.lf_emeta = emeta.data();
+  T.pdinv = pdinv.data();
+  T.kin = kin.data();
+  T.svoff = nullptr;  // as on the device: no sorted spans in early builds
+  T.svlen = nullptr;
+  for (uint64_t i = 0; i < m; ++i) op_pd_scatter(T, i);
+  // the device reads whole aligned words around each span: replay on an 8-byte-aligned
+  // copy of the values with a zero word either side (host memory is not page-granular)
+  std::vector<uint64_t> vbuf(voff[n] / 8 + 3, 0);
+  memcpy((uint8_t*)vbuf.data() + 8, vals, voff[n]);
+  T.vals = (const uint8_t*)vbuf.data() + 8;
+  {
+    const uint32_t vmis = 0;
+    const uint64_t* vw = (const uint64_t*)T.vals;
+    for (uint64_t j = 0; j < n; ++j) {
+      uint32_t in1 = 0, lb = 0;
+      uint32_t p = op_leaf_in(T, j, vw, vmis, hdr.data(), 1, &in1, &lb);
       perms += p;
       hashes += p ? 1 : 0;
       inl += in1;
+      longb += lb;
     }
   }
   uint64_t C = 0;
