@@ -63,6 +63,9 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-cpu-batch", action="store_true", help="skip the all-core full-size CPU root")
     p.add_argument("--sharded", action="store_true", help="force the nibble-sharded RCCL path (any N)")
+    p.add_argument("--workload", choices=("state", "lists"), default="state",
+                   help="state: the BASELINE metric (default); lists: transactions roots (SURVEY §8 f4)")
+    p.add_argument("--blocks", type=int, default=10_000, help="lists: blocks per step")
     return p.parse_args()
 
 
@@ -237,6 +240,98 @@ def single(args):
     print(json.dumps(out), flush=True)
 
 
+def list_workload(nblk, seed=11):
+    """nblk blocks of 1..300 transactions (mean ~150) of 100..220 bytes each (signed
+    transactions), packed: (items uint8, item offsets uint64[n+1], block offsets uint64[nblk+1])."""
+    r = np.random.default_rng(seed)
+    cnt = r.integers(1, 301, nblk)
+    so = np.zeros(nblk + 1, np.uint64)
+    so[1:] = np.cumsum(cnt)
+    n = int(so[-1])
+    ln = r.integers(100, 221, n)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(ln)
+    items = r.integers(0, 256, int(off[-1]) + 64, dtype=np.uint8)
+    return items, off, so
+
+
+def lists(args):
+    """f4: every block's transactions root (MptListValidator.scala:15-46) for `--blocks`
+    blocks in one kh_dev_list_roots call (items already in HBM; rlp(i) keys made on the
+    device).  CPU legs: the batch builder over the same lists on all cores, and the
+    sequential khipu-faithful fold on a 200-block sample; every root is asserted equal."""
+    import torch
+    from khipu_amd.device import Ctx
+    ctx = Ctx(0)
+    items, off, so = list_workload(args.blocks)
+    n, nblk = int(so[-1]), len(so) - 1
+    d_items = torch.from_numpy(items).to("cuda:0")
+    d_off = torch.from_numpy(off.astype(np.int64)).to("cuda:0")
+    for _ in range(args.warmup):
+        ctx.list_roots(d_items, d_off, so)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        roots, st = ctx.list_roots(d_items, d_off, so)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    s = st.as_dict()
+    perms_leaf = s["n_leaves"]
+    leaf_ms = s["t_leaf_ms"]
+    achieved = perms_leaf * OPS_PER_PERM / max(leaf_ms * 1e-3, 1e-12)
+    out = {
+        "metric": "list-roots/sec (transactions roots, rlp(i) keys)", "value": nblk / dt, "unit": "roots/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic (1..300 transactions of 100..220 random bytes per block)",
+        "config": {"workload": f"{nblk} blocks, {n} transactions -> one transactions root per block",
+                   "blocks": nblk, "items": n, "parallelism": "single GPU"},
+        "items_per_s": n / dt, "node_hashes": s["n_node_hashes"], "device_ms_per_step": s["t_total_ms"],
+        "stage_ms": {k: s[k] for k in ("t_keys_ms", "t_sort_ms", "t_topo_ms", "t_leaf_ms", "t_branch_ms")},
+        "roofline": {"kernel": "k_leaf_prep+k_leaf_hash", "bound": "valu", "achieved": achieved / 1e12,
+                     "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "T int32-lane-ops/s",
+                     "frac": achieved / VALU_PEAK_LANE_OPS, "traffic": None,
+                     "note": "leaf stage priced on one permutation per leaf (long leaves take two)"},
+    }
+    if not args.no_cpu:
+        from oracle import oracle
+        keys = []
+        for b in range(nblk):
+            keys += [oracle_list_key(i) for i in range(int(so[b + 1] - so[b]))]
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        t1 = time.perf_counter()
+        croots, _ = oracle.batch_roots(keys, (items, off), seg_off=so, nthreads=threads)
+        tb = time.perf_counter() - t1
+        assert croots == roots, "GPU list roots differ from the CPU batch builder"
+        sample = min(200, nblk)
+        t2 = time.perf_counter()
+        for b in range(sample):
+            t = oracle.Trie()
+            for i in range(int(so[b + 1] - so[b])):
+                j = int(so[b]) + i
+                t.put(oracle_list_key(i), items[int(off[j]):int(off[j + 1])].tobytes())
+            assert t.root_hash() == roots[b], f"block {b}: GPU root differs from the sequential fold"
+        ts = time.perf_counter() - t2
+        out["cpu_baseline"] = {"value": sample / ts, "unit": "roots/s", "cores": 1, "kind": "port",
+                               "sample": f"the first {sample} blocks of the same lists, sequential put of every "
+                                         f"item (MerklePatriciaTrie.put, MptListValidator.scala:30-46); "
+                                         f"{ts:.2f} s; every root asserted equal; CPU: {cpu_model()}"}
+        out["cpu_batch_allcore"] = {"value": nblk / tb, "unit": "roots/s", "cores": threads, "kind": "port",
+                                    "seconds": round(tb, 3), "roots_match": True,
+                                    "sample": "all blocks, independent batch builder (oracle/batch_root.cc)"}
+    print(json.dumps(out), flush=True)
+
+
+def oracle_list_key(i):
+    """rlp.encode(i: Int) (RLP.scala integer encoding): 0 -> 0x80, 1..127 the byte, else 0x80+len, BE bytes."""
+    if i == 0:
+        return b"\x80"
+    if i < 0x80:
+        return bytes([i])
+    b = i.to_bytes((i.bit_length() + 7) // 8, "big")
+    return bytes([0x80 + len(b)]) + b
+
+
 def relaunch(args):
     """`bench.py --gpus N` without a launcher: start torch.distributed.run as a child (no
     GPU call has been made in this process) and exit with its status."""
@@ -256,7 +351,9 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 or args.gpus > 1 or args.sharded:
+    if args.workload == "lists":
+        lists(args)
+    elif world > 1 or args.gpus > 1 or args.sharded:
         from khipu_amd import sharded
         sharded.bench_main(args)
     else:

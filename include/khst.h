@@ -60,6 +60,7 @@ extern "C" {
 /* flags */
 #define KH_HASH_KEYS 0x1u   /* trie key = kec256(input key) */
 #define KH_EMIT_NODES 0x2u  /* resident tries: keep each commit's write-back set (kh_trie_emit_nodes) */
+typedef struct kh_ctx kh_ctx;
 #define KH_NO_TRIE 0xFFFFFFFFu  /* kh_block_commit: an account upsert without a storage trie */
 
 typedef struct kh_stats {
@@ -124,6 +125,12 @@ int kh_list_roots(const uint8_t* items, const uint64_t* off, const uint64_t* seg
 int kh_trie_root_sharded(const int* devices, int ngpus, const uint8_t* keys, uint32_t klen, const uint8_t* vals,
                          const uint64_t* voff, uint64_t n, uint32_t flags, uint8_t root32[32], kh_stats* stats);
 
+/* kh_list_roots with the items in HBM: d_off holds the offsets of every item of the call
+ * into d_items (item j at d_items[d_off[j] .. d_off[j+1]), j from h_seg_off[0]); the
+ * segment offsets are host memory. */
+int kh_dev_list_roots(kh_ctx* ctx, const uint8_t* d_items, const uint64_t* d_off, const uint64_t* h_seg_off,
+                      uint64_t nseg, uint8_t* roots32, kh_stats* stats);
+
 /* Root plus every node a fresh node store needs: each node reachable from the root
  * whose encoding is >= 32 B, plus the root node (MerklePatriciaTrie.scala:505-511).
  * Node j: hash hashes32[32j..), encoding rlp[off[j] .. off[j+1]) (off has n_nodes+1
@@ -136,7 +143,6 @@ int kh_trie_root_nodes(const uint8_t* keys, uint32_t klen, const uint8_t* vals, 
 /* ---- device-resident interface (inputs already in HBM; used by bench.py and the
  *      multi-GPU driver).  One context per device; a context is not shared across
  *      threads without external synchronisation. ---- */
-typedef struct kh_ctx kh_ctx;
 
 int kh_ctx_create(int device, kh_ctx** out);
 int kh_ctx_destroy(kh_ctx* ctx);

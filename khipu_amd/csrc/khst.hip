@@ -184,6 +184,63 @@ __global__ void __launch_bounds__(BS) k_tie_fix(const uint64_t* ck, uint64_t n, 
   if (dup) atomicOr(flags, 2ULL);
 }
 
+// Unsegmented plain builds sort (first key word, index) pairs only; runs of equal top-32
+// bits are ordered here by the whole key (the first word, then the input key through its
+// index), stable, and the sorted keys are gathered later, beside the leaf kernel.
+__device__ __forceinline__ bool ck_less(uint64_t a, uint64_t b, const uint64_t* K, uint32_t ia, uint32_t ib) {
+  if (a != b) return a < b;
+  return key_less(K + 4ull * ia, K + 4ull * ib);
+}
+__device__ __forceinline__ bool ck_equal(uint64_t a, uint64_t b, const uint64_t* K, uint32_t ia, uint32_t ib) {
+  if (a != b) return false;
+  const uint64_t* x = K + 4ull * ia;
+  const uint64_t* y = K + 4ull * ib;
+  return x[1] == y[1] && x[2] == y[2] && x[3] == y[3];
+}
+__global__ void __launch_bounds__(BS) k_tie_fix_ck(uint64_t* ck, uint32_t* idx, uint64_t n, const uint64_t* K,
+                                                   unsigned long long* flags) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i + 1 >= n) return;
+  uint32_t hi = (uint32_t)(ck[i] >> 32);
+  if ((uint32_t)(ck[i + 1] >> 32) != hi) return;
+  if (i > 0 && (uint32_t)(ck[i - 1] >> 32) == hi) return;
+  uint64_t e = i + 1;
+  while (e < n && (uint32_t)(ck[e] >> 32) == hi && e - i <= TIE_RUN_MAX) ++e;
+  if (e - i > TIE_RUN_MAX) {
+    atomicOr(flags, 1ULL);
+    return;
+  }
+  for (uint64_t a = i + 1; a < e; ++a) {
+    const uint64_t c = ck[a];
+    const uint32_t ix = idx[a];
+    uint64_t b = a;
+    while (b > i && ck_less(c, ck[b - 1], K, ix, idx[b - 1])) {
+      ck[b] = ck[b - 1];
+      idx[b] = idx[b - 1];
+      --b;
+    }
+    ck[b] = c;
+    idx[b] = ix;
+  }
+  bool dup = false;
+  for (uint64_t a = i + 1; a < e; ++a) dup |= ck_equal(ck[a - 1], ck[a], K, idx[a - 1], idx[a]);
+  if (dup) atomicOr(flags, 2ULL);
+}
+__global__ void __launch_bounds__(BS) k_dup_ck(const uint64_t* ck, const uint32_t* idx, const uint64_t* K, uint64_t n,
+                                               uint32_t* keep) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  keep[i] = (i + 1 < n && ck_equal(ck[i], ck[i + 1], K, idx[i], idx[i + 1])) ? 0u : 1u;
+}
+__global__ void __launch_bounds__(BS) k_compact_ck(const uint64_t* ck, const uint32_t* idx, const uint32_t* keep_pos,
+                                                   const uint32_t* keep, uint64_t n, uint64_t* ock, uint32_t* oidx) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n || !keep[i]) return;
+  const uint32_t p = keep_pos[i];
+  ock[p] = ck[i];
+  oidx[p] = idx[i];
+}
+
 // 32-byte keys move as two 16-byte vectors, both loads issued before any store
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void copy_key(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst) {
@@ -983,7 +1040,9 @@ struct SortIO {
   unsigned long long* ctr;
   const uint8_t* kn;  // variable-length keys: nibble counts (input order; nullable)
   bool ck_ready = false;  // ck0/idx0 already hold the unsegmented sort keys (k_hash_keys_ck)
+  bool ck_path = false;   // unsegmented plain build: sort (ck, idx) only, gather the keys later
   // out
+  const uint64_t* sck = nullptr;  // ck_path: the sorted first key words (skey not gathered yet)
   uint64_t m;
   uint32_t* sidx;
   bool fallback;
@@ -1015,6 +1074,43 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
   uint64_t* cks = flip ? ck1 : ck0;
   uint32_t* idxs = flip ? idx1 : idx0;
   LAUNCH_CHECK();
+  if (S.ck_path) {
+    hipLaunchKernelGGL(k_tie_fix_ck, GRID(n, BS), dim3(BS), 0, st, cks, idxs, n, (const uint64_t*)K32, T.ctr + CTR_TIE);
+    LAUNCH_CHECK();
+    HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint64_t tf = c->h_pinned[0];
+    if (!(tf & 1)) {  // no long run: keys stay ungathered
+      uint64_t m = n;
+      uint64_t* ock = cks;
+      uint32_t* oidx = idxs;
+      if (tf & 2) {  // keep the last of equal keys
+        uint32_t* keep = (uint32_t*)(cks == ck0 ? ck1 : ck0);
+        uint32_t* keep_pos = idxs == idx0 ? idx1 : idx0;
+        hipLaunchKernelGGL(k_dup_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, (const uint32_t*)idxs,
+                           (const uint64_t*)K32, n, keep);
+        LAUNCH_CHECK();
+        uint32_t* mtot = (uint32_t*)(T.ctr + CTR_M);
+        scan_exclusive<uint32_t>(keep, keep_pos, n, mtot, scan_scratch, st);
+        HIPCHK(hipMemcpyAsync(c->h_pinned, mtot, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        m = (uint32_t)c->h_pinned[0];
+        c->ws3.ensure(carve_size({n * 8, n * 4}));
+        Carver c3{(char*)c->ws3.p, 0, c->ws3.cap};
+        ock = c3.take<uint64_t>(n);
+        oidx = c3.take<uint32_t>(n);
+        hipLaunchKernelGGL(k_compact_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, (const uint32_t*)idxs,
+                           (const uint32_t*)keep_pos, (const uint32_t*)keep, n, ock, oidx);
+        LAUNCH_CHECK();
+      }
+      S.m = m;
+      S.sidx = oidx;
+      S.sck = ock;
+      S.fallback = false;
+      return;
+    }
+    // a run longer than TIE_RUN_MAX: the general path below (full sort from the input order)
+  }
   hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, (const uint32_t*)idxs, n,
                      skey, sseg);
   LAUNCH_CHECK();
@@ -1236,12 +1332,14 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   {
     SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr,
              A.kn, ck_ready};
+    S.ck_path = early && !segmented && !A.kn;
     sort_dedup(c, S);
     m = S.m;
     sidx = S.sidx;
     skey = S.skey;
     sseg = S.sseg;
     fallback = S.fallback;
+    T.sck = S.sck;  // non-null: the sorted keys are gathered beside the leaf kernel (below)
   }
   const bool ties = fallback;
   T.m = m;
@@ -1306,6 +1404,11 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, c->st2, T, n);
     LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[10], c->st2));
+  }
+  if (T.sck) {  // the sorted keys (leaf publish, extensions), off the critical path
+    hipLaunchKernelGGL(k_gather, GRID(m, BS), dim3(BS), 0, st, (const uint64_t*)K32, (const uint32_t*)nullptr,
+                       (const uint32_t*)sidx, m, skey, (uint32_t*)nullptr);
+    LAUNCH_CHECK();
   }
   if (nb > 0) {
     P.lv[0] = T.u;
@@ -1588,6 +1691,20 @@ __global__ void __launch_bounds__(BS) k_list_keys(const uint32_t* seg, const uin
   K32[4 * i] = w;
   K32[4 * i + 1] = K32[4 * i + 2] = K32[4 * i + 3] = 0;
   kn[i] = (uint8_t)(2 * nb);
+}
+
+// per-item segment id from device segment offsets (binary search; item i of the call is
+// input seg_off[0] + i)
+__global__ void __launch_bounds__(BS) k_seg_ids(const uint64_t* seg_off, uint64_t nseg, uint64_t n, uint32_t* seg) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t x = seg_off[0] + i;
+  uint64_t lo = 0, hi = nseg;  // last s with seg_off[s] <= x
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (seg_off[mid] <= x) lo = mid; else hi = mid;
+  }
+  seg[i] = (uint32_t)lo;
 }
 
 static std::vector<uint32_t> seg_ids(const uint64_t* seg_off, uint64_t nseg) {
@@ -2584,6 +2701,40 @@ int kh_list_roots(const uint8_t* items, const uint64_t* off, const uint64_t* seg
                        (uint64_t*)c->in_keys.p, (uint8_t*)c->in_kn.p);
     LAUNCH_CHECK();
     BuildArgs A{(const uint8_t*)c->in_keys.p, 32, S.vals, S.voff, n, nseg > 1 ? S.seg : nullptr, nseg, 0, 0, false};
+    A.kn = (const uint8_t*)c->in_kn.p;
+    BuildOut O;
+    run_build(c, A, O, stats);
+    for (uint64_t s = 0; s < nseg; ++s) copy_root(O, s, roots32 + 32 * s);
+  })
+}
+
+// kh_list_roots with the items already in HBM (d_off: n + 1 offsets into d_items of the
+// n = h_seg_off[nseg] - h_seg_off[0] items; the segment offsets on the host)
+int kh_dev_list_roots(kh_ctx* c, const uint8_t* d_items, const uint64_t* d_off, const uint64_t* h_seg_off,
+                      uint64_t nseg, uint8_t* roots32, kh_stats* stats) {
+  if (!c) return set_err(KH_EINVAL, "null context");
+  API_TRY({
+    if (nseg == 0) return KH_OK;
+    HIPCHK(hipSetDevice(c->dev));
+    const uint64_t n = h_seg_off[nseg] - h_seg_off[0];
+    if (stats) memset(stats, 0, sizeof(*stats));
+    if (n == 0) {
+      for (uint64_t s = 0; s < nseg; ++s) memcpy(roots32 + 32 * s, EMPTY_TRIE_HASH, 32);
+      return KH_OK;
+    }
+    hipStream_t st = c->st;
+    c->in_aux.ensure((nseg + 1) * 8 + 64);
+    c->in_seg.ensure(n * 4 + 64);
+    c->in_kn.ensure(n + 64);
+    c->in_keys.ensure(n * 32 + 64);
+    HIPCHK(hipMemcpyAsync(c->in_aux.p, h_seg_off, (nseg + 1) * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_seg_ids, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)c->in_aux.p, nseg, n,
+                       (uint32_t*)c->in_seg.p);
+    hipLaunchKernelGGL(k_list_keys, GRID(n, BS), dim3(BS), 0, st, (const uint32_t*)c->in_seg.p,
+                       (const uint64_t*)c->in_aux.p, n, (uint64_t*)c->in_keys.p, (uint8_t*)c->in_kn.p);
+    LAUNCH_CHECK();
+    BuildArgs A{(const uint8_t*)c->in_keys.p, 32, d_items, d_off + h_seg_off[0], n,
+                nseg > 1 ? (const uint32_t*)c->in_seg.p : nullptr, nseg, 0, 0, false};
     A.kn = (const uint8_t*)c->in_kn.p;
     BuildOut O;
     run_build(c, A, O, stats);

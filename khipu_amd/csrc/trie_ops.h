@@ -154,6 +154,8 @@ struct Topo {
   const uint32_t* sidx;   // [m] input index of sorted key i
   const uint32_t* sseg;   // [m] segment id (segmented only)
   const uint8_t* kn;      // [m] key length in nibbles (variable-length key builds; nullable: 64)
+  const uint64_t* sck;    // [m] sorted big-endian first key words (unsegmented plain builds; nullable):
+                          //     boundary values come from them before the sorted keys are gathered
   const uint8_t* vals;    // input values
   const uint64_t* voff;   // [n+1] (or [n] offsets with vlen_in)
   const uint32_t* vlen_in; // [n] value lengths (nullable: voff[i+1] - voff[i])
@@ -299,8 +301,13 @@ KH_HD uint32_t ext_enc_len(uint32_t e, uint32_t brl) {
 
 // ---- stage: boundary values
 KH_HD void op_lcp(const Topo& T, uint64_t b) {
-  Key4 a = load_key(T.skey, b), c = load_key(T.skey, b + 1);
-  int l = lcp_nibbles(a, c);
+  int l;
+  if (T.sck) {  // the first 16 nibbles from the sorted prefixes; the input keys only past them
+    const uint64_t x = T.sck[b] ^ T.sck[b + 1];
+    l = x ? (int)(clz64(x) >> 2) : lcp_nibbles(load_key(T.kin, T.sidx[b]), load_key(T.kin, T.sidx[b + 1]));
+  } else {
+    l = lcp_nibbles(load_key(T.skey, b), load_key(T.skey, b + 1));
+  }
   if (T.kn) {  // padded keys: the common prefix ends with the shorter key
     if (l > (int)T.kn[b]) l = T.kn[b];
     if (l > (int)T.kn[b + 1]) l = T.kn[b + 1];

@@ -74,6 +74,18 @@ class Ctx:
                                       flags, hh.ctypes.data, ll.ctypes.data, ii.ctypes.data, ctypes.byref(st)))
         return hh.reshape(nres, 32), ll, ii.reshape(nres, 32), st
 
+    def list_roots(self, items, off, seg_off):
+        """kh_dev_list_roots: items / off (n + 1 int64 offsets) device tensors, seg_off host
+        (numpy uint64, nseg + 1).  Returns (list of 32-byte roots, KhStats)."""
+        so = np.ascontiguousarray(seg_off, dtype=np.uint64)
+        nseg = len(so) - 1
+        out = np.zeros(32 * max(nseg, 1), np.uint8)
+        st = KhStats()
+        self._sync()
+        check(lib().kh_dev_list_roots(self.h, _ptr(items), _ptr(off), so.ctypes.data, nseg, out.ctypes.data,
+                                      ctypes.byref(st)))
+        return [out[32 * i:32 * i + 32].tobytes() for i in range(nseg)], st
+
 
 def fold_root16(hash32x16, len16, inline32x16):
     """Root over 16 capped top-nibble references (kh_fold_root16)."""

@@ -110,6 +110,15 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   uint64_t B = 0;
   std::vector<std::vector<uint8_t>> pyr;
   Pyr P{};
+  // unsegmented builds take the device's ck path: boundary values from the sorted first
+  // key words (the input keys past them), before the sorted keys are used
+  std::vector<uint64_t> kin(4 * n + 4), sck(m + 1);
+  memcpy(kin.data(), keys, 32 * n);
+  T.kin = kin.data();
+  if (!segmented) {
+    for (uint64_t i = 0; i < m; ++i) sck[i] = bswap64(skey[4 * i]);
+    T.sck = sck.data();
+  }
   if (nb > 0) {
     for (uint64_t b = 0; b < nb; ++b) op_lcp(T, b);
     P.lv[0] = T.u;
@@ -147,16 +156,14 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   // order (k_pd_scatter), leaves hashed in input order (k_leaf_in), references stashed
   // per input and published after the topology (k_leaf_topo_early)
   const bool early = true;
-  std::vector<uint64_t> eref(4 * m + 4), kin(4 * n + 4);
+  std::vector<uint64_t> eref(4 * m + 4);
   std::vector<uint8_t> emeta(m + 1);
   std::vector<uint64_t> pdinv(n + 1, PDINV_SKIP);
   std::vector<uint64_t> hdr(8);
   uint64_t perms = 0, hashes = 0, inl = 0, longb = 0;
-  memcpy(kin.data(), keys, 32 * n);
   T.lf_eref = eref.data();
   T.lf_emeta = emeta.data();
   T.pdinv = pdinv.data();
-  T.kin = kin.data();
   T.svoff = nullptr;  // as on the device: no sorted spans in early builds
   T.svlen = nullptr;
   for (uint64_t i = 0; i < m; ++i) op_pd_scatter(T, i);

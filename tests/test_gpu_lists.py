@@ -132,3 +132,29 @@ def test_varkeys_rejects_long_keys():
     from khipu_amd._lib import MPTException
     with pytest.raises(MPTException):
         trie_roots_varkeys([([bytes(33)], [b"x"])])
+
+
+def test_dev_list_roots_matches_host(oracle):
+    """kh_dev_list_roots (items in HBM, segment ids and rlp(i) keys made on the device)
+    against the host entry point and the oracle, including empty lists and a sub-range of
+    the item offsets (seg_off[0] > 0)."""
+    import numpy as np
+    import torch
+    import bench
+    from khipu_amd.device import Ctx
+    from khipu_amd.trie import list_roots
+    items, off, so = bench.list_workload(60, seed=3)
+    so[5] = so[4]  # an empty list
+    so[6] = so[4]
+    lists = [[items[int(off[j]):int(off[j + 1])].tobytes() for j in range(int(so[b]), int(so[b + 1]))]
+             for b in range(len(so) - 1)]
+    ctx = Ctx(0)
+    d_items = torch.from_numpy(items).to("cuda:0")
+    d_off = torch.from_numpy(off.astype(np.int64)).to("cuda:0")
+    got, st = ctx.list_roots(d_items, d_off, so)
+    assert got == list_roots(lists)
+    for b in (0, 4, 5, 17, 59):
+        exp = _seq_root(oracle, [C.list_key(i) for i in range(len(lists[b]))], lists[b]) if lists[b] else EMPTY
+        assert got[b] == exp, b
+    sub, _ = ctx.list_roots(d_items, d_off, so[10:21])
+    assert sub == got[10:20]
