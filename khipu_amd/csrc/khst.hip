@@ -583,6 +583,7 @@ __global__ void __launch_bounds__(BS) k_branch_hash(Topo T, uint64_t first, uint
 // HBM: the level reads its contiguous child records once and writes one 34-byte
 // reference per node.  Slot layout [thread][word]: a wave's 8-byte slot accesses are
 // bank-conflict-free within each 16-lane group (stride 34 dwords).
+template <bool VARKEYS>
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8))) k_branch_fused(Topo T, uint64_t first, uint64_t cnt) {
   __shared__ uint64_t slots[BS * LEAF_WORDS];
   uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -590,7 +591,10 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8)))
   if (t < cnt) {
     uint32_t j = (uint32_t)(first + t);
     uint32_t in1 = 0;
-    perms = op_branch_fused(T, j, slots + threadIdx.x * LEAF_WORDS, 1, &in1);
+    // fixed-length keys: direct window assembly; variable-length keys (branch values):
+    // the byte stream through the windowed writer
+    perms = VARKEYS ? op_branch_fused(T, j, slots + threadIdx.x * LEAF_WORDS, 1, &in1)
+                    : op_branch_direct(T, j, slots + threadIdx.x * LEAF_WORDS, 1, &in1);
     hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
   }
@@ -1544,7 +1548,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     } else if (coop) {
       hipLaunchKernelGGL(k_branch_coop, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     } else {
-      hipLaunchKernelGGL(k_branch_fused, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+      if (A.kn)
+        hipLaunchKernelGGL(k_branch_fused<true>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+      else
+        hipLaunchKernelGGL(k_branch_fused<false>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     }
     LAUNCH_CHECK();
     ++levels;

@@ -1186,6 +1186,114 @@ KH_HD uint32_t op_branch_fused(const Topo& T, uint32_t j, uint64_t* slot, uint64
   return perms;
 }
 
+// ---- N1 lane variant with direct window assembly (fixed-length keys: no branch values).
+// Every empty slot and the terminator of a branch encoding are 0x80, so a 136-byte window
+// is prefilled with 0x80 over the encoding's bytes and the list header and each child
+// item are XOR-placed at their byte offsets: item c starts at hdr + nibble_c + the running
+// sum of (item length - 1) over the children before it.  Per window only the children
+// overlapping it are loaded and placed; no byte-serial stream.
+KH_HD void window_place(uint64_t* slot, uint64_t stride, uint32_t w0, uint32_t off, uint32_t ilen,
+                        const uint64_t I[5]) {
+  const uint32_t sh = off & 7, wfirst = off >> 3;
+#pragma unroll
+  for (uint32_t q = 0; q < 6; ++q) {
+    const uint64_t cur = q < 5 ? I[q] : 0, prv = q ? I[q - 1] : 0;
+    const uint64_t y = sh ? (cur << (8 * sh)) | (prv >> (64 - 8 * sh)) : cur;
+    const uint32_t W = wfirst + q;  // absolute word of the encoding
+    const int32_t lo = (int32_t)off - 8 * (int32_t)W, hi = (int32_t)(off + ilen) - 8 * (int32_t)W;
+    const uint32_t blo = lo > 0 ? (uint32_t)lo : 0, bhi = hi < 8 ? (hi > 0 ? (uint32_t)hi : 0) : 8;
+    if (bhi <= blo || W < w0 / 8 || W >= w0 / 8 + 17) continue;
+    const uint64_t m = low_bytes_mask(bhi) & ~low_bytes_mask(blo);
+    slot[(W - w0 / 8) * stride] ^= (y ^ 0x8080808080808080ULL) & m;
+  }
+}
+KH_HD uint32_t op_branch_direct(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl) {
+  const uint32_t ext = T.br_ext[j];
+  const bool top = T.br_parent[j] == NONE;
+  *inl = 0;
+  uint64_t hb[4] = {0, 0, 0, 0}, bhead[4] = {0, 0, 0, 0};
+  uint32_t L, perms = 0, ninl = 0;
+  {
+    const uint32_t k = T.br_k[j];
+    const uint64_t cb = T.br_cbase[j];
+    const uint16_t* cm = T.cmeta + cb;
+    const uint64_t* cr = T.cref + 4 * cb;
+    const uint32_t payload = branch_payload(T, j);
+    const uint32_t hh = rlp_hdr_len(payload);
+    L = hh + payload;
+    T.br_len[j] = L;
+    const bool hashit = L >= 32 || (top && ext == 0);
+    const uint32_t nfull = L / 136;
+    KState S = {};
+    for (uint32_t b = 0; b <= nfull; ++b) {
+      const uint32_t w0 = 136u * b;
+#pragma unroll
+      for (int q = 0; q < 17; ++q) {  // 0x80 over the encoding's bytes of this window
+        const uint32_t a = w0 + 8u * (uint32_t)q;
+        const uint32_t n80 = L > a ? (L - a < 8 ? L - a : 8) : 0;
+        slot[q * stride] = low_bytes_mask(n80) & 0x8080808080808080ULL;
+      }
+      if (b == 0) {  // the list header
+        const uint32_t pl = payload;
+        const uint64_t hdr = hh == 1 ? (0xC0 + pl)
+                             : hh == 2 ? (0xF8 | ((uint64_t)pl << 8))
+                                       : (0xF9 | ((uint64_t)(pl >> 8) << 8) | ((uint64_t)(pl & 0xFF) << 16));
+        slot[0] ^= (hdr ^ 0x8080808080808080ULL) & low_bytes_mask(hh);
+      }
+      uint32_t run = 0;  // sum of (item length - 1) over the children placed so far
+      for (uint32_t c = 0; c < k; ++c) {
+        const uint32_t mc = cm[c], len = mc & 0xFF, ilen = len == 32 ? 33 : len;
+        const uint32_t off = hh + (mc >> 8) + run;
+        run += ilen - 1;
+        if (off + ilen <= w0) continue;
+        if (off >= w0 + 136) break;
+        const uint64_t r0 = cr[4 * c], r1 = cr[4 * c + 1], r2 = cr[4 * c + 2], r3 = cr[4 * c + 3];
+        uint64_t I[5];
+        if (len == 32) {
+          I[0] = 0xA0 | (r0 << 8);
+          I[1] = (r0 >> 56) | (r1 << 8);
+          I[2] = (r1 >> 56) | (r2 << 8);
+          I[3] = (r2 >> 56) | (r3 << 8);
+          I[4] = r3 >> 56;
+        } else {  // an embedded child: its bytes (the capped reference is zero past len)
+          I[0] = r0;
+          I[1] = r1;
+          I[2] = r2;
+          I[3] = r3;
+          I[4] = 0;
+        }
+        window_place(slot, stride, w0, off, ilen, I);
+      }
+      if (!hashit) break;  // embedded in its parent: never hashed (Node.scala:114)
+      const uint32_t rem = b < nfull ? 136 : L - 136 * nfull;
+#pragma unroll
+      for (int q = 0; q < 17; ++q) {
+        uint64_t x = slot[q * stride];  // zero past the encoding already
+        if (b == nfull) {
+          if ((rem >> 3) == (uint32_t)q) x ^= 0x01ULL << (8 * (rem & 7));
+          if (q == 16) x ^= 0x80ULL << 56;
+        }
+        kxor(S, q, x);
+      }
+      keccakf(S);
+    }
+    if (hashit) {
+      for (int q = 0; q < 4; ++q) hb[q] = lane(S, q);
+      perms = nfull + 1;
+    }
+    if (L < 32)
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t base = 8u * (uint32_t)q;
+        bhead[q] = base < L ? slot[q * stride] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0;
+      }
+    ninl = hashit ? 0 : 1;
+    branch_keep(T, j, L, hb, bhead);
+  }
+  perms += branch_publish(T, j, L, hb, bhead, Slot{slot, stride}, &ninl);
+  *inl = ninl;
+  return perms;
+}
+
 // node hashes op_branch_hash(T, j, ...) spent `perms` on: the branch if it was
 // re-encoded and its encoding is >= 32 B or it is the top; its extension likewise
 // (an extension is re-encoded only when perms were spent on it or its branch)

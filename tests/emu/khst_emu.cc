@@ -239,7 +239,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       uint32_t j = lorder[g];
       uint32_t in1 = 0;
       uint64_t slot[LEAF_WORDS + 1];
-      uint32_t p = op_branch_fused(T, j, slot, 1, &in1);
+      uint32_t p = T.kn ? op_branch_fused(T, j, slot, 1, &in1) : op_branch_direct(T, j, slot, 1, &in1);
       perms += p;
       hashes += branch_hash_count(T, j, p);
       inl += in1;
