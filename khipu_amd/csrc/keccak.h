@@ -190,6 +190,30 @@ KH_HD void kec256_msg(const uint8_t* p, uint32_t len, uint64_t out[4]) {
   out[3] = lane(s, 3);
 }
 
+// kec256 of a message shorter than one block (len <= 135) at any alignment: one
+// permutation, no block loop (fewer live registers than kec256_msg's general form)
+KH_HD void kec256_short(const uint8_t* p, uint32_t len, uint64_t out[4]) {
+  KState s = {};
+#pragma unroll
+  for (int i = 0; i < 17; ++i) {
+    uint64_t w = 0;
+    const uint32_t base = 8u * (uint32_t)i;
+    if (base < len) {
+      const uint32_t nb = len - base < 8 ? len - base : 8;
+      w = load64u_n(p + base, nb) & low_bytes_mask(nb);
+    }
+    if ((len >> 3) == (uint32_t)i) w ^= 0x01ULL << (8 * (len & 7));
+    if (i == 16) w ^= 0x80ULL << 56;
+    s.lo[i] = (uint32_t)w;
+    s.hi[i] = (uint32_t)(w >> 32);
+  }
+  keccakf(s);
+  out[0] = lane(s, 0);
+  out[1] = lane(s, 1);
+  out[2] = lane(s, 2);
+  out[3] = lane(s, 3);
+}
+
 KH_HD uint32_t perms_for_len(uint32_t len) { return len / 136 + 1; }
 
 }  // namespace khst

@@ -98,22 +98,30 @@ __global__ void __launch_bounds__(BS) k_verify_nodes(const uint8_t* data, const 
   status[i] = op_node_children(data + o, len, kind, child32 + 512 * i, child_kind + 16 * i, nchild + i);
 }
 
+template <bool SHORT>
 __global__ void __launch_bounds__(BS) k_hash_keys(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
   uint64_t h[4];
-  kec256_msg<false>(keys + i * klen, klen, h);
+  if (SHORT)
+    kec256_short(keys + i * klen, klen, h);
+  else
+    kec256_msg<false>(keys + i * klen, klen, h);
   for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
 }
 
 // ... and the unsegmented sort key (the key's leading 64 bits, big-endian) with the
 // identity index in the same pass (saves k_make_ck's re-read of the keys)
+template <bool SHORT>
 __global__ void __launch_bounds__(BS) k_hash_keys_ck(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out,
                                                      uint64_t* ck, uint32_t* idx) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
   uint64_t h[4];
-  kec256_msg<false>(keys + i * klen, klen, h);
+  if (SHORT)  // keys of <= 135 bytes (addresses, slot words): one block
+    kec256_short(keys + i * klen, klen, h);
+  else
+    kec256_msg<false>(keys + i * klen, klen, h);
   for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
   ck[i] = bswap64(h[0]);
   idx[i] = (uint32_t)i;
@@ -1319,10 +1327,16 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // ---- 1. keys
   const bool ck_ready = (A.flags & KH_HASH_KEYS) && !segmented;
   if (ck_ready) {
-    hipLaunchKernelGGL(k_hash_keys_ck, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, ck0, idx0);
+    if (A.klen <= 135)
+      hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, ck0, idx0);
+    else
+      hipLaunchKernelGGL(k_hash_keys_ck<false>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, ck0, idx0);
     LAUNCH_CHECK();
   } else if (A.flags & KH_HASH_KEYS) {
-    hipLaunchKernelGGL(k_hash_keys, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32);
+    if (A.klen <= 135)
+      hipLaunchKernelGGL(k_hash_keys<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32);
+    else
+      hipLaunchKernelGGL(k_hash_keys<false>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32);
     LAUNCH_CHECK();
   } else if (own_keys) {
     HIPCHK(hipMemcpyAsync(K32, A.keys, n * 32, hipMemcpyDeviceToDevice, st));
@@ -2298,9 +2312,17 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   uint32_t* ur = cv.take<uint32_t>(nops);
   HIPCHK(hipMemsetAsync(S.ctr, 0, CTR_N * 8, st));
   if (h->flags & KH_HASH_KEYS) {
-    if (F.nup) hipLaunchKernelGGL(k_hash_keys, GRID(F.nup, BS), dim3(BS), 0, st, F.up_keys, F.klen, F.nup, K);
+    if (F.nup) {
+      if (F.klen <= 135)
+        hipLaunchKernelGGL(k_hash_keys<true>, GRID(F.nup, BS), dim3(BS), 0, st, F.up_keys, F.klen, F.nup, K);
+      else
+        hipLaunchKernelGGL(k_hash_keys<false>, GRID(F.nup, BS), dim3(BS), 0, st, F.up_keys, F.klen, F.nup, K);
+    }
     if (F.ndel)
-      hipLaunchKernelGGL(k_hash_keys, GRID(F.ndel, BS), dim3(BS), 0, st, F.del_keys, F.klen, F.ndel, K + 4 * F.nup);
+      if (F.klen <= 135)
+        hipLaunchKernelGGL(k_hash_keys<true>, GRID(F.ndel, BS), dim3(BS), 0, st, F.del_keys, F.klen, F.ndel, K + 4 * F.nup);
+      else
+        hipLaunchKernelGGL(k_hash_keys<false>, GRID(F.ndel, BS), dim3(BS), 0, st, F.del_keys, F.klen, F.ndel, K + 4 * F.nup);
     LAUNCH_CHECK();
   } else {
     if (F.nup) HIPCHK(hipMemcpyAsync(K, F.up_keys, F.nup * 32, hipMemcpyDeviceToDevice, st));
@@ -2942,7 +2964,10 @@ int kh_dev_hash_keys(kh_ctx* c, const uint8_t* d_keys, uint32_t klen, uint64_t n
   API_TRY({
     HIPCHK(hipSetDevice(c->dev));
     if (n) {
-      hipLaunchKernelGGL(k_hash_keys, GRID(n, BS), dim3(BS), 0, c->st, d_keys, klen, n, (uint64_t*)d_out32);
+      if (klen <= 135)
+        hipLaunchKernelGGL(k_hash_keys<true>, GRID(n, BS), dim3(BS), 0, c->st, d_keys, klen, n, (uint64_t*)d_out32);
+      else
+        hipLaunchKernelGGL(k_hash_keys<false>, GRID(n, BS), dim3(BS), 0, c->st, d_keys, klen, n, (uint64_t*)d_out32);
       LAUNCH_CHECK();
     }
   })

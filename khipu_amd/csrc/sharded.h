@@ -152,7 +152,10 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
     const uint8_t* K = in.keys;
     if (flags & KH_HASH_KEYS) {
       s.k32.ensure(s.n * 32 + 64);
-      hipLaunchKernelGGL(k_hash_keys, GRID(s.n, BS), dim3(BS), 0, c->st, in.keys, klen, s.n, (uint64_t*)s.k32.p);
+      if (klen <= 135)
+        hipLaunchKernelGGL(k_hash_keys<true>, GRID(s.n, BS), dim3(BS), 0, c->st, in.keys, klen, s.n, (uint64_t*)s.k32.p);
+      else
+        hipLaunchKernelGGL(k_hash_keys<false>, GRID(s.n, BS), dim3(BS), 0, c->st, in.keys, klen, s.n, (uint64_t*)s.k32.p);
       LAUNCH_CHECK();
       K = (const uint8_t*)s.k32.p;
     }
