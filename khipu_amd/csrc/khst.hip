@@ -2318,11 +2318,12 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
       else
         hipLaunchKernelGGL(k_hash_keys<false>, GRID(F.nup, BS), dim3(BS), 0, st, F.up_keys, F.klen, F.nup, K);
     }
-    if (F.ndel)
+    if (F.ndel) {
       if (F.klen <= 135)
         hipLaunchKernelGGL(k_hash_keys<true>, GRID(F.ndel, BS), dim3(BS), 0, st, F.del_keys, F.klen, F.ndel, K + 4 * F.nup);
       else
         hipLaunchKernelGGL(k_hash_keys<false>, GRID(F.ndel, BS), dim3(BS), 0, st, F.del_keys, F.klen, F.ndel, K + 4 * F.nup);
+    }
     LAUNCH_CHECK();
   } else {
     if (F.nup) HIPCHK(hipMemcpyAsync(K, F.up_keys, F.nup * 32, hipMemcpyDeviceToDevice, st));
