@@ -244,7 +244,9 @@ int kh_trie_apply_host(kh_trie* h, const uint8_t* up_keys, const uint8_t* up_val
                        uint64_t nup, const uint8_t* del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
                        uint8_t root32[32], kh_stats* stats);
 
-/* A forest of tries (empty).  Each op names its trie (any uint32 id).  After a commit,
+/* A forest of tries (empty).  ctx NULL: the shared context of the current device, the one
+ * the *_host entry points use (so kh_block_commit_host can pair it with a trie opened by
+ * kh_trie_open_host).  Each op names its trie (any uint32 id).  After a commit,
  * h_tries / h_roots32 receive the touched tries (ascending ids) and their new roots
  * (EMPTY_TRIE_HASH for a trie left empty); KH_ENOSPC with *n_tries when cap is short. */
 int kh_forest_open(kh_ctx* ctx, uint32_t flags, kh_trie** out);

@@ -3331,8 +3331,11 @@ int kh_trie_apply_host(kh_trie* h, const uint8_t* up_keys, const uint8_t* up_val
 }
 
 int kh_forest_open(kh_ctx* c, uint32_t flags, kh_trie** out) {
-  if (!c || !out) return set_err(KH_EINVAL, "null context or handle");
-  API_TRY({ *out = trie_new(c, flags, true); })
+  if (!out) return set_err(KH_EINVAL, "null handle");
+  API_TRY({
+    if (!c) c = shared_ctx(current_device());  // the context the *_host entry points use
+    *out = trie_new(c, flags, true);
+  })
 }
 
 static int forest_out(kh_trie* f, uint32_t* h_tries, uint8_t* h_roots32, uint64_t cap, uint64_t* n_tries) {

@@ -287,3 +287,52 @@ def test_block_commit_host_matches_device(khst):
     w = Twin(ctx, 30_000, 2, nc=40, ns=100, dirty=2_000)
     for b in range(2):
         w.block(b)
+
+
+def test_host_handles_pair_on_the_shared_context(khst, oracle):
+    """The JVM sequence of INTEGRATION.md: kh_trie_open_host + kh_forest_open(NULL) share
+    the host entry points' context, so kh_block_commit_host accepts the pair."""
+    import ctypes
+    import random
+    import numpy as np
+    from khipu_amd import _lib
+    from khipu_amd._lib import check, lib
+    from khipu_amd.device import block_commit_host
+    from khipu_amd import codec
+    r = random.Random(21)
+    keys = [bytes(r.getrandbits(8) for _ in range(32)) for _ in range(300)]
+    vals = [codec.account_rlp(i, 10 ** 18 + i) for i in range(300)]
+    kb = np.frombuffer(b"".join(keys), np.uint8)
+    vb = np.frombuffer(b"".join(vals) + bytes(8), np.uint8)
+    vo = np.concatenate([[0], np.cumsum([len(v) for v in vals])]).astype(np.uint64)
+    root = np.zeros(32, np.uint8)
+    st_h, fo_h = ctypes.c_void_p(), ctypes.c_void_p()
+    check(lib().kh_trie_open_host(kb.ctypes.data, 32, vb.ctypes.data, vo.ctypes.data, 300, 0, root.ctypes.data,
+                                  ctypes.byref(st_h)))
+    check(lib().kh_forest_open(None, _lib.KH_HASH_KEYS, ctypes.byref(fo_h)))
+
+    class H:  # the minimal handle shape block_commit_host needs
+        def __init__(self, h):
+            self.h = h
+            self.ctx = type("C", (), {"_sync": staticmethod(lambda: None)})()
+    state, forest = H(st_h), H(fo_h)
+    # one slot in trie 0 for account 0 (its body gets the storage root), one plain update
+    sk = np.frombuffer(bytes(31) + b"\x01", np.uint8)
+    sv = np.frombuffer(b"\x05" + bytes(8), np.uint8)
+    so = np.array([0, 1], np.uint64)
+    ak = np.frombuffer(keys[0] + keys[1], np.uint8)
+    bodies = [codec.account_rlp(1, 5), codec.account_rlp(2, 6)]
+    av = np.frombuffer(b"".join(bodies) + bytes(8), np.uint8).copy()
+    ao = np.array([0, len(bodies[0]), len(bodies[0]) + len(bodies[1])], np.uint64)
+    at = np.array([0, _lib.KH_NO_TRIE], np.uint32)
+    got = block_commit_host(state, forest, np.array([0], np.uint32), sk, sv, so, None, None, ak, av, ao, at, None)
+    # expected: the oracle fold with the storage root written into account 0's body
+    t = oracle.Trie()
+    t.put(oracle.kec256(bytes(31) + b"\x01"), b"\x05")
+    sroot = t.root_hash()
+    b0 = bytearray(bodies[0])
+    b0[len(b0) - 65:len(b0) - 33] = sroot
+    exp_vals = [bytes(b0), bodies[1]] + vals[2:]
+    assert got == oracle.seq_root(keys, exp_vals)
+    lib().kh_trie_free(st_h)
+    lib().kh_trie_free(fo_h)
