@@ -1357,7 +1357,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     skey = S.skey;
     sseg = S.sseg;
     fallback = S.fallback;
-    T.sck = S.sck;  // non-null: the sorted keys are gathered beside the leaf kernel (below)
+    T.sck = S.sck;  // non-null: no sorted keys materialised (trie_ops.h sorted_key)
   }
   const bool ties = fallback;
   T.m = m;
@@ -1419,14 +1419,13 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     HIPCHK(hipEventRecord(c->ev[8], st));
     HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
     HIPCHK(hipEventRecord(c->ev[9], c->st2));
-    hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, c->st2, T, n);
+    // measurement switch: extra dynamic LDS per block caps the leaf kernel's occupancy
+    // (how it shares the CUs with the topology kernels on the other stream)
+    const char* dl = getenv("KHST_LEAF_DYN_LDS");
+    const unsigned dyn = dl ? (unsigned)atoi(dl) : 0u;
+    hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), dyn, c->st2, T, n);
     LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[10], c->st2));
-  }
-  if (T.sck) {  // the sorted keys (leaf publish, extensions), off the critical path
-    hipLaunchKernelGGL(k_gather, GRID(m, BS), dim3(BS), 0, st, (const uint64_t*)K32, (const uint32_t*)nullptr,
-                       (const uint32_t*)sidx, m, skey, (uint32_t*)nullptr);
-    LAUNCH_CHECK();
   }
   if (nb > 0) {
     P.lv[0] = T.u;

@@ -262,9 +262,18 @@ KH_HD Slot branch_slot(const Topo& T, uint64_t g, uint32_t d, bool ext) {
   return Slot{base + (g - first), cnt};
 }
 
+// sorted key i where nibbles [0, need) are read: the gathered sorted keys, or on the
+// unsegmented plain path (sck set, no sorted keys materialised) the first word from the
+// sorted prefixes and, past nibble 16, the input key through its index
+KH_HD Key4 sorted_key(const Topo& T, uint64_t i, uint32_t need) {
+  if (!T.sck) return load_key(T.skey, i);
+  if (need <= 16) return Key4{bswap64(T.sck[i]), 0, 0, 0};
+  return load_key(T.kin, T.sidx[i]);
+}
+
 KH_HD uint32_t result_index(const Topo& T, uint64_t first_key) {
   if (T.segmented) return T.sseg[first_key];
-  if (T.depth0 == 1) return (uint32_t)(T.skey[4 * first_key] & 0xFF) >> 4;
+  if (T.depth0 == 1) return (uint32_t)(sorted_key(T, first_key, 1).w0 & 0xFF) >> 4;
   return 0;
 }
 
@@ -662,7 +671,7 @@ KH_HD void leaf_header(BW& w, const Key4& k, const LeafGeom& g, uint64_t vlen) {
 
 // vp: the value bytes (global memory, or a staged copy in LDS on the device)
 KH_HD void op_leaf_prep(const Topo& T, uint64_t i, const uint8_t* vp, uint64_t vlen) {
-  Key4 k = load_key(T.skey, i);
+  const Key4 k = sorted_key(T, i, 64);
   if (el_cached(T, i, (uint32_t)(T.lf_pd[i] + 1))) return;
   if (el_subtree(T, i)) {  // extension over the unchanged branch (nothing when it hangs at its own depth)
     const uint32_t a = (uint32_t)(T.lf_pd[i] + 1), e = el_ext_nibbles(T, i, a);
@@ -723,9 +732,8 @@ KH_HD void kec256_strided(const uint64_t* w, uint64_t stride, uint32_t len, uint
 
 // ---- leaf hash (thread per leaf).  Returns permutations spent.
 KH_HD uint32_t leaf_nibble(const Topo& T, uint64_t i) {
-  uint32_t pd = (uint32_t)T.lf_pd[i];
-  uint32_t b = (uint32_t)(T.skey[4 * i + (pd >> 4)] >> (8 * ((pd >> 1) & 7))) & 0xFF;
-  return (pd & 1) ? (b & 0xF) : (b >> 4);
+  const uint32_t pd = (uint32_t)T.lf_pd[i];
+  return key_nibble(sorted_key(T, i, pd + 1), (int)pd);
 }
 // publish of leaf i after hashing: hh = its hash (zero if not hashed: L < 32 and not the
 // top), head = its first 4 message words (the inline reference when L < 32)
@@ -928,7 +936,7 @@ KH_HD void op_leaf_topo_early(const Topo& T, uint64_t i, AllocFn alloc) {
     publish_ref(T, NONE, 0, 0, i, r, 32, r);
     return;
   }
-  Key4 k = load_key(T.skey, i);
+  const Key4 k = sorted_key(T, i, (uint32_t)P.pd + 1);
   uint64_t slot = (uint64_t)T.br_cbase[P.bid] + P.pord;
   for (int q = 0; q < 4; ++q) T.cref[4 * slot + q] = r[q];
   T.cmeta[slot] = (uint16_t)(em | (key_nibble(k, P.pd) << 8));
@@ -1055,7 +1063,7 @@ KH_HD uint32_t branch_publish(const Topo& T, uint32_t j, uint32_t L, const uint6
   uint32_t d = T.br_depth[j];
   int32_t pd = (int32_t)d - (int32_t)ext - 1;
   bool top = parent == NONE;
-  Key4 key = load_key(T.skey, first);
+  const Key4 key = sorted_key(T, first, d);
   uint32_t nib = top ? 0 : key_nibble(key, pd);
   if (ext == 0) {
     publish_ref(T, parent, T.br_pord[j], nib, first, bhead, L, hb);

@@ -118,6 +118,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   if (!segmented) {
     for (uint64_t i = 0; i < m; ++i) sck[i] = bswap64(skey[4 * i]);
     T.sck = sck.data();
+    T.skey = nullptr;  // as on the device: no sorted keys on this path
   }
   if (nb > 0) {
     for (uint64_t b = 0; b < nb; ++b) op_lcp(T, b);
