@@ -64,7 +64,8 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* lds_waves, T* total) {
 }
 
 template <typename T>
-__global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const T* in, T* out, uint64_t n, T* tile_sums) {
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const T* in, T* out, uint64_t n, T* tile_sums,
+                                                             T* last_in) {
   __shared__ T lw[SCAN_THREADS / 64];
   uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
   T v[SCAN_ITEMS];
@@ -72,6 +73,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const T* in, T* out
 #pragma unroll
   for (int i = 0; i < SCAN_ITEMS; ++i) {
     v[i] = (base + i < n) ? in[base + i] : (T)0;
+    if (last_in && base + i == n - 1) *last_in = v[i];  // read before any output of this tile lands
     s += v[i];
   }
   T tot;
@@ -116,11 +118,11 @@ void scan_exclusive(const T* in, T* out, uint64_t n, T* total, void* scratch, hi
     return;
   }
   uint64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-  // keep the last input element before it may be overwritten (in == out)
+  // the last input element is kept by the tile that reads it (in == out allowed)
   T* sums = (T*)scratch;
   T* last_in = sums + tiles;  // one slot after the tile sums
-  (void)hipMemcpyAsync(last_in, in + (n - 1), sizeof(T), hipMemcpyDeviceToDevice, st);
-  hipLaunchKernelGGL(k_scan_tiles<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, in, out, n, sums);
+  hipLaunchKernelGGL(k_scan_tiles<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, in, out, n, sums,
+                     total ? last_in : (T*)nullptr);
   if (tiles > 1) {
     char* next = (char*)scratch + (((tiles + 1) * sizeof(T) + 63) / 64) * 64 + 64;
     scan_exclusive<T>(sums, sums, tiles, (T*)nullptr, next, st);
