@@ -1414,6 +1414,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   }
   if (early) {  // leaves need only the boundaries: hash them (input order) beside the topology
     if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, st));  // dropped duplicates: PDINV_SKIP
+    HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));                  // every leaf a hash unless it says otherwise
     hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[8], st));

@@ -211,7 +211,7 @@ struct Topo {
   // early leaves (plain root builds; nullable): capped reference and its length
   // (32 = hash, EMETA_LONG = not hashed yet: longer than one Keccak block)
   uint64_t* lf_eref;   // [m*4]
-  uint8_t* lf_emeta;   // [m]
+  uint8_t* lf_emeta;   // [m] preset to 32 (a hash): only inline and long leaves write theirs
   const uint64_t* kin; // [n*4] the keys in input order (the early leaf kernel reads them sequentially)
   uint64_t* pdinv;     // [n] per INPUT position: parent depth << 32 | sorted position; PDINV_SKIP for
                        //     a dropped duplicate
@@ -899,7 +899,8 @@ KH_HD uint32_t op_leaf_in(const Topo& T, uint64_t j, WP vw, uint32_t vmis, uint6
   }
   // a top leaf is >= 35 B (its path is >= 63 nibbles: an HP of >= 33 B), so its stash is
   // always the hash
-  T.lf_emeta[si] = (uint8_t)(L >= 32 ? 32 : L);
+  if (L < 32) T.lf_emeta[si] = (uint8_t)L;  // the preset 32 stands for every hashed leaf (one scattered
+                                           // byte write less per leaf)
   return perms;
 }
 // value span of sorted leaf i (early builds gather no spans: through the input index)

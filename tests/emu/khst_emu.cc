@@ -158,7 +158,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   // per input and published after the topology (k_leaf_topo_early)
   const bool early = true;
   std::vector<uint64_t> eref(4 * m + 4);
-  std::vector<uint8_t> emeta(m + 1);
+  std::vector<uint8_t> emeta(m + 1, 32);  // preset as on the device
   std::vector<uint64_t> pdinv(n + 1, PDINV_SKIP);
   std::vector<uint64_t> hdr(8);
   uint64_t perms = 0, hashes = 0, inl = 0, longb = 0;
