@@ -346,10 +346,21 @@ def relaunch(args):
     return subprocess.call(cmd, env=env)
 
 
+def keep_stdout_for_json():
+    """Native libraries print banners on fd 1 (RCCL's version block at communicator
+    creation): point fd 1 at stderr and keep Python's sys.stdout on the original stream,
+    so stdout carries only the JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    sys.stdout = os.fdopen(saved, "w", buffering=1)
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch(args))
+    keep_stdout_for_json()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.workload == "lists":
         lists(args)
