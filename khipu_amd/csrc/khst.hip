@@ -1412,21 +1412,19 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
   }
-  if (early) {  // leaves need only the boundaries: hash them (input order) beside the topology
-    if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, st));  // dropped duplicates: PDINV_SKIP
-    HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));                  // every leaf a hash unless it says otherwise
-    hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, st, T);
-    LAUNCH_CHECK();
+  if (early) {  // leaves need only the boundaries: hash them (input order) on st2 beside the
+                // topology, which starts right after k_lcp (the parent-depth scatter included)
     HIPCHK(hipEventRecord(c->ev[8], st));
     HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
-    HIPCHK(hipEventRecord(c->ev[9], c->st2));
-    // measurement switch: extra dynamic LDS per block caps the leaf kernel's occupancy
-    // (how it shares the CUs with the topology kernels on the other stream)
-    const char* dl = getenv("KHST_LEAF_DYN_LDS");
-    const unsigned dyn = dl ? (unsigned)atoi(dl) : 0u;
-    hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), dyn, c->st2, T, n);
+    hipStream_t s2 = c->st2;
+    if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, s2));  // dropped duplicates: PDINV_SKIP
+    HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, s2));                  // every leaf a hash unless it says otherwise
+    hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, s2, T);
     LAUNCH_CHECK();
-    HIPCHK(hipEventRecord(c->ev[10], c->st2));
+    HIPCHK(hipEventRecord(c->ev[9], s2));
+    hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, s2, T, n);
+    LAUNCH_CHECK();
+    HIPCHK(hipEventRecord(c->ev[10], s2));
   }
   if (nb > 0) {
     P.lv[0] = T.u;
