@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(BS) k_hash_keys(const uint8_t* keys, uint32_t 
 // identity index in the same pass (saves k_make_ck's re-read of the keys)
 template <bool SHORT>
 __global__ void __launch_bounds__(BS) k_hash_keys_ck(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out,
-                                                     uint64_t* ck, uint32_t* idx) {
+                                                     uint64_t* ck, uint32_t* idx, uint64_t base) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
   uint64_t h[4];
@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(BS) k_hash_keys_ck(const uint8_t* keys, uint32
     kec256_msg<false>(keys + i * klen, klen, h);
   for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
   ck[i] = bswap64(h[0]);
-  idx[i] = (uint32_t)i;
+  idx[i] = (uint32_t)(base + i);
 }
 
 // composite sort key: segment id in the top sb bits, then the key's leading bits (big-endian)
@@ -145,6 +145,12 @@ __global__ void __launch_bounds__(BS) k_make_ck(const uint64_t* K, const uint32_
 // (later put last) is kept.  flags |= 2 if equal keys exist (dedup needed),
 // |= 1 if a run exceeds TIE_RUN_MAX (take the full-sort path instead).
 constexpr uint32_t TIE_RUN_MAX = 64;
+// builds from 4M keys hash their second half beside the first sort (KHST_SPLIT_MIN
+// overrides the threshold: the tests run every parity case through the split path)
+static uint64_t split_min() {
+  const char* e = getenv("KHST_SPLIT_MIN");
+  return e ? strtoull(e, nullptr, 10) : (1ull << 22);
+}
 // variable-length keys (zero padded, kn nibbles): a key sorts before the longer keys it
 // prefixes, i.e. (padded key, length) order
 __device__ __forceinline__ bool key_less(const uint64_t* a, const uint64_t* b, uint32_t kna = 0, uint32_t knb = 0) {
@@ -980,7 +986,8 @@ struct kh_ctx {
   hipStream_t st2 = nullptr;  // leaf hashing, concurrent with the branch topology
   std::mutex mu;
   DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, in_kn, in_aux, in_block, out_emit, emit_dev;
-  hipEvent_t ev[11] = {};  // [8] boundaries ready (st), [9] / [10] leaf kernel start / end (st2)
+  hipEvent_t ev[13] = {};  // [8] boundaries ready (st), [9] / [10] leaf kernel start / end (st2),
+                          // [11] / [12] split hashing: st2 start / second half hashed
   unsigned long long* h_pinned = nullptr;  // small pinned staging for syncs
   // last build (for emission)
   Topo T{};
@@ -1053,6 +1060,8 @@ struct SortIO {
   const uint8_t* kn;  // variable-length keys: nibble counts (input order; nullable)
   bool ck_ready = false;  // ck0/idx0 already hold the unsegmented sort keys (k_hash_keys_ck)
   bool ck_path = false;   // unsegmented plain build: sort (ck, idx) only, gather the keys later
+  const uint64_t* pck = nullptr;  // already sorted on the top 32 bits (the split hash + sort)
+  const uint32_t* pidx = nullptr;
   // out
   const uint64_t* sck = nullptr;  // ck_path: the sorted first key words (skey not gathered yet)
   uint64_t m;
@@ -1078,13 +1087,20 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
   // ---- 2. sort: LSD radix on the top 32 bits of the composite (segment | key) prefix,
   // then fix the rare runs of equal prefixes locally (k_tie_fix); a full 256-bit sort
   // only if a run is longer than TIE_RUN_MAX (adversarial keys)
-  if (!S.ck_ready) {
-    hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, sb, n, ck0, idx0);
-    LAUNCH_CHECK();
+  uint64_t* cks;
+  uint32_t* idxs;
+  if (S.pck) {  // sorted while the keys were hashed (run_build)
+    cks = (uint64_t*)S.pck;
+    idxs = (uint32_t*)S.pidx;
+  } else {
+    if (!S.ck_ready) {
+      hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, sb, n, ck0, idx0);
+      LAUNCH_CHECK();
+    }
+    bool flip = radix_sort_pairs(ck0, idx0, ck1, idx1, n, 32, 64, rs_scratch, st);
+    cks = flip ? ck1 : ck0;
+    idxs = flip ? idx1 : idx0;
   }
-  bool flip = radix_sort_pairs(ck0, idx0, ck1, idx1, n, 32, 64, rs_scratch, st);
-  uint64_t* cks = flip ? ck1 : ck0;
-  uint32_t* idxs = flip ? idx1 : idx0;
   LAUNCH_CHECK();
   if (S.ck_path) {
     hipLaunchKernelGGL(k_tie_fix_ck, GRID(n, BS), dim3(BS), 0, st, cks, idxs, n, (const uint64_t*)K32, T.ctr + CTR_TIE);
@@ -1326,12 +1342,45 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   HIPCHK(hipEventRecord(c->ev[0], st));
   // ---- 1. keys
   const bool ck_ready = (A.flags & KH_HASH_KEYS) && !segmented;
-  if (ck_ready) {
+  // large hashed builds: the second half of the keys is hashed on st2 while st sorts the
+  // first half (VALU-bound hashing beside the memory-bound radix passes), then the two
+  // sorted halves are merged (stable: the first half's inputs come first)
+  const bool split = ck_ready && !A.kn && n >= 2 && n >= split_min();
+  const uint64_t* pck = nullptr;
+  const uint32_t* pidx = nullptr;
+  auto hash_ck = [&](uint64_t lo, uint64_t cnt, hipStream_t s) {
     if (A.klen <= 135)
-      hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, ck0, idx0);
+      hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(cnt, BS), dim3(BS), 0, s, A.keys + lo * A.klen, A.klen, cnt,
+                         K32 + 4 * lo, ck0 + lo, idx0 + lo, lo);
     else
-      hipLaunchKernelGGL(k_hash_keys_ck<false>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, ck0, idx0);
+      hipLaunchKernelGGL(k_hash_keys_ck<false>, GRID(cnt, BS), dim3(BS), 0, s, A.keys + lo * A.klen, A.klen, cnt,
+                         K32 + 4 * lo, ck0 + lo, idx0 + lo, lo);
     LAUNCH_CHECK();
+  };
+  if (split) {
+    const uint64_t n0 = n / 2, n1 = n - n0;
+    HIPCHK(hipEventRecord(c->ev[11], st));
+    HIPCHK(hipStreamWaitEvent(c->st2, c->ev[11], 0));
+    hash_ck(0, n0, st);
+    hash_ck(n0, n1, c->st2);
+    HIPCHK(hipEventRecord(c->ev[12], c->st2));
+    HIPCHK(hipEventRecord(c->ev[1], st));  // (the key stage is now the first half's hashing)
+    const bool f0 = radix_sort_pairs(ck0, idx0, ck1, idx1, n0, 32, 64, rs_scratch, st);
+    HIPCHK(hipStreamWaitEvent(st, c->ev[12], 0));
+    const bool f1 = radix_sort_pairs(ck0 + n0, idx0 + n0, ck1 + n0, idx1 + n0, n1, 32, 64, rs_scratch, st);
+    if (f0 != f1) throw KhError{KH_EINTERNAL, "split sort: pass parity differs"};
+    uint64_t* ka = f0 ? ck1 : ck0;
+    uint32_t* va = f0 ? idx1 : idx0;
+    uint64_t* ko = f0 ? ck0 : ck1;
+    uint32_t* vo = f0 ? idx0 : idx1;
+    hipLaunchKernelGGL(k_merge_runs, dim3((unsigned)((n + MG_TILE - 1) / MG_TILE)), dim3(MG_THREADS), 0, st,
+                       (const uint64_t*)ka, (const uint32_t*)va, n0, (const uint64_t*)(ka + n0),
+                       (const uint32_t*)(va + n0), n1, ko, vo);
+    LAUNCH_CHECK();
+    pck = ko;
+    pidx = vo;
+  } else if (ck_ready) {
+    hash_ck(0, n, st);
   } else if (A.flags & KH_HASH_KEYS) {
     if (A.klen <= 135)
       hipLaunchKernelGGL(k_hash_keys<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32);
@@ -1341,7 +1390,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   } else if (own_keys) {
     HIPCHK(hipMemcpyAsync(K32, A.keys, n * 32, hipMemcpyDeviceToDevice, st));
   }
-  HIPCHK(hipEventRecord(c->ev[1], st));
+  if (!split) HIPCHK(hipEventRecord(c->ev[1], st));
 
   // ---- 2. sort + dedup
   uint64_t m = n;
@@ -1351,6 +1400,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr,
              A.kn, ck_ready};
     S.ck_path = early && !segmented && !A.kn;
+    S.pck = pck;
+    S.pidx = pidx;
     sort_dedup(c, S);
     m = S.m;
     sidx = S.sidx;
@@ -1591,7 +1642,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     stats->arena_bytes = lmsg_words * 8 + lf_bytes + (bmsg_words + xmsg_words) * 8;  // node RLP kept in HBM
     stats->n_levels = levels;
     stats->full_sort = ties ? 1 : 0;
-    stats->t_keys_ms = ev_ms(c->ev[0], c->ev[1]);
+    // split builds: until both halves are hashed (the second half overlaps the first sort)
+    stats->t_keys_ms = split ? std::max(ev_ms(c->ev[0], c->ev[1]), ev_ms(c->ev[0], c->ev[12])) : ev_ms(c->ev[0], c->ev[1]);
     stats->t_sort_ms = ev_ms(c->ev[1], c->ev[2]);
     stats->t_topo_ms = ev_ms(c->ev[2], c->ev[3]);
     // early: the leaf kernel's own span on st2, where it overlaps the topology (the

@@ -270,4 +270,69 @@ inline bool radix_sort_pairs(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t*
   return flip;
 }
 
+// ---------------------------------------------------------------------------
+// Stable merge of two runs sorted on the top 32 bits of their keys (merge path): run A =
+// (ka, va)[0, na), run B = (kb, vb)[0, nb); on equal top bits A comes first.  One tile of
+// MG_TILE outputs per block: the tile's split is found by a diagonal binary search, its
+// slices of A and B are staged in LDS, then every thread merges MG_ITEMS outputs.
+// ---------------------------------------------------------------------------
+constexpr int MG_THREADS = 256;
+constexpr int MG_ITEMS = 8;
+constexpr int MG_TILE = MG_THREADS * MG_ITEMS;
+
+// number of A elements among the first d outputs (A wins ties)
+template <typename GetA, typename GetB>
+__device__ __forceinline__ uint64_t merge_split(GetA a, GetB b, uint64_t na, uint64_t nb, uint64_t d) {
+  uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;  // take mid + 1 elements of A?
+    if ((a(mid) >> 32) <= (b(d - 1 - mid) >> 32)) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(MG_THREADS) k_merge_runs(const uint64_t* ka, const uint32_t* va, uint64_t na,
+                                                          const uint64_t* kb, const uint32_t* vb, uint64_t nb,
+                                                          uint64_t* ko, uint32_t* vo) {
+  __shared__ uint64_t sk[MG_TILE];
+  __shared__ uint32_t sv[MG_TILE];
+  __shared__ uint64_t s_split[2];
+  const uint64_t n = na + nb;
+  const uint64_t d0 = (uint64_t)blockIdx.x * MG_TILE;
+  const uint64_t d1 = d0 + MG_TILE < n ? d0 + MG_TILE : n;
+  if (threadIdx.x < 2) {
+    const uint64_t d = threadIdx.x ? d1 : d0;
+    s_split[threadIdx.x] = merge_split([&](uint64_t i) { return ka[i]; }, [&](uint64_t i) { return kb[i]; }, na, nb, d);
+  }
+  __syncthreads();
+  const uint64_t a0 = s_split[0], a1 = s_split[1];
+  const uint64_t b0 = d0 - a0, b1 = d1 - a1;
+  const uint32_t la = (uint32_t)(a1 - a0), lb = (uint32_t)(b1 - b0);
+  for (uint32_t t = threadIdx.x; t < la; t += MG_THREADS) {
+    sk[t] = ka[a0 + t];
+    sv[t] = va[a0 + t];
+  }
+  for (uint32_t t = threadIdx.x; t < lb; t += MG_THREADS) {
+    sk[la + t] = kb[b0 + t];
+    sv[la + t] = vb[b0 + t];
+  }
+  __syncthreads();
+  const uint32_t tot = la + lb;
+  const uint32_t e0 = threadIdx.x * MG_ITEMS;
+  if (e0 >= tot) return;
+  const uint32_t e1 = e0 + MG_ITEMS < tot ? e0 + MG_ITEMS : tot;
+  const uint64_t* A = sk;
+  const uint64_t* B = sk + la;
+  uint32_t i = (uint32_t)merge_split([&](uint64_t x) { return A[x]; }, [&](uint64_t x) { return B[x]; }, la, lb, e0);
+  uint32_t j = e0 - i;
+  for (uint32_t e = e0; e < e1; ++e) {
+    const bool takeA = i < la && (j >= lb || (A[i] >> 32) <= (B[j] >> 32));
+    const uint32_t src = takeA ? i : la + j;
+    ko[d0 + e] = sk[src];
+    vo[d0 + e] = sv[src];
+    if (takeA) ++i; else ++j;
+  }
+}
+
 }  // namespace khst

@@ -281,3 +281,63 @@ def test_branch_variants_vs_oracle(khst, oracle, variant, monkeypatch):
     vo = voff.cpu().numpy().astype(np.uint64)
     roots, bst = oracle.batch_roots(a, (vals[:int(vo[-1])].cpu().numpy(), vo), klen=20, hash_keys=True)
     assert hh[0].tobytes() == roots[0] and st.n_node_perms == bst["node_perms"], variant
+
+
+def test_split_hash_sort_paths(khst, oracle):
+    """Hashed-key builds from 4M keys hash the second half on the second stream while the
+    first half is radix-sorted, then merge the halves (stable: the first half's puts come
+    first).  KHST_SPLIT_MIN lowers the threshold so small inputs with duplicates inside and
+    across the halves take that path; roots must equal the oracle's and the unsplit build's."""
+    import os
+    import random
+    r = random.Random(17)
+    cases = []
+    for n in (2, 3, 17, 255, 256, 257, 1000, 4099):
+        base = [bytes(r.getrandbits(8) for _ in range(20)) for _ in range(n)]
+        keys = base + [base[r.randrange(n)] for _ in range(n // 3)]  # repeats, many in the other half
+        r.shuffle(keys)
+        vals = [bytes([r.getrandbits(8) | 1]) * r.choice([1, 3, 40, 90]) for _ in keys]
+        cases.append((keys, vals))
+    old = os.environ.get("KHST_SPLIT_MIN")
+    try:
+        os.environ["KHST_SPLIT_MIN"] = "2"
+        split = [khst.trie_root(k, v, hash_keys=True) for k, v in cases]
+    finally:
+        if old is None:
+            os.environ.pop("KHST_SPLIT_MIN", None)
+        else:
+            os.environ["KHST_SPLIT_MIN"] = old
+    for (k, v), g in zip(cases, split):
+        assert g == khst.trie_root(k, v, hash_keys=True)
+        assert g == oracle.batch_root(k, v, klen=20, hash_keys=True, nthreads=2)
+
+
+def test_split_path_6m_with_repeats(khst, oracle):
+    """6M accounts (the split path at its default threshold) plus 200k repeated addresses
+    with new bodies in both halves, against the CPU batch builder."""
+    import torch
+    from khipu_amd.device import Ctx
+    ctx = Ctx(0)
+    n = 6_000_000
+    addr, vals, voff = ctx.synth_accounts(5, 0, n)
+    torch.cuda.synchronize()
+    a = addr[:20 * n].cpu().numpy().reshape(n, 20)
+    vo = voff.cpu().numpy().astype(np.uint64)
+    vb = vals[:int(vo[n])].cpu().numpy()
+    rng = np.random.default_rng(8)
+    rep = rng.integers(0, n, 200_000)
+    rk = a[rep]
+    rv = rng.integers(0, 256, 200_000 * 70, dtype=np.uint8)
+    keys = np.concatenate([rk[:100_000], a, rk[100_000:]]).reshape(-1)
+    vbytes = np.concatenate([rv[:100_000 * 70], vb, rv[100_000 * 70:]])
+    lens = np.concatenate([np.full(100_000, 70), np.diff(vo), np.full(100_000, 70)]).astype(np.uint64)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    d_k = torch.from_numpy(np.ascontiguousarray(keys)).to("cuda:0")
+    d_v = torch.from_numpy(np.concatenate([vbytes, np.zeros(64, np.uint8)])).to("cuda:0")
+    d_o = torch.from_numpy(off.astype(np.int64)).to("cuda:0")
+    N = len(lens)
+    hh, _, _, st = ctx.build(d_k, 20, d_v, d_o, N, hash_keys=True)
+    roots, bst = oracle.batch_roots(keys, (vbytes, off), klen=20, hash_keys=True)
+    assert hh[0].tobytes() == roots[0]
+    assert st.n_leaves == bst["leaves"]
