@@ -313,10 +313,12 @@ def test_split_hash_sort_paths(khst, oracle):
 
 
 def test_split_path_6m_with_repeats(khst, oracle):
-    """6M accounts (the split path at its default threshold) plus 200k repeated addresses
+    """6M accounts through the split path (KHST_SPLIT_MIN) plus 200k repeated addresses
     with new bodies in both halves, against the CPU batch builder."""
+    import os
     import torch
     from khipu_amd.device import Ctx
+    os.environ["KHST_SPLIT_MIN"] = "4000000"
     ctx = Ctx(0)
     n = 6_000_000
     addr, vals, voff = ctx.synth_accounts(5, 0, n)
@@ -337,7 +339,12 @@ def test_split_path_6m_with_repeats(khst, oracle):
     d_v = torch.from_numpy(np.concatenate([vbytes, np.zeros(64, np.uint8)])).to("cuda:0")
     d_o = torch.from_numpy(off.astype(np.int64)).to("cuda:0")
     N = len(lens)
-    hh, _, _, st = ctx.build(d_k, 20, d_v, d_o, N, hash_keys=True)
+    try:
+        hh, _, _, st = ctx.build(d_k, 20, d_v, d_o, N, hash_keys=True)
+    finally:
+        os.environ.pop("KHST_SPLIT_MIN", None)
+    hh2, _, _, _ = ctx.build(d_k, 20, d_v, d_o, N, hash_keys=True)  # the default (unsplit) path
+    assert hh2[0].tobytes() == hh[0].tobytes()
     roots, bst = oracle.batch_roots(keys, (vbytes, off), klen=20, hash_keys=True)
     assert hh[0].tobytes() == roots[0]
     assert st.n_leaves == bst["leaves"]
