@@ -386,11 +386,6 @@ __device__ __forceinline__ void block_add3(unsigned long long* c0, unsigned long
   }
 }
 
-__global__ void __launch_bounds__(BS) k_group_bid(Topo T, uint64_t nb) {
-  uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (b < nb) op_group_bid(T, b);
-}
-
 __global__ void __launch_bounds__(BS) k_branch_topo(Topo T, Pyr P, uint64_t nb) {
   uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long ext = 0;
@@ -464,9 +459,7 @@ __global__ void __launch_bounds__(BS) k_branch_permute(Topo T, BrTab J, const ui
 // group reps carry level-order branch ids from here on (leaf parents, resident tables)
 __global__ void __launch_bounds__(BS) k_bid_remap(Topo T, const uint32_t* pos, uint64_t nb) {
   const uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (b >= nb || T.u[b] == 0) return;
-  T.gbid[b] = pos[T.gbid[b]];
-  if (T.rep[b] == (uint32_t)b) T.isrep_bid[b] = pos[T.isrep_bid[b]];
+  if (b < nb && T.u[b] != 0 && T.rep[b] == (uint32_t)b) T.isrep_bid[b] = pos[T.isrep_bid[b]];
 }
 
 // level bounds: lb[d] = first position of depth d in `order`, lb[64] = B
@@ -542,23 +535,18 @@ __global__ void __launch_bounds__(BS) k_pd_scatter(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i < T.m) op_pd_scatter(T, i);
 }
-template <int ITEMS>
 __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
   __shared__ uint64_t hdr[HDR_WORDS * BS];
+  const uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
   typedef const __attribute__((address_space(1))) uint64_t gword;  // global (not flat) loads
   const uint32_t vmis = (uint32_t)((uintptr_t)T.vals & 7);
   gword* vw = (gword*)(T.vals - vmis);
   unsigned long long perms = 0, inl = 0, longb = 0;
-  // ITEMS consecutive inputs per thread: the later ones find their key / value lines in
-  // the cache the earlier one's loads brought in
-  for (int q = 0; q < ITEMS; ++q) {
-    const uint64_t j = ((uint64_t)blockIdx.x * BS + threadIdx.x) * ITEMS + q;
-    if (j < n) {
-      uint32_t in1 = 0, lb = 0;
-      perms += op_leaf_in(T, j, vw, vmis, hdr + threadIdx.x, BS, &in1, &lb);
-      inl += in1;
-      longb += lb;
-    }
+  if (j < n) {
+    uint32_t in1 = 0, lb = 0;
+    perms = op_leaf_in(T, j, vw, vmis, hdr + threadIdx.x, BS, &in1, &lb);
+    inl = in1;
+    longb = lb;
   }
   block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], perms, &T.ctr[CTR_INLINE], inl);
   __syncthreads();  // block_add3's LDS slots are reused
@@ -1268,7 +1256,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       n * 32, segmented ? n * 4 : 0,          // skey sseg
       radix_scratch_bytes(n), scan_scratch_bytes(n, 8),
       nb1, nb1 / 32 + 1024,                   // u, pyramid
-      nb1 * 4, nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1 * 4, nb1, nb1, nb1 * 4,  // psv nsv pse rep ord isrep glast gk gbid
+      nb1 * 4, nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1 * 4, nb1, nb1,  // psv nsv pse rep ord isrep glast gk
       nb1 * 4, nb1 * 4, nb1, nb1, nb1 * 4, nb1, nb1 * 4, nb1 * 8, nb1 * 4, nb1 * 4,  // branches
       n * 4, n, n, n * 8, n * 4, n * 8, n * 4,  // leaves, svoff, svlen
       A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
@@ -1300,7 +1288,6 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.isrep_bid = cv.take<uint32_t>(nb1);
   T.glast = cv.take<uint8_t>(nb1);
   T.gk = cv.take<uint8_t>(nb1);
-  T.gbid = cv.take<uint32_t>(nb1);
   T.br_k = cv.take<uint32_t>(nb1);
   T.br_cbase = cv.take<uint32_t>(nb1);
   T.br_depth = cv.take<uint8_t>(nb1);
@@ -1489,11 +1476,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, s2, T);
     LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[9], s2));
-    const char* li = getenv("KHST_LEAF_ITEMS");  // measurement switch: inputs per thread (1, 2)
-    if (li && atoi(li) == 2)
-      hipLaunchKernelGGL(k_leaf_in<2>, GRID((n + 1) / 2, BS), dim3(BS), 0, s2, T, n);
-    else
-      hipLaunchKernelGGL(k_leaf_in<1>, GRID(n, BS), dim3(BS), 0, s2, T, n);
+    hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, s2, T, n);
     LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[10], s2));
   }
@@ -1518,8 +1501,6 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     hipLaunchKernelGGL(k_chain, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
     scan_exclusive<uint32_t>(T.isrep_bid, T.isrep_bid, nb, Bp, scan_scratch, st);
-    hipLaunchKernelGGL(k_group_bid, GRID(nb, BS), dim3(BS), 0, st, T, nb);
-    LAUNCH_CHECK();
     // branch tables in key-order ids first (k_branch_topo writes them, thread per boundary)
     Topo TJ = T;
     TJ.br_k = J.k;

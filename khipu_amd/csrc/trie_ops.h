@@ -168,8 +168,6 @@ struct Topo {
   uint32_t* rep;          // [m-1] group representative of b
   uint8_t* ord;           // [m-1] ordinal of b within its group
   uint32_t* isrep_bid;     // [m-1] 1 if rep, then (after scan) branch id of rep
-  uint32_t* gbid;         // [m-1] the branch id of b's group (0 boundaries: NONE): one load
-                          //       where the parent resolution walked rep -> isrep_bid
   uint8_t* glast;         // [nb] 1 unless a later boundary of the same group exists (preset 1)
   uint8_t* gk;            // [nb] at a group's representative: its branch's child count
   // branches (B <= m-1)
@@ -488,20 +486,15 @@ KH_HD Parent resolve_parent(const Topo& T, int64_t a, int64_t c) {
     P.pd = (int32_t)T.depth0 - 1;
     P.pord = 0;
   } else if (va >= vc) {
-    P.bid = T.gbid[a];
+    P.bid = T.isrep_bid[T.rep[a]];
     P.pd = (int32_t)va - 1;
     P.pord = T.ord[a] + 1u;
   } else {
-    P.bid = T.gbid[c];
+    P.bid = T.isrep_bid[T.rep[c]];
     P.pd = (int32_t)vc - 1;
     P.pord = T.ord[c];
   }
   return P;
-}
-
-// ---- stage: every boundary's group branch id (after the scan turned rep flags into ids)
-KH_HD void op_group_bid(const Topo& T, uint64_t b) {
-  T.gbid[b] = T.u[b] ? T.isrep_bid[T.rep[b]] : NONE;
 }
 
 // ---- stage: branch records (thread per boundary; only reps act).  The child count

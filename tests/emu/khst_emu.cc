@@ -70,7 +70,6 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   for (uint64_t i = 0; i < m; ++i) op_val_gather(T, i);
   const uint64_t nbb = nb + 1;
   std::vector<uint8_t> glast(nbb, 1), gk(nbb, 0);
-  std::vector<uint32_t> gbid(nbb, NONE);
   std::vector<uint8_t> u(nbb), ord(nbb), br_depth(nbb), br_ext(nbb), br_pord(nbb), lf_pord(m);
   std::vector<int32_t> psv(nbb), nsv(nbb), pse(nbb);
   std::vector<uint32_t> rep(nbb), isrep(nbb), br_k(nbb, 0), br_cbase(nbb), br_parent(nbb), br_first(nbb),
@@ -87,7 +86,6 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.ord = ord.data();
   T.isrep_bid = isrep.data();
   T.glast = glast.data();
-  T.gbid = gbid.data();
   T.gk = gk.data();
   T.br_k = br_k.data();
   T.br_cbase = br_cbase.data();
@@ -146,7 +144,6 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       run += f;
     }
     B = run;
-    for (uint64_t b = 0; b < nb; ++b) op_group_bid(T, b);
     for (uint64_t b = 0; b < nb; ++b) {
       op_branch_topo(T, P, nb, b);
       if (u[b] != 0 && rep[b] == b) {
