@@ -478,21 +478,27 @@ struct Parent {
   int32_t pd;    // parent depth (depth0-1 for a top)
   uint32_t pord;
 };
+// Both sides are looked up before the deeper one is chosen: three dependent load rounds
+// (boundary value + rep + ordinal of a and c, then the reps' branch ids) instead of four.
 KH_HD Parent resolve_parent(const Topo& T, int64_t a, int64_t c) {
-  uint32_t va = a >= 0 ? T.u[a] : 0, vc = c >= 0 ? T.u[c] : 0;
+  const uint32_t va = a >= 0 ? T.u[a] : 0, vc = c >= 0 ? T.u[c] : 0;
+  const uint32_t ra = a >= 0 ? T.rep[a] : NONE, rc = c >= 0 ? T.rep[c] : NONE;
+  const uint32_t oa = a >= 0 ? T.ord[a] : 0, oc = c >= 0 ? T.ord[c] : 0;
+  const uint32_t ba = (va && ra != NONE) ? T.isrep_bid[ra] : NONE;
+  const uint32_t bc = (vc && rc != NONE) ? T.isrep_bid[rc] : NONE;
   Parent P;
   if (va == 0 && vc == 0) {
     P.bid = NONE;
     P.pd = (int32_t)T.depth0 - 1;
     P.pord = 0;
   } else if (va >= vc) {
-    P.bid = T.isrep_bid[T.rep[a]];
+    P.bid = ba;
     P.pd = (int32_t)va - 1;
-    P.pord = T.ord[a] + 1u;
+    P.pord = oa + 1u;
   } else {
-    P.bid = T.isrep_bid[T.rep[c]];
+    P.bid = bc;
     P.pd = (int32_t)vc - 1;
-    P.pord = T.ord[c];
+    P.pord = oc;
   }
   return P;
 }
