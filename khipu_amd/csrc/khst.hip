@@ -393,7 +393,7 @@ __global__ void __launch_bounds__(BS) k_branch_topo(Topo T, Pyr P, uint64_t nb) 
     op_branch_topo(T, P, nb, b);
     if (T.u[b] != 0 && T.rep[b] == (uint32_t)b) ext = T.br_ext[T.isrep_bid[b]] ? 1 : 0;
   }
-  block_add3(&T.ctr[CTR_EXT], ext, nullptr, 0, nullptr, 0);
+  block_add3(ctr_stat(T.ctr, CTR_EXT, blockIdx.x), ext, nullptr, 0, nullptr, 0);
 }
 
 __global__ void __launch_bounds__(BS) k_leaf_topo(Topo T) {
@@ -522,7 +522,8 @@ __global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
     hashes = perms ? 1 : 0;
     inl = in1;
   }
-  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
+  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
+             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
 }
 
 // Early leaves (plain root builds; trie_ops.h op_leaf_in): one thread per INPUT,
@@ -548,7 +549,8 @@ __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
     inl = in1;
     longb = lb;
   }
-  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], perms, &T.ctr[CTR_INLINE], inl);
+  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), perms,
+             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
   __syncthreads();  // block_add3's LDS slots are reused
   block_add3(&T.ctr[CTR_LONGB], longb, nullptr, 0, nullptr, 0);
 }
@@ -571,7 +573,8 @@ __global__ void __launch_bounds__(BS) k_leaf_long(Topo T) {
     hashes = perms ? 1 : 0;
     inl = in1;
   }
-  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
+  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
+             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
 }
 
 // one level: `first` = its first position in the level order, `cnt` = its size;
@@ -591,7 +594,8 @@ __global__ void __launch_bounds__(BS) k_branch_hash(Topo T, uint64_t first, uint
     hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
   }
-  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
+  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
+             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
 }
 
 // Fused per-level branch kernel (root-only and incremental builds; row N1): each thread
@@ -615,7 +619,8 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8)))
     hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
   }
-  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
+  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
+             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
 }
 
 // LDS ordering between lanes of ONE wave (the wave's LDS operations execute in
@@ -783,7 +788,8 @@ __global__ void __launch_bounds__(BS) k_branch_coop(Topo T, uint64_t first, uint
     hashes = branch_hash_count(T, j, p);
     inl = ninl;
   }
-  block_add3(&T.ctr[CTR_PERMS], perms, &T.ctr[CTR_HASHES], hashes, &T.ctr[CTR_INLINE], inl);
+  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
+             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
 }
 
 // write-back emission: node q in [0, m + 2B): leaf q, or branch / extension of branch (q-m)/2.
@@ -1261,7 +1267,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       n * 4, n, n, n * 8, n * 4, n * 8, n * 4,  // leaves, svoff, svlen
       A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
       nres * 32, nres * 4, nres * 32,         // results
-      CTR_N * 8, 64 * 4, 80 * 4, 512 * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
+      CTR_N * CTR_SHARDS * 8, 64 * 4, 80 * 4, 512 * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
       early ? n * 32 : 0, early ? n : 0, early ? n * 8 : 0,  // early leaves: stashed references, meta, pd|position
       A.kn ? n : 0,                           // sorted key lengths
       nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1, nb1,  // branch tables in key-order ids (BrTab J)
@@ -1311,7 +1317,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.res_hash = cv.take<uint64_t>(nres * 4);
   T.res_len = cv.take<uint32_t>(nres);
   T.res_inl = cv.take<uint64_t>(nres * 4);
-  T.ctr = cv.take<unsigned long long>(CTR_N);
+  T.ctr = cv.take<unsigned long long>(CTR_N * CTR_SHARDS);
   T.depth_hist = cv.take<uint32_t>(64);
   uint32_t* lb = cv.take<uint32_t>(80);
   const uint32_t nblk_max = (uint32_t)((nb1 + LV_TILE - 1) / LV_TILE);
@@ -1335,7 +1341,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.voff = A.voff;
   T.vlen_in = A.vlen;
 
-  HIPCHK(hipMemsetAsync(T.ctr, 0, CTR_N * 8, st));
+  HIPCHK(hipMemsetAsync(T.ctr, 0, CTR_N * CTR_SHARDS * 8, st));
   HIPCHK(hipMemsetAsync(T.depth_hist, 0, 64 * 4, st));
   HIPCHK(hipMemsetAsync(lb, 0, 80 * 4, st));
   HIPCHK(hipMemsetAsync(T.res_len, 0, nres * 4, st));
@@ -1628,7 +1634,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   HIPCHK(hipMemcpyAsync(O.res_hash.data(), T.res_hash, nres * 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(O.res_len.data(), T.res_len, nres * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(O.res_inl.data(), T.res_inl, nres * 32, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(c->h_pinned, ctr, CTR_N * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(c->h_pinned, ctr, CTR_N * CTR_SHARDS * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if (c->h_pinned[CTR_ERR]) throw KhError{KH_EINTERNAL, "build: device invariant violated"};
   c->T = T;
@@ -1637,10 +1643,15 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   if (stats) {
     stats->n_leaves = m;
     stats->n_branches = B;
-    stats->n_node_hashes = c->h_pinned[CTR_HASHES];
-    stats->n_node_perms = c->h_pinned[CTR_PERMS];
-    stats->n_inline = c->h_pinned[CTR_INLINE];
-    stats->n_extensions = c->h_pinned[CTR_EXT];
+    auto stat = [&](int idx) {
+      unsigned long long t = 0;
+      for (int r = 0; r < CTR_SHARDS; ++r) t += c->h_pinned[r * CTR_N + idx];
+      return t;
+    };
+    stats->n_node_hashes = stat(CTR_HASHES);
+    stats->n_node_perms = stat(CTR_PERMS);
+    stats->n_inline = stat(CTR_INLINE);
+    stats->n_extensions = stat(CTR_EXT);
     stats->n_key_perms = (A.flags & KH_HASH_KEYS) ? n * (uint64_t)(A.klen / 136 + 1) : 0;
     stats->arena_bytes = lmsg_words * 8 + lf_bytes + (bmsg_words + xmsg_words) * 8;  // node RLP kept in HBM
     stats->n_levels = levels;
@@ -1680,7 +1691,7 @@ static kh_ctx* ctx_new(int dev) {
   HIPCHK(hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, leaf_hi ? prio_hi : prio_lo));
   c->st = c->own;
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
-  HIPCHK(hipHostMalloc((void**)&c->h_pinned, 4096, hipHostMallocDefault));
+  HIPCHK(hipHostMalloc((void**)&c->h_pinned, 16384, hipHostMallocDefault));  // >= CTR_N * CTR_SHARDS words
   return c;
 }
 

@@ -242,6 +242,14 @@ enum {
   CTR_TIE = 8, CTR_M = 9, CTR_B = 10, CTR_BRBYTES = 11, CTR_LFBYTES = 12, CTR_C = 13, CTR_E0 = 14, CTR_E1 = 15,
   CTR_N = 16
 };
+// The statistics counters (node hashes, permutations, inline nodes, extensions) are added
+// by one atomic per block; with ~400k blocks per 100M-key kernel a single address
+// serialises them, so they are spread over CTR_SHARDS rows of CTR_N (one 128-byte line
+// each) by block index and summed on the host.  Row 0 holds every other counter.
+constexpr int CTR_SHARDS = 64;
+KH_HD unsigned long long* ctr_stat(unsigned long long* ctr, int idx, uint32_t block) {
+  return ctr + (uint64_t)(block % CTR_SHARDS) * CTR_N + idx;
+}
 
 constexpr uint32_t LEAF_SHORT_MAX = 135;  // one Keccak block: the transposed leaf layout
 constexpr uint32_t LEAF_WORDS = 17;
