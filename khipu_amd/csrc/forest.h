@@ -149,9 +149,13 @@ KH_HD uint32_t seg_of(const uint32_t* tries, uint32_t nt, uint32_t t) {
   return lo;
 }
 
+KH_HD void elem_fill(const Recs& R, uint32_t r, uint32_t seg, const Elems& E, uint64_t e);
 template <typename PushFn>
 KH_HD void elem_from_record(const Recs& R, uint32_t r, uint32_t seg, const Elems& E, PushFn push) {
-  const uint64_t e = push();
+  elem_fill(R, r, seg, E, push());
+}
+// element e from record r (e claimed from E.n by the caller)
+KH_HD void elem_fill(const Recs& R, uint32_t r, uint32_t seg, const Elems& E, uint64_t e) {
   if (e >= E.cap) return;  // the host sized the buffer; overflow flagged by the counter
   for (int q = 0; q < 4; ++q) E.key[4 * e + q] = R.rk[4ull * r + q];
   E.seg[e] = seg;

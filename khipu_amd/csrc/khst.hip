@@ -1823,7 +1823,9 @@ __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32
   if (o >= O.n) return;
   // ctr[0] touched list size, [1] replaced leaves, [2] error
   auto mark = [&](uint32_t r) {
-    if (atomicExch(&touched[r], 1u) == 0u) tlist[atomicAdd(&ctr[0], 1ULL)] = r;
+    const bool first = atomicExch(&touched[r], 1u) == 0u;
+    const uint64_t slot = wave_claim(&ctr[0], first);
+    if (first) tlist[slot] = r;
   };
   const uint64_t* K = O.key + 4 * o;
   const uint32_t t = O.trie[o];
@@ -1907,27 +1909,28 @@ __global__ void __launch_bounds__(BS) k_f_gather(AMap M, Recs R, const uint32_t*
                                                  uint32_t nt, Elems E, unsigned long long* ctr) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= ntl) return;
-  auto push = [&]() { return (uint64_t)atomicAdd(E.n, 1ULL); };
   // touched is u32 here; forest.h's gather reads it as a flag
   const uint32_t r = tlist[i];
   if (R.rlive[r] != REC_LIVE) return;
   const uint32_t t = R.rt[r], seg = seg_of(tries, nt, t), db = R.rdb[r];
   if (db == EL_LEAF) {
-    if (!replaced[r]) elem_from_record(R, r, seg, E, push);
+    const bool want = !replaced[r];
+    const uint64_t e = wave_claim(E.n, want);
+    if (want) elem_fill(R, r, seg, E, e);
     return;
   }
   const uint32_t mask = R.rmask[r];
   uint64_t ck[4] = {R.rk[4ull * r], R.rk[4ull * r + 1], R.rk[4ull * r + 2], R.rk[4ull * r + 3]};
-  for (uint32_t v = 0; v < 16; ++v) {
-    if (!((mask >> v) & 1)) continue;
-    set_nibble(ck, db, v);
-    const uint32_t cr = map_find(M, R, t, db + 1, ck);
-    if (cr == NONE) {
-      ctr[2] = 4;
-      continue;
+  for (uint32_t v = 0; v < 16; ++v) {  // every lane runs all 16 steps: one claim per wave per step
+    uint32_t cr = NONE;
+    if ((mask >> v) & 1) {
+      set_nibble(ck, db, v);
+      cr = map_find(M, R, t, db + 1, ck);
+      if (cr == NONE) ctr[2] = 4;
     }
-    if (touched[cr]) continue;
-    elem_from_record(R, cr, seg, E, push);
+    const bool want = cr != NONE && !touched[cr];
+    const uint64_t e = wave_claim(E.n, want);
+    if (want) elem_fill(R, cr, seg, E, e);
   }
 }
 __global__ void k_f_gather_roots(AMap M, Recs R, const uint32_t* touched, const uint32_t* tries, uint32_t nt, Elems E) {

@@ -20,6 +20,20 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return lane == 0 ? 0ULL : (~0ULL >> (64 - lane));
 }
 
+// One atomicAdd per wave: the active lanes with `want` get consecutive slots of *ctr (a
+// counter shared by a whole grid would otherwise serialise one atomic per lane).  Every
+// active lane must call it (divergent paths aggregate among their own lanes).
+__device__ __forceinline__ uint64_t wave_claim(unsigned long long* ctr, bool want) {
+  const uint64_t m = __ballot(want);
+  if (m == 0) return 0;
+  const int leader = __ffsll((long long)m) - 1;
+  unsigned long long base = 0;
+  if ((int)__lane_id() == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(m));
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)base, leader);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(base >> 32), leader);
+  return (((uint64_t)hi << 32) | lo) + (uint64_t)__popcll(m & lanemask_lt());
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
