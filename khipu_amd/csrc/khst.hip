@@ -1562,7 +1562,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // ---- phase-2 workspace: child records + node arena
   // leaf encodings are kept (transposed message slots) for the write-back, element and
   // variable-key builds (the plain root build hashed its leaves in LDS)
-  const bool lmsgs = A.emit || A.kn;
+  const bool lmsgs = A.emit || A.kn || A.el;
   const uint64_t lmsg_words = lmsgs ? (uint64_t)LEAF_WORDS * m : 0;
   const uint64_t bmsg_words = A.emit ? (uint64_t)BR_WORDS * B : 0, xmsg_words = A.emit ? (uint64_t)EXT_WORDS * B : 0;
   c->ws2.ensure(carve_size({C * 32, C * 2, lmsg_words * 8, lf_bytes + 64, bmsg_words * 8, xmsg_words * 8}));
@@ -2513,8 +2513,10 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   const bool keep_em = h->flags & KH_EMIT_NODES;
   if (ne) {
     ElemArgs EA{E.db, E.bref, E.brl, E.oldd, E.cref, E.crl, &h->elout, &h->eloutb};
+    // encodings are kept (emit path) only when the handle hands out its write-back set;
+    // otherwise the fused branch levels (one launch per level, no message arena)
     BuildArgs A{(const uint8_t*)E.key, 32, (const uint8_t*)h->heap.p, (const uint64_t*)E.vo, ne,
-                nt > 1 ? (const uint32_t*)E.seg : nullptr, nt, 0, 0, true};
+                nt > 1 ? (const uint32_t*)E.seg : nullptr, nt, 0, 0, keep_em};
     A.vlen = E.vl;
     A.el = &EA;
     run_build(c, A, O2, &bst);
