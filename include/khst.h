@@ -120,8 +120,10 @@ int kh_list_roots(const uint8_t* items, const uint64_t* off, const uint64_t* seg
  * point-to-point (xGMI), every owner builds its subtries from nibble 1, and the 16
  * references are folded into the root branch.  Devices must be distinct for the RCCL
  * exchange; a list that repeats a device runs several shards on it (device copies).
+ * The keys are exchanged first; the value lengths and bytes follow on a stream of their
+ * own while every owner sorts its keys and derives the topology.
  * stats: sums over the shards; t_keys_ms / t_sort_ms / t_total_ms are the host wall
- * times of stage+hash+partition / exchange / the whole call.  Host buffers. */
+ * times of stage+hash+partition / key exchange / the whole call.  Host buffers. */
 int kh_trie_root_sharded(const int* devices, int ngpus, const uint8_t* keys, uint32_t klen, const uint8_t* vals,
                          const uint64_t* voff, uint64_t n, uint32_t flags, uint8_t root32[32], kh_stats* stats);
 
@@ -164,6 +166,16 @@ int kh_dev_trie_build(kh_ctx* ctx, const uint8_t* d_keys, uint32_t klen, const u
                       uint32_t flags, uint8_t* h_hash32, uint32_t* h_enc_len, uint8_t* h_inline32,
                       kh_stats* stats);
 
+/* kh_dev_trie_build whose values arrive later (the multi-GPU exchange): the keys must be
+ * in place when it is called; d_vals / d_voff are read only after the HIP event
+ * vals_ready (a hipEvent_t recorded on any stream of the context's device; NULL = ready)
+ * has completed, so the key sort and the branch topology run while the values are
+ * still in flight. */
+int kh_dev_trie_build_ev(kh_ctx* ctx, void* vals_ready, const uint8_t* d_keys, uint32_t klen,
+                         const uint8_t* d_vals, const uint64_t* d_voff, uint64_t n, const uint32_t* d_seg,
+                         uint64_t nseg, uint32_t depth0, uint32_t flags, uint8_t* h_hash32, uint32_t* h_enc_len,
+                         uint8_t* h_inline32, kh_stats* stats);
+
 /* Fold 16 capped top-nibble references (as produced by kh_dev_trie_build with depth0 = 1,
  * gathered from every shard) into the root: kec256(RLP[ref_0..ref_15, ""]).
  * Requires >= 2 non-empty references (otherwise the root is not a branch: returns KH_EINVAL
@@ -178,7 +190,8 @@ int kh_dev_hash_keys(kh_ctx* ctx, const uint8_t* d_keys, uint32_t klen, uint64_t
  * owner = top nibble * nparts / 16 (nparts <= 16).  Writes the records grouped by owner
  * (input order kept inside a group, so later puts still win after the exchange):
  * d_out_keys (n*32 B), d_out_vals (total value bytes), d_out_vlen (n value lengths);
- * h_counts[p] / h_bytes[p] = records / value bytes for owner p (host). */
+ * h_counts[p] / h_bytes[p] = records / value bytes for owner p (host).  d_keys32, d_voff,
+ * d_out_keys, d_out_vals and d_out_vlen must be 8-byte aligned (KH_EINVAL otherwise). */
 int kh_dev_partition(kh_ctx* ctx, const uint8_t* d_keys32, const uint8_t* d_vals, const uint64_t* d_voff,
                      uint64_t n, uint32_t nparts, uint8_t* d_out_keys, uint8_t* d_out_vals, uint64_t* d_out_vlen,
                      uint64_t* h_counts, uint64_t* h_bytes);

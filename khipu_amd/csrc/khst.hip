@@ -869,7 +869,6 @@ __global__ void __launch_bounds__(BS) k_emit_copy(Topo T, uint64_t B, const uint
 // gathers (resident merge, multi-GPU partition) are HBM-bound; one thread per span
 // left them at <1 TB/s.
 constexpr uint32_t CG = 8;
-constexpr uint64_t PART_BLOCKS = 256 * 16;  // k_part_copy: 16 blocks per CU
 __device__ __forceinline__ void copy_bytes_group(uint8_t* dst, const uint8_t* src, uint64_t L, uint32_t lane) {
   uint64_t hb = (8 - ((uintptr_t)dst & 7)) & 7;
   if (hb > L) hb = L;
@@ -885,46 +884,96 @@ __device__ __forceinline__ void copy_bytes_group(uint8_t* dst, const uint8_t* sr
 __device__ __forceinline__ uint32_t nibble_owner(uint64_t w0, uint32_t nparts) {
   return (((uint32_t)(w0 & 0xFF) >> 4) * nparts) >> 4;
 }
-__global__ void __launch_bounds__(BS) k_owner_key(const uint64_t* K, uint64_t n, uint32_t nparts, uint64_t* ck,
-                                                  uint32_t* idx) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i >= n) return;
-  ck[i] = nibble_owner(K[4 * i], nparts);
-  idx[i] = (uint32_t)i;
+// Stable partition in source order, three passes over tiles of PT_TILE consecutive
+// records: k_part_count (records per owner per tile), an exclusive scan of that
+// owner-major table (= the first destination of every (owner, tile)), k_part_place
+// (each record's destination: the tile base + its rank among the tile's earlier records
+// of the same owner; keys and lengths written there), a scan of the placed lengths
+// (value byte offsets), then k_part_vcopy copies the value spans in source order
+// (coalesced reads; each record's bytes go to one contiguous destination run).
+constexpr uint32_t PT_R = 8;
+constexpr uint64_t PT_TILE = (uint64_t)BS * PT_R;
+constexpr uint32_t PT_WAVES = BS / 64;
+// lanes of this wave with the same owner (owners < 32; invalid lanes excluded)
+__device__ __forceinline__ uint64_t owner_match(bool ok, uint32_t o) {
+  uint64_t mask = __ballot(ok);
+  for (int b = 0; b < 5; ++b) {
+    const bool bit = (o >> b) & 1;
+    const uint64_t m = __ballot(ok && bit);
+    mask &= bit ? m : ~m;
+  }
+  return mask;
 }
-__global__ void __launch_bounds__(BS) k_part_len(const uint32_t* idx, const uint64_t* voff, uint64_t n,
-                                                 uint64_t* vlen) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i >= n) return;
-  uint32_t s = idx[i];
-  vlen[i] = voff[s + 1] - voff[s];
-}
-__global__ void __launch_bounds__(BS) k_part_copy(const uint64_t* K, const uint8_t* vals, const uint64_t* voff,
-                                                  const uint32_t* idx, const uint64_t* ooff, uint64_t n,
-                                                  const uint64_t* ck, uint64_t* okeys, uint8_t* ovals,
-                                                  unsigned long long* cnt, unsigned long long* bytes) {
-  __shared__ unsigned long long c[16], b[16];
-  if (threadIdx.x < 16) c[threadIdx.x] = b[threadIdx.x] = 0;
+__global__ void __launch_bounds__(BS) k_part_count(const uint64_t* K, uint64_t n, uint32_t nparts, uint32_t ntile,
+                                                   uint32_t* hist) {
+  __shared__ uint32_t c[16];
+  if (threadIdx.x < 16) c[threadIdx.x] = 0;
   __syncthreads();
-  // grid-stride over records (PART_BLOCKS blocks): the per-block owner counters are
-  // flushed with 2 global atomics per owner, so the block count must stay small
-  const uint32_t lane = threadIdx.x % CG;
-  for (uint64_t i = ((uint64_t)blockIdx.x * BS + threadIdx.x) / CG; i < n; i += (uint64_t)gridDim.x * (BS / CG)) {
-    uint32_t s = idx[i];
-    if (lane < 4) okeys[4 * i + lane] = K[4 * (uint64_t)s + lane];
-    uint64_t o = voff[s], L = voff[s + 1] - o;
-    copy_bytes_group(ovals + ooff[i], vals + o, L, lane);
-    if (lane == 0) {
-      uint32_t p = (uint32_t)ck[i];
-      atomicAdd(&c[p], 1ULL);
-      atomicAdd(&b[p], (unsigned long long)L);
+  const uint64_t t0 = (uint64_t)blockIdx.x * PT_TILE;
+  for (uint32_t r = 0; r < PT_R; ++r) {
+    const uint64_t i = t0 + r * BS + threadIdx.x;
+    const bool ok = i < n;
+    const uint32_t o = ok ? nibble_owner(K[4 * i], nparts) : 0;
+    const uint64_t mask = owner_match(ok, o);
+    if (ok && (mask & lanemask_lt()) == 0) atomicAdd(&c[o], (uint32_t)__popcll(mask));  // one add per group
+  }
+  __syncthreads();
+  if (threadIdx.x < nparts) hist[(uint64_t)threadIdx.x * ntile + blockIdx.x] = c[threadIdx.x];
+}
+__global__ void __launch_bounds__(BS) k_part_place(const uint64_t* K, const uint64_t* voff, uint64_t n,
+                                                   uint32_t nparts, uint32_t ntile, const uint32_t* base,
+                                                   uint64_t* okeys, uint64_t* olen, uint32_t* pos) {
+  __shared__ uint32_t run[16];
+  __shared__ uint32_t wc[PT_WAVES][16];
+  const uint32_t wv = threadIdx.x >> 6;
+  if (threadIdx.x < 16) run[threadIdx.x] = threadIdx.x < nparts ? base[(uint64_t)threadIdx.x * ntile + blockIdx.x] : 0;
+  const uint64_t t0 = (uint64_t)blockIdx.x * PT_TILE;
+  for (uint32_t r = 0; r < PT_R; ++r) {
+    if (threadIdx.x < PT_WAVES * 16) wc[threadIdx.x >> 4][threadIdx.x & 15] = 0;
+    __syncthreads();
+    const uint64_t i = t0 + r * BS + threadIdx.x;
+    const bool ok = i < n;
+    const uint32_t o = ok ? nibble_owner(K[4 * i], nparts) : 0;
+    const uint64_t mask = owner_match(ok, o);
+    const uint32_t rk = (uint32_t)__popcll(mask & lanemask_lt());
+    if (ok && rk == 0) wc[wv][o] = (uint32_t)__popcll(mask);
+    __syncthreads();
+    if (ok) {
+      uint32_t d = run[o] + rk;
+      for (uint32_t w = 0; w < wv; ++w) d += wc[w][o];
+      pos[i] = d;
+      for (int q = 0; q < 4; ++q) okeys[4 * (uint64_t)d + q] = K[4 * i + q];
+      olen[d] = voff[i + 1] - voff[i];
     }
+    __syncthreads();
+    if (threadIdx.x < nparts) {
+      uint32_t t = 0;
+      for (uint32_t w = 0; w < PT_WAVES; ++w) t += wc[w][threadIdx.x];
+      run[threadIdx.x] += t;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  if (threadIdx.x < 16 && c[threadIdx.x]) {
-    atomicAdd(&cnt[threadIdx.x], c[threadIdx.x]);
-    atomicAdd(&bytes[threadIdx.x], b[threadIdx.x]);
-  }
+}
+// Value spans to their placed offsets, in source order: one CG-lane group per record
+// (consecutive groups read consecutive source bytes)
+__global__ void __launch_bounds__(BS) k_part_vcopy(const uint8_t* vals, const uint64_t* voff, const uint32_t* pos,
+                                                   const uint64_t* ooff, uint64_t n, uint8_t* ovals) {
+  const uint64_t i = ((uint64_t)blockIdx.x * BS + threadIdx.x) / CG;
+  const uint32_t lane = threadIdx.x % CG;
+  if (i >= n) return;
+  const uint64_t o = voff[i];
+  copy_bytes_group(ovals + ooff[pos[i]], vals + o, voff[i + 1] - o, lane);
+}
+// records and value bytes per owner, from the owner-major scanned tile table (base) and
+// the byte offsets of the placed records (ooff, *tot their total)
+__global__ void k_part_bounds(const uint32_t* base, uint32_t ntile, const uint64_t* ooff, const uint64_t* tot,
+                              uint64_t n, uint32_t nparts, unsigned long long* cnt, unsigned long long* bytes) {
+  const uint32_t p = threadIdx.x;
+  if (p >= nparts) return;
+  const uint64_t a = base[(uint64_t)p * ntile];
+  const uint64_t b = p + 1 < nparts ? base[(uint64_t)(p + 1) * ntile] : n;
+  cnt[p] = b - a;
+  bytes[p] = (b < n ? ooff[b] : *tot) - (a < n ? ooff[a] : *tot);
 }
 
 __global__ void __launch_bounds__(BS) k_synth_len(uint32_t cfg, uint64_t first, uint64_t n, uint64_t* voff) {
@@ -1021,6 +1070,7 @@ struct BuildArgs {
   const uint32_t* vlen = nullptr;  // per-input value lengths (element builds: spans in a value heap)
   const uint8_t* kn = nullptr;     // variable-length keys (zero-padded to 32 B): nibble counts (list tries)
   struct ElemArgs* el = nullptr;   // element build of a resident forest commit (forest.h; nullable)
+  hipEvent_t vals_ready = nullptr; // the values / offsets land later (multi-GPU exchange): wait before reading them
 };
 // element build (forest.h): inputs are leaves and subtree elements; the capped reference
 // of every element node, branch and extension is kept for the forest's records
@@ -1428,6 +1478,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     T.svoff = nullptr;
     T.svlen = nullptr;
   } else {
+    if (A.vals_ready) HIPCHK(hipStreamWaitEvent(st, A.vals_ready, 0));
     hipLaunchKernelGGL(k_val_gather, GRID(m, BS), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
   }
@@ -1481,6 +1532,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, s2));                  // every leaf a hash unless it says otherwise
     hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, s2, T);
     LAUNCH_CHECK();
+    if (A.vals_ready) HIPCHK(hipStreamWaitEvent(s2, A.vals_ready, 0));  // the topology need not wait
     HIPCHK(hipEventRecord(c->ev[9], s2));
     hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, s2, T, n);
     LAUNCH_CHECK();
@@ -2936,10 +2988,19 @@ int kh_trie_root_nodes(const uint8_t* keys, uint32_t klen, const uint8_t* vals, 
 int kh_dev_trie_build(kh_ctx* c, const uint8_t* d_keys, uint32_t klen, const uint8_t* d_vals, const uint64_t* d_voff,
                       uint64_t n, const uint32_t* d_seg, uint64_t nseg, uint32_t depth0, uint32_t flags,
                       uint8_t* h_hash32, uint32_t* h_enc_len, uint8_t* h_inline32, kh_stats* stats) {
+  return kh_dev_trie_build_ev(c, nullptr, d_keys, klen, d_vals, d_voff, n, d_seg, nseg, depth0, flags, h_hash32,
+                              h_enc_len, h_inline32, stats);
+}
+
+int kh_dev_trie_build_ev(kh_ctx* c, void* vals_ready, const uint8_t* d_keys, uint32_t klen, const uint8_t* d_vals,
+                         const uint64_t* d_voff, uint64_t n, const uint32_t* d_seg, uint64_t nseg, uint32_t depth0,
+                         uint32_t flags, uint8_t* h_hash32, uint32_t* h_enc_len, uint8_t* h_inline32,
+                         kh_stats* stats) {
   if (!c) return set_err(KH_EINVAL, "null context");
   API_TRY({
     HIPCHK(hipSetDevice(c->dev));
     BuildArgs A{d_keys, klen, d_vals, d_voff, n, d_seg, d_seg ? nseg : 1, depth0, flags, false};
+    A.vals_ready = (hipEvent_t)vals_ready;
     BuildOut O;
     run_build(c, A, O, stats);
     uint64_t nres = O.res_len.size();
@@ -2992,33 +3053,33 @@ int kh_dev_partition(kh_ctx* c, const uint8_t* d_keys32, const uint8_t* d_vals, 
     memset(h_bytes, 0, nparts * 8);
     if (n == 0) return KH_OK;
     if (n >= (1ULL << 31)) throw KhError{KH_EINVAL, "n must be < 2^31 per device"};
+    if ((uintptr_t)d_keys32 & 7 || (uintptr_t)d_out_keys & 7 || (uintptr_t)d_voff & 7 || (uintptr_t)d_out_vlen & 7 ||
+        (uintptr_t)d_out_vals & 7)
+      throw KhError{KH_EINVAL, "partition: keys, offsets, lengths and the value output must be 8-byte aligned"};
     hipStream_t st = c->st;
-    c->ws3.ensure(carve_size({n * 8, n * 8, n * 4, n * 4, n * 8, radix_scratch_bytes(n), scan_scratch_bytes(n, 8),
-                              256}));
+    const uint32_t ntile = (uint32_t)((n + PT_TILE - 1) / PT_TILE);
+    const uint64_t nh = (uint64_t)nparts * ntile;
+    c->ws3.ensure(carve_size({nh * 4, n * 4, n * 8, scan_scratch_bytes(std::max<uint64_t>(n, nh), 8), 40 * 8}));
     Carver cv{(char*)c->ws3.p, 0, c->ws3.cap};
-    uint64_t* ck0 = cv.take<uint64_t>(n);
-    uint64_t* ck1 = cv.take<uint64_t>(n);
-    uint32_t* i0 = cv.take<uint32_t>(n);
-    uint32_t* i1 = cv.take<uint32_t>(n);
+    uint32_t* hist = cv.take<uint32_t>(nh);
+    uint32_t* pos = cv.take<uint32_t>(n);
     uint64_t* ooff = cv.take<uint64_t>(n);
-    void* rs = cv.take<char>(radix_scratch_bytes(n));
-    void* sc = cv.take<char>(scan_scratch_bytes(n, 8));
-    unsigned long long* tot = cv.take<unsigned long long>(32);
+    void* sc = cv.take<char>(scan_scratch_bytes(std::max<uint64_t>(n, nh), 8));
+    unsigned long long* tot = cv.take<unsigned long long>(40);  // counts | bytes | byte total
     const uint64_t* K = (const uint64_t*)d_keys32;
-    hipLaunchKernelGGL(k_owner_key, GRID(n, BS), dim3(BS), 0, st, K, n, nparts, ck0, i0);
+    hipLaunchKernelGGL(k_part_count, dim3(ntile), dim3(BS), 0, st, K, n, nparts, ntile, hist);
     LAUNCH_CHECK();
-    if (radix_sort_pairs(ck0, i0, ck1, i1, n, 0, 8, rs, st)) {  // one stable pass
-      std::swap(ck0, ck1);
-      std::swap(i0, i1);
-    }
-    hipLaunchKernelGGL(k_part_len, GRID(n, BS), dim3(BS), 0, st, (const uint32_t*)i0, d_voff, n, d_out_vlen);
+    scan_exclusive<uint32_t>(hist, hist, nh, (uint32_t*)nullptr, sc, st);
+    hipLaunchKernelGGL(k_part_place, dim3(ntile), dim3(BS), 0, st, K, d_voff, n, nparts, ntile,
+                       (const uint32_t*)hist, (uint64_t*)d_out_keys, d_out_vlen, pos);
     LAUNCH_CHECK();
-    scan_exclusive<uint64_t>(d_out_vlen, ooff, n, (uint64_t*)nullptr, sc, st);
+    scan_exclusive<uint64_t>(d_out_vlen, ooff, n, (uint64_t*)(tot + 32), sc, st);
+    hipLaunchKernelGGL(k_part_vcopy, GRID(n * CG, BS), dim3(BS), 0, st, d_vals, d_voff, (const uint32_t*)pos,
+                       (const uint64_t*)ooff, n, d_out_vals);
+    LAUNCH_CHECK();
     HIPCHK(hipMemsetAsync(tot, 0, 256, st));
-    const unsigned pgrid = (unsigned)std::min<uint64_t>(PART_BLOCKS, (n * CG + BS - 1) / BS);
-    hipLaunchKernelGGL(k_part_copy, dim3(pgrid), dim3(BS), 0, st, K, d_vals, d_voff, (const uint32_t*)i0,
-                       (const uint64_t*)ooff, n, (const uint64_t*)ck0, (uint64_t*)d_out_keys, d_out_vals, tot,
-                       tot + 16);
+    hipLaunchKernelGGL(k_part_bounds, dim3(1), dim3(64), 0, st, (const uint32_t*)hist, ntile, (const uint64_t*)ooff,
+                       (const uint64_t*)(tot + 32), n, nparts, tot, tot + 16);
     LAUNCH_CHECK();
     HIPCHK(hipMemcpyAsync(c->h_pinned, tot, 256, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));

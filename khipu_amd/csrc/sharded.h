@@ -8,9 +8,12 @@
 //      hashed there (KH_HASH_KEYS), and its records partitioned by owner
 //      (kh_dev_partition: one stable 8-bit radix pass + a value copy);
 //   2. exchange: every (source, owner) block of keys, value lengths and value bytes goes
-//      over RCCL point-to-point (ncclSend / ncclRecv fused in one group: xGMI links,
-//      no host staging), received source-major so "later put wins" holds;
-//   3. device g builds its nibbles' subtries from depth 1 (run_build, depth0 = 1);
+//      over RCCL point-to-point (ncclSend / ncclRecv fused in groups: xGMI links, no host
+//      staging), received source-major so "later put wins" holds.  The keys go first;
+//      the lengths and value bytes follow on a stream of their own;
+//   3. device g builds its nibbles' subtries from depth 1 (run_build, depth0 = 1) as soon
+//      as its keys have landed: the key sort and the branch topology run while the
+//      values are still in flight, the leaf stage waits for them (BuildArgs.vals_ready);
 //   4. the 16 capped references are folded into the root branch on the host
 //      (kh_fold_root16; MerklePatriciaTrie.scala:169: the root is always hashed).
 // The reference-counts exchange and the 16-reference gather need no collective: one
@@ -70,7 +73,14 @@ static Rccl& rccl() {
 // per-shard state, kept between calls (HBM buffers grow, never shrink)
 struct Shard {
   kh_ctx* c = nullptr;  // private context (shards may share a device)
-  DevBuf k32, pk, pv, pl, rk, rv, rl, rvo;
+  DevBuf k32, pk, pv, pl, rk, rv, rl, rvo, vscan;
+  hipStream_t cs = nullptr;      // value exchange + offsets (beside the build's streams)
+  hipEvent_t ev_vals = nullptr;  // ... done
+  ~Shard() {
+    if (cs) (void)hipStreamDestroy(cs);
+    if (ev_vals) (void)hipEventDestroy(ev_vals);
+    if (c) kh_ctx_destroy(c);
+  }
   uint64_t lo = 0, n = 0;            // input slice
   uint64_t cnt[16] = {}, nb[16] = {};  // records / value bytes for each owner
   uint64_t m = 0, mb = 0;            // received records / value bytes
@@ -126,7 +136,12 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
       delete S[g];
       S[g] = g_shards[g] = new Shard();
     }
-    if (!S[g]->c) S[g]->c = ctx_new(dev[g]);
+    if (!S[g]->c) {
+      S[g]->c = ctx_new(dev[g]);
+      HIPCHK(hipSetDevice(dev[g]));
+      HIPCHK(hipStreamCreateWithFlags(&S[g]->cs, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&S[g]->ev_vals, hipEventDisableTiming));
+    }
     S[g]->lo = n * g / N;
     S[g]->n = n * (g + 1) / N - S[g]->lo;
   }
@@ -196,28 +211,45 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
     }
   }
   const auto t1 = std::chrono::steady_clock::now();
+  for (uint32_t p = 0; p < N; ++p) S[p]->vscan.ensure(scan_scratch_bytes(S[p]->m, 8) + 256);
+  // the offsets of the received values, on the shard's exchange stream once its lengths
+  // and bytes have landed; the build's leaf stage waits for ev_vals
+  auto value_offsets = [&](Shard& s) {
+    HIPCHK(hipSetDevice(s.c->dev));
+    if (s.m)
+      scan_exclusive<uint64_t>((const uint64_t*)s.rl.p, (uint64_t*)s.rvo.p, s.m, (uint64_t*)s.rvo.p + s.m, s.vscan.p,
+                               s.cs);
+    HIPCHK(hipEventRecord(s.ev_vals, s.cs));
+  };
   if (distinct) {
     Rccl& R = rccl();
-    NCCLCHK(R.GroupStart());
-    for (uint32_t g = 0; g < N; ++g)
-      for (uint32_t p = 0; p < N; ++p) {
-        const uint64_t c = S[g]->cnt[p], b = S[g]->nb[p];
-        if (!c) continue;  // both sides know the block sizes
-        Shard& src = *S[g];
-        Shard& dst = *S[p];
-        ncclComm_t cs = (*comms)[g], cd = (*comms)[p];
-        NCCLCHK(R.Send((uint8_t*)src.pk.p + soff[g * N + p] * 32, c * 32, ncclUint8, (int)p, cs, src.c->st));
-        NCCLCHK(R.Recv((uint8_t*)dst.rk.p + roff[p * N + g] * 32, c * 32, ncclUint8, (int)g, cd, dst.c->st));
-        NCCLCHK(R.Send((uint64_t*)src.pl.p + soff[g * N + p], c, ncclUint64, (int)p, cs, src.c->st));
-        NCCLCHK(R.Recv((uint64_t*)dst.rl.p + roff[p * N + g], c, ncclUint64, (int)g, cd, dst.c->st));
-        if (b) {
-          NCCLCHK(R.Send((uint8_t*)src.pv.p + sboff[g * N + p], b, ncclUint8, (int)p, cs, src.c->st));
-          NCCLCHK(R.Recv((uint8_t*)dst.rv.p + rboff[p * N + g], b, ncclUint8, (int)g, cd, dst.c->st));
+    for (int part = 0; part < 2; ++part) {  // 0: keys (build streams), 1: lengths + values (exchange streams)
+      NCCLCHK(R.GroupStart());
+      for (uint32_t g = 0; g < N; ++g)
+        for (uint32_t p = 0; p < N; ++p) {
+          const uint64_t c = S[g]->cnt[p], b = S[g]->nb[p];
+          if (!c) continue;  // both sides know the block sizes
+          Shard& src = *S[g];
+          Shard& dst = *S[p];
+          ncclComm_t cs = (*comms)[g], cd = (*comms)[p];
+          if (part == 0) {
+            NCCLCHK(R.Send((uint8_t*)src.pk.p + soff[g * N + p] * 32, c * 32, ncclUint8, (int)p, cs, src.c->st));
+            NCCLCHK(R.Recv((uint8_t*)dst.rk.p + roff[p * N + g] * 32, c * 32, ncclUint8, (int)g, cd, dst.c->st));
+            continue;
+          }
+          NCCLCHK(R.Send((uint64_t*)src.pl.p + soff[g * N + p], c, ncclUint64, (int)p, cs, src.cs));
+          NCCLCHK(R.Recv((uint64_t*)dst.rl.p + roff[p * N + g], c, ncclUint64, (int)g, cd, dst.cs));
+          if (b) {
+            NCCLCHK(R.Send((uint8_t*)src.pv.p + sboff[g * N + p], b, ncclUint8, (int)p, cs, src.cs));
+            NCCLCHK(R.Recv((uint8_t*)dst.rv.p + rboff[p * N + g], b, ncclUint8, (int)g, cd, dst.cs));
+          }
         }
-      }
-    NCCLCHK(R.GroupEnd());
+      NCCLCHK(R.GroupEnd());
+    }
+    for (uint32_t g = 0; g < N; ++g) value_offsets(*S[g]);
   } else {
-    // shards sharing devices: same-device or peer copies, ordered on the sources' streams
+    // shards sharing devices: same-device or peer copies, ordered on the sources' streams,
+    // every block landed before any build starts
     for (uint32_t g = 0; g < N; ++g) {
       Shard& src = *S[g];
       HIPCHK(hipSetDevice(dev[g]));
@@ -234,8 +266,13 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
                                     (uint8_t*)src.pv.p + sboff[g * N + p], dev[g], b, src.c->st));
       }
     }
+    for (uint32_t g = 0; g < N; ++g) {
+      HIPCHK(hipSetDevice(dev[g]));
+      HIPCHK(hipStreamSynchronize(S[g]->c->st));
+    }
+    for (uint32_t g = 0; g < N; ++g) value_offsets(*S[g]);
   }
-  for (uint32_t g = 0; g < N; ++g) {  // every block has landed before any build starts
+  for (uint32_t g = 0; g < N; ++g) {  // the keys have landed (the values may still be in flight)
     HIPCHK(hipSetDevice(dev[g]));
     HIPCHK(hipStreamSynchronize(S[g]->c->st));
   }
@@ -253,11 +290,9 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
       s.O.res_inl.assign(16 * 4, 0);
       return;
     }
-    c->ws3.ensure(scan_scratch_bytes(s.m, 8) + 256);
-    scan_exclusive<uint64_t>((const uint64_t*)s.rl.p, (uint64_t*)s.rvo.p, s.m, (uint64_t*)s.rvo.p + s.m, c->ws3.p,
-                             c->st);
     BuildArgs A{(const uint8_t*)s.rk.p, 32, (const uint8_t*)s.rv.p, (const uint64_t*)s.rvo.p, s.m, nullptr, 1, 1, 0,
                 false};
+    A.vals_ready = s.ev_vals;
     run_build(c, A, s.O, &s.st);
   });
   const double t_build = ms_since(t2);
@@ -312,7 +347,7 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
     stats->n_key_perms = (flags & KH_HASH_KEYS) ? n * (uint64_t)(klen / 136 + 1) : 0;
     // host wall clock of the phases (the shards run concurrently)
     stats->t_keys_ms = t_part;   // stage + key hashing + partition
-    stats->t_sort_ms = t_xchg;   // the exchange
+    stats->t_sort_ms = t_xchg;   // the key exchange (the values land during the build)
     stats->t_total_ms = ms_since(t0);
     (void)t_build;
   }

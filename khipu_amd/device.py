@@ -61,17 +61,25 @@ class Ctx:
         self._sync()
         return out[:32 * n]
 
-    def build(self, keys, klen, vals, voff, n, seg=None, nseg=1, depth0=0, hash_keys=False):
-        """Returns (hash32 [nres,32] uint8, enc_len [nres] uint32, inline [nres,32] uint8, KhStats)."""
+    def build(self, keys, klen, vals, voff, n, seg=None, nseg=1, depth0=0, hash_keys=False, vals_ready=None):
+        """Returns (hash32 [nres,32] uint8, enc_len [nres] uint32, inline [nres,32] uint8, KhStats).
+        vals_ready: a torch.cuda.Event after which vals / voff are in place
+        (kh_dev_trie_build_ev); the keys must be in place already, and the build does
+        not synchronise the device first."""
         nres = nseg if seg is not None else (16 if depth0 == 1 else 1)
         hh = np.zeros(32 * nres, np.uint8)
         ll = np.zeros(nres, np.uint32)
         ii = np.zeros(32 * nres, np.uint8)
         st = KhStats()
         flags = _lib.KH_HASH_KEYS if hash_keys else 0
-        self._sync()
-        check(lib().kh_dev_trie_build(self.h, _ptr(keys), klen, _ptr(vals), _ptr(voff), n, _ptr(seg), nseg, depth0,
-                                      flags, hh.ctypes.data, ll.ctypes.data, ii.ctypes.data, ctypes.byref(st)))
+        if vals_ready is None:
+            self._sync()
+            ev = None
+        else:
+            ev = ctypes.c_void_p(vals_ready.cuda_event)
+        check(lib().kh_dev_trie_build_ev(self.h, ev, _ptr(keys), klen, _ptr(vals), _ptr(voff), n, _ptr(seg), nseg,
+                                         depth0, flags, hh.ctypes.data, ll.ctypes.data, ii.ctypes.data,
+                                         ctypes.byref(st)))
         return hh.reshape(nres, 32), ll, ii.reshape(nres, 32), st
 
     def list_roots(self, items, off, seg_off):

@@ -36,6 +36,7 @@ class GpuBackend:
         self.ctx = Ctx(device)
         self.device = torch.device(f"cuda:{device}")
         self.last_stats = None
+        self.overlap = True  # value exchange beside the key sort / topology (exchange())
 
     def hash_keys(self, addr, n, klen=20):
         from ._lib import check, lib
@@ -58,10 +59,18 @@ class GpuBackend:
                                      _ptr(pl), cnt.ctypes.data, nb.ctypes.data))
         return pk, pv, pl, cnt[:nparts].astype(np.int64), nb[:nparts].astype(np.int64)
 
-    def build(self, keys32, vals, voff, n, depth0):
-        hh, ll, ii, st = self.ctx.build(keys32, 32, vals, voff, n, depth0=depth0)
+    def build(self, keys32, vals, voff, n, depth0, vals_ready=None):
+        """vals_ready: a torch.cuda.Event after which vals / voff are in place (the keys
+        must be in place already); the sort and the topology do not wait for it."""
+        hh, ll, ii, st = self.ctx.build(keys32, 32, vals, voff, n, depth0=depth0, vals_ready=vals_ready)
         self.last_stats = st
         return hh, ll, ii
+
+    def event(self):
+        """An event on the current (torch) stream: everything enqueued so far."""
+        e = torch.cuda.Event()
+        e.record()
+        return e
 
     def fold(self, hh, ll, ii):
         from .device import fold_root16
@@ -77,19 +86,22 @@ class GpuBackend:
 A2A_CHUNK = 1 << 30  # bytes per peer per all-to-all round (keeps every count < 2^31)
 
 
-def a2a_bytes(out, inp, out_splits, in_splits, chunk=None):
-    """all_to_all_single of uint8 buffers with per-peer byte splits, in rounds of at
-    most `chunk` bytes per peer so no message count reaches 2^31 (RCCL / c10d take
-    int counts)."""
+def a2a_rounds(biggest, chunk=None):
+    """Rounds a2a_bytes needs for a largest per-peer split of `biggest` bytes over all
+    ranks (every rank must run the same number)."""
+    return int(-(-int(biggest) // (chunk or A2A_CHUNK)))
+
+
+def a2a_bytes(out, inp, out_splits, in_splits, rounds, chunk=None, async_op=False):
+    """all_to_all_single of uint8 buffers with per-peer byte splits, in `rounds` rounds
+    of at most `chunk` bytes per peer so no message count reaches 2^31 (RCCL / c10d
+    take int counts).  async_op: returns the works to wait on (single-round only; the
+    multi-round path copies between rounds and so runs synchronously)."""
     world = len(in_splits)
     chunk = chunk or A2A_CHUNK
-    # every rank must run the same number of rounds: agree on the largest split
-    big = torch.tensor([max(list(out_splits) + list(in_splits) + [0])], dtype=torch.int64, device=inp.device)
-    dist.all_reduce(big, op=dist.ReduceOp.MAX)
-    rounds = int(-(-int(big.item()) // chunk))
     if rounds <= 1:
-        dist.all_to_all_single(out, inp, list(out_splits), list(in_splits))
-        return
+        w = dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), async_op=async_op)
+        return [w] if async_op else []
     ioff = np.concatenate([[0], np.cumsum(in_splits)])
     ooff = np.concatenate([[0], np.cumsum(out_splits)])
     for r in range(rounds):
@@ -103,19 +115,18 @@ def a2a_bytes(out, inp, out_splits, in_splits, chunk=None):
         for p in range(world):
             out[int(ooff[p]) + lo:int(ooff[p]) + lo + osz[p]].copy_(recv[o:o + osz[p]])
             o += osz[p]
+    return []
 
 
 def exchange(be, pkeys, pvals, pvlen, counts, nbytes):
-    """All-to-all of the partitioned records.  Returns (keys32, vals, voff, m) of the
-    records this rank owns, ordered by source rank then source order."""
+    """All-to-all of the partitioned records.  Returns (keys32, vals, voff, m, vals_ready)
+    of the records this rank owns, ordered by source rank then source order.  The keys
+    are in place on return; the value lengths and bytes may still be in flight:
+    vals_ready (a device event, or None when everything has landed) orders the build's
+    value reads after them, so the key sort and the topology overlap the larger
+    transfer."""
     world = dist.get_world_size()
     dev = pkeys.device
-    if world == 1:  # nothing to route
-        m = int(counts[0])
-        voff = torch.zeros(m + 1, dtype=torch.int64, device=dev)
-        if m:
-            torch.cumsum(pvlen[:m], 0, out=voff[1:])
-        return pkeys, pvals, voff, m
     # counts and byte counts in one all-to-all: rank p receives (counts[p], nbytes[p]) pairs
     send = torch.tensor(np.stack([counts, nbytes], 1).reshape(-1).astype(np.int64), device=dev)
     recv = torch.empty_like(send)
@@ -126,17 +137,29 @@ def exchange(be, pkeys, pvals, pvlen, counts, nbytes):
     tot_b = int(rb.sum())
     cl, bl = [int(x) for x in counts], [int(x) for x in nbytes]
     n_send, b_send = sum(cl), sum(bl)
+    # every rank runs the same number of rounds per transfer: agree on the largest splits
+    big = torch.tensor([max(cl + [int(c) for c in rc] + [0]) * 32, max(bl + [int(b) for b in rb] + [0])],
+                       dtype=torch.int64, device=dev)
+    dist.all_reduce(big, op=dist.ReduceOp.MAX)
+    kr, vr = (a2a_rounds(x) for x in big.cpu().tolist())
     rkeys = be.empty(m * 32 + 64)
-    a2a_bytes(rkeys[:m * 32], pkeys[:n_send * 32], [int(c) * 32 for c in rc], [c * 32 for c in cl])
+    a2a_bytes(rkeys[:m * 32], pkeys[:n_send * 32], [int(c) * 32 for c in rc], [c * 32 for c in cl], kr)
+    keys_done = be.event() if be.overlap else None
     rlen = be.empty(max(m, 1), torch.int64)
-    a2a_bytes(rlen[:m].view(torch.uint8), pvlen[:n_send].view(torch.uint8), [int(c) * 8 for c in rc],
-              [c * 8 for c in cl])
     rvals = be.empty(tot_b + 64)
-    a2a_bytes(rvals[:tot_b], pvals[:b_send], [int(b) for b in rb], bl)
+    works = a2a_bytes(rlen[:m].view(torch.uint8), pvlen[:n_send].view(torch.uint8), [int(c) * 8 for c in rc],
+                      [c * 8 for c in cl], kr, async_op=be.overlap)
+    works += a2a_bytes(rvals[:tot_b], pvals[:b_send], [int(b) for b in rb], bl, vr, async_op=be.overlap)
+    for w in works:
+        w.wait()  # the current stream waits; the host does not
     voff = torch.zeros(m + 1, dtype=torch.int64, device=dev)
     if m:
         torch.cumsum(rlen[:m], 0, out=voff[1:])
-    return rkeys, rvals, voff, m
+    if keys_done is None:
+        return rkeys, rvals, voff, m, None
+    vals_ready = be.event()
+    keys_done.synchronize()  # the keys have landed (the values may not have)
+    return rkeys, rvals, voff, m, vals_ready
 
 
 def gather_refs(be, hh, ll, ii):
@@ -178,11 +201,16 @@ def sharded_root(be, addr, vals, voff, n, klen=20, keys_prehashed=False, phases=
 
     keys32 = addr if keys_prehashed else be.hash_keys(addr, n, klen)
     mark()
-    pk, pv, pl, cnt, nb = be.partition(keys32, vals, voff, n, world)
-    mark()
-    rk, rv, ro, m = exchange(be, pk, pv, pl, cnt, nb)
-    mark()
-    hh, ll, ii = be.build(rk, rv, ro, m, depth0=1)
+    if world == 1:  # nothing to route: the build reads the records where they are
+        rk, rv, ro, m, ready = keys32, vals, voff, n, None
+        mark()
+        mark()
+    else:
+        pk, pv, pl, cnt, nb = be.partition(keys32, vals, voff, n, world)
+        mark()
+        rk, rv, ro, m, ready = exchange(be, pk, pv, pl, cnt, nb)
+        mark()
+    hh, ll, ii = be.build(rk, rv, ro, m, depth0=1, vals_ready=None if phases is not None else ready)
     mark()
     H, L, I = gather_refs(be, hh, ll, ii)
     mark()
@@ -211,6 +239,12 @@ def bench_main(args):
     import json
     import os
     import time
+    if "RANK" not in os.environ:  # `bench.py --sharded` without a launcher: a world of one
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -209,6 +209,35 @@ def test_sharded_driver_rccl_world1(khst, oracle):
         dist.destroy_process_group()
 
 
+def test_build_waits_for_late_values(khst, oracle):
+    """kh_dev_trie_build_ev (the multi-GPU exchange's overlap): the values and offsets land
+    on another stream after a delay; the build sorts and derives the topology meanwhile
+    and reads them only after the event.  Without the wait it would hash zero bytes."""
+    import torch
+    from khipu_amd.device import Ctx
+    ctx = Ctx(0)
+    for n in (5_000, 300_000):
+        (h0, _, _, _), (addr, vals, voff) = _device_synth_root(ctx, n, cfg=3)
+        keys = torch.empty(n * 32 + 64, dtype=torch.uint8, device="cuda:0")
+        ctx.build(addr, 20, vals, voff, n, hash_keys=True)  # warm the workspace
+        from khipu_amd._lib import check, lib
+        from khipu_amd.device import _ptr
+        check(lib().kh_dev_hash_keys(ctx.h, _ptr(addr), 20, n, _ptr(keys)))
+        torch.cuda.synchronize()
+        late_v = torch.zeros_like(vals)
+        late_o = torch.zeros_like(voff)
+        side = torch.cuda.Stream()
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(50_000_000)  # ~20 ms of spinning before the copies
+            late_v.copy_(vals)
+            late_o.copy_(voff)
+            ev = torch.cuda.Event()
+            ev.record()
+        hh, _, _, _ = ctx.build(keys, 32, late_v, late_o, n, depth0=0, vals_ready=ev)
+        assert hh[0].tobytes() == h0[0].tobytes(), n
+        torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("koff,voff_shift", [(8, 0), (1, 3), (0, 5)])
 def test_device_build_misaligned_buffers(khst, oracle, koff, voff_shift):
     """Device keys / values at arbitrary byte offsets (the ABI takes plain pointers):
