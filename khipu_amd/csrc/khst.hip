@@ -110,11 +110,11 @@ __global__ void __launch_bounds__(BS) k_hash_keys(const uint8_t* keys, uint32_t 
   for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
 }
 
-// ... and the unsegmented sort key (the key's leading 64 bits, big-endian) with the
+// ... and the unsegmented sort key (the key's leading 32 bits, big-endian) with the
 // identity index in the same pass (saves k_make_ck's re-read of the keys)
 template <bool SHORT>
 __global__ void __launch_bounds__(BS) k_hash_keys_ck(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out,
-                                                     uint64_t* ck, uint32_t* idx, uint64_t base) {
+                                                     uint32_t* ck, uint32_t* idx, uint64_t base) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
   uint64_t h[4];
@@ -123,8 +123,15 @@ __global__ void __launch_bounds__(BS) k_hash_keys_ck(const uint8_t* keys, uint32
   else
     kec256_msg<false>(keys + i * klen, klen, h);
   for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
-  ck[i] = bswap64(h[0]);
+  ck[i] = (uint32_t)(bswap64(h[0]) >> 32);
   idx[i] = (uint32_t)(base + i);
+}
+// the same sort keys for caller-hashed keys
+__global__ void __launch_bounds__(BS) k_make_ck32(const uint64_t* K, uint64_t n, uint32_t* ck, uint32_t* idx) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  ck[i] = (uint32_t)(bswap64(K[4 * i]) >> 32);
+  idx[i] = (uint32_t)i;
 }
 
 // composite sort key: segment id in the top sb bits, then the key's leading bits (big-endian)
@@ -145,15 +152,6 @@ __global__ void __launch_bounds__(BS) k_make_ck(const uint64_t* K, const uint32_
 // (later put last) is kept.  flags |= 2 if equal keys exist (dedup needed),
 // |= 1 if a run exceeds TIE_RUN_MAX (take the full-sort path instead).
 constexpr uint32_t TIE_RUN_MAX = 64;
-// Split hashing + sort (the second half of the keys hashed on st2 beside the first half's
-// radix passes, then a stable merge): OFF by default -- measured at 100M it is slower
-// (57.3 vs 56.0 ms: both halves' hashing slows to ~9.5 ms each beside the radix scatter,
-// the VALU-bound and the LDS/memory-bound kernels do not overlap on the CUs).
-// KHST_SPLIT_MIN=<n> enables it from n keys (the tests run parity cases through it).
-static uint64_t split_min() {
-  const char* e = getenv("KHST_SPLIT_MIN");
-  return e ? strtoull(e, nullptr, 10) : ~0ull;
-}
 // variable-length keys (zero padded, kn nibbles): a key sorts before the longer keys it
 // prefixes, i.e. (padded key, length) order
 __device__ __forceinline__ bool key_less(const uint64_t* a, const uint64_t* b, uint32_t kna = 0, uint32_t knb = 0) {
@@ -201,34 +199,34 @@ __global__ void __launch_bounds__(BS) k_tie_fix(const uint64_t* ck, uint64_t n, 
   if (dup) atomicOr(flags, 2ULL);
 }
 
-// Unsegmented plain builds sort (first key word, index) pairs only; runs of equal top-32
-// bits are ordered here by the whole key (the first word, then the input key through its
-// index), stable, and the sorted keys are gathered later, beside the leaf kernel.
-__device__ __forceinline__ bool ck_less(uint64_t a, uint64_t b, const uint64_t* K, uint32_t ia, uint32_t ib) {
+// Unsegmented plain builds sort (leading 32 key bits, index) pairs only; runs of equal
+// prefixes are ordered here by the whole input key (through the index), stable; the keys
+// themselves are never gathered into sorted order.
+__device__ __forceinline__ bool ck_less(uint32_t a, uint32_t b, const uint64_t* K, uint32_t ia, uint32_t ib) {
   if (a != b) return a < b;
   return key_less(K + 4ull * ia, K + 4ull * ib);
 }
-__device__ __forceinline__ bool ck_equal(uint64_t a, uint64_t b, const uint64_t* K, uint32_t ia, uint32_t ib) {
+__device__ __forceinline__ bool ck_equal(uint32_t a, uint32_t b, const uint64_t* K, uint32_t ia, uint32_t ib) {
   if (a != b) return false;
   const uint64_t* x = K + 4ull * ia;
   const uint64_t* y = K + 4ull * ib;
-  return x[1] == y[1] && x[2] == y[2] && x[3] == y[3];
+  return x[0] == y[0] && x[1] == y[1] && x[2] == y[2] && x[3] == y[3];
 }
-__global__ void __launch_bounds__(BS) k_tie_fix_ck(uint64_t* ck, uint32_t* idx, uint64_t n, const uint64_t* K,
+__global__ void __launch_bounds__(BS) k_tie_fix_ck(uint32_t* ck, uint32_t* idx, uint64_t n, const uint64_t* K,
                                                    unsigned long long* flags) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i + 1 >= n) return;
-  uint32_t hi = (uint32_t)(ck[i] >> 32);
-  if ((uint32_t)(ck[i + 1] >> 32) != hi) return;
-  if (i > 0 && (uint32_t)(ck[i - 1] >> 32) == hi) return;
+  const uint32_t hi = ck[i];
+  if (ck[i + 1] != hi) return;
+  if (i > 0 && ck[i - 1] == hi) return;
   uint64_t e = i + 1;
-  while (e < n && (uint32_t)(ck[e] >> 32) == hi && e - i <= TIE_RUN_MAX) ++e;
+  while (e < n && ck[e] == hi && e - i <= TIE_RUN_MAX) ++e;
   if (e - i > TIE_RUN_MAX) {
     atomicOr(flags, 1ULL);
     return;
   }
   for (uint64_t a = i + 1; a < e; ++a) {
-    const uint64_t c = ck[a];
+    const uint32_t c = ck[a];
     const uint32_t ix = idx[a];
     uint64_t b = a;
     while (b > i && ck_less(c, ck[b - 1], K, ix, idx[b - 1])) {
@@ -243,14 +241,14 @@ __global__ void __launch_bounds__(BS) k_tie_fix_ck(uint64_t* ck, uint32_t* idx, 
   for (uint64_t a = i + 1; a < e; ++a) dup |= ck_equal(ck[a - 1], ck[a], K, idx[a - 1], idx[a]);
   if (dup) atomicOr(flags, 2ULL);
 }
-__global__ void __launch_bounds__(BS) k_dup_ck(const uint64_t* ck, const uint32_t* idx, const uint64_t* K, uint64_t n,
+__global__ void __launch_bounds__(BS) k_dup_ck(const uint32_t* ck, const uint32_t* idx, const uint64_t* K, uint64_t n,
                                                uint32_t* keep) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
   keep[i] = (i + 1 < n && ck_equal(ck[i], ck[i + 1], K, idx[i], idx[i + 1])) ? 0u : 1u;
 }
-__global__ void __launch_bounds__(BS) k_compact_ck(const uint64_t* ck, const uint32_t* idx, const uint32_t* keep_pos,
-                                                   const uint32_t* keep, uint64_t n, uint64_t* ock, uint32_t* oidx) {
+__global__ void __launch_bounds__(BS) k_compact_ck(const uint32_t* ck, const uint32_t* idx, const uint32_t* keep_pos,
+                                                   const uint32_t* keep, uint64_t n, uint32_t* ock, uint32_t* oidx) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n || !keep[i]) return;
   const uint32_t p = keep_pos[i];
@@ -1117,12 +1115,10 @@ struct SortIO {
   void* scan_scratch;
   unsigned long long* ctr;
   const uint8_t* kn;  // variable-length keys: nibble counts (input order; nullable)
-  bool ck_ready = false;  // ck0/idx0 already hold the unsegmented sort keys (k_hash_keys_ck)
-  bool ck_path = false;   // unsegmented plain build: sort (ck, idx) only, gather the keys later
-  const uint64_t* pck = nullptr;  // already sorted on the top 32 bits (the split hash + sort)
-  const uint32_t* pidx = nullptr;
+  bool ck_ready = false;  // ck_path: ck0/idx0 already hold the 32-bit sort keys (k_hash_keys_ck)
+  bool ck_path = false;   // unsegmented plain build: sort (32-bit prefix, idx) only, never gather the keys
   // out
-  const uint64_t* sck = nullptr;  // ck_path: the sorted first key words (skey not gathered yet)
+  const uint32_t* sck = nullptr;  // ck_path: the sorted 32-bit key prefixes (skey not gathered)
   uint64_t m;
   uint32_t* sidx;
   bool fallback;
@@ -1146,35 +1142,33 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
   // ---- 2. sort: LSD radix on the top 32 bits of the composite (segment | key) prefix,
   // then fix the rare runs of equal prefixes locally (k_tie_fix); a full 256-bit sort
   // only if a run is longer than TIE_RUN_MAX (adversarial keys)
-  uint64_t* cks;
-  uint32_t* idxs;
-  if (S.pck) {  // sorted while the keys were hashed (run_build)
-    cks = (uint64_t*)S.pck;
-    idxs = (uint32_t*)S.pidx;
-  } else {
+  uint64_t* cks = nullptr;
+  uint32_t* idxs = nullptr;
+  bool long_run = false;  // the plain path met a run longer than TIE_RUN_MAX: full sort
+  if (S.ck_path) {  // 32-bit prefixes: 8 bytes a pair per radix pass
+    uint32_t* c0 = (uint32_t*)ck0;
+    uint32_t* c1 = (uint32_t*)ck1;
     if (!S.ck_ready) {
-      hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, sb, n, ck0, idx0);
+      hipLaunchKernelGGL(k_make_ck32, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, n, c0, idx0);
       LAUNCH_CHECK();
     }
-    bool flip = radix_sort_pairs(ck0, idx0, ck1, idx1, n, 32, 64, rs_scratch, st);
-    cks = flip ? ck1 : ck0;
+    const bool flip = radix_sort_pairs<uint32_t>(c0, idx0, c1, idx1, n, 0, 32, rs_scratch, st);
+    uint32_t* c32 = flip ? c1 : c0;
     idxs = flip ? idx1 : idx0;
-  }
-  LAUNCH_CHECK();
-  if (S.ck_path) {
-    hipLaunchKernelGGL(k_tie_fix_ck, GRID(n, BS), dim3(BS), 0, st, cks, idxs, n, (const uint64_t*)K32, T.ctr + CTR_TIE);
+    hipLaunchKernelGGL(k_tie_fix_ck, GRID(n, BS), dim3(BS), 0, st, c32, idxs, n, (const uint64_t*)K32, T.ctr + CTR_TIE);
     LAUNCH_CHECK();
     HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const uint64_t tf = c->h_pinned[0];
-    if (!(tf & 1)) {  // no long run: keys stay ungathered
+    long_run = tf & 1;
+    if (!long_run) {
       uint64_t m = n;
-      uint64_t* ock = cks;
+      uint32_t* ock = c32;
       uint32_t* oidx = idxs;
       if (tf & 2) {  // keep the last of equal keys
-        uint32_t* keep = (uint32_t*)(cks == ck0 ? ck1 : ck0);
+        uint32_t* keep = c32 == c0 ? c1 : c0;
         uint32_t* keep_pos = idxs == idx0 ? idx1 : idx0;
-        hipLaunchKernelGGL(k_dup_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, (const uint32_t*)idxs,
+        hipLaunchKernelGGL(k_dup_ck, GRID(n, BS), dim3(BS), 0, st, (const uint32_t*)c32, (const uint32_t*)idxs,
                            (const uint64_t*)K32, n, keep);
         LAUNCH_CHECK();
         uint32_t* mtot = (uint32_t*)(T.ctr + CTR_M);
@@ -1182,11 +1176,11 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
         HIPCHK(hipMemcpyAsync(c->h_pinned, mtot, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         m = (uint32_t)c->h_pinned[0];
-        c->ws3.ensure(carve_size({n * 8, n * 4}));
+        c->ws3.ensure(carve_size({n * 4, n * 4}));
         Carver c3{(char*)c->ws3.p, 0, c->ws3.cap};
-        ock = c3.take<uint64_t>(n);
+        ock = c3.take<uint32_t>(n);
         oidx = c3.take<uint32_t>(n);
-        hipLaunchKernelGGL(k_compact_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, (const uint32_t*)idxs,
+        hipLaunchKernelGGL(k_compact_ck, GRID(n, BS), dim3(BS), 0, st, (const uint32_t*)c32, (const uint32_t*)idxs,
                            (const uint32_t*)keep_pos, (const uint32_t*)keep, n, ock, oidx);
         LAUNCH_CHECK();
       }
@@ -1196,17 +1190,28 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
       S.fallback = false;
       return;
     }
-    // a run longer than TIE_RUN_MAX: the general path below (full sort from the input order)
+  } else {
+    if (!S.ck_ready) {
+      hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, sb, n, ck0, idx0);
+      LAUNCH_CHECK();
+    }
+    bool flip = radix_sort_pairs<uint64_t>(ck0, idx0, ck1, idx1, n, 32, 64, rs_scratch, st);
+    cks = flip ? ck1 : ck0;
+    idxs = flip ? idx1 : idx0;
+    LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, (const uint32_t*)idxs, n,
-                     skey, sseg);
-  LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_tie_fix, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, n, skey, idxs, sseg, S.kn,
-                     T.ctr + CTR_TIE);
-  LAUNCH_CHECK();
-  HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  const uint64_t tie_flags = c->h_pinned[0];
+  uint64_t tie_flags = 1;  // long_run: straight to the full sort
+  if (!long_run) {
+    hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, (const uint32_t*)idxs, n,
+                       skey, sseg);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_tie_fix, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, n, skey, idxs, sseg, S.kn,
+                       T.ctr + CTR_TIE);
+    LAUNCH_CHECK();
+    HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    tie_flags = c->h_pinned[0];
+  }
   const bool fallback = tie_flags & 1, dups = tie_flags & 2;
   uint64_t m = n;
   uint32_t* sidx = idxs;
@@ -1399,47 +1404,16 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   HIPCHK(hipMemsetAsync(T.res_inl, 0, nres * 32, st));
 
   HIPCHK(hipEventRecord(c->ev[0], st));
-  // ---- 1. keys
-  const bool ck_ready = (A.flags & KH_HASH_KEYS) && !segmented;
-  // large hashed builds: the second half of the keys is hashed on st2 while st sorts the
-  // first half (VALU-bound hashing beside the memory-bound radix passes), then the two
-  // sorted halves are merged (stable: the first half's inputs come first)
-  const bool split = ck_ready && !A.kn && n >= 2 && n >= split_min();
-  const uint64_t* pck = nullptr;
-  const uint32_t* pidx = nullptr;
-  auto hash_ck = [&](uint64_t lo, uint64_t cnt, hipStream_t s) {
+  // ---- 1. keys (the plain path takes its 32-bit sort keys from the hashing pass)
+  const bool ck_path = early && !segmented && !A.kn;
+  const bool ck_ready = ck_path && (A.flags & KH_HASH_KEYS);
+  if (ck_ready) {
+    uint32_t* c0 = (uint32_t*)ck0;
     if (A.klen <= 135)
-      hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(cnt, BS), dim3(BS), 0, s, A.keys + lo * A.klen, A.klen, cnt,
-                         K32 + 4 * lo, ck0 + lo, idx0 + lo, lo);
+      hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, c0, idx0, 0ull);
     else
-      hipLaunchKernelGGL(k_hash_keys_ck<false>, GRID(cnt, BS), dim3(BS), 0, s, A.keys + lo * A.klen, A.klen, cnt,
-                         K32 + 4 * lo, ck0 + lo, idx0 + lo, lo);
+      hipLaunchKernelGGL(k_hash_keys_ck<false>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, c0, idx0, 0ull);
     LAUNCH_CHECK();
-  };
-  if (split) {
-    const uint64_t n0 = n / 2, n1 = n - n0;
-    HIPCHK(hipEventRecord(c->ev[11], st));
-    HIPCHK(hipStreamWaitEvent(c->st2, c->ev[11], 0));
-    hash_ck(0, n0, st);
-    hash_ck(n0, n1, c->st2);
-    HIPCHK(hipEventRecord(c->ev[12], c->st2));
-    HIPCHK(hipEventRecord(c->ev[1], st));  // (the key stage is now the first half's hashing)
-    const bool f0 = radix_sort_pairs(ck0, idx0, ck1, idx1, n0, 32, 64, rs_scratch, st);
-    HIPCHK(hipStreamWaitEvent(st, c->ev[12], 0));
-    const bool f1 = radix_sort_pairs(ck0 + n0, idx0 + n0, ck1 + n0, idx1 + n0, n1, 32, 64, rs_scratch, st);
-    if (f0 != f1) throw KhError{KH_EINTERNAL, "split sort: pass parity differs"};
-    uint64_t* ka = f0 ? ck1 : ck0;
-    uint32_t* va = f0 ? idx1 : idx0;
-    uint64_t* ko = f0 ? ck0 : ck1;
-    uint32_t* vo = f0 ? idx0 : idx1;
-    hipLaunchKernelGGL(k_merge_runs, dim3((unsigned)((n + MG_TILE - 1) / MG_TILE)), dim3(MG_THREADS), 0, st,
-                       (const uint64_t*)ka, (const uint32_t*)va, n0, (const uint64_t*)(ka + n0),
-                       (const uint32_t*)(va + n0), n1, ko, vo);
-    LAUNCH_CHECK();
-    pck = ko;
-    pidx = vo;
-  } else if (ck_ready) {
-    hash_ck(0, n, st);
   } else if (A.flags & KH_HASH_KEYS) {
     if (A.klen <= 135)
       hipLaunchKernelGGL(k_hash_keys<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32);
@@ -1449,7 +1423,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   } else if (own_keys) {
     HIPCHK(hipMemcpyAsync(K32, A.keys, n * 32, hipMemcpyDeviceToDevice, st));
   }
-  if (!split) HIPCHK(hipEventRecord(c->ev[1], st));
+  HIPCHK(hipEventRecord(c->ev[1], st));
 
   // ---- 2. sort + dedup
   uint64_t m = n;
@@ -1458,9 +1432,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   {
     SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr,
              A.kn, ck_ready};
-    S.ck_path = early && !segmented && !A.kn;
-    S.pck = pck;
-    S.pidx = pidx;
+    S.ck_path = ck_path;
     sort_dedup(c, S);
     m = S.m;
     sidx = S.sidx;
@@ -1709,7 +1681,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     stats->n_levels = levels;
     stats->full_sort = ties ? 1 : 0;
     // split builds: until both halves are hashed (the second half overlaps the first sort)
-    stats->t_keys_ms = split ? std::max(ev_ms(c->ev[0], c->ev[1]), ev_ms(c->ev[0], c->ev[12])) : ev_ms(c->ev[0], c->ev[1]);
+    stats->t_keys_ms = ev_ms(c->ev[0], c->ev[1]);
     stats->t_sort_ms = ev_ms(c->ev[1], c->ev[2]);
     stats->t_topo_ms = ev_ms(c->ev[2], c->ev[3]);
     // early: the leaf kernel's own span on st2, where it overlaps the topology (the

@@ -146,7 +146,9 @@ void scan_exclusive(const T* in, T* out, uint64_t n, T* total, void* scratch, hi
 }
 
 // ---------------------------------------------------------------------------
-// Radix sort of (uint64 key, uint32 val) pairs on key bits [lo_bit, hi_bit).
+// Radix sort of (key, uint32 val) pairs on key bits [lo_bit, hi_bit); keys are uint64
+// (composite segment | key prefixes) or uint32 (the plain path's 32-bit key prefixes:
+// 8 bytes a pair moved per pass instead of 12).
 // ---------------------------------------------------------------------------
 constexpr int RS_THREADS = 256;
 constexpr int RS_ITEMS = 8;
@@ -154,7 +156,8 @@ constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 2048 keys: 24 KiB of LDS stag
 constexpr int RS_WAVES = RS_THREADS / 64;
 constexpr int RS_WSLICE = RS_TILE / RS_WAVES;   // 512 keys per wave
 
-__global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const uint64_t* keys, uint64_t n, int shift, uint32_t* counts,
+template <typename K>
+__global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const K* keys, uint64_t n, int shift, uint32_t* counts,
                                                         uint32_t ntiles) {
   __shared__ uint32_t h[RS_WAVES][256];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -179,20 +182,21 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const uint64_t* keys, ui
 // LDS in digit order for the whole tile, then written out so that each digit's
 // run of the tile goes to consecutive global addresses (coalesced stores instead
 // of one scattered 8-byte store per key).
-__global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const uint64_t* keys, const uint32_t* vals, uint64_t* okeys,
+template <typename K>
+__global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const uint32_t* vals, K* okeys,
                                                            uint32_t* ovals, uint64_t n, int shift,
                                                            const uint32_t* offs, uint32_t ntiles) {
   __shared__ uint32_t wc[RS_WAVES][256];
   __shared__ uint32_t tstart[256], gbase[256];
   __shared__ uint32_t lw[RS_THREADS / 64];
-  __shared__ uint64_t sk[RS_TILE];
+  __shared__ K sk[RS_TILE];
   __shared__ uint32_t sv[RS_TILE];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&wc[0][0])[i] = 0;
   __syncthreads();
   const uint64_t tbase = (uint64_t)blockIdx.x * RS_TILE;
   const uint64_t base = tbase + (uint64_t)w * RS_WSLICE;
-  uint64_t k[RS_ITEMS];
+  K k[RS_ITEMS];
   uint32_t v[RS_ITEMS];
   uint32_t r[RS_ITEMS];
   const uint64_t lt = lanemask_lt();
@@ -246,7 +250,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const uint64_t* keys,
   __syncthreads();
   const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)RS_TILE ? (n - tbase) : (uint64_t)RS_TILE);
   for (uint32_t li = threadIdx.x; li < tn; li += RS_THREADS) {
-    uint64_t key = sk[li];
+    K key = sk[li];
     uint32_t d = (uint32_t)(key >> shift) & 0xFF;
     uint32_t pos = gbase[d] + (li - tstart[d]);
     okeys[pos] = key;
@@ -263,90 +267,26 @@ inline size_t radix_scratch_bytes(uint64_t n) {
 // Sorts (k0, v0) on bits [lo_bit, hi_bit) (multiples of 8), using (k1, v1) as
 // ping-pong buffers.  Returns true if the result ended in (k1, v1).
 // n must be < 2^32.
-inline bool radix_sort_pairs(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, uint64_t n, int lo_bit,
-                             int hi_bit, void* scratch, hipStream_t st) {
+template <typename K>
+inline bool radix_sort_pairs(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n, int lo_bit, int hi_bit,
+                             void* scratch, hipStream_t st) {
   if (n <= 1) return false;
   uint32_t tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
   uint32_t* counts = (uint32_t*)scratch;
   void* scan_ws = (char*)scratch + (((uint64_t)tiles * 256 * sizeof(uint32_t) + 255) / 256) * 256;
   bool flip = false;
   for (int sh = lo_bit; sh < hi_bit; sh += 8) {
-    uint64_t* ik = flip ? k1 : k0;
+    K* ik = flip ? k1 : k0;
     uint32_t* iv = flip ? v1 : v0;
-    uint64_t* ok = flip ? k0 : k1;
+    K* ok = flip ? k0 : k1;
     uint32_t* ov = flip ? v0 : v1;
-    hipLaunchKernelGGL(k_rs_hist, dim3(tiles), dim3(RS_THREADS), 0, st, (const uint64_t*)ik, n, sh, counts, tiles);
+    hipLaunchKernelGGL(k_rs_hist<K>, dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik, n, sh, counts, tiles);
     scan_exclusive<uint32_t>(counts, counts, (uint64_t)tiles * 256, (uint32_t*)nullptr, scan_ws, st);
-    hipLaunchKernelGGL(k_rs_scatter, dim3(tiles), dim3(RS_THREADS), 0, st, (const uint64_t*)ik, (const uint32_t*)iv, ok,
+    hipLaunchKernelGGL(k_rs_scatter<K>, dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik, (const uint32_t*)iv, ok,
                        ov, n, sh, (const uint32_t*)counts, tiles);
     flip = !flip;
   }
   return flip;
-}
-
-// ---------------------------------------------------------------------------
-// Stable merge of two runs sorted on the top 32 bits of their keys (merge path): run A =
-// (ka, va)[0, na), run B = (kb, vb)[0, nb); on equal top bits A comes first.  One tile of
-// MG_TILE outputs per block: the tile's split is found by a diagonal binary search, its
-// slices of A and B are staged in LDS, then every thread merges MG_ITEMS outputs.
-// ---------------------------------------------------------------------------
-constexpr int MG_THREADS = 256;
-constexpr int MG_ITEMS = 8;
-constexpr int MG_TILE = MG_THREADS * MG_ITEMS;
-
-// number of A elements among the first d outputs (A wins ties)
-template <typename GetA, typename GetB>
-__device__ __forceinline__ uint64_t merge_split(GetA a, GetB b, uint64_t na, uint64_t nb, uint64_t d) {
-  uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;  // take mid + 1 elements of A?
-    if ((a(mid) >> 32) <= (b(d - 1 - mid) >> 32)) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
-__global__ void __launch_bounds__(MG_THREADS) k_merge_runs(const uint64_t* ka, const uint32_t* va, uint64_t na,
-                                                          const uint64_t* kb, const uint32_t* vb, uint64_t nb,
-                                                          uint64_t* ko, uint32_t* vo) {
-  __shared__ uint64_t sk[MG_TILE];
-  __shared__ uint32_t sv[MG_TILE];
-  __shared__ uint64_t s_split[2];
-  const uint64_t n = na + nb;
-  const uint64_t d0 = (uint64_t)blockIdx.x * MG_TILE;
-  const uint64_t d1 = d0 + MG_TILE < n ? d0 + MG_TILE : n;
-  if (threadIdx.x < 2) {
-    const uint64_t d = threadIdx.x ? d1 : d0;
-    s_split[threadIdx.x] = merge_split([&](uint64_t i) { return ka[i]; }, [&](uint64_t i) { return kb[i]; }, na, nb, d);
-  }
-  __syncthreads();
-  const uint64_t a0 = s_split[0], a1 = s_split[1];
-  const uint64_t b0 = d0 - a0, b1 = d1 - a1;
-  const uint32_t la = (uint32_t)(a1 - a0), lb = (uint32_t)(b1 - b0);
-  for (uint32_t t = threadIdx.x; t < la; t += MG_THREADS) {
-    sk[t] = ka[a0 + t];
-    sv[t] = va[a0 + t];
-  }
-  for (uint32_t t = threadIdx.x; t < lb; t += MG_THREADS) {
-    sk[la + t] = kb[b0 + t];
-    sv[la + t] = vb[b0 + t];
-  }
-  __syncthreads();
-  const uint32_t tot = la + lb;
-  const uint32_t e0 = threadIdx.x * MG_ITEMS;
-  if (e0 >= tot) return;
-  const uint32_t e1 = e0 + MG_ITEMS < tot ? e0 + MG_ITEMS : tot;
-  const uint64_t* A = sk;
-  const uint64_t* B = sk + la;
-  uint32_t i = (uint32_t)merge_split([&](uint64_t x) { return A[x]; }, [&](uint64_t x) { return B[x]; }, la, lb, e0);
-  uint32_t j = e0 - i;
-  for (uint32_t e = e0; e < e1; ++e) {
-    const bool takeA = i < la && (j >= lb || (A[i] >> 32) <= (B[j] >> 32));
-    const uint32_t src = takeA ? i : la + j;
-    ko[d0 + e] = sk[src];
-    vo[d0 + e] = sv[src];
-    if (takeA) ++i; else ++j;
-  }
 }
 
 }  // namespace khst

@@ -154,7 +154,7 @@ struct Topo {
   const uint32_t* sidx;   // [m] input index of sorted key i
   const uint32_t* sseg;   // [m] segment id (segmented only)
   const uint8_t* kn;      // [m] key length in nibbles (variable-length key builds; nullable: 64)
-  const uint64_t* sck;    // [m] sorted big-endian first key words (unsegmented plain builds; nullable):
+  const uint32_t* sck;    // [m] sorted big-endian leading 32 key bits (unsegmented plain builds; nullable):
                           //     boundary values come from them before the sorted keys are gathered
   const uint8_t* vals;    // input values
   const uint64_t* voff;   // [n+1] (or [n] offsets with vlen_in)
@@ -271,11 +271,11 @@ KH_HD Slot branch_slot(const Topo& T, uint64_t g, uint32_t d, bool ext) {
 }
 
 // sorted key i where nibbles [0, need) are read: the gathered sorted keys, or on the
-// unsegmented plain path (sck set, no sorted keys materialised) the first word from the
-// sorted prefixes and, past nibble 16, the input key through its index
+// unsegmented plain path (sck set, no sorted keys materialised) the first 8 nibbles from
+// the sorted prefixes and, past them, the input key through its index
 KH_HD Key4 sorted_key(const Topo& T, uint64_t i, uint32_t need) {
   if (!T.sck) return load_key(T.skey, i);
-  if (need <= 16) return Key4{bswap64(T.sck[i]), 0, 0, 0};
+  if (need <= 8) return Key4{bswap64((uint64_t)T.sck[i] << 32), 0, 0, 0};
   return load_key(T.kin, T.sidx[i]);
 }
 
@@ -319,9 +319,10 @@ KH_HD uint32_t ext_enc_len(uint32_t e, uint32_t brl) {
 // ---- stage: boundary values
 KH_HD void op_lcp(const Topo& T, uint64_t b) {
   int l;
-  if (T.sck) {  // the first 16 nibbles from the sorted prefixes; the input keys only past them
-    const uint64_t x = T.sck[b] ^ T.sck[b + 1];
-    l = x ? (int)(clz64(x) >> 2) : lcp_nibbles(load_key(T.kin, T.sidx[b]), load_key(T.kin, T.sidx[b + 1]));
+  if (T.sck) {  // the first 8 nibbles from the sorted prefixes; the input keys only past them
+    const uint32_t x = T.sck[b] ^ T.sck[b + 1];
+    l = x ? (int)((uint32_t)clz64((uint64_t)x << 32) >> 2)
+          : lcp_nibbles(load_key(T.kin, T.sidx[b]), load_key(T.kin, T.sidx[b + 1]));
   } else {
     l = lcp_nibbles(load_key(T.skey, b), load_key(T.skey, b + 1));
   }

@@ -112,11 +112,12 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   Pyr P{};
   // unsegmented builds take the device's ck path: boundary values from the sorted first
   // key words (the input keys past them), before the sorted keys are used
-  std::vector<uint64_t> kin(4 * n + 4), sck(m + 1);
+  std::vector<uint64_t> kin(4 * n + 4);
+  std::vector<uint32_t> sck(m + 1);
   memcpy(kin.data(), keys, 32 * n);
   T.kin = kin.data();
   if (!segmented) {
-    for (uint64_t i = 0; i < m; ++i) sck[i] = bswap64(skey[4 * i]);
+    for (uint64_t i = 0; i < m; ++i) sck[i] = (uint32_t)(bswap64(skey[4 * i]) >> 32);
     T.sck = sck.data();
     T.skey = nullptr;  // as on the device: no sorted keys on this path
   }

@@ -312,42 +312,26 @@ def test_branch_variants_vs_oracle(khst, oracle, variant, monkeypatch):
     assert hh[0].tobytes() == roots[0] and st.n_node_perms == bst["node_perms"], variant
 
 
-def test_split_hash_sort_paths(khst, oracle):
-    """Hashed-key builds from 4M keys hash the second half on the second stream while the
-    first half is radix-sorted, then merge the halves (stable: the first half's puts come
-    first).  KHST_SPLIT_MIN lowers the threshold so small inputs with duplicates inside and
-    across the halves take that path; roots must equal the oracle's and the unsplit build's."""
-    import os
+def test_hashed_keys_with_repeats(khst, oracle):
+    """Hashed-key builds (the plain path: 32-bit sort prefixes from the hashing pass, ties
+    ordered by the whole key, the last put of a repeated key kept) over sizes around the
+    radix tile and wave boundaries; roots equal the CPU batch builder's."""
     import random
     r = random.Random(17)
-    cases = []
-    for n in (2, 3, 17, 255, 256, 257, 1000, 4099):
+    for n in (2, 3, 17, 255, 256, 257, 1000, 2049, 4099):
         base = [bytes(r.getrandbits(8) for _ in range(20)) for _ in range(n)]
-        keys = base + [base[r.randrange(n)] for _ in range(n // 3)]  # repeats, many in the other half
+        keys = base + [base[r.randrange(n)] for _ in range(n // 3)]  # repeats anywhere
         r.shuffle(keys)
         vals = [bytes([r.getrandbits(8) | 1]) * r.choice([1, 3, 40, 90]) for _ in keys]
-        cases.append((keys, vals))
-    old = os.environ.get("KHST_SPLIT_MIN")
-    try:
-        os.environ["KHST_SPLIT_MIN"] = "2"
-        split = [khst.trie_root(k, v, hash_keys=True) for k, v in cases]
-    finally:
-        if old is None:
-            os.environ.pop("KHST_SPLIT_MIN", None)
-        else:
-            os.environ["KHST_SPLIT_MIN"] = old
-    for (k, v), g in zip(cases, split):
-        assert g == khst.trie_root(k, v, hash_keys=True)
-        assert g == oracle.batch_root(k, v, klen=20, hash_keys=True, nthreads=2)
+        assert khst.trie_root(keys, vals, hash_keys=True) == oracle.batch_root(keys, vals, klen=20, hash_keys=True,
+                                                                                nthreads=2), n
 
 
-def test_split_path_6m_with_repeats(khst, oracle):
-    """6M accounts through the split path (KHST_SPLIT_MIN) plus 200k repeated addresses
-    with new bodies in both halves, against the CPU batch builder."""
-    import os
+def test_6m_with_repeats(khst, oracle):
+    """6M accounts plus 200k repeated addresses with new bodies before and after them,
+    against the CPU batch builder (later puts win)."""
     import torch
     from khipu_amd.device import Ctx
-    os.environ["KHST_SPLIT_MIN"] = "4000000"
     ctx = Ctx(0)
     n = 6_000_000
     addr, vals, voff = ctx.synth_accounts(5, 0, n)
@@ -368,12 +352,7 @@ def test_split_path_6m_with_repeats(khst, oracle):
     d_v = torch.from_numpy(np.concatenate([vbytes, np.zeros(64, np.uint8)])).to("cuda:0")
     d_o = torch.from_numpy(off.astype(np.int64)).to("cuda:0")
     N = len(lens)
-    try:
-        hh, _, _, st = ctx.build(d_k, 20, d_v, d_o, N, hash_keys=True)
-    finally:
-        os.environ.pop("KHST_SPLIT_MIN", None)
-    hh2, _, _, _ = ctx.build(d_k, 20, d_v, d_o, N, hash_keys=True)  # the default (unsplit) path
-    assert hh2[0].tobytes() == hh[0].tobytes()
+    hh, _, _, st = ctx.build(d_k, 20, d_v, d_o, N, hash_keys=True)
     roots, bst = oracle.batch_roots(keys, (vbytes, off), klen=20, hash_keys=True)
     assert hh[0].tobytes() == roots[0]
     assert st.n_leaves == bst["leaves"]
