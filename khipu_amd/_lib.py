@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkhst.so")
+LIB_PATH = os.environ.get("KHST_LIB_AB") or os.path.join(_HERE, "libkhst.so")  # KHST_LIB_AB: an A/B build (measurement only)
 
 KH_OK = 0
 KH_EINVAL = -1

@@ -526,24 +526,28 @@ __global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
 
 // Early leaves (plain root builds; trie_ops.h op_leaf_in): one thread per INPUT,
 // launched on the second stream right after op_pd_scatter, beside the branch topology.
-// The keys and packed values are read in input order (sequential), the message is
-// assembled in registers straight into the Keccak state; only the <= 37-byte header goes
-// through a 5-word LDS slot per lane ([word][lane]: conflict-free).
-constexpr uint32_t HDR_WORDS = 5;
+// The keys and packed values are read in input order (sequential), the message, header
+// included, is assembled in registers straight into the Keccak state.
 __global__ void __launch_bounds__(BS) k_pd_scatter(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i < T.m) op_pd_scatter(T, i);
 }
+// 82 VGPRs, 5 waves per SIMD.  Measured at 100M (r2v): 14.6 ms; forcing 6 waves spills
+// 4 VGPRs and takes 15.7 ms; 4 waves gives 14.7 ms.
 __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
-  __shared__ uint64_t hdr[HDR_WORDS * BS];
   const uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  typedef const __attribute__((address_space(1))) uint64_t gword;  // global (not flat) loads
-  const uint32_t vmis = (uint32_t)((uintptr_t)T.vals & 7);
-  gword* vw = (gword*)(T.vals - vmis);
+  typedef const __attribute__((address_space(1))) u64x2 gpair;  // global (not flat) 16-byte loads
+  const uint32_t vmis = (uint32_t)((uintptr_t)T.vals & 15);
+  gpair* vp = (gpair*)(T.vals - vmis);
   unsigned long long perms = 0, inl = 0, longb = 0;
   if (j < n) {
     uint32_t in1 = 0, lb = 0;
-    perms = op_leaf_in(T, j, vw, vmis, hdr + threadIdx.x, BS, &in1, &lb);
+    auto ld2 = [vp](int64_t p, uint64_t& lo, uint64_t& hi) {
+      const u64x2 v = vp[p];
+      lo = v.x;
+      hi = v.y;
+    };
+    perms = op_leaf_in(T, j, ld2, vmis, &in1, &lb);
     inl = in1;
     longb = lb;
   }

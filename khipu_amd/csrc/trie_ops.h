@@ -823,6 +823,49 @@ KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
   return leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, L, inl);
 }
 
+// Leaf header of a 32-byte key (leaf_header's bytes, <= 38 B) built in 5 registers, no
+// byte stream: [list prefix][0x80 + h if h > 1][HP first byte] at bytes [0, o1), the key
+// bytes [kb0, 32) at [o1, o1 + h - 1) (the key shifted by o1 - kb0 bytes: a byte funnel
+// and a word shift of 0..4), then the value's string prefix (0, 1 or 2 bytes).  Bytes
+// past the header are zero.
+KH_HD void leaf_header_regs(const Key4& k, const LeafGeom& g, uint64_t vlen, uint64_t hw[5]) {
+  const uint32_t lhl = g.payload < 56 ? 1u : 2u;  // short leaf: payload <= 133
+  const uint64_t lh = lhl == 1 ? (0xC0 + g.payload) : (0xF8 | (g.payload << 8));
+  const uint32_t o1 = lhl + (g.h > 1 ? 1u : 0u) + 1u;
+  uint64_t pw = lh;
+  if (g.h > 1) pw |= (uint64_t)(0x80 + g.h) << (8 * lhl);
+  pw |= (uint64_t)g.hp0 << (8 * (o1 - 1));
+  const uint32_t kb0 = (g.s + 1) / 2;
+  const int32_t dl = (int32_t)o1 - (int32_t)kb0;  // message byte x holds key byte x - dl
+  const uint32_t rb = (uint32_t)dl & 7u;
+  const uint32_t sw = (uint32_t)(-(dl >> 3));  // 0..4: word q = Y[q + sw]
+  const uint64_t K[4] = {k.w0, k.w1, k.w2, k.w3};
+  uint64_t A[9];  // Y[t] = bytes [8t - rb, 8t - rb + 8) of the key
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const uint64_t cur = t < 4 ? K[t] : 0, prv = (t >= 1 && t <= 4) ? K[t - 1] : 0;
+    A[t] = rb ? (cur << (8 * rb)) | (prv >> (64 - 8 * rb)) : cur;
+  }
+#pragma unroll
+  for (int st = 0; st < 3; ++st) {  // A[v] <- A[v + sw]
+    const int d = 1 << st;
+    const bool on = (sw >> st) & 1;
+#pragma unroll
+    for (int v = 0; v < 9; ++v) A[v] = on ? (v + d < 9 ? A[v + d] : 0) : A[v];
+  }
+  const uint32_t e = o1 + g.h - 1;  // the value prefix's first byte
+  const bool vh_on = !(vlen == 1 && g.v0 < 0x80);
+  const uint64_t vh = !vh_on ? 0 : vlen < 56 ? (0x80 + vlen) : (0xB8 | (vlen << 8));
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    uint64_t x = q == 0 ? (A[0] & ~low_bytes_mask(o1)) | pw : A[q];
+    const int32_t d = (int32_t)e - 8 * q;
+    if (d >= 0 && d < 8) x |= vh << (8 * d);
+    else if (d == -1) x |= vh >> 8;
+    hw[q] = x;
+  }
+}
+
 // ---- early leaves: parent depth from the two adjacent boundaries (= resolve_parent's pd)
 constexpr uint8_t EMETA_LONG = 0xFF;
 constexpr uint64_t PDINV_SKIP = ~0ULL;
@@ -842,24 +885,41 @@ KH_HD void op_pd_scatter(const Topo& T, uint64_t i) {
   const uint32_t pd = (uint32_t)(uint8_t)(int8_t)leaf_pd_early(T, i);
   T.pdinv[T.sidx ? T.sidx[i] : i] = ((uint64_t)pd << 32) | i;
 }
-// One input j.  The message (<= 135 B) is assembled in registers straight into the
-// Keccak state: the header bytes [0, P) come from `hdr` (5 words, stride hstride: a
-// per-lane LDS slot on the device), the value bytes [P, L) from the aligned words of the
-// value buffer `vw` (vals - vmis) funnel-shifted into place.  Returns permutations;
-// *inl / *longb count inline leaves and long-leaf arena bytes.
-template <typename WP>
-KH_HD uint32_t op_leaf_in(const Topo& T, uint64_t j, WP vw, uint32_t vmis, uint64_t* hdr, uint64_t hstride,
-                          uint32_t* inl, uint32_t* longb) {
+// One input j.  Every load is issued up front, independent of each other's results
+// except the span offsets: the scatter record, the key, the value span's offsets, then
+// the 16-byte pairs of the value buffer that hold the span (`ld2(p, lo, hi)` loads pair
+// p of the buffer whose byte `vmis` is value byte 0; only pairs overlapping the span are
+// read).  The addresses do not depend on the parent depth or on the header length, so
+// the value reads overlap the other loads (one dependent round trip, not three).
+// The message (<= 135 B) is then assembled in registers straight into the Keccak
+// state: header bytes [0, P) from leaf_header_regs, value bytes [P, L) moved into place
+// by a byte funnel and a 3-stage word shift.  Returns permutations; *inl / *longb count inline leaves and long-leaf
+// arena bytes.
+constexpr int LEAF_IN_PAIRS = 10;  // covers any span of a short leaf (<= 132 B) at any alignment
+template <typename LD2>
+KH_HD uint32_t op_leaf_in(const Topo& T, uint64_t j, LD2 ld2, uint32_t vmis, uint32_t* inl, uint32_t* longb) {
   *inl = 0;
   *longb = 0;
   const uint64_t pv = T.pdinv[j];
-  if (pv == PDINV_SKIP) return 0;  // an earlier put of a key put again later
-  const int32_t pd = (int8_t)(uint8_t)(pv >> 32);
-  const uint64_t si = (uint32_t)pv;  // sorted position: where the reference is stashed
   const Key4 k = load_key(T.kin, j);
   const uint64_t off = T.voff[j];
   const uint32_t vlen = (uint32_t)(T.voff[j + 1] - off);
-  const uint32_t v0 = vlen == 1 ? (uint32_t)T.vals[off] : 0;
+  const uint64_t vb = off + vmis;  // buffer byte of value byte 0
+  const uint32_t mis = (uint32_t)(vb & 15);
+  const int64_t pf = (int64_t)(vb >> 4);
+  const uint64_t np = vlen ? ((vb + vlen - 1) >> 4) - (vb >> 4) + 1 : 0;  // pairs under the span
+  uint64_t W[2 * LEAF_IN_PAIRS];
+#pragma unroll
+  for (int p = 0; p < LEAF_IN_PAIRS; ++p) {
+    uint64_t lo = 0, hi = 0;
+    if ((uint64_t)p < np) ld2(pf + p, lo, hi);
+    W[2 * p] = lo;
+    W[2 * p + 1] = hi;
+  }
+  if (pv == PDINV_SKIP) return 0;  // an earlier put of a key put again later
+  const int32_t pd = (int8_t)(uint8_t)(pv >> 32);
+  const uint64_t si = (uint32_t)pv;  // sorted position: where the reference is stashed
+  const uint32_t v0 = vlen == 1 ? (uint32_t)(((mis & 8) ? W[1] : W[0]) >> (8 * (mis & 7))) & 0xFF : 0;
   const LeafGeom g = leaf_geom(k, pd, vlen, v0);
   if (g.L > LEAF_SHORT_MAX) {  // encoded + hashed by op_leaf_long into its arena slot
     T.lf_emeta[si] = EMETA_LONG;
@@ -867,32 +927,40 @@ KH_HD uint32_t op_leaf_in(const Topo& T, uint64_t j, WP vw, uint32_t vmis, uint6
     return 0;
   }
   const bool top = pd == (int32_t)T.depth0 - 1;
-  {
-    BW w(hdr, hstride);
-    leaf_header(w, k, g, vlen);
-    w.flush();
-  }
+  uint64_t hw[5];
+  leaf_header_regs(k, g, vlen, hw);
   const uint32_t L = g.L, P = L - vlen;
-  const int64_t base = (int64_t)(off + vmis) - (int64_t)P;  // buffer byte of message byte 0
-  const int64_t a0 = base >> 3;                             // floor
-  const uint32_t sh = (uint32_t)(base & 7);
-  const int64_t wf = (int64_t)((off + vmis) >> 3), wl = vlen ? (int64_t)((off + vmis + vlen - 1) >> 3) : wf - 1;
+  // message byte x in [P, L) is byte x - P + mis of W.  With P - mis = 8a + r (0 <= r < 8;
+  // a 32-byte key's header is <= 38 B, so -2 <= a <= 4): message word q is bytes
+  // [8(q - a) - r, +8) of W = Y[q - a], Y[t] = bytes [8t - r, 8t - r + 8) of W (rb = r).
+  const int32_t D = (int32_t)P - (int32_t)mis;
+  const uint32_t rb = (uint32_t)D & 7u;
+  const uint32_t s = (uint32_t)((D >> 3) + 2);  // word shift, 0..6: message word q = Y[q + 2 - s]
+  uint64_t A[2 * LEAF_IN_PAIRS - 1];
+#pragma unroll
+  for (int t = 0; t < 2 * LEAF_IN_PAIRS - 1; ++t) {
+    const uint64_t lo = t ? W[t - 1] : 0;
+    A[t] = rb ? (W[t] << (8 * rb)) | (lo >> (64 - 8 * rb)) : W[t];
+  }
+#pragma unroll
+  for (int st = 0; st < 3; ++st) {  // A[v] <- A[v - s] (zeros shifted in)
+    const int d = 1 << st;
+    const bool on = (s >> st) & 1;
+#pragma unroll
+    for (int v = 2 * LEAF_IN_PAIRS - 2; v >= 0; --v) A[v] = on ? (v >= d ? A[v - d] : 0) : A[v];
+  }
   KState S = {};
   uint64_t head[4] = {0, 0, 0, 0};
-  uint64_t prev = (a0 >= wf && a0 <= wl) ? vw[a0] : 0;
 #pragma unroll
   for (int q = 0; q < 17; ++q) {
-    const int64_t a = a0 + q + 1;
-    const uint64_t cur = (a >= wf && a <= wl) ? vw[a] : 0;
-    uint64_t x = sh ? (prev >> (8 * sh)) | (cur << (64 - 8 * sh)) : prev;
-    prev = cur;
+    uint64_t x = A[q + 2];
     const uint32_t b0 = 8u * (uint32_t)q;
     if (b0 + 8 <= P || b0 >= L) x = 0;  // header-only or past the end
     else {
       if (b0 < P) x &= ~low_bytes_mask(P - b0);
       if (b0 + 8 > L) x &= low_bytes_mask(L - b0);
     }
-    if (q < 5 && b0 < P) x |= hdr[q * hstride];
+    if (q < 5) x |= hw[q];
     if (q < 4) head[q] = x;
     if ((L >> 3) == (uint32_t)q) x ^= 0x01ULL << (8 * (L & 7));
     if (q == 16) x ^= 0x80ULL << 56;

@@ -161,7 +161,6 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   std::vector<uint64_t> eref(4 * m + 4);
   std::vector<uint8_t> emeta(m + 1, 32);  // preset as on the device
   std::vector<uint64_t> pdinv(n + 1, PDINV_SKIP);
-  std::vector<uint64_t> hdr(8);
   uint64_t perms = 0, hashes = 0, inl = 0, longb = 0;
   T.lf_eref = eref.data();
   T.lf_emeta = emeta.data();
@@ -169,17 +168,23 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.svoff = nullptr;  // as on the device: no sorted spans in early builds
   T.svlen = nullptr;
   for (uint64_t i = 0; i < m; ++i) op_pd_scatter(T, i);
-  // the device reads whole aligned words around each span: replay on an 8-byte-aligned
-  // copy of the values with a zero word either side (host memory is not page-granular)
-  std::vector<uint64_t> vbuf(voff[n] / 8 + 3, 0);
-  memcpy((uint8_t*)vbuf.data() + 8, vals, voff[n]);
-  T.vals = (const uint8_t*)vbuf.data() + 8;
+  // the device reads whole 16-byte-aligned pairs around each span: replay on a copy of
+  // the values at byte 8 of a 16-byte pair, with zero pairs either side (host memory is
+  // not page-granular)
+  std::vector<uint64_t> vbuf(voff[n] / 8 + 8, 0);
+  uint8_t* vbase = (uint8_t*)(((uintptr_t)vbuf.data() + 15) & ~(uintptr_t)15);
+  memcpy(vbase + 24, vals, voff[n]);
+  T.vals = vbase + 24;
   {
-    const uint32_t vmis = 0;
-    const uint64_t* vw = (const uint64_t*)T.vals;
+    const uint32_t vmis = (uint32_t)((uintptr_t)T.vals & 15);
+    const uint8_t* vp = T.vals - vmis;
+    auto ld2 = [vp](int64_t p, uint64_t& lo, uint64_t& hi) {
+      memcpy(&lo, vp + 16 * p, 8);
+      memcpy(&hi, vp + 16 * p + 8, 8);
+    };
     for (uint64_t j = 0; j < n; ++j) {
       uint32_t in1 = 0, lb = 0;
-      uint32_t p = op_leaf_in(T, j, vw, vmis, hdr.data(), 1, &in1, &lb);
+      uint32_t p = op_leaf_in(T, j, ld2, vmis, &in1, &lb);
       perms += p;
       hashes += p ? 1 : 0;
       inl += in1;
