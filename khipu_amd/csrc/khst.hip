@@ -346,7 +346,6 @@ __global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb) {
   uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (b < nb) op_lcp(T, b);
 }
-
 __global__ void __launch_bounds__(BS) k_min64(const uint8_t* in, uint64_t nin, uint8_t* out, uint64_t nout) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i < nout) op_min64(in, nin, out, i);
@@ -360,6 +359,14 @@ __global__ void __launch_bounds__(BS) k_ansv(Topo T, Pyr P, uint64_t nb) {
 __global__ void __launch_bounds__(BS) k_chain(Topo T, uint64_t nb) {
   uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (b < nb) op_chain(T, b);
+}
+// k_ansv with the early leaves' parent-depth scatter folded in (thread i also scatters
+// leaf i; grid over the m leaves): the leaf kernel waits for this kernel instead of a
+// separate k_pd_scatter racing the topology for the memory system (run_build)
+__global__ void __launch_bounds__(BS) k_ansv_pd(Topo T, Pyr P, uint64_t nb) {
+  uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (b < nb) op_ansv(T, P, b);
+  if (b < T.m) op_pd_scatter(T, b);
 }
 
 // sum three per-thread counters over the block; one atomic per counter per block
@@ -528,6 +535,7 @@ __global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
 // launched on the second stream right after op_pd_scatter, beside the branch topology.
 // The keys and packed values are read in input order (sequential), the message, header
 // included, is assembled in registers straight into the Keccak state.
+constexpr int PD_DEFAULT = 1;  // where the early leaves' parent depths are scattered (run_build)
 __global__ void __launch_bounds__(BS) k_pd_scatter(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i < T.m) op_pd_scatter(T, i);
@@ -1495,25 +1503,43 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint32_t* Bp = (uint32_t*)(ctr + CTR_B);
   HIPCHK(hipMemsetAsync(ctr + CTR_B, 0, 8 * 6, st));  // B, br bytes, lf bytes, C, E0, E1
   Pyr P{};
+  static const int pd_env = [] {
+    const char* e = getenv("KHST_PD");  // measurement switch
+    return !e ? PD_DEFAULT : strcmp(e, "ansv") == 0 ? 1 : 0;
+  }();
+  const int pd_mode = (early && nb > 0) ? pd_env : 0;
+  if (pd_mode) {  // presets for the scatter folded into k_ansv (on st)
+    if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, st));  // dropped duplicates: PDINV_SKIP
+    HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));                  // every leaf a hash unless it says otherwise
+  }
   if (nb > 0) {
     hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
   }
-  if (early) {  // leaves need only the boundaries: hash them (input order) on st2 beside the
-                // topology, which starts right after k_lcp (the parent-depth scatter included)
+  // Early leaves (plain root builds) need only the boundaries: they are hashed in input
+  // order on st2 beside the topology.  Their parent depths are scattered inside k_ansv on
+  // st and the leaf kernel starts after it (pd_mode 1), or by a separate k_pd_scatter on
+  // st2 right after k_lcp (pd_mode 0; KHST_PD=sep, and tries too small for a topology).
+  // Measured at 100M (profiles/r2y_pd_ab_100m.json): 49.9 ms (ansv) against 52.2 (sep);
+  // folded into k_chain 50.6; into k_lcp, the leaf kernel starting right after it, 50.7
+  // (it then runs beside the whole topology: 19.7 ms instead of 14.9).
+  auto launch_leaves = [&](bool scatter) {  // on st2, after everything enqueued on st so far
     HIPCHK(hipEventRecord(c->ev[8], st));
     HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
     hipStream_t s2 = c->st2;
-    if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, s2));  // dropped duplicates: PDINV_SKIP
-    HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, s2));                  // every leaf a hash unless it says otherwise
-    hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, s2, T);
-    LAUNCH_CHECK();
+    if (scatter) {
+      if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, s2));  // dropped duplicates: PDINV_SKIP
+      HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, s2));                  // every leaf a hash unless it says otherwise
+      hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, s2, T);
+      LAUNCH_CHECK();
+    }
     if (A.vals_ready) HIPCHK(hipStreamWaitEvent(s2, A.vals_ready, 0));  // the topology need not wait
     HIPCHK(hipEventRecord(c->ev[9], s2));
     hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, s2, T, n);
     LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[10], s2));
-  }
+  };
+  if (early && pd_mode == 0) launch_leaves(true);
   if (nb > 0) {
     P.lv[0] = T.u;
     P.sz[0] = nb;
@@ -1530,8 +1556,12 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       pp += (nout + 255) & ~(uint64_t)255;
     }
     HIPCHK(hipMemsetAsync(T.glast, 1, nb, st));
-    hipLaunchKernelGGL(k_ansv, GRID(nb, BS), dim3(BS), 0, st, T, P, nb);
+    if (pd_mode == 1)
+      hipLaunchKernelGGL(k_ansv_pd, GRID(m, BS), dim3(BS), 0, st, T, P, nb);
+    else
+      hipLaunchKernelGGL(k_ansv, GRID(nb, BS), dim3(BS), 0, st, T, P, nb);
     LAUNCH_CHECK();
+    if (pd_mode == 1) launch_leaves(false);
     hipLaunchKernelGGL(k_chain, GRID(nb, BS), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
     scan_exclusive<uint32_t>(T.isrep_bid, T.isrep_bid, nb, Bp, scan_scratch, st);

@@ -317,7 +317,7 @@ KH_HD uint32_t ext_enc_len(uint32_t e, uint32_t brl) {
 }
 
 // ---- stage: boundary values
-KH_HD void op_lcp(const Topo& T, uint64_t b) {
+KH_HD uint8_t lcp_value(const Topo& T, uint64_t b) {
   int l;
   if (T.sck) {  // the first 8 nibbles from the sorted prefixes; the input keys only past them
     const uint32_t x = T.sck[b] ^ T.sck[b + 1];
@@ -333,7 +333,14 @@ KH_HD void op_lcp(const Topo& T, uint64_t b) {
   uint8_t v = (uint8_t)(l + 1);
   if (l < (int)T.depth0 || l > 63) v = 0;  // 64 cannot occur after dedup
   if (T.segmented && T.sseg[b] != T.sseg[b + 1]) v = 0;
-  T.u[b] = v;
+  return v;
+}
+KH_HD void op_lcp(const Topo& T, uint64_t b) { T.u[b] = lcp_value(T, b); }
+// the early leaves' scatter record of sorted leaf i from its two boundary values
+KH_HD void pd_scatter_vals(const Topo& T, uint64_t i, uint32_t va, uint32_t vc) {
+  const uint32_t v = va > vc ? va : vc;
+  const int32_t pd = v == 0 ? (int32_t)T.depth0 - 1 : (int32_t)v - 1;
+  T.pdinv[T.sidx ? T.sidx[i] : i] = ((uint64_t)(uint8_t)(int8_t)pd << 32) | i;
 }
 
 // ---- stage: all nearest smaller values over a 64-ary min pyramid
@@ -882,8 +889,7 @@ KH_HD int32_t leaf_pd_early(const Topo& T, uint64_t i) {
 // position, where the leaf kernel stashes the reference (one scattered 33-byte write,
 // fire-and-forget); op_leaf_topo_early then moves it into the parent's child record.
 KH_HD void op_pd_scatter(const Topo& T, uint64_t i) {
-  const uint32_t pd = (uint32_t)(uint8_t)(int8_t)leaf_pd_early(T, i);
-  T.pdinv[T.sidx ? T.sidx[i] : i] = ((uint64_t)pd << 32) | i;
+  pd_scatter_vals(T, i, i > 0 ? T.u[i - 1] : 0, i + 1 < T.m ? T.u[i] : 0);
 }
 // One input j.  Every load is issued up front, independent of each other's results
 // except the span offsets: the scatter record, the key, the value span's offsets, then
