@@ -573,6 +573,16 @@ __global__ void __launch_bounds__(BS) k_leaf_topo_early(Topo T) {
     op_leaf_topo_early(T, i,
                        [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); });
 }
+// the same publish split in two (trie_ops.h op_leaf_link / op_leaf_move)
+__global__ void __launch_bounds__(BS) k_leaf_link(Topo T) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < T.m) op_leaf_link(T, i);
+}
+__global__ void __launch_bounds__(BS) k_leaf_move(Topo T) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < T.m)
+    op_leaf_move(T, i, [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); });
+}
 
 __global__ void __launch_bounds__(BS) k_leaf_long(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -614,7 +624,10 @@ __global__ void __launch_bounds__(BS) k_branch_hash(Topo T, uint64_t first, uint
 // HBM: the level reads its contiguous child records once and writes one 34-byte
 // reference per node.  Slot layout [thread][word]: a wave's 8-byte slot accesses are
 // bank-conflict-free within each 16-lane group (stride 34 dwords).
-template <bool VARKEYS>
+// V: 0 variable-length keys (op_branch_fused), 1 direct window assembly re-scanning the
+// children per window (op_branch_direct), 2 the children streamed once with the next
+// record prefetched (op_branch_stream)
+template <int V>
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8))) k_branch_fused(Topo T, uint64_t first, uint64_t cnt) {
   __shared__ uint64_t slots[BS * LEAF_WORDS];
   uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -624,8 +637,10 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8)))
     uint32_t in1 = 0;
     // fixed-length keys: direct window assembly; variable-length keys (branch values):
     // the byte stream through the windowed writer
-    perms = VARKEYS ? op_branch_fused(T, j, slots + threadIdx.x * LEAF_WORDS, 1, &in1)
-                    : op_branch_direct(T, j, slots + threadIdx.x * LEAF_WORDS, 1, &in1);
+    uint64_t* sl = slots + threadIdx.x * LEAF_WORDS;
+    perms = V == 0 ? op_branch_fused(T, j, sl, 1, &in1)
+            : V == 1 ? op_branch_direct(T, j, sl, 1, &in1)
+                     : op_branch_stream(T, j, sl, 1, &in1);
     hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
   }
@@ -1335,7 +1350,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
       nres * 32, nres * 4, nres * 32,         // results
       CTR_N * CTR_SHARDS * 8, 64 * 4, 80 * 4, 512 * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
-      early ? n * 32 : 0, early ? n : 0, early ? n * 8 : 0,  // early leaves: stashed references, meta, pd|position
+      early ? n * 32 : 0, early ? n : 0, early ? n * 8 : 0, early ? n * 8 : 0,  // early leaves: stashed references,
+                                                                  // meta, pd|position, link slots
       A.kn ? n : 0,                           // sorted key lengths
       nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1, nb1,  // branch tables in key-order ids (BrTab J)
   };
@@ -1393,6 +1409,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.lf_eref = early ? cv.take<uint64_t>(n * 4) : nullptr;
   T.lf_emeta = early ? cv.take<uint8_t>(n) : nullptr;
   T.pdinv = early ? cv.take<uint64_t>(n) : nullptr;
+  T.lf_dst = early ? cv.take<uint64_t>(n) : nullptr;
   T.kin = K32;
   uint8_t* skn = A.kn ? cv.take<uint8_t>(n) : nullptr;
   BrTab J{};
@@ -1596,6 +1613,11 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     // child record bases
     scan_exclusive<uint32_t>(T.br_k, T.br_cbase, nb, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
   }
+  static const bool split_publish = !getenv("KHST_PUBLISH_ONE");  // measurement switch
+  if (early && split_publish) {  // the leaves' slots, while they are still being hashed
+    hipLaunchKernelGGL(k_leaf_link, GRID(m, BS), dim3(BS), 0, st, T);
+    LAUNCH_CHECK();
+  }
   if (early) {
     HIPCHK(hipEventRecord(c->ev[3], st));      // topology done (the leaves may still run)
     HIPCHK(hipStreamWaitEvent(st, c->ev[10], 0));  // ... and the leaves: their long-leaf bytes
@@ -1648,7 +1670,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // ---- 4. leaves: encode + hash in LDS (root only), or encode into message slots
   //         that the node-set emitter reads back, then hash
   if (early) {  // hashed already: publish into the child records; long leaves now
-    hipLaunchKernelGGL(k_leaf_topo_early, GRID(m, BS), dim3(BS), 0, st, T);
+    if (split_publish)
+      hipLaunchKernelGGL(k_leaf_move, GRID(m, BS), dim3(BS), 0, st, T);
+    else
+      hipLaunchKernelGGL(k_leaf_topo_early, GRID(m, BS), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
     if (lf_bytes) {
       hipLaunchKernelGGL(k_leaf_long, GRID(m, BS), dim3(BS), 0, st, T);
@@ -1668,6 +1693,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // wave-cooperative DPP assembly (KHST_BRANCH=coop; DESIGN.md §5 has the measurement)
   const char* bv = getenv("KHST_BRANCH");
   const bool coop = bv && strcmp(bv, "coop") == 0 && !A.kn;  // (the coop assembly has no branch values)
+  const bool rescan = bv && strcmp(bv, "rescan") == 0;          // op_branch_direct (measurement switch)
   for (int d = 63; d >= 0; --d) {
     uint32_t cnt = lbh[d + 1] - lbh[d];
     if (!cnt) continue;
@@ -1679,9 +1705,11 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       hipLaunchKernelGGL(k_branch_coop, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     } else {
       if (A.kn)
-        hipLaunchKernelGGL(k_branch_fused<true>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+        hipLaunchKernelGGL(k_branch_fused<0>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+      else if (rescan)
+        hipLaunchKernelGGL(k_branch_fused<1>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
       else
-        hipLaunchKernelGGL(k_branch_fused<false>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+        hipLaunchKernelGGL(k_branch_fused<2>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     }
     LAUNCH_CHECK();
     ++levels;

@@ -215,6 +215,7 @@ struct Topo {
   const uint64_t* kin; // [n*4] the keys in input order (the early leaf kernel reads them sequentially)
   uint64_t* pdinv;     // [n] per INPUT position: parent depth << 32 | sorted position; PDINV_SKIP for
                        //     a dropped duplicate
+  uint64_t* lf_dst;    // [m] nibble << 56 | parent child-record slot, LINK_TOP for a top leaf (op_leaf_link)
   // element builds (resident commits, forest.h; all nullable): an element is a leaf, or
   // a SUBTREE standing for an unchanged branch at depth el_db[i] whose capped reference
   // is el_bref / el_brl (its keys all share key i's first el_db nibbles)
@@ -1003,6 +1004,42 @@ KH_HD void leaf_span_early(const Topo& T, uint64_t i, uint64_t* off, uint32_t* l
   *off = T.voff[j];
   *len = (uint32_t)(T.voff[j + 1] - *off);
 }
+// The early leaves' publish in two halves.  op_leaf_link runs on the topology stream
+// right after the branch topology, while the leaves are still being hashed on the other
+// stream: sorted leaf i's parent (resolve_parent), child-record slot and nibble.
+// op_leaf_move runs after both: the stashed reference is copied to its slot (a streaming
+// pass); long and top leaves take op_leaf_topo_early.
+constexpr uint64_t LINK_TOP = ~0ULL;
+constexpr uint64_t LINK_SLOT = (1ULL << 56) - 1;
+KH_HD void op_leaf_link(const Topo& T, uint64_t i) {
+  const int64_t a = (int64_t)i - 1, c = (i + 1 < T.m) ? (int64_t)i : -1;
+  const Parent P = resolve_parent(T, a, c);
+  if (P.bid == NONE) {
+    T.lf_dst[i] = LINK_TOP;
+    return;
+  }
+  const Key4 k = sorted_key(T, i, (uint32_t)P.pd + 1);
+  T.lf_dst[i] = ((uint64_t)key_nibble(k, P.pd) << 56) | ((uint64_t)T.br_cbase[P.bid] + P.pord);
+}
+template <typename AllocFn>
+KH_HD void op_leaf_topo_early(const Topo& T, uint64_t i, AllocFn alloc);
+template <typename AllocFn>
+KH_HD void op_leaf_move(const Topo& T, uint64_t i, AllocFn alloc) {
+  const uint8_t em = T.lf_emeta[i];
+  const uint64_t d = T.lf_dst[i];
+  if (em == EMETA_LONG || d == LINK_TOP) {
+    op_leaf_topo_early(T, i, alloc);
+    return;
+  }
+  const uint64_t slot = d & LINK_SLOT;
+  const uint64_t* r = T.lf_eref + 4 * i;
+  const uint64_t r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+  T.cref[4 * slot] = r0;
+  T.cref[4 * slot + 1] = r1;
+  T.cref[4 * slot + 2] = r2;
+  T.cref[4 * slot + 3] = r3;
+  T.cmeta[slot] = (uint16_t)(em | ((d >> 56) << 8));
+}
 // after the branch topology: the stashed reference goes to the parent's child
 // record; a long leaf gets its arena slot (as in op_leaf_topo) for op_leaf_long
 template <typename AllocFn>
@@ -1361,6 +1398,128 @@ KH_HD uint32_t op_branch_direct(const Topo& T, uint32_t j, uint64_t* slot, uint6
           I[4] = 0;
         }
         window_place(slot, stride, w0, off, ilen, I);
+      }
+      if (!hashit) break;  // embedded in its parent: never hashed (Node.scala:114)
+      const uint32_t rem = b < nfull ? 136 : L - 136 * nfull;
+#pragma unroll
+      for (int q = 0; q < 17; ++q) {
+        uint64_t x = slot[q * stride];  // zero past the encoding already
+        if (b == nfull) {
+          if ((rem >> 3) == (uint32_t)q) x ^= 0x01ULL << (8 * (rem & 7));
+          if (q == 16) x ^= 0x80ULL << 56;
+        }
+        kxor(S, q, x);
+      }
+      keccakf(S);
+    }
+    if (hashit) {
+      for (int q = 0; q < 4; ++q) hb[q] = lane(S, q);
+      perms = nfull + 1;
+    }
+    if (L < 32)
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t base = 8u * (uint32_t)q;
+        bhead[q] = base < L ? slot[q * stride] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0;
+      }
+    ninl = hashit ? 0 : 1;
+    branch_keep(T, j, L, hb, bhead);
+  }
+  perms += branch_publish(T, j, L, hb, bhead, Slot{slot, stride}, &ninl);
+  *inl = ninl;
+  return perms;
+}
+
+// The same direct assembly with the children streamed ONCE in order: the window loop
+// resumes at the first child not yet placed (an item crossing a window edge is placed
+// again, its tail, in the next window), the next child's record is loaded while the
+// current one is placed, and the child lengths for the payload are loaded as one batch
+// (16 predicated loads issued together).  One Keccak call site (the block loop).
+KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl) {
+  const uint32_t ext = T.br_ext[j];
+  const bool top = T.br_parent[j] == NONE;
+  *inl = 0;
+  uint64_t hb[4] = {0, 0, 0, 0}, bhead[4] = {0, 0, 0, 0};
+  uint32_t L, perms = 0, ninl = 0;
+  {
+    const uint32_t k = T.br_k[j];
+    const uint64_t cb = T.br_cbase[j];
+    const uint16_t* cm = T.cmeta + cb;
+    const uint64_t* cr = T.cref + 4 * cb;
+    uint32_t payload = 1 + (16 - k);  // terminator "" + empty slots
+#pragma unroll
+    for (uint32_t c = 0; c < 16; ++c) {
+      const uint32_t len = c < k ? (uint32_t)(cm[c] & 0xFF) : 0;
+      payload += len == 32 ? 33 : len;
+    }
+    const uint32_t hh = rlp_hdr_len(payload);
+    L = hh + payload;
+    T.br_len[j] = L;
+    const bool hashit = L >= 32 || (top && ext == 0);
+    const uint32_t nfull = L / 136;
+    KState S = {};
+    auto prefill = [&](uint32_t w0) {  // 0x80 over the encoding's bytes of the window
+#pragma unroll
+      for (int q = 0; q < 17; ++q) {
+        const uint32_t a = w0 + 8u * (uint32_t)q;
+        const uint32_t n80 = L > a ? (L - a < 8 ? L - a : 8) : 0;
+        slot[q * stride] = low_bytes_mask(n80) & 0x8080808080808080ULL;
+      }
+    };
+    prefill(0);
+    {  // the list header
+      const uint32_t pl = payload;
+      const uint64_t hdr = hh == 1 ? (0xC0 + pl)
+                           : hh == 2 ? (0xF8 | ((uint64_t)pl << 8))
+                                     : (0xF9 | ((uint64_t)(pl >> 8) << 8) | ((uint64_t)(pl & 0xFF) << 16));
+      slot[0] ^= (hdr ^ 0x8080808080808080ULL) & low_bytes_mask(hh);
+    }
+    // child c's item: I[] and its byte offset / length; the next child's record in flight
+    uint32_t c = 0, run = 0, off = 0, ilen = 0;
+    uint64_t I[5] = {0, 0, 0, 0, 0};
+    uint64_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+    uint32_t nm = 0;
+    if (k) {
+      nm = cm[0];
+      n0 = cr[0], n1 = cr[1], n2 = cr[2], n3 = cr[3];
+    }
+    bool have = false;  // I / off / ilen hold child c, not yet completely placed
+    auto take = [&]() {  // child c from the prefetch registers; prefetch child c + 1
+      const uint32_t mc = nm, len = mc & 0xFF;
+      ilen = len == 32 ? 33 : len;
+      off = hh + (mc >> 8) + run;
+      run += ilen - 1;
+      if (len == 32) {
+        I[0] = 0xA0 | (n0 << 8);
+        I[1] = (n0 >> 56) | (n1 << 8);
+        I[2] = (n1 >> 56) | (n2 << 8);
+        I[3] = (n2 >> 56) | (n3 << 8);
+        I[4] = n3 >> 56;
+      } else {  // an embedded child: its bytes (the capped reference is zero past len)
+        I[0] = n0;
+        I[1] = n1;
+        I[2] = n2;
+        I[3] = n3;
+        I[4] = 0;
+      }
+      if (c + 1 < k) {
+        nm = cm[c + 1];
+        n0 = cr[4 * (c + 1)], n1 = cr[4 * (c + 1) + 1], n2 = cr[4 * (c + 1) + 2], n3 = cr[4 * (c + 1) + 3];
+      }
+      have = true;
+    };
+    for (uint32_t b = 0; b <= nfull; ++b) {
+      const uint32_t w0 = 136u * b;
+      if (b) prefill(w0);
+      for (;;) {  // place the children overlapping this window, in order
+        if (!have) {
+          if (c >= k) break;
+          take();
+        }
+        if (off >= w0 + 136) break;  // starts in a later window
+        window_place(slot, stride, w0, off, ilen, I);
+        if (off + ilen > w0 + 136) break;  // its tail goes into the next window too
+        have = false;
+        ++c;
       }
       if (!hashit) break;  // embedded in its parent: never hashed (Node.scala:114)
       const uint32_t rem = b < nfull ? 136 : L - 136 * nfull;

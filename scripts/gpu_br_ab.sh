@@ -1,0 +1,6 @@
+#!/bin/bash
+# parity tests of the plain-root path, then A/B of the branch window assembly (measurement only)
+export TMPDIR=/tmp
+tag=${1:-br}
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_${tag}.log 2>&1; rc=$?; tail -1 gpurun_out/pytest_${tag}.log; [ $rc -eq 0 ] || exit $rc
+bash scripts/gpu_ab_lib.sh $tag "stream:X=1" "rescan:KHST_BRANCH=rescan" "leafhi:KHST_LEAF_PRIO=hi"

@@ -206,9 +206,13 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
     lfb += b;
     return o;
   };
+  std::vector<uint64_t> dst(m + 1);
+  T.lf_dst = dst.data();
+  if (early)  // the device's split publish: slots during the hashing, then the copy
+    for (uint64_t i = 0; i < m; ++i) op_leaf_link(T, i);
   for (uint64_t i = 0; i < m; ++i) {
     if (early)
-      op_leaf_topo_early(T, i, bump);
+      op_leaf_move(T, i, bump);
     else
       op_leaf_topo(T, i, bump);
   }
@@ -246,7 +250,10 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       uint32_t j = lorder[g];
       uint32_t in1 = 0;
       uint64_t slot[LEAF_WORDS + 1];
-      uint32_t p = T.kn ? op_branch_fused(T, j, slot, 1, &in1) : op_branch_direct(T, j, slot, 1, &in1);
+      // fixed-length keys: both device assemblies, on alternate branches
+      uint32_t p = T.kn      ? op_branch_fused(T, j, slot, 1, &in1)
+                   : (j & 1) ? op_branch_direct(T, j, slot, 1, &in1)
+                             : op_branch_stream(T, j, slot, 1, &in1);
       perms += p;
       hashes += branch_hash_count(T, j, p);
       inl += in1;
