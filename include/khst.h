@@ -195,6 +195,13 @@ int kh_dev_hash_keys(kh_ctx* ctx, const uint8_t* d_keys, uint32_t klen, uint64_t
 int kh_dev_partition(kh_ctx* ctx, const uint8_t* d_keys32, const uint8_t* d_vals, const uint64_t* d_voff,
                      uint64_t n, uint32_t nparts, uint8_t* d_out_keys, uint8_t* d_out_vals, uint64_t* d_out_vlen,
                      uint64_t* h_counts, uint64_t* h_bytes);
+/* The same with the value copy deferred: it returns once the keys, the lengths and the
+ * counts are in place, the value bytes still being copied on the context's stream;
+ * vals_done (a hipEvent_t of the context's device) is recorded after them.  NULL
+ * vals_done: kh_dev_partition. */
+int kh_dev_partition_ev(kh_ctx* ctx, void* vals_done, const uint8_t* d_keys32, const uint8_t* d_vals,
+                        const uint64_t* d_voff, uint64_t n, uint32_t nparts, uint8_t* d_out_keys,
+                        uint8_t* d_out_vals, uint64_t* d_out_vlen, uint64_t* h_counts, uint64_t* h_bytes);
 
 /* ---- fast-sync NodeData verification ----
  * NodeDatasRequest.processResponse (sync/package.scala:81-125) over a batch of peer

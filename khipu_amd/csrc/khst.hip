@@ -1771,7 +1771,12 @@ static kh_ctx* ctx_new(int dev) {
   // over the VALU-bound leaf kernel they overlap with (st2)
   int prio_lo = 0, prio_hi = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  const char* lp = getenv("KHST_LEAF_PRIO");  // measurement switch: "hi" gives the leaf stream priority
+  // The topology stream (st) has the priority over the leaf stream (st2): the leaf kernel
+  // then shares the CUs with the topology (18 ms instead of 14.7 alone) but the topology
+  // stays off the critical path.  Measured (profiles/r2za_*, r2zc_*): the leaf stream first
+  // (KHST_LEAF_PRIO=hi) or equal priorities starve the topology (22.3 ms) and cost 0.5 ms;
+  // restricting the topology stream to 1/2 or 3/4 of the CUs changes nothing.
+  const char* lp = getenv("KHST_LEAF_PRIO");  // measurement switch
   const bool leaf_hi = lp && strcmp(lp, "hi") == 0;
   HIPCHK(hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, leaf_hi ? prio_lo : prio_hi));
   HIPCHK(hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, leaf_hi ? prio_hi : prio_lo));
@@ -3079,6 +3084,13 @@ int kh_fold_root16(const uint8_t* hash32x16, const uint32_t* enc_len16, const ui
 int kh_dev_partition(kh_ctx* c, const uint8_t* d_keys32, const uint8_t* d_vals, const uint64_t* d_voff, uint64_t n,
                      uint32_t nparts, uint8_t* d_out_keys, uint8_t* d_out_vals, uint64_t* d_out_vlen,
                      uint64_t* h_counts, uint64_t* h_bytes) {
+  return kh_dev_partition_ev(c, nullptr, d_keys32, d_vals, d_voff, n, nparts, d_out_keys, d_out_vals, d_out_vlen,
+                             h_counts, h_bytes);
+}
+
+int kh_dev_partition_ev(kh_ctx* c, void* vals_done, const uint8_t* d_keys32, const uint8_t* d_vals,
+                        const uint64_t* d_voff, uint64_t n, uint32_t nparts, uint8_t* d_out_keys,
+                        uint8_t* d_out_vals, uint64_t* d_out_vlen, uint64_t* h_counts, uint64_t* h_bytes) {
   if (!c) return set_err(KH_EINVAL, "null context");
   API_TRY({
     if (nparts < 1 || nparts > 16) throw KhError{KH_EINVAL, "nparts must be in [1, 16]"};
@@ -3108,15 +3120,23 @@ int kh_dev_partition(kh_ctx* c, const uint8_t* d_keys32, const uint8_t* d_vals, 
                        (const uint32_t*)hist, (uint64_t*)d_out_keys, d_out_vlen, pos);
     LAUNCH_CHECK();
     scan_exclusive<uint64_t>(d_out_vlen, ooff, n, (uint64_t*)(tot + 32), sc, st);
-    hipLaunchKernelGGL(k_part_vcopy, GRID(n * CG, BS), dim3(BS), 0, st, d_vals, d_voff, (const uint32_t*)pos,
-                       (const uint64_t*)ooff, n, d_out_vals);
-    LAUNCH_CHECK();
+    auto vcopy = [&] {
+      hipLaunchKernelGGL(k_part_vcopy, GRID(n * CG, BS), dim3(BS), 0, st, d_vals, d_voff, (const uint32_t*)pos,
+                         (const uint64_t*)ooff, n, d_out_vals);
+      LAUNCH_CHECK();
+    };
+    if (!vals_done) vcopy();
     HIPCHK(hipMemsetAsync(tot, 0, 256, st));
     hipLaunchKernelGGL(k_part_bounds, dim3(1), dim3(64), 0, st, (const uint32_t*)hist, ntile, (const uint64_t*)ooff,
                        (const uint64_t*)(tot + 32), n, nparts, tot, tot + 16);
     LAUNCH_CHECK();
     HIPCHK(hipMemcpyAsync(c->h_pinned, tot, 256, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (vals_done) {  // the value bytes move after the counts are back: the caller routes the
+                      // keys meanwhile and orders the value exchange after vals_done
+      vcopy();
+      HIPCHK(hipEventRecord((hipEvent_t)vals_done, st));
+    }
     for (uint32_t p = 0; p < nparts; ++p) {
       h_counts[p] = c->h_pinned[p];
       h_bytes[p] = c->h_pinned[16 + p];

@@ -4,7 +4,8 @@ SURVEY §8(e).  Rank r of N owns top nibbles q with q * N // 16 == r (2 per GPU 
 N = 8).  One step, from (address, account body) records spread over the ranks:
 
   1. kec256 of the local addresses                         (libkhst, k_hash_keys)
-  2. stable partition of the local records by owner rank   (libkhst, kh_dev_partition)
+  2. stable partition of the local records by owner rank   (libkhst, kh_dev_partition_ev:
+     the value bytes are still being copied while the keys are exchanged)
   3. exchange: all-to-all of counts, keys, value lengths and value bytes
      (torch.distributed = RCCL over xGMI; rank-major order keeps "later put wins")
   4. build the owned subtries from nibble 1 down           (libkhst, depth0 = 1)
@@ -47,6 +48,9 @@ class GpuBackend:
         return out
 
     def partition(self, keys32, vals, voff, n, nparts):
+        """With self.overlap the value bytes are still being copied on return (the keys,
+        lengths and counts are in place): self.vals_done is the event after them, which
+        exchange() orders the value all-to-all after (kh_dev_partition_ev)."""
         from ._lib import check, lib
         from .device import _ptr
         pk = torch.empty(n * 32 + 64, dtype=torch.uint8, device=self.device)
@@ -55,9 +59,19 @@ class GpuBackend:
         cnt = np.zeros(16, np.uint64)
         nb = np.zeros(16, np.uint64)
         torch.cuda.synchronize(self.device)
-        check(lib().kh_dev_partition(self.ctx.h, _ptr(keys32), _ptr(vals), _ptr(voff), n, nparts, _ptr(pk), _ptr(pv),
-                                     _ptr(pl), cnt.ctypes.data, nb.ctypes.data))
+        self.vals_done = None
+        ev = None
+        if self.overlap:
+            self.vals_done = torch.cuda.Event()
+            self.vals_done.record()  # creates the event; the library records it again on its stream
+            ev = self.vals_done.cuda_event
+        check(lib().kh_dev_partition_ev(self.ctx.h, ev, _ptr(keys32), _ptr(vals), _ptr(voff), n, nparts, _ptr(pk),
+                                        _ptr(pv), _ptr(pl), cnt.ctypes.data, nb.ctypes.data))
         return pk, pv, pl, cnt[:nparts].astype(np.int64), nb[:nparts].astype(np.int64)
+
+    def wait(self, ev):
+        """The current (torch) stream waits for ev; the host does not."""
+        torch.cuda.current_stream(self.device).wait_event(ev)
 
     def build(self, keys32, vals, voff, n, depth0, vals_ready=None):
         """vals_ready: a torch.cuda.Event after which vals / voff are in place (the keys
@@ -149,6 +163,9 @@ def exchange(be, pkeys, pvals, pvlen, counts, nbytes):
     rvals = be.empty(tot_b + 64)
     works = a2a_bytes(rlen[:m].view(torch.uint8), pvlen[:n_send].view(torch.uint8), [int(c) * 8 for c in rc],
                       [c * 8 for c in cl], kr, async_op=be.overlap)
+    vals_done = getattr(be, "vals_done", None)  # the partition's value copy may still be running
+    if vals_done is not None:
+        be.wait(vals_done)
     works += a2a_bytes(rvals[:tot_b], pvals[:b_send], [int(b) for b in rb], bl, vr, async_op=be.overlap)
     for w in works:
         w.wait()  # the current stream waits; the host does not

@@ -264,12 +264,15 @@ def test_device_build_misaligned_buffers(khst, oracle, koff, voff_shift):
 def test_partition_vs_host(khst, nparts):
     """kh_dev_partition (grouped span copy) == a stable numpy partition by top-nibble owner:
     keys, value bytes, value lengths, per-owner counts and bytes; ragged 0..300-byte values
-    at unaligned offsets, plus the empty batch."""
+    at unaligned offsets, plus the empty batch.  Both the synchronous copy and the deferred
+    one (kh_dev_partition_ev: the values checked after the current stream waits on
+    vals_done, as exchange() orders the value all-to-all)."""
     import torch
     from khipu_amd import sharded
     rng = np.random.default_rng(nparts)
     be = sharded.GpuBackend(0)
-    for n in (0, 1, 777, 100_003):
+    for overlap, n in [(o, n) for o in (True, False) for n in (0, 1, 777, 100_003)]:
+        be.overlap = overlap
         lens = rng.integers(0, 301, n).astype(np.int64)
         short = rng.random(n) < 0.5
         lens[short] = rng.integers(0, 12, int(short.sum()))
@@ -278,6 +281,10 @@ def test_partition_vs_host(khst, nparts):
         k = rng.integers(0, 256, n * 32 + 64, dtype=np.uint8)
         kd, vd, od = (torch.from_numpy(x).to("cuda:0") for x in (k, v, vo))
         pk, pv, pl, cnt, nb = be.partition(kd, vd, od, n, nparts)
+        assert (be.vals_done is not None) == overlap
+        if overlap:
+            be.wait(be.vals_done)
+            pv = pv.clone()  # on the current stream, after the wait
         torch.cuda.synchronize()
         kk = k[:n * 32].reshape(n, 32)
         owner = ((kk[:, 0] >> 4).astype(np.int64) * nparts) >> 4
