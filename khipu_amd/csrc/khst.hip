@@ -212,13 +212,12 @@ __device__ __forceinline__ bool ck_equal(uint32_t a, uint32_t b, const uint64_t*
   const uint64_t* y = K + 4ull * ib;
   return x[0] == y[0] && x[1] == y[1] && x[2] == y[2] && x[3] == y[3];
 }
-__global__ void __launch_bounds__(BS) k_tie_fix_ck(uint32_t* ck, uint32_t* idx, uint64_t n, const uint64_t* K,
-                                                   unsigned long long* flags) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i + 1 >= n) return;
+// the run of equal prefixes starting at i (ck[i] == ck[i + 1], i the run's first)
+// u (nullable): also the boundary values inside the run, from the whole keys (k_lcp then
+// skips boundaries between equal prefixes unless a dedup shifts the positions)
+__device__ void tie_run_ck(uint32_t* ck, uint32_t* idx, uint64_t n, const uint64_t* K, unsigned long long* flags,
+                           uint64_t i, uint8_t* u = nullptr, uint32_t depth0 = 0) {
   const uint32_t hi = ck[i];
-  if (ck[i + 1] != hi) return;
-  if (i > 0 && ck[i - 1] == hi) return;
   uint64_t e = i + 1;
   while (e < n && ck[e] == hi && e - i <= TIE_RUN_MAX) ++e;
   if (e - i > TIE_RUN_MAX) {
@@ -240,7 +239,47 @@ __global__ void __launch_bounds__(BS) k_tie_fix_ck(uint32_t* ck, uint32_t* idx, 
   bool dup = false;
   for (uint64_t a = i + 1; a < e; ++a) dup |= ck_equal(ck[a - 1], ck[a], K, idx[a - 1], idx[a]);
   if (dup) atomicOr(flags, 2ULL);
+  if (u)
+    for (uint64_t a = i; a + 1 < e; ++a) {  // lcp_value's rule
+      const int l = lcp_nibbles(load_key(K, idx[a]), load_key(K, idx[a + 1]));
+      u[a] = (l < (int)depth0 || l > 63) ? 0 : (uint8_t)(l + 1);
+    }
 }
+__device__ __forceinline__ bool tie_run_start(const uint32_t* ck, uint64_t n, uint64_t i) {
+  if (i + 1 >= n) return false;
+  const uint32_t hi = ck[i];
+  return ck[i + 1] == hi && !(i > 0 && ck[i - 1] == hi);
+}
+// one thread per sorted position: the thread at a run's start orders the run
+__global__ void __launch_bounds__(BS) k_tie_fix_ck(uint32_t* ck, uint32_t* idx, uint64_t n, const uint64_t* K,
+                                                   unsigned long long* flags) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (tie_run_start(ck, n, i)) tie_run_ck(ck, idx, n, K, flags, i);
+}
+// Block-local run list (default): a block covers TF_ITEMS * BS sorted positions, lists
+// its run starts in LDS, and its first threads order the runs (wave 0 for the ~1 % of
+// starting positions of random keys), so one wave per TF_ITEMS * 4 waves' worth of
+// positions waits on a run's dependent key reads instead of nearly every wave (the
+// one-thread-per-position kernel above).  A global list with one atomic per wave was
+// measured far slower (a single contended counter: +9 ms at 100M).
+constexpr int TF_ITEMS = 4;
+__global__ void __launch_bounds__(BS) k_tie_fix_ck_blk(uint32_t* ck, uint32_t* idx, uint64_t n, const uint64_t* K,
+                                                       unsigned long long* flags, uint8_t* u, uint32_t depth0) {
+  __shared__ uint32_t list[TF_ITEMS * BS];
+  __shared__ uint32_t cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * (TF_ITEMS * BS);
+#pragma unroll
+  for (int q = 0; q < TF_ITEMS; ++q) {
+    const uint64_t i = base + (uint64_t)q * BS + threadIdx.x;
+    if (tie_run_start(ck, n, i)) list[atomicAdd(&cnt, 1u)] = (uint32_t)(i - base);
+  }
+  __syncthreads();
+  const uint32_t nr = cnt;
+  for (uint32_t t = threadIdx.x; t < nr; t += BS) tie_run_ck(ck, idx, n, K, flags, base + list[t], u, depth0);
+}
+
 __global__ void __launch_bounds__(BS) k_dup_ck(const uint32_t* ck, const uint32_t* idx, const uint64_t* K, uint64_t n,
                                                uint32_t* keep) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -342,9 +381,12 @@ __global__ void __launch_bounds__(BS) k_el_gather(const uint32_t* sidx, uint64_t
   obrl[i] = brl[s];
 }
 
-__global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb) {
+// ties_u: boundaries between equal 32-bit prefixes were valued by the tie-run kernel
+__global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb, bool ties_u) {
   uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (b < nb) op_lcp(T, b);
+  if (b >= nb) return;
+  if (ties_u && T.sck[b] == T.sck[b + 1]) return;
+  op_lcp(T, b);
 }
 __global__ void __launch_bounds__(BS) k_min64(const uint8_t* in, uint64_t nin, uint8_t* out, uint64_t nout) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -1145,7 +1187,10 @@ struct SortIO {
   bool ck_ready = false;  // ck_path: ck0/idx0 already hold the 32-bit sort keys (k_hash_keys_ck)
   bool ck_path = false;   // unsegmented plain build: sort (32-bit prefix, idx) only, never gather the keys
   // out
+  uint8_t* u = nullptr;  // ck_path: boundary values, written for the tie runs' inner boundaries
+  uint32_t depth0 = 0;
   const uint32_t* sck = nullptr;  // ck_path: the sorted 32-bit key prefixes (skey not gathered)
+  bool ties_u = false;            // u holds the tie runs' boundaries (k_lcp skips them)
   uint64_t m;
   uint32_t* sidx;
   bool fallback;
@@ -1182,7 +1227,14 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
     const bool flip = radix_sort_pairs<uint32_t>(c0, idx0, c1, idx1, n, 0, 32, rs_scratch, st);
     uint32_t* c32 = flip ? c1 : c0;
     idxs = flip ? idx1 : idx0;
-    hipLaunchKernelGGL(k_tie_fix_ck, GRID(n, BS), dim3(BS), 0, st, c32, idxs, n, (const uint64_t*)K32, T.ctr + CTR_TIE);
+    static const bool tie_one = getenv("KHST_TIE_ONE") != nullptr;  // measurement switch
+    if (tie_one) {
+      hipLaunchKernelGGL(k_tie_fix_ck, GRID(n, BS), dim3(BS), 0, st, c32, idxs, n, (const uint64_t*)K32,
+                         T.ctr + CTR_TIE);
+    } else {
+      hipLaunchKernelGGL(k_tie_fix_ck_blk, GRID(n, TF_ITEMS * BS), dim3(BS), 0, st, c32, idxs, n,
+                         (const uint64_t*)K32, T.ctr + CTR_TIE, S.u, S.depth0);
+    }
     LAUNCH_CHECK();
     HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -1215,6 +1267,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
       S.sidx = oidx;
       S.sck = ock;
       S.fallback = false;
+      S.ties_u = !tie_one && S.u && m == n;  // no dedup: the run boundaries' values stand
       return;
     }
   } else {
@@ -1458,10 +1511,13 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint64_t m = n;
   uint32_t* sidx = nullptr;
   bool fallback = false;
+  bool ties_u = false;
   {
     SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr,
              A.kn, ck_ready};
     S.ck_path = ck_path;
+    S.u = T.u;
+    S.depth0 = A.depth0;
     sort_dedup(c, S);
     m = S.m;
     sidx = S.sidx;
@@ -1469,6 +1525,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     sseg = S.sseg;
     fallback = S.fallback;
     T.sck = S.sck;  // non-null: no sorted keys materialised (trie_ops.h sorted_key)
+    ties_u = S.ties_u;
   }
   const bool ties = fallback;
   T.m = m;
@@ -1530,7 +1587,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));                  // every leaf a hash unless it says otherwise
   }
   if (nb > 0) {
-    hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb);
+    hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb, ties_u);
     LAUNCH_CHECK();
   }
   // Early leaves (plain root builds) need only the boundaries: they are hashed in input

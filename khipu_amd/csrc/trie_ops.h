@@ -164,7 +164,8 @@ struct Topo {
   uint8_t* u;             // [m-1] boundary values
   int32_t* psv;           // [m-1] previous strictly smaller boundary (-1: none)
   int32_t* nsv;           // [m-1] next strictly smaller boundary (-1: none)
-  int32_t* pse;           // [m-1] previous smaller-or-equal boundary (-1: none)
+  int32_t* pse;           // [m-1] previous boundary of the same group (its smaller-or-equal neighbour
+                          //       when that carries the same value; -1: the group's first)
   uint32_t* rep;          // [m-1] group representative of b
   uint8_t* ord;           // [m-1] ordinal of b within its group
   uint32_t* isrep_bid;     // [m-1] 1 if rep, then (after scan) branch id of rep
@@ -454,11 +455,12 @@ KH_HD void op_ansv(const Topo& T, const Pyr& P, uint64_t b) {
     return;
   }
   int64_t pse = ansv_left(P, b, t + 1);
-  T.pse[b] = (int32_t)pse;
   if (pse >= 0 && T.u[pse] == t) {
-    T.glast[pse] = 0;  // the predecessor has a later member
+    T.pse[b] = (int32_t)pse;  // the previous member of b's group
+    T.glast[pse] = 0;         // the predecessor has a later member
     return;
   }
+  T.pse[b] = -1;  // b is its group's first (the chain walk stops here)
   T.psv[b] = (int32_t)pse;
   T.nsv[b] = (int32_t)ansv_right(P, b, t);
 }
@@ -474,9 +476,9 @@ KH_HD void op_chain(const Topo& T, uint64_t b) {
   }
   int64_t j = (int64_t)b;
   uint32_t o = 0;
-  for (;;) {
+  for (;;) {  // one dependent load per step: pse holds same-group predecessors only
     int32_t q = T.pse[j];
-    if (q < 0 || T.u[q] != t) break;
+    if (q < 0) break;
     j = q;
     if (++o > 15) {  // impossible for a 16-ary trie: flag corruption
       T.ctr[CTR_ERR] = 1;
