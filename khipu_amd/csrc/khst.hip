@@ -398,9 +398,11 @@ __global__ void __launch_bounds__(BS) k_ansv(Topo T, Pyr P, uint64_t nb) {
   if (b < nb) op_ansv(T, P, b);
 }
 
+// The topology kernels that run beside the leaf kernel are grid-stride loops, so their
+// grid can be capped (topo_grid) to leave the leaf kernel more of the machine.
+#define GRID_STRIDE(i, n) for (uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x; i < (n); i += (uint64_t)gridDim.x * BS)
 __global__ void __launch_bounds__(BS) k_chain(Topo T, uint64_t nb) {
-  uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (b < nb) op_chain(T, b);
+  GRID_STRIDE(b, nb) op_chain(T, b);
 }
 // k_ansv with the early leaves' parent-depth scatter folded in (thread i also scatters
 // leaf i; grid over the m leaves): the leaf kernel waits for this kernel instead of a
@@ -434,11 +436,10 @@ __device__ __forceinline__ void block_add3(unsigned long long* c0, unsigned long
 }
 
 __global__ void __launch_bounds__(BS) k_branch_topo(Topo T, Pyr P, uint64_t nb) {
-  uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long ext = 0;
-  if (b < nb) {
+  GRID_STRIDE(b, nb) {
     op_branch_topo(T, P, nb, b);
-    if (T.u[b] != 0 && T.rep[b] == (uint32_t)b) ext = T.br_ext[T.isrep_bid[b]] ? 1 : 0;
+    if (T.u[b] != 0 && T.rep[b] == (uint32_t)b) ext += T.br_ext[T.isrep_bid[b]] ? 1 : 0;
   }
   block_add3(ctr_stat(T.ctr, CTR_EXT, blockIdx.x), ext, nullptr, 0, nullptr, 0);
 }
@@ -493,20 +494,20 @@ struct BrTab {
   uint8_t *depth, *ext, *pord;
 };
 __global__ void __launch_bounds__(BS) k_branch_permute(Topo T, BrTab J, const uint32_t* pos, const uint32_t* Bp) {
-  const uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (j >= *Bp) return;
-  const uint32_t g = pos[j], p = J.parent[j];
-  T.br_k[g] = J.k[j];
-  T.br_depth[g] = J.depth[j];
-  T.br_ext[g] = J.ext[j];
-  T.br_pord[g] = J.pord[j];
-  T.br_first[g] = J.first[j];
-  T.br_parent[g] = p == NONE ? NONE : pos[p];  // parents of neighbouring branches are neighbours
+  const uint64_t B = *Bp;
+  GRID_STRIDE(j, B) {
+    const uint32_t g = pos[j], p = J.parent[j];
+    T.br_k[g] = J.k[j];
+    T.br_depth[g] = J.depth[j];
+    T.br_ext[g] = J.ext[j];
+    T.br_pord[g] = J.pord[j];
+    T.br_first[g] = J.first[j];
+    T.br_parent[g] = p == NONE ? NONE : pos[p];  // parents of neighbouring branches are neighbours
+  }
 }
 // group reps carry level-order branch ids from here on (leaf parents, resident tables)
 __global__ void __launch_bounds__(BS) k_bid_remap(Topo T, const uint32_t* pos, uint64_t nb) {
-  const uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (b < nb && T.u[b] != 0 && T.rep[b] == (uint32_t)b) T.isrep_bid[b] = pos[T.isrep_bid[b]];
+  GRID_STRIDE(b, nb) if (T.u[b] != 0 && T.rep[b] == (uint32_t)b) T.isrep_bid[b] = pos[T.isrep_bid[b]];
 }
 
 // level bounds: lb[d] = first position of depth d in `order`, lb[64] = B
@@ -617,8 +618,7 @@ __global__ void __launch_bounds__(BS) k_leaf_topo_early(Topo T) {
 }
 // the same publish split in two (trie_ops.h op_leaf_link / op_leaf_move)
 __global__ void __launch_bounds__(BS) k_leaf_link(Topo T) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i < T.m) op_leaf_link(T, i);
+  GRID_STRIDE(i, T.m) op_leaf_link(T, i);
 }
 __global__ void __launch_bounds__(BS) k_leaf_move(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -1106,6 +1106,7 @@ static size_t carve_size(const std::vector<size_t>& items) {
 
 struct kh_ctx {
   int dev = 0;
+  int n_cu = 256;  // compute units of the device
   hipStream_t own = nullptr;
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // leaf hashing, concurrent with the branch topology
@@ -1577,6 +1578,18 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint32_t* Bp = (uint32_t*)(ctr + CTR_B);
   HIPCHK(hipMemsetAsync(ctr + CTR_B, 0, 8 * 6, st));  // B, br bytes, lf bytes, C, E0, E1
   Pyr P{};
+  // Grid of the topology kernels that run beside the leaf kernel (early builds): capped at
+  // 4 blocks per CU, so they leave the leaf kernel more of the machine and still finish
+  // first.  Measured at 100M (profiles/r2zg_cap_ab_100m.json): 46.5 ms against 47.4 uncapped
+  // (one thread per element); 2 blocks per CU starve the topology (23.7 ms, step 49.2),
+  // 8 per CU slow the leaf kernel (18.8 ms, step 48.5).  KHST_TOPO_BPC: blocks per CU
+  // (measurement switch; 0 = one thread per element).
+  static const int topo_bpc = getenv("KHST_TOPO_BPC") ? atoi(getenv("KHST_TOPO_BPC")) : 4;
+  const uint32_t topo_cap = topo_bpc > 0 ? (uint32_t)(topo_bpc * c->n_cu) : 0u;
+  auto topo_grid = [&](uint64_t cnt) {
+    const uint64_t g = (cnt + BS - 1) / BS;
+    return dim3((unsigned)(early && topo_cap && g > topo_cap ? topo_cap : (g ? g : 1)));
+  };
   static const int pd_env = [] {
     const char* e = getenv("KHST_PD");  // measurement switch
     return !e ? PD_DEFAULT : strcmp(e, "ansv") == 0 ? 1 : 0;
@@ -1636,7 +1649,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       hipLaunchKernelGGL(k_ansv, GRID(nb, BS), dim3(BS), 0, st, T, P, nb);
     LAUNCH_CHECK();
     if (pd_mode == 1) launch_leaves(false);
-    hipLaunchKernelGGL(k_chain, GRID(nb, BS), dim3(BS), 0, st, T, nb);
+    hipLaunchKernelGGL(k_chain, topo_grid(nb), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
     scan_exclusive<uint32_t>(T.isrep_bid, T.isrep_bid, nb, Bp, scan_scratch, st);
     // branch tables in key-order ids first (k_branch_topo writes them, thread per boundary)
@@ -1647,7 +1660,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     TJ.br_depth = J.depth;
     TJ.br_ext = J.ext;
     TJ.br_pord = J.pord;
-    hipLaunchKernelGGL(k_branch_topo, GRID(nb, BS), dim3(BS), 0, st, TJ, P, nb);
+    hipLaunchKernelGGL(k_branch_topo, topo_grid(nb), dim3(BS), 0, st, TJ, P, nb);
     LAUNCH_CHECK();
     // level order (grids sized by nb; threads past B exit), then every branch id
     // becomes its level position
@@ -1662,17 +1675,17 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
                        lb);
     LAUNCH_CHECK();
     HIPCHK(hipMemsetAsync(T.br_k, 0, nb * 4, st));  // entries past B must scan as 0
-    hipLaunchKernelGGL(k_branch_permute, GRID(nb, BS), dim3(BS), 0, st, T, J, (const uint32_t*)order,
+    hipLaunchKernelGGL(k_branch_permute, topo_grid(nb), dim3(BS), 0, st, T, J, (const uint32_t*)order,
                        (const uint32_t*)Bp);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_bid_remap, GRID(nb, BS), dim3(BS), 0, st, T, (const uint32_t*)order, nb);
+    hipLaunchKernelGGL(k_bid_remap, topo_grid(nb), dim3(BS), 0, st, T, (const uint32_t*)order, nb);
     LAUNCH_CHECK();
     // child record bases
     scan_exclusive<uint32_t>(T.br_k, T.br_cbase, nb, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
   }
   static const bool split_publish = !getenv("KHST_PUBLISH_ONE");  // measurement switch
   if (early && split_publish) {  // the leaves' slots, while they are still being hashed
-    hipLaunchKernelGGL(k_leaf_link, GRID(m, BS), dim3(BS), 0, st, T);
+    hipLaunchKernelGGL(k_leaf_link, topo_grid(m), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
   }
   if (early) {
@@ -1828,6 +1841,7 @@ static kh_ctx* ctx_new(int dev) {
   // over the VALU-bound leaf kernel they overlap with (st2)
   int prio_lo = 0, prio_hi = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  HIPCHK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->dev));
   // The topology stream (st) has the priority over the leaf stream (st2): the leaf kernel
   // then shares the CUs with the topology (18 ms instead of 14.7 alone) but the topology
   // stays off the critical path.  Measured (profiles/r2za_*, r2zc_*): the leaf stream first
