@@ -319,6 +319,31 @@ def test_branch_variants_vs_oracle(khst, oracle, variant, monkeypatch):
     assert hh[0].tobytes() == roots[0] and st.n_node_perms == bst["node_perms"], variant
 
 
+def test_tie_runs_across_blocks(khst, oracle):
+    """Many runs of equal 32-bit sort prefixes (2..64 keys each, some spanning the tie
+    kernel's 1,024-position blocks), raw 32-byte keys: the runs are ordered by the whole
+    key and their inner boundaries valued by the tie kernel (k_lcp skips them); with and
+    without repeated keys (a dedup shifts positions: k_lcp then values every boundary).
+    Roots equal the CPU batch builder's."""
+    import random
+    r = random.Random(23)
+    keys = []
+    while len(keys) < 60_000:
+        pre = bytes(r.getrandbits(8) for _ in range(4))
+        keys += [pre + bytes(r.getrandbits(8) for _ in range(28)) for _ in range(r.randint(2, 64))]
+    keys += [bytes(r.getrandbits(8) for _ in range(32)) for _ in range(20_000)]
+    r.shuffle(keys)
+    vals = [bytes([r.getrandbits(8) | 1]) * r.choice([1, 5, 40, 80]) for _ in keys]
+    from khipu_amd._lib import KhStats
+    want = oracle.batch_root(keys, vals, nthreads=4)
+    st = KhStats()
+    assert khst.trie_root(keys, vals, stats=st) == want
+    assert st.full_sort == 0
+    rep = keys + [keys[r.randrange(len(keys))] for _ in range(500)]
+    rvals = vals + [bytes([7]) * 33 for _ in range(500)]
+    assert khst.trie_root(rep, rvals) == oracle.batch_root(rep, rvals, nthreads=4)
+
+
 def test_hashed_keys_with_repeats(khst, oracle):
     """Hashed-key builds (the plain path: 32-bit sort prefixes from the hashing pass, ties
     ordered by the whole key, the last put of a repeated key kept) over sizes around the
