@@ -1070,6 +1070,9 @@ struct DevBuf {
   ~DevBuf() { release(); }  // a throw between ensure() and release() does not leak HBM
   void ensure(size_t bytes) {
     if (bytes <= cap) return;
+    // work still reading the old buffer may be in flight (kh_dev_partition_ev returns before
+    // its value copy ends): drain the device before the buffer goes (growth is rare)
+    if (p) HIPCHK(hipDeviceSynchronize());
     if (p) HIPCHK(hipFree(p));
     p = nullptr;
     cap = 0;
