@@ -201,11 +201,14 @@ KH_HD void hp_nibbles(const uint8_t* b, uint32_t len, uint32_t* n, bool* leaf, u
   // HexPrefix.decode (HexPrefix.scala:30-40): flag nibble, optional pad nibble
   const uint32_t f = b[0] >> 4;
   *leaf = (f & 2) != 0;
+  // *n is the FULL nibble count (it may exceed 64: the caller rejects such a path); only the
+  // first 64 nibbles are written to out
   uint32_t k = 0;
   if (f & 1) out[k++] = b[0] & 0xF;
-  for (uint32_t i = 1; i < len && k < 64; ++i) {
-    out[k++] = b[i] >> 4;
-    if (k < 64) out[k++] = b[i] & 0xF;
+  for (uint32_t i = 1; i < len; ++i) {
+    if (k < 64) out[k] = b[i] >> 4;
+    if (k + 1 < 64) out[k + 1] = b[i] & 0xF;
+    k += 2;
   }
   *n = k;
 }

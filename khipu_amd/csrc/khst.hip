@@ -1061,29 +1061,58 @@ __global__ void __launch_bounds__(BS) k_synth_write(uint32_t cfg, uint64_t first
 // ---------------------------------------------------------------------------
 // device workspace
 // ---------------------------------------------------------------------------
+// selects device d (d >= 0) for the guard's scope, restoring the caller's device after
+struct DevScope {
+  int prev = -1;
+  explicit DevScope(int d) {
+    int cur = -1;
+    if (d >= 0 && hipGetDevice(&cur) == hipSuccess && cur != d && hipSetDevice(d) == hipSuccess) prev = cur;
+  }
+  ~DevScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DevScope(const DevScope&) = delete;
+  DevScope& operator=(const DevScope&) = delete;
+};
+
+// A device buffer that remembers the GPU it lives on: growth drains and frees on THAT
+// device, and allocates on `on` (or on the current device when on < 0).
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  int dev = -1;
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }  // a throw between ensure() and release() does not leak HBM
-  void ensure(size_t bytes) {
-    if (bytes <= cap) return;
-    // work still reading the old buffer may be in flight (kh_dev_partition_ev returns before
-    // its value copy ends): drain the device before the buffer goes (growth is rare)
-    if (p) HIPCHK(hipDeviceSynchronize());
-    if (p) HIPCHK(hipFree(p));
+  void ensure(size_t bytes, int on = -1) {
+    if (on < 0) {
+      if (hipGetDevice(&on) != hipSuccess) on = 0;
+    }
+    if (bytes <= cap && dev == on) return;
+    if (p) {
+      // work still reading the old buffer may be in flight (kh_dev_partition_ev returns before
+      // its value copy ends): drain its device before the buffer goes (growth is rare)
+      DevScope ds(dev);
+      HIPCHK(hipDeviceSynchronize());
+      HIPCHK(hipFree(p));
+    }
     p = nullptr;
     cap = 0;
     size_t want = bytes + bytes / 8 + 4096;
+    DevScope ds(on);
     HIPCHK(hipMalloc(&p, want));
     cap = want;
+    dev = on;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      DevScope ds(dev);
+      (void)hipFree(p);
+    }
     p = nullptr;
     cap = 0;
+    dev = -1;
   }
 };
 
@@ -3171,7 +3200,10 @@ int kh_dev_partition_ev(kh_ctx* c, void* vals_done, const uint8_t* d_keys32, con
     HIPCHK(hipSetDevice(c->dev));
     memset(h_counts, 0, nparts * 8);
     memset(h_bytes, 0, nparts * 8);
-    if (n == 0) return KH_OK;
+    if (n == 0) {  // nothing to copy: vals_done is still recorded, as khst.h promises
+      if (vals_done) HIPCHK(hipEventRecord((hipEvent_t)vals_done, c->st));
+      return KH_OK;
+    }
     if (n >= (1ULL << 31)) throw KhError{KH_EINVAL, "n must be < 2^31 per device"};
     if ((uintptr_t)d_keys32 & 7 || (uintptr_t)d_out_keys & 7 || (uintptr_t)d_voff & 7 || (uintptr_t)d_out_vlen & 7 ||
         (uintptr_t)d_out_vals & 7)

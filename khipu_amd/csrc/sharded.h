@@ -166,7 +166,7 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
     Staged in = stage_inputs(c, keys + s.lo * klen, klen, vals, voff + s.lo, s.n, nullptr);
     const uint8_t* K = in.keys;
     if (flags & KH_HASH_KEYS) {
-      s.k32.ensure(s.n * 32 + 64);
+      s.k32.ensure(s.n * 32 + 64, c->dev);
       if (klen <= 135)
         hipLaunchKernelGGL(k_hash_keys<true>, GRID(s.n, BS), dim3(BS), 0, c->st, in.keys, klen, s.n, (uint64_t*)s.k32.p);
       else
@@ -175,9 +175,9 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
       K = (const uint8_t*)s.k32.p;
     }
     const uint64_t vb = voff[s.lo + s.n] - voff[s.lo];
-    s.pk.ensure(s.n * 32 + 64);
-    s.pv.ensure(vb + 64);
-    s.pl.ensure(s.n * 8 + 64);
+    s.pk.ensure(s.n * 32 + 64, c->dev);
+    s.pv.ensure(vb + 64, c->dev);
+    s.pl.ensure(s.n * 8 + 64, c->dev);
     int rc = kh_dev_partition(c, K, in.vals, in.voff, s.n, N, (uint8_t*)s.pk.p, (uint8_t*)s.pv.p, (uint64_t*)s.pl.p,
                               s.cnt, s.nb);
     if (rc != KH_OK) throw KhError{rc, "partition: " + g_err};
@@ -196,10 +196,12 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
     }
     S[p]->m = m;
     S[p]->mb = mb;
-    S[p]->rk.ensure(m * 32 + 64);
-    S[p]->rl.ensure(m * 8 + 64);
-    S[p]->rv.ensure(mb + 64);
-    S[p]->rvo.ensure((m + 1) * 8 + 64);
+    // receive buffers live on the OWNER's device (this loop runs on the caller's thread)
+    const int pd = S[p]->c->dev;
+    S[p]->rk.ensure(m * 32 + 64, pd);
+    S[p]->rl.ensure(m * 8 + 64, pd);
+    S[p]->rv.ensure(mb + 64, pd);
+    S[p]->rvo.ensure((m + 1) * 8 + 64, pd);
   }
   for (uint32_t g = 0; g < N; ++g) {
     uint64_t o = 0, ob = 0;
@@ -211,7 +213,7 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
     }
   }
   const auto t1 = std::chrono::steady_clock::now();
-  for (uint32_t p = 0; p < N; ++p) S[p]->vscan.ensure(scan_scratch_bytes(S[p]->m, 8) + 256);
+  for (uint32_t p = 0; p < N; ++p) S[p]->vscan.ensure(scan_scratch_bytes(S[p]->m, 8) + 256, S[p]->c->dev);
   // the offsets of the received values, on the shard's exchange stream once its lengths
   // and bytes have landed; the build's leaf stage waits for ev_vals
   auto value_offsets = [&](Shard& s) {
