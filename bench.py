@@ -47,7 +47,7 @@ sys.path.insert(0, ROOT)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 HBM_PEAK = 8.0e12
 OPS_PER_PERM = 5760  # 24 rounds x 240 int32 ops
-SEQ_SAMPLES = (20_000, 50_000, 100_000)
+SEQ_SAMPLES = (20_000, 50_000, 100_000, 1_000_000)
 
 
 def parse():
@@ -93,14 +93,15 @@ def cpu_threads(req=0):
 
 def fit_put_cost(samples):
     """Least-squares fit of us/put = a + b * log16(n) over (n, seconds) samples (the
-    sequential put descends ~log16(n) levels)."""
+    sequential put descends ~log16(n) levels).  Returns (a, b, residuals in us/put)."""
     xs = np.array([math.log(n, 16) for n, _ in samples])
     ys = np.array([t / n * 1e6 for n, t in samples])
     if len(samples) < 2:
-        return float(ys[0]), 0.0
+        return float(ys[0]), 0.0, [0.0]
     A = np.stack([np.ones_like(xs), xs], 1)
     (a, b), *_ = np.linalg.lstsq(A, ys, rcond=None)
-    return float(a), float(b)
+    res = ys - (a + b * xs)
+    return float(a), float(b), [round(float(r), 4) for r in res]
 
 
 def host_inputs(addr, vals, voff, n):
@@ -120,20 +121,20 @@ def cpu_baseline(ctx, cfg, addr, vals, voff, samples):
         hh, _, _, _ = ctx.build(addr, 20, vals, voff, s, hash_keys=True)
         a, vb, vo = host_inputs(addr, vals, voff, s)
         t0 = time.perf_counter()
-        keys = np.frombuffer(b"".join(oracle.kec256(a[20 * i:20 * i + 20].tobytes()) for i in range(s)), np.uint8)
-        root = oracle.seq_root_packed(keys, 32, vb, vo, s)
+        root = oracle.seq_root_packed(a, 20, vb, vo, s, mode=2)  # keys hashed in C, inside the put loop
         dt = time.perf_counter() - t0
         assert hh[0].tobytes() == root, f"GPU/CPU root mismatch on the {s}-account sample"
         rows.append({"accounts": s, "seconds": round(dt, 3), "us_per_put": round(dt / s * 1e6, 3),
                      "node_hashes": int(st.n_node_hashes)})
-    a, b = fit_put_cost([(r["accounts"], r["seconds"]) for r in rows])
+    a, b, res = fit_put_cost([(r["accounts"], r["seconds"]) for r in rows])
     big = rows[-1]
     est = 1e8 * (a + b * math.log(1e8, 16)) * 1e-6
     return {"value": big["node_hashes"] / big["seconds"], "unit": "node-hashes/s", "cores": 1, "kind": "port",
             "sample": f"first {big['accounts']} accounts of the same synthetic workload, sequential put per account "
                       f"(MerklePatriciaTrie.scala:157-281 as driven by TrieAccounts.flush), key hashing included; "
                       f"{big['seconds']:.2f} s; GPU root asserted equal on every sample; CPU: {cpu_model()}",
-            "samples": rows, "fit_us_per_put": {"a": round(a, 4), "b_per_log16n": round(b, 4)},
+            "samples": rows, "fit_us_per_put": {"a": round(a, 4), "b_per_log16n": round(b, 4),
+                                                "residual_us_per_put": res},
             "state_root_s_extrapolated_100M": round(est, 1),
             "extrapolation": "100M x (a + b log16 100M) us from the fitted samples (not run)"}
 

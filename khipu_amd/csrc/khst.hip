@@ -2034,6 +2034,11 @@ __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32
       if (L[0] == K[0] && L[1] == K[1] && L[2] == K[2] && L[3] == K[3]) {
         replaced[r] = 1;  // keys are unique in the batch: one op per leaf
         atomicAdd(&ctr[1], 1ULL);
+        // khipu's put into a leaf whose remaining path is EMPTY (it hangs under a depth-63
+        // branch) turns it into a childless value-only branch (putInLeafNode, ml == 0 with
+        // an empty existingKey: MerklePatriciaTrie.scala:187-199 -> putInBranchNode
+        // :258-262), a non-canonical node this engine does not build: refused, not diverged
+        if (d == 64 && O.kind[o] == FOP_UPSERT) atomicOr(&ctr[3], 1ULL);
       }
       return;
     }
@@ -2226,6 +2231,14 @@ __global__ void __launch_bounds__(BS) k_map_delete(AMap M, Recs R, const uint32_
   if (i >= n || list[i] == NONE) return;
   const uint64_t sl = map_slot_of(M, R, list[i]);
   if (sl != ~0ULL) M.tag[sl] = 1;  // tombstone
+}
+// an aborted commit: the records its descent flagged are left as they were
+__global__ void __launch_bounds__(BS) k_f_untouch(const uint32_t* list, uint64_t n, uint32_t* touched,
+                                                  uint8_t* replaced) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  touched[list[i]] = 0;
+  replaced[list[i]] = 0;
 }
 __global__ void __launch_bounds__(BS) k_rec_dead(Recs R, const uint32_t* list, uint64_t n, uint32_t* touched,
                                                  uint8_t* replaced) {
@@ -2644,10 +2657,22 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   hipLaunchKernelGGL(k_f_descend, GRID(nd, BS), dim3(BS), 0, st, O, map_of(h), recs_of(h), (uint32_t*)h->touched.p,
                      (uint8_t*)h->replaced.p, tlist, fctr);
   LAUNCH_CHECK();
-  HIPCHK(hipMemcpyAsync(c->h_pinned, fctr, 24, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(c->h_pinned, fctr, 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const uint64_t ntl = c->h_pinned[0], nrep = c->h_pinned[1];
   if (c->h_pinned[2]) throw KhError{KH_EINTERNAL, "forest descent: corrupt anchor map"};
+  if (c->h_pinned[3]) {  // nothing has changed yet: clear the descent's flags and refuse the batch
+    if (ntl) {
+      hipLaunchKernelGGL(k_f_untouch, GRID(ntl, BS), dim3(BS), 0, st, (const uint32_t*)tlist, ntl,
+                         (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p);
+      LAUNCH_CHECK();
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    throw KhError{KH_EINVAL,
+                  "put of a key whose leaf has an empty remaining path (63 nibbles shared with another key): khipu "
+                  "turns that leaf into a value-only branch (MerklePatriciaTrie.scala:187-199), which this engine "
+                  "does not reproduce; the trie is unchanged"};
+  }
   // ---- 3. elements: upserts (values appended to the heap), untouched children, kept leaves, roots
   const uint64_t ecap = (uint64_t)nups + 16 * ntl + nt + 16;
   regrow(h->heap, h->heap_n, h->heap_n + ubytes + 64, st);

@@ -250,6 +250,30 @@ def sharded_root(be, addr, vals, voff, n, klen=20, keys_prehashed=False, phases=
     return root.cpu().numpy().tobytes()
 
 
+# State roots of the synthetic workloads (csrc/synth.h), keyed by (config id, accounts),
+# each asserted equal to the independent CPU batch builder (oracle/batch_root.cc) by a
+# full-size `bench.py` run (profiles/r2zp_bench_100m.json, profiles/r3a_bench_100m.json).
+PINNED_ROOTS = {
+    (5, 100_000_000): "577f095224664dc395ca23578afe7bd0c82dbeb5a863285af99e8271a81b9cad",
+}
+
+
+def self_check(be, cfg, n_total, root):
+    """Rank 0: the sharded root must equal the single-GPU root of the SAME workload
+    (regenerated in full on this rank: the synthesis is counter-based) and, where one is
+    pinned, the CPU-checked root.  Returns (ok, report)."""
+    import torch as _t
+    A, V, O = be.ctx.synth_accounts(cfg, 0, n_total)
+    hh, _, _, _ = be.ctx.build(A, 20, V, O, n_total, hash_keys=True)
+    single = hh[0].tobytes()
+    del A, V, O
+    _t.cuda.empty_cache()
+    pinned = PINNED_ROOTS.get((cfg, n_total))
+    ok = single == root and (pinned is None or pinned == root.hex())
+    return ok, {"single_gpu_root": single.hex(), "pinned_root": pinned,
+                "sharded_root_equal": ok}
+
+
 def bench_main(args):
     """bench.py --gpus N under torch.distributed.run: strong scaling of the fixed
     args.accounts trie over WORLD_SIZE GPUs (one rank per GPU, RCCL)."""
@@ -313,6 +337,20 @@ def bench_main(args):
     ph = torch.tensor([phases[k] for k in sorted(phases)], dtype=torch.float64, device=f"cuda:{local}")
     dist.all_reduce(ph, op=dist.ReduceOp.MAX)
     phases = {k: round(float(v), 3) for k, v in zip(sorted(phases), ph.tolist())}
+    # self-check (after the timed region): a wrong root must not be reported as throughput
+    ok = torch.ones(1, dtype=torch.int64, device=f"cuda:{local}")
+    check = None
+    if rank == 0:
+        good, check = self_check(be, args.cfg, n_total, root)
+        ok[0] = int(good)
+    dist.broadcast(ok, 0)
+    if not int(ok.item()):
+        if rank == 0:
+            import sys
+            print(f"sharded root {root.hex()} FAILED its self-check: {check}", file=sys.stderr, flush=True)
+        dist.barrier()
+        dist.destroy_process_group()
+        raise SystemExit(1)
     if rank == 0:
         out = {
             "metric": "node-hashes/sec (full state root, 100M-account trie)",
@@ -325,6 +363,7 @@ def bench_main(args):
             "state_root": root.hex(),
             "topology": {"n_leaves": int(hashes[1].item()), "n_branches": int(hashes[2].item()) + 1,
                          "n_node_hashes": node_hashes},
+            "parity": check,
             "phase_ms_max_over_ranks": phases,
             "per_rank_build_ms": st.t_total_ms,
             "roofline": roof,

@@ -1026,22 +1026,30 @@ int64_t or_trie_reachable(or_trie* t, uint8_t* hashes, uint64_t hcap, uint8_t* e
 
 // Sequential batch: the TrieAccounts.flush pattern (TrieAccounts.scala:22-28):
 // one trie instance, foldLeft of put (or remove when `is_del[i]`), then rootHash.
-// keys: n * klen bytes; vals packed with voff[n+1].  mode 1 = GenesisDataLoader
+// keys: n * klen bytes; vals packed with voff[n+1].  mode bit 1 = GenesisDataLoader
 // pattern (GenesisDataLoader.scala:139-147): a fresh instance per put, persist
-// after each.
+// after each; mode bit 2 = the key is kec256 of the given bytes, hashed inside the
+// loop (Address.hashedAddressEncoder, Address.scala:15-17).
 int or_seq_root(const uint8_t* keys, uint64_t klen, const uint8_t* vals, const uint64_t* voff, const uint8_t* is_del,
                 uint64_t n, int mode, uint8_t* out32) {
   try {
     Storage st;
     MPT m(&st, EMPTY_TRIE_HASH);
+    const bool genesis = (mode & 1) != 0;
+    const bool hash_keys = (mode & 2) != 0;  // key = kec256(key bytes): Address.hashedAddressEncoder
     for (uint64_t i = 0; i < n; ++i) {
-      if (mode == 1) m = MPT(&st, m.rootHash());
+      if (genesis) m = MPT(&st, m.rootHash());
       Bytes k((const char*)keys + i * klen, klen);
+      if (hash_keys) {
+        uint8_t h[32];
+        keccak256_pad((const uint8_t*)k.data(), k.size(), 0x01, h);
+        k.assign((const char*)h, 32);
+      }
       if (is_del && is_del[i])
         m.remove(k);
       else
         m.put(k, Bytes((const char*)vals + voff[i], voff[i + 1] - voff[i]));
-      if (mode == 1) m.persist();
+      if (genesis) m.persist();
     }
     Bytes r = m.rootHash();
     memcpy(out32, r.data(), 32);

@@ -176,6 +176,7 @@ def seq_root(keys, vals, dels=None, mode=0) -> bytes:
 
     mode 0: TrieAccounts.flush pattern (TrieAccounts.scala:22-28), one instance.
     mode 1: GenesisDataLoader pattern (GenesisDataLoader.scala:139-147).
+    mode | 2: every key is kec256 of the given bytes, hashed in C inside the loop.
     keys: list of equal-length bytes; vals: list of bytes.
     """
     import numpy as np

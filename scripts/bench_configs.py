@@ -13,7 +13,9 @@
 Inputs are generated on the device before the timed region.  Prints one JSON line per
 config.  Parity of these paths is tests/test_gpu_configs.py, test_gpu_resident.py and
 test_gpu_parity.py; here every root is also cross-checked against a from-scratch device
-build of the same final set.
+build of the same final set and (unless --no-cpu) against the independent CPU batch builder
+(oracle/batch_root.cc: the 50M final state root, all 2,000 storage roots, all 100k
+segmented roots).
 """
 import argparse
 import json
@@ -110,17 +112,35 @@ def cfg3(args):
     K, V, O, N = w.final_accounts()
     hf, _, _, _ = ctx.build(K, 32, V, O, N)
     assert hf[0].tobytes() == root, "block-commit state root != full build of the final state"
+    checked = "state root and all 2,000 storage roots == full GPU builds"
+    if not args.no_cpu:  # the independent CPU batch builder over the whole final state
+        from oracle import oracle
+        vo = O.cpu().numpy().astype(np.uint64)
+        tc = time.perf_counter()
+        cpu, _ = oracle.batch_roots(K.cpu().numpy(), (V[:int(vo[-1])].cpu().numpy(), vo), klen=32,
+                                    nthreads=args.cpu_threads)
+        cpu_s = time.perf_counter() - tc
+        assert cpu[0] == root, "block-commit state root != CPU batch build of the final state"
     del K, V, O
     K, V, O, T, N = w.final_storage()
     hh, _, _, _ = ctx.build(K, 32, V, O, N, seg=T, nseg=w.nc, hash_keys=True)
     bad = [c for c in range(w.nc) if hh[c].tobytes() != w.roots[c]]
     assert not bad, f"storage roots differ from full builds: {bad[:5]}"
+    if not args.no_cpu:
+        so = O.cpu().numpy().astype(np.uint64)
+        seg_off = np.searchsorted(T.cpu().numpy(), np.arange(w.nc + 1)).astype(np.uint64)
+        cs, _ = oracle.batch_roots(K.cpu().numpy(), (V[:int(so[-1])].cpu().numpy(), so), klen=32, seg_off=seg_off,
+                                   hash_keys=True, nthreads=args.cpu_threads)
+        bad = [c for c in range(w.nc) if cs[c] != w.roots[c]]
+        assert not bad, f"storage roots differ from the CPU batch builder: {bad[:5]}"
+        checked = (f"state root and all 2,000 storage roots == full GPU builds AND == the CPU batch builder "
+                   f"(oracle/batch_root.cc, {args.cpu_threads} threads, state root {cpu_s:.1f} s)")
     return {"config": f"configs[2]: 20k dirty accounts + 2,000 storage tries x 10 dirty slots per block over a "
                       f"{args.resident // 10**6}M-account resident trie (kh_block_commit)",
             "open_s": open_s, "block_ms_median": float(np.median(ms)), "block_ms_all": ms.tolist(),
             "rehashed_nodes_median": int(np.median([x[1] for x in blocks])),
             "ops_per_block": int(blocks[0][2]), "resident_accounts_after": len(w.state),
-            "state_root_after": root.hex(), "checked": "state root and all 2,000 storage roots == full GPU builds"}
+            "state_root_after": root.hex(), "checked": checked}
 
 
 def cfg4(args):
@@ -159,10 +179,21 @@ def cfg4(args):
         o1 = (voff[lo:hi + 1] - voff[lo]).contiguous()
         h1, _, _, _ = ctx.build(k1, 32, v1, o1, hi - lo, hash_keys=True)
         assert h1[0].tobytes() == hh[s].tobytes(), f"segment {s} root differs"
+    checked = f"segments {checks} rebuilt alone give the same roots"
+    if not args.no_cpu:  # every one of the 100k roots against the independent CPU batch builder
+        from oracle import oracle
+        tc = time.perf_counter()
+        cpu, _ = oracle.batch_roots(keys.cpu().numpy(), (vals[:int(so[-1])].cpu().numpy(), so.astype(np.uint64)),
+                                    klen=32, seg_off=offs.astype(np.uint64), hash_keys=True,
+                                    nthreads=args.cpu_threads)
+        gpu = [hh[s].tobytes() if c[s] else None for s in range(nseg)]
+        bad = [s for s in range(nseg) if cpu[s] != gpu[s]]
+        assert not bad, f"segmented roots differ from the CPU batch builder: {bad[:5]}"
+        checked += f"; all {nseg} roots == the CPU batch builder ({time.perf_counter() - tc:.1f} s)"
     return {"config": f"configs[3]: {nseg} storage tries, {n} slots (log-uniform 1..1e4 per trie)",
             "ms": dt * 1e3, "device_ms": st.t_total_ms, "slots": n, "node_hashes": st.n_node_hashes,
             "node_hashes_per_s": st.n_node_hashes / dt, "node_perms": st.n_node_perms,
-            "key_perms": st.n_key_perms, "checked_segments": checks,
+            "key_perms": st.n_key_perms, "checked": checked,
             "stage_ms": {"keys": st.t_keys_ms, "sort": st.t_sort_ms, "topology": st.t_topo_ms,
                          "leaves": st.t_leaf_ms, "branches": st.t_branch_ms}}
 
@@ -173,6 +204,8 @@ def main():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--resident", type=int, default=50_000_000)
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU batch-builder checks")
+    p.add_argument("--cpu-threads", type=int, default=16)
     args = p.parse_args()
     for c in args.cfg:
         r = {2: cfg2, 3: cfg3, 4: cfg4}[c](args)

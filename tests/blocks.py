@@ -91,6 +91,8 @@ class BlockWorkload:
         self.state._open(self.keys, 32, self.vals, self.voff, n, False, emit=False)
         self.forest = ResidentForest(ctx, hash_keys=True)
         self.ups = []        # every block's account upserts (keys, bodies, offsets) in order
+        self.ups_pristine = []  # the same bodies as handed in, before kh_block_commit patched
+                                # the contracts' stateRoot fields in place
         self.slot_ups = []   # every block's storage upserts (trie, slot keys, values, offsets)
         self.roots = {}      # last root per storage trie
         self.t_commit = []
@@ -109,6 +111,7 @@ class BlockWorkload:
         na_up = a_tid.numel()
         na_del = 0 if a_del is None else a_del.numel() // 32
         st = KhStats()
+        self.ups_pristine.append(a_vals.clone())
         torch.cuda.synchronize()
         import time
         t0 = time.perf_counter()
@@ -155,16 +158,19 @@ class BlockWorkload:
         return self._commit(s_tid, s_keys, s_vals, s_voff, d_tid, d_keys, a_keys, a_vals, a_voff, a_tid, a_del)
 
     # ---- verification: one plain build of the final sequence of puts
-    def final_accounts(self):
+    def final_accounts(self, bodies=None):
         """(keys, vals, voff, N) device tensors: the initial records minus the deleted tail,
-        then every block's upserts in order (later puts win)."""
+        then every block's upserts in order (later puts win).  bodies: optional list of
+        per-block body buffers replacing the committed ones (same offsets)."""
         m = self.n - self.nblocks * self.ndel
         parts_k = [self.keys[:32 * m]]
         v0 = int(self.voff[m])
         parts_v = [self.vals[:v0]]
         parts_o = [self.voff[:m]]
         base = v0
-        for k, v, o, cnt in self.ups:
+        for bi, (k, v, o, cnt) in enumerate(self.ups):
+            if bodies is not None:
+                v = bodies[bi]
             parts_k.append(k[:32 * cnt])
             parts_v.append(v[:int(o[cnt])])
             parts_o.append(o[:cnt] + base)

@@ -47,5 +47,21 @@ def test_extrapolation_fit():
     import math
     a, b = 3.0, 4.0
     samples = [(n, n * (a + b * math.log(n, 16)) * 1e-6) for n in (20000, 50000, 100000)]
-    fa, fb = bench.fit_put_cost(samples)
+    fa, fb, res = bench.fit_put_cost(samples)
     assert abs(fa - a) < 1e-6 and abs(fb - b) < 1e-6
+    assert max(abs(r) for r in res) < 1e-6
+
+
+def test_seq_root_hashes_keys_in_c(oracle):
+    """mode 2 (keys hashed inside the C put loop) == hashing them first."""
+    import numpy as np
+    from khipu_amd import codec
+    rnd = np.random.default_rng(5)
+    addrs = [rnd.integers(0, 256, 20, dtype=np.uint8).tobytes() for _ in range(300)]
+    vals = [codec.account_rlp(i, 10 ** 18 + i) for i in range(300)]
+    vo = np.zeros(301, np.uint64)
+    vo[1:] = np.cumsum([len(v) for v in vals])
+    a = np.frombuffer(b"".join(addrs), np.uint8)
+    vb = np.frombuffer(b"".join(vals), np.uint8)
+    assert oracle.seq_root_packed(a, 20, vb, vo, 300, mode=2) == \
+        oracle.seq_root([oracle.kec256(x) for x in addrs], vals)

@@ -89,13 +89,31 @@ def test_config2_block_commits(khst, oracle):
         for i in range(a, e):
             t.put(oracle.kec256(kb[32 * i:32 * i + 32].tobytes()), vb[int(so[i]):int(so[i + 1])].tobytes())
         assert t.root_hash() == w.roots[c], c
-    # state trie
-    K, V, O, N = w.final_accounts()
-    hf, _, _, _ = ctx.build(K, 32, V, O, N)
-    assert hf[0].tobytes() == root
+    # storage-root injection (Account.withStateRoot, BlockWorldState.scala:243-248): every
+    # contract body of the last block carries its CPU-built storage root in bytes
+    # [len-65, len-33), every other byte is what the caller handed in
+    _, a_vals, a_voff, cnt = w.ups[-1]
+    av = a_vals.cpu().numpy()
+    pv = w.ups_pristine[-1].cpu().numpy()
+    ao = a_voff.cpu().numpy().astype(np.int64)
+    expect = pv.copy()
+    for c in range(w.nc):  # a_tid[c] = c (tests/blocks.py)
+        e = int(ao[c + 1])
+        assert av[e - 65:e - 33].tobytes() == cpu[c], c
+        assert pv[e - 66] == 0xa0 and av[e - 66] == 0xa0
+        expect[e - 65:e - 33] = np.frombuffer(cpu[c], np.uint8)
+    assert (av[:int(ao[cnt])] == expect[:int(ao[cnt])]).all()
+    # state trie: the committed state against a CPU batch build of the expected final state
+    # (the bodies as handed in, contracts patched with the CPU storage roots)
+    bodies = [torch.from_numpy(x.cpu().numpy()).to(x.device) for x in w.ups_pristine]
+    bodies[-1] = torch.from_numpy(expect).to(bodies[-1].device)
+    K, V, O, N = w.final_accounts(bodies=bodies)
     vo = O.cpu().numpy().astype(np.uint64)
     cpu, cst = oracle.batch_roots(K.cpu().numpy(), (V[:int(vo[-1])].cpu().numpy(), vo), klen=32)
     assert cpu[0] == root
     assert len(w.state) == cst["distinct"]
+    K, V, O, N = w.final_accounts()
+    hf, _, _, _ = ctx.build(K, 32, V, O, N)
+    assert hf[0].tobytes() == root
     # O(dirty) work: a block re-hashes a small fraction of the 1.36M nodes of a full build
     assert max(x[1] for x in w.t_commit) < 400_000, w.t_commit

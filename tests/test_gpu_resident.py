@@ -336,3 +336,43 @@ def test_host_handles_pair_on_the_shared_context(khst, oracle):
     assert got == oracle.seq_root(keys, exp_vals)
     lib().kh_trie_free(st_h)
     lib().kh_trie_free(fo_h)
+
+
+def test_update_of_empty_path_leaf_is_refused(khst, oracle):
+    """A later block updating a key whose leaf hangs under a depth-63 branch (its remaining
+    path is empty): khipu's putInLeafNode turns that leaf into a childless value-only branch
+    (MerklePatriciaTrie.scala:187-199 -> :258-262; tests/test_oracle.py pins the quirk), a
+    node the canonical builder never makes.  The resident commit refuses the batch with
+    MPTException and leaves the trie unchanged instead of returning a root that differs
+    from the JVM's; batches that do not hit the shape still match the oracle fold, including
+    the same key once its sibling is gone (its leaf then has a path again)."""
+    from khipu_amd.device import Ctx, ResidentTrie
+    from khipu_amd._lib import MPTException
+    r = random.Random(63)
+    k1 = bytearray(C._rk(r))
+    k2 = bytearray(k1)
+    k2[31] ^= 0x01  # 63 shared nibbles: k1 and k2 hang under a depth-63 branch
+    k1, k2 = bytes(k1), bytes(k2)
+    others = [C._rk(r) for _ in range(200)]
+    ks = others + [k1, k2]
+    vs = [C.account_value(r) for _ in ks]
+    o = oracle.Trie()
+    for k, v in zip(ks, vs):
+        o.put(k, v)
+    t = ResidentTrie(Ctx(0), ks, vs)
+    assert t.root == o.root_hash()
+    before = t.root
+    with pytest.raises(MPTException, match="value-only branch"):
+        t.commit([(others[0], C.account_value(r)), (k1, C.account_value(r))], [])
+    assert t.root_hash == before
+    # the trie is intact: a valid batch (removing the sibling) matches the oracle fold ...
+    ups = [(others[1], C.account_value(r))]
+    for k, v in ups:
+        o.put(k, v)
+    o.remove(k2)
+    assert t.commit(ups, [k2]) == o.root_hash()
+    # ... and k1 (now a leaf with a path under a shallower branch) updates normally
+    v1 = C.account_value(r)
+    o.put(k1, v1)
+    assert t.commit([(k1, v1)], []) == o.root_hash()
+    t.close()

@@ -143,7 +143,7 @@ def _run(case, world=2):
     return roots[0]
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 def test_sharded_root_matches_oracle(oracle, world):
     addrs, vals = _records(1, 600)
     root = _run((addrs, vals, False), world)

@@ -151,3 +151,28 @@ def test_identical_subtree_quirk(oracle):
     vals = [same, same, codec.account_rlp(3, 4), codec.account_rlp(5, 6)]
     with pytest.raises(oracle.OracleError):
         oracle.seq_root(keys, vals)
+
+
+def test_reference_value_branch_quirk(oracle):
+    """Pins what the oracle (and khipu) does on a re-put of a key whose leaf has an empty
+    remaining path: putInLeafNode with ml == 0 and an empty existingKey builds
+    BranchNode.withValueOnly and puts into it (MerklePatriciaTrie.scala:187-199,258-262),
+    so the root differs from the canonical trie of the same (key, value) set.  The GPU
+    resident commit refuses such a batch (tests/test_gpu_resident.py)."""
+    import random
+    r = random.Random(63)
+    k1 = bytearray(r.getrandbits(8) for _ in range(32))
+    k2 = bytearray(k1)
+    k2[31] ^= 0x01
+    k1, k2 = bytes(k1), bytes(k2)
+    t = oracle.Trie()
+    t.put(k1, b"\x01")
+    t.put(k2, b"\x02")
+    t.put(k1, b"\x03")
+    canonical = oracle.batch_root([k1, k2], [b"\x03", b"\x02"])
+    assert t.root_hash() != canonical
+    assert t.get(k1) == b"\x03"
+    fresh = oracle.Trie()
+    fresh.put(k2, b"\x02")
+    fresh.put(k1, b"\x03")
+    assert fresh.root_hash() == canonical
