@@ -8,9 +8,11 @@
 //
 // gfx950's VALU is 32-bit: the permutation is written on 32-bit halves so that
 // theta's 5-way XOR becomes v_xor3_b32 pairs, every 64-bit rotate two
-// v_alignbit_b32 (funnel shifts); gfx950's v_bitop3_b32 does theta's 3-way XOR and
-// chi's a ^ (~b & c) in one instruction each: 190 VALU ops per round against the
-// canonical 240 of SURVEY §8d (which assumes v_xor3 + v_bfi + v_xor).  Every state index is a
+// v_alignbit_b32 (funnel shifts); gfx950's v_bitop3_b32 does theta's 3-way XORs (the
+// column parities, and A ^ C[x-1] ^ rot(C[x+1], 1) in one step: D is never formed) and
+// chi's a ^ (~b & c) in one instruction each: 180 VALU ops per round (120 v_bitop3,
+// 58 v_alignbit, iota) against the canonical 240 of SURVEY §8d (which assumes v_xor3 +
+// v_bfi + v_xor).  Every state index is a
 // compile-time constant after unrolling, so the state never leaves registers.
 #pragma once
 #include <stdint.h>
@@ -92,25 +94,27 @@ struct KState {
 
 KH_HD void keccak_round(KState& S, uint64_t rc) {
   constexpr int ROT[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
-  uint32_t CL[5], CH[5], DL[5], DH[5], BL[25], BH[25];
+  uint32_t CL[5], CH[5], RL[5], RH[5], BL[25], BH[25];
 #pragma unroll
   for (int x = 0; x < 5; ++x) {  // theta: column parities
     CL[x] = xor3(xor3(S.lo[x], S.lo[x + 5], S.lo[x + 10]), S.lo[x + 15], S.lo[x + 20]);
     CH[x] = xor3(xor3(S.hi[x], S.hi[x + 5], S.hi[x + 10]), S.hi[x + 15], S.hi[x + 20]);
   }
 #pragma unroll
-  for (int x = 0; x < 5; ++x) {  // D[x] = C[x-1] ^ rot(C[x+1], 1)
-    uint32_t rl = CL[(x + 1) % 5], rh = CH[(x + 1) % 5];
+  for (int x = 0; x < 5; ++x) {  // rot(C[x], 1)
+    uint32_t rl = CL[x], rh = CH[x];
     rotl_hl(rl, rh, 1);
-    DL[x] = CL[(x + 4) % 5] ^ rl;
-    DH[x] = CH[(x + 4) % 5] ^ rh;
+    RL[x] = rl;
+    RH[x] = rh;
   }
 #pragma unroll
   for (int x = 0; x < 5; ++x)
 #pragma unroll
-    for (int y = 0; y < 5; ++y) {  // theta apply, rho, pi
+    for (int y = 0; y < 5; ++y) {  // theta apply (A ^= C[x-1] ^ rot(C[x+1], 1): one v_bitop3 per
+                                   // half, D is never formed), rho, pi
       const int i = x + 5 * y;
-      uint32_t l = S.lo[i] ^ DL[x], h = S.hi[i] ^ DH[x];
+      uint32_t l = xor3(S.lo[i], CL[(x + 4) % 5], RL[(x + 1) % 5]);
+      uint32_t h = xor3(S.hi[i], CH[(x + 4) % 5], RH[(x + 1) % 5]);
       rotl_hl(l, h, ROT[i]);
       const int d = y + 5 * ((2 * x + 3 * y) % 5);
       BL[d] = l;

@@ -583,9 +583,11 @@ __global__ void __launch_bounds__(BS) k_pd_scatter(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i < T.m) op_pd_scatter(T, i);
 }
-// 82 VGPRs, 5 waves per SIMD.  Measured at 100M (r2v): 14.6 ms; forcing 6 waves spills
-// 4 VGPRs and takes 15.7 ms; 4 waves gives 14.7 ms.
-__global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
+// Round-2 form (KHST_LEAF=v2, measurement switch): every load up front at addresses that
+// do not depend on the parent depth, the message moved into place by 64-bit byte funnels
+// and word-select networks.  82 VGPRs, 5 waves per SIMD; 5,472 VALU instructions per wave
+// (profiles/r2zs_pmc_instmix_100m.json).
+__global__ void __launch_bounds__(BS) k_leaf_in_v2(Topo T, uint64_t n) {
   const uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
   typedef const __attribute__((address_space(1))) u64x2 gpair;  // global (not flat) 16-byte loads
   const uint32_t vmis = (uint32_t)((uintptr_t)T.vals & 15);
@@ -606,6 +608,45 @@ __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
              ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
   __syncthreads();  // block_add3's LDS slots are reused
   block_add3(&T.ctr[CTR_LONGB], longb, nullptr, 0, nullptr, 0);
+}
+
+// max over the wave's 64 lanes (DPP row shifts + row broadcasts), returned to every lane
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true));  // row_shr:1
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true));  // row_shr:2
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true));  // row_shr:4
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true));  // row_shr:8
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+// per-wave counter add: the lanes' flags counted by ballot, one atomic per wave
+__device__ __forceinline__ void wave_count(unsigned long long* dst, bool f) {
+  const uint64_t b = __ballot(f);
+  if (b && __lane_id() == 0) atomicAdd(dst, (unsigned long long)__popcll(b));
+}
+// Early leaves (plain root builds; trie_ops.h op_leaf_in3): one thread per INPUT, on the
+// second stream beside the branch topology.  Keys and packed values are read in input
+// order; the parent depth gives the header geometry, the key and value are then loaded at
+// their message shifts, and the message is assembled dword by dword (v_perm_b32) straight
+// into the Keccak state.  Every lane of a wave runs the wave-bound reductions, so threads
+// past n take part with neutral values.
+__global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
+  const uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {
+    WaveBounds b;
+    b.emax = wave_max_u32(use ? e : 0u);
+    b.emin = 255u - wave_max_u32(use ? 255u - e : 0u);
+    b.Lmax = wave_max_u32(use ? lhi : 0u);
+    b.Lmin = 255u - wave_max_u32(use ? 255u - llo : 0u);
+    return b;
+  };
+  uint32_t inl = 0, lb = 0;
+  const uint32_t perms = op_leaf_in3(T, j, n, wave, &inl, &lb);
+  wave_count(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms != 0);
+  wave_count(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), perms != 0);
+  wave_count(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl != 0);
+  if (lb) atomicAdd(&T.ctr[CTR_LONGB], (unsigned long long)lb);
 }
 
 // after the branch topology (plain root builds): stashed leaf references into the
@@ -706,13 +747,6 @@ __device__ __forceinline__ uint32_t row16_scan(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
   return x;
-}
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    uint32_t w = (uint32_t)__shfl_xor((int)v, o);
-    v = w > v ? w : v;
-  }
-  return v;
 }
 
 // Wave-cooperative variant of k_branch_fused (row N1, measured against it: see
@@ -1654,7 +1688,11 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     }
     if (A.vals_ready) HIPCHK(hipStreamWaitEvent(s2, A.vals_ready, 0));  // the topology need not wait
     HIPCHK(hipEventRecord(c->ev[9], s2));
-    hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, s2, T, n);
+    static const bool leaf_v2 = getenv("KHST_LEAF") && !strcmp(getenv("KHST_LEAF"), "v2");  // measurement switch
+    if (leaf_v2)
+      hipLaunchKernelGGL(k_leaf_in_v2, GRID(n, BS), dim3(BS), 0, s2, T, n);
+    else
+      hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, s2, T, n);
     LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[10], s2));
   };

@@ -995,6 +995,207 @@ KH_HD uint32_t op_leaf_in(const Topo& T, uint64_t j, LD2 ld2, uint32_t vmis, uin
                                            // byte write less per leaf)
   return perms;
 }
+// ---- leaf message assembly on 32-bit dwords (k_leaf_in).  The message of a short
+// account leaf is prefix [0, o1) | key bytes [kb0, 32) at [o1, e) | value prefix [e, P) |
+// value [P, L) (leaf_header's bytes).  The key and the value are loaded at addresses
+// shifted by their message position (a second, dependent round trip: the loads then land
+// one byte funnel away from their message dwords), so every message dword is one v_perm_b32
+// of two loaded dwords, plus byte masks only where a boundary (e, P, L) can fall.  Which
+// dwords can hold a boundary is decided per WAVE: the wave's min/max of e and L (DPP
+// reductions on the device) make every other dword a single perm, chosen by a scalar
+// branch.  WAVE(use, e, Llo, Lhi) returns bounds containing every using lane's values; the
+// host replay (tests/emu) passes both the loosest bounds (every dword masked) and the
+// lane's own (every dword classified), so both forms are checked against the oracle.
+struct WaveBounds {
+  uint32_t emin, emax, Lmin, Lmax;
+};
+// v_perm_b32 with selectors 0..7 (bytes of {hi:lo})
+KH_HD uint32_t perm_b32(uint32_t hi, uint32_t lo, uint32_t sel) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_perm(hi, lo, sel);
+#else
+  const uint64_t d = ((uint64_t)hi << 32) | lo;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; ++i) r |= (uint32_t)((d >> (8 * ((sel >> (8 * i)) & 7))) & 0xFF) << (8 * i);
+  return r;
+#endif
+}
+// bytes below bit position y8 (= 8 x byte count, any int): 0 for y8 <= 0, ~0 for y8 >= 32
+KH_HD uint32_t below_mask(int32_t y8) {
+  const int32_t c = y8 < 0 ? 0 : y8 > 32 ? 32 : y8;
+  return (uint32_t)((0xFFFFFFFFull << c) >> 32);
+}
+#ifdef __HIP_DEVICE_COMPILE__
+#define KH_NOSPEC() asm volatile("")  // not speculated: the enclosing branch stays a branch
+#else
+#define KH_NOSPEC() ((void)0)
+#endif
+// 4 / 16 bytes from a 4-byte-aligned global address
+#ifdef __HIP_DEVICE_COMPILE__
+typedef uint32_t v4u_a4 __attribute__((ext_vector_type(4), aligned(4)));
+KH_HD uint32_t ld32_a4(uintptr_t a) { return *(const __attribute__((address_space(1))) uint32_t*)a; }
+KH_HD void ld128_a4(uintptr_t a, uint32_t* o) {  // global_load_dwordx4 (gfx950 allows 4-byte alignment)
+  const v4u_a4 x = *(const __attribute__((address_space(1))) v4u_a4*)a;
+  o[0] = x.x;
+  o[1] = x.y;
+  o[2] = x.z;
+  o[3] = x.w;
+}
+#else
+KH_HD uint32_t ld32_a4(uintptr_t a) {
+  uint32_t x;
+  memcpy(&x, (const void*)a, 4);
+  return x;
+}
+KH_HD void ld128_a4(uintptr_t a, uint32_t* o) { memcpy(o, (const void*)a, 16); }
+#endif
+constexpr uint32_t LEAF_VD = 36;  // value dwords loaded per lane (the message's 34 + funnel)
+constexpr uint32_t LEAF_KD = 12;  // key dwords (message dwords 0..9 + funnel)
+
+KH_HD uint32_t rlp_hdr_len32(uint32_t x) {  // rlp_hdr_len of a 32-bit length
+  return x < 56 ? 1u : x < 0x100u ? 2u : x < 0x10000u ? 3u : x < 0x1000000u ? 4u : 5u;
+}
+template <typename WAVE>
+KH_HD uint32_t op_leaf_in3(const Topo& T, uint64_t j, uint64_t n, WAVE wave, uint32_t* inl, uint32_t* longb) {
+  *inl = 0;
+  *longb = 0;
+  const bool active = j < n;
+  const uint64_t pv = active ? T.pdinv[j] : PDINV_SKIP;
+  const uint64_t off = active ? T.voff[j] : 0;
+  const uint32_t vlen = active ? (uint32_t)(T.voff[j + 1] - off) : 0;
+  const bool live = pv != PDINV_SKIP;  // not an earlier put of a key put again later
+  const int32_t pd = live ? (int32_t)(int8_t)(uint8_t)(pv >> 32) : 0;
+  const uint32_t si = (uint32_t)pv;  // sorted position: where the reference is stashed
+  // geometry (leaf_geom / leaf_header), 32-bit.  A 1-byte value < 0x80 is its own encoding
+  // (no prefix): that only shortens L by one and never changes the list-prefix length
+  // (the payload stays < 56), so everything up to P is known before the value is read.
+  const uint32_t s = (uint32_t)(pd + 1), p = 64 - s, h = p / 2 + 1, hpl = h == 1 ? 1 : 1 + h;
+  const uint32_t vhl = rlp_hdr_len32(vlen);
+  const uint32_t pay = hpl + vhl + vlen;
+  const uint32_t lhl = rlp_hdr_len32(pay);  // 1 or 2 for a short leaf; exact for the long ones
+  const uint32_t Lnr = lhl + pay;  // L unless the value is a raw single byte
+  const bool lng = Lnr > LEAF_SHORT_MAX;
+  const bool use = live && !lng;
+  const uint32_t o1 = lhl + (h > 1 ? 1 : 0) + 1, kb0 = (s + 1) >> 1, e = o1 + 32 - kb0, P = e + vhl;
+  const WaveBounds B = wave(use, e, vlen == 1 ? e + 1 : Lnr, Lnr);
+  if (live && lng) {  // encoded + hashed by op_leaf_long into its arena slot
+    T.lf_emeta[si] = EMETA_LONG;
+    *longb = (Lnr + 7) & ~7u;
+  }
+  if (!use) return 0;
+  // ---- second round trip: the value's first byte, the key and the value at their shifts
+  const uint32_t v0 = vlen == 1 ? (uint32_t)T.vals[off] : 0;
+  const bool raw = vlen == 1 && v0 < 0x80;
+  const uint32_t L = raw ? e + 1 : Lnr;
+  uint32_t KD[LEAF_KD], VD[LEAF_VD];
+  {  // message byte x <- key byte x + kd  (x in [o1, e))
+    const uintptr_t kb = (uintptr_t)(T.kin + 4 * j);
+    const int32_t kd = (int32_t)kb0 - (int32_t)o1;
+    const int32_t kd0 = kd >> 2;
+    if (j == 0 || j + 3 > n) {  // the shifted window would leave the key buffer: clamped dwords
+#pragma unroll
+      for (uint32_t i = 0; i < LEAF_KD; ++i) {
+        const int32_t q = kd0 + (int32_t)i;
+        KD[i] = ld32_a4(kb + 4 * (uint32_t)(q < 0 ? 0 : q > 7 ? 7 : q));
+      }
+    } else {
+#pragma unroll
+      for (uint32_t g = 0; g < LEAF_KD / 4; ++g) ld128_a4(kb + (intptr_t)4 * kd0 + 16 * g, KD + 4 * g);
+    }
+  }
+  const uintptr_t VB = (uintptr_t)(T.vals + off) - P;  // address of message byte 0 in value space
+  const uintptr_t VBa = VB & ~(uintptr_t)3;
+  {
+    const uintptr_t lo4 = (uintptr_t)T.vals & ~(uintptr_t)3;
+    const uintptr_t hi4 = ((uintptr_t)T.vals + T.voff[n] + 3) & ~(uintptr_t)3;
+    if (VBa < lo4 || VBa + 4 * LEAF_VD > hi4) {  // the window leaves the value buffer: dword by dword
+#pragma unroll
+      for (uint32_t i = 0; i < LEAF_VD; ++i) {
+        const uintptr_t a = VBa + 4 * i;
+        VD[i] = (a >= lo4 && a < hi4) ? ld32_a4(a) : 0;
+      }
+    } else {
+#pragma unroll
+      for (uint32_t g = 0; g < LEAF_VD / 4; ++g) ld128_a4(VBa + 16 * g, VD + 4 * g);
+    }
+  }
+  // ---- assembly
+  const uint32_t ksel = 0x03020100u + (uint32_t)(((int32_t)kb0 - (int32_t)o1) & 3) * 0x01010101u;
+  const uint32_t vsel = 0x03020100u + (uint32_t)(VB & 3) * 0x01010101u;
+  const int32_t E8 = 8 * (int32_t)e, P8 = 8 * (int32_t)P, L8 = 8 * (int32_t)L, O8 = 8 * (int32_t)o1;
+  const uint32_t vh = raw ? v0 : vlen < 56 ? 0x80 + vlen : (0xB8u | (vlen << 8));  // bytes [e, P) (raw: [e, L))
+  const uint64_t vhw = (uint64_t)vh << (8 * (e & 3));
+  const uint32_t me = e >> 2, mL = L >> 2, pb = 1u << (8 * (L & 3));
+  const uint32_t payl = L - lhl;
+  uint32_t pre = lhl == 1 ? 0xC0u + payl : (0xF8u | (payl << 8));  // bytes [0, o1)
+  if (h > 1) pre |= (0x80u + h) << (8 * lhl);
+  pre |= ((p & 1) ? 0x30u : 0x20u) << (8 * (o1 - 1));
+  const uint32_t k0keep = (p & 1) ? 0x0Fu << (8 * (o1 - 1)) : 0;  // the first path nibble rides in the HP byte
+  KState S;
+  uint32_t hd[8];
+#pragma unroll
+  for (int m = 0; m < 34; ++m) {
+    const uint32_t b0 = 4u * (uint32_t)m;
+    // (the conditions are wave-uniform: KH_NOSPEC keeps each masked form behind its scalar
+    // branch instead of letting the compiler compute every mask and select)
+    uint32_t x = 0;
+    if (m <= 9 && b0 < B.emax) {  // key bytes can be here
+      uint32_t k = perm_b32(KD[m + 1], KD[m], ksel);
+      if (m == 0) {
+        k &= (below_mask(E8) & ~below_mask(O8)) | k0keep;
+      } else if (b0 + 4 > B.emin) {
+        KH_NOSPEC();
+        k &= below_mask(E8 - 32 * m);
+      }
+      x = k;
+    }
+    if (b0 + 4 > B.emin + 1 && b0 < B.Lmax) {  // value bytes can be here (P >= e + 1, P <= e + 2)
+      uint32_t v = perm_b32(VD[m + 1], VD[m], vsel);
+      if (b0 < B.emax + 2) {
+        KH_NOSPEC();
+        v &= ~below_mask(P8 - 32 * m);
+      }
+      if (b0 + 4 > B.Lmin) {
+        KH_NOSPEC();
+        v &= below_mask(L8 - 32 * m);
+      }
+      x |= v;
+    }
+    if (b0 + 4 > B.emin && b0 <= B.emax + 1) {  // the value prefix can be here
+      KH_NOSPEC();
+      x |= (uint32_t)m == me ? (uint32_t)vhw : (uint32_t)m == me + 1 ? (uint32_t)(vhw >> 32) : 0u;
+    }
+    if (m == 0) x |= pre;
+    if (m < 8) hd[m] = x;
+    if (b0 + 4 > B.Lmin && b0 <= B.Lmax) {  // padding (KeccakCore.scala:537-546)
+      KH_NOSPEC();
+      x ^= (uint32_t)m == mL ? pb : 0u;
+    }
+    if (m == 33) x ^= 0x80u << 24;
+    if (m & 1)
+      S.hi[m >> 1] = x;
+    else
+      S.lo[m >> 1] = x;
+  }
+#pragma unroll
+  for (int q = 17; q < 25; ++q) S.lo[q] = S.hi[q] = 0;
+  const bool top = pd == (int32_t)T.depth0 - 1;
+  uint64_t* r = T.lf_eref + 4 * si;
+  uint32_t perms = 0;
+  if (L >= 32 || top) {  // a leaf embedded in its parent is never hashed (Node.scala:114)
+    keccakf(S);
+    for (int q = 0; q < 4; ++q) r[q] = lane(S, q);
+    perms = 1;
+  } else {  // bytes >= L are zero in hd (padding is applied after it was taken)
+    for (int q = 0; q < 4; ++q) r[q] = ((uint64_t)hd[2 * q + 1] << 32) | hd[2 * q];
+    *inl = 1;
+  }
+  // a top leaf is >= 35 B, so its stash is always the hash; the preset 32 stands for every
+  // hashed leaf (one scattered byte write less per leaf)
+  if (L < 32) T.lf_emeta[si] = (uint8_t)L;
+  return perms;
+}
+
 // value span of sorted leaf i (early builds gather no spans: through the input index)
 KH_HD void leaf_span_early(const Topo& T, uint64_t i, uint64_t* off, uint32_t* len) {
   if (T.svoff) {

@@ -22,8 +22,14 @@ def lib():
         L.emu_synth.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, vp, vp, vp]
         L.emu_fold16.argtypes = [vp, vp, vp, vp]
         L.emu_node_children.argtypes = [vp, ctypes.c_uint64, ctypes.c_int, vp, vp, vp]
+        L.emu_set_leaf_mode.argtypes = [ctypes.c_int]
         _lib = L
     return _lib
+
+
+def set_leaf_mode(mode):
+    """0 / 1: op_leaf_in3 with the loosest / the lane's own wave bounds; 2: op_leaf_in."""
+    lib().emu_set_leaf_mode(mode)
 
 
 def _buf(b):

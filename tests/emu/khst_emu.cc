@@ -19,6 +19,10 @@
 
 using namespace khst;
 
+// which form of the early leaf kernel the replay runs: 0 / 1 = op_leaf_in3 with the
+// loosest / the lane's own wave bounds, 2 = op_leaf_in (KHST_LEAF=v2)
+static int g_leaf_mode = 0;
+
 // keys: n*32 (already keccak'd), vals/voff packed; seg nullable.
 // Outputs per result r: hash (32 B), enc length, inline bytes (32 B).
 // stats_out[0..5] = m, B, node hashes, node perms, inline nodes, extensions.
@@ -175,7 +179,12 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   uint8_t* vbase = (uint8_t*)(((uintptr_t)vbuf.data() + 15) & ~(uintptr_t)15);
   memcpy(vbase + 24, vals, voff[n]);
   T.vals = vbase + 24;
-  {
+  // the keys likewise: the device kernel reads a shifted window of up to 3 keys past the
+  // current one (edge lanes take clamped loads)
+  std::vector<uint64_t> kbuf(4 * n + 16, 0);
+  if (n) memcpy(kbuf.data(), T.kin, 32 * n);
+  T.kin = kbuf.data();
+  if (g_leaf_mode == 2) {  // the round-2 kernel's form (KHST_LEAF=v2)
     const uint32_t vmis = (uint32_t)((uintptr_t)T.vals & 15);
     const uint8_t* vp = T.vals - vmis;
     auto ld2 = [vp](int64_t p, uint64_t& lo, uint64_t& hi) {
@@ -185,6 +194,21 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
     for (uint64_t j = 0; j < n; ++j) {
       uint32_t in1 = 0, lb = 0;
       uint32_t p = op_leaf_in(T, j, ld2, vmis, &in1, &lb);
+      perms += p;
+      hashes += p ? 1 : 0;
+      inl += in1;
+      longb += lb;
+    }
+  } else {
+    // op_leaf_in3 with the loosest wave bounds (mode 0: every dword takes its masked form)
+    // or the lane's own values (mode 1: every dword takes its classified form)
+    auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {
+      if (g_leaf_mode == 0 || !use) return WaveBounds{0, 255, 0, 255};
+      return WaveBounds{e, e, llo, lhi};
+    };
+    for (uint64_t j = 0; j < n + 3; ++j) {  // lanes past n take part as on the device
+      uint32_t in1 = 0, lb = 0;
+      uint32_t p = op_leaf_in3(T, j, n, wave, &in1, &lb);
       perms += p;
       hashes += p ? 1 : 0;
       inl += in1;
@@ -274,6 +298,8 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
 }
 
 extern "C" {
+
+void emu_set_leaf_mode(int mode) { g_leaf_mode = mode; }
 
 int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, uint64_t n, const uint32_t* seg,
               uint64_t nseg, uint32_t depth0, uint8_t* out_hash, uint32_t* out_len, uint8_t* out_inl,

@@ -16,8 +16,16 @@ def _root(r):
     return r[0] if r[1] else codec.EMPTY_TRIE_HASH
 
 
+@pytest.fixture(params=[0, 1, 2], ids=["leaf3_masked", "leaf3_classified", "leaf_v2"])
+def leaf_mode(request):
+    """The early leaf kernel's forms (tests/emu/khst_emu.cc g_leaf_mode)."""
+    E.set_leaf_mode(request.param)
+    yield request.param
+    E.set_leaf_mode(0)
+
+
 @pytest.mark.parametrize("case", C.all_cases(), ids=lambda c: c[0])
-def test_replay_root_vs_oracle(oracle, case):
+def test_replay_root_vs_oracle(oracle, case, leaf_mode):
     name, keys, vals = case
     res, st = E.build(keys, vals)
     assert _root(res[0]) == oracle.seq_root(keys, vals), name
@@ -58,7 +66,7 @@ def test_replay_top_nibble_fold(oracle, n):
     assert out.tobytes() == oracle.seq_root(keys, vals)
 
 
-def test_replay_genesis(oracle):
+def test_replay_genesis(oracle, leaf_mode):
     keys, vals = [], []
     with open(os.path.join(os.path.dirname(__file__), "golden", "genesis_alloc.txt")) as f:
         for line in f:
