@@ -310,6 +310,20 @@ int kh_block_commit_host(kh_trie* state, kh_trie* storage, const uint32_t* s_up_
 int kh_trie_emit_nodes(kh_trie* h, uint8_t* hashes32, uint64_t node_cap, uint8_t* rlp, uint64_t rlp_cap,
                        uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len);
 
+/* Batched get on a resident trie or forest: MerklePatriciaTrie.get (MerklePatriciaTrie.scala:
+ * 90-147; callers Blockchain.scala:336-342) answered from the records in HBM by the commit's
+ * anchor descent, so a JVM holding state in HBM can read it without its own node store.
+ * n queries: key i (klen bytes; kec256'd on the device when the trie was opened with
+ * KH_HASH_KEYS, as its commits are) in trie trie[i] (forests; NULL for a single trie).
+ * found[i] = 1 iff the key is present (None otherwise); the values are packed into vals with
+ * voff[n+1] (an absent key has an empty span).  When the values need more than val_cap
+ * bytes the call returns KH_ENOSPC and writes only *val_bytes (the size needed).
+ * Device-buffer form on the handle's context stream; _host form with host buffers. */
+int kh_trie_get(kh_trie* h, const uint32_t* d_trie, const uint8_t* d_keys, uint32_t klen, uint64_t n,
+                uint8_t* d_vals, uint64_t val_cap, uint64_t* d_voff, uint8_t* d_found, uint64_t* val_bytes);
+int kh_trie_get_host(kh_trie* h, const uint32_t* trie, const uint8_t* keys, uint32_t klen, uint64_t n,
+                     uint8_t* vals, uint64_t val_cap, uint64_t* voff, uint8_t* found, uint64_t* val_bytes);
+
 /* Leaves of a trie (of all tries of a forest). */
 int kh_trie_size(const kh_trie* h, uint64_t* n);
 int kh_trie_free(kh_trie* h);

@@ -114,6 +114,25 @@ KH_HD uint64_t map_slot_of(const AMap& M, const Recs& R, uint32_t r) {
   return ~0ULL;
 }
 
+// MerklePatriciaTrie.get (MerklePatriciaTrie.scala:90-147) on the records: the anchor
+// descent of a commit (a branch whose extension the key leaves, or an empty child
+// anchor, ends the search); the leaf record holding exactly `key`, or NONE
+KH_HD uint32_t forest_get(const AMap& M, const Recs& R, uint32_t t, const uint64_t* key) {
+  uint32_t d = 0;
+  for (int step = 0; step < 70; ++step) {
+    const uint32_t r = map_find(M, R, t, d, key);
+    if (r == NONE) return NONE;
+    const uint32_t db = R.rdb[r];
+    if (db == EL_LEAF) {
+      const uint64_t* L = R.rk + 4ull * r;
+      return (L[0] == key[0] && L[1] == key[1] && L[2] == key[2] && L[3] == key[3]) ? r : NONE;
+    }
+    if (lcp_nibbles(load_key(key, 0), load_key(R.rk, r)) < (int)db) return NONE;  // leaves the extension
+    d = db + 1;
+  }
+  return NONE;
+}
+
 // ---- the batch of ops, sorted by (trie, key), one op per key (the last one wins)
 enum : uint8_t { FOP_UPSERT = 1, FOP_DELETE = 2 };
 struct FOps {

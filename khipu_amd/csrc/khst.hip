@@ -649,6 +649,28 @@ __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
   if (lb) atomicAdd(&T.ctr[CTR_LONGB], (unsigned long long)lb);
 }
 
+// The same leaves in SORTED order (KHST_LEAF=sorted, measurement switch): the parent depth
+// comes from the two adjacent boundaries, so the kernel starts right after k_lcp with no
+// scatter (k_ansv_pd becomes k_ansv); keys and values are read through the sorted input
+// index (random 32-byte key and value-span reads) and the stash is written in order.
+__global__ void __launch_bounds__(BS) k_leaf_sorted(Topo T, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {
+    WaveBounds b;
+    b.emax = wave_max_u32(use ? e : 0u);
+    b.emin = 255u - wave_max_u32(use ? 255u - e : 0u);
+    b.Lmax = wave_max_u32(use ? lhi : 0u);
+    b.Lmin = 255u - wave_max_u32(use ? 255u - llo : 0u);
+    return b;
+  };
+  uint32_t inl = 0, lb = 0;
+  const uint32_t perms = op_leaf_sorted(T, i, n, wave, &inl, &lb);
+  wave_count(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms != 0);
+  wave_count(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), perms != 0);
+  wave_count(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl != 0);
+  if (lb) atomicAdd(&T.ctr[CTR_LONGB], (unsigned long long)lb);
+}
+
 // after the branch topology (plain root builds): stashed leaf references into the
 // parents' child records, arena slots for long leaves
 __global__ void __launch_bounds__(BS) k_leaf_topo_early(Topo T) {
@@ -1657,11 +1679,15 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     return dim3((unsigned)(early && topo_cap && g > topo_cap ? topo_cap : (g ? g : 1)));
   };
   static const int pd_env = [] {
+    const char* l = getenv("KHST_LEAF");  // measurement switch: leaves hashed in sorted order
+    if (l && strcmp(l, "sorted") == 0) return 2;
     const char* e = getenv("KHST_PD");  // measurement switch
     return !e ? PD_DEFAULT : strcmp(e, "ansv") == 0 ? 1 : 0;
   }();
   const int pd_mode = (early && nb > 0) ? pd_env : 0;
-  if (pd_mode) {  // presets for the scatter folded into k_ansv (on st)
+  if (pd_mode == 2) {  // sorted leaves: no scatter, the stash is written in sorted order
+    HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));
+  } else if (pd_mode) {  // presets for the scatter folded into k_ansv (on st)
     if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, st));  // dropped duplicates: PDINV_SKIP
     HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));                  // every leaf a hash unless it says otherwise
   }
@@ -1713,6 +1739,15 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       pp += (nout + 255) & ~(uint64_t)255;
     }
     HIPCHK(hipMemsetAsync(T.glast, 1, nb, st));
+    if (pd_mode == 2) {  // the leaves need only u: they start here, beside the whole topology
+      HIPCHK(hipEventRecord(c->ev[8], st));
+      HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
+      if (A.vals_ready) HIPCHK(hipStreamWaitEvent(c->st2, A.vals_ready, 0));
+      HIPCHK(hipEventRecord(c->ev[9], c->st2));
+      hipLaunchKernelGGL(k_leaf_sorted, GRID(m, BS), dim3(BS), 0, c->st2, T, n);
+      LAUNCH_CHECK();
+      HIPCHK(hipEventRecord(c->ev[10], c->st2));
+    }
     if (pd_mode == 1)
       hipLaunchKernelGGL(k_ansv_pd, GRID(m, BS), dim3(BS), 0, st, T, P, nb);
     else
@@ -2344,6 +2379,7 @@ struct kh_trie {
   uint8_t root[32] = {};
   DevBuf ws, elout, eloutb, em;  // commit scratch, element-build outputs, last write-back set
   DevBuf tlb, ebuf, tbuf, ubuf, selb, merr;  // touched list, elements, trie ids + roots, upsert offsets, selections
+  DevBuf gbuf;                                // batched get: keys, records, lengths, scan scratch
   uint64_t em_n = 0, em_bytes = 0;
   bool em_valid = false;
   std::vector<uint32_t> tries;  // last commit: touched tries and their roots
@@ -3883,6 +3919,128 @@ int kh_trie_emit_nodes(kh_trie* h, uint8_t* hashes32, uint64_t node_cap, uint8_t
       return KH_OK;
     }
     return emit_to_host(h->c, h->em, h->em_n, h->em_bytes, hashes32, node_cap, rlp, rlp_cap, off, n_nodes, rlp_len);
+  })
+}
+
+// ---- batched get (MerklePatriciaTrie.get, MerklePatriciaTrie.scala:90-147)
+__global__ void __launch_bounds__(BS) k_get_find(AMap M, Recs R, const uint64_t* K, const uint32_t* trie, uint64_t n,
+                                                 uint32_t* rec, uint64_t* len) {
+  const uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o >= n) return;
+  const uint32_t r = forest_get(M, R, trie ? trie[o] : 0u, K + 4 * o);
+  rec[o] = r;
+  len[o] = r == NONE ? 0 : R.rvl[r];
+}
+// value bytes into the packed output (one thread per query; values are short)
+__global__ void __launch_bounds__(BS) k_get_copy(Recs R, const uint8_t* heap, const uint32_t* rec, const uint64_t* voff,
+                                                 uint64_t n, uint8_t* out, uint8_t* found) {
+  const uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o >= n) return;
+  const uint32_t r = rec[o];
+  found[o] = r != NONE;
+  if (r == NONE) return;
+  const uint8_t* src = heap + R.rvo[r];
+  uint8_t* dst = out + voff[o];
+  for (uint32_t b = 0, L = R.rvl[r]; b < L; ++b) dst[b] = src[b];
+}
+
+// n queries (device buffers): the keys (the trie's key encoder applied, as in a commit),
+// their trie ids (forests; NULL = trie 0), then the found flags, the packed values and
+// their offsets.  Returns KH_ENOSPC (writing only *val_bytes) when val_cap is too small.
+static int trie_get(kh_trie* h, const uint32_t* d_trie, const uint8_t* d_keys, uint32_t klen, uint64_t n,
+                    uint8_t* d_vals, uint64_t val_cap, uint64_t* d_voff, uint8_t* d_found, uint64_t* val_bytes) {
+  kh_ctx* c = h->c;
+  hipStream_t st = c->st;
+  if (h->forest && n && !d_trie) throw KhError{KH_EINVAL, "forest queries need trie ids"};
+  if (!(h->flags & KH_HASH_KEYS) && klen != 32) throw KhError{KH_EINVAL, "keys must be 32 bytes unless KH_HASH_KEYS"};
+  if (klen == 0 || klen > 4096) throw KhError{KH_EINVAL, "bad key length"};
+  if (n >= (1ULL << 31)) throw KhError{KH_EINVAL, "too many queries"};
+  h->gbuf.ensure(carve_size({n * 32 + 64, n * 4, (n + 1) * 8, scan_scratch_bytes(n + 1, 8), 64}));
+  Carver cv{(char*)h->gbuf.p, 0, h->gbuf.cap};
+  uint64_t* K = cv.take<uint64_t>(n * 4 + 8);
+  uint32_t* rec = cv.take<uint32_t>(n);
+  uint64_t* len = cv.take<uint64_t>(n + 1);
+  char* scr = cv.take<char>(scan_scratch_bytes(n + 1, 8));
+  uint64_t* tot = cv.take<uint64_t>(8);
+  if (n) {
+    if (h->flags & KH_HASH_KEYS) {
+      if (klen <= 135)
+        hipLaunchKernelGGL(k_hash_keys<true>, GRID(n, BS), dim3(BS), 0, st, d_keys, klen, n, K);
+      else
+        hipLaunchKernelGGL(k_hash_keys<false>, GRID(n, BS), dim3(BS), 0, st, d_keys, klen, n, K);
+      LAUNCH_CHECK();
+    } else {
+      HIPCHK(hipMemcpyAsync(K, d_keys, n * 32, hipMemcpyDeviceToDevice, st));
+    }
+    if (h->rn && h->mcap) {
+      hipLaunchKernelGGL(k_get_find, GRID(n, BS), dim3(BS), 0, st, map_of(h), recs_of(h), (const uint64_t*)K, d_trie,
+                         n, rec, len);
+      LAUNCH_CHECK();
+    } else {  // an empty trie or forest
+      HIPCHK(hipMemsetAsync(rec, 0xFF, n * 4, st));
+      HIPCHK(hipMemsetAsync(len, 0, n * 8, st));
+    }
+    scan_exclusive<uint64_t>(len, d_voff, n, tot, scr, st);
+    HIPCHK(hipMemcpyAsync(d_voff + n, tot, 8, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned, tot, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  } else {
+    HIPCHK(hipMemsetAsync(d_voff, 0, 8, st));
+    HIPCHK(hipStreamSynchronize(st));
+    c->h_pinned[0] = 0;
+  }
+  const uint64_t total = c->h_pinned[0];
+  if (val_bytes) *val_bytes = total;
+  if (total > val_cap) return set_err(KH_ENOSPC, "value output too small (*val_bytes holds the size needed)");
+  if (n) {
+    hipLaunchKernelGGL(k_get_copy, GRID(n, BS), dim3(BS), 0, st, recs_of(h), (const uint8_t*)h->heap.p,
+                       (const uint32_t*)rec, (const uint64_t*)d_voff, n, d_vals, d_found);
+    LAUNCH_CHECK();
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  return KH_OK;
+}
+
+int kh_trie_get(kh_trie* h, const uint32_t* d_trie, const uint8_t* d_keys, uint32_t klen, uint64_t n, uint8_t* d_vals,
+                uint64_t val_cap, uint64_t* d_voff, uint8_t* d_found, uint64_t* val_bytes) {
+  if (!h) return set_err(KH_EINVAL, "null handle");
+  if (!d_voff || (n && (!d_keys || !d_found))) return set_err(KH_EINVAL, "null buffer");
+  API_TRY({
+    HIPCHK(hipSetDevice(h->c->dev));
+    return trie_get(h, d_trie, d_keys, klen, n, d_vals, val_cap, d_voff, d_found, val_bytes);
+  })
+}
+
+int kh_trie_get_host(kh_trie* h, const uint32_t* trie, const uint8_t* keys, uint32_t klen, uint64_t n, uint8_t* vals,
+                     uint64_t val_cap, uint64_t* voff, uint8_t* found, uint64_t* val_bytes) {
+  if (!h) return set_err(KH_EINVAL, "null handle");
+  if (!voff || (n && (!keys || !found))) return set_err(KH_EINVAL, "null buffer");
+  API_TRY({
+    std::lock_guard<std::mutex> g(h->c->mu);
+    kh_ctx* c = h->c;
+    HIPCHK(hipSetDevice(c->dev));
+    hipStream_t st = c->st;
+    // staging: keys and trie ids in, found flags, offsets and values out
+    c->in_keys.ensure(carve_size({n * klen + 64, trie ? n * 4 : 0}));
+    Carver ck{(char*)c->in_keys.p, 0, c->in_keys.cap};
+    uint8_t* dk = ck.take<uint8_t>(n * klen + 64);
+    uint32_t* dt = trie ? ck.take<uint32_t>(n) : nullptr;
+    c->in_voff.ensure((n + 1) * 8 + 64);
+    c->out_emit.ensure(carve_size({n + 64, val_cap + 64}));
+    Carver co{(char*)c->out_emit.p, 0, c->out_emit.cap};
+    uint8_t* df = co.take<uint8_t>(n + 64);
+    uint8_t* dv = co.take<uint8_t>(val_cap + 64);
+    if (n) HIPCHK(hipMemcpyAsync(dk, keys, n * klen, hipMemcpyHostToDevice, st));
+    if (dt) HIPCHK(hipMemcpyAsync(dt, trie, n * 4, hipMemcpyHostToDevice, st));
+    const int rc = trie_get(h, dt, dk, klen, n, dv, val_cap, (uint64_t*)c->in_voff.p, df, val_bytes);
+    if (rc != KH_OK) return rc;
+    HIPCHK(hipMemcpyAsync(voff, c->in_voff.p, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (n) HIPCHK(hipMemcpyAsync(found, df, n, hipMemcpyDeviceToHost, st));
+    const uint64_t tot = val_bytes ? *val_bytes : 0;
+    HIPCHK(hipStreamSynchronize(st));
+    const uint64_t total = n ? voff[n] : tot;
+    if (total) HIPCHK(hipMemcpyAsync(vals, dv, total, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
   })
 }
 

@@ -1055,17 +1055,16 @@ constexpr uint32_t LEAF_KD = 12;  // key dwords (message dwords 0..9 + funnel)
 KH_HD uint32_t rlp_hdr_len32(uint32_t x) {  // rlp_hdr_len of a 32-bit length
   return x < 56 ? 1u : x < 0x100u ? 2u : x < 0x10000u ? 3u : x < 0x1000000u ? 4u : 5u;
 }
+// One leaf: input j (key kin[j], value voff[j]..voff[j+1]) with parent depth pd, stashed at
+// sorted position si.  live = false: a lane that only takes part in the wave reductions.
 template <typename WAVE>
-KH_HD uint32_t op_leaf_in3(const Topo& T, uint64_t j, uint64_t n, WAVE wave, uint32_t* inl, uint32_t* longb) {
+KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, uint64_t j, uint64_t n, WAVE wave,
+                            uint32_t* inl, uint32_t* longb) {
   *inl = 0;
   *longb = 0;
-  const bool active = j < n;
-  const uint64_t pv = active ? T.pdinv[j] : PDINV_SKIP;
-  const uint64_t off = active ? T.voff[j] : 0;
-  const uint32_t vlen = active ? (uint32_t)(T.voff[j + 1] - off) : 0;
-  const bool live = pv != PDINV_SKIP;  // not an earlier put of a key put again later
-  const int32_t pd = live ? (int32_t)(int8_t)(uint8_t)(pv >> 32) : 0;
-  const uint32_t si = (uint32_t)pv;  // sorted position: where the reference is stashed
+  const uint64_t off = live ? T.voff[j] : 0;
+  const uint32_t vlen = live ? (uint32_t)(T.voff[j + 1] - off) : 0;
+  if (!live) pd = 0;
   // geometry (leaf_geom / leaf_header), 32-bit.  A 1-byte value < 0x80 is its own encoding
   // (no prefix): that only shortens L by one and never changes the list-prefix length
   // (the payload stays < 56), so everything up to P is known before the value is read.
@@ -1194,6 +1193,21 @@ KH_HD uint32_t op_leaf_in3(const Topo& T, uint64_t j, uint64_t n, WAVE wave, uin
   // hashed leaf (one scattered byte write less per leaf)
   if (L < 32) T.lf_emeta[si] = (uint8_t)L;
   return perms;
+}
+// input order (k_leaf_in): the parent depth and sorted position scattered by k_ansv_pd
+template <typename WAVE>
+KH_HD uint32_t op_leaf_in3(const Topo& T, uint64_t j, uint64_t n, WAVE wave, uint32_t* inl, uint32_t* longb) {
+  const uint64_t pv = j < n ? T.pdinv[j] : PDINV_SKIP;
+  const bool live = pv != PDINV_SKIP;  // not an earlier put of a key put again later
+  return op_leaf_core(T, live, (int32_t)(int8_t)(uint8_t)(pv >> 32), (uint32_t)pv, j, n, wave, inl, longb);
+}
+// sorted order (k_leaf_sorted, KHST_LEAF=sorted): the parent depth straight from the two
+// adjacent boundaries, the key and value through the sorted input index (random reads)
+template <typename WAVE>
+KH_HD uint32_t op_leaf_sorted(const Topo& T, uint64_t i, uint64_t n, WAVE wave, uint32_t* inl, uint32_t* longb) {
+  const bool live = i < T.m;
+  const uint64_t j = live ? (T.sidx ? T.sidx[i] : i) : 0;
+  return op_leaf_core(T, live, live ? leaf_pd_early(T, i) : 0, (uint32_t)i, j, n, wave, inl, longb);
 }
 
 // value span of sorted leaf i (early builds gather no spans: through the input index)

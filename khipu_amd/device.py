@@ -208,6 +208,10 @@ class ResidentTrie:
         created, every one reachable from the new root with an encoding >= 32 B, plus a changed root."""
         return emitted_nodes(lambda *a: lib().kh_trie_emit_nodes(self.h, *a))
 
+    def get(self, keys):
+        """Batched get (kh_trie_get): [value or None] per key (raw keys with hash_keys)."""
+        return trie_get(self.h, keys)
+
     @property
     def root_hash(self):
         return self.root
@@ -227,6 +231,30 @@ class ResidentTrie:
             self.close()
         except Exception:
             pass
+
+
+def trie_get(h, keys, trie_ids=None):
+    """Batched get through kh_trie_get_host: [value bytes or None] per key
+    (MerklePatriciaTrie.get, MerklePatriciaTrie.scala:90-147)."""
+    keys = list(keys)
+    n = len(keys)
+    klen = len(keys[0]) if keys else 32
+    kb = np.frombuffer(b"".join(keys) + b"\0", np.uint8).copy()
+    tb = np.asarray(trie_ids, np.uint32) if trie_ids is not None else None
+    found = np.zeros(max(n, 1), np.uint8)
+    voff = np.zeros(n + 1, np.uint64)
+    need = ctypes.c_uint64(0)
+    cap = 0
+    for _ in range(2):
+        vals = np.zeros(max(cap, 1), np.uint8)
+        rc = lib().kh_trie_get_host(h, tb.ctypes.data if tb is not None else None, kb.ctypes.data, klen, n,
+                                    vals.ctypes.data, cap, voff.ctypes.data, found.ctypes.data, ctypes.byref(need))
+        if rc == _lib.KH_ENOSPC:
+            cap = need.value
+            continue
+        check(rc)
+        return [vals[voff[i]:voff[i + 1]].tobytes() if found[i] else None for i in range(n)]
+    raise RuntimeError("kh_trie_get: size negotiation failed")
 
 
 def emitted_nodes(call):
@@ -282,6 +310,11 @@ class ResidentForest:
 
     def nodes(self):
         return emitted_nodes(lambda *a: lib().kh_trie_emit_nodes(self.h, *a))
+
+    def get(self, queries):
+        """queries: [(trie_id, key)] -> [value or None] (kh_trie_get)."""
+        q = list(queries)
+        return trie_get(self.h, [k for _, k in q], [t for t, _ in q])
 
     def last_roots(self):
         """{trie_id: root} of the last commit (kh_forest_last_roots; also after block_commit)."""

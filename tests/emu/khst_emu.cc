@@ -20,7 +20,8 @@
 using namespace khst;
 
 // which form of the early leaf kernel the replay runs: 0 / 1 = op_leaf_in3 with the
-// loosest / the lane's own wave bounds, 2 = op_leaf_in (KHST_LEAF=v2)
+// loosest / the lane's own wave bounds, 2 = op_leaf_in (KHST_LEAF=v2), 3 = op_leaf_sorted
+// (KHST_LEAF=sorted) with the loosest bounds
 static int g_leaf_mode = 0;
 
 // keys: n*32 (already keccak'd), vals/voff packed; seg nullable.
@@ -206,9 +207,11 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       if (g_leaf_mode == 0 || !use) return WaveBounds{0, 255, 0, 255};
       return WaveBounds{e, e, llo, lhi};
     };
-    for (uint64_t j = 0; j < n + 3; ++j) {  // lanes past n take part as on the device
+    const bool sorted_order = g_leaf_mode == 3;  // KHST_LEAF=sorted (k_leaf_sorted)
+    if (sorted_order) std::fill(emeta.begin(), emeta.end(), (uint8_t)32);
+    for (uint64_t j = 0; j < (sorted_order ? m : n) + 3; ++j) {  // lanes past the end take part as on the device
       uint32_t in1 = 0, lb = 0;
-      uint32_t p = op_leaf_in3(T, j, n, wave, &in1, &lb);
+      uint32_t p = sorted_order ? op_leaf_sorted(T, j, n, wave, &in1, &lb) : op_leaf_in3(T, j, n, wave, &in1, &lb);
       perms += p;
       hashes += p ? 1 : 0;
       inl += in1;

@@ -16,7 +16,7 @@ def _root(r):
     return r[0] if r[1] else codec.EMPTY_TRIE_HASH
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["leaf3_masked", "leaf3_classified", "leaf_v2"])
+@pytest.fixture(params=[0, 1, 2, 3], ids=["leaf3_masked", "leaf3_classified", "leaf_v2", "leaf_sorted"])
 def leaf_mode(request):
     """The early leaf kernel's forms (tests/emu/khst_emu.cc g_leaf_mode)."""
     E.set_leaf_mode(request.param)

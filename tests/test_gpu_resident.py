@@ -376,3 +376,65 @@ def test_update_of_empty_path_leaf_is_refused(khst, oracle):
     o.put(k1, v1)
     assert t.commit([(k1, v1)], []) == o.root_hash()
     t.close()
+
+
+@pytest.mark.parametrize("sc", C.commit_scenarios()[:4] + C.commit_scenarios()[5:6], ids=lambda s: s[0])
+def test_batched_get_vs_oracle(khst, oracle, sc):
+    """kh_trie_get (MerklePatriciaTrie.get, MerklePatriciaTrie.scala:90-147) after open and
+    after every commit: every key ever put (present, updated, or removed by the last commit),
+    absent keys sharing long prefixes with present ones (they end inside an extension or at
+    an empty branch slot), and inline leaves of the storage / deep tries."""
+    from khipu_amd.device import Ctx, ResidentTrie
+    name, ks, vs, batches = sc
+    r = random.Random(17)
+    o = oracle.Trie()
+    for k, v in zip(ks, vs):
+        o.put(k, v)
+    t = ResidentTrie(Ctx(0), ks, vs)
+    seen = list(ks)
+
+    def probes():
+        near = []
+        for k in r.sample(seen, min(20, len(seen))):
+            b = bytearray(k)
+            b[r.randrange(32)] ^= 1 << r.randrange(8)
+            near.append(bytes(b))
+            b = bytearray(k)
+            b[31] ^= 0x01  # shares 63 nibbles
+            near.append(bytes(b))
+        return list(dict.fromkeys(seen + near + [C._rk(r) for _ in range(10)]))
+
+    q = probes()
+    assert t.get(q) == [o.get(k) for k in q], name
+    for ups, dels in batches:
+        for k, v in ups:
+            o.put(k, v)
+        for k in dels:
+            o.remove(k)
+        t.commit(ups, dels)
+        seen += [k for k, _ in ups]
+        q = probes()
+        assert t.get(q) == [o.get(k) for k in q], name
+    assert t.get([]) == []
+    t.close()
+
+
+def test_batched_get_hash_keys_and_forest(khst, oracle):
+    """Raw keys on a KH_HASH_KEYS trie (hashed on the device, as its commits are), and a
+    forest answering (trie id, key) queries, including ids of tries it does not hold."""
+    from khipu_amd.device import Ctx, ResidentForest, ResidentTrie
+    r = random.Random(23)
+    ctx = Ctx(0)
+    addrs = [bytes(r.getrandbits(8) for _ in range(20)) for _ in range(300)]
+    vals = [C.account_value(r) for _ in addrs]
+    t = ResidentTrie(ctx, addrs, vals, hash_keys=True)
+    t.commit([(addrs[0], b"\x01" * 70)], addrs[1:3], hash_keys=True)
+    want = [b"\x01" * 70, None, None] + vals[3:] + [None]
+    assert t.get(addrs + [bytes(20)]) == want
+    t.close()
+    f = ResidentForest(ctx)
+    tries = {tid: {C._rk(r): C.storage_value(r) for _ in range(r.randrange(1, 60))} for tid in (3, 7, 1000)}
+    f.commit([(tid, k, v) for tid, kv in tries.items() for k, v in kv.items()])
+    q = [(tid, k) for tid, kv in tries.items() for k in kv] + [(5, next(iter(tries[3])))] + [(7, C._rk(r))]
+    assert f.get(q) == [tries[tid].get(k) for tid, k in q]
+    f.close()
