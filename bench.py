@@ -63,8 +63,10 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-cpu-batch", action="store_true", help="skip the all-core full-size CPU root")
     p.add_argument("--sharded", action="store_true", help="force the nibble-sharded RCCL path (any N)")
-    p.add_argument("--workload", choices=("state", "lists"), default="state",
-                   help="state: the BASELINE metric (default); lists: transactions roots (SURVEY §8 f4)")
+    p.add_argument("--workload", choices=("state", "lists", "storage"), default="state",
+                   help="state: the BASELINE metric (default); lists: transactions roots (SURVEY §8 f4); "
+                        "storage: configs[3], 100k storage tries (trie-id shards over --gpus N)")
+    p.add_argument("--tries", type=int, default=100_000, help="storage: storage tries per step")
     p.add_argument("--blocks", type=int, default=10_000, help="lists: blocks per step")
     return p.parse_args()
 
@@ -323,6 +325,146 @@ def lists(args):
     print(json.dumps(out), flush=True)
 
 
+def storage_ranges(seg_off, world):
+    """Contiguous trie ranges [b[g], b[g+1]) of about equal slot counts (seg_off: the tries'
+    slot offsets, nt + 1 entries from 0), one per rank; every trie in exactly one range."""
+    nt = len(seg_off) - 1
+    tot = int(seg_off[-1])
+    b = [0] + [int(np.searchsorted(seg_off, tot * g // world, side="left")) for g in range(1, world)] + [nt]
+    for g in range(1, world + 1):
+        b[g] = min(max(b[g], b[g - 1]), nt)
+    return b
+
+
+def storage(args):
+    """configs[3]: the roots of 100k synthetic contract storage tries (csrc/synth.h: log-uniform
+    1..10^4 slots, kec256 slot keys hashed on the GPU, RLP(trimmed 1-32 B) values) as one
+    segmented build per GPU.  N > 1 (torch.distributed, one rank per GPU): the tries are split
+    into contiguous ranges of equal slot counts, each rank generates and builds its own range,
+    and the roots are gathered (SURVEY §8e "Other configs": no exchange, the tries are
+    independent; TrieStorage.scala:52-60 via BlockWorldState.scala:243-252).  Total work is
+    fixed as N grows ("strong").  Rank 0 checks the gathered roots against a single-GPU build
+    of all tries and, at N = 1, against the CPU batch builder."""
+    import torch
+    import torch.distributed as dist
+    from khipu_amd.device import Ctx
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    ctx = Ctx(local)
+    cfg, NT = 4, args.tries
+    so_all, n_all, _ = ctx.storage_slot_counts(cfg, 0, NT)
+    so_h = so_all.cpu().numpy()
+    bnd = storage_ranges(so_h, world)
+    t0, t1 = bnd[rank], bnd[rank + 1]
+    nt = t1 - t0
+    so, keys, vals, voff, seg = ctx.synth_storage(cfg, t0, nt)
+    n = int(so[-1].item()) if nt else 0
+    torch.cuda.synchronize()
+
+    def step():
+        return ctx.build(keys, 32, vals, voff, n, seg=seg, nseg=max(nt, 1), hash_keys=True) if n else None
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_0 = time.perf_counter()
+    dev_ms = []
+    for _ in range(args.steps):
+        out = step()
+        if out:
+            dev_ms.append(out[3].t_total_ms)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t_0) / args.steps
+    hh = out[0][:nt] if out else np.zeros((0, 32), np.uint8)
+    st = out[3].as_dict() if out else None
+    mine = np.zeros((max(bnd[g + 1] - bnd[g] for g in range(world)), 32), np.uint8)
+    mine[:nt] = hh
+    hashes = st["n_node_hashes"] if st else 0
+    if world > 1:
+        dtt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(dtt, op=dist.ReduceOp.MAX)
+        dt = float(dtt.item())
+        ht = torch.tensor([hashes], dtype=torch.int64, device=f"cuda:{local}")
+        dist.all_reduce(ht)
+        hashes = int(ht.item())
+        allr = [torch.zeros_like(torch.from_numpy(mine)).to(f"cuda:{local}") for _ in range(world)]
+        dist.all_gather(allr, torch.from_numpy(mine).to(f"cuda:{local}"))
+        roots = np.concatenate([allr[g].cpu().numpy()[:bnd[g + 1] - bnd[g]] for g in range(world)])
+    else:
+        roots = hh
+    ok = torch.ones(1, dtype=torch.int64, device=f"cuda:{local}")
+    res = None
+    if rank == 0:
+        # self-check: every root against one single-GPU segmented build of ALL the tries
+        if world > 1:
+            del keys, vals, voff, seg
+            torch.cuda.empty_cache()
+        so1, k1, v1, o1, s1 = ctx.synth_storage(cfg, 0, NT)
+        h1, _, _, st1 = ctx.build(k1, 32, v1, o1, n_all, seg=s1, nseg=NT, hash_keys=True)
+        single_ok = bool((h1[:NT] == roots).all())
+        ok[0] = int(single_ok)
+        s = st1.as_dict()
+        leaf_ms = s["t_leaf_ms"]
+        achieved = s["n_leaves"] * OPS_PER_PERM / max(leaf_ms * 1e-3, 1e-12)
+        res = {
+            "metric": "node-hashes/sec (configs[3]: 100k storage tries, one root each)",
+            "value": hashes / dt, "unit": "node-hashes/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (counter-based storage tries, csrc/synth.h synth_storage_*)",
+            "config": {"workload": f"{NT} storage tries, {n_all} slots (log-uniform 1..1e4 per trie) -> one root each",
+                       "tries": NT, "slots": n_all,
+                       "parallelism": f"trie-id shards x{world} (slot-balanced ranges, roots gathered)"},
+            "trie_ranges": [[bnd[g], bnd[g + 1]] for g in range(world)],
+            "rank0_device_ms_per_step": [round(x, 3) for x in dev_ms],
+            "parity": {"roots_vs_single_gpu_build": "equal" if single_ok else "DIFFER"},
+            "stage_ms_single_gpu_build": {k: round(s[k], 3) for k in ("t_keys_ms", "t_sort_ms", "t_topo_ms",
+                                                                        "t_leaf_ms", "t_branch_ms", "t_total_ms")},
+            "roofline": {"kernel": "k_leaf_in (single-GPU build of all tries)", "bound": "valu",
+                         "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
+                         "unit": "T int32-lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS, "traffic": None,
+                         "avg_ms": leaf_ms, "perms_per_launch": s["n_leaves"]},
+        }
+        if world == 1 and not args.no_cpu and single_ok:
+            from oracle import oracle
+            thr = cpu_threads(args.cpu_threads)
+            vo = o1.cpu().numpy().astype(np.uint64)
+            tc = time.perf_counter()
+            cr, cst = oracle.batch_roots(k1[:32 * n_all].cpu().numpy(), (v1[:int(vo[-1])].cpu().numpy(), vo), klen=32,
+                                         seg_off=so1.cpu().numpy().astype(np.uint64), hash_keys=True, nthreads=thr)
+            tcpu = time.perf_counter() - tc
+            cpu_ok = cr == [bytes(x) for x in h1[:NT]]
+            ok[0] = int(cpu_ok)
+            res["parity"]["roots_vs_cpu_batch"] = "equal" if cpu_ok else "DIFFER"
+            res["cpu_baseline"] = {"value": cst["node_hashes"] / tcpu, "unit": "node-hashes/s", "cores": thr,
+                                   "kind": "port", "seconds": round(tcpu, 3),
+                                   "sample": f"all {NT} tries, independent batch builder (oracle/batch_root.cc) on "
+                                             f"{thr} threads, key hashing included; CPU: {cpu_model()}"}
+    if world > 1:
+        dist.broadcast(ok, 0)
+    if not int(ok.item()):
+        if rank == 0:
+            print(f"storage roots FAILED their self-check: {res and res['parity']}", file=sys.stderr, flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(1)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def oracle_list_key(i):
     """rlp.encode(i: Int) (RLP.scala integer encoding): 0 -> 0x80, 1..127 the byte, else 0x80+len, BE bytes."""
     if i == 0:
@@ -365,6 +507,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.workload == "lists":
         lists(args)
+    elif args.workload == "storage":
+        storage(args)
     elif world > 1 or args.gpus > 1 or args.sharded:
         from khipu_amd import sharded
         sharded.bench_main(args)

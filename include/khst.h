@@ -114,6 +114,14 @@ int kh_trie_roots_varkeys(const uint8_t* keys, const uint64_t* koff, const uint8
 int kh_list_roots(const uint8_t* items, const uint64_t* off, const uint64_t* seg_off, uint64_t nseg,
                   uint8_t* roots32, kh_stats* stats);
 
+/* kh_trie_roots_segmented over ngpus GPUs of this process (SURVEY §8e, configs[3]): the
+ * tries are split into contiguous ranges of about equal slot counts, one per device (a
+ * device may repeat), each built as one segmented build; roots32 receives every trie's
+ * root in order.  The tries are independent: no data moves between the GPUs. */
+int kh_trie_roots_segmented_sharded(const int* devices, int ngpus, const uint8_t* keys, uint32_t klen,
+                                    const uint8_t* vals, const uint64_t* voff, const uint64_t* seg_off, uint64_t nseg,
+                                    uint32_t flags, uint8_t* roots32, kh_stats* stats);
+
 /* The kh_trie_root result computed on ngpus GPUs of this process: the
  * puts are split into ngpus contiguous slices, slice g staged to devices[g], keys hashed
  * there, records routed to the owner of their top key nibble (q * ngpus >> 4) over RCCL
@@ -334,6 +342,16 @@ int kh_trie_free(kh_trie* h);
  * must hold n*96 B).  Deterministic; the CPU restatement lives in tests. */
 int kh_dev_synth_accounts(kh_ctx* ctx, uint32_t cfg, uint64_t first, uint64_t n, uint8_t* d_addr,
                           uint8_t* d_vals, uint64_t* d_voff);
+
+/* Synthetic contract storage tries [t0, t0+nt) of config cfg (pinned in
+ * khipu_amd/csrc/synth.h: log-uniform 1..10^4 slots per trie, 32-byte big-endian slot
+ * words as keys -- hash them with KH_HASH_KEYS -- and RLP(trimmed 1-32 byte) values).
+ * Always: d_seg_off[nt+1] (each trie's first slot, from 0), *n_slots, *val_bytes.  With
+ * d_keys non-NULL also the slots: keys (n_slots*32 B), packed values (d_vals, val_bytes B)
+ * with d_voff[n_slots+1], and d_seg[n_slots] = trie - t0 (the segment ids of
+ * kh_dev_trie_build).  Deterministic per trie: any range can be made on any GPU. */
+int kh_dev_synth_storage(kh_ctx* ctx, uint32_t cfg, uint64_t t0, uint64_t nt, uint64_t* d_seg_off, uint64_t* n_slots,
+                         uint64_t* val_bytes, uint8_t* d_keys, uint8_t* d_vals, uint64_t* d_voff, uint32_t* d_seg);
 
 #ifdef __cplusplus
 }

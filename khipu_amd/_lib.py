@@ -31,6 +31,7 @@ EXPORTS = (
     "kh_forest_apply_host", "kh_block_commit", "kh_forest_last_roots", "kh_trie_open_nodes",
     "kh_trie_open_nodes_host", "kh_trie_roots_varkeys", "kh_list_roots",
     "kh_trie_root_sharded", "kh_block_commit_host", "kh_dev_list_roots", "kh_trie_get", "kh_trie_get_host",
+    "kh_dev_synth_storage", "kh_trie_roots_segmented_sharded",
 )
 
 
@@ -128,6 +129,8 @@ def lib():
     L.kh_block_commit_host.argtypes = L.kh_block_commit.argtypes
     L.kh_dev_list_roots.argtypes = [vp, vp, vp, vp, u64, vp, vp]
     L.kh_trie_get.argtypes = [vp, vp, vp, u32, u64, vp, u64, vp, vp, ctypes.POINTER(u64)]
+    L.kh_dev_synth_storage.argtypes = [vp, u32, u64, u64, vp, ctypes.POINTER(u64), ctypes.POINTER(u64), vp, vp, vp, vp]
+    L.kh_trie_roots_segmented_sharded.argtypes = [vp, i32, vp, u32, vp, vp, vp, u64, u32, vp, vp]
     L.kh_trie_get_host.argtypes = [vp, vp, vp, u32, u64, vp, u64, vp, vp, ctypes.POINTER(u64)]
     for name in EXPORTS:
         fn = getattr(L, name)

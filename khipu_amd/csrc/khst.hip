@@ -112,9 +112,15 @@ __global__ void __launch_bounds__(BS) k_hash_keys(const uint8_t* keys, uint32_t 
 
 // ... and the unsegmented sort key (the key's leading 32 bits, big-endian) with the
 // identity index in the same pass (saves k_make_ck's re-read of the keys)
+// 32-bit sort word: the segment id in the top sb bits (segmented builds, sb <= CK_SEG_BITS),
+// then the key's leading 32 - sb bits (big-endian)
+__device__ __forceinline__ uint32_t ck_word(uint64_t h0, const uint32_t* seg, uint32_t sb, uint64_t i) {
+  const uint32_t kb = (uint32_t)(bswap64(h0) >> 32);
+  return sb ? (seg[i] << (32 - sb)) | (kb >> sb) : kb;
+}
 template <bool SHORT>
 __global__ void __launch_bounds__(BS) k_hash_keys_ck(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out,
-                                                     uint32_t* ck, uint32_t* idx, uint64_t base) {
+                                                     uint32_t* ck, uint32_t* idx, const uint32_t* seg, uint32_t sb) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
   uint64_t h[4];
@@ -123,15 +129,21 @@ __global__ void __launch_bounds__(BS) k_hash_keys_ck(const uint8_t* keys, uint32
   else
     kec256_msg<false>(keys + i * klen, klen, h);
   for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
-  ck[i] = (uint32_t)(bswap64(h[0]) >> 32);
-  idx[i] = (uint32_t)(base + i);
+  ck[i] = ck_word(h[0], seg, sb, i);
+  idx[i] = (uint32_t)i;
 }
 // the same sort keys for caller-hashed keys
-__global__ void __launch_bounds__(BS) k_make_ck32(const uint64_t* K, uint64_t n, uint32_t* ck, uint32_t* idx) {
+__global__ void __launch_bounds__(BS) k_make_ck32(const uint64_t* K, uint64_t n, uint32_t* ck, uint32_t* idx,
+                                                  const uint32_t* seg, uint32_t sb) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
-  ck[i] = (uint32_t)(bswap64(K[4 * i]) >> 32);
+  ck[i] = ck_word(K[4 * i], seg, sb, i);
   idx[i] = (uint32_t)i;
+}
+// the sorted segment ids from the sorted 32-bit words (segmented ck path)
+__global__ void __launch_bounds__(BS) k_sseg_from_ck(const uint32_t* sck, uint64_t m, uint32_t sb, uint32_t* sseg) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < m) sseg[i] = sb ? sck[i] >> (32 - sb) : 0u;  // sb = 0: one segment (a 32-bit shift would be undefined)
 }
 
 // composite sort key: segment id in the top sb bits, then the key's leading bits (big-endian)
@@ -1246,6 +1258,7 @@ struct BuildOut {
   std::vector<uint64_t> res_inl;
 };
 
+constexpr uint32_t CK_KEY_BITS = 12;  // segmented ck path: fewest key bits left in the 32-bit sort word
 static uint32_t bits_for(uint64_t nseg) {
   uint32_t b = 0;
   while (b < 64 && (1ULL << b) < nseg) ++b;
@@ -1310,7 +1323,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
     uint32_t* c0 = (uint32_t*)ck0;
     uint32_t* c1 = (uint32_t*)ck1;
     if (!S.ck_ready) {
-      hipLaunchKernelGGL(k_make_ck32, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, n, c0, idx0);
+      hipLaunchKernelGGL(k_make_ck32, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, n, c0, idx0, seg, sb);
       LAUNCH_CHECK();
     }
     const bool flip = radix_sort_pairs<uint32_t>(c0, idx0, c1, idx1, n, 0, 32, rs_scratch, st);
@@ -1352,9 +1365,14 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
                            (const uint32_t*)keep_pos, (const uint32_t*)keep, n, ock, oidx);
         LAUNCH_CHECK();
       }
+      if (segmented) {  // the sorted segment ids (result_index, segment breaks) from the words
+        hipLaunchKernelGGL(k_sseg_from_ck, GRID(m, BS), dim3(BS), 0, st, (const uint32_t*)ock, m, sb, sseg);
+        LAUNCH_CHECK();
+      }
       S.m = m;
       S.sidx = oidx;
       S.sck = ock;
+      S.sseg = sseg;
       S.fallback = false;
       S.ties_u = !tie_one && S.u && m == n;  // no dedup: the run boundaries' values stand
       return;
@@ -1576,14 +1594,23 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
 
   HIPCHK(hipEventRecord(c->ev[0], st));
   // ---- 1. keys (the plain path takes its 32-bit sort keys from the hashing pass)
-  const bool ck_path = early && !segmented && !A.kn;
+  // plain root builds sort 32-bit words (segment id | leading key bits) with the input
+  // index and never gather the sorted keys.  Segmented builds too while the key bits left
+  // beside the segment id keep runs of equal words short (the block-local tie fix orders
+  // them; one longer than TIE_RUN_MAX falls back to the full sort): at most one key per
+  // four word values on average.  KHST_SEG_CK=0: the 64-bit composite sort (measurement switch).
+  static const bool seg_ck = !getenv("KHST_SEG_CK") || strcmp(getenv("KHST_SEG_CK"), "0") != 0;
+  const bool seg_words_ok = segmented && sb + CK_KEY_BITS <= 32 && (n / A.nseg) <= (1ULL << (32 - sb - 2));
+  const bool ck_path = early && !A.kn && (!segmented || (seg_ck && seg_words_ok));
   const bool ck_ready = ck_path && (A.flags & KH_HASH_KEYS);
   if (ck_ready) {
     uint32_t* c0 = (uint32_t*)ck0;
     if (A.klen <= 135)
-      hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, c0, idx0, 0ull);
+      hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, c0, idx0, A.seg,
+                         sb);
     else
-      hipLaunchKernelGGL(k_hash_keys_ck<false>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, c0, idx0, 0ull);
+      hipLaunchKernelGGL(k_hash_keys_ck<false>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, c0, idx0, A.seg,
+                         sb);
     LAUNCH_CHECK();
   } else if (A.flags & KH_HASH_KEYS) {
     if (A.klen <= 135)
@@ -1614,6 +1641,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     sseg = S.sseg;
     fallback = S.fallback;
     T.sck = S.sck;  // non-null: no sorted keys materialised (trie_ops.h sorted_key)
+    T.ck_sb = S.sck ? sb : 0;
     ties_u = S.ties_u;
   }
   const bool ties = fallback;
@@ -3359,6 +3387,74 @@ int kh_dev_hash_keys(kh_ctx* c, const uint8_t* d_keys, uint32_t klen, uint64_t n
       else
         hipLaunchKernelGGL(k_hash_keys<false>, GRID(n, BS), dim3(BS), 0, c->st, d_keys, klen, n, (uint64_t*)d_out32);
       LAUNCH_CHECK();
+    }
+  })
+}
+
+// ---- synthetic storage tries (csrc/synth.h): slot counts, slot value lengths, slots
+__global__ void __launch_bounds__(BS) k_st_count(uint32_t cfg, uint64_t t0, uint64_t nt, uint64_t* cnt) {
+  const uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (t <= nt) cnt[t] = t < nt ? synth_storage_slots(cfg, t0 + t) : 0;
+}
+__global__ void __launch_bounds__(BS) k_st_vlen(uint32_t cfg, uint64_t t0, const uint64_t* seg_off, const uint32_t* seg,
+                                                uint64_t n, uint64_t* vlen) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i > n) return;
+  if (i == n) {
+    vlen[n] = 0;
+    return;
+  }
+  const uint32_t t = seg[i];
+  vlen[i] = synth_slot(cfg, t0 + t, (uint32_t)(i - seg_off[t])).enc;
+}
+__global__ void __launch_bounds__(BS) k_st_write(uint32_t cfg, uint64_t t0, const uint64_t* seg_off, const uint32_t* seg,
+                                                 uint64_t n, const uint64_t* voff, uint8_t* keys, uint8_t* vals) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t t = seg[i], slot = (uint32_t)(i - seg_off[t]);
+  synth_slot_write(synth_slot(cfg, t0 + t, slot), slot, keys + 32 * i, vals + voff[i]);
+}
+
+int kh_dev_synth_storage(kh_ctx* c, uint32_t cfg, uint64_t t0, uint64_t nt, uint64_t* d_seg_off, uint64_t* n_slots,
+                         uint64_t* val_bytes, uint8_t* d_keys, uint8_t* d_vals, uint64_t* d_voff, uint32_t* d_seg) {
+  if (!c) return set_err(KH_EINVAL, "null context");
+  if (!d_seg_off || !n_slots || !val_bytes) return set_err(KH_EINVAL, "null output");
+  API_TRY({
+    HIPCHK(hipSetDevice(c->dev));
+    hipStream_t st = c->st;
+    if (nt >= (1ULL << 31)) throw KhError{KH_EINVAL, "too many tries"};
+    hipLaunchKernelGGL(k_st_count, GRID(nt + 1, BS), dim3(BS), 0, st, cfg, t0, nt, d_seg_off);
+    LAUNCH_CHECK();
+    c->out_emit.ensure(scan_scratch_bytes(nt + 1, 8) + 256);
+    scan_exclusive<uint64_t>(d_seg_off, d_seg_off, nt + 1, (uint64_t*)nullptr, c->out_emit.p, st);
+    HIPCHK(hipMemcpyAsync(c->h_pinned, d_seg_off + nt, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint64_t n = c->h_pinned[0];
+    if (n >= (1ULL << 31)) throw KhError{KH_EINVAL, "more than 2^31 slots"};
+    *n_slots = n;
+    const bool write = d_keys != nullptr;
+    if (write && (!d_vals || !d_voff || !d_seg)) throw KhError{KH_EINVAL, "null output"};
+    c->ws3.ensure(carve_size({n * 4 + 64, (n + 1) * 8 + 64}));
+    Carver cv{(char*)c->ws3.p, 0, c->ws3.cap};
+    uint32_t* seg = write ? d_seg : cv.take<uint32_t>(n + 16);
+    uint64_t* vo = write ? d_voff : cv.take<uint64_t>(n + 1);
+    if (n) {
+      hipLaunchKernelGGL(k_seg_ids, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)d_seg_off, nt, n, seg);
+      LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_st_vlen, GRID(n + 1, BS), dim3(BS), 0, st, cfg, t0, (const uint64_t*)d_seg_off,
+                       (const uint32_t*)seg, n, vo);
+    LAUNCH_CHECK();
+    c->out_emit.ensure(scan_scratch_bytes(n + 1, 8) + 256);
+    scan_exclusive<uint64_t>(vo, vo, n + 1, (uint64_t*)nullptr, c->out_emit.p, st);
+    HIPCHK(hipMemcpyAsync(c->h_pinned, vo + n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *val_bytes = c->h_pinned[0];
+    if (write && n) {
+      hipLaunchKernelGGL(k_st_write, GRID(n, BS), dim3(BS), 0, st, cfg, t0, (const uint64_t*)d_seg_off,
+                         (const uint32_t*)seg, n, (const uint64_t*)vo, d_keys, d_vals);
+      LAUNCH_CHECK();
+      HIPCHK(hipStreamSynchronize(st));
     }
   })
 }

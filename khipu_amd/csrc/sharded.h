@@ -355,7 +355,102 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
   }
 }
 
+// Many independent tries (configs[3]: every contract's storage trie, TrieStorage.flush per
+// contract via BlockWorldState.scala:243-252) over several GPUs of one process (SURVEY §8e
+// "Other configs"): the tries are split into ngpus contiguous ranges of about equal slot
+// counts; each device stages and builds its range as one segmented build; the roots land in
+// roots32 in trie order.  No exchange: the tries are independent.
+static void segmented_sharded(const int* devices, int ngpus, const uint8_t* keys, uint32_t klen, const uint8_t* vals,
+                              const uint64_t* voff, const uint64_t* seg_off, uint64_t nseg, uint32_t flags,
+                              uint8_t* roots32, kh_stats* stats) {
+  if (ngpus < 1 || ngpus > 16) throw KhError{KH_EINVAL, "ngpus must be in [1, 16]"};
+  const uint32_t N = (uint32_t)ngpus;
+  std::vector<int> dev(devices, devices + N);
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  for (uint32_t g = 0; g < N; ++g)
+    if (dev[g] < 0 || dev[g] >= ndev) throw KhError{KH_EDEVICE, "no such device"};
+  for (uint64_t s = 0; s < nseg; ++s)
+    if (seg_off[s + 1] < seg_off[s]) throw KhError{KH_EINVAL, "seg_off not monotone"};
+  // trie ranges [b[g], b[g+1]) balanced by slots
+  const uint64_t tot = seg_off[nseg] - seg_off[0];
+  std::vector<uint64_t> b(N + 1, nseg);
+  b[0] = 0;
+  for (uint32_t g = 1; g < N; ++g) {
+    const uint64_t want = seg_off[0] + tot * g / N;
+    b[g] = (uint64_t)(std::lower_bound(seg_off, seg_off + nseg, want) - seg_off);
+    if (b[g] < b[g - 1]) b[g] = b[g - 1];
+  }
+  std::lock_guard<std::mutex> lk(g_shard_mu);
+  while (g_shards.size() < N) g_shards.push_back(new Shard());
+  std::vector<Shard*> S(g_shards.begin(), g_shards.begin() + N);
+  for (uint32_t g = 0; g < N; ++g) {
+    if (S[g]->c && S[g]->c->dev != dev[g]) {
+      delete S[g];
+      S[g] = g_shards[g] = new Shard();
+    }
+    if (!S[g]->c) {
+      S[g]->c = ctx_new(dev[g]);
+      HIPCHK(hipSetDevice(dev[g]));
+      HIPCHK(hipStreamCreateWithFlags(&S[g]->cs, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&S[g]->ev_vals, hipEventDisableTiming));
+    }
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  on_shards(S, dev, [&](size_t g, Shard& s) {
+    memset(&s.st, 0, sizeof(s.st));
+    const uint64_t lo = b[g], hi = b[g + 1], ns = hi - lo;
+    if (ns == 0) return;
+    const uint64_t i0 = seg_off[lo], n = seg_off[hi] - i0;
+    if (n == 0) {
+      for (uint64_t t = lo; t < hi; ++t) memcpy(roots32 + 32 * t, EMPTY_TRIE_HASH, 32);
+      return;
+    }
+    std::vector<uint32_t> seg(n);
+    for (uint64_t t = lo; t < hi; ++t)
+      for (uint64_t i = seg_off[t]; i < seg_off[t + 1]; ++i) seg[i - i0] = (uint32_t)(t - lo);
+    Staged in = stage_inputs(s.c, keys + i0 * klen, klen, vals, voff + i0, n, &seg);
+    BuildArgs A{in.keys, klen, in.vals, in.voff, n, in.seg, ns, 0, flags, false};
+    BuildOut O;
+    run_build(s.c, A, O, &s.st);
+    for (uint64_t t = lo; t < hi; ++t) copy_root(O, t - lo, roots32 + 32 * t);
+  });
+  if (stats) {
+    memset(stats, 0, sizeof(*stats));
+    stats->n_inputs = tot;
+    for (uint32_t g = 0; g < N; ++g) {
+      const kh_stats& t = S[g]->st;
+      stats->n_leaves += t.n_leaves;
+      stats->n_branches += t.n_branches;
+      stats->n_extensions += t.n_extensions;
+      stats->n_inline += t.n_inline;
+      stats->n_node_hashes += t.n_node_hashes;
+      stats->n_node_perms += t.n_node_perms;
+      stats->n_key_perms += t.n_key_perms;
+      stats->n_levels = std::max(stats->n_levels, t.n_levels);
+      stats->t_leaf_ms = std::max(stats->t_leaf_ms, t.t_leaf_ms);
+      stats->t_branch_ms = std::max(stats->t_branch_ms, t.t_branch_ms);
+      stats->t_topo_ms = std::max(stats->t_topo_ms, t.t_topo_ms);
+      stats->t_sort_ms = std::max(stats->t_sort_ms, t.t_sort_ms);
+      stats->t_keys_ms = std::max(stats->t_keys_ms, t.t_keys_ms);
+    }
+    stats->t_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+}
+
 }  // namespace khst
+
+extern "C" int kh_trie_roots_segmented_sharded(const int* devices, int ngpus, const uint8_t* keys, uint32_t klen,
+                                               const uint8_t* vals, const uint64_t* voff, const uint64_t* seg_off,
+                                               uint64_t nseg, uint32_t flags, uint8_t* roots32, kh_stats* stats) {
+  API_TRY({
+    if (!devices) throw KhError{KH_EINVAL, "null device list"};
+    if (nseg == 0) return KH_OK;
+    if (!seg_off || !roots32 || (seg_off[nseg] > seg_off[0] && (!keys || !voff)))
+      throw KhError{KH_EINVAL, "null input"};
+    khst::segmented_sharded(devices, ngpus, keys, klen, vals, voff, seg_off, nseg, flags, roots32, stats);
+  })
+}
 
 extern "C" int kh_trie_root_sharded(const int* devices, int ngpus, const uint8_t* keys, uint32_t klen,
                                     const uint8_t* vals, const uint64_t* voff, uint64_t n, uint32_t flags,

@@ -11,6 +11,8 @@
 //   body     = RLP[nonce, balance, stateRoot, codeHash]          (PV63.scala:46-51)
 // with integers as minimal big-endian strings, zero as "" (rlp/package.scala:56-57).
 #pragma once
+#include <math.h>
+
 #include "trie_ops.h"
 
 namespace khst {
@@ -134,6 +136,47 @@ KH_HD uint32_t synth_body_write(const SynthAcct& a, uint64_t i, uint8_t* dst) {
 
 KH_HD void synth_addr_write(const SynthAcct& a, uint8_t* dst) {
   for (int q = 0; q < 20; ++q) dst[q] = (uint8_t)(a.addr[q >> 3] >> (8 * (q & 7)));
+}
+
+// Synthetic contract storage tries (BASELINE configs[3]), counter-based
+// per trie so any range of tries can be generated on any GPU:
+//   slots(t) = clamp(floor(exp(u * ln(10^4 + 1))), 1, 10^4), u = draw(t) / 2^64
+//              (log-uniform in [1, 10^4]; mean ~1.1k slots)
+//   slot i   : key = the 32-byte big-endian i (DataWord; hashed with KH_HASH_KEYS as
+//              hashDataWordSerializable does, trie/package.scala:34-36)
+//              value = RLP(b[0..L)) with w_q = draw(4 * (2^40 + 16384 t + i) + q),
+//              L = 1 + (w_3 >> 56) % 32, b = LE(w_0..w_3), b[0] forced non-zero (a trimmed
+//              DataWord, rlpDataWordSerializer, trie/package.scala:28-32): a 1-byte value
+//              < 0x80 is its own encoding (inline leaves occur)
+// The device's exp is the only floating-point step: every GPU generates the same data, and
+// CPU checks read the generated buffers back.
+constexpr uint32_t SYNTH_STORAGE_MAX_SLOTS = 10000;
+KH_HD uint32_t synth_storage_slots(uint32_t cfg, uint64_t t) {
+  const double u = (double)(synth_draw(cfg, t) >> 11) * (1.0 / 9007199254740992.0);
+  double c = exp(u * log((double)SYNTH_STORAGE_MAX_SLOTS + 1.0));
+  if (c < 1.0) c = 1.0;
+  if (c > (double)SYNTH_STORAGE_MAX_SLOTS) c = (double)SYNTH_STORAGE_MAX_SLOTS;
+  return (uint32_t)c;
+}
+struct SynthSlot {
+  uint64_t w[4];
+  uint32_t L;    // value bytes
+  uint32_t enc;  // RLP-encoded length
+};
+KH_HD SynthSlot synth_slot(uint32_t cfg, uint64_t t, uint32_t i) {
+  SynthSlot s;
+  const uint64_t j = 4 * ((1ULL << 40) + 16384ULL * t + i);
+  for (int q = 0; q < 4; ++q) s.w[q] = synth_draw(cfg, j + q);
+  if ((s.w[0] & 0xFF) == 0) s.w[0] |= 1;
+  s.L = 1 + (uint32_t)((s.w[3] >> 56) % 32);
+  s.enc = (s.L == 1 && (s.w[0] & 0xFF) < 0x80) ? 1 : s.L + 1;
+  return s;
+}
+KH_HD void synth_slot_write(const SynthSlot& s, uint32_t i, uint8_t* key32, uint8_t* val) {
+  for (int q = 0; q < 32; ++q) key32[q] = q < 28 ? 0 : (uint8_t)(i >> (8 * (31 - q)));
+  uint32_t n = 0;
+  if (s.enc != 1) val[n++] = (uint8_t)(0x80 + s.L);
+  for (uint32_t q = 0; q < s.L; ++q) val[n++] = (uint8_t)(s.w[q >> 3] >> (8 * (q & 7)));
 }
 
 }  // namespace khst

@@ -154,8 +154,10 @@ struct Topo {
   const uint32_t* sidx;   // [m] input index of sorted key i
   const uint32_t* sseg;   // [m] segment id (segmented only)
   const uint8_t* kn;      // [m] key length in nibbles (variable-length key builds; nullable: 64)
-  const uint32_t* sck;    // [m] sorted big-endian leading 32 key bits (unsegmented plain builds; nullable):
-                          //     boundary values come from them before the sorted keys are gathered
+  const uint32_t* sck;    // [m] sorted 32-bit sort words (plain builds; nullable): the segment id in the
+                          //     top ck_sb bits, then the big-endian leading key bits; the sorted keys are
+                          //     never gathered (sorted_key reads the input keys past these bits)
+  uint32_t ck_sb;         // segment bits at the top of sck (0: unsegmented)
   const uint8_t* vals;    // input values
   const uint64_t* voff;   // [n+1] (or [n] offsets with vlen_in)
   const uint32_t* vlen_in; // [n] value lengths (nullable: voff[i+1] - voff[i])
@@ -277,7 +279,7 @@ KH_HD Slot branch_slot(const Topo& T, uint64_t g, uint32_t d, bool ext) {
 // the sorted prefixes and, past them, the input key through its index
 KH_HD Key4 sorted_key(const Topo& T, uint64_t i, uint32_t need) {
   if (!T.sck) return load_key(T.skey, i);
-  if (need <= 8) return Key4{bswap64((uint64_t)T.sck[i] << 32), 0, 0, 0};
+  if (need <= (32 - T.ck_sb) / 4) return Key4{bswap64((uint64_t)(T.sck[i] << T.ck_sb) << 32), 0, 0, 0};
   return load_key(T.kin, T.sidx[i]);
 }
 
@@ -322,7 +324,7 @@ KH_HD uint32_t ext_enc_len(uint32_t e, uint32_t brl) {
 KH_HD uint8_t lcp_value(const Topo& T, uint64_t b) {
   int l;
   if (T.sck) {  // the first 8 nibbles from the sorted prefixes; the input keys only past them
-    const uint32_t x = T.sck[b] ^ T.sck[b + 1];
+    const uint32_t x = (T.sck[b] ^ T.sck[b + 1]) << T.ck_sb;  // the key bits (a segment break: v = 0 below)
     l = x ? (int)((uint32_t)clz64((uint64_t)x << 32) >> 2)
           : lcp_nibbles(load_key(T.kin, T.sidx[b]), load_key(T.kin, T.sidx[b + 1]));
   } else {

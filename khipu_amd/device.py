@@ -53,6 +53,32 @@ class Ctx:
         check(lib().kh_dev_synth_accounts(self.h, cfg, first, n, _ptr(addr), _ptr(vals), _ptr(voff)))
         return addr, vals, voff
 
+    def storage_slot_counts(self, cfg, t0, nt):
+        """Slot offsets int64[nt+1] (device) of synthetic storage tries [t0, t0+nt) and the total."""
+        t = self.torch
+        so = t.empty(nt + 1, dtype=t.int64, device=f"cuda:{self.device}")
+        ns, vb = ctypes.c_uint64(), ctypes.c_uint64()
+        self._sync()
+        check(lib().kh_dev_synth_storage(self.h, cfg, t0, nt, _ptr(so), ctypes.byref(ns), ctypes.byref(vb), None, None,
+                                         None, None))
+        return so, int(ns.value), int(vb.value)
+
+    def synth_storage(self, cfg, t0, nt):
+        """Synthetic storage tries [t0, t0+nt) of config cfg (csrc/synth.h): (slot offsets
+        int64[nt+1], keys uint8[n*32] (32-byte slot words: build with hash_keys), values,
+        value offsets int64[n+1], segment ids int32[n]) on the device."""
+        t = self.torch
+        dev = f"cuda:{self.device}"
+        so, n, vb = self.storage_slot_counts(cfg, t0, nt)
+        keys = t.empty(n * 32 + 64, dtype=t.uint8, device=dev)
+        vals = t.empty(vb + 64, dtype=t.uint8, device=dev)
+        voff = t.empty(n + 1, dtype=t.int64, device=dev)
+        seg = t.empty(n + 16, dtype=t.int32, device=dev)
+        ns, vb2 = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().kh_dev_synth_storage(self.h, cfg, t0, nt, _ptr(so), ctypes.byref(ns), ctypes.byref(vb2),
+                                         _ptr(keys), _ptr(vals), _ptr(voff), _ptr(seg)))
+        return so, keys, vals, voff, seg
+
     def kec256(self, data, off, n):
         t = self.torch
         out = t.empty(32 * max(n, 1), dtype=t.uint8, device=data.device)

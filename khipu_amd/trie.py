@@ -110,8 +110,10 @@ def trie_root_sharded(keys, vals, devices, hash_keys=False, klen=None, stats=Non
     return out.tobytes()
 
 
-def trie_roots(tries, hash_keys=False, stats=None):
-    """Roots of many independent tries in one device call.  tries: list of (keys, vals)."""
+def trie_roots(tries, hash_keys=False, stats=None, devices=None):
+    """Roots of many independent tries in one device call.  tries: list of (keys, vals).
+    devices: a list of GPU ids -> kh_trie_roots_segmented_sharded (contiguous trie ranges
+    balanced by slot count, one per device)."""
     keys, vals, seg_off = [], [], [0]
     klen = None
     for ks, vs in tries:
@@ -130,8 +132,14 @@ def trie_roots(tries, hash_keys=False, stats=None):
     out = np.zeros(32 * max(nseg, 1), dtype=np.uint8)
     st = stats if stats is not None else KhStats()
     flags = _lib.KH_HASH_KEYS if hash_keys else 0
-    check(lib().kh_trie_roots_segmented(kb.ctypes.data, klen, vb.ctypes.data, off.ctypes.data, so.ctypes.data, nseg,
-                                        flags, out.ctypes.data, ctypes.byref(st)))
+    if devices is None:
+        check(lib().kh_trie_roots_segmented(kb.ctypes.data, klen, vb.ctypes.data, off.ctypes.data, so.ctypes.data,
+                                            nseg, flags, out.ctypes.data, ctypes.byref(st)))
+    else:
+        dv = np.asarray(list(devices), dtype=np.int32)
+        check(lib().kh_trie_roots_segmented_sharded(dv.ctypes.data, len(dv), kb.ctypes.data, klen, vb.ctypes.data,
+                                                    off.ctypes.data, so.ctypes.data, nseg, flags, out.ctypes.data,
+                                                    ctypes.byref(st)))
     return [out[32 * i:32 * i + 32].tobytes() for i in range(nseg)]
 
 

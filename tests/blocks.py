@@ -127,6 +127,14 @@ class BlockWorkload:
 
     def block(self, b):
         """One block's ops (device tensors) and its kh_block_commit; returns the state root."""
+        return self._commit(*self.prepare(b))
+
+    def commit_prepared(self, ops):
+        """kh_block_commit of ops made by prepare(b) (profiling: inputs made beforehand)."""
+        return self._commit(*ops)
+
+    def prepare(self, b):
+        """Block b's ops as device tensors (the arguments of _commit)."""
         nc, ns, dev, g = self.nc, self.ns, self.dev, self.g
         D = self.nblocks * self.ndel
         pool = torch.randperm(self.n - D - nc, generator=g, device=dev)[:self.nupd - nc] + nc
@@ -155,7 +163,7 @@ class BlockWorkload:
         s_vals, s_voff = storage_values(g, nc * 9, dev)
         d_tid = torch.arange(nc, device=dev, dtype=torch.int32)
         d_keys = slot_keys(torch.full((nc,), ns - 1 - b, device=dev, dtype=torch.int64))
-        return self._commit(s_tid, s_keys, s_vals, s_voff, d_tid, d_keys, a_keys, a_vals, a_voff, a_tid, a_del)
+        return (s_tid, s_keys, s_vals, s_voff, d_tid, d_keys, a_keys, a_vals, a_voff, a_tid, a_del)
 
     # ---- verification: one plain build of the final sequence of puts
     def final_accounts(self, bodies=None):

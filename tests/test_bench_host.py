@@ -65,3 +65,18 @@ def test_seq_root_hashes_keys_in_c(oracle):
     vb = np.frombuffer(b"".join(vals), np.uint8)
     assert oracle.seq_root_packed(a, 20, vb, vo, 300, mode=2) == \
         oracle.seq_root([oracle.kec256(x) for x in addrs], vals)
+
+
+def test_storage_ranges_balanced():
+    """bench.py --workload storage: slot-balanced contiguous trie ranges cover every trie once."""
+    import numpy as np
+    r = np.random.default_rng(1)
+    for nt, world in ((100_000, 8), (10, 16), (1, 4), (1000, 1), (5000, 3)):
+        cnt = np.exp(r.uniform(0, np.log(10_001), nt)).astype(np.int64).clip(1, 10_000)
+        so = np.concatenate([[0], np.cumsum(cnt)])
+        b = bench.storage_ranges(so, world)
+        assert b[0] == 0 and b[-1] == nt and all(b[g] <= b[g + 1] for g in range(world))
+        slots = [int(so[b[g + 1]] - so[b[g]]) for g in range(world)]
+        assert sum(slots) == int(so[-1])
+        if nt >= 100 * world:
+            assert max(slots) <= 1.02 * so[-1] / world + 10_000

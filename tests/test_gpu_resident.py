@@ -436,5 +436,5 @@ def test_batched_get_hash_keys_and_forest(khst, oracle):
     tries = {tid: {C._rk(r): C.storage_value(r) for _ in range(r.randrange(1, 60))} for tid in (3, 7, 1000)}
     f.commit([(tid, k, v) for tid, kv in tries.items() for k, v in kv.items()])
     q = [(tid, k) for tid, kv in tries.items() for k in kv] + [(5, next(iter(tries[3])))] + [(7, C._rk(r))]
-    assert f.get(q) == [tries[tid].get(k) for tid, k in q]
+    assert f.get(q) == [tries.get(tid, {}).get(k) for tid, k in q]
     f.close()

@@ -81,3 +81,55 @@ def test_sharded_rejects_bad_args():
         trie_root_sharded([bytes(32)], [b"x"], [])
     with pytest.raises(KhError):
         trie_root_sharded([bytes(32)], [b"x"], [7])  # no such device on a 1-GPU box
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0], [0] * 8, [0] * 16], ids=lambda d: f"x{len(d)}")
+def test_segmented_sharded_vs_cpu_batch(oracle, devices):
+    """kh_trie_roots_segmented_sharded (configs[3] across GPUs, SURVEY §8e "Other configs"):
+    storage tries split into slot-balanced trie ranges, one per device; every root against
+    the CPU batch builder, including empty tries and ranges of a single huge trie."""
+    from khipu_amd.trie import trie_roots
+    r = random.Random(len(devices))
+    tries = []
+    for t in range(300):
+        n = 0 if t % 37 == 0 else (3000 if t == 150 else r.randrange(1, 60))
+        ks = [bytes(r.getrandbits(8) for _ in range(20)) for _ in range(n)]
+        vs = [bytes([r.randrange(1, 256)]) * r.randrange(1, 33) for _ in range(n)]
+        tries.append((ks, vs))
+    got = trie_roots(tries, hash_keys=True, devices=devices)
+    assert got == trie_roots(tries, hash_keys=True)
+    keys = [k for ks, _ in tries for k in ks]
+    vals = [v for _, vs in tries for v in vs]
+    so = np.cumsum([0] + [len(ks) for ks, _ in tries]).astype(np.uint64)
+    cpu, _ = oracle.batch_roots(keys, vals, klen=20, seg_off=so, hash_keys=True)
+    assert got == cpu
+    # more devices than tries
+    few = tries[:3]
+    assert trie_roots(few, hash_keys=True, devices=devices) == trie_roots(few, hash_keys=True)
+
+
+def test_synth_storage_tries_vs_cpu(oracle):
+    """kh_dev_synth_storage (csrc/synth.h configs[3] generator): a range of tries generated on
+    the device equals the same tries cut out of a larger range (per-trie determinism), and
+    their segmented GPU roots equal the CPU batch builder's on the generated bytes."""
+    from khipu_amd.device import Ctx
+    ctx = Ctx(0)
+    so, keys, vals, voff, seg = ctx.synth_storage(4, 0, 400)
+    so2, keys2, vals2, voff2, seg2 = ctx.synth_storage(4, 100, 50)
+    a, b = int(so[100]), int(so[150])
+    assert int(so2[-1]) == b - a
+    assert bytes(keys[32 * a:32 * b].cpu().numpy()) == bytes(keys2[:32 * (b - a)].cpu().numpy())
+    v0, v1 = int(voff[a]), int(voff[b])
+    assert bytes(vals[v0:v1].cpu().numpy()) == bytes(vals2[:v1 - v0].cpu().numpy())
+    counts = np.diff(so.cpu().numpy())
+    assert counts.min() >= 1 and counts.max() <= 10_000
+    n = int(so[-1])
+    hh, ll, _, st = ctx.build(keys, 32, vals, voff, n, seg=seg, nseg=400, hash_keys=True)
+    gpu = [hh[s].tobytes() for s in range(400)]
+    vo = voff.cpu().numpy().astype(np.uint64)
+    cpu, _ = oracle.batch_roots(keys[:32 * n].cpu().numpy(), (vals[:int(vo[-1])].cpu().numpy(), vo), klen=32,
+                                seg_off=so.cpu().numpy().astype(np.uint64), hash_keys=True)
+    assert gpu == cpu
+    # 1-byte values < 0x80 (raw, inline leaves) occur
+    lens = np.diff(vo)
+    assert (lens == 1).any() and (lens > 1).any()
