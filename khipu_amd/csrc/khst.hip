@@ -413,6 +413,10 @@ __global__ void __launch_bounds__(BS) k_ansv(Topo T, Pyr P, uint64_t nb) {
 // The topology kernels that run beside the leaf kernel are grid-stride loops, so their
 // grid can be capped (topo_grid) to leave the leaf kernel more of the machine.
 #define GRID_STRIDE(i, n) for (uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x; i < (n); i += (uint64_t)gridDim.x * BS)
+// the same with every thread of a block iterating together (i may pass n: wave-wide ballots)
+#define GRID_STRIDE_WAVE(i, n)                                                                     \
+  for (uint64_t i##_b = (uint64_t)blockIdx.x * BS, i = i##_b + threadIdx.x; i##_b < (n);        \
+       i##_b += (uint64_t)gridDim.x * BS, i = i##_b + threadIdx.x)
 __global__ void __launch_bounds__(BS) k_chain(Topo T, uint64_t nb) {
   GRID_STRIDE(b, nb) op_chain(T, b);
 }
@@ -694,6 +698,25 @@ __global__ void __launch_bounds__(BS) k_leaf_topo_early(Topo T) {
 // the same publish split in two (trie_ops.h op_leaf_link / op_leaf_move)
 __global__ void __launch_bounds__(BS) k_leaf_link(Topo T) {
   GRID_STRIDE(i, T.m) op_leaf_link(T, i);
+}
+__global__ void __launch_bounds__(BS) k_leaf_link_rec(Topo T) {
+  GRID_STRIDE_WAVE(i, T.m) {  // every lane of a wave runs the ballot (threads past m list nothing)
+    const bool listed = i < T.m && op_leaf_link_rec(T, i);
+    const uint64_t slot = wave_claim(&T.ctr[CTR_FIXN], listed);
+    if (listed) T.fixlist[slot] = (uint32_t)i;
+  }
+}
+// after the join: fix-list leaves (unless long) take the copy pass; long leaves their arena
+// slot and parent (op_leaf_topo_early), for k_leaf_long
+__global__ void __launch_bounds__(BS) k_leaf_fix(Topo T, uint64_t nfix, uint64_t nlong) {
+  const uint64_t q = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  auto alloc = [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); };
+  if (q < nfix) {
+    const uint32_t i = T.fixlist[q];
+    if (T.lf_emeta[i] != EMETA_LONG) op_leaf_move(T, i, alloc);
+  } else if (q < nfix + nlong) {
+    op_leaf_topo_early(T, T.longlist[q - nfix], alloc);
+  }
 }
 __global__ void __launch_bounds__(BS) k_leaf_move(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -1215,6 +1238,8 @@ struct kh_ctx {
   hipEvent_t ev[13] = {};  // [8] boundaries ready (st), [9] / [10] leaf kernel start / end (st2),
                           // [11] / [12] split hashing: st2 start / second half hashed
   unsigned long long* h_pinned = nullptr;  // small pinned staging for syncs
+  uint8_t* h_res = nullptr;                // pinned staging of the per-result outputs (grown; a pageable
+  size_t h_res_cap = 0;                    // copy of 100k roots cost 20-30 ms of page pinning per build)
   // last build (for emission)
   Topo T{};
   uint64_t last_B = 0;
@@ -1484,6 +1509,21 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   const bool early = !A.emit && !A.el && !A.kn;
   if (A.kn && (A.emit || A.el || (A.flags & KH_HASH_KEYS)))
     throw KhError{KH_EINVAL, "variable-length keys: root-only builds of unhashed keys"};
+  // The early leaves reach their parents' child records by a link pass on the topology
+  // stream (slot of each sorted leaf) and a copy pass after the join (k_leaf_move).
+  // KHST_LEAF_LINKS=1 (measurement switch) writes the child records themselves during the
+  // hashing as LINKS to the stashes, which the branch kernel follows (trie_ops.h
+  // op_leaf_link_rec; records in the phase-1 workspace, sized by the bound C <= 2n): measured
+  // at 100M, 50.9 ms against 43.5 (profiles/r3j_leaf_links_ab_100m.json): 100M scattered
+  // 10-byte record writes cost the topology stream 10 ms beside the leaf kernel.
+  // Other switches: KHST_PUBLISH_ONE (one publish pass after the join), KHST_BRANCH=coop|rescan.
+  static const bool split_publish = !getenv("KHST_PUBLISH_ONE");
+  static const bool leaf_move = !getenv("KHST_LEAF_LINKS") || strcmp(getenv("KHST_LEAF_LINKS"), "1") != 0;
+  const char* bv = getenv("KHST_BRANCH");
+  const bool coop = bv && strcmp(bv, "coop") == 0 && !A.kn;  // (the coop assembly has no branch values)
+  const bool rescan = bv && strcmp(bv, "rescan") == 0;          // op_branch_direct
+  const bool links = early && split_publish && !leaf_move && !coop && !rescan;
+  const uint64_t cbound = links ? 2 * n + 16 : 0;
 
   O.res_hash.assign(nres * 4, 0);
   O.res_len.assign(nres, 0);
@@ -1514,6 +1554,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
                                                                   // meta, pd|position, link slots
       A.kn ? n : 0,                           // sorted key lengths
       nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1, nb1,  // branch tables in key-order ids (BrTab J)
+      cbound * 32, cbound * 2, links ? n * 4 : 0, links ? n * 4 : 0,  // link mode: child records, fix / long lists
   };
   c->ws1.ensure(carve_size(sz));
   Carver cv{(char*)c->ws1.p, 0, c->ws1.cap};
@@ -1579,6 +1620,12 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   J.depth = cv.take<uint8_t>(nb1);
   J.ext = cv.take<uint8_t>(nb1);
   J.pord = cv.take<uint8_t>(nb1);
+  if (links) {
+    T.cref = cv.take<uint64_t>(cbound * 4);
+    T.cmeta = cv.take<uint16_t>(cbound);
+    T.fixlist = cv.take<uint32_t>(n);
+    T.longlist = cv.take<uint32_t>(n);
+  }
   T.depth0 = A.depth0;
   T.segmented = segmented ? 1 : 0;
   T.vals = A.vals;
@@ -1816,8 +1863,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     // child record bases
     scan_exclusive<uint32_t>(T.br_k, T.br_cbase, nb, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
   }
-  static const bool split_publish = !getenv("KHST_PUBLISH_ONE");  // measurement switch
-  if (early && split_publish) {  // the leaves' slots, while they are still being hashed
+  if (links) {  // the leaves' child records as links, while they are still being hashed
+    hipLaunchKernelGGL(k_leaf_link_rec, topo_grid(m), dim3(BS), 0, st, T);
+    LAUNCH_CHECK();
+  } else if (early && split_publish) {  // the leaves' slots, while they are still being hashed
     hipLaunchKernelGGL(k_leaf_link, topo_grid(m), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
   }
@@ -1832,6 +1881,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   HIPCHK(hipMemcpyAsync(c->h_pinned + 5, ctr + CTR_LONGB, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_pinned, ctr + CTR_B, 8 * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_pinned + 4, ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(c->h_pinned + 6, ctr + CTR_FIXN, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(c->h_pinned + 7, ctr + CTR_LONGN, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_pinned + 8, lb, 65 * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const uint64_t B = (uint32_t)c->h_pinned[0];
@@ -1848,10 +1899,15 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   const bool lmsgs = A.emit || A.kn || A.el;
   const uint64_t lmsg_words = lmsgs ? (uint64_t)LEAF_WORDS * m : 0;
   const uint64_t bmsg_words = A.emit ? (uint64_t)BR_WORDS * B : 0, xmsg_words = A.emit ? (uint64_t)EXT_WORDS * B : 0;
-  c->ws2.ensure(carve_size({C * 32, C * 2, lmsg_words * 8, lf_bytes + 64, bmsg_words * 8, xmsg_words * 8}));
+  const uint64_t nfix = links ? c->h_pinned[6] : 0, nlong = links ? c->h_pinned[7] : 0;
+  if (links && C > cbound) throw KhError{KH_EINTERNAL, "child records exceed their bound"};
+  c->ws2.ensure(carve_size({links ? 0 : C * 32, links ? 0 : C * 2, lmsg_words * 8, lf_bytes + 64, bmsg_words * 8,
+                            xmsg_words * 8}));
   Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
-  T.cref = cv2.take<uint64_t>(C * 4);
-  T.cmeta = cv2.take<uint16_t>(C);
+  if (!links) {
+    T.cref = cv2.take<uint64_t>(C * 4);
+    T.cmeta = cv2.take<uint16_t>(C);
+  }
   T.lmsg = lmsgs ? cv2.take<uint64_t>(lmsg_words) : nullptr;
   T.lstride = m;
   T.arena = cv2.take<uint8_t>(lf_bytes + 64);  // long leaves
@@ -1873,11 +1929,19 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // ---- 4. leaves: encode + hash in LDS (root only), or encode into message slots
   //         that the node-set emitter reads back, then hash
   if (early) {  // hashed already: publish into the child records; long leaves now
-    if (split_publish)
+    if (links) {  // only the listed leaves: the top one, those under deep parents, long ones
+      if (nfix + nlong) {
+        hipLaunchKernelGGL(k_leaf_fix, GRID(nfix + nlong, BS), dim3(BS), 0, st, T, nfix, nlong);
+        LAUNCH_CHECK();
+      }
+      T.links = 1;
+    } else if (split_publish) {
       hipLaunchKernelGGL(k_leaf_move, GRID(m, BS), dim3(BS), 0, st, T);
-    else
+      LAUNCH_CHECK();
+    } else {
       hipLaunchKernelGGL(k_leaf_topo_early, GRID(m, BS), dim3(BS), 0, st, T);
-    LAUNCH_CHECK();
+      LAUNCH_CHECK();
+    }
     if (lf_bytes) {
       hipLaunchKernelGGL(k_leaf_long, GRID(m, BS), dim3(BS), 0, st, T);
       LAUNCH_CHECK();
@@ -1894,9 +1958,6 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint32_t levels = 0;
   // N1 variant: one thread per branch assembling its own window (default) or the
   // wave-cooperative DPP assembly (KHST_BRANCH=coop; DESIGN.md §5 has the measurement)
-  const char* bv = getenv("KHST_BRANCH");
-  const bool coop = bv && strcmp(bv, "coop") == 0 && !A.kn;  // (the coop assembly has no branch values)
-  const bool rescan = bv && strcmp(bv, "rescan") == 0;          // op_branch_direct (measurement switch)
   for (int d = 63; d >= 0; --d) {
     uint32_t cnt = lbh[d + 1] - lbh[d];
     if (!cnt) continue;
@@ -1920,11 +1981,25 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   HIPCHK(hipEventRecord(c->ev[5], st));
 
   // ---- results
-  HIPCHK(hipMemcpyAsync(O.res_hash.data(), T.res_hash, nres * 32, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(O.res_len.data(), T.res_len, nres * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(O.res_inl.data(), T.res_inl, nres * 32, hipMemcpyDeviceToHost, st));
+  // through pinned staging: device-to-host copies into pageable memory pin its pages on
+  // every call (measured: 20-30 ms per build for 100k roots, scripts/storage_wall_probe.py)
+  const size_t rbytes = nres * (32 + 4 + 32);
+  if (rbytes > c->h_res_cap) {
+    HIPCHK(hipStreamSynchronize(st));
+    if (c->h_res) HIPCHK(hipHostFree(c->h_res));
+    c->h_res = nullptr;
+    c->h_res_cap = 0;
+    HIPCHK(hipHostMalloc((void**)&c->h_res, rbytes + rbytes / 4 + 4096, hipHostMallocDefault));
+    c->h_res_cap = rbytes + rbytes / 4 + 4096;
+  }
+  HIPCHK(hipMemcpyAsync(c->h_res, T.res_hash, nres * 32, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(c->h_res + nres * 32, T.res_len, nres * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(c->h_res + nres * 36, T.res_inl, nres * 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_pinned, ctr, CTR_N * CTR_SHARDS * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  memcpy(O.res_hash.data(), c->h_res, nres * 32);
+  memcpy(O.res_len.data(), c->h_res + nres * 32, nres * 4);
+  memcpy(O.res_inl.data(), c->h_res + nres * 36, nres * 32);
   if (c->h_pinned[CTR_ERR]) throw KhError{KH_EINTERNAL, "build: device invariant violated"};
   c->T = T;
   c->last_B = B;
@@ -2968,6 +3043,7 @@ int kh_ctx_destroy(kh_ctx* c) {
     for (auto& e : c->ev)
       if (e) (void)hipEventDestroy(e);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->own) (void)hipStreamDestroy(c->own);
     if (c->st2) (void)hipStreamDestroy(c->st2);
     delete c;
@@ -3270,7 +3346,7 @@ int kh_dev_trie_build_ev(kh_ctx* c, void* vals_ready, const uint8_t* d_keys, uin
     HIPCHK(hipSetDevice(c->dev));
     BuildArgs A{d_keys, klen, d_vals, d_voff, n, d_seg, d_seg ? nseg : 1, depth0, flags, false};
     A.vals_ready = (hipEvent_t)vals_ready;
-    BuildOut O;
+    static thread_local BuildOut O;  // capacity kept between calls (100k-result builds: no fresh pages)
     run_build(c, A, O, stats);
     uint64_t nres = O.res_len.size();
     if (h_hash32) memcpy(h_hash32, O.res_hash.data(), nres * 32);

@@ -219,6 +219,10 @@ struct Topo {
   uint64_t* pdinv;     // [n] per INPUT position: parent depth << 32 | sorted position; PDINV_SKIP for
                        //     a dropped duplicate
   uint64_t* lf_dst;    // [m] nibble << 56 | parent child-record slot, LINK_TOP for a top leaf (op_leaf_link)
+  uint32_t links;      // child records may be leaf LINKS (CM_LINK: cref holds the sorted position whose
+                       // stash lf_eref is the reference; op_leaf_link_rec, op_branch_stream)
+  uint32_t* fixlist;   // [m] sorted leaves the post-join pass publishes (top, or parent depth >= LINK_PD_MAX)
+  uint32_t* longlist;  // [m] sorted leaves longer than one Keccak block (the leaf kernel lists them)
   // element builds (resident commits, forest.h; all nullable): an element is a leaf, or
   // a SUBTREE standing for an unchanged branch at depth el_db[i] whose capped reference
   // is el_bref / el_brl (its keys all share key i's first el_db nibbles)
@@ -242,6 +246,7 @@ struct Topo {
 
 enum {
   CTR_HASHES = 0, CTR_PERMS = 1, CTR_INLINE = 2, CTR_ARENA = 3, CTR_ERR = 4, CTR_EXT = 5, CTR_LONGB = 6,
+  CTR_FIXN = 7,  // fixlist length (row 0; the stat shards use indices 0-2 and 5 of their rows)
   // scratch slots for device-side totals read back by the host
   CTR_TIE = 8, CTR_M = 9, CTR_B = 10, CTR_BRBYTES = 11, CTR_LFBYTES = 12, CTR_C = 13, CTR_E0 = 14, CTR_E1 = 15,
   CTR_N = 16
@@ -251,6 +256,17 @@ enum {
 // serialises them, so they are spread over CTR_SHARDS rows of CTR_N (one 128-byte line
 // each) by block index and summed on the host.  Row 0 holds every other counter.
 constexpr int CTR_SHARDS = 64;
+constexpr int CTR_LONGN = 16 + 7;  // longlist length (row 1, index 7: unused by the stat shards)
+// counter add returning the old value (the host replay is single-threaded)
+KH_HD unsigned long long ctr_add(unsigned long long* p, unsigned long long v) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return atomicAdd(p, v);
+#else
+  const unsigned long long o = *p;
+  *p += v;
+  return o;
+#endif
+}
 KH_HD unsigned long long* ctr_stat(unsigned long long* ctr, int idx, uint32_t block) {
   return ctr + (uint64_t)(block % CTR_SHARDS) * CTR_N + idx;
 }
@@ -935,6 +951,7 @@ KH_HD uint32_t op_leaf_in(const Topo& T, uint64_t j, LD2 ld2, uint32_t vmis, uin
   if (g.L > LEAF_SHORT_MAX) {  // encoded + hashed by op_leaf_long into its arena slot
     T.lf_emeta[si] = EMETA_LONG;
     *longb = (g.L + 7) & ~7u;
+    if (T.longlist) T.longlist[ctr_add(&T.ctr[CTR_LONGN], 1)] = si;
     return 0;
   }
   const bool top = pd == (int32_t)T.depth0 - 1;
@@ -1082,6 +1099,7 @@ KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, u
   if (live && lng) {  // encoded + hashed by op_leaf_long into its arena slot
     T.lf_emeta[si] = EMETA_LONG;
     *longb = (Lnr + 7) & ~7u;
+    if (T.longlist) T.longlist[ctr_add(&T.ctr[CTR_LONGN], 1)] = si;  // link mode: the post-join pass finds it
   }
   if (!use) return 0;
   // ---- second round trip: the value's first byte, the key and the value at their shifts
@@ -1239,6 +1257,33 @@ KH_HD void op_leaf_link(const Topo& T, uint64_t i) {
   }
   const Key4 k = sorted_key(T, i, (uint32_t)P.pd + 1);
   T.lf_dst[i] = ((uint64_t)key_nibble(k, P.pd) << 56) | ((uint64_t)T.br_cbase[P.bid] + P.pord);
+}
+// Link records (default for plain root builds): a leaf under a parent of depth < LINK_PD_MAX
+// has a path of >= 56 nibbles, so its encoding is >= 32 B and its reference is its hash (a
+// long leaf's hash is published over the link later by op_leaf_long).  Its child record is
+// written right here, while it is still being hashed, as a LINK to its stash: length 32,
+// the nibble, and the sorted position, which the branch kernel follows (op_branch_stream).
+// Every other leaf (the top one, and those under deeper parents, which may be inline) goes
+// on the fix list for the post-join pass (op_leaf_move).  Returns true when listed.
+constexpr int32_t LINK_PD_MAX = 8;
+constexpr uint16_t CM_LINK = 0x8000;
+KH_HD bool op_leaf_link_rec(const Topo& T, uint64_t i) {
+  const int64_t a = (int64_t)i - 1, c = (i + 1 < T.m) ? (int64_t)i : -1;
+  const Parent P = resolve_parent(T, a, c);
+  if (P.bid == NONE) {
+    T.lf_dst[i] = LINK_TOP;
+    return true;
+  }
+  const Key4 k = sorted_key(T, i, (uint32_t)P.pd + 1);
+  const uint32_t nib = key_nibble(k, P.pd);
+  const uint64_t slot = (uint64_t)T.br_cbase[P.bid] + P.pord;
+  if (P.pd >= LINK_PD_MAX) {
+    T.lf_dst[i] = ((uint64_t)nib << 56) | slot;
+    return true;
+  }
+  T.cref[4 * slot] = i;
+  T.cmeta[slot] = (uint16_t)(32u | (nib << 8) | CM_LINK);
+  return false;
 }
 template <typename AllocFn>
 KH_HD void op_leaf_topo_early(const Topo& T, uint64_t i, AllocFn alloc);
@@ -1697,15 +1742,19 @@ KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint6
     uint64_t I[5] = {0, 0, 0, 0, 0};
     uint64_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
     uint32_t nm = 0;
-    if (k) {
-      nm = cm[0];
-      n0 = cr[0], n1 = cr[1], n2 = cr[2], n3 = cr[3];
-    }
+    // child c's reference: its record, or the stash a LINK record points at (op_leaf_link_rec)
+    auto load_child = [&](uint32_t cc) {
+      nm = cm[cc];
+      const uint64_t* p = cr + 4 * cc;
+      if (T.links && (nm & CM_LINK)) p = T.lf_eref + 4 * p[0];
+      n0 = p[0], n1 = p[1], n2 = p[2], n3 = p[3];
+    };
+    if (k) load_child(0);
     bool have = false;  // I / off / ilen hold child c, not yet completely placed
     auto take = [&]() {  // child c from the prefetch registers; prefetch child c + 1
       const uint32_t mc = nm, len = mc & 0xFF;
       ilen = len == 32 ? 33 : len;
-      off = hh + (mc >> 8) + run;
+      off = hh + ((mc >> 8) & 0xF) + run;
       run += ilen - 1;
       if (len == 32) {
         I[0] = 0xA0 | (n0 << 8);
@@ -1720,10 +1769,7 @@ KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint6
         I[3] = n3;
         I[4] = 0;
       }
-      if (c + 1 < k) {
-        nm = cm[c + 1];
-        n0 = cr[4 * (c + 1)], n1 = cr[4 * (c + 1) + 1], n2 = cr[4 * (c + 1) + 2], n3 = cr[4 * (c + 1) + 3];
-      }
+      if (c + 1 < k) load_child(c + 1);
       have = true;
     };
     for (uint32_t b = 0; b <= nfull; ++b) {

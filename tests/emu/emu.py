@@ -23,6 +23,7 @@ def lib():
         L.emu_fold16.argtypes = [vp, vp, vp, vp]
         L.emu_node_children.argtypes = [vp, ctypes.c_uint64, ctypes.c_int, vp, vp, vp]
         L.emu_set_leaf_mode.argtypes = [ctypes.c_int]
+        L.emu_set_link_mode.argtypes = [ctypes.c_int]
         _lib = L
     return _lib
 
@@ -30,6 +31,11 @@ def lib():
 def set_leaf_mode(mode):
     """0 / 1: op_leaf_in3 with the loosest / the lane's own wave bounds; 2: op_leaf_in."""
     lib().emu_set_leaf_mode(mode)
+
+
+def set_link_mode(mode):
+    """1: leaf link records + fix pass (KHST_LEAF_LINKS=1); 0: link slots + copy pass (default)."""
+    lib().emu_set_link_mode(mode)
 
 
 def _buf(b):

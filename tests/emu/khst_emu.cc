@@ -23,6 +23,10 @@ using namespace khst;
 // loosest / the lane's own wave bounds, 2 = op_leaf_in (KHST_LEAF=v2), 3 = op_leaf_sorted
 // (KHST_LEAF=sorted) with the loosest bounds
 static int g_leaf_mode = 0;
+// 1: the leaves' child records as links (op_leaf_link_rec, KHST_LEAF_LINKS=1) with the
+// post-join fix pass and op_branch_stream on every branch; 0: link slots + the copy pass
+// (the device default)
+static int g_link_mode = 0;
 
 // keys: n*32 (already keccak'd), vals/voff packed; seg nullable.
 // Outputs per result r: hash (32 B), enc length, inline bytes (32 B).
@@ -81,7 +85,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       br_len(nbb), ex_len(nbb), lf_parent(m), lf_len(m);
   std::vector<int8_t> lf_pd(m);
   std::vector<uint64_t> br_aoff(nbb), lf_aoff(m);
-  std::vector<unsigned long long> ctr(CTR_N, 0);
+  std::vector<unsigned long long> ctr(2 * CTR_N, 0);
   std::vector<uint32_t> hist(64, 0);
   T.u = u.data();
   T.psv = psv.data();
@@ -170,6 +174,8 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.lf_eref = eref.data();
   T.lf_emeta = emeta.data();
   T.pdinv = pdinv.data();
+  std::vector<uint32_t> longlist(m + 1);
+  T.longlist = g_link_mode ? longlist.data() : nullptr;
   T.svoff = nullptr;  // as on the device: no sorted spans in early builds
   T.svlen = nullptr;
   for (uint64_t i = 0; i < m; ++i) op_pd_scatter(T, i);
@@ -235,13 +241,24 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   };
   std::vector<uint64_t> dst(m + 1);
   T.lf_dst = dst.data();
-  if (early)  // the device's split publish: slots during the hashing, then the copy
-    for (uint64_t i = 0; i < m; ++i) op_leaf_link(T, i);
-  for (uint64_t i = 0; i < m; ++i) {
-    if (early)
-      op_leaf_move(T, i, bump);
-    else
-      op_leaf_topo(T, i, bump);
+  const bool links = early && g_link_mode;
+  if (links) {  // the device default: link records, then the fix pass over the listed leaves
+    std::vector<uint32_t> fix;
+    for (uint64_t i = 0; i < m; ++i)
+      if (op_leaf_link_rec(T, i)) fix.push_back((uint32_t)i);
+    for (uint32_t i : fix)
+      if (T.lf_emeta[i] != EMETA_LONG) op_leaf_move(T, i, bump);
+    for (uint64_t q = 0; q < ctr[CTR_LONGN]; ++q) op_leaf_topo_early(T, longlist[q], bump);
+    T.links = 1;
+  } else {
+    if (early)  // the device's split publish: slots during the hashing, then the copy
+      for (uint64_t i = 0; i < m; ++i) op_leaf_link(T, i);
+    for (uint64_t i = 0; i < m; ++i) {
+      if (early)
+        op_leaf_move(T, i, bump);
+      else
+        op_leaf_topo(T, i, bump);
+    }
   }
   if (early && lfb != longb) return -7;  // the arena is sized by the early count
   std::vector<uint64_t> arena((lfb + 64) / 8 + 1), lmsg(LEAF_WORDS * m + 1), bmsg(BR_WORDS * B + 1),
@@ -278,9 +295,9 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       uint32_t in1 = 0;
       uint64_t slot[LEAF_WORDS + 1];
       // fixed-length keys: both device assemblies, on alternate branches
-      uint32_t p = T.kn      ? op_branch_fused(T, j, slot, 1, &in1)
-                   : (j & 1) ? op_branch_direct(T, j, slot, 1, &in1)
-                             : op_branch_stream(T, j, slot, 1, &in1);
+      uint32_t p = T.kn                  ? op_branch_fused(T, j, slot, 1, &in1)
+                   : ((j & 1) && !T.links) ? op_branch_direct(T, j, slot, 1, &in1)
+                                           : op_branch_stream(T, j, slot, 1, &in1);
       perms += p;
       hashes += branch_hash_count(T, j, p);
       inl += in1;
@@ -303,6 +320,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
 extern "C" {
 
 void emu_set_leaf_mode(int mode) { g_leaf_mode = mode; }
+void emu_set_link_mode(int mode) { g_link_mode = mode; }
 
 int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, uint64_t n, const uint32_t* seg,
               uint64_t nseg, uint32_t depth0, uint8_t* out_hash, uint32_t* out_len, uint8_t* out_inl,

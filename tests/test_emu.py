@@ -24,8 +24,16 @@ def leaf_mode(request):
     E.set_leaf_mode(0)
 
 
+@pytest.fixture(params=[0, 1], ids=["move", "links"])
+def link_mode(request):
+    """How the early leaves reach their parents' child records (g_link_mode)."""
+    E.set_link_mode(request.param)
+    yield request.param
+    E.set_link_mode(0)
+
+
 @pytest.mark.parametrize("case", C.all_cases(), ids=lambda c: c[0])
-def test_replay_root_vs_oracle(oracle, case, leaf_mode):
+def test_replay_root_vs_oracle(oracle, case, leaf_mode, link_mode):
     name, keys, vals = case
     res, st = E.build(keys, vals)
     assert _root(res[0]) == oracle.seq_root(keys, vals), name
