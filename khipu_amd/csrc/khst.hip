@@ -112,6 +112,9 @@ __global__ void __launch_bounds__(BS) k_hash_keys(const uint8_t* keys, uint32_t 
 
 // ... and the unsegmented sort key (the key's leading 32 bits, big-endian) with the
 // identity index in the same pass (saves k_make_ck's re-read of the keys)
+#ifndef KH_KEYS_WAVES  // measurement build switch (-DKH_KEYS_WAVES=...): occupancy of key hashing
+#define KH_KEYS_WAVES
+#endif
 // 32-bit sort word: the segment id in the top sb bits (segmented builds, sb <= CK_SEG_BITS),
 // then the key's leading 32 - sb bits (big-endian)
 __device__ __forceinline__ uint32_t ck_word(uint64_t h0, const uint32_t* seg, uint32_t sb, uint64_t i) {
@@ -119,7 +122,7 @@ __device__ __forceinline__ uint32_t ck_word(uint64_t h0, const uint32_t* seg, ui
   return sb ? (seg[i] << (32 - sb)) | (kb >> sb) : kb;
 }
 template <bool SHORT>
-__global__ void __launch_bounds__(BS) k_hash_keys_ck(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out,
+__global__ void __launch_bounds__(BS) KH_KEYS_WAVES k_hash_keys_ck(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out,
                                                      uint32_t* ck, uint32_t* idx, const uint32_t* seg, uint32_t sb) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
@@ -647,6 +650,8 @@ __device__ __forceinline__ void wave_count(unsigned long long* dst, bool f) {
 // their message shifts, and the message is assembled dword by dword (v_perm_b32) straight
 // into the Keccak state.  Every lane of a wave runs the wave-bound reductions, so threads
 // past n take part with neutral values.
+// 78 VGPRs, 6 waves per SIMD.  Forced to 7 waves (72 VGPRs, no spills) it runs 1.0 ms slower
+// in the step (profiles/r3l_occupancy_ab_100m.json), as key hashing forced to 8 (+2 ms).
 __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
   const uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
   auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {

@@ -1151,7 +1151,6 @@ KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, u
   pre |= ((p & 1) ? 0x30u : 0x20u) << (8 * (o1 - 1));
   const uint32_t k0keep = (p & 1) ? 0x0Fu << (8 * (o1 - 1)) : 0;  // the first path nibble rides in the HP byte
   KState S;
-  uint32_t hd[8];
 #pragma unroll
   for (int m = 0; m < 34; ++m) {
     const uint32_t b0 = 4u * (uint32_t)m;
@@ -1185,7 +1184,6 @@ KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, u
       x |= (uint32_t)m == me ? (uint32_t)vhw : (uint32_t)m == me + 1 ? (uint32_t)(vhw >> 32) : 0u;
     }
     if (m == 0) x |= pre;
-    if (m < 8) hd[m] = x;
     if (b0 + 4 > B.Lmin && b0 <= B.Lmax) {  // padding (KeccakCore.scala:537-546)
       KH_NOSPEC();
       x ^= (uint32_t)m == mL ? pb : 0u;
@@ -1205,8 +1203,14 @@ KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, u
     keccakf(S);
     for (int q = 0; q < 4; ++q) r[q] = lane(S, q);
     perms = 1;
-  } else {  // bytes >= L are zero in hd (padding is applied after it was taken)
-    for (int q = 0; q < 4; ++q) r[q] = ((uint64_t)hd[2 * q + 1] << 32) | hd[2 * q];
+  } else {  // the encoding itself: the message words without the padding byte at L (< 32);
+            // rebuilt here rather than kept live across the permutation (VGPRs)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t lo = S.lo[q] ^ ((uint32_t)(2 * q) == mL ? pb : 0u);
+      const uint32_t hi = S.hi[q] ^ ((uint32_t)(2 * q + 1) == mL ? pb : 0u);
+      r[q] = ((uint64_t)hi << 32) | lo;
+    }
     *inl = 1;
   }
   // a top leaf is >= 35 B, so its stash is always the hash; the preset 32 stands for every
