@@ -602,6 +602,15 @@ __global__ void __launch_bounds__(BS) k_pd_scatter(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i < T.m) op_pd_scatter(T, i);
 }
+// The same scatter restricted to the inputs [lo, hi) (KHST_PD_CHUNKS=c, measurement switch:
+// c launches after a plain k_ansv, each scattering into a 1/c slice of pdinv, so that the
+// partial-line writes of one launch may merge in the memory-side cache)
+__global__ void __launch_bounds__(BS) k_pd_scatter_rng(Topo T, uint64_t lo, uint64_t hi) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= T.m) return;
+  const uint64_t t = T.sidx ? T.sidx[i] : i;
+  if (t >= lo && t < hi) op_pd_scatter(T, i);
+}
 // Round-2 form (KHST_LEAF=v2, measurement switch): every load up front at addresses that
 // do not depend on the parent depth, the message moved into place by 64-bit byte funnels
 // and word-select networks.  82 VGPRs, 5 waves per SIMD; 5,472 VALU instructions per wave
@@ -1828,11 +1837,19 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       LAUNCH_CHECK();
       HIPCHK(hipEventRecord(c->ev[10], c->st2));
     }
-    if (pd_mode == 1)
+    static const uint32_t pd_chunks = getenv("KHST_PD_CHUNKS") ? (uint32_t)atoi(getenv("KHST_PD_CHUNKS")) : 1u;
+    if (pd_mode == 1 && pd_chunks <= 1)
       hipLaunchKernelGGL(k_ansv_pd, GRID(m, BS), dim3(BS), 0, st, T, P, nb);
     else
       hipLaunchKernelGGL(k_ansv, GRID(nb, BS), dim3(BS), 0, st, T, P, nb);
     LAUNCH_CHECK();
+    if (pd_mode == 1 && pd_chunks > 1) {
+      const uint64_t step = (n + pd_chunks - 1) / pd_chunks;
+      for (uint64_t lo = 0; lo < n; lo += step) {
+        hipLaunchKernelGGL(k_pd_scatter_rng, GRID(m, BS), dim3(BS), 0, st, T, lo, lo + step);
+        LAUNCH_CHECK();
+      }
+    }
     if (pd_mode == 1) launch_leaves(false);
     hipLaunchKernelGGL(k_chain, topo_grid(nb), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
@@ -2287,31 +2304,34 @@ __global__ void __launch_bounds__(BS) k_f_trie_list(const uint32_t* trie, const 
 __global__ void __launch_bounds__(BS) k_f_gather(AMap M, Recs R, const uint32_t* touched, const uint8_t* replaced,
                                                  const uint32_t* tlist, uint64_t ntl, const uint32_t* tries,
                                                  uint32_t nt, Elems E, unsigned long long* ctr) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i >= ntl) return;
-  // touched is u32 here; forest.h's gather reads it as a flag
-  const uint32_t r = tlist[i];
-  if (R.rlive[r] != REC_LIVE) return;
-  const uint32_t t = R.rt[r], seg = seg_of(tries, nt, t), db = R.rdb[r];
-  if (db == EL_LEAF) {
-    const bool want = !replaced[r];
-    const uint64_t e = wave_claim(E.n, want);
-    if (want) elem_fill(R, r, seg, E, e);
-    return;
-  }
-  const uint32_t mask = R.rmask[r];
-  uint64_t ck[4] = {R.rk[4ull * r], R.rk[4ull * r + 1], R.rk[4ull * r + 2], R.rk[4ull * r + 3]};
-  for (uint32_t v = 0; v < 16; ++v) {  // every lane runs all 16 steps: one claim per wave per step
-    uint32_t cr = NONE;
-    if ((mask >> v) & 1) {
-      set_nibble(ck, db, v);
-      cr = map_find(M, R, t, db + 1, ck);
-      if (cr == NONE) ctr[2] = 4;
+  // one thread per (touched record, child nibble v): the 16 child lookups of an opened
+  // branch are independent map probes (dependent HBM round trips), so they run in 16
+  // threads instead of one thread's sequence (block-commit trace: 0.29 ms per launch)
+  const uint64_t g = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  const uint64_t i = g >> 4;
+  const uint32_t v = (uint32_t)(g & 15);
+  bool want = false;
+  uint32_t er = NONE, seg = 0;
+  if (i < ntl) {
+    // touched is u32 here; forest.h's gather reads it as a flag
+    const uint32_t r = tlist[i];
+    if (R.rlive[r] == REC_LIVE) {
+      const uint32_t t = R.rt[r], db = R.rdb[r];
+      seg = seg_of(tries, nt, t);
+      if (db == EL_LEAF) {
+        want = v == 0 && !replaced[r];
+        er = r;
+      } else if ((R.rmask[r] >> v) & 1) {
+        uint64_t ck[4] = {R.rk[4ull * r], R.rk[4ull * r + 1], R.rk[4ull * r + 2], R.rk[4ull * r + 3]};
+        set_nibble(ck, db, v);
+        er = map_find(M, R, t, db + 1, ck);
+        if (er == NONE) ctr[2] = 4;
+        want = er != NONE && !touched[er];
+      }
     }
-    const bool want = cr != NONE && !touched[cr];
-    const uint64_t e = wave_claim(E.n, want);
-    if (want) elem_fill(R, cr, seg, E, e);
   }
+  const uint64_t e = wave_claim(E.n, want);  // every lane of the wave reaches the claim
+  if (want) elem_fill(R, er, seg, E, e);
 }
 __global__ void k_f_gather_roots(AMap M, Recs R, const uint32_t* touched, const uint32_t* tries, uint32_t nt, Elems E) {
   uint64_t s = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -2893,7 +2913,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                      (const uint32_t*)ur, (const uint64_t*)uo, E, hb);
   LAUNCH_CHECK();
   if (ntl)
-    hipLaunchKernelGGL(k_f_gather, GRID(ntl, BS), dim3(BS), 0, st, map_of(h), recs_of(h),
+    hipLaunchKernelGGL(k_f_gather, GRID(ntl * 16, BS), dim3(BS), 0, st, map_of(h), recs_of(h),
                        (const uint32_t*)h->touched.p, (const uint8_t*)h->replaced.p, (const uint32_t*)tlist, ntl,
                        (const uint32_t*)tries, nt, E, fctr);
   hipLaunchKernelGGL(k_f_gather_roots, GRID(nt, BS), dim3(BS), 0, st, map_of(h), recs_of(h),

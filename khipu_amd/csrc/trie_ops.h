@@ -1726,6 +1726,11 @@ KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint6
     const uint32_t nfull = L / 136;
     KState S = {};
     auto prefill = [&](uint32_t w0) {  // 0x80 over the encoding's bytes of the window
+      if (w0 + 136 <= L) {  // a whole window of the encoding: no masks
+#pragma unroll
+        for (int q = 0; q < 17; ++q) slot[q * stride] = 0x8080808080808080ULL;
+        return;
+      }
 #pragma unroll
       for (int q = 0; q < 17; ++q) {
         const uint32_t a = w0 + 8u * (uint32_t)q;
@@ -1791,16 +1796,14 @@ KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint6
         ++c;
       }
       if (!hashit) break;  // embedded in its parent: never hashed (Node.scala:114)
-      const uint32_t rem = b < nfull ? 136 : L - 136 * nfull;
-#pragma unroll
-      for (int q = 0; q < 17; ++q) {
-        uint64_t x = slot[q * stride];  // zero past the encoding already
-        if (b == nfull) {
-          if ((rem >> 3) == (uint32_t)q) x ^= 0x01ULL << (8 * (rem & 7));
-          if (q == 16) x ^= 0x80ULL << 56;
-        }
-        kxor(S, q, x);
+      if (b == nfull) {  // the padding, written into the window (two words) rather than
+                         // tested for on every word of the absorb
+        const uint32_t rem = L - 136 * nfull;
+        slot[(rem >> 3) * stride] ^= 0x01ULL << (8 * (rem & 7));
+        slot[16 * stride] ^= 0x80ULL << 56;
       }
+#pragma unroll
+      for (int q = 0; q < 17; ++q) kxor(S, q, slot[q * stride]);  // zero past the encoding already
       keccakf(S);
     }
     if (hashit) {
