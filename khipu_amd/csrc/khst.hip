@@ -738,6 +738,19 @@ __global__ void __launch_bounds__(BS) k_leaf_move(Topo T) {
     op_leaf_move(T, i, [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); });
 }
 
+// The copy pass in two parts split at a child-record slot (*thr: the first child record
+// of the branches at depth >= D, run_build): the leaves under parents of depth >= D, and
+// every top or long leaf, before the branch levels (upper = 1); the others on the second
+// stream beside the levels deeper than D - 1, which never read their records (upper = 0)
+__global__ void __launch_bounds__(BS) k_leaf_move_part(Topo T, const uint32_t* thr, int upper) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= T.m) return;
+  const uint64_t d = T.lf_dst[i];
+  const bool hi = T.lf_emeta[i] == EMETA_LONG || d == LINK_TOP || (d & LINK_SLOT) >= *thr;
+  if (hi == (upper != 0))
+    op_leaf_move(T, i, [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); });
+}
+
 __global__ void __launch_bounds__(BS) k_leaf_long(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long perms = 0, hashes = 0, inl = 0;
@@ -1250,7 +1263,7 @@ struct kh_ctx {
   std::mutex mu;
   DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, in_kn, in_aux, in_block, out_emit, emit_dev;
   hipEvent_t ev[13] = {};  // [8] boundaries ready (st), [9] / [10] leaf kernel start / end (st2),
-                          // [11] / [12] split hashing: st2 start / second half hashed
+                          // [11] second part of the leaf copy pass done (st2), [12] unused
   unsigned long long* h_pinned = nullptr;  // small pinned staging for syncs
   uint8_t* h_res = nullptr;                // pinned staging of the per-result outputs (grown; a pageable
   size_t h_res_cap = 0;                    // copy of 100k roots cost 20-30 ms of page pinning per build)
@@ -1950,6 +1963,22 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
 
   // ---- 4. leaves: encode + hash in LDS (root only), or encode into message slots
   //         that the node-set emitter reads back, then hash
+  // KHST_MOVE_SPLIT=1 (measurement switch): the copy pass of the early leaves split at
+  // depth move_d (0: not split), D = one below the busiest branch level, so the records of
+  // the leaves under the busiest levels' branches are written beside the deeper levels.
+  // Measured at 100M (profiles/r3n_move_split_ab_100m.json): 44.86 ms against 45.00 in one
+  // pass, within the noise -- the second part slows the levels it runs beside by as much as
+  // it takes off the join (branch levels 7.76 -> 8.9 ms), so it stays off.
+  uint32_t move_d = 0;
+  {
+    static const bool msplit = getenv("KHST_MOVE_SPLIT") && atoi(getenv("KHST_MOVE_SPLIT")) != 0;
+    if (early && split_publish && !links && msplit && m >= (1u << 18) && nb > 0) {
+      uint32_t best = 0, dbest = 0;
+      for (uint32_t d = 0; d < 64; ++d)
+        if (lbh[d + 1] - lbh[d] > best) best = lbh[d + 1] - lbh[d], dbest = d;
+      if (dbest + 1 < 64 && lbh[dbest + 1] < lbh[64]) move_d = dbest + 1;  // levels >= D exist
+    }
+  }
   if (early) {  // hashed already: publish into the child records; long leaves now
     if (links) {  // only the listed leaves: the top one, those under deep parents, long ones
       if (nfix + nlong) {
@@ -1957,6 +1986,13 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
         LAUNCH_CHECK();
       }
       T.links = 1;
+    } else if (split_publish && move_d) {
+      const uint32_t* thr = T.br_cbase + lbh[move_d];
+      hipLaunchKernelGGL(k_leaf_move_part, GRID(m, BS), dim3(BS), 0, c->st2, T, thr, 0);
+      LAUNCH_CHECK();
+      HIPCHK(hipEventRecord(c->ev[11], c->st2));
+      hipLaunchKernelGGL(k_leaf_move_part, GRID(m, BS), dim3(BS), 0, st, T, thr, 1);
+      LAUNCH_CHECK();
     } else if (split_publish) {
       hipLaunchKernelGGL(k_leaf_move, GRID(m, BS), dim3(BS), 0, st, T);
       LAUNCH_CHECK();
@@ -1980,9 +2016,14 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint32_t levels = 0;
   // N1 variant: one thread per branch assembling its own window (default) or the
   // wave-cooperative DPP assembly (KHST_BRANCH=coop; DESIGN.md §5 has the measurement)
+  bool moved = move_d == 0;
   for (int d = 63; d >= 0; --d) {
     uint32_t cnt = lbh[d + 1] - lbh[d];
     if (!cnt) continue;
+    if (!moved && d < (int)move_d) {  // this level reads the second part's records
+      HIPCHK(hipStreamWaitEvent(st, c->ev[11], 0));
+      moved = true;
+    }
     if (A.emit) {  // the write-back build keeps every encoding in its message slot for emission
       hipLaunchKernelGGL(k_branch_prep, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
       LAUNCH_CHECK();
@@ -2000,6 +2041,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     LAUNCH_CHECK();
     ++levels;
   }
+  if (!moved) HIPCHK(hipStreamWaitEvent(st, c->ev[11], 0));
   HIPCHK(hipEventRecord(c->ev[5], st));
 
   // ---- results
