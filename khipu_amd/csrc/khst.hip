@@ -794,10 +794,13 @@ __global__ void __launch_bounds__(BS) k_branch_hash(Topo T, uint64_t first, uint
 // V: 0 variable-length keys (op_branch_fused), 1 direct window assembly re-scanning the
 // children per window (op_branch_direct), 2 the children streamed once with the next
 // record prefetched (op_branch_stream)
-template <int V>
-__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8))) k_branch_fused(Topo T, uint64_t first, uint64_t cnt) {
-  __shared__ uint64_t slots[BS * LEAF_WORDS];
-  uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
+// WB: threads per block.  WB = 64 (KHST_BRANCH_BS=64, measurement switch): one wave per
+// block, 8,704 B of LDS, so a CU holds 18 waves instead of the 16 that 35 KB blocks of 256
+// threads allow (4.5 per SIMD instead of 4); the counters are summed per wave.
+template <int V, int WB = BS>
+__global__ void __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(4, 8))) k_branch_fused(Topo T, uint64_t first, uint64_t cnt) {
+  __shared__ uint64_t slots[WB * LEAF_WORDS];
+  uint64_t t = (uint64_t)blockIdx.x * WB + threadIdx.x;
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (t < cnt) {
     uint32_t j = (uint32_t)(first + t);
@@ -811,8 +814,19 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8)))
     hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
   }
-  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
-             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
+  if (WB == BS) {
+    block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
+               ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
+  } else {
+    perms = wave_sum(perms);
+    hashes = wave_sum(hashes);
+    inl = wave_sum(inl);
+    if ((threadIdx.x & 63) == 0) {
+      if (perms) atomicAdd(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms);
+      if (hashes) atomicAdd(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes);
+      if (inl) atomicAdd(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
+    }
+  }
 }
 
 // LDS ordering between lanes of ONE wave (the wave's LDS operations execute in
@@ -2016,6 +2030,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint32_t levels = 0;
   // N1 variant: one thread per branch assembling its own window (default) or the
   // wave-cooperative DPP assembly (KHST_BRANCH=coop; DESIGN.md §5 has the measurement)
+  static const bool branch_bs64 = getenv("KHST_BRANCH_BS") && atoi(getenv("KHST_BRANCH_BS")) == 64;
   bool moved = move_d == 0;
   for (int d = 63; d >= 0; --d) {
     uint32_t cnt = lbh[d + 1] - lbh[d];
@@ -2035,6 +2050,9 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
         hipLaunchKernelGGL(k_branch_fused<0>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
       else if (rescan)
         hipLaunchKernelGGL(k_branch_fused<1>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+      else if (branch_bs64)
+        hipLaunchKernelGGL((k_branch_fused<2, 64>), dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, T,
+                           (uint64_t)lbh[d], (uint64_t)cnt);
       else
         hipLaunchKernelGGL(k_branch_fused<2>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     }
