@@ -210,6 +210,14 @@ int kh_dev_partition(kh_ctx* ctx, const uint8_t* d_keys32, const uint8_t* d_vals
 int kh_dev_partition_ev(kh_ctx* ctx, void* vals_done, const uint8_t* d_keys32, const uint8_t* d_vals,
                         const uint64_t* d_voff, uint64_t n, uint32_t nparts, uint8_t* d_out_keys,
                         uint8_t* d_out_vals, uint64_t* d_out_vlen, uint64_t* h_counts, uint64_t* h_bytes);
+/* kh_dev_hash_keys and kh_dev_partition_ev in one call: the n klen-byte keys (addresses)
+ * are kec256'd in the pass that counts the owners, so the partition does not re-read the
+ * hashed keys to count them.  Same outputs as kh_dev_partition_ev over
+ * kh_dev_hash_keys(d_keys) (the hashed keys are written only to d_out_keys, grouped). */
+int kh_dev_hash_partition_ev(kh_ctx* ctx, void* vals_done, const uint8_t* d_keys, uint32_t klen,
+                             const uint8_t* d_vals, const uint64_t* d_voff, uint64_t n, uint32_t nparts,
+                             uint8_t* d_out_keys, uint8_t* d_out_vals, uint64_t* d_out_vlen, uint64_t* h_counts,
+                             uint64_t* h_bytes);
 
 /* ---- fast-sync NodeData verification ----
  * NodeDatasRequest.processResponse (sync/package.scala:81-125) over a batch of peer

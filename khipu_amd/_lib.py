@@ -26,7 +26,7 @@ EXPORTS = (
     "kh_last_error", "kh_version", "kh_device_count", "kh_kec256_batch", "kh_trie_root",
     "kh_trie_roots_segmented", "kh_trie_root_nodes", "kh_ctx_create", "kh_ctx_destroy", "kh_ctx_set_stream",
     "kh_dev_kec256_batch", "kh_dev_trie_build", "kh_dev_trie_build_ev", "kh_fold_root16", "kh_dev_synth_accounts", "kh_dev_hash_keys",
-    "kh_dev_partition", "kh_dev_partition_ev", "kh_trie_open", "kh_trie_apply", "kh_trie_emit_nodes", "kh_trie_size", "kh_trie_free",
+    "kh_dev_partition", "kh_dev_partition_ev", "kh_dev_hash_partition_ev", "kh_trie_open", "kh_trie_apply", "kh_trie_emit_nodes", "kh_trie_size", "kh_trie_free",
     "kh_verify_nodes", "kh_trie_open_host", "kh_trie_apply_host", "kh_forest_open", "kh_forest_apply",
     "kh_forest_apply_host", "kh_block_commit", "kh_forest_last_roots", "kh_trie_open_nodes",
     "kh_trie_open_nodes_host", "kh_trie_roots_varkeys", "kh_list_roots",
@@ -107,6 +107,7 @@ def lib():
     L.kh_dev_hash_keys.argtypes = [vp, vp, u32, u64, vp]
     L.kh_dev_partition.argtypes = [vp, vp, vp, vp, u64, u32, vp, vp, vp, vp, vp]
     L.kh_dev_partition_ev.argtypes = [vp, vp, vp, vp, vp, u64, u32, vp, vp, vp, vp, vp]
+    L.kh_dev_hash_partition_ev.argtypes = [vp, vp, vp, u32, vp, vp, u64, u32, vp, vp, vp, vp, vp]
     L.kh_trie_open.argtypes = [vp, vp, u32, vp, vp, u64, u32, vp, ctypes.POINTER(vp)]
     L.kh_trie_apply.argtypes = [vp, vp, vp, vp, u64, vp, u64, u32, u32, vp, vp]
     L.kh_trie_emit_nodes.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp]

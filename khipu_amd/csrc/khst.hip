@@ -1119,6 +1119,46 @@ __global__ void __launch_bounds__(BS) k_part_count(const uint64_t* K, uint64_t n
   __syncthreads();
   if (threadIdx.x < nparts) hist[(uint64_t)threadIdx.x * ntile + blockIdx.x] = c[threadIdx.x];
 }
+// Key hashing with k_part_count folded in (kh_dev_hash_partition_ev): each block hashes
+// BS keys and adds its owner counts into the (owner, tile) table, zeroed beforehand; a tile
+// is PT_R consecutive blocks, as k_part_place reads it
+template <bool SHORT>
+__device__ __forceinline__ void hash_keys_owner(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out,
+                                                uint32_t nparts, uint32_t ntile, uint32_t* hist) {
+  __shared__ uint32_t c[16];
+  if (threadIdx.x < 16) c[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  const bool ok = i < n;
+  uint32_t o = 0;
+  if (ok) {
+    uint64_t h[4];
+    if (SHORT)
+      kec256_short(keys + i * klen, klen, h);
+    else
+      kec256_msg<false>(keys + i * klen, klen, h);
+    for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
+    o = nibble_owner(h[0], nparts);
+  }
+  const uint64_t mask = owner_match(ok, o);
+  if (ok && (mask & lanemask_lt()) == 0) atomicAdd(&c[o], (uint32_t)__popcll(mask));  // one add per group
+  __syncthreads();
+  if (threadIdx.x < nparts && c[threadIdx.x])
+    atomicAdd(&hist[(uint64_t)threadIdx.x * ntile + blockIdx.x / PT_R], c[threadIdx.x]);
+}
+// single-block keys (addresses) held to 7 waves per SIMD, as k_hash_keys runs: the owner
+// count adds 5 VGPRs, which at 77 left it at 6 and made the fused call 0.1-0.5 ms slower
+// than hashing + k_part_count
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(7)))
+k_hash_keys_owner_s(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out, uint32_t nparts, uint32_t ntile,
+                    uint32_t* hist) {
+  hash_keys_owner<true>(keys, klen, n, out, nparts, ntile, hist);
+}
+__global__ void __launch_bounds__(BS) k_hash_keys_owner_l(const uint8_t* keys, uint32_t klen, uint64_t n,
+                                                          uint64_t* out, uint32_t nparts, uint32_t ntile,
+                                                          uint32_t* hist) {
+  hash_keys_owner<false>(keys, klen, n, out, nparts, ntile, hist);
+}
 __global__ void __launch_bounds__(BS) k_part_place(const uint64_t* K, const uint64_t* voff, uint64_t n,
                                                    uint32_t nparts, uint32_t ntile, const uint32_t* base,
                                                    uint64_t* okeys, uint64_t* olen, uint32_t* pos) {
@@ -2271,40 +2311,58 @@ static void copy_root(const BuildOut& O, uint64_t r, uint8_t* out32) {
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32_t* touched, uint8_t* replaced,
                                                   uint32_t* tlist, unsigned long long* ctr) {
-  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (o >= O.n) return;
-  // ctr[0] touched list size, [1] replaced leaves, [2] error
-  auto mark = [&](uint32_t r) {
-    const bool first = atomicExch(&touched[r], 1u) == 0u;
+  const uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  // ctr[0] touched list size, [1] replaced leaves, [2] error.  Every op of a commit passes
+  // through its trie's top records: the touched flag is read before it is exchanged, so
+  // only the first few ops contend for a hot record's atomic (a stale 0 from the vector
+  // cache costs one extra exchange, never a wrong mark), and the replacements are counted
+  // per wave.  All lanes stay in the loop until the wave is done (the marks are ballots).
+  auto mark = [&](bool want, uint32_t r) {
+    bool first = false;
+    if (want && __hip_atomic_load(&touched[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+      first = atomicExch(&touched[r], 1u) == 0u;
     const uint64_t slot = wave_claim(&ctr[0], first);
     if (first) tlist[slot] = r;
   };
-  const uint64_t* K = O.key + 4 * o;
-  const uint32_t t = O.trie[o];
+  const bool live = o < O.n;
+  const uint64_t* K = O.key + 4 * (live ? o : 0);
+  const uint32_t t = live ? O.trie[o] : 0;
   uint32_t d = 0;
-  for (int step = 0; step < 70; ++step) {
-    const uint32_t r = map_find(M, R, t, d, K);
-    if (r == NONE) return;
-    const uint32_t db = R.rdb[r];
-    if (db == EL_LEAF) {
-      mark(r);
-      const uint64_t* L = R.rk + 4ull * r;
-      if (L[0] == K[0] && L[1] == K[1] && L[2] == K[2] && L[3] == K[3]) {
-        replaced[r] = 1;  // keys are unique in the batch: one op per leaf
-        atomicAdd(&ctr[1], 1ULL);
-        // khipu's put into a leaf whose remaining path is EMPTY (it hangs under a depth-63
-        // branch) turns it into a childless value-only branch (putInLeafNode, ml == 0 with
-        // an empty existingKey: MerklePatriciaTrie.scala:187-199 -> putInBranchNode
-        // :258-262), a non-canonical node this engine does not build: refused, not diverged
-        if (d == 64 && O.kind[o] == FOP_UPSERT) atomicOr(&ctr[3], 1ULL);
+  bool active = live, repl = false, lost = live;
+  for (int step = 0; step < 70 && __ballot(active); ++step) {
+    uint32_t r = NONE;
+    bool leaf = false;
+    if (active) {
+      r = map_find(M, R, t, d, K);
+      if (r == NONE) {
+        active = lost = false;
+      } else {
+        const uint32_t db = R.rdb[r];
+        leaf = db == EL_LEAF;
+        if (leaf) {
+          const uint64_t* L = R.rk + 4ull * r;
+          if (L[0] == K[0] && L[1] == K[1] && L[2] == K[2] && L[3] == K[3]) {
+            replaced[r] = 1;  // keys are unique in the batch: one op per leaf
+            repl = true;
+            // khipu's put into a leaf whose remaining path is EMPTY (it hangs under a depth-63
+            // branch) turns it into a childless value-only branch (putInLeafNode, ml == 0 with
+            // an empty existingKey: MerklePatriciaTrie.scala:187-199 -> putInBranchNode
+            // :258-262), a non-canonical node this engine does not build: refused, not diverged
+            if (d == 64 && O.kind[o] == FOP_UPSERT) atomicOr(&ctr[3], 1ULL);
+          }
+          active = lost = false;
+        } else if (lcp_nibbles(load_key(K, 0), load_key(R.rk, r)) < (int)db) {
+          r = NONE;  // diverges in the extension
+          active = lost = false;
+        } else {
+          d = db + 1;
+        }
       }
-      return;
     }
-    if (lcp_nibbles(load_key(K, 0), load_key(R.rk, r)) < (int)db) return;  // diverges in the extension
-    mark(r);
-    d = db + 1;
+    mark(r != NONE, r);
   }
-  ctr[2] = 3;
+  wave_count(&ctr[1], repl);
+  if (lost) ctr[2] = 3;
 }
 
 // upsert op o (its rank among the batch's upserts = ur[o]) -> leaf element; value into the heap
@@ -3479,18 +3537,21 @@ int kh_dev_partition(kh_ctx* c, const uint8_t* d_keys32, const uint8_t* d_vals, 
                              h_counts, h_bytes);
 }
 
-int kh_dev_partition_ev(kh_ctx* c, void* vals_done, const uint8_t* d_keys32, const uint8_t* d_vals,
-                        const uint64_t* d_voff, uint64_t n, uint32_t nparts, uint8_t* d_out_keys,
-                        uint8_t* d_out_vals, uint64_t* d_out_vlen, uint64_t* h_counts, uint64_t* h_bytes) {
-  if (!c) return set_err(KH_EINVAL, "null context");
-  API_TRY({
+// The owner partition; with d_addr (klen-byte keys) the keys are hashed first, in the same
+// pass that counts the owners (kh_dev_hash_partition_ev), otherwise d_keys32 are the keys
+static void partition_impl(kh_ctx* c, void* vals_done, const uint8_t* d_addr, uint32_t klen, const uint8_t* d_keys32,
+                           const uint8_t* d_vals, const uint64_t* d_voff, uint64_t n, uint32_t nparts,
+                           uint8_t* d_out_keys, uint8_t* d_out_vals, uint64_t* d_out_vlen, uint64_t* h_counts,
+                           uint64_t* h_bytes) {
+  {
     if (nparts < 1 || nparts > 16) throw KhError{KH_EINVAL, "nparts must be in [1, 16]"};
+    if (d_addr && (klen == 0 || klen > 4096)) throw KhError{KH_EINVAL, "bad key length"};
     HIPCHK(hipSetDevice(c->dev));
     memset(h_counts, 0, nparts * 8);
     memset(h_bytes, 0, nparts * 8);
     if (n == 0) {  // nothing to copy: vals_done is still recorded, as khst.h promises
       if (vals_done) HIPCHK(hipEventRecord((hipEvent_t)vals_done, c->st));
-      return KH_OK;
+      return;
     }
     if (n >= (1ULL << 31)) throw KhError{KH_EINVAL, "n must be < 2^31 per device"};
     if ((uintptr_t)d_keys32 & 7 || (uintptr_t)d_out_keys & 7 || (uintptr_t)d_voff & 7 || (uintptr_t)d_out_vlen & 7 ||
@@ -3499,7 +3560,8 @@ int kh_dev_partition_ev(kh_ctx* c, void* vals_done, const uint8_t* d_keys32, con
     hipStream_t st = c->st;
     const uint32_t ntile = (uint32_t)((n + PT_TILE - 1) / PT_TILE);
     const uint64_t nh = (uint64_t)nparts * ntile;
-    c->ws3.ensure(carve_size({nh * 4, n * 4, n * 8, scan_scratch_bytes(std::max<uint64_t>(n, nh), 8), 40 * 8}));
+    c->ws3.ensure(carve_size({nh * 4, n * 4, n * 8, scan_scratch_bytes(std::max<uint64_t>(n, nh), 8), 40 * 8,
+                              d_addr ? n * 32 : 0}));
     Carver cv{(char*)c->ws3.p, 0, c->ws3.cap};
     uint32_t* hist = cv.take<uint32_t>(nh);
     uint32_t* pos = cv.take<uint32_t>(n);
@@ -3507,8 +3569,21 @@ int kh_dev_partition_ev(kh_ctx* c, void* vals_done, const uint8_t* d_keys32, con
     void* sc = cv.take<char>(scan_scratch_bytes(std::max<uint64_t>(n, nh), 8));
     unsigned long long* tot = cv.take<unsigned long long>(40);  // counts | bytes | byte total
     const uint64_t* K = (const uint64_t*)d_keys32;
-    hipLaunchKernelGGL(k_part_count, dim3(ntile), dim3(BS), 0, st, K, n, nparts, ntile, hist);
-    LAUNCH_CHECK();
+    if (d_addr) {  // hashed here, the owners counted in the same pass (no k_part_count re-read)
+      uint64_t* hk = cv.take<uint64_t>(n * 4);
+      HIPCHK(hipMemsetAsync(hist, 0, nh * 4, st));
+      if (klen <= 135)
+        hipLaunchKernelGGL(k_hash_keys_owner_s, GRID(n, BS), dim3(BS), 0, st, d_addr, klen, n, hk, nparts, ntile,
+                           hist);
+      else
+        hipLaunchKernelGGL(k_hash_keys_owner_l, GRID(n, BS), dim3(BS), 0, st, d_addr, klen, n, hk, nparts, ntile,
+                           hist);
+      LAUNCH_CHECK();
+      K = hk;
+    } else {
+      hipLaunchKernelGGL(k_part_count, dim3(ntile), dim3(BS), 0, st, K, n, nparts, ntile, hist);
+      LAUNCH_CHECK();
+    }
     scan_exclusive<uint32_t>(hist, hist, nh, (uint32_t*)nullptr, sc, st);
     hipLaunchKernelGGL(k_part_place, dim3(ntile), dim3(BS), 0, st, K, d_voff, n, nparts, ntile,
                        (const uint32_t*)hist, (uint64_t*)d_out_keys, d_out_vlen, pos);
@@ -3535,6 +3610,25 @@ int kh_dev_partition_ev(kh_ctx* c, void* vals_done, const uint8_t* d_keys32, con
       h_counts[p] = c->h_pinned[p];
       h_bytes[p] = c->h_pinned[16 + p];
     }
+  }
+}
+int kh_dev_partition_ev(kh_ctx* c, void* vals_done, const uint8_t* d_keys32, const uint8_t* d_vals,
+                        const uint64_t* d_voff, uint64_t n, uint32_t nparts, uint8_t* d_out_keys,
+                        uint8_t* d_out_vals, uint64_t* d_out_vlen, uint64_t* h_counts, uint64_t* h_bytes) {
+  if (!c) return set_err(KH_EINVAL, "null context");
+  API_TRY({
+    partition_impl(c, vals_done, nullptr, 0, d_keys32, d_vals, d_voff, n, nparts, d_out_keys, d_out_vals, d_out_vlen,
+                   h_counts, h_bytes);
+  })
+}
+int kh_dev_hash_partition_ev(kh_ctx* c, void* vals_done, const uint8_t* d_keys, uint32_t klen, const uint8_t* d_vals,
+                             const uint64_t* d_voff, uint64_t n, uint32_t nparts, uint8_t* d_out_keys,
+                             uint8_t* d_out_vals, uint64_t* d_out_vlen, uint64_t* h_counts, uint64_t* h_bytes) {
+  if (!c) return set_err(KH_EINVAL, "null context");
+  API_TRY({
+    if (n && !d_keys) throw KhError{KH_EINVAL, "null keys"};
+    partition_impl(c, vals_done, d_keys, klen, nullptr, d_vals, d_voff, n, nparts, d_out_keys, d_out_vals,
+                   d_out_vlen, h_counts, h_bytes);
   })
 }
 

@@ -69,6 +69,28 @@ class GpuBackend:
                                         _ptr(pv), _ptr(pl), cnt.ctypes.data, nb.ctypes.data))
         return pk, pv, pl, cnt[:nparts].astype(np.int64), nb[:nparts].astype(np.int64)
 
+    def hash_partition(self, addr, vals, voff, n, nparts, klen=20):
+        """hash_keys + partition in one library call (kh_dev_hash_partition_ev: the owners
+        are counted in the hashing pass); same outputs and overlap as partition().  Not what
+        the step runs: measured slower than the two calls (scripts/shard_rank_sim.py)."""
+        from ._lib import check, lib
+        from .device import _ptr
+        pk = torch.empty(n * 32 + 64, dtype=torch.uint8, device=self.device)
+        pv = torch.empty(vals.numel() + 64, dtype=torch.uint8, device=self.device)
+        pl = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        cnt = np.zeros(16, np.uint64)
+        nb = np.zeros(16, np.uint64)
+        torch.cuda.synchronize(self.device)
+        self.vals_done = None
+        ev = None
+        if self.overlap:
+            self.vals_done = torch.cuda.Event()
+            self.vals_done.record()  # creates the event; the library records it again on its stream
+            ev = self.vals_done.cuda_event
+        check(lib().kh_dev_hash_partition_ev(self.ctx.h, ev, _ptr(addr), klen, _ptr(vals), _ptr(voff), n, nparts,
+                                             _ptr(pk), _ptr(pv), _ptr(pl), cnt.ctypes.data, nb.ctypes.data))
+        return pk, pv, pl, cnt[:nparts].astype(np.int64), nb[:nparts].astype(np.int64)
+
     def wait(self, ev):
         """The current (torch) stream waits for ev; the host does not."""
         torch.cuda.current_stream(self.device).wait_event(ev)
@@ -223,6 +245,8 @@ def sharded_root(be, addr, vals, voff, n, klen=20, keys_prehashed=False, phases=
         mark()
         mark()
     else:
+        # (hashing and partition as two calls: the fused kh_dev_hash_partition_ev measured
+        # 0.1-0.3 ms slower per rank, profiles/r3t_shard_rank_sim_world*.json)
         pk, pv, pl, cnt, nb = be.partition(keys32, vals, voff, n, world)
         mark()
         rk, rv, ro, m, ready = exchange(be, pk, pv, pl, cnt, nb)

@@ -2,7 +2,9 @@
 
   hash      kec256 of the rank's 100M/N slice of the addresses;
   partition the slice into N owners (kh_dev_partition_ev: keys, lengths, counts; the value
-            copy, which the step overlaps with the key exchange, is timed on its own);
+            copy, which the step overlaps with the key exchange, is timed on its own); and
+            both in one call (kh_dev_hash_partition_ev, the owners counted in the hashing
+            pass; measured slower, so the step does not use it);
   build     the OWNER-SHAPED shard from nibble 1 (depth0 = 1): the records of all 100M
             accounts whose top key nibble q has q * N >> 4 == 0 -- exactly what rank 0
             receives (100M/N records under 16/N root nibbles), not the rank's own slice.
@@ -51,7 +53,7 @@ def main():
     # this rank's own slice for the source-side phases
     addr, vals, voff = be.ctx.synth_accounts(a.cfg, 0, n)
     be.sync()
-    times = {"hash_keys": [], "partition_keys": [], "value_copy": [], "build": []}
+    times = {"hash_keys": [], "partition_keys": [], "value_copy": [], "build": [], "hash_partition_keys": []}
     hh = None
     for _ in range(a.steps + 1):
         t0 = time.perf_counter()
@@ -67,8 +69,12 @@ def main():
         hh, ll, ii = be.build(sk, sv, so, m, depth0=1)
         be.sync()
         t4 = time.perf_counter()
+        be.hash_partition(addr, vals, voff, n, N)  # hashing + partition in one call (measured, not run by the step)
+        t5 = time.perf_counter()
+        be.vals_done.synchronize()
+        be.sync()
         for name, x, y in (("hash_keys", t0, t1), ("partition_keys", t1, t2), ("value_copy", t2, t3),
-                           ("build", t3, t4)):
+                           ("build", t3, t4), ("hash_partition_keys", t4, t5)):
             times[name].append((y - x) * 1e3)
     st = be.last_stats
     med = {k: round(float(np.median(v[1:])), 3) for k, v in times.items()}
@@ -78,6 +84,7 @@ def main():
            "shard_nibbles": [q for q in range(16) if (q * N) >> 4 == 0],
            "ms": med,
            "critical_path_ms_excl_exchange": round(med["hash_keys"] + med["partition_keys"] + med["build"], 3),
+           "critical_path_ms_excl_exchange_fused": round(med["hash_partition_keys"] + med["build"], 3),
            "build_stages_ms": {"sort": st.t_sort_ms, "topology": st.t_topo_ms, "leaves": st.t_leaf_ms,
                                "branches": st.t_branch_ms, "total": st.t_total_ms},
            "subtrie_refs_occupied": int((ll > 0).sum()),

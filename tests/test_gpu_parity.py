@@ -299,6 +299,41 @@ def test_partition_vs_host(khst, nparts):
         assert np.array_equal(pv[:len(want)].cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("nparts", [2, 8, 16])
+def test_hash_partition_vs_host(khst, oracle, nparts):
+    """kh_dev_hash_partition_ev (the keys kec256'd in the pass that counts the owners) ==
+    the oracle's kec256 of every address, partitioned stably by top-nibble owner: keys,
+    lengths, value bytes, counts and bytes per owner; 20-byte addresses (the short
+    single-block hash), 200-byte keys (multi-block), n not a multiple of the 2,048-record
+    tile, and the empty batch."""
+    import torch
+    from khipu_amd import sharded
+    rng = np.random.default_rng(100 + nparts)
+    be = sharded.GpuBackend(0)
+    for klen, n in ((20, 0), (20, 5_000), (20, 70_001), (200, 3_001)):
+        lens = rng.integers(0, 120, n).astype(np.int64)
+        vo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        v = rng.integers(0, 256, int(vo[-1]) + 64, dtype=np.uint8)
+        a = rng.integers(0, 256, n * klen + 64, dtype=np.uint8)
+        ad, vd, od = (torch.from_numpy(x).to("cuda:0") for x in (a, v, vo))
+        pk, pv, pl, cnt, nb = be.hash_partition(ad, vd, od, n, nparts, klen)
+        be.wait(be.vals_done)
+        pv = pv.clone()
+        torch.cuda.synchronize()
+        kk = np.frombuffer(b"".join(oracle.kec256(a[klen * i:klen * i + klen].tobytes()) for i in range(n)),
+                           np.uint8).reshape(n, 32)
+        owner = ((kk[:, 0] >> 4).astype(np.int64) * nparts) >> 4
+        order = np.argsort(owner, kind="stable")
+        assert np.array_equal(cnt, np.bincount(owner, minlength=nparts)[:nparts]), (klen, n)
+        assert np.array_equal(nb, np.bincount(owner, weights=lens, minlength=nparts)[:nparts].astype(np.int64))
+        if n == 0:
+            continue
+        assert np.array_equal(pk[:n * 32].cpu().numpy(), kk[order].reshape(-1)), (klen, n)
+        assert np.array_equal(pl[:n].cpu().numpy(), lens[order])
+        want = np.concatenate([v[vo[i]:vo[i + 1]] for i in order])
+        assert np.array_equal(pv[:len(want)].cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("variant", ["lane", "coop"])
 def test_branch_variants_vs_oracle(khst, oracle, variant, monkeypatch):
     """Both N1 branch kernels (KHST_BRANCH: one thread per branch, or the wave-cooperative
