@@ -1371,6 +1371,20 @@ static uint32_t bits_for(uint64_t nseg) {
   return b;
 }
 
+// the context's pinned result staging, grown to at least `bytes` (the device is drained
+// first: an earlier copy into the old buffer may still be in flight)
+static uint8_t* pinned_stage(kh_ctx* c, size_t bytes) {
+  if (bytes > c->h_res_cap) {
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (c->h_res) HIPCHK(hipHostFree(c->h_res));
+    c->h_res = nullptr;
+    c->h_res_cap = 0;
+    HIPCHK(hipHostMalloc((void**)&c->h_res, bytes + bytes / 4 + 4096, hipHostMallocDefault));
+    c->h_res_cap = bytes + bytes / 4 + 4096;
+  }
+  return c->h_res;
+}
+
 static float ev_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0;
   if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
@@ -1713,12 +1727,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.voff = A.voff;
   T.vlen_in = A.vlen;
 
-  HIPCHK(hipMemsetAsync(T.ctr, 0, CTR_N * CTR_SHARDS * 8, st));
-  HIPCHK(hipMemsetAsync(T.depth_hist, 0, 64 * 4, st));
-  HIPCHK(hipMemsetAsync(lb, 0, 80 * 4, st));
-  HIPCHK(hipMemsetAsync(T.res_len, 0, nres * 4, st));
-  HIPCHK(hipMemsetAsync(T.res_hash, 0, nres * 32, st));
-  HIPCHK(hipMemsetAsync(T.res_inl, 0, nres * 32, st));
+  // results, counters, depth histogram and level bounds are carved back to back: one memset
+  HIPCHK(hipMemsetAsync(T.res_hash, 0, (size_t)((char*)(lb + 80) - (char*)T.res_hash), st));
 
   HIPCHK(hipEventRecord(c->ev[0], st));
   // ---- 1. keys (the plain path takes its 32-bit sort keys from the hashing pass)
@@ -2105,15 +2115,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // ---- results
   // through pinned staging: device-to-host copies into pageable memory pin its pages on
   // every call (measured: 20-30 ms per build for 100k roots, scripts/storage_wall_probe.py)
-  const size_t rbytes = nres * (32 + 4 + 32);
-  if (rbytes > c->h_res_cap) {
-    HIPCHK(hipStreamSynchronize(st));
-    if (c->h_res) HIPCHK(hipHostFree(c->h_res));
-    c->h_res = nullptr;
-    c->h_res_cap = 0;
-    HIPCHK(hipHostMalloc((void**)&c->h_res, rbytes + rbytes / 4 + 4096, hipHostMallocDefault));
-    c->h_res_cap = rbytes + rbytes / 4 + 4096;
-  }
+  pinned_stage(c, nres * (32 + 4 + 32));
   HIPCHK(hipMemcpyAsync(c->h_res, T.res_hash, nres * 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_res + nres * 32, T.res_len, nres * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_res + nres * 36, T.res_inl, nres * 32, hipMemcpyDeviceToHost, st));
@@ -2317,9 +2319,16 @@ __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32
   // only the first few ops contend for a hot record's atomic (a stale 0 from the vector
   // cache costs one extra exchange, never a wrong mark), and the replacements are counted
   // per wave.  All lanes stay in the loop until the wave is done (the marks are ballots).
+  // The ops are sorted by (trie, key), so the lanes of a wave that reach the same record at
+  // a step are adjacent: only the first lane of each run reads and exchanges the flag (at the
+  // top levels every lane of every wave reaches the same few records, and one atomic per
+  // lane serialised there: the block-commit trace's 355 us account descent).
   auto mark = [&](bool want, uint32_t r) {
+    const uint32_t rr = want ? r : NONE;
+    const uint32_t prev = __shfl_up(rr, 1);
+    const bool lead = want && ((threadIdx.x & 63) == 0 || prev != rr);
     bool first = false;
-    if (want && __hip_atomic_load(&touched[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    if (lead && __hip_atomic_load(&touched[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
       first = atomicExch(&touched[r], 1u) == 0u;
     const uint64_t slot = wave_claim(&ctr[0], first);
     if (first) tlist[slot] = r;
@@ -2367,8 +2376,10 @@ __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32
 
 // upsert op o (its rank among the batch's upserts = ur[o]) -> leaf element; value into the heap
 __global__ void __launch_bounds__(BS) k_f_upsert_elems(FOps O, const uint32_t* tries, uint32_t nt, const uint32_t* ur,
-                                                       const uint64_t* uoff, Elems E, uint64_t heap_base) {
+                                                       const uint64_t* uoff, Elems E, uint64_t heap_base,
+                                                       uint64_t nups) {
   uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o == 0) *E.n = nups;
   if (o >= O.n || O.kind[o] != FOP_UPSERT) return;
   const uint64_t e = ur[o];
   for (int q = 0; q < 4; ++q) E.key[4 * e + q] = O.key[4 * o + q];
@@ -2383,41 +2394,44 @@ __global__ void __launch_bounds__(BS) k_f_upsert_elems(FOps O, const uint32_t* t
   for (int q = 0; q < 4; ++q) E.cref[4 * e + q] = 0;
   E.crl[e] = 0;
 }
-// op o's value: (batch offset, length) -> for the heap copy
-__global__ void __launch_bounds__(BS) k_f_upsert_len(FOps O, const uint32_t* sidx, const uint64_t* voff,
-                                                     uint64_t* ulen, uint32_t* isup) {
-  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+// after the counts are known, CG threads per sorted op o: an upsert's value into the heap at
+// its offset uoff[o] (the exclusive scan of the upsert lengths over the sorted ops) and that
+// offset by upsert rank (uo[ur[o]]; uo[nups] = the total); a new trie's id into the list
+__global__ void __launch_bounds__(BS) k_f_ops_post(FOps O, const uint32_t* sidx, const uint32_t* ur,
+                                                   const uint8_t* vals, const uint64_t* voff, const uint64_t* uoff,
+                                                   uint64_t* uo, uint64_t nups, uint64_t total, uint8_t* heap,
+                                                   uint64_t heap_base, const uint32_t* tflag, const uint32_t* tpos,
+                                                   uint32_t* tries) {
+  const uint64_t g = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  const uint64_t o = g / CG;
+  const uint32_t sub = threadIdx.x % CG;
+  if (g == 0) uo[nups] = total;
   if (o >= O.n) return;
-  const bool up = O.kind[o] == FOP_UPSERT;
+  if (sub == 0 && tflag[o]) tries[tpos[o]] = O.trie[o];
+  if (O.kind[o] != FOP_UPSERT) return;
+  if (sub == 0) uo[ur[o]] = uoff[o];
+  const uint64_t s = sidx[o];
+  copy_bytes_group(heap + heap_base + uoff[o], vals + voff[s], voff[s + 1] - voff[s], sub);
+}
+// sorted op o: its kind, the flag of a new trie (the segments of the element build), and for
+// an upsert its rank flag and value length (the heap copy); one launch over the sorted ops.
+// A single-trie commit (segd false) writes its trie ids (0) here too.
+__global__ void __launch_bounds__(BS) k_f_prep(const uint32_t* sidx, uint64_t n, uint64_t nup, bool segd,
+                                               uint32_t* trie, const uint64_t* voff, uint8_t* kind, uint32_t* tflag,
+                                               uint32_t* isup, uint64_t* ulen) {
+  const uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o >= n) return;
+  const uint32_t s = sidx[o];
+  const bool up = s < nup;
+  kind[o] = up ? FOP_UPSERT : FOP_DELETE;
+  if (segd) {
+    tflag[o] = (o == 0 || trie[o] != trie[o - 1]) ? 1u : 0u;
+  } else {
+    trie[o] = 0;
+    tflag[o] = o == 0 ? 1u : 0u;
+  }
   isup[o] = up ? 1u : 0u;
-  ulen[o] = up ? voff[sidx[o] + 1] - voff[sidx[o]] : 0;
-}
-__global__ void __launch_bounds__(BS) k_f_rank_scatter(FOps O, const uint32_t* ur, const uint64_t* uoff, uint64_t* uo,
-                                                       uint64_t nups, uint64_t total) {
-  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (o == 0) uo[nups] = total;
-  if (o < O.n && O.kind[o] == FOP_UPSERT) uo[ur[o]] = uoff[o];
-}
-__global__ void __launch_bounds__(BS) k_f_heap_copy(FOps O, const uint32_t* sidx, const uint32_t* ur,
-                                                    const uint8_t* vals, const uint64_t* voff, const uint64_t* uoff,
-                                                    uint8_t* heap, uint64_t heap_base) {
-  uint64_t o = ((uint64_t)blockIdx.x * BS + threadIdx.x) / CG;
-  if (o >= O.n || O.kind[o] != FOP_UPSERT) return;
-  const uint64_t e = ur[o], s = sidx[o];
-  copy_bytes_group(heap + heap_base + uoff[e], vals + voff[s], voff[s + 1] - voff[s], threadIdx.x % CG);
-}
-__global__ void __launch_bounds__(BS) k_f_kinds(const uint32_t* sidx, uint64_t n, uint64_t nup, uint8_t* kind) {
-  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (o < n) kind[o] = sidx[o] < nup ? FOP_UPSERT : FOP_DELETE;
-}
-__global__ void __launch_bounds__(BS) k_f_trie_flags(const uint32_t* trie, uint64_t n, uint32_t* flag) {
-  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (o < n) flag[o] = (o == 0 || trie[o] != trie[o - 1]) ? 1u : 0u;
-}
-__global__ void __launch_bounds__(BS) k_f_trie_list(const uint32_t* trie, const uint32_t* flag, const uint32_t* pos,
-                                                    uint64_t n, uint32_t* tries) {
-  uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (o < n && flag[o]) tries[pos[o]] = trie[o];
+  ulen[o] = up ? voff[s + 1] - voff[s] : 0;
 }
 __global__ void __launch_bounds__(BS) k_f_gather(AMap M, Recs R, const uint32_t* touched, const uint8_t* replaced,
                                                  const uint32_t* tlist, uint64_t ntl, const uint32_t* tries,
@@ -2502,18 +2516,18 @@ __global__ void __launch_bounds__(BS) k_f_branch_recs(Topo T, const uint32_t* Bp
   sel[T.m + 2 * j] = same_b ? 0 : 1;
   sel[T.m + 2 * j + 1] = same_x ? 0 : 1;
 }
-// elements (sorted position i): flag of a new record (an upsert) for the scan of their ids
-__global__ void __launch_bounds__(BS) k_f_elem_new(Topo T, Elems E, uint32_t* isnew) {
-  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i < T.m) isnew[i] = E.src[T.sidx[i]] == NONE ? 1u : 0u;
-}
-// write-back selection of element i: an upsert's leaf, a leaf whose anchor moved, and a
-// subtree's new extension (a subtree hanging at its own depth has no node of its own)
-__global__ void __launch_bounds__(BS) k_f_elem_sel(Topo T, Elems E, uint8_t* sel) {
+// elements (sorted position i): the source record (src), the flag of a new record (an
+// upsert) for the scan of their ids, and the write-back selection: an upsert's leaf, a leaf
+// whose anchor moved, and a subtree's new extension (a subtree hanging at its own depth has
+// no node of its own)
+__global__ void __launch_bounds__(BS) k_f_elem_flags(Topo T, Elems E, uint8_t* sel, uint32_t* isnew, uint32_t* src) {
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= T.m) return;
   const uint32_t s = T.sidx[i], a = (uint32_t)(T.lf_pd[i] + 1);
-  const bool moved = E.src[s] == NONE || E.oldd[s] != a;
+  const uint32_t es = E.src[s];
+  src[i] = es;
+  isnew[i] = es == NONE ? 1u : 0u;
+  const bool moved = es == NONE || E.oldd[s] != a;
   const bool sub = T.el_db[i] != EL_LEAF;
   sel[i] = (moved && !(sub && T.el_db[i] == a)) ? 1 : 0;
 }
@@ -2540,15 +2554,15 @@ __global__ void __launch_bounds__(BS) k_f_elem_recs(Topo T, Elems E, const uint3
   R.rbrl[r] = T.el_brl[i];
   R.rlive[r] = REC_LIVE;
 }
-__global__ void __launch_bounds__(BS) k_f_elem_src(Topo T, Elems E, uint32_t* src) {
+// map maintenance: delete records' current anchors (two lists in one launch: the touched
+// records, then the element sources), mark dead, insert
+__global__ void __launch_bounds__(BS) k_map_delete(AMap M, Recs R, const uint32_t* list, uint64_t n,
+                                                   const uint32_t* list2, uint64_t n2) {
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i < T.m) src[i] = E.src[T.sidx[i]];
-}
-// map maintenance: delete records' current anchors, mark dead, insert
-__global__ void __launch_bounds__(BS) k_map_delete(AMap M, Recs R, const uint32_t* list, uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i >= n || list[i] == NONE) return;
-  const uint64_t sl = map_slot_of(M, R, list[i]);
+  if (i >= n + n2) return;
+  const uint32_t r = i < n ? list[i] : list2[i - n];
+  if (r == NONE) return;
+  const uint64_t sl = map_slot_of(M, R, r);
   if (sl != ~0ULL) M.tag[sl] = 1;  // tombstone
 }
 // an aborted commit: the records its descent flagged are left as they were
@@ -2568,12 +2582,13 @@ __global__ void __launch_bounds__(BS) k_rec_dead(Recs R, const uint32_t* list, u
   touched[r] = 0;
   replaced[r] = 0;
 }
-// insert records list[i] (or base + i when list is null) at their anchors
-__global__ void __launch_bounds__(BS) k_map_insert(AMap M, Recs R, const uint32_t* list, uint64_t base, uint64_t n,
-                                                   unsigned long long* err) {
+// insert records at their anchors: base + i for i < nb, then list[i - nb] for the next n
+// (list may be null when n is 0)
+__global__ void __launch_bounds__(BS) k_map_insert(AMap M, Recs R, uint64_t base, uint64_t nb, const uint32_t* list,
+                                                   uint64_t n, unsigned long long* err) {
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t r = list ? list[i] : (uint32_t)(base + i);
+  if (i >= nb + n) return;
+  const uint32_t r = i < nb ? (uint32_t)(base + i) : list[i - nb];
   if (R.rlive[r] != REC_LIVE) return;
   const unsigned long long h = anchor_tag(R.rt[r], R.rd[r], R.rk + 4ull * r);
   for (uint64_t s = h & M.mask, k = 0; k <= M.mask; s = (s + 1) & M.mask, ++k) {
@@ -2630,6 +2645,8 @@ struct kh_trie {
   bool em_valid = false;
   std::vector<uint32_t> tries;  // last commit: touched tries and their roots
   std::vector<uint8_t> roots;
+  uint32_t* d_tries = nullptr;  // ... the same on the device (in tbuf; the block commit's injection reads them)
+  uint64_t* d_roots = nullptr;
 };
 
 static Recs recs_of(kh_trie* h) {
@@ -2697,8 +2714,8 @@ static void map_rebuild(kh_trie* h, uint64_t headroom) {
   unsigned long long* err = (unsigned long long*)h->merr.p;
   HIPCHK(hipMemsetAsync(err, 0, 16, st));
   if (h->rn) {
-    hipLaunchKernelGGL(k_map_insert, GRID(h->rn, BS), dim3(BS), 0, st, map_of(h), recs_of(h), (const uint32_t*)nullptr,
-                       (uint64_t)0, h->rn, err);
+    hipLaunchKernelGGL(k_map_insert, GRID(h->rn, BS), dim3(BS), 0, st, map_of(h), recs_of(h), (uint64_t)0, h->rn,
+                       (const uint32_t*)nullptr, (uint64_t)0, err);
     hipLaunchKernelGGL(k_rec_count_live, GRID(h->rn, BS), dim3(BS), 0, st, (const uint8_t*)h->rlive.p, h->rn, err + 1);
   }
   LAUNCH_CHECK();
@@ -2851,11 +2868,6 @@ struct FCommit {  // one commit's inputs (device buffers)
   uint32_t klen = 32;
 };
 
-__global__ void __launch_bounds__(BS) k_u32_fill(uint32_t* out, uint64_t n, uint32_t v) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i < n) out[i] = v;
-}
-
 static int emit_nodes_dev(kh_ctx* c, DevBuf& out, uint64_t* n_nodes, uint64_t* rlp_len);
 
 // One commit of a block's ops into the forest: upserts then deletes, the last op on a
@@ -2936,21 +2948,14 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   sort_dedup(c, S);
   const uint64_t nd = S.m;
   uint32_t* otrie = segd ? S.sseg : sseg;  // the compaction of duplicates moves the sorted ids
-  if (!segd) {
-    hipLaunchKernelGGL(k_u32_fill, GRID(nd, BS), dim3(BS), 0, st, otrie, nd, 0u);
-    LAUNCH_CHECK();
-  }
-  hipLaunchKernelGGL(k_f_kinds, GRID(nd, BS), dim3(BS), 0, st, (const uint32_t*)S.sidx, nd, F.nup, kind);
+  // kinds, the distinct tries of the batch (sorted: the segments of the element build), and
+  // the upserts' ranks and value offsets (their values go to the heap)
+  hipLaunchKernelGGL(k_f_prep, GRID(nd, BS), dim3(BS), 0, st, (const uint32_t*)S.sidx, nd, F.nup, segd, otrie,
+                     F.up_voff, kind, tflag, isup, ulen);
   LAUNCH_CHECK();
   FOps O{(const uint64_t*)S.skey, (const uint32_t*)otrie, (const uint8_t*)kind, nd};
-  // distinct tries of the batch (sorted): the segments of the element build
-  hipLaunchKernelGGL(k_f_trie_flags, GRID(nd, BS), dim3(BS), 0, st, (const uint32_t*)otrie, nd, tflag);
-  LAUNCH_CHECK();
   uint32_t* ntp = (uint32_t*)(S.ctr + 12);
   scan_exclusive<uint32_t>(tflag, tpos, nd, ntp, S.scan_scratch, st);
-  // upserts: ranks and value offsets (their values go to the heap)
-  hipLaunchKernelGGL(k_f_upsert_len, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)S.sidx, F.up_voff, ulen, isup);
-  LAUNCH_CHECK();
   uint32_t* nupp = (uint32_t*)(S.ctr + 13);
   scan_exclusive<uint32_t>(isup, ur, nd, nupp, S.scan_scratch, st);
   scan_exclusive<uint64_t>(ulen, uoff, nd, (uint64_t*)(S.ctr + 14), S.scan_scratch, st);
@@ -2958,13 +2963,22 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   HIPCHK(hipStreamSynchronize(st));
   const uint32_t nt = (uint32_t)c->h_pinned[0], nups = (uint32_t)c->h_pinned[1];
   const uint64_t ubytes = c->h_pinned[2];
-  // ---- trie list
+  // ---- trie list; upsert values into the heap (appended past heap_n, which moves only once
+  // the commit is accepted): uoff is the exclusive scan of their lengths over the sorted
+  // ops, uo the same offsets by upsert rank (uo[nups] = total)
   h->tbuf.ensure(carve_size({(uint64_t)nt * 4, (uint64_t)nt * 32}));
   Carver ct{(char*)h->tbuf.p, 0, h->tbuf.cap};
   uint32_t* tries = ct.take<uint32_t>(nt);
   uint64_t* roots = ct.take<uint64_t>((uint64_t)nt * 4);
-  hipLaunchKernelGGL(k_f_trie_list, GRID(nd, BS), dim3(BS), 0, st, (const uint32_t*)otrie, (const uint32_t*)tflag,
-                     (const uint32_t*)tpos, nd, tries);
+  h->d_tries = tries;
+  h->d_roots = roots;
+  regrow(h->heap, h->heap_n, h->heap_n + ubytes + 64, st);
+  const uint64_t hb = h->heap_n;
+  h->ubuf.ensure(((uint64_t)nups + 1) * 8 + 64);
+  uint64_t* uo = (uint64_t*)h->ubuf.p;
+  hipLaunchKernelGGL(k_f_ops_post, GRID(nd * CG, BS), dim3(BS), 0, st, O, (const uint32_t*)S.sidx, (const uint32_t*)ur,
+                     F.up_vals, F.up_voff, (const uint64_t*)uoff, uo, (uint64_t)nups, ubytes, (uint8_t*)h->heap.p, hb,
+                     (const uint32_t*)tflag, (const uint32_t*)tpos, tries);
   LAUNCH_CHECK();
   // ---- 2. descent: opened branches and touched leaves
   recs_reserve(h, h->rn + 16);
@@ -2995,8 +3009,6 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   }
   // ---- 3. elements: upserts (values appended to the heap), untouched children, kept leaves, roots
   const uint64_t ecap = (uint64_t)nups + 16 * ntl + nt + 16;
-  regrow(h->heap, h->heap_n, h->heap_n + ubytes + 64, st);
-  const uint64_t hb = h->heap_n;
   h->ebuf.ensure(
       carve_size({ecap * 32, ecap * 4, ecap, ecap * 32, ecap, ecap * 8, ecap * 4, ecap * 4, ecap, ecap * 32, ecap, 64}));
   Carver ce{(char*)h->ebuf.p, 0, h->ebuf.cap};
@@ -3014,21 +3026,9 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   E.crl = ce.take<uint8_t>(ecap);
   E.n = ce.take<unsigned long long>(8);
   E.cap = ecap;
-  // upsert values: uoff is the exclusive scan of their lengths over the sorted ops;
-  // uo = the same offsets indexed by upsert rank (uo[nups] = total)
-  h->ubuf.ensure(((uint64_t)nups + 1) * 8 + 64);
-  uint64_t* uo = (uint64_t*)h->ubuf.p;
-  hipLaunchKernelGGL(k_f_rank_scatter, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)ur, (const uint64_t*)uoff,
-                     uo, (uint64_t)nups, ubytes);
-  LAUNCH_CHECK();
-  if (ubytes)
-    hipLaunchKernelGGL(k_f_heap_copy, GRID(nd * CG, BS), dim3(BS), 0, st, O, (const uint32_t*)S.sidx,
-                       (const uint32_t*)ur, F.up_vals, F.up_voff, (const uint64_t*)uo, (uint8_t*)h->heap.p, hb);
-  LAUNCH_CHECK();
-  c->h_pinned[8] = nups;  // the record elements are pushed after the upserts
-  HIPCHK(hipMemcpyAsync(E.n, c->h_pinned + 8, 8, hipMemcpyHostToDevice, st));
+  // (the record elements are pushed after the upserts: k_f_upsert_elems sets E.n = nups)
   hipLaunchKernelGGL(k_f_upsert_elems, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)tries, nt,
-                     (const uint32_t*)ur, (const uint64_t*)uo, E, hb);
+                     (const uint32_t*)ur, (const uint64_t*)uo, E, hb, (uint64_t)nups);
   LAUNCH_CHECK();
   if (ntl)
     hipLaunchKernelGGL(k_f_gather, GRID(ntl * 16, BS), dim3(BS), 0, st, map_of(h), recs_of(h),
@@ -3086,14 +3086,12 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
       hipLaunchKernelGGL(k_f_branch_recs, GRID(B, BS), dim3(BS), 0, st, T, (const uint32_t*)(T.ctr + CTR_B),
                          (const uint32_t*)tries, M, R, base_b, sel);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_f_elem_sel, GRID(m, BS), dim3(BS), 0, st, T, E, sel);
-    hipLaunchKernelGGL(k_f_elem_new, GRID(m, BS), dim3(BS), 0, st, T, E, isnew);
-    hipLaunchKernelGGL(k_f_elem_src, GRID(m, BS), dim3(BS), 0, st, T, E, esrc);
+    hipLaunchKernelGGL(k_f_elem_flags, GRID(m, BS), dim3(BS), 0, st, T, E, sel, isnew, esrc);
     LAUNCH_CHECK();
     scan_exclusive<uint32_t>(isnew, nrank, m, tot, sscr, st);
     // old anchors out of the map (touched records, element sources), then touched records die
-    if (ntl) hipLaunchKernelGGL(k_map_delete, GRID(ntl, BS), dim3(BS), 0, st, M, R, (const uint32_t*)tlist, ntl);
-    hipLaunchKernelGGL(k_map_delete, GRID(m, BS), dim3(BS), 0, st, M, R, (const uint32_t*)esrc, m);
+    hipLaunchKernelGGL(k_map_delete, GRID(ntl + m, BS), dim3(BS), 0, st, M, R, (const uint32_t*)tlist, ntl,
+                       (const uint32_t*)esrc, m);
     LAUNCH_CHECK();
     if (ntl)
       hipLaunchKernelGGL(k_rec_dead, GRID(ntl, BS), dim3(BS), 0, st, R, (const uint32_t*)tlist, ntl,
@@ -3108,9 +3106,8 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
       map_rebuild(h, B + m);
     } else {
       unsigned long long* err = fctr + 3;
-      if (B)
-        hipLaunchKernelGGL(k_map_insert, GRID(B, BS), dim3(BS), 0, st, M, R, (const uint32_t*)nullptr, base_b, B, err);
-      hipLaunchKernelGGL(k_map_insert, GRID(m, BS), dim3(BS), 0, st, M, R, (const uint32_t*)eid, (uint64_t)0, m, err);
+      hipLaunchKernelGGL(k_map_insert, GRID(B + m, BS), dim3(BS), 0, st, M, R, base_b, B, (const uint32_t*)eid, m,
+                         err);
       LAUNCH_CHECK();
       h->mused += B + m;
     }
@@ -3118,7 +3115,9 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                        (const uint32_t*)T.res_len, nt, roots);
     LAUNCH_CHECK();
   } else {
-    if (ntl) hipLaunchKernelGGL(k_map_delete, GRID(ntl, BS), dim3(BS), 0, st, M, R, (const uint32_t*)tlist, ntl);
+    if (ntl)
+      hipLaunchKernelGGL(k_map_delete, GRID(ntl, BS), dim3(BS), 0, st, M, R, (const uint32_t*)tlist, ntl,
+                         (const uint32_t*)nullptr, (uint64_t)0);
     if (ntl)
       hipLaunchKernelGGL(k_rec_dead, GRID(ntl, BS), dim3(BS), 0, st, R, (const uint32_t*)tlist, ntl,
                          (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p);
@@ -3142,12 +3141,16 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     h->em_valid = true;
   }
   // ---- roots to the host
+  // (through the pinned staging: a pageable destination pins its pages on every copy)
   h->tries.resize(nt);
   h->roots.resize((uint64_t)nt * 32);
-  HIPCHK(hipMemcpyAsync(h->tries.data(), tries, (uint64_t)nt * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(h->roots.data(), roots, (uint64_t)nt * 32, hipMemcpyDeviceToHost, st));
+  uint8_t* hs = pinned_stage(c, (uint64_t)nt * 36);
+  HIPCHK(hipMemcpyAsync(hs, tries, (uint64_t)nt * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(hs + (uint64_t)nt * 4, roots, (uint64_t)nt * 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_pinned, fctr + 3, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  memcpy(h->tries.data(), hs, (uint64_t)nt * 4);
+  memcpy(h->roots.data(), hs + (uint64_t)nt * 4, (uint64_t)nt * 32);
   if (c->h_pinned[0]) throw KhError{KH_EINTERNAL, "anchor map insert failed"};
   if (!h->forest) memcpy(h->root, nt ? h->roots.data() : h->root, 32);
   float merge_ms = ev_ms(c->ev[6], c->ev[7]);
@@ -4159,16 +4162,12 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     // 2. account.withStateRoot: the new storage roots into the account bodies
     const uint32_t nt = (uint32_t)storage->tries.size();
     if (nt && na_up && d_a_up_trie) {
-      c->ws3.ensure(carve_size({(uint64_t)nt * 4, (uint64_t)nt * 32, 64}));
-      Carver cw{(char*)c->ws3.p, 0, c->ws3.cap};
-      uint32_t* tr = cw.take<uint32_t>(nt);
-      uint64_t* ro = cw.take<uint64_t>((uint64_t)nt * 4);
-      unsigned long long* err = cw.take<unsigned long long>(8);
-      HIPCHK(hipMemcpyAsync(tr, storage->tries.data(), (uint64_t)nt * 4, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(ro, storage->roots.data(), (uint64_t)nt * 32, hipMemcpyHostToDevice, st));
+      // the forest's trie list and roots are still on the device (its commit's tbuf)
+      c->ws3.ensure(64);
+      unsigned long long* err = (unsigned long long*)c->ws3.p;
       HIPCHK(hipMemsetAsync(err, 0, 8, st));
       hipLaunchKernelGGL(k_inject_roots, GRID(na_up, BS), dim3(BS), 0, st, d_a_up_vals, d_a_up_voff, d_a_up_trie,
-                         na_up, (const uint32_t*)tr, nt, (const uint64_t*)ro, err);
+                         na_up, (const uint32_t*)storage->d_tries, nt, (const uint64_t*)storage->d_roots, err);
       LAUNCH_CHECK();
       HIPCHK(hipMemcpyAsync(c->h_pinned, err, 8, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));

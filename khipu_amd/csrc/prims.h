@@ -113,6 +113,104 @@ __global__ void k_scan_total(const T* in_last, const T* out_last, T* total) {
   *total = *in_last + *out_last;
 }
 
+// Small scans (a block commit's op and element counts): one block walks the tiles in order
+// carrying the running sum, one launch instead of the tile / recursive / add / total chain
+// (each launch of that chain costs ~5 us of dispatch at these sizes).  A tile is loaded
+// coalesced (element i * 1024 + thread) and transposed through LDS so that each thread
+// scans SMALL_ITEMS consecutive elements; the next tile's loads are in flight during the
+// current tile's scan.  (Loaded thread-contiguous instead, one CU's vector memory path ran
+// at ~13 us per 8192-element tile: profiles/r3w_block_commit_trace_50m.json.)
+constexpr int SCAN_SMALL_THREADS = 1024;
+constexpr uint64_t SCAN_SMALL_MAX = 32768;
+template <typename T>
+__global__ void __launch_bounds__(SCAN_SMALL_THREADS) k_scan_small(const T* in, T* out, uint64_t n, T* total) {
+  constexpr int IT = sizeof(T) == 8 ? 4 : 8;  // items per thread (LDS: 32 KiB + padding)
+  constexpr uint32_t TILE = SCAN_SMALL_THREADS * IT;
+  __shared__ T buf[TILE + TILE / 32];  // element p at p + p / 32 (the thread-contiguous reads
+                                       // then fall in distinct banks)
+  __shared__ T lw[SCAN_SMALL_THREADS / 64];
+  const uint32_t tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  T carry = 0;
+  T v[IT];
+  auto load = [&](uint64_t t0) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const uint64_t idx = t0 + (uint64_t)i * SCAN_SMALL_THREADS + tid;
+      v[i] = idx < n ? in[idx] : (T)0;
+    }
+  };
+  auto at = [](uint32_t p) { return p + (p >> 5); };
+  load(0);
+  for (uint64_t t0 = 0; t0 < n; t0 += TILE) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) buf[at(i * SCAN_SMALL_THREADS + tid)] = v[i];
+    __syncthreads();
+    if (t0 + TILE < n) load(t0 + TILE);  // (in == out: a later tile's inputs)
+    T cur[IT];
+    T s = 0;
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+      cur[j] = buf[at(tid * IT + j)];
+      s += cur[j];
+    }
+    T x = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      T y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) lw[w] = x;
+    __syncthreads();
+    T wbase = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_SMALL_THREADS / 64; ++i) {
+      const T q = lw[i];
+      if (i < w) wbase += q;
+      tot += q;
+    }
+    T ex = carry + wbase + x - s;
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+      buf[at(tid * IT + j)] = ex;
+      ex += cur[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const uint32_t p = i * SCAN_SMALL_THREADS + tid;
+      if (t0 + p < n) out[t0 + p] = buf[at(p)];
+    }
+    carry += tot;
+    __syncthreads();  // buf and lw are rewritten by the next tile
+  }
+  if (total && tid == 0) *total = carry;
+}
+
+// Mid-size scans (up to SCAN_TWO_MAX_TILES tiles): after k_scan_tiles, each block sums the
+// tile sums before it itself (no recursive scan of the sums) and adds them; the last block
+// writes the total.  Two launches.
+constexpr uint64_t SCAN_TWO_MAX_TILES = 2048;
+template <typename T>
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_add_sums(T* out, uint64_t n, const T* sums, uint32_t tiles,
+                                                                T* total) {
+  __shared__ T lw[SCAN_THREADS / 64];
+  const uint32_t b = blockIdx.x;
+  T s = 0;
+  for (uint32_t t = threadIdx.x; t < b; t += SCAN_THREADS) s += sums[t];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) lw[threadIdx.x >> 6] = s;
+  __syncthreads();
+  T add = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_THREADS / 64; ++i) add += lw[i];
+  const uint64_t base = (uint64_t)b * SCAN_TILE;
+  if (add)
+    for (int i = threadIdx.x; i < SCAN_TILE; i += SCAN_THREADS)
+      if (base + i < n) out[base + i] += add;
+  if (total && b == tiles - 1 && threadIdx.x == 0) *total = add + sums[b];
+}
+
 // Scratch needed by scan_exclusive for n elements (bytes).
 inline size_t scan_scratch_bytes(uint64_t n, size_t elem) {
   size_t b = 0;
@@ -131,10 +229,21 @@ void scan_exclusive(const T* in, T* out, uint64_t n, T* total, void* scratch, hi
     if (total) (void)hipMemsetAsync(total, 0, sizeof(T), st);
     return;
   }
+  if (n <= SCAN_SMALL_MAX) {
+    hipLaunchKernelGGL(k_scan_small<T>, dim3(1), dim3(SCAN_SMALL_THREADS), 0, st, in, out, n, total);
+    return;
+  }
   uint64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
   // the last input element is kept by the tile that reads it (in == out allowed)
   T* sums = (T*)scratch;
   T* last_in = sums + tiles;  // one slot after the tile sums
+  if (tiles <= SCAN_TWO_MAX_TILES) {
+    hipLaunchKernelGGL(k_scan_tiles<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, in, out, n, sums,
+                       (T*)nullptr);
+    hipLaunchKernelGGL(k_scan_add_sums<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, out, n, (const T*)sums,
+                       (uint32_t)tiles, total);
+    return;
+  }
   hipLaunchKernelGGL(k_scan_tiles<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, in, out, n, sums,
                      total ? last_in : (T*)nullptr);
   if (tiles > 1) {
@@ -161,6 +270,7 @@ constexpr int RS_ITEMS = KHST_RS_ITEMS;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 keys: 36 KiB of LDS staging (32-bit keys)
 constexpr int RS_WAVES = RS_THREADS / 64;
 constexpr int RS_WSLICE = RS_TILE / RS_WAVES;   // 512 keys per wave
+constexpr uint32_t RS_FUSE_TILES = 64;          // radix_sort_pairs: scan-free passes up to 256k keys
 
 template <typename K>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const K* keys, uint64_t n, int shift, uint32_t* counts,
@@ -191,7 +301,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const K* keys, uint64_t 
 template <typename K>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const uint32_t* vals, K* okeys,
                                                            uint32_t* ovals, uint64_t n, int shift,
-                                                           const uint32_t* offs, uint32_t ntiles) {
+                                                           const uint32_t* offs, uint32_t ntiles, bool fused) {
   __shared__ uint32_t wc[RS_WAVES][256];
   __shared__ uint32_t tstart[256], gbase[256];
   __shared__ uint32_t lw[RS_THREADS / 64];
@@ -240,7 +350,18 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const 
     }
     uint32_t tot;
     tstart[d] = block_exclusive_scan<uint32_t>(run, lw, &tot);
-    gbase[d] = offs[(uint64_t)d * ntiles + blockIdx.x];
+    if (fused) {  // offs holds the raw tile counts: the digit's total and this tile's share before it
+      uint32_t all = 0, pre = 0;
+      const uint32_t* cd = offs + (uint64_t)d * ntiles;
+      for (uint32_t t = 0; t < ntiles; ++t) {
+        const uint32_t q = cd[t];
+        all += q;
+        pre += t < blockIdx.x ? q : 0u;
+      }
+      gbase[d] = block_exclusive_scan<uint32_t>(all, lw, &tot) + pre;
+    } else {
+      gbase[d] = offs[(uint64_t)d * ntiles + blockIdx.x];
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -281,15 +402,18 @@ inline bool radix_sort_pairs(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t 
   uint32_t* counts = (uint32_t*)scratch;
   void* scan_ws = (char*)scratch + (((uint64_t)tiles * 256 * sizeof(uint32_t) + 255) / 256) * 256;
   bool flip = false;
+  // up to RS_FUSE_TILES tiles (small sorts: a block commit's ops and elements) the scatter
+  // computes its digit bases from the raw counts itself: 2 launches a pass instead of 3-5
+  const bool fused = tiles <= RS_FUSE_TILES;
   for (int sh = lo_bit; sh < hi_bit; sh += 8) {
     K* ik = flip ? k1 : k0;
     uint32_t* iv = flip ? v1 : v0;
     K* ok = flip ? k0 : k1;
     uint32_t* ov = flip ? v0 : v1;
     hipLaunchKernelGGL(k_rs_hist<K>, dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik, n, sh, counts, tiles);
-    scan_exclusive<uint32_t>(counts, counts, (uint64_t)tiles * 256, (uint32_t*)nullptr, scan_ws, st);
+    if (!fused) scan_exclusive<uint32_t>(counts, counts, (uint64_t)tiles * 256, (uint32_t*)nullptr, scan_ws, st);
     hipLaunchKernelGGL(k_rs_scatter<K>, dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik, (const uint32_t*)iv, ok,
-                       ov, n, sh, (const uint32_t*)counts, tiles);
+                       ov, n, sh, (const uint32_t*)counts, tiles, fused);
     flip = !flip;
   }
   return flip;

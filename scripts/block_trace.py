@@ -16,6 +16,7 @@ def main():
     p.add_argument("dir")
     p.add_argument("--blocks", type=int, default=3)
     p.add_argument("--gap", type=float, default=30.0)
+    p.add_argument("--timeline", default=None, help="write the last window's launches to this JSON file")
     a = p.parse_args()
     rows = []
     for f in glob.glob(f"{a.dir}/**/*kernel_trace.csv", recursive=True):
@@ -42,6 +43,16 @@ def main():
         out.append({"launches": len(w), "kernel_ms": round(busy, 3), "span_ms": round(span, 3),
                     "idle_in_span_ms": round(span - busy, 3),
                     "top": {k: {"n": v[0], "ms": round(v[1], 3)} for k, v in top}})
+    if a.timeline and wins:  # the last window launch by launch: start offset, duration, gap before
+        w = wins[-1]
+        t0, prev = w[0][0], w[0][0]
+        tl = []
+        for e in w:
+            k = e[2].replace("void ", "").replace("khst::", "").split("<")[0][:40]
+            tl.append([k, round((e[0] - t0) / 1e3, 1), round((e[1] - e[0]) / 1e3, 1), round((e[0] - prev) / 1e3, 1)])
+            prev = max(prev, e[1])
+        with open(a.timeline, "w") as f:
+            json.dump({"columns": ["kernel", "start_us", "dur_us", "gap_before_us"], "launches": tl}, f)
     print(json.dumps(out, indent=1))
 
 
