@@ -24,6 +24,7 @@
 
 #include "../../include/khst.h"
 #include "keccak.h"
+#include "keccak_xlane.h"
 #include "prims.h"
 #include "synth.h"
 #include "trie_ops.h"
@@ -829,6 +830,61 @@ __global__ void __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(4, 8)))
   }
 }
 
+// Small levels (a block commit's dirty paths, the few branches at the top of a full build):
+// latency-bound, a wave or less per CU.  op_branch_stream prefetches one child record
+// ahead, so a full branch waits for 16 HBM round trips in a row.  Here every child record
+// of the branch is loaded at once (16 x 32 B in flight per thread) and copied to LDS
+// (lane-interleaved, conflict-free), and the stream reads it from there.  One wave per
+// block; the VGPR budget is free at this occupancy.
+constexpr uint32_t SMALL_LEVEL = 32768;  // branches per level below which k_branch_small runs
+__global__ void __launch_bounds__(64) k_branch_small(Topo T, uint64_t first, uint64_t cnt) {
+  constexpr uint32_t WB = 64;
+  __shared__ uint64_t slots[WB * LEAF_WORDS];
+  __shared__ uint64_t crs[64 * WB];
+  __shared__ uint16_t cms[16 * WB];
+  const uint64_t t = (uint64_t)blockIdx.x * WB + threadIdx.x;
+  unsigned long long perms = 0, hashes = 0, inl = 0;
+  if (t < cnt) {
+    const uint32_t j = (uint32_t)(first + t), tid = threadIdx.x;
+    const uint32_t k = T.br_k[j];
+    const uint64_t cb = T.br_cbase[j];
+    uint64_t r[64];
+    uint32_t mm[16];
+#pragma unroll
+    for (uint32_t c = 0; c < 16; ++c) {
+      if (c < k) {
+        const ulonglong2* p = (const ulonglong2*)(T.cref + 4 * (cb + c));
+        const ulonglong2 a = p[0], b = p[1];
+        r[4 * c] = a.x;
+        r[4 * c + 1] = a.y;
+        r[4 * c + 2] = b.x;
+        r[4 * c + 3] = b.y;
+        mm[c] = T.cmeta[cb + c];
+      }
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < 16; ++c) {
+      if (c < k) {
+        cms[c * WB + tid] = (uint16_t)mm[c];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) crs[(4 * c + q) * WB + tid] = r[4 * c + q];
+      }
+    }
+    uint32_t in1 = 0;
+    perms = op_branch_stream(T, j, slots + tid * LEAF_WORDS, 1, &in1, ChildSrc{cms + tid, crs + tid, WB});
+    hashes = branch_hash_count(T, j, (uint32_t)perms);
+    inl = in1;
+  }
+  perms = wave_sum(perms);
+  hashes = wave_sum(hashes);
+  inl = wave_sum(inl);
+  if (threadIdx.x == 0) {
+    if (perms) atomicAdd(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms);
+    if (hashes) atomicAdd(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes);
+    if (inl) atomicAdd(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
+  }
+}
+
 // LDS ordering between lanes of ONE wave (the wave's LDS operations execute in
 // order; the fences stop the compiler from moving them across): no block barrier
 __device__ __forceinline__ void wave_lds_sync() {
@@ -845,6 +901,123 @@ __device__ __forceinline__ uint32_t row16_scan(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
   return x;
+}
+
+// The smallest levels (the top of a block commit's tries: 1, 16, 256, 4096 branches):
+// 32 lanes per branch, two branches per wave.  Lane c < 16 loads child record c (one round
+// trip for all 16), the item offsets are a DPP prefix sum over the group's first row, the
+// items are XOR-placed (ds_xor) into the group's 0x80-prefilled encoding in LDS, and the
+// permutation runs spread over the group (keccak_xlane.h): ~3x shorter than one thread's
+// permutation, which at this occupancy is the level's latency.  Lane 0 of the group then
+// keeps and publishes the reference as op_branch_stream does.
+constexpr uint32_t XL_LEVEL = 8192;  // branches per level below which k_branch_xl runs
+constexpr uint32_t XL_ENC_WORDS = 68;  // 4 windows: a branch of fixed-length keys is <= 532 B
+__global__ void __launch_bounds__(64) k_branch_xl(Topo T, uint64_t first, uint64_t cnt) {
+  __shared__ uint64_t enc[2][XL_ENC_WORDS];
+  __shared__ uint64_t kb[2][64];
+  const uint32_t g = threadIdx.x >> 5, sub = threadIdx.x & 31, gbase = threadIdx.x & 32u;
+  const uint64_t t = (uint64_t)blockIdx.x * 2 + g;
+  if (t >= cnt) return;  // the whole group (no cross-group operations below)
+  const uint32_t j = (uint32_t)(first + t);
+  uint64_t* E = enc[g];
+  const uint32_t k = T.br_k[j];
+  const uint64_t cb = T.br_cbase[j];
+  const uint32_t ext = T.br_ext[j];
+  const bool top = T.br_parent[j] == NONE;
+  uint32_t len = 0, nib = 0;
+  uint64_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  if (sub < k) {
+    const uint32_t mc = T.cmeta[cb + sub];
+    len = mc & 0xFF;
+    nib = (mc >> 8) & 0xF;
+    const ulonglong2* p = (const ulonglong2*)(T.cref + 4 * (cb + sub));
+    const ulonglong2 a = p[0], b = p[1];
+    r0 = a.x, r1 = a.y, r2 = b.x, r3 = b.y;
+  }
+  const uint32_t ilen = len == 32 ? 33 : len;
+  const uint32_t incl = row16_scan(ilen ? ilen - 1 : 0);  // lanes 0..15 of the group: one DPP row
+  const uint32_t sum = (uint32_t)__shfl((int)incl, (int)(gbase + 15));
+  const uint32_t payload = 17 + sum;  // 16 - k empty slots + the terminator + sum of item lengths
+  const uint32_t hh = rlp_hdr_len(payload), L = hh + payload;
+  const bool hashit = L >= 32 || (top && ext == 0);
+  const uint32_t nfull = L / 136;
+  // 0x80 over the encoding's bytes, zero past them
+  for (uint32_t w = sub; w < XL_ENC_WORDS; w += 32) {
+    const uint32_t a = 8 * w, n80 = L > a ? (L - a < 8 ? L - a : 8) : 0;
+    E[w] = low_bytes_mask(n80) & 0x8080808080808080ULL;
+  }
+  xl_sync();
+  if (sub == 0) {  // the list header
+    const uint64_t hdr = hh == 1 ? (0xC0 + payload)
+                         : hh == 2 ? (0xF8 | ((uint64_t)payload << 8))
+                                   : (0xF9 | ((uint64_t)(payload >> 8) << 8) | ((uint64_t)(payload & 0xFF) << 16));
+    atomicXor((unsigned long long*)E, (unsigned long long)((hdr ^ 0x8080808080808080ULL) & low_bytes_mask(hh)));
+  }
+  if (ilen) {  // child sub's item (0xa0 + hash, or the embedded encoding) at its offset
+    const uint32_t off = hh + nib + incl - (ilen - 1);
+    uint64_t I[5];
+    if (len == 32) {
+      I[0] = 0xA0 | (r0 << 8);
+      I[1] = (r0 >> 56) | (r1 << 8);
+      I[2] = (r1 >> 56) | (r2 << 8);
+      I[3] = (r2 >> 56) | (r3 << 8);
+      I[4] = r3 >> 56;
+    } else {
+      I[0] = r0, I[1] = r1, I[2] = r2, I[3] = r3, I[4] = 0;
+    }
+    const uint32_t sh = off & 7, wfirst = off >> 3;
+#pragma unroll
+    for (uint32_t q = 0; q < 6; ++q) {
+      const uint64_t cur = q < 5 ? I[q] : 0, prv = q ? I[q - 1] : 0;
+      const uint64_t y = sh ? (cur << (8 * sh)) | (prv >> (64 - 8 * sh)) : cur;
+      const uint32_t W = wfirst + q;
+      const int32_t lo = (int32_t)off - 8 * (int32_t)W, hi = (int32_t)(off + ilen) - 8 * (int32_t)W;
+      const uint32_t blo = lo > 0 ? (uint32_t)lo : 0, bhi = hi < 8 ? (hi > 0 ? (uint32_t)hi : 0) : 8;
+      if (bhi <= blo) continue;
+      const uint64_t m = low_bytes_mask(bhi) & ~low_bytes_mask(blo);
+      atomicXor((unsigned long long*)(E + W), (unsigned long long)((y ^ 0x8080808080808080ULL) & m));
+    }
+  }
+  xl_sync();
+  // absorb + permute, spread over the group; the padding is added at absorb time so the
+  // encoding stays intact in LDS (the inline reference of a short node)
+  uint32_t lo = 0, hi = 0;
+  if (hashit) {
+    const XLane X = xlane_setup(sub);
+    const uint32_t rem = L - 136 * nfull;
+    for (uint32_t b = 0; b <= nfull; ++b) {
+      if (sub < 17) {
+        uint64_t w = E[17 * b + sub];
+        if (b == nfull) {
+          if ((rem >> 3) == sub) w ^= 0x01ULL << (8 * (rem & 7));
+          if (sub == 16) w ^= 0x80ULL << 56;
+        }
+        lo ^= (uint32_t)w;
+        hi ^= (uint32_t)(w >> 32);
+      }
+      keccakf_xlane(lo, hi, kb[g], X);
+    }
+  }
+  uint64_t hb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t l = (uint32_t)__shfl((int)lo, (int)(gbase + q)), h = (uint32_t)__shfl((int)hi, (int)(gbase + q));
+    hb[q] = hashit ? ((uint64_t)h << 32) | l : 0;
+  }
+  if (sub != 0) return;
+  T.br_len[j] = L;
+  uint64_t bhead[4] = {0, 0, 0, 0};
+  if (L < 32)
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t base = 8u * (uint32_t)q;
+      bhead[q] = base < L ? E[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0;
+    }
+  uint32_t ninl = hashit ? 0 : 1;
+  branch_keep(T, j, L, hb, bhead);
+  const uint32_t perms = (hashit ? nfull + 1 : 0) + branch_publish(T, j, L, hb, bhead, Slot{E, 1}, &ninl);
+  atomicAdd(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), (unsigned long long)perms);
+  atomicAdd(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), (unsigned long long)branch_hash_count(T, j, perms));
+  if (ninl) atomicAdd(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), (unsigned long long)ninl);
 }
 
 // Wave-cooperative variant of k_branch_fused (row N1, measured against it: see
@@ -1308,6 +1481,11 @@ static size_t carve_size(const std::vector<size_t>& items) {
   return s + 256;
 }
 
+struct BuildInfo {  // the last build's sizes, for build_stats
+  uint64_t n = 0, m = 0, B = 0, key_perms = 0, arena = 0;
+  uint32_t levels = 0;
+  bool full_sort = false, early = false;
+};
 struct kh_ctx {
   int dev = 0;
   int n_cu = 256;  // compute units of the device
@@ -1325,6 +1503,7 @@ struct kh_ctx {
   Topo T{};
   uint64_t last_B = 0;
   uint64_t last_nres = 0;
+  BuildInfo binfo;
 };
 
 // ---------------------------------------------------------------------------
@@ -1345,6 +1524,7 @@ struct BuildArgs {
   const uint8_t* kn = nullptr;     // variable-length keys (zero-padded to 32 B): nibble counts (list tries)
   struct ElemArgs* el = nullptr;   // element build of a resident forest commit (forest.h; nullable)
   hipEvent_t vals_ready = nullptr; // the values / offsets land later (multi-GPU exchange): wait before reading them
+  bool dev_results = false;        // results and counters stay on the device (no host sync at the end)
 };
 // element build (forest.h): inputs are leaves and subtree elements; the capped reference
 // of every element node, branch and extension is kept for the forest's records
@@ -1586,6 +1766,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
   S.fallback = fallback;
 }
 
+static void build_stats(kh_ctx* c, const unsigned long long* hc, kh_stats* stats);
 static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats) {
   hipStream_t st = c->st;
   const uint64_t n = A.n;
@@ -1976,21 +2157,21 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     hipLaunchKernelGGL(k_leaf_topo, GRID(m, BS), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
   }
-  // one host sync for every size the second workspace needs
-  HIPCHK(hipMemcpyAsync(c->h_pinned + 5, ctr + CTR_LONGB, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(c->h_pinned, ctr + CTR_B, 8 * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(c->h_pinned + 4, ctr + CTR_ERR, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(c->h_pinned + 6, ctr + CTR_FIXN, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(c->h_pinned + 7, ctr + CTR_LONGN, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(c->h_pinned + 8, lb, 65 * 4, hipMemcpyDeviceToHost, st));
+  // one host sync for every size the second workspace needs: the counters, the depth
+  // histogram and the level bounds are carved back to back, one copy
+  const size_t tcopy = (size_t)((char*)(lb + 65) - (char*)ctr);
+  if (tcopy > 16384) throw KhError{KH_EINTERNAL, "counter block exceeds the pinned staging"};
+  HIPCHK(hipMemcpyAsync(c->h_pinned, ctr, tcopy, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  const uint64_t B = (uint32_t)c->h_pinned[0];
-  const uint64_t lf_bytes = early ? c->h_pinned[5] : c->h_pinned[2];
-  const uint64_t C = (uint32_t)c->h_pinned[3];
-  if (c->h_pinned[4]) throw KhError{KH_EINTERNAL, "topology invariant violated (group chain > 15)"};
+  const unsigned long long* hc = c->h_pinned;
+  const uint64_t B = (uint32_t)hc[CTR_B];
+  const uint64_t lf_bytes = early ? hc[CTR_LONGB] : hc[CTR_B + 2];
+  const uint64_t C = (uint32_t)hc[CTR_B + 3];
+  if (hc[CTR_ERR]) throw KhError{KH_EINTERNAL, "topology invariant violated (group chain > 15)"};
   std::vector<uint32_t> lbh(65, 0);
-  memcpy(lbh.data(), c->h_pinned + 8, 65 * 4);
+  memcpy(lbh.data(), (const char*)hc + ((char*)lb - (char*)ctr), 65 * 4);
   if (nb == 0) std::fill(lbh.begin(), lbh.end(), 0u);
+  const uint64_t nfix = links ? hc[CTR_FIXN] : 0, nlong = links ? hc[CTR_LONGN] : 0;
 
   // ---- phase-2 workspace: child records + node arena
   // leaf encodings are kept (transposed message slots) for the write-back, element and
@@ -1998,7 +2179,6 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   const bool lmsgs = A.emit || A.kn || A.el;
   const uint64_t lmsg_words = lmsgs ? (uint64_t)LEAF_WORDS * m : 0;
   const uint64_t bmsg_words = A.emit ? (uint64_t)BR_WORDS * B : 0, xmsg_words = A.emit ? (uint64_t)EXT_WORDS * B : 0;
-  const uint64_t nfix = links ? c->h_pinned[6] : 0, nlong = links ? c->h_pinned[7] : 0;
   if (links && C > cbound) throw KhError{KH_EINTERNAL, "child records exceed their bound"};
   c->ws2.ensure(carve_size({links ? 0 : C * 32, links ? 0 : C * 2, lmsg_words * 8, lf_bytes + 64, bmsg_words * 8,
                             xmsg_words * 8}));
@@ -2081,6 +2261,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // N1 variant: one thread per branch assembling its own window (default) or the
   // wave-cooperative DPP assembly (KHST_BRANCH=coop; DESIGN.md §5 has the measurement)
   static const bool branch_bs64 = getenv("KHST_BRANCH_BS") && atoi(getenv("KHST_BRANCH_BS")) == 64;
+  // levels of at most XL_LEVEL branches: k_branch_xl (32 lanes per branch, the permutation
+  // spread over them); of at most SMALL_LEVEL: k_branch_small (every child record loaded at
+  // once); KHST_BRANCH_SMALL=0 (measurement switch) keeps them all on k_branch_fused
+  static const bool small_levels = !getenv("KHST_BRANCH_SMALL") || atoi(getenv("KHST_BRANCH_SMALL")) != 0;
   bool moved = move_d == 0;
   for (int d = 63; d >= 0; --d) {
     uint32_t cnt = lbh[d + 1] - lbh[d];
@@ -2100,6 +2284,12 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
         hipLaunchKernelGGL(k_branch_fused<0>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
       else if (rescan)
         hipLaunchKernelGGL(k_branch_fused<1>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+      else if (small_levels && !T.links && cnt <= XL_LEVEL)
+        hipLaunchKernelGGL(k_branch_xl, dim3((unsigned)((cnt + 1) / 2)), dim3(64), 0, st, T, (uint64_t)lbh[d],
+                           (uint64_t)cnt);
+      else if (small_levels && cnt <= SMALL_LEVEL)
+        hipLaunchKernelGGL(k_branch_small, dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, T, (uint64_t)lbh[d],
+                           (uint64_t)cnt);
       else if (branch_bs64)
         hipLaunchKernelGGL((k_branch_fused<2, 64>), dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, T,
                            (uint64_t)lbh[d], (uint64_t)cnt);
@@ -2113,47 +2303,67 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   HIPCHK(hipEventRecord(c->ev[5], st));
 
   // ---- results
-  // through pinned staging: device-to-host copies into pageable memory pin its pages on
-  // every call (measured: 20-30 ms per build for 100k roots, scripts/storage_wall_probe.py)
-  pinned_stage(c, nres * (32 + 4 + 32));
-  HIPCHK(hipMemcpyAsync(c->h_res, T.res_hash, nres * 32, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(c->h_res + nres * 32, T.res_len, nres * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(c->h_res + nres * 36, T.res_inl, nres * 32, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(c->h_pinned, ctr, CTR_N * CTR_SHARDS * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  memcpy(O.res_hash.data(), c->h_res, nres * 32);
-  memcpy(O.res_len.data(), c->h_res + nres * 32, nres * 4);
-  memcpy(O.res_inl.data(), c->h_res + nres * 36, nres * 32);
-  if (c->h_pinned[CTR_ERR]) throw KhError{KH_EINTERNAL, "build: device invariant violated"};
   c->T = T;
   c->last_B = B;
   c->last_nres = nres;
-  if (stats) {
-    stats->n_leaves = m;
-    stats->n_branches = B;
-    auto stat = [&](int idx) {
-      unsigned long long t = 0;
-      for (int r = 0; r < CTR_SHARDS; ++r) t += c->h_pinned[r * CTR_N + idx];
-      return t;
-    };
-    stats->n_node_hashes = stat(CTR_HASHES);
-    stats->n_node_perms = stat(CTR_PERMS);
-    stats->n_inline = stat(CTR_INLINE);
-    stats->n_extensions = stat(CTR_EXT);
-    stats->n_key_perms = (A.flags & KH_HASH_KEYS) ? n * (uint64_t)(A.klen / 136 + 1) : 0;
-    stats->arena_bytes = lmsg_words * 8 + lf_bytes + (bmsg_words + xmsg_words) * 8;  // node RLP kept in HBM
-    stats->n_levels = levels;
-    stats->full_sort = ties ? 1 : 0;
-    // split builds: until both halves are hashed (the second half overlaps the first sort)
-    stats->t_keys_ms = ev_ms(c->ev[0], c->ev[1]);
-    stats->t_sort_ms = ev_ms(c->ev[1], c->ev[2]);
-    stats->t_topo_ms = ev_ms(c->ev[2], c->ev[3]);
-    // early: the leaf kernel's own span on st2, where it overlaps the topology (the
-    // publish of its references runs on st after both; t_total_ms holds it)
-    stats->t_leaf_ms = early ? ev_ms(c->ev[9], c->ev[10]) : ev_ms(c->ev[3], c->ev[4]);
-    stats->t_branch_ms = ev_ms(c->ev[4], c->ev[5]);
-    stats->t_total_ms = ev_ms(c->ev[0], c->ev[5]);
-  }
+  BuildInfo& bi = c->binfo;
+  bi.n = n;
+  bi.m = m;
+  bi.B = B;
+  bi.key_perms = (A.flags & KH_HASH_KEYS) ? n * (uint64_t)(A.klen / 136 + 1) : 0;
+  bi.arena = lmsg_words * 8 + lf_bytes + (bmsg_words + xmsg_words) * 8;  // node RLP kept in HBM
+  bi.levels = levels;
+  bi.full_sort = ties;
+  bi.early = early;
+  // A.dev_results (a forest's element build): the results stay on the device and the caller
+  // reads the counters at its own next sync (build_stats) -- one host round trip less
+  if (A.dev_results) return;
+  // through pinned staging: device-to-host copies into pageable memory pin its pages on
+  // every call (measured: 20-30 ms per build for 100k roots, scripts/storage_wall_probe.py).
+  // The results and the counters are carved back to back: one copy.
+  const size_t o_len = (size_t)((char*)T.res_len - (char*)T.res_hash);
+  const size_t o_inl = (size_t)((char*)T.res_inl - (char*)T.res_hash);
+  const size_t o_ctr = (size_t)((char*)ctr - (char*)T.res_hash);
+  uint8_t* hr = pinned_stage(c, o_ctr + CTR_N * CTR_SHARDS * 8);
+  HIPCHK(hipMemcpyAsync(hr, T.res_hash, o_ctr + CTR_N * CTR_SHARDS * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  memcpy(O.res_hash.data(), hr, nres * 32);
+  memcpy(O.res_len.data(), hr + o_len, nres * 4);
+  memcpy(O.res_inl.data(), hr + o_inl, nres * 32);
+  build_stats(c, (const unsigned long long*)(hr + o_ctr), stats);
+}
+
+// The counters of the last build (host copy hc of T.ctr) -> kh_stats; throws on a device
+// invariant flag.  Call once the build's stream work has completed (its events are read).
+static void build_stats(kh_ctx* c, const unsigned long long* hc, kh_stats* stats) {
+  if (hc[CTR_ERR]) throw KhError{KH_EINTERNAL, "build: device invariant violated"};
+  if (!stats) return;
+  const BuildInfo& bi = c->binfo;
+  stats->n_inputs = bi.n;
+  stats->n_leaves = bi.m;
+  stats->n_branches = bi.B;
+  auto stat = [&](int idx) {
+    unsigned long long t = 0;
+    for (int r = 0; r < CTR_SHARDS; ++r) t += hc[r * CTR_N + idx];
+    return t;
+  };
+  stats->n_node_hashes = stat(CTR_HASHES);
+  stats->n_node_perms = stat(CTR_PERMS);
+  stats->n_inline = stat(CTR_INLINE);
+  stats->n_extensions = stat(CTR_EXT);
+  stats->n_key_perms = bi.key_perms;
+  stats->arena_bytes = bi.arena;
+  stats->n_levels = bi.levels;
+  stats->full_sort = bi.full_sort ? 1 : 0;
+  // split builds: until both halves are hashed (the second half overlaps the first sort)
+  stats->t_keys_ms = ev_ms(c->ev[0], c->ev[1]);
+  stats->t_sort_ms = ev_ms(c->ev[1], c->ev[2]);
+  stats->t_topo_ms = ev_ms(c->ev[2], c->ev[3]);
+  // early: the leaf kernel's own span on st2, where it overlaps the topology (the
+  // publish of its references runs on st after both; t_total_ms holds it)
+  stats->t_leaf_ms = bi.early ? ev_ms(c->ev[9], c->ev[10]) : ev_ms(c->ev[3], c->ev[4]);
+  stats->t_branch_ms = ev_ms(c->ev[4], c->ev[5]);
+  stats->t_total_ms = ev_ms(c->ev[0], c->ev[5]);
 }
 
 // ---------------------------------------------------------------------------
@@ -2375,6 +2585,20 @@ __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32
 }
 
 // upsert op o (its rank among the batch's upserts = ur[o]) -> leaf element; value into the heap
+// a commit's inputs staged as one batch: 32-byte keys (copy_keys) and trie ids (when given)
+__global__ void __launch_bounds__(BS) k_f_inputs(const uint64_t* up_keys, uint64_t nup, const uint64_t* del_keys,
+                                                 uint64_t ndel, bool copy_keys, const uint32_t* up_trie,
+                                                 const uint32_t* del_trie, uint64_t* K, uint32_t* Tid) {
+  const uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o >= nup + ndel) return;
+  const bool up = o < nup;
+  const uint64_t q = up ? o : o - nup;
+  if (copy_keys) {
+    const uint64_t* src = (up ? up_keys : del_keys) + 4 * q;
+    for (int w = 0; w < 4; ++w) K[4 * o + w] = src[w];
+  }
+  if (up_trie || del_trie) Tid[o] = up ? up_trie[q] : del_trie[q];
+}
 __global__ void __launch_bounds__(BS) k_f_upsert_elems(FOps O, const uint32_t* tries, uint32_t nt, const uint32_t* ur,
                                                        const uint64_t* uoff, Elems E, uint64_t heap_base,
                                                        uint64_t nups) {
@@ -2434,36 +2658,41 @@ __global__ void __launch_bounds__(BS) k_f_prep(const uint32_t* sidx, uint64_t n,
   ulen[o] = up ? voff[s + 1] - voff[s] : 0;
 }
 __global__ void __launch_bounds__(BS) k_f_gather(AMap M, Recs R, const uint32_t* touched, const uint8_t* replaced,
-                                                 const uint32_t* tlist, uint64_t ntl, const uint32_t* tries,
-                                                 uint32_t nt, Elems E, unsigned long long* ctr) {
+                                                 const uint32_t* tlist, const unsigned long long* ntl_p,
+                                                 const uint32_t* tries, uint32_t nt, Elems E, unsigned long long* ctr) {
   // one thread per (touched record, child nibble v): the 16 child lookups of an opened
   // branch are independent map probes (dependent HBM round trips), so they run in 16
-  // threads instead of one thread's sequence (block-commit trace: 0.29 ms per launch)
-  const uint64_t g = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  const uint64_t i = g >> 4;
-  const uint32_t v = (uint32_t)(g & 15);
-  bool want = false;
-  uint32_t er = NONE, seg = 0;
-  if (i < ntl) {
-    // touched is u32 here; forest.h's gather reads it as a flag
-    const uint32_t r = tlist[i];
-    if (R.rlive[r] == REC_LIVE) {
-      const uint32_t t = R.rt[r], db = R.rdb[r];
-      seg = seg_of(tries, nt, t);
-      if (db == EL_LEAF) {
-        want = v == 0 && !replaced[r];
-        er = r;
-      } else if ((R.rmask[r] >> v) & 1) {
-        uint64_t ck[4] = {R.rk[4ull * r], R.rk[4ull * r + 1], R.rk[4ull * r + 2], R.rk[4ull * r + 3]};
-        set_nibble(ck, db, v);
-        er = map_find(M, R, t, db + 1, ck);
-        if (er == NONE) ctr[2] = 4;
-        want = er != NONE && !touched[er];
+  // threads instead of one thread's sequence.  The touched count is read on the device
+  // (the descent's counter): a grid-stride loop, no host round trip between the descent
+  // and the gather.  Whole blocks iterate together, so every lane reaches the claim.
+  const uint64_t ntl = *ntl_p;
+  for (uint64_t g0 = (uint64_t)blockIdx.x * BS; g0 < ntl * 16; g0 += (uint64_t)gridDim.x * BS) {
+    const uint64_t g = g0 + threadIdx.x;
+    const uint64_t i = g >> 4;
+    const uint32_t v = (uint32_t)(g & 15);
+    bool want = false;
+    uint32_t er = NONE, seg = 0;
+    if (i < ntl) {
+      // touched is u32 here; forest.h's gather reads it as a flag
+      const uint32_t r = tlist[i];
+      if (R.rlive[r] == REC_LIVE) {
+        const uint32_t t = R.rt[r], db = R.rdb[r];
+        seg = seg_of(tries, nt, t);
+        if (db == EL_LEAF) {
+          want = v == 0 && !replaced[r];
+          er = r;
+        } else if ((R.rmask[r] >> v) & 1) {
+          uint64_t ck[4] = {R.rk[4ull * r], R.rk[4ull * r + 1], R.rk[4ull * r + 2], R.rk[4ull * r + 3]};
+          set_nibble(ck, db, v);
+          er = map_find(M, R, t, db + 1, ck);
+          if (er == NONE) ctr[2] = 4;
+          want = er != NONE && !touched[er];
+        }
       }
     }
+    const uint64_t e = wave_claim(E.n, want);  // every lane of the wave reaches the claim
+    if (want) elem_fill(R, er, seg, E, e);
   }
-  const uint64_t e = wave_claim(E.n, want);  // every lane of the wave reaches the claim
-  if (want) elem_fill(R, er, seg, E, e);
 }
 __global__ void k_f_gather_roots(AMap M, Recs R, const uint32_t* touched, const uint32_t* tries, uint32_t nt, Elems E) {
   uint64_t s = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -2643,6 +2872,7 @@ struct kh_trie {
   DevBuf gbuf;                                // batched get: keys, records, lengths, scan scratch
   uint64_t em_n = 0, em_bytes = 0;
   bool em_valid = false;
+  uint64_t ntl_hint = 0;  // touched records of the last commit (sizes the next element buffer)
   std::vector<uint32_t> tries;  // last commit: touched tries and their roots
   std::vector<uint8_t> roots;
   uint32_t* d_tries = nullptr;  // ... the same on the device (in tbuf; the block commit's injection reads them)
@@ -2931,19 +3161,20 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
         hipLaunchKernelGGL(k_hash_keys<false>, GRID(F.ndel, BS), dim3(BS), 0, st, F.del_keys, F.klen, F.ndel, K + 4 * F.nup);
     }
     LAUNCH_CHECK();
-  } else {
+  }
+  if (segd && ((F.nup && !F.up_trie) || (F.ndel && !F.del_trie))) throw KhError{KH_EINVAL, "forest ops need trie ids"};
+  // the op keys (unless hashed above) and trie ids, upserts then deletes: one launch
+  bool copy_keys = !(h->flags & KH_HASH_KEYS);
+  if (copy_keys && (((uintptr_t)F.up_keys | (uintptr_t)F.del_keys) & 7)) {  // unaligned caller keys: copies
     if (F.nup) HIPCHK(hipMemcpyAsync(K, F.up_keys, F.nup * 32, hipMemcpyDeviceToDevice, st));
     if (F.ndel) HIPCHK(hipMemcpyAsync(K + 4 * F.nup, F.del_keys, F.ndel * 32, hipMemcpyDeviceToDevice, st));
+    copy_keys = false;
   }
-  if (segd) {
-    if (F.nup) {
-      if (!F.up_trie) throw KhError{KH_EINVAL, "forest ops need trie ids"};
-      HIPCHK(hipMemcpyAsync(Tid, F.up_trie, F.nup * 4, hipMemcpyDeviceToDevice, st));
-    }
-    if (F.ndel) {
-      if (!F.del_trie) throw KhError{KH_EINVAL, "forest ops need trie ids"};
-      HIPCHK(hipMemcpyAsync(Tid + F.nup, F.del_trie, F.ndel * 4, hipMemcpyDeviceToDevice, st));
-    }
+  if (copy_keys || segd) {
+    hipLaunchKernelGGL(k_f_inputs, GRID(nops, BS), dim3(BS), 0, st, (const uint64_t*)F.up_keys, F.nup,
+                       (const uint64_t*)F.del_keys, F.ndel, copy_keys, segd ? F.up_trie : nullptr,
+                       segd ? F.del_trie : nullptr, K, Tid);
+    LAUNCH_CHECK();
   }
   sort_dedup(c, S);
   const uint64_t nd = S.m;
@@ -2991,10 +3222,54 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   hipLaunchKernelGGL(k_f_descend, GRID(nd, BS), dim3(BS), 0, st, O, map_of(h), recs_of(h), (uint32_t*)h->touched.p,
                      (uint8_t*)h->replaced.p, tlist, fctr);
   LAUNCH_CHECK();
-  HIPCHK(hipMemcpyAsync(c->h_pinned, fctr, 32, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  // ---- 3. elements: upserts (values in the heap already), untouched children, kept leaves,
+  // roots.  No host round trip after the descent: the element capacity is sized from the
+  // last commit's touched count (or 4 per op), and a short buffer is grown to the exact
+  // size and gathered again after the one sync below.
+  const uint64_t tl_cap = nd * 70 + 16;
+  // (touched records are live records: at most rn - rdead; a guess past 1M touched records
+  // -- 16M elements -- is left to the exact second pass)
+  uint64_t ntl_guess = std::max<uint64_t>(4 * nd, h->ntl_hint + h->ntl_hint / 4);
+  ntl_guess = std::min({ntl_guess, tl_cap, h->rn - h->rdead + 16, (uint64_t)1 << 20});
+  Elems E{};
+  auto gather = [&](uint64_t ntl_cap) {
+    const uint64_t ecap = (uint64_t)nups + 16 * ntl_cap + nt + 16;
+    h->ebuf.ensure(
+        carve_size({ecap * 32, ecap * 4, ecap, ecap * 32, ecap, ecap * 8, ecap * 4, ecap * 4, ecap, ecap * 32, ecap, 64}));
+    Carver ce{(char*)h->ebuf.p, 0, h->ebuf.cap};
+    E = Elems{};
+    E.key = ce.take<uint64_t>(ecap * 4);
+    E.seg = ce.take<uint32_t>(ecap);
+    E.db = ce.take<uint8_t>(ecap);
+    E.bref = ce.take<uint64_t>(ecap * 4);
+    E.brl = ce.take<uint8_t>(ecap);
+    E.vo = ce.take<uint64_t>(ecap);
+    E.vl = ce.take<uint32_t>(ecap);
+    E.src = ce.take<uint32_t>(ecap);
+    E.oldd = ce.take<uint8_t>(ecap);
+    E.cref = ce.take<uint64_t>(ecap * 4);
+    E.crl = ce.take<uint8_t>(ecap);
+    E.n = ce.take<unsigned long long>(8);
+    E.cap = ecap;
+    // (the record elements are pushed after the upserts: k_f_upsert_elems sets E.n = nups)
+    hipLaunchKernelGGL(k_f_upsert_elems, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)tries, nt,
+                       (const uint32_t*)ur, (const uint64_t*)uo, E, hb, (uint64_t)nups);
+    LAUNCH_CHECK();
+    const uint64_t gblocks = std::min<uint64_t>((uint64_t)c->n_cu * 8, (nd * 16 * 8 + BS - 1) / BS);
+    hipLaunchKernelGGL(k_f_gather, dim3((unsigned)std::max<uint64_t>(gblocks, 1)), dim3(BS), 0, st, map_of(h),
+                       recs_of(h), (const uint32_t*)h->touched.p, (const uint8_t*)h->replaced.p,
+                       (const uint32_t*)tlist, (const unsigned long long*)fctr, (const uint32_t*)tries, nt, E, fctr);
+    hipLaunchKernelGGL(k_f_gather_roots, GRID(nt, BS), dim3(BS), 0, st, map_of(h), recs_of(h),
+                       (const uint32_t*)h->touched.p, (const uint32_t*)tries, nt, E);
+    LAUNCH_CHECK();
+    HIPCHK(hipMemcpyAsync(c->h_pinned, fctr, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned + 4, E.n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return ecap;
+  };
+  uint64_t ecap = gather(ntl_guess);
   const uint64_t ntl = c->h_pinned[0], nrep = c->h_pinned[1];
-  if (c->h_pinned[2]) throw KhError{KH_EINTERNAL, "forest descent: corrupt anchor map"};
+  if (c->h_pinned[2] == 3) throw KhError{KH_EINTERNAL, "forest descent: corrupt anchor map"};
   if (c->h_pinned[3]) {  // nothing has changed yet: clear the descent's flags and refuse the batch
     if (ntl) {
       hipLaunchKernelGGL(k_f_untouch, GRID(ntl, BS), dim3(BS), 0, st, (const uint32_t*)tlist, ntl,
@@ -3007,42 +3282,15 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                   "turns that leaf into a value-only branch (MerklePatriciaTrie.scala:187-199), which this engine "
                   "does not reproduce; the trie is unchanged"};
   }
-  // ---- 3. elements: upserts (values appended to the heap), untouched children, kept leaves, roots
-  const uint64_t ecap = (uint64_t)nups + 16 * ntl + nt + 16;
-  h->ebuf.ensure(
-      carve_size({ecap * 32, ecap * 4, ecap, ecap * 32, ecap, ecap * 8, ecap * 4, ecap * 4, ecap, ecap * 32, ecap, 64}));
-  Carver ce{(char*)h->ebuf.p, 0, h->ebuf.cap};
-  Elems E{};
-  E.key = ce.take<uint64_t>(ecap * 4);
-  E.seg = ce.take<uint32_t>(ecap);
-  E.db = ce.take<uint8_t>(ecap);
-  E.bref = ce.take<uint64_t>(ecap * 4);
-  E.brl = ce.take<uint8_t>(ecap);
-  E.vo = ce.take<uint64_t>(ecap);
-  E.vl = ce.take<uint32_t>(ecap);
-  E.src = ce.take<uint32_t>(ecap);
-  E.oldd = ce.take<uint8_t>(ecap);
-  E.cref = ce.take<uint64_t>(ecap * 4);
-  E.crl = ce.take<uint8_t>(ecap);
-  E.n = ce.take<unsigned long long>(8);
-  E.cap = ecap;
-  // (the record elements are pushed after the upserts: k_f_upsert_elems sets E.n = nups)
-  hipLaunchKernelGGL(k_f_upsert_elems, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)tries, nt,
-                     (const uint32_t*)ur, (const uint64_t*)uo, E, hb, (uint64_t)nups);
-  LAUNCH_CHECK();
-  if (ntl)
-    hipLaunchKernelGGL(k_f_gather, GRID(ntl * 16, BS), dim3(BS), 0, st, map_of(h), recs_of(h),
-                       (const uint32_t*)h->touched.p, (const uint8_t*)h->replaced.p, (const uint32_t*)tlist, ntl,
-                       (const uint32_t*)tries, nt, E, fctr);
-  hipLaunchKernelGGL(k_f_gather_roots, GRID(nt, BS), dim3(BS), 0, st, map_of(h), recs_of(h),
-                     (const uint32_t*)h->touched.p, (const uint32_t*)tries, nt, E);
-  LAUNCH_CHECK();
-  HIPCHK(hipMemcpyAsync(c->h_pinned, E.n, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(c->h_pinned + 1, fctr + 2, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  const uint64_t ne = c->h_pinned[0];
-  if (c->h_pinned[1]) throw KhError{KH_EINTERNAL, "forest gather: corrupt anchor map"};
+  if (c->h_pinned[2]) throw KhError{KH_EINTERNAL, "forest gather: corrupt anchor map"};
+  uint64_t ne = c->h_pinned[4];
+  if (ne > ecap) {  // the guess was short: the exact capacity, gathered again
+    ecap = gather(ntl);
+    ne = c->h_pinned[4];
+    if (c->h_pinned[2]) throw KhError{KH_EINTERNAL, "forest gather: corrupt anchor map"};
+  }
   if (ne > ecap) throw KhError{KH_EINTERNAL, "forest gather: element overflow"};
+  h->ntl_hint = ntl;
   h->heap_n = hb + ubytes;
   HIPCHK(hipEventRecord(c->ev[7], st));
   // ---- 4. element build (every touched trie a segment), or all tries emptied
@@ -3058,6 +3306,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                 nt > 1 ? (const uint32_t*)E.seg : nullptr, nt, 0, 0, keep_em};
     A.vlen = E.vl;
     A.el = &EA;
+    A.dev_results = true;  // the counters come back with the roots (build_stats below)
     run_build(c, A, O2, &bst);
     B = c->last_B;
     m = c->T.m;
@@ -3142,15 +3391,20 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   }
   // ---- roots to the host
   // (through the pinned staging: a pageable destination pins its pages on every copy)
+  // One sync: the trie list and roots (carved back to back), the element build's counters
+  // and the map's error flag.
   h->tries.resize(nt);
   h->roots.resize((uint64_t)nt * 32);
-  uint8_t* hs = pinned_stage(c, (uint64_t)nt * 36);
-  HIPCHK(hipMemcpyAsync(hs, tries, (uint64_t)nt * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(hs + (uint64_t)nt * 4, roots, (uint64_t)nt * 32, hipMemcpyDeviceToHost, st));
+  const size_t o_roots = (size_t)((char*)roots - (char*)tries), tr_bytes = o_roots + (size_t)nt * 32;
+  const size_t o_ctr = (tr_bytes + 63) & ~(size_t)63, ctr_bytes = (size_t)CTR_N * CTR_SHARDS * 8;
+  uint8_t* hs = pinned_stage(c, o_ctr + ctr_bytes);
+  if (nt) HIPCHK(hipMemcpyAsync(hs, tries, tr_bytes, hipMemcpyDeviceToHost, st));
+  if (ne) HIPCHK(hipMemcpyAsync(hs + o_ctr, c->T.ctr, ctr_bytes, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(c->h_pinned, fctr + 3, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   memcpy(h->tries.data(), hs, (uint64_t)nt * 4);
-  memcpy(h->roots.data(), hs + (uint64_t)nt * 4, (uint64_t)nt * 32);
+  memcpy(h->roots.data(), hs + o_roots, (uint64_t)nt * 32);
+  if (ne) build_stats(c, (const unsigned long long*)(hs + o_ctr), &bst);
   if (c->h_pinned[0]) throw KhError{KH_EINTERNAL, "anchor map insert failed"};
   if (!h->forest) memcpy(h->root, nt ? h->roots.data() : h->root, 32);
   float merge_ms = ev_ms(c->ev[6], c->ev[7]);

@@ -223,13 +223,16 @@ inline size_t scan_scratch_bytes(uint64_t n, size_t elem) {
 
 // out[i] = sum_{j<i} in[i]; in == out allowed.  If total != nullptr, *total (device)
 // receives the sum of all n inputs.  scratch: scan_scratch_bytes(n) bytes.
+// small_ok = false: never the one-block k_scan_small (the nested scan of a large scan's tile
+// sums, which may run beside the leaf kernel: a 1024-thread block waits for a whole CU to
+// drain there -- the topology stream of a 100M build lost 6 ms to it).
 template <typename T>
-void scan_exclusive(const T* in, T* out, uint64_t n, T* total, void* scratch, hipStream_t st) {
+void scan_exclusive(const T* in, T* out, uint64_t n, T* total, void* scratch, hipStream_t st, bool small_ok = true) {
   if (n == 0) {
     if (total) (void)hipMemsetAsync(total, 0, sizeof(T), st);
     return;
   }
-  if (n <= SCAN_SMALL_MAX) {
+  if (small_ok && n <= SCAN_SMALL_MAX) {
     hipLaunchKernelGGL(k_scan_small<T>, dim3(1), dim3(SCAN_SMALL_THREADS), 0, st, in, out, n, total);
     return;
   }
@@ -248,7 +251,7 @@ void scan_exclusive(const T* in, T* out, uint64_t n, T* total, void* scratch, hi
                      total ? last_in : (T*)nullptr);
   if (tiles > 1) {
     char* next = (char*)scratch + (((tiles + 1) * sizeof(T) + 63) / 64) * 64 + 64;
-    scan_exclusive<T>(sums, sums, tiles, (T*)nullptr, next, st);
+    scan_exclusive<T>(sums, sums, tiles, (T*)nullptr, next, st, false);
     hipLaunchKernelGGL(k_scan_add<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, out, n, (const T*)sums);
   }
   if (total) hipLaunchKernelGGL(k_scan_total<T>, dim3(1), dim3(1), 0, st, (const T*)last_in, (const T*)(out + n - 1), total);

@@ -1702,7 +1702,16 @@ KH_HD uint32_t op_branch_direct(const Topo& T, uint32_t j, uint64_t* slot, uint6
 // again, its tail, in the next window), the next child's record is loaded while the
 // current one is placed, and the child lengths for the payload are loaded as one batch
 // (16 predicated loads issued together).  One Keccak call site (the block loop).
-KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl) {
+// The child records: by default the level's records in HBM (cm / cr at the branch's child
+// base, word q of child c at cr[4c + q]); k_branch_fused<3> (small levels) passes a copy in
+// LDS, lane-interleaved: child c's meta at cm[c * cs], word q at cr[(4c + q) * cs].
+struct ChildSrc {
+  const uint16_t* cm = nullptr;
+  const uint64_t* cr = nullptr;
+  uint32_t cs = 1;
+};
+KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl,
+                                ChildSrc src = ChildSrc{}) {
   const uint32_t ext = T.br_ext[j];
   const bool top = T.br_parent[j] == NONE;
   *inl = 0;
@@ -1710,13 +1719,18 @@ KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint6
   uint32_t L, perms = 0, ninl = 0;
   {
     const uint32_t k = T.br_k[j];
-    const uint64_t cb = T.br_cbase[j];
-    const uint16_t* cm = T.cmeta + cb;
-    const uint64_t* cr = T.cref + 4 * cb;
+    const uint32_t cs = src.cs;
+    const uint16_t* cm = src.cm;
+    const uint64_t* cr = src.cr;
+    if (!cm) {
+      const uint64_t cb = T.br_cbase[j];
+      cm = T.cmeta + cb;
+      cr = T.cref + 4 * cb;
+    }
     uint32_t payload = 1 + (16 - k);  // terminator "" + empty slots
 #pragma unroll
     for (uint32_t c = 0; c < 16; ++c) {
-      const uint32_t len = c < k ? (uint32_t)(cm[c] & 0xFF) : 0;
+      const uint32_t len = c < k ? (uint32_t)(cm[c * cs] & 0xFF) : 0;
       payload += len == 32 ? 33 : len;
     }
     const uint32_t hh = rlp_hdr_len(payload);
@@ -1753,10 +1767,14 @@ KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint6
     uint32_t nm = 0;
     // child c's reference: its record, or the stash a LINK record points at (op_leaf_link_rec)
     auto load_child = [&](uint32_t cc) {
-      nm = cm[cc];
-      const uint64_t* p = cr + 4 * cc;
-      if (T.links && (nm & CM_LINK)) p = T.lf_eref + 4 * p[0];
-      n0 = p[0], n1 = p[1], n2 = p[2], n3 = p[3];
+      nm = cm[cc * cs];
+      const uint64_t* p = cr + 4 * cc * cs;
+      if (T.links && (nm & CM_LINK)) {
+        p = T.lf_eref + 4 * p[0];
+        n0 = p[0], n1 = p[1], n2 = p[2], n3 = p[3];
+      } else {
+        n0 = p[0], n1 = p[cs], n2 = p[2 * cs], n3 = p[3 * cs];
+      }
     };
     if (k) load_child(0);
     bool have = false;  // I / off / ilen hold child c, not yet completely placed
