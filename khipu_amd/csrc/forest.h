@@ -69,26 +69,92 @@ KH_HD void set_nibble(uint64_t* key, uint32_t i, uint32_t v) {
 
 constexpr uint8_t REC_DEAD = 0, REC_LIVE = 1;
 
-// node records (structure of arrays)
-struct Recs {
-  uint64_t* rk;    // [cap*4] a key under the node (a leaf: its key)
-  uint32_t* rt;    // trie id
-  uint8_t* rd;     // anchor depth
-  uint8_t* rdb;    // EL_LEAF, or the branch depth
-  uint64_t* rvo;   // leaf: value offset in the heap
-  uint32_t* rvl;   // leaf: value length
-  uint64_t* rref;  // [cap*4] capped reference the parent holds (the extension's, if any)
-  uint8_t* rrl;    //   its length (32 = hash)
-  uint64_t* rbref; // [cap*4] branch: the branch's own capped reference
-  uint8_t* rbrl;
-  uint16_t* rmask; // branch: child nibbles
-  uint8_t* rlive;
+// Node records: one 128-byte record per node (array of structures), so a probe's check
+// (trie, anchor depth, key) and a descent step read ONE 64-byte line, and a whole record
+// (an element of the next build) two; round 3's twelve arrays cost up to twelve lines per
+// record (the block-commit gather: profiles/r3x_block_commit_timeline_50m.json).
+//   [0, 32)  k: a key under the node (a leaf: its key)
+//   32 t (u32) trie id | 36 d: anchor depth | 37 db: EL_LEAF or the branch depth |
+//   38 mask (u16): branch child nibbles | 40 live | 41 rl | 42 brl | 44 vl (u32) |
+//   48 vo (u64): leaf value offset in the heap
+//   [64, 96)  ref: capped reference the parent holds (the extension's, if any); rl its length
+//   [96, 128) bref: a branch's own capped reference; brl its length
+// The accessors keep the structure-of-arrays indexing of the code that uses them: R.rt[r],
+// and word q of the key R.rk[4 * r + q] (R.key(r) is the key's address).
+constexpr uint64_t REC_BYTES = 128;
+template <typename T, uint32_t OFF>
+struct RecField {
+  uint8_t* b;
+  KH_HD T& operator[](uint64_t r) const { return *(T*)(b + r * REC_BYTES + OFF); }
 };
+template <uint32_t OFF>
+struct RecWords {  // 4 words per record: index 4 r + q
+  uint8_t* b;
+  KH_HD uint64_t& operator[](uint64_t i) const { return *(uint64_t*)(b + (i >> 2) * REC_BYTES + OFF + (i & 3) * 8); }
+};
+struct Recs {
+  RecWords<0> rk;
+  RecField<uint32_t, 32> rt;
+  RecField<uint8_t, 36> rd;
+  RecField<uint8_t, 37> rdb;
+  RecField<uint16_t, 38> rmask;
+  RecField<uint8_t, 40> rlive;
+  RecField<uint8_t, 41> rrl;
+  RecField<uint8_t, 42> rbrl;
+  RecField<uint32_t, 44> rvl;
+  RecField<uint64_t, 48> rvo;
+  RecWords<64> rref;
+  RecWords<96> rbref;
+  KH_HD uint64_t* key(uint64_t r) const { return (uint64_t*)(rk.b + r * REC_BYTES); }
+};
+// one whole record, composed in registers and written as 16-byte stores (a record written
+// field by field across a wave touches one line per field and lane)
+struct RecVal {
+  uint64_t k[4];
+  uint32_t t;
+  uint8_t d, db;
+  uint16_t mask;
+  uint8_t live, rl, brl;
+  uint32_t vl;
+  uint64_t vo;
+  uint64_t ref[4], bref[4];
+};
+KH_HD void rec_store(uint8_t* base, uint64_t r, const RecVal& v) {
+  uint64_t w[16];
+  for (int q = 0; q < 4; ++q) {
+    w[q] = v.k[q];
+    w[8 + q] = v.ref[q];
+    w[12 + q] = v.bref[q];
+  }
+  w[4] = (uint64_t)v.t | ((uint64_t)v.d << 32) | ((uint64_t)v.db << 40) | ((uint64_t)v.mask << 48);
+  w[5] = (uint64_t)v.live | ((uint64_t)v.rl << 8) | ((uint64_t)v.brl << 16) | ((uint64_t)v.vl << 32);
+  w[6] = v.vo;
+  w[7] = 0;
+#ifdef __HIP_DEVICE_COMPILE__
+  ulonglong2* d = (ulonglong2*)(base + r * REC_BYTES);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) d[q] = make_ulonglong2(w[2 * q], w[2 * q + 1]);
+#else
+  memcpy(base + r * REC_BYTES, w, REC_BYTES);
+#endif
+}
+KH_HD Recs recs_at(uint8_t* base) {
+  return Recs{{base}, {base}, {base}, {base}, {base}, {base}, {base}, {base}, {base}, {base}, {base}, {base}};
+}
 
+// The anchor -> record map: 16-byte slots (tag, record) so a probe reads one line.
+struct MapTag {
+  uint8_t* b;
+  KH_HD unsigned long long& operator[](uint64_t s) const { return *(unsigned long long*)(b + s * 16); }
+};
+struct MapRec {
+  uint8_t* b;
+  KH_HD uint32_t& operator[](uint64_t s) const { return *(uint32_t*)(b + s * 16 + 8); }
+};
 struct AMap {
-  unsigned long long* tag;  // [cap] 0 empty, 1 tombstone
-  uint32_t* rec;
-  uint64_t mask;            // cap - 1 (cap a power of two, load <= 1/2 incl. tombstones)
+  MapTag tag;    // [cap] 0 empty, 1 tombstone
+  MapRec rec;
+  uint64_t mask; // cap - 1 (cap a power of two, load <= 1/2 incl. tombstones)
 };
 
 KH_HD uint32_t map_find(const AMap& M, const Recs& R, uint32_t t, uint32_t d, const uint64_t* key) {
@@ -98,14 +164,14 @@ KH_HD uint32_t map_find(const AMap& M, const Recs& R, uint32_t t, uint32_t d, co
     if (g == 0) return NONE;
     if (g == h) {
       const uint32_t r = M.rec[s];
-      if (R.rt[r] == t && R.rd[r] == d && prefix_eq(R.rk + 4ull * r, key, d)) return r;
+      if (R.rt[r] == t && R.rd[r] == d && prefix_eq(R.key(r), key, d)) return r;
     }
   }
   return NONE;
 }
 // slot of record r at its current anchor (NONE if absent)
 KH_HD uint64_t map_slot_of(const AMap& M, const Recs& R, uint32_t r) {
-  const uint64_t h = anchor_tag(R.rt[r], R.rd[r], R.rk + 4ull * r);
+  const uint64_t h = anchor_tag(R.rt[r], R.rd[r], R.key(r));
   for (uint64_t s = h & M.mask, n = 0; n <= M.mask; s = (s + 1) & M.mask, ++n) {
     const uint64_t g = M.tag[s];
     if (g == 0) return ~0ULL;
@@ -124,10 +190,10 @@ KH_HD uint32_t forest_get(const AMap& M, const Recs& R, uint32_t t, const uint64
     if (r == NONE) return NONE;
     const uint32_t db = R.rdb[r];
     if (db == EL_LEAF) {
-      const uint64_t* L = R.rk + 4ull * r;
+      const uint64_t* L = R.key(r);
       return (L[0] == key[0] && L[1] == key[1] && L[2] == key[2] && L[3] == key[3]) ? r : NONE;
     }
-    if (lcp_nibbles(load_key(key, 0), load_key(R.rk, r)) < (int)db) return NONE;  // leaves the extension
+    if (lcp_nibbles(load_key(key, 0), load_key(R.key(r), 0)) < (int)db) return NONE;  // leaves the extension
     d = db + 1;
   }
   return NONE;

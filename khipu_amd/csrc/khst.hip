@@ -2559,7 +2559,7 @@ __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32
         const uint32_t db = R.rdb[r];
         leaf = db == EL_LEAF;
         if (leaf) {
-          const uint64_t* L = R.rk + 4ull * r;
+          const uint64_t* L = R.key(r);
           if (L[0] == K[0] && L[1] == K[1] && L[2] == K[2] && L[3] == K[3]) {
             replaced[r] = 1;  // keys are unique in the batch: one op per leaf
             repl = true;
@@ -2570,7 +2570,7 @@ __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32
             if (d == 64 && O.kind[o] == FOP_UPSERT) atomicOr(&ctr[3], 1ULL);
           }
           active = lost = false;
-        } else if (lcp_nibbles(load_key(K, 0), load_key(R.rk, r)) < (int)db) {
+        } else if (lcp_nibbles(load_key(K, 0), load_key(R.key(r), 0)) < (int)db) {
           r = NONE;  // diverges in the extension
           active = lost = false;
         } else {
@@ -2657,7 +2657,29 @@ __global__ void __launch_bounds__(BS) k_f_prep(const uint32_t* sidx, uint64_t n,
   isup[o] = up ? 1u : 0u;
   ulen[o] = up ? voff[s + 1] - voff[s] : 0;
 }
-__global__ void __launch_bounds__(BS) k_f_gather(AMap M, Recs R, const uint32_t* touched, const uint8_t* replaced,
+// Slots for a whole block at once: one atomic per block (the gather's per-wave claims on the
+// one element counter serialised in L2).  Every thread of the block must call it.
+__device__ __forceinline__ uint64_t block_claim(unsigned long long* ctr, bool want, unsigned long long* lds) {
+  const uint64_t m = __ballot(want);
+  const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) lds[w] = (unsigned long long)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long run = 0;
+    for (uint32_t q = 0; q < nw; ++q) {
+      const unsigned long long c = lds[q];
+      lds[q] = run;
+      run += c;
+    }
+    lds[nw] = run ? atomicAdd(ctr, run) : 0;
+  }
+  __syncthreads();
+  const uint64_t e = lds[nw] + lds[w] + (uint64_t)__popcll(m & lanemask_lt());
+  __syncthreads();  // lds is reused by the next call
+  return e;
+}
+constexpr uint32_t GATHER_BS = 1024;
+__global__ void __launch_bounds__(GATHER_BS) k_f_gather(AMap M, Recs R, const uint32_t* touched, const uint8_t* replaced,
                                                  const uint32_t* tlist, const unsigned long long* ntl_p,
                                                  const uint32_t* tries, uint32_t nt, Elems E, unsigned long long* ctr) {
   // one thread per (touched record, child nibble v): the 16 child lookups of an opened
@@ -2665,8 +2687,9 @@ __global__ void __launch_bounds__(BS) k_f_gather(AMap M, Recs R, const uint32_t*
   // threads instead of one thread's sequence.  The touched count is read on the device
   // (the descent's counter): a grid-stride loop, no host round trip between the descent
   // and the gather.  Whole blocks iterate together, so every lane reaches the claim.
+  __shared__ unsigned long long claim[GATHER_BS / 64 + 1];
   const uint64_t ntl = *ntl_p;
-  for (uint64_t g0 = (uint64_t)blockIdx.x * BS; g0 < ntl * 16; g0 += (uint64_t)gridDim.x * BS) {
+  for (uint64_t g0 = (uint64_t)blockIdx.x * GATHER_BS; g0 < ntl * 16; g0 += (uint64_t)gridDim.x * GATHER_BS) {
     const uint64_t g = g0 + threadIdx.x;
     const uint64_t i = g >> 4;
     const uint32_t v = (uint32_t)(g & 15);
@@ -2690,7 +2713,7 @@ __global__ void __launch_bounds__(BS) k_f_gather(AMap M, Recs R, const uint32_t*
         }
       }
     }
-    const uint64_t e = wave_claim(E.n, want);  // every lane of the wave reaches the claim
+    const uint64_t e = block_claim(E.n, want, claim);  // every thread of the block reaches the claim
     if (want) elem_fill(R, er, seg, E, e);
   }
 }
@@ -2715,25 +2738,27 @@ __global__ void __launch_bounds__(BS) k_f_branch_recs(Topo T, const uint32_t* Bp
   const uint32_t t = tries[T.sseg ? T.sseg[f] : 0];
   const uint32_t db = T.br_depth[j], ext = T.br_ext[j], d = db - ext;
   const uint64_t* K = T.skey + 4 * f;
-  for (int q = 0; q < 4; ++q) R.rk[4 * r + q] = K[q];
-  R.rt[r] = t;
-  R.rd[r] = (uint8_t)d;
-  R.rdb[r] = (uint8_t)db;
-  R.rvo[r] = 0;
-  R.rvl[r] = 0;
   const uint32_t brl = T.br_rlen[j] >= 32 ? 32 : T.br_rlen[j];
   const uint32_t xrl = ext ? (T.ex_rlen[j] >= 32 ? 32 : T.ex_rlen[j]) : brl;
   const uint64_t* xr = ext ? T.ex_ref + 4 * j : T.br_ref + 4 * j;
-  for (int q = 0; q < 4; ++q) {
-    R.rbref[4 * r + q] = T.br_ref[4 * j + q];
-    R.rref[4 * r + q] = xr[q];
-  }
-  R.rbrl[r] = (uint8_t)brl;
-  R.rrl[r] = (uint8_t)xrl;
   uint32_t mask = 0;
   for (uint32_t c = 0; c < T.br_k[j]; ++c) mask |= 1u << (T.cmeta[T.br_cbase[j] + c] >> 8);
-  R.rmask[r] = (uint16_t)mask;
-  R.rlive[r] = REC_LIVE;
+  RecVal v;
+  for (int q = 0; q < 4; ++q) {
+    v.k[q] = K[q];
+    v.bref[q] = T.br_ref[4 * j + q];
+    v.ref[q] = xr[q];
+  }
+  v.t = t;
+  v.d = (uint8_t)d;
+  v.db = (uint8_t)db;
+  v.mask = (uint16_t)mask;
+  v.live = REC_LIVE;
+  v.rl = (uint8_t)xrl;
+  v.brl = (uint8_t)brl;
+  v.vl = 0;
+  v.vo = 0;
+  rec_store(R.rk.b, r, v);
   const uint32_t old = map_find(M, R, t, d, K);
   bool same_b = false, same_x = false;
   if (old != NONE && R.rdb[old] == db && R.rbrl[old] == brl) {
@@ -2765,23 +2790,26 @@ __global__ void __launch_bounds__(BS) k_f_elem_recs(Topo T, Elems E, const uint3
                                                     Recs R, uint64_t base, uint32_t* eid) {
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= T.m) return;
-  const uint32_t s = T.sidx[i];
-  const uint64_t r = E.src[s] == NONE ? base + newrank[i] : E.src[s];
+  const uint32_t s = T.sidx[i], src = E.src[s];
+  const uint64_t r = src == NONE ? base + newrank[i] : src;
   eid[i] = (uint32_t)r;
-  for (int q = 0; q < 4; ++q) R.rk[4 * r + q] = T.skey[4 * i + q];
-  R.rt[r] = tries[T.sseg ? T.sseg[i] : 0];
-  R.rd[r] = (uint8_t)(T.lf_pd[i] + 1);
-  R.rdb[r] = T.el_db[i];
-  R.rvo[r] = E.vo[s];
-  R.rvl[r] = E.vl[s];
-  const uint32_t L = T.lf_rlen[i];
+  RecVal v;
   for (int q = 0; q < 4; ++q) {
-    R.rref[4 * r + q] = T.lf_ref[4 * i + q];
-    R.rbref[4 * r + q] = T.el_bref[4 * i + q];
+    v.k[q] = T.skey[4 * i + q];
+    v.ref[q] = T.lf_ref[4 * i + q];
+    v.bref[q] = T.el_bref[4 * i + q];
   }
-  R.rrl[r] = (uint8_t)(L >= 32 ? 32 : L);
-  R.rbrl[r] = T.el_brl[i];
-  R.rlive[r] = REC_LIVE;
+  v.t = tries[T.sseg ? T.sseg[i] : 0];
+  v.d = (uint8_t)(T.lf_pd[i] + 1);
+  v.db = T.el_db[i];
+  v.mask = src == NONE ? 0 : R.rmask[r];  // a re-anchored subtree keeps its children
+  v.live = REC_LIVE;
+  const uint32_t L = T.lf_rlen[i];
+  v.rl = (uint8_t)(L >= 32 ? 32 : L);
+  v.brl = T.el_brl[i];
+  v.vl = E.vl[s];
+  v.vo = E.vo[s];
+  rec_store(R.rk.b, r, v);
 }
 // map maintenance: delete records' current anchors (two lists in one launch: the touched
 // records, then the element sources), mark dead, insert
@@ -2819,7 +2847,7 @@ __global__ void __launch_bounds__(BS) k_map_insert(AMap M, Recs R, uint64_t base
   if (i >= nb + n) return;
   const uint32_t r = i < nb ? (uint32_t)(base + i) : list[i - nb];
   if (R.rlive[r] != REC_LIVE) return;
-  const unsigned long long h = anchor_tag(R.rt[r], R.rd[r], R.rk + 4ull * r);
+  const unsigned long long h = anchor_tag(R.rt[r], R.rd[r], R.key(r));
   for (uint64_t s = h & M.mask, k = 0; k <= M.mask; s = (s + 1) & M.mask, ++k) {
     unsigned long long g = M.tag[s];
     if (g > 1) continue;
@@ -2859,9 +2887,9 @@ struct kh_trie {
   kh_ctx* c = nullptr;
   uint32_t flags = 0;  // KH_HASH_KEYS: the trie's key encoder; KH_EMIT_NODES: keep each commit's write-back set
   bool forest = false;
-  DevBuf rk, rt, rd, rdb, rvo, rvl, rref, rrl, rbref, rbrl, rmask, rlive, touched, replaced;
+  DevBuf recs, touched, replaced;  // node records (forest.h Recs: 128 B each), per-commit flags
   uint64_t rcap = 0, rn = 0, rdead = 0;
-  DevBuf mtag, mrec;
+  DevBuf mslots;  // anchor map: 16-byte (tag, record) slots
   uint64_t mcap = 0, mused = 0;
   DevBuf heap;
   uint64_t heap_n = 0;
@@ -2880,11 +2908,9 @@ struct kh_trie {
 };
 
 static Recs recs_of(kh_trie* h) {
-  return Recs{(uint64_t*)h->rk.p,   (uint32_t*)h->rt.p,   (uint8_t*)h->rd.p,   (uint8_t*)h->rdb.p,
-              (uint64_t*)h->rvo.p,  (uint32_t*)h->rvl.p,  (uint64_t*)h->rref.p, (uint8_t*)h->rrl.p,
-              (uint64_t*)h->rbref.p, (uint8_t*)h->rbrl.p, (uint16_t*)h->rmask.p, (uint8_t*)h->rlive.p};
+  return recs_at((uint8_t*)h->recs.p);
 }
-static AMap map_of(kh_trie* h) { return AMap{(unsigned long long*)h->mtag.p, (uint32_t*)h->mrec.p, h->mcap - 1}; }
+static AMap map_of(kh_trie* h) { return AMap{{(uint8_t*)h->mslots.p}, {(uint8_t*)h->mslots.p}, h->mcap - 1}; }
 
 // grow a device array, keeping its first `keep` bytes
 static void regrow(DevBuf& b, size_t keep, size_t bytes, hipStream_t st) {
@@ -2903,31 +2929,18 @@ static void recs_reserve(kh_trie* h, uint64_t need) {
   if (need <= h->rcap) return;
   hipStream_t st = h->c->st;
   const uint64_t cap = std::max<uint64_t>(need + need / 2, 4096), n = h->rn;
-  regrow(h->rk, n * 32, cap * 32, st);
-  regrow(h->rt, n * 4, cap * 4, st);
-  regrow(h->rd, n, cap, st);
-  regrow(h->rdb, n, cap, st);
-  regrow(h->rvo, n * 8, cap * 8, st);
-  regrow(h->rvl, n * 4, cap * 4, st);
-  regrow(h->rref, n * 32, cap * 32, st);
-  regrow(h->rrl, n, cap, st);
-  regrow(h->rbref, n * 32, cap * 32, st);
-  regrow(h->rbrl, n, cap, st);
-  regrow(h->rmask, n * 2, cap * 2, st);
-  regrow(h->rlive, n, cap, st);
+  regrow(h->recs, n * REC_BYTES, cap * REC_BYTES, st);
   regrow(h->touched, n * 4, cap * 4, st);
   regrow(h->replaced, n, cap, st);
   // the new tail: not live, not touched
-  HIPCHK(hipMemsetAsync((uint8_t*)h->rlive.p + n, 0, h->rlive.cap - n, st));
+  HIPCHK(hipMemsetAsync((uint8_t*)h->recs.p + n * REC_BYTES, 0, h->recs.cap - n * REC_BYTES, st));
   HIPCHK(hipMemsetAsync((uint8_t*)h->touched.p + 4 * n, 0, h->touched.cap - 4 * n, st));
   HIPCHK(hipMemsetAsync((uint8_t*)h->replaced.p + n, 0, h->replaced.cap - n, st));
-  h->rcap = std::min({h->rk.cap / 32, h->rt.cap / 4, h->rd.cap, h->rdb.cap, h->rvo.cap / 8, h->rvl.cap / 4,
-                      h->rref.cap / 32, h->rrl.cap, h->rbref.cap / 32, h->rbrl.cap, h->rmask.cap / 2, h->rlive.cap,
-                      h->touched.cap / 4, h->replaced.cap});
+  h->rcap = std::min({h->recs.cap / REC_BYTES, h->touched.cap / 4, h->replaced.cap});
 }
-__global__ void __launch_bounds__(BS) k_rec_count_live(const uint8_t* live, uint64_t n, unsigned long long* cnt) {
+__global__ void __launch_bounds__(BS) k_rec_count_live(Recs R, uint64_t n, unsigned long long* cnt) {
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  unsigned long long v = (i < n && live[i] == REC_LIVE) ? 1 : 0;
+  unsigned long long v = (i < n && R.rlive[i] == REC_LIVE) ? 1 : 0;
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(cnt, v);
 }
@@ -2936,17 +2949,16 @@ static void map_rebuild(kh_trie* h, uint64_t headroom) {
   hipStream_t st = h->c->st;
   uint64_t cap = 1024;
   while (cap < 2 * (h->rn + headroom) + 1024) cap <<= 1;
-  h->mtag.ensure(cap * 8);
-  h->mrec.ensure(cap * 4);
+  h->mslots.ensure(cap * 16);
   h->mcap = cap;
-  HIPCHK(hipMemsetAsync(h->mtag.p, 0, cap * 8, st));
+  HIPCHK(hipMemsetAsync(h->mslots.p, 0, cap * 16, st));
   h->merr.ensure(64);
   unsigned long long* err = (unsigned long long*)h->merr.p;
   HIPCHK(hipMemsetAsync(err, 0, 16, st));
   if (h->rn) {
     hipLaunchKernelGGL(k_map_insert, GRID(h->rn, BS), dim3(BS), 0, st, map_of(h), recs_of(h), (uint64_t)0, h->rn,
                        (const uint32_t*)nullptr, (uint64_t)0, err);
-    hipLaunchKernelGGL(k_rec_count_live, GRID(h->rn, BS), dim3(BS), 0, st, (const uint8_t*)h->rlive.p, h->rn, err + 1);
+    hipLaunchKernelGGL(k_rec_count_live, GRID(h->rn, BS), dim3(BS), 0, st, recs_of(h), h->rn, err + 1);
   }
   LAUNCH_CHECK();
   HIPCHK(hipMemcpyAsync(h->c->h_pinned, err, 16, hipMemcpyDeviceToHost, st));
@@ -3255,8 +3267,8 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     hipLaunchKernelGGL(k_f_upsert_elems, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)tries, nt,
                        (const uint32_t*)ur, (const uint64_t*)uo, E, hb, (uint64_t)nups);
     LAUNCH_CHECK();
-    const uint64_t gblocks = std::min<uint64_t>((uint64_t)c->n_cu * 8, (nd * 16 * 8 + BS - 1) / BS);
-    hipLaunchKernelGGL(k_f_gather, dim3((unsigned)std::max<uint64_t>(gblocks, 1)), dim3(BS), 0, st, map_of(h),
+    const uint64_t gblocks = std::min<uint64_t>((uint64_t)c->n_cu * 2, (nd * 16 * 8 + GATHER_BS - 1) / GATHER_BS);
+    hipLaunchKernelGGL(k_f_gather, dim3((unsigned)std::max<uint64_t>(gblocks, 1)), dim3(GATHER_BS), 0, st, map_of(h),
                        recs_of(h), (const uint32_t*)h->touched.p, (const uint8_t*)h->replaced.p,
                        (const uint32_t*)tlist, (const unsigned long long*)fctr, (const uint32_t*)tries, nt, E, fctr);
     hipLaunchKernelGGL(k_f_gather_roots, GRID(nt, BS), dim3(BS), 0, st, map_of(h), recs_of(h),
