@@ -546,6 +546,27 @@ __global__ void k_level_bounds(const uint32_t* bbase, uint32_t nblk, const uint3
 // read from global memory directly (long values; such leaves go to the arena).
 constexpr uint32_t STAGE_WORDS = 19;  // aligned 8-byte words per staged value span
 
+// Slots for a whole block at once: one atomic per block (the gather's per-wave claims on the
+// one element counter serialised in L2).  Every thread of the block must call it.
+__device__ __forceinline__ uint64_t block_claim(unsigned long long* ctr, bool want, unsigned long long* lds) {
+  const uint64_t m = __ballot(want);
+  const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) lds[w] = (unsigned long long)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long run = 0;
+    for (uint32_t q = 0; q < nw; ++q) {
+      const unsigned long long c = lds[q];
+      lds[q] = run;
+      run += c;
+    }
+    lds[nw] = run ? atomicAdd(ctr, run) : 0;
+  }
+  __syncthreads();
+  const uint64_t e = lds[nw] + lds[w] + (uint64_t)__popcll(m & lanemask_lt());
+  __syncthreads();  // lds is reused by the next call
+  return e;
+}
 __global__ void __launch_bounds__(BS) k_leaf_prep(Topo T) {
   __shared__ uint64_t stage[BS * STAGE_WORDS];
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -589,6 +610,46 @@ __global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
     perms = op_leaf_hash(T, i, &in1);
     hashes = perms ? 1 : 0;
     inl = in1;
+  }
+  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
+             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
+}
+// Element builds (a block commit): most elements are unchanged subtrees or leaves whose
+// reference is only handed to the new parent; the few that are re-encoded (the block's
+// upserts, moved leaves, new extensions) sit scattered among them, so a thread-per-element
+// hash pass runs a permutation in nearly every wave.  k_leaf_pub publishes the cheap ones
+// and lists the others (one claim per block); k_leaf_hash_list hashes the list in full waves.
+__device__ __forceinline__ bool leaf_listed(const Topo& T, uint64_t i) {
+  if (is_branch_value(T, i)) return false;
+  const uint32_t a = (uint32_t)(T.lf_pd[i] + 1);
+  return !(el_cached(T, i, a) || (el_subtree(T, i) && el_ext_nibbles(T, i, a) == 0));
+}
+__global__ void __launch_bounds__(BS) k_leaf_pub(Topo T, uint32_t* list, unsigned long long* nlist) {
+  __shared__ unsigned long long claim[BS / 64 + 1];
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  const bool live = i < T.m;
+  const bool listed = live && leaf_listed(T, i);
+  unsigned long long perms = 0, hashes = 0, inl = 0;
+  if (live && !listed) {
+    uint32_t in1 = 0;
+    perms = op_leaf_hash(T, i, &in1);
+    hashes = perms ? 1 : 0;
+    inl = in1;
+  }
+  const uint64_t e = block_claim(nlist, listed, claim);
+  if (listed) list[e] = (uint32_t)i;
+  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
+             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
+}
+__global__ void __launch_bounds__(BS) k_leaf_hash_list(Topo T, const uint32_t* list, const unsigned long long* nlist) {
+  const uint64_t n = *nlist;
+  unsigned long long perms = 0, hashes = 0, inl = 0;
+  for (uint64_t k = (uint64_t)blockIdx.x * BS + threadIdx.x; k < n; k += (uint64_t)gridDim.x * BS) {
+    uint32_t in1 = 0;
+    const uint32_t p = op_leaf_hash(T, list[k], &in1);
+    perms += p;
+    hashes += p ? 1 : 0;
+    inl += in1;
   }
   block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
              ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
@@ -1493,6 +1554,7 @@ struct kh_ctx {
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // leaf hashing, concurrent with the branch topology
   std::mutex mu;
+  DevBuf ws_list;  // element builds: the list of leaves to hash (k_leaf_pub)
   DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, in_kn, in_aux, in_block, out_emit, emit_dev;
   hipEvent_t ev[13] = {};  // [8] boundaries ready (st), [9] / [10] leaf kernel start / end (st2),
                           // [11] second part of the leaf copy pass done (st2), [12] unused
@@ -2251,7 +2313,19 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   } else {  // write-back and element builds: encodings kept in message slots, then hashed
     hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_leaf_hash, GRID(m, BS), dim3(BS), 0, st, T);
+    if (A.el) {  // the re-encoded elements hashed from a list (k_leaf_pub)
+      c->ws_list.ensure(carve_size({64, m * 4}));
+      Carver cl{(char*)c->ws_list.p, 0, c->ws_list.cap};
+      unsigned long long* nlist = cl.take<unsigned long long>(8);
+      uint32_t* list = cl.take<uint32_t>(m);
+      HIPCHK(hipMemsetAsync(nlist, 0, 8, st));
+      hipLaunchKernelGGL(k_leaf_pub, GRID(m, BS), dim3(BS), 0, st, T, list, nlist);
+      const uint64_t lblocks = std::min<uint64_t>((uint64_t)c->n_cu * 4, (m + BS - 1) / BS);
+      hipLaunchKernelGGL(k_leaf_hash_list, dim3((unsigned)std::max<uint64_t>(lblocks, 1)), dim3(BS), 0, st, T,
+                         (const uint32_t*)list, (const unsigned long long*)nlist);
+    } else {
+      hipLaunchKernelGGL(k_leaf_hash, GRID(m, BS), dim3(BS), 0, st, T);
+    }
     LAUNCH_CHECK();
   }
   HIPCHK(hipEventRecord(c->ev[4], st));
@@ -2657,27 +2731,6 @@ __global__ void __launch_bounds__(BS) k_f_prep(const uint32_t* sidx, uint64_t n,
   isup[o] = up ? 1u : 0u;
   ulen[o] = up ? voff[s + 1] - voff[s] : 0;
 }
-// Slots for a whole block at once: one atomic per block (the gather's per-wave claims on the
-// one element counter serialised in L2).  Every thread of the block must call it.
-__device__ __forceinline__ uint64_t block_claim(unsigned long long* ctr, bool want, unsigned long long* lds) {
-  const uint64_t m = __ballot(want);
-  const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if ((threadIdx.x & 63) == 0) lds[w] = (unsigned long long)__popcll(m);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long run = 0;
-    for (uint32_t q = 0; q < nw; ++q) {
-      const unsigned long long c = lds[q];
-      lds[q] = run;
-      run += c;
-    }
-    lds[nw] = run ? atomicAdd(ctr, run) : 0;
-  }
-  __syncthreads();
-  const uint64_t e = lds[nw] + lds[w] + (uint64_t)__popcll(m & lanemask_lt());
-  __syncthreads();  // lds is reused by the next call
-  return e;
-}
 constexpr uint32_t GATHER_BS = 1024;
 __global__ void __launch_bounds__(GATHER_BS) k_f_gather(AMap M, Recs R, const uint32_t* touched, const uint8_t* replaced,
                                                  const uint32_t* tlist, const unsigned long long* ntl_p,
@@ -2774,25 +2827,34 @@ __global__ void __launch_bounds__(BS) k_f_branch_recs(Topo T, const uint32_t* Bp
 // upsert) for the scan of their ids, and the write-back selection: an upsert's leaf, a leaf
 // whose anchor moved, and a subtree's new extension (a subtree hanging at its own depth has
 // no node of its own)
-__global__ void __launch_bounds__(BS) k_f_elem_flags(Topo T, Elems E, uint8_t* sel, uint32_t* isnew, uint32_t* src) {
+// The anchor map is touched only where an anchor changes: an element keeping its source
+// record at the same anchor (most of them: the untouched children of the opened branches)
+// keeps its map slot.  src[i]: the source record to take out of the map (moved, not touched:
+// the touched ones go with the touched list), NONE otherwise; rein[i]: the element's record
+// is (re)inserted (new, moved, or a touched leaf no op replaced, whose anchor goes with the
+// touched list).
+__global__ void __launch_bounds__(BS) k_f_elem_flags(Topo T, Elems E, const uint32_t* touched, uint8_t* sel,
+                                                     uint32_t* isnew, uint32_t* src, uint8_t* rein) {
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= T.m) return;
   const uint32_t s = T.sidx[i], a = (uint32_t)(T.lf_pd[i] + 1);
   const uint32_t es = E.src[s];
-  src[i] = es;
-  isnew[i] = es == NONE ? 1u : 0u;
   const bool moved = es == NONE || E.oldd[s] != a;
+  const bool tch = es != NONE && touched[es] != 0;
+  src[i] = (moved && es != NONE && !tch) ? es : NONE;
+  rein[i] = (moved || tch) ? 1 : 0;
+  isnew[i] = es == NONE ? 1u : 0u;
   const bool sub = T.el_db[i] != EL_LEAF;
   sel[i] = (moved && !(sub && T.el_db[i] == a)) ? 1 : 0;
 }
 // element records: an upsert's new record (id base + rank), or its source record re-anchored
 __global__ void __launch_bounds__(BS) k_f_elem_recs(Topo T, Elems E, const uint32_t* tries, const uint32_t* newrank,
-                                                    Recs R, uint64_t base, uint32_t* eid) {
+                                                    const uint8_t* rein, Recs R, uint64_t base, uint32_t* eid) {
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= T.m) return;
   const uint32_t s = T.sidx[i], src = E.src[s];
   const uint64_t r = src == NONE ? base + newrank[i] : src;
-  eid[i] = (uint32_t)r;
+  eid[i] = rein[i] ? (uint32_t)r : NONE;
   RecVal v;
   for (int q = 0; q < 4; ++q) {
     v.k[q] = T.skey[4 * i + q];
@@ -2841,22 +2903,31 @@ __global__ void __launch_bounds__(BS) k_rec_dead(Recs R, const uint32_t* list, u
 }
 // insert records at their anchors: base + i for i < nb, then list[i - nb] for the next n
 // (list may be null when n is 0)
+// (list entries NONE are skipped; used, when given, counts the inserts that took an empty
+// slot: the table's load, live + tombstones)
 __global__ void __launch_bounds__(BS) k_map_insert(AMap M, Recs R, uint64_t base, uint64_t nb, const uint32_t* list,
-                                                   uint64_t n, unsigned long long* err) {
+                                                   uint64_t n, unsigned long long* err, unsigned long long* used) {
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i >= nb + n) return;
-  const uint32_t r = i < nb ? (uint32_t)(base + i) : list[i - nb];
-  if (R.rlive[r] != REC_LIVE) return;
-  const unsigned long long h = anchor_tag(R.rt[r], R.rd[r], R.key(r));
-  for (uint64_t s = h & M.mask, k = 0; k <= M.mask; s = (s + 1) & M.mask, ++k) {
-    unsigned long long g = M.tag[s];
-    if (g > 1) continue;
-    if (atomicCAS(&M.tag[s], g, h) == g) {
-      M.rec[s] = r;
-      return;
+  bool fresh = false;
+  if (i < nb + n) {
+    const uint32_t r = i < nb ? (uint32_t)(base + i) : list[i - nb];
+    if (r != NONE && R.rlive[r] == REC_LIVE) {
+      const unsigned long long h = anchor_tag(R.rt[r], R.rd[r], R.key(r));
+      bool done = false;
+      for (uint64_t s = h & M.mask, k = 0; k <= M.mask; s = (s + 1) & M.mask, ++k) {
+        unsigned long long g = M.tag[s];
+        if (g > 1) continue;
+        if (atomicCAS(&M.tag[s], g, h) == g) {
+          M.rec[s] = r;
+          fresh = g == 0;
+          done = true;
+          break;
+        }
+      }
+      if (!done) *err = 5;  // full table
     }
   }
-  *err = 5;  // full table
+  if (used) wave_atomic_add(used, fresh ? 1ULL : 0ULL);
 }
 // per touched trie: its new root (segment result), EMPTY when no element remained
 __global__ void k_f_roots(const uint64_t* res_hash, const uint32_t* res_len, uint32_t nt, uint64_t* roots) {
@@ -2957,7 +3028,7 @@ static void map_rebuild(kh_trie* h, uint64_t headroom) {
   HIPCHK(hipMemsetAsync(err, 0, 16, st));
   if (h->rn) {
     hipLaunchKernelGGL(k_map_insert, GRID(h->rn, BS), dim3(BS), 0, st, map_of(h), recs_of(h), (uint64_t)0, h->rn,
-                       (const uint32_t*)nullptr, (uint64_t)0, err);
+                       (const uint32_t*)nullptr, (uint64_t)0, err, (unsigned long long*)nullptr);
     hipLaunchKernelGGL(k_rec_count_live, GRID(h->rn, BS), dim3(BS), 0, st, recs_of(h), h->rn, err + 1);
   }
   LAUNCH_CHECK();
@@ -3330,12 +3401,14 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   const uint64_t base_b = h->rn, base_e = h->rn + B;
   Recs R = recs_of(h);
   AMap M = map_of(h);
+  bool count_fresh = false;  // fctr[4] holds this commit's fresh map slots
   uint32_t *isnew = nullptr, *nrank = nullptr, *eid = nullptr, *esrc = nullptr;
   uint8_t* sel = nullptr;
   if (ne) {
-    h->selb.ensure(carve_size({m + 2 * B, m * 4, m * 4, m * 4, m * 4, scan_scratch_bytes(m + 1, 4), 64}));
+    h->selb.ensure(carve_size({m + 2 * B, m * 4, m * 4, m * 4, m * 4, m, scan_scratch_bytes(m + 1, 4), 64}));
     Carver cs{(char*)h->selb.p, 0, h->selb.cap};
     sel = cs.take<uint8_t>(m + 2 * B);
+    uint8_t* rein = cs.take<uint8_t>(m);
     isnew = cs.take<uint32_t>(m);
     nrank = cs.take<uint32_t>(m);
     eid = cs.take<uint32_t>(m);
@@ -3347,7 +3420,8 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
       hipLaunchKernelGGL(k_f_branch_recs, GRID(B, BS), dim3(BS), 0, st, T, (const uint32_t*)(T.ctr + CTR_B),
                          (const uint32_t*)tries, M, R, base_b, sel);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_f_elem_flags, GRID(m, BS), dim3(BS), 0, st, T, E, sel, isnew, esrc);
+    hipLaunchKernelGGL(k_f_elem_flags, GRID(m, BS), dim3(BS), 0, st, T, E, (const uint32_t*)h->touched.p, sel, isnew,
+                       esrc, rein);
     LAUNCH_CHECK();
     scan_exclusive<uint32_t>(isnew, nrank, m, tot, sscr, st);
     // old anchors out of the map (touched records, element sources), then touched records die
@@ -3359,18 +3433,19 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                          (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_f_elem_recs, GRID(m, BS), dim3(BS), 0, st, T, E, (const uint32_t*)tries,
-                       (const uint32_t*)nrank, R, base_e, eid);
+                       (const uint32_t*)nrank, (const uint8_t*)rein, R, base_e, eid);
     LAUNCH_CHECK();
     // map capacity: rebuild when live + tombstones would pass half the table
     h->rn = base_e + nnew;
     if (2 * (h->mused + B + m + 1024) > h->mcap) {
       map_rebuild(h, B + m);
     } else {
-      unsigned long long* err = fctr + 3;
+      // (the table's load grows by the inserts that took an empty slot: fctr[4], read at the
+      // final sync; B + m bounds it for the rebuild test above)
       hipLaunchKernelGGL(k_map_insert, GRID(B + m, BS), dim3(BS), 0, st, M, R, base_b, B, (const uint32_t*)eid, m,
-                         err);
+                         fctr + 3, fctr + 4);
       LAUNCH_CHECK();
-      h->mused += B + m;
+      count_fresh = true;
     }
     hipLaunchKernelGGL(k_f_roots, GRID(nt, BS), dim3(BS), 0, st, (const uint64_t*)T.res_hash,
                        (const uint32_t*)T.res_len, nt, roots);
@@ -3412,8 +3487,9 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   uint8_t* hs = pinned_stage(c, o_ctr + ctr_bytes);
   if (nt) HIPCHK(hipMemcpyAsync(hs, tries, tr_bytes, hipMemcpyDeviceToHost, st));
   if (ne) HIPCHK(hipMemcpyAsync(hs + o_ctr, c->T.ctr, ctr_bytes, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(c->h_pinned, fctr + 3, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(c->h_pinned, fctr + 3, 16, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (count_fresh) h->mused += c->h_pinned[1];
   memcpy(h->tries.data(), hs, (uint64_t)nt * 4);
   memcpy(h->roots.data(), hs + o_roots, (uint64_t)nt * 32);
   if (ne) build_stats(c, (const unsigned long long*)(hs + o_ctr), &bst);
@@ -3449,7 +3525,7 @@ int kh_ctx_destroy(kh_ctx* c) {
   API_TRY({
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->st);
-    for (DevBuf* b : {&c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->in_kn, &c->in_aux, &c->in_block, &c->out_emit,
+    for (DevBuf* b : {&c->ws_list, &c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->in_kn, &c->in_aux, &c->in_block, &c->out_emit,
                       &c->emit_dev})
       b->release();
     for (auto& e : c->ev)

@@ -275,16 +275,17 @@ constexpr int RS_WAVES = RS_THREADS / 64;
 constexpr int RS_WSLICE = RS_TILE / RS_WAVES;   // 512 keys per wave
 constexpr uint32_t RS_FUSE_TILES = 64;          // radix_sort_pairs: scan-free passes up to 256k keys
 
-template <typename K>
+template <typename K, int IT = RS_ITEMS>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const K* keys, uint64_t n, int shift, uint32_t* counts,
                                                         uint32_t ntiles) {
+  constexpr int TILE = RS_THREADS * IT, WSLICE = TILE / RS_WAVES;
   __shared__ uint32_t h[RS_WAVES][256];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
   __syncthreads();
-  uint64_t base = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * RS_WSLICE;
+  uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)w * WSLICE;
 #pragma unroll 4
-  for (int it = 0; it < RS_WSLICE / 64; ++it) {
+  for (int it = 0; it < WSLICE / 64; ++it) {
     uint64_t i = base + (uint64_t)it * 64 + lane;
     if (i < n) atomicAdd(&h[w][(keys[i] >> shift) & 0xFF], 1u);
   }
@@ -301,26 +302,27 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const K* keys, uint64_t 
 // LDS in digit order for the whole tile, then written out so that each digit's
 // run of the tile goes to consecutive global addresses (coalesced stores instead
 // of one scattered 8-byte store per key).
-template <typename K>
+template <typename K, int IT = RS_ITEMS>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const uint32_t* vals, K* okeys,
                                                            uint32_t* ovals, uint64_t n, int shift,
                                                            const uint32_t* offs, uint32_t ntiles, bool fused) {
+  constexpr int TILE = RS_THREADS * IT, WSLICE = TILE / RS_WAVES;
   __shared__ uint32_t wc[RS_WAVES][256];
   __shared__ uint32_t tstart[256], gbase[256];
   __shared__ uint32_t lw[RS_THREADS / 64];
-  __shared__ K sk[RS_TILE];
-  __shared__ uint32_t sv[RS_TILE];
+  __shared__ K sk[TILE];
+  __shared__ uint32_t sv[TILE];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&wc[0][0])[i] = 0;
   __syncthreads();
-  const uint64_t tbase = (uint64_t)blockIdx.x * RS_TILE;
-  const uint64_t base = tbase + (uint64_t)w * RS_WSLICE;
-  K k[RS_ITEMS];
-  uint32_t v[RS_ITEMS];
-  uint32_t r[RS_ITEMS];
+  const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
+  const uint64_t base = tbase + (uint64_t)w * WSLICE;
+  K k[IT];
+  uint32_t v[IT];
+  uint32_t r[IT];
   const uint64_t lt = lanemask_lt();
 #pragma unroll
-  for (int it = 0; it < RS_ITEMS; ++it) {
+  for (int it = 0; it < IT; ++it) {
     uint64_t i = base + (uint64_t)it * 64 + lane;
     bool valid = i < n;
     k[it] = valid ? keys[i] : 0;
@@ -368,7 +370,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const 
   }
   __syncthreads();
 #pragma unroll
-  for (int it = 0; it < RS_ITEMS; ++it) {
+  for (int it = 0; it < IT; ++it) {
     uint64_t i = base + (uint64_t)it * 64 + lane;
     if (i < n) {
       uint32_t d = (uint32_t)(k[it] >> shift) & 0xFF;
@@ -378,7 +380,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const 
     }
   }
   __syncthreads();
-  const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)RS_TILE ? (n - tbase) : (uint64_t)RS_TILE);
+  const uint32_t tn = (uint32_t)((n - tbase) < (uint64_t)TILE ? (n - tbase) : (uint64_t)TILE);
   for (uint32_t li = threadIdx.x; li < tn; li += RS_THREADS) {
     K key = sk[li];
     uint32_t d = (uint32_t)(key >> shift) & 0xFF;
@@ -388,8 +390,14 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const 
   }
 }
 
+// Small sorts (a block commit's ops and elements, up to RS_SMALL_N keys) take 1024-key tiles
+// (4 keys per thread): 4x the blocks, a quarter of each block's serial ranking -- the passes
+// are latency-bound at these sizes.
+constexpr int RS_SMALL_ITEMS = 4;
+constexpr uint64_t RS_SMALL_N = (uint64_t)RS_FUSE_TILES * RS_THREADS * RS_SMALL_ITEMS;  // 65536
 inline size_t radix_scratch_bytes(uint64_t n) {
   uint64_t tiles = (n + RS_TILE - 1) / RS_TILE;
+  if (n <= RS_SMALL_N) tiles = (n + RS_THREADS * RS_SMALL_ITEMS - 1) / (RS_THREADS * RS_SMALL_ITEMS);
   uint64_t c = tiles * 256;
   return c * sizeof(uint32_t) + 256 + scan_scratch_bytes(c, sizeof(uint32_t));
 }
@@ -401,7 +409,9 @@ template <typename K>
 inline bool radix_sort_pairs(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n, int lo_bit, int hi_bit,
                              void* scratch, hipStream_t st) {
   if (n <= 1) return false;
-  uint32_t tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+  const bool small = n <= RS_SMALL_N;
+  const uint32_t tile = small ? RS_THREADS * RS_SMALL_ITEMS : RS_TILE;
+  uint32_t tiles = (uint32_t)((n + tile - 1) / tile);
   uint32_t* counts = (uint32_t*)scratch;
   void* scan_ws = (char*)scratch + (((uint64_t)tiles * 256 * sizeof(uint32_t) + 255) / 256) * 256;
   bool flip = false;
@@ -413,10 +423,17 @@ inline bool radix_sort_pairs(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t 
     uint32_t* iv = flip ? v1 : v0;
     K* ok = flip ? k0 : k1;
     uint32_t* ov = flip ? v0 : v1;
-    hipLaunchKernelGGL(k_rs_hist<K>, dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik, n, sh, counts, tiles);
-    if (!fused) scan_exclusive<uint32_t>(counts, counts, (uint64_t)tiles * 256, (uint32_t*)nullptr, scan_ws, st);
-    hipLaunchKernelGGL(k_rs_scatter<K>, dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik, (const uint32_t*)iv, ok,
-                       ov, n, sh, (const uint32_t*)counts, tiles, fused);
+    if (small) {
+      hipLaunchKernelGGL((k_rs_hist<K, RS_SMALL_ITEMS>), dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik, n, sh,
+                         counts, tiles);
+      hipLaunchKernelGGL((k_rs_scatter<K, RS_SMALL_ITEMS>), dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik,
+                         (const uint32_t*)iv, ok, ov, n, sh, (const uint32_t*)counts, tiles, true);
+    } else {
+      hipLaunchKernelGGL(k_rs_hist<K>, dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik, n, sh, counts, tiles);
+      if (!fused) scan_exclusive<uint32_t>(counts, counts, (uint64_t)tiles * 256, (uint32_t*)nullptr, scan_ws, st);
+      hipLaunchKernelGGL(k_rs_scatter<K>, dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik, (const uint32_t*)iv, ok,
+                         ov, n, sh, (const uint32_t*)counts, tiles, fused);
+    }
     flip = !flip;
   }
   return flip;
