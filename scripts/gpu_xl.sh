@@ -15,3 +15,5 @@ step CFG2 timeout -k 10 400 python scripts/bench_configs.py --cfg 3 > gpurun_out
 cut -c180-330 gpurun_out/cfg2_$tag.jsonl
 step BENCH timeout -k 10 600 python bench.py --no-cpu > gpurun_out/bench_$tag.json 2> gpurun_out/bench_$tag.err
 cut -c1-700 gpurun_out/bench_$tag.json
+step API timeout -k 10 400 rocprofv3 --kernel-trace --hip-trace --output-format csv -d gpurun_out/bca_$tag -o bca -- python3 scripts/block_commit_prof.py > gpurun_out/bca_$tag.log 2>&1
+python3 scripts/api_trace.py gpurun_out/bca_$tag > gpurun_out/api_$tag.json && head -60 gpurun_out/api_$tag.json
