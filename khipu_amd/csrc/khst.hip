@@ -386,15 +386,24 @@ __global__ void __launch_bounds__(BS) k_val_gather(Topo T) {
 }
 
 // element builds: the element properties in sorted order
-__global__ void __launch_bounds__(BS) k_el_gather(const uint32_t* sidx, uint64_t m, const uint8_t* db,
-                                                  const uint64_t* bref, const uint8_t* brl, uint8_t* odb,
-                                                  uint64_t* obref, uint8_t* obrl) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i >= m) return;
-  const uint32_t s = sidx[i];
+// element build: the value spans (op_val_gather) and both element property sets in sorted
+// order, one launch
+__global__ void __launch_bounds__(BS) k_el_gather3(Topo T, const uint8_t* db, const uint64_t* bref, const uint8_t* brl,
+                                                   uint8_t* odb, uint64_t* obref, uint8_t* obrl, const uint8_t* db2,
+                                                   const uint64_t* bref2, const uint8_t* brl2, uint8_t* odb2,
+                                                   uint64_t* obref2, uint8_t* obrl2) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= T.m) return;
+  op_val_gather(T, i);
+  const uint32_t s = T.sidx[i];
   odb[i] = db[s];
-  for (int q = 0; q < 4; ++q) obref[4 * i + q] = bref[4ull * s + q];
+  odb2[i] = db2[s];
+  for (int q = 0; q < 4; ++q) {
+    obref[4 * i + q] = bref[4ull * s + q];
+    obref2[4 * i + q] = bref2[4ull * s + q];
+  }
   obrl[i] = brl[s];
+  obrl2[i] = brl2[s];
 }
 
 // ties_u: boundaries between equal 32-bit prefixes were valued by the tie-run kernel
@@ -404,9 +413,23 @@ __global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb, bool ties_u) {
   if (ties_u && T.sck[b] == T.sck[b + 1]) return;
   op_lcp(T, b);
 }
-__global__ void __launch_bounds__(BS) k_min64(const uint8_t* in, uint64_t nin, uint8_t* out, uint64_t nout) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i < nout) op_min64(in, nin, out, i);
+// the 64-ary min pyramid over the boundary values: level 1 by the whole grid, the (small)
+// upper levels by the last block to finish (the counter *done starts at zero)
+__global__ void __launch_bounds__(BS) k_pyramid(Pyr P, unsigned int* done) {
+  __shared__ bool last;
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < P.sz[1]) op_min64(P.lv[0], P.sz[0], (uint8_t*)P.lv[1], i);
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  for (int l = 2; l < P.nl; ++l) {
+    for (uint64_t k = threadIdx.x; k < P.sz[l]; k += BS) op_min64(P.lv[l - 1], P.sz[l - 1], (uint8_t*)P.lv[l], k);
+    __threadfence_block();
+    __syncthreads();
+  }
 }
 
 __global__ void __launch_bounds__(BS) k_ansv(Topo T, Pyr P, uint64_t nb) {
@@ -567,9 +590,10 @@ __device__ __forceinline__ uint64_t block_claim(unsigned long long* ctr, bool wa
   __syncthreads();  // lds is reused by the next call
   return e;
 }
-__global__ void __launch_bounds__(BS) k_leaf_prep(Topo T) {
+__global__ void __launch_bounds__(BS) k_leaf_prep(Topo T, unsigned long long* zero) {
   __shared__ uint64_t stage[BS * STAGE_WORDS];
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (zero && i == 0) *zero = 0;  // (a counter of the next kernel)
   const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u;
   uint64_t off = 0;
   uint32_t vlen = 0;
@@ -2035,8 +2059,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     T.svlen = nullptr;
   } else {
     if (A.vals_ready) HIPCHK(hipStreamWaitEvent(st, A.vals_ready, 0));
-    hipLaunchKernelGGL(k_val_gather, GRID(m, BS), dim3(BS), 0, st, T);
-    LAUNCH_CHECK();
+    if (!A.el) {  // (element builds gather their spans with the element properties below)
+      hipLaunchKernelGGL(k_val_gather, GRID(m, BS), dim3(BS), 0, st, T);
+      LAUNCH_CHECK();
+    }
   }
   if (A.kn) {
     hipLaunchKernelGGL(k_kn_gather, GRID(m, BS), dim3(BS), 0, st, A.kn, (const uint32_t*)sidx, m, skn);
@@ -2055,10 +2081,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     uint8_t* ecrl = ce.take<uint8_t>(m);
     T.lf_ref = ce.take<uint64_t>(m * 4);
     T.lf_rlen = ce.take<uint32_t>(m);
-    hipLaunchKernelGGL(k_el_gather, GRID(m, BS), dim3(BS), 0, st, (const uint32_t*)T.sidx, m, E.db, E.bref, E.brl,
-                       edb, ebref, ebrl);
-    hipLaunchKernelGGL(k_el_gather, GRID(m, BS), dim3(BS), 0, st, (const uint32_t*)T.sidx, m, E.oldd, E.cref, E.crl,
-                       eoldd, ecref, ecrl);
+    hipLaunchKernelGGL(k_el_gather3, GRID(m, BS), dim3(BS), 0, st, T, E.db, E.bref, E.brl, edb, ebref, ebrl, E.oldd,
+                       E.cref, E.crl, eoldd, ecref, ecrl);
     LAUNCH_CHECK();
     T.el_db = edb;
     T.el_bref = ebref;
@@ -2073,7 +2097,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   const uint64_t nb = m - 1;
   unsigned long long* ctr = T.ctr;
   uint32_t* Bp = (uint32_t*)(ctr + CTR_B);
-  HIPCHK(hipMemsetAsync(ctr + CTR_B, 0, 8 * 6, st));  // B, br bytes, lf bytes, C, E0, E1
+  // (B, br bytes, lf bytes, C, E0, E1: zero since the counter block's memset; the sort uses
+  // only CTR_TIE / CTR_M)
   Pyr P{};
   // Grid of the topology kernels that run beside the leaf kernel (early builds): capped at
   // 4 blocks per CU, so they leave the leaf kernel more of the machine and still finish
@@ -2140,12 +2165,14 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     while (P.sz[P.nl - 1] > 64) {
       if (P.nl >= 8) throw KhError{KH_EINTERNAL, "pyramid too deep"};
       uint64_t nin = P.sz[P.nl - 1], nout = (nin + 63) / 64;
-      hipLaunchKernelGGL(k_min64, GRID(nout, BS), dim3(BS), 0, st, P.lv[P.nl - 1], nin, pp, nout);
-      LAUNCH_CHECK();
       P.lv[P.nl] = pp;
       P.sz[P.nl] = nout;
       P.nl++;
       pp += (nout + 255) & ~(uint64_t)255;
+    }
+    if (P.nl > 1) {  // every level in one launch (the last block to finish level 1 does the rest)
+      hipLaunchKernelGGL(k_pyramid, GRID(P.sz[1], BS), dim3(BS), 0, st, P, (unsigned int*)(ctr + CTR_PYR));
+      LAUNCH_CHECK();
     }
     HIPCHK(hipMemsetAsync(T.glast, 1, nb, st));
     if (pd_mode == 2) {  // the leaves need only u: they start here, beside the whole topology
@@ -2311,14 +2338,17 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       LAUNCH_CHECK();
     }
   } else {  // write-back and element builds: encodings kept in message slots, then hashed
-    hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T);
-    LAUNCH_CHECK();
-    if (A.el) {  // the re-encoded elements hashed from a list (k_leaf_pub)
+    unsigned long long* nlist = nullptr;  // element builds: the re-encoded leaves' list (k_leaf_pub)
+    uint32_t* list = nullptr;
+    if (A.el) {
       c->ws_list.ensure(carve_size({64, m * 4}));
       Carver cl{(char*)c->ws_list.p, 0, c->ws_list.cap};
-      unsigned long long* nlist = cl.take<unsigned long long>(8);
-      uint32_t* list = cl.take<uint32_t>(m);
-      HIPCHK(hipMemsetAsync(nlist, 0, 8, st));
+      nlist = cl.take<unsigned long long>(8);
+      list = cl.take<uint32_t>(m);
+    }
+    hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T, nlist);  // (zeroes *nlist)
+    LAUNCH_CHECK();
+    if (A.el) {  // the re-encoded elements hashed from a list
       hipLaunchKernelGGL(k_leaf_pub, GRID(m, BS), dim3(BS), 0, st, T, list, nlist);
       const uint64_t lblocks = std::min<uint64_t>((uint64_t)c->n_cu * 4, (m + BS - 1) / BS);
       hipLaunchKernelGGL(k_leaf_hash_list, dim3((unsigned)std::max<uint64_t>(lblocks, 1)), dim3(BS), 0, st, T,
@@ -2409,22 +2439,27 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
 
 // The counters of the last build (host copy hc of T.ctr) -> kh_stats; throws on a device
 // invariant flag.  Call once the build's stream work has completed (its events are read).
+// the build's counters summed over their shards: hashes, perms, inline, extensions, error
+constexpr int BSUM_N = 5;
+static void build_stats_sums(kh_ctx* c, const unsigned long long* sums, kh_stats* stats);
 static void build_stats(kh_ctx* c, const unsigned long long* hc, kh_stats* stats) {
-  if (hc[CTR_ERR]) throw KhError{KH_EINTERNAL, "build: device invariant violated"};
+  unsigned long long sums[BSUM_N] = {0, 0, 0, 0, hc[CTR_ERR]};
+  const int idx[4] = {CTR_HASHES, CTR_PERMS, CTR_INLINE, CTR_EXT};
+  for (int k = 0; k < 4; ++k)
+    for (int r = 0; r < CTR_SHARDS; ++r) sums[k] += hc[r * CTR_N + idx[k]];
+  build_stats_sums(c, sums, stats);
+}
+static void build_stats_sums(kh_ctx* c, const unsigned long long* sums, kh_stats* stats) {
+  if (sums[4]) throw KhError{KH_EINTERNAL, "build: device invariant violated"};
   if (!stats) return;
   const BuildInfo& bi = c->binfo;
   stats->n_inputs = bi.n;
   stats->n_leaves = bi.m;
   stats->n_branches = bi.B;
-  auto stat = [&](int idx) {
-    unsigned long long t = 0;
-    for (int r = 0; r < CTR_SHARDS; ++r) t += hc[r * CTR_N + idx];
-    return t;
-  };
-  stats->n_node_hashes = stat(CTR_HASHES);
-  stats->n_node_perms = stat(CTR_PERMS);
-  stats->n_inline = stat(CTR_INLINE);
-  stats->n_extensions = stat(CTR_EXT);
+  stats->n_node_hashes = sums[0];
+  stats->n_node_perms = sums[1];
+  stats->n_inline = sums[2];
+  stats->n_extensions = sums[3];
   stats->n_key_perms = bi.key_perms;
   stats->arena_bytes = bi.arena;
   stats->n_levels = bi.levels;
@@ -2716,8 +2751,9 @@ __global__ void __launch_bounds__(BS) k_f_ops_post(FOps O, const uint32_t* sidx,
 // A single-trie commit (segd false) writes its trie ids (0) here too.
 __global__ void __launch_bounds__(BS) k_f_prep(const uint32_t* sidx, uint64_t n, uint64_t nup, bool segd,
                                                uint32_t* trie, const uint64_t* voff, uint8_t* kind, uint32_t* tflag,
-                                               uint32_t* isup, uint64_t* ulen) {
+                                               uint32_t* isup, uint64_t* ulen, unsigned long long* fctr) {
   const uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o < 8) fctr[o] = 0;
   if (o >= n) return;
   const uint32_t s = sidx[o];
   const bool up = s < nup;
@@ -2875,14 +2911,21 @@ __global__ void __launch_bounds__(BS) k_f_elem_recs(Topo T, Elems E, const uint3
 }
 // map maintenance: delete records' current anchors (two lists in one launch: the touched
 // records, then the element sources), mark dead, insert
+// (the first list's records -- the touched ones -- also die here: marked dead, flags cleared)
 __global__ void __launch_bounds__(BS) k_map_delete(AMap M, Recs R, const uint32_t* list, uint64_t n,
-                                                   const uint32_t* list2, uint64_t n2) {
+                                                   const uint32_t* list2, uint64_t n2, uint32_t* touched,
+                                                   uint8_t* replaced) {
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n + n2) return;
   const uint32_t r = i < n ? list[i] : list2[i - n];
   if (r == NONE) return;
   const uint64_t sl = map_slot_of(M, R, r);
   if (sl != ~0ULL) M.tag[sl] = 1;  // tombstone
+  if (i < n) {
+    R.rlive[r] = REC_DEAD;
+    touched[r] = 0;
+    replaced[r] = 0;
+  }
 }
 // an aborted commit: the records its descent flagged are left as they were
 __global__ void __launch_bounds__(BS) k_f_untouch(const uint32_t* list, uint64_t n, uint32_t* touched,
@@ -2891,15 +2934,6 @@ __global__ void __launch_bounds__(BS) k_f_untouch(const uint32_t* list, uint64_t
   if (i >= n) return;
   touched[list[i]] = 0;
   replaced[list[i]] = 0;
-}
-__global__ void __launch_bounds__(BS) k_rec_dead(Recs R, const uint32_t* list, uint64_t n, uint32_t* touched,
-                                                 uint8_t* replaced) {
-  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t r = list[i];
-  R.rlive[r] = REC_DEAD;
-  touched[r] = 0;
-  replaced[r] = 0;
 }
 // insert records at their anchors: base + i for i < nb, then list[i - nb] for the next n
 // (list may be null when n is 0)
@@ -2930,7 +2964,24 @@ __global__ void __launch_bounds__(BS) k_map_insert(AMap M, Recs R, uint64_t base
   if (used) wave_atomic_add(used, fresh ? 1ULL : 0ULL);
 }
 // per touched trie: its new root (segment result), EMPTY when no element remained
-__global__ void k_f_roots(const uint64_t* res_hash, const uint32_t* res_len, uint32_t nt, uint64_t* roots) {
+// (block 0 also leaves the commit's final flags in tail: the element build's counters summed
+// over their shards (hashes, perms, inline, extensions, error; ctr null: none), the map
+// insert's error and fresh-slot count -- so the commit's last sync is one copy)
+__global__ void k_f_roots(const uint64_t* res_hash, const uint32_t* res_len, uint32_t nt, uint64_t* roots,
+                          const unsigned long long* ctr, const unsigned long long* fctr, unsigned long long* tail) {
+  if (blockIdx.x == 0 && threadIdx.x < 8) {
+    const int idx[5] = {CTR_HASHES, CTR_PERMS, CTR_INLINE, CTR_EXT, CTR_ERR};
+    unsigned long long v = 0;
+    if (threadIdx.x < 4) {
+      if (ctr)
+        for (int r = 0; r < CTR_SHARDS; ++r) v += ctr[r * CTR_N + idx[threadIdx.x]];
+    } else if (threadIdx.x == 4) {
+      v = ctr ? ctr[CTR_ERR] : 0;
+    } else if (threadIdx.x < 7) {
+      v = fctr[threadIdx.x - 2];  // 5: fctr[3] (map insert error), 6: fctr[4] (fresh slots)
+    }
+    tail[threadIdx.x] = v;
+  }
   const uint32_t s = blockIdx.x * BS + threadIdx.x;
   if (s >= nt) return;
   const uint64_t E[4] = {0xa655cc1b171fe856ULL, 0x6ef8c092e64583ffULL, 0xc0ad6c991be0485bULL, 0x21b463e3b52f6201ULL};
@@ -3262,17 +3313,30 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   sort_dedup(c, S);
   const uint64_t nd = S.m;
   uint32_t* otrie = segd ? S.sseg : sseg;  // the compaction of duplicates moves the sorted ids
+  // the descent's touched list and the commit's flags (fctr, zeroed by k_f_prep): [0] touched
+  // count, [1] replaced leaves, [2] anchor-map error, [3] refusal / map insert error,
+  // [4] fresh map slots, [5] element count
+  h->tlb.ensure(carve_size({nd * 70 * 4 + 64, 64}));
+  Carver c3{(char*)h->tlb.p, 0, h->tlb.cap};
+  uint32_t* tlist = c3.take<uint32_t>(nd * 70 + 16);
+  unsigned long long* fctr = c3.take<unsigned long long>(8);
   // kinds, the distinct tries of the batch (sorted: the segments of the element build), and
   // the upserts' ranks and value offsets (their values go to the heap)
   hipLaunchKernelGGL(k_f_prep, GRID(nd, BS), dim3(BS), 0, st, (const uint32_t*)S.sidx, nd, F.nup, segd, otrie,
-                     F.up_voff, kind, tflag, isup, ulen);
+                     F.up_voff, kind, tflag, isup, ulen, fctr);
   LAUNCH_CHECK();
   FOps O{(const uint64_t*)S.skey, (const uint32_t*)otrie, (const uint8_t*)kind, nd};
   uint32_t* ntp = (uint32_t*)(S.ctr + 12);
-  scan_exclusive<uint32_t>(tflag, tpos, nd, ntp, S.scan_scratch, st);
   uint32_t* nupp = (uint32_t*)(S.ctr + 13);
-  scan_exclusive<uint32_t>(isup, ur, nd, nupp, S.scan_scratch, st);
-  scan_exclusive<uint64_t>(ulen, uoff, nd, (uint64_t*)(S.ctr + 14), S.scan_scratch, st);
+  if (nd <= SCAN_SMALL_MAX) {  // the three scans in one launch
+    hipLaunchKernelGGL(k_scan_small3, dim3(3), dim3(SCAN_SMALL_THREADS), 0, st, ScanJob{tflag, tpos, ntp, false},
+                       ScanJob{isup, ur, nupp, false}, ScanJob{ulen, uoff, S.ctr + 14, true}, nd);
+    LAUNCH_CHECK();
+  } else {
+    scan_exclusive<uint32_t>(tflag, tpos, nd, ntp, S.scan_scratch, st);
+    scan_exclusive<uint32_t>(isup, ur, nd, nupp, S.scan_scratch, st);
+    scan_exclusive<uint64_t>(ulen, uoff, nd, (uint64_t*)(S.ctr + 14), S.scan_scratch, st);
+  }
   HIPCHK(hipMemcpyAsync(c->h_pinned, S.ctr + 12, 3 * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const uint32_t nt = (uint32_t)c->h_pinned[0], nups = (uint32_t)c->h_pinned[1];
@@ -3280,10 +3344,11 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   // ---- trie list; upsert values into the heap (appended past heap_n, which moves only once
   // the commit is accepted): uoff is the exclusive scan of their lengths over the sorted
   // ops, uo the same offsets by upsert rank (uo[nups] = total)
-  h->tbuf.ensure(carve_size({(uint64_t)nt * 4, (uint64_t)nt * 32}));
+  h->tbuf.ensure(carve_size({(uint64_t)nt * 4, (uint64_t)nt * 32, 64}));
   Carver ct{(char*)h->tbuf.p, 0, h->tbuf.cap};
   uint32_t* tries = ct.take<uint32_t>(nt);
   uint64_t* roots = ct.take<uint64_t>((uint64_t)nt * 4);
+  unsigned long long* tail = ct.take<unsigned long long>(8);  // k_f_roots: the final flags
   h->d_tries = tries;
   h->d_roots = roots;
   regrow(h->heap, h->heap_n, h->heap_n + ubytes + 64, st);
@@ -3297,11 +3362,6 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   // ---- 2. descent: opened branches and touched leaves
   recs_reserve(h, h->rn + 16);
   if (h->mcap == 0) map_rebuild(h, nops + 1024);
-  h->tlb.ensure(carve_size({nd * 70 * 4 + 64, 64}));
-  Carver c3{(char*)h->tlb.p, 0, h->tlb.cap};
-  uint32_t* tlist = c3.take<uint32_t>(nd * 70 + 16);
-  unsigned long long* fctr = c3.take<unsigned long long>(8);
-  HIPCHK(hipMemsetAsync(fctr, 0, 64, st));
   hipLaunchKernelGGL(k_f_descend, GRID(nd, BS), dim3(BS), 0, st, O, map_of(h), recs_of(h), (uint32_t*)h->touched.p,
                      (uint8_t*)h->replaced.p, tlist, fctr);
   LAUNCH_CHECK();
@@ -3332,7 +3392,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     E.oldd = ce.take<uint8_t>(ecap);
     E.cref = ce.take<uint64_t>(ecap * 4);
     E.crl = ce.take<uint8_t>(ecap);
-    E.n = ce.take<unsigned long long>(8);
+    E.n = fctr + 5;
     E.cap = ecap;
     // (the record elements are pushed after the upserts: k_f_upsert_elems sets E.n = nups)
     hipLaunchKernelGGL(k_f_upsert_elems, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)tries, nt,
@@ -3345,8 +3405,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     hipLaunchKernelGGL(k_f_gather_roots, GRID(nt, BS), dim3(BS), 0, st, map_of(h), recs_of(h),
                        (const uint32_t*)h->touched.p, (const uint32_t*)tries, nt, E);
     LAUNCH_CHECK();
-    HIPCHK(hipMemcpyAsync(c->h_pinned, fctr, 32, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(c->h_pinned + 4, E.n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned, fctr, 48, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return ecap;
   };
@@ -3366,10 +3425,10 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                   "does not reproduce; the trie is unchanged"};
   }
   if (c->h_pinned[2]) throw KhError{KH_EINTERNAL, "forest gather: corrupt anchor map"};
-  uint64_t ne = c->h_pinned[4];
+  uint64_t ne = c->h_pinned[5];
   if (ne > ecap) {  // the guess was short: the exact capacity, gathered again
     ecap = gather(ntl);
-    ne = c->h_pinned[4];
+    ne = c->h_pinned[5];
     if (c->h_pinned[2]) throw KhError{KH_EINTERNAL, "forest gather: corrupt anchor map"};
   }
   if (ne > ecap) throw KhError{KH_EINTERNAL, "forest gather: element overflow"};
@@ -3426,11 +3485,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     scan_exclusive<uint32_t>(isnew, nrank, m, tot, sscr, st);
     // old anchors out of the map (touched records, element sources), then touched records die
     hipLaunchKernelGGL(k_map_delete, GRID(ntl + m, BS), dim3(BS), 0, st, M, R, (const uint32_t*)tlist, ntl,
-                       (const uint32_t*)esrc, m);
-    LAUNCH_CHECK();
-    if (ntl)
-      hipLaunchKernelGGL(k_rec_dead, GRID(ntl, BS), dim3(BS), 0, st, R, (const uint32_t*)tlist, ntl,
-                         (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p);
+                       (const uint32_t*)esrc, m, (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_f_elem_recs, GRID(m, BS), dim3(BS), 0, st, T, E, (const uint32_t*)tries,
                        (const uint32_t*)nrank, (const uint8_t*)rein, R, base_e, eid);
@@ -3448,17 +3503,15 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
       count_fresh = true;
     }
     hipLaunchKernelGGL(k_f_roots, GRID(nt, BS), dim3(BS), 0, st, (const uint64_t*)T.res_hash,
-                       (const uint32_t*)T.res_len, nt, roots);
+                       (const uint32_t*)T.res_len, nt, roots, (const unsigned long long*)T.ctr,
+                       (const unsigned long long*)fctr, tail);
     LAUNCH_CHECK();
   } else {
     if (ntl)
       hipLaunchKernelGGL(k_map_delete, GRID(ntl, BS), dim3(BS), 0, st, M, R, (const uint32_t*)tlist, ntl,
-                         (const uint32_t*)nullptr, (uint64_t)0);
-    if (ntl)
-      hipLaunchKernelGGL(k_rec_dead, GRID(ntl, BS), dim3(BS), 0, st, R, (const uint32_t*)tlist, ntl,
-                         (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p);
+                         (const uint32_t*)nullptr, (uint64_t)0, (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p);
     hipLaunchKernelGGL(k_f_roots, GRID(nt, BS), dim3(BS), 0, st, (const uint64_t*)nullptr, (const uint32_t*)nullptr,
-                       nt, roots);
+                       nt, roots, (const unsigned long long*)nullptr, (const unsigned long long*)fctr, tail);
     LAUNCH_CHECK();
   }
   h->rn = base_e + nnew;
@@ -3482,18 +3535,17 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   // and the map's error flag.
   h->tries.resize(nt);
   h->roots.resize((uint64_t)nt * 32);
-  const size_t o_roots = (size_t)((char*)roots - (char*)tries), tr_bytes = o_roots + (size_t)nt * 32;
-  const size_t o_ctr = (tr_bytes + 63) & ~(size_t)63, ctr_bytes = (size_t)CTR_N * CTR_SHARDS * 8;
-  uint8_t* hs = pinned_stage(c, o_ctr + ctr_bytes);
-  if (nt) HIPCHK(hipMemcpyAsync(hs, tries, tr_bytes, hipMemcpyDeviceToHost, st));
-  if (ne) HIPCHK(hipMemcpyAsync(hs + o_ctr, c->T.ctr, ctr_bytes, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(c->h_pinned, fctr + 3, 16, hipMemcpyDeviceToHost, st));
+  // (k_f_roots left the final flags in the tail after the roots: one copy)
+  const size_t o_roots = (size_t)((char*)roots - (char*)tries), o_tail = (size_t)((char*)tail - (char*)tries);
+  uint8_t* hs = pinned_stage(c, o_tail + 64);
+  HIPCHK(hipMemcpyAsync(hs, tries, o_tail + 64, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  if (count_fresh) h->mused += c->h_pinned[1];
+  const unsigned long long* ht = (const unsigned long long*)(hs + o_tail);
+  if (count_fresh) h->mused += ht[6];
   memcpy(h->tries.data(), hs, (uint64_t)nt * 4);
   memcpy(h->roots.data(), hs + o_roots, (uint64_t)nt * 32);
-  if (ne) build_stats(c, (const unsigned long long*)(hs + o_ctr), &bst);
-  if (c->h_pinned[0]) throw KhError{KH_EINTERNAL, "anchor map insert failed"};
+  if (ne) build_stats_sums(c, ht, &bst);
+  if (ht[5]) throw KhError{KH_EINTERNAL, "anchor map insert failed"};
   if (!h->forest) memcpy(h->root, nt ? h->roots.data() : h->root, 32);
   float merge_ms = ev_ms(c->ev[6], c->ev[7]);
   if (stats) {

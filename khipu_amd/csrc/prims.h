@@ -123,7 +123,7 @@ __global__ void k_scan_total(const T* in_last, const T* out_last, T* total) {
 constexpr int SCAN_SMALL_THREADS = 1024;
 constexpr uint64_t SCAN_SMALL_MAX = 32768;
 template <typename T>
-__global__ void __launch_bounds__(SCAN_SMALL_THREADS) k_scan_small(const T* in, T* out, uint64_t n, T* total) {
+__device__ __forceinline__ void scan_small_block(const T* in, T* out, uint64_t n, T* total) {
   constexpr int IT = sizeof(T) == 8 ? 4 : 8;  // items per thread (LDS: 32 KiB + padding)
   constexpr uint32_t TILE = SCAN_SMALL_THREADS * IT;
   __shared__ T buf[TILE + TILE / 32];  // element p at p + p / 32 (the thread-contiguous reads
@@ -185,6 +185,26 @@ __global__ void __launch_bounds__(SCAN_SMALL_THREADS) k_scan_small(const T* in, 
     __syncthreads();  // buf and lw are rewritten by the next tile
   }
   if (total && tid == 0) *total = carry;
+}
+template <typename T>
+__global__ void __launch_bounds__(SCAN_SMALL_THREADS) k_scan_small(const T* in, T* out, uint64_t n, T* total) {
+  scan_small_block<T>(in, out, n, total);
+}
+// Up to three small scans of n elements in one launch, one block each (a commit's per-op
+// flags: new-trie starts, upsert ranks, value offsets); a null input skips its block.
+struct ScanJob {
+  const void* in;
+  void* out;
+  void* total;
+  bool wide;  // uint64_t elements (else uint32_t)
+};
+__global__ void __launch_bounds__(SCAN_SMALL_THREADS) k_scan_small3(ScanJob a, ScanJob b, ScanJob c, uint64_t n) {
+  const ScanJob& j = blockIdx.x == 0 ? a : blockIdx.x == 1 ? b : c;
+  if (!j.in) return;
+  if (j.wide)
+    scan_small_block<uint64_t>((const uint64_t*)j.in, (uint64_t*)j.out, n, (uint64_t*)j.total);
+  else
+    scan_small_block<uint32_t>((const uint32_t*)j.in, (uint32_t*)j.out, n, (uint32_t*)j.total);
 }
 
 // Mid-size scans (up to SCAN_TWO_MAX_TILES tiles): after k_scan_tiles, each block sums the

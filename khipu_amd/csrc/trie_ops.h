@@ -257,6 +257,7 @@ enum {
 // each) by block index and summed on the host.  Row 0 holds every other counter.
 constexpr int CTR_SHARDS = 64;
 constexpr int CTR_LONGN = 16 + 7;  // longlist length (row 1, index 7: unused by the stat shards)
+constexpr int CTR_PYR = 16 + 8;    // k_pyramid's finished-block count (row 1, index 8)
 // counter add returning the old value (the host replay is single-threaded)
 KH_HD unsigned long long ctr_add(unsigned long long* p, unsigned long long v) {
 #ifdef __HIP_DEVICE_COMPILE__
