@@ -2369,6 +2369,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // spread over them); of at most SMALL_LEVEL: k_branch_small (every child record loaded at
   // once); KHST_BRANCH_SMALL=0 (measurement switch) keeps them all on k_branch_fused
   static const bool small_levels = !getenv("KHST_BRANCH_SMALL") || atoi(getenv("KHST_BRANCH_SMALL")) != 0;
+  // (measurement switches: the level sizes below which the two small-level kernels run)
+  static const uint32_t xl_level = getenv("KHST_XL_LEVEL") ? (uint32_t)atoi(getenv("KHST_XL_LEVEL")) : XL_LEVEL;
+  static const uint32_t small_level =
+      getenv("KHST_SMALL_LEVEL") ? (uint32_t)atoi(getenv("KHST_SMALL_LEVEL")) : SMALL_LEVEL;
   bool moved = move_d == 0;
   for (int d = 63; d >= 0; --d) {
     uint32_t cnt = lbh[d + 1] - lbh[d];
@@ -2388,10 +2392,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
         hipLaunchKernelGGL(k_branch_fused<0>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
       else if (rescan)
         hipLaunchKernelGGL(k_branch_fused<1>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
-      else if (small_levels && !T.links && cnt <= XL_LEVEL)
+      else if (small_levels && !T.links && cnt <= xl_level)
         hipLaunchKernelGGL(k_branch_xl, dim3((unsigned)((cnt + 1) / 2)), dim3(64), 0, st, T, (uint64_t)lbh[d],
                            (uint64_t)cnt);
-      else if (small_levels && cnt <= SMALL_LEVEL)
+      else if (small_levels && cnt <= small_level)
         hipLaunchKernelGGL(k_branch_small, dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, T, (uint64_t)lbh[d],
                            (uint64_t)cnt);
       else if (branch_bs64)
