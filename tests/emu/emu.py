@@ -24,6 +24,7 @@ def lib():
         L.emu_node_children.argtypes = [vp, ctypes.c_uint64, ctypes.c_int, vp, vp, vp]
         L.emu_set_leaf_mode.argtypes = [ctypes.c_int]
         L.emu_set_link_mode.argtypes = [ctypes.c_int]
+        L.emu_xlane_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -92,3 +93,9 @@ def node_children(value: bytes, kind: int):
     buf = _buf(value + b"\0" * 16)
     st = lib().emu_node_children(buf.ctypes.data, len(value), kind, out.ctypes.data, kinds.ctypes.data, n.ctypes.data)
     return st, [(out[32 * i:32 * i + 32].tobytes(), int(kinds[i])) for i in range(int(n[0]))]
+
+
+def xlane_check(seed, iters):
+    """Mismatching state lanes of the lane-spread permutation (keccak_xlane.h, replayed lane
+    by lane) against the one-thread permutation (keccak.h) over `iters` random states."""
+    return lib().emu_xlane_check(seed, iters)

@@ -16,6 +16,7 @@
 #include "../../khipu_amd/csrc/nodedata.h"
 #include "../../khipu_amd/csrc/keyorder.h"
 #include "../../khipu_amd/csrc/synth.h"
+#include "../../khipu_amd/csrc/keccak_xlane.h"
 
 using namespace khst;
 
@@ -419,4 +420,33 @@ extern "C" int emu_ansv_check(uint64_t seed, int iters) {
     }
   }
   return 0;
+}
+
+// The lane-spread permutation (keccak_xlane.h) replayed lane by lane -- each round's two
+// steps over all 32 lanes of a group, with the LDS buffers as arrays -- against the
+// one-thread permutation (keccak.h) on random states.  Returns the number of mismatches.
+extern "C" int emu_xlane_check(uint64_t seed, int iters) {
+  std::mt19937_64 r(seed);
+  int bad = 0;
+  XLane g[32];
+  for (uint32_t l = 0; l < 32; ++l) g[l] = xlane_setup(l);
+  for (int it = 0; it < iters; ++it) {
+    KState S;
+    uint64_t A[32] = {};
+    for (int i = 0; i < 25; ++i) {
+      A[i] = r();
+      S.lo[i] = (uint32_t)A[i];
+      S.hi[i] = (uint32_t)(A[i] >> 32);
+    }
+    for (uint32_t l = 25; l < 32; ++l) A[l] = r();  // lanes past the state carry garbage
+    keccakf(S);
+    for (int rd = 0; rd < 24; ++rd) {
+      uint64_t bA[32], B[32];
+      for (int l = 0; l < 32; ++l) bA[l] = A[l];
+      for (int l = 0; l < 32; ++l) B[l] = xl_step_theta_rho(g[l], bA);
+      for (int l = 0; l < 32; ++l) A[l] = xl_step_chi(g[l], B[l], B, rd);
+    }
+    for (int i = 0; i < 25; ++i) bad += A[i] != lane(S, i);
+  }
+  return bad;
 }

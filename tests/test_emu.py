@@ -109,3 +109,10 @@ def test_nearest_smaller_value_searches():
     L = E.lib()
     L.emu_ansv_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
     assert L.emu_ansv_check(7, 150) == 0
+
+
+def test_lane_spread_keccak():
+    """keccak_xlane.h (the N1 small-level permutation: 25 lanes per state, two LDS steps per
+    round), replayed lane by lane, == keccak.h's one-thread Keccak-f[1600] (which the oracle
+    KATs pin) on 300 random states; lanes 25..31 start with garbage and must not leak in."""
+    assert E.xlane_check(11, 300) == 0

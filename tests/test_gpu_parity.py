@@ -423,3 +423,19 @@ def test_6m_with_repeats(khst, oracle):
     roots, bst = oracle.batch_roots(keys, (vbytes, off), klen=20, hash_keys=True)
     assert hh[0].tobytes() == roots[0]
     assert st.n_leaves == bst["leaves"]
+
+
+@pytest.mark.gpu
+def test_lane_spread_keccak_on_device(khst):
+    """N1: the lane-spread permutation (keccak_xlane.h, 25 lanes per state in 32-lane groups,
+    LDS round trips) == keccak.h's one-thread permutation on 512 random states, 1 and 3
+    permutations in a row, run as the real device code (scripts/xlane_check, built by
+    __graft_entry__.build()); it also reports the latency per permutation of both forms."""
+    import json
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts", "xlane_check")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["equal"] is True
+    assert d["us_per_perm"]["xlane_1wave"] < d["us_per_perm"]["thread_1wave"]
