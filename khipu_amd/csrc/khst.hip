@@ -1579,6 +1579,8 @@ struct kh_ctx {
   hipStream_t st2 = nullptr;  // leaf hashing, concurrent with the branch topology
   std::mutex mu;
   DevBuf ws_list;  // element builds: the list of leaves to hash (k_leaf_pub)
+  DevBuf ws_inject;                    // kh_block_commit: the injection's error word
+  unsigned long long inject_tok = 0;   //   and the token the last call writes there on error
   DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, in_kn, in_aux, in_block, out_emit, emit_dev;
   hipEvent_t ev[13] = {};  // [8] boundaries ready (st), [9] / [10] leaf kernel start / end (st2),
                           // [11] second part of the leaf copy pass done (st2), [12] unused
@@ -2174,7 +2176,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       hipLaunchKernelGGL(k_pyramid, GRID(P.sz[1], BS), dim3(BS), 0, st, P, (unsigned int*)(ctr + CTR_PYR));
       LAUNCH_CHECK();
     }
-    HIPCHK(hipMemsetAsync(T.glast, 1, nb, st));
+    HIPCHK(hipMemsetAsync(T.glast, 1, (nb + 15) & ~(uint64_t)15, st));  // (whole 16-byte words: one fill kernel)
     if (pd_mode == 2) {  // the leaves need only u: they start here, beside the whole topology
       HIPCHK(hipEventRecord(c->ev[8], st));
       HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
@@ -2223,7 +2225,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     hipLaunchKernelGGL(k_level_bounds, dim3(1), dim3(64), 0, st, (const uint32_t*)bcnt, nblk, (const uint32_t*)Bp,
                        lb);
     LAUNCH_CHECK();
-    HIPCHK(hipMemsetAsync(T.br_k, 0, nb * 4, st));  // entries past B must scan as 0
+    HIPCHK(hipMemsetAsync(T.br_k, 0, (nb * 4 + 15) & ~(uint64_t)15, st));  // entries past B must scan as 0
     hipLaunchKernelGGL(k_branch_permute, topo_grid(nb), dim3(BS), 0, st, T, J, (const uint32_t*)order,
                        (const uint32_t*)Bp);
     LAUNCH_CHECK();
@@ -2701,8 +2703,10 @@ __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32
 // a commit's inputs staged as one batch: 32-byte keys (copy_keys) and trie ids (when given)
 __global__ void __launch_bounds__(BS) k_f_inputs(const uint64_t* up_keys, uint64_t nup, const uint64_t* del_keys,
                                                  uint64_t ndel, bool copy_keys, const uint32_t* up_trie,
-                                                 const uint32_t* del_trie, uint64_t* K, uint32_t* Tid) {
+                                                 const uint32_t* del_trie, uint64_t* K, uint32_t* Tid,
+                                                 unsigned long long* zero) {
   const uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o < CTR_N) zero[o] = 0;
   if (o >= nup + ndel) return;
   const bool up = o < nup;
   const uint64_t q = up ? o : o - nup;
@@ -2995,14 +2999,15 @@ __global__ void k_f_roots(const uint64_t* res_hash, const uint32_t* res_len, uin
 // of its body (RLP[nonce, balance, stateRoot, codeHash], PV63.scala:46-51)
 __global__ void __launch_bounds__(BS) k_inject_roots(uint8_t* vals, const uint64_t* voff, const uint32_t* acct_trie,
                                                      uint64_t n, const uint32_t* tries, uint32_t nt,
-                                                     const uint64_t* roots, unsigned long long* err) {
+                                                     const uint64_t* roots, unsigned long long* err,
+                                                     unsigned long long tok) {
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n || acct_trie[i] == 0xFFFFFFFFu) return;
   const uint32_t s = seg_of(tries, nt, acct_trie[i]);
   if (s >= nt || tries[s] != acct_trie[i]) return;  // storage unchanged this block
   const uint64_t e = voff[i + 1];
   if (e - voff[i] < 66 || vals[e - 66] != 0xA0 || vals[e - 33] != 0xA0) {
-    *err = 6;  // not an account body
+    *err = tok;  // not an account body
     return;
   }
   const uint8_t* rb = (const uint8_t*)(roots + 4 * s);
@@ -3284,7 +3289,6 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   uint64_t* uoff = cv.take<uint64_t>(nops + 1);
   uint64_t* ulen = cv.take<uint64_t>(nops);
   uint32_t* ur = cv.take<uint32_t>(nops);
-  HIPCHK(hipMemsetAsync(S.ctr, 0, CTR_N * 8, st));
   if (h->flags & KH_HASH_KEYS) {
     if (F.nup) {
       if (F.klen <= 135)
@@ -3308,12 +3312,11 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     if (F.ndel) HIPCHK(hipMemcpyAsync(K + 4 * F.nup, F.del_keys, F.ndel * 32, hipMemcpyDeviceToDevice, st));
     copy_keys = false;
   }
-  if (copy_keys || segd) {
-    hipLaunchKernelGGL(k_f_inputs, GRID(nops, BS), dim3(BS), 0, st, (const uint64_t*)F.up_keys, F.nup,
-                       (const uint64_t*)F.del_keys, F.ndel, copy_keys, segd ? F.up_trie : nullptr,
-                       segd ? F.del_trie : nullptr, K, Tid);
-    LAUNCH_CHECK();
-  }
+  // (also zeroes the sort's counters S.ctr)
+  hipLaunchKernelGGL(k_f_inputs, GRID(nops, BS), dim3(BS), 0, st, (const uint64_t*)F.up_keys, F.nup,
+                     (const uint64_t*)F.del_keys, F.ndel, copy_keys, segd ? F.up_trie : nullptr,
+                     segd ? F.del_trie : nullptr, K, Tid, S.ctr);
+  LAUNCH_CHECK();
   sort_dedup(c, S);
   const uint64_t nd = S.m;
   uint32_t* otrie = segd ? S.sseg : sseg;  // the compaction of duplicates moves the sorted ids
@@ -3581,7 +3584,7 @@ int kh_ctx_destroy(kh_ctx* c) {
   API_TRY({
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->st);
-    for (DevBuf* b : {&c->ws_list, &c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->in_kn, &c->in_aux, &c->in_block, &c->out_emit,
+    for (DevBuf* b : {&c->ws_inject, &c->ws_list, &c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->in_kn, &c->in_aux, &c->in_block, &c->out_emit,
                       &c->emit_dev})
       b->release();
     for (auto& e : c->ev)
@@ -4561,15 +4564,19 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     const uint32_t nt = (uint32_t)storage->tries.size();
     if (nt && na_up && d_a_up_trie) {
       // the forest's trie list and roots are still on the device (its commit's tbuf)
-      c->ws3.ensure(64);
-      unsigned long long* err = (unsigned long long*)c->ws3.p;
-      HIPCHK(hipMemsetAsync(err, 0, 8, st));
+      // (the error word is never cleared: a failing call writes its own token into it)
+      if (!c->ws_inject.p) {
+        c->ws_inject.ensure(64);
+        HIPCHK(hipMemsetAsync(c->ws_inject.p, 0, 64, st));
+      }
+      unsigned long long* err = (unsigned long long*)c->ws_inject.p;
+      const unsigned long long tok = ++c->inject_tok;
       hipLaunchKernelGGL(k_inject_roots, GRID(na_up, BS), dim3(BS), 0, st, d_a_up_vals, d_a_up_voff, d_a_up_trie,
-                         na_up, (const uint32_t*)storage->d_tries, nt, (const uint64_t*)storage->d_roots, err);
+                         na_up, (const uint32_t*)storage->d_tries, nt, (const uint64_t*)storage->d_roots, err, tok);
       LAUNCH_CHECK();
       HIPCHK(hipMemcpyAsync(c->h_pinned, err, 8, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
-      if (c->h_pinned[0]) throw KhError{KH_EINVAL, "an account upsert with a storage trie is not an account body"};
+      if (c->h_pinned[0] == tok) throw KhError{KH_EINVAL, "an account upsert with a storage trie is not an account body"};
     }
     // 3. the accounts (TrieAccounts.flush, TrieAccounts.scala:22-28)
     FCommit A;
