@@ -590,10 +590,20 @@ __device__ __forceinline__ uint64_t block_claim(unsigned long long* ctr, bool wa
   __syncthreads();  // lds is reused by the next call
   return e;
 }
-__global__ void __launch_bounds__(BS) k_leaf_prep(Topo T, unsigned long long* zero) {
+// Element builds (a block commit): most elements are unchanged subtrees or leaves whose
+// reference is only handed to the new parent; the few that are re-encoded (the block's
+// upserts, moved leaves, new extensions) sit scattered among them, so a thread-per-element
+// hash pass runs a permutation in nearly every wave.  k_leaf_prep publishes the cheap ones
+// and lists the others (one claim per block); k_leaf_hash_list hashes the list in full waves.
+__device__ __forceinline__ bool leaf_listed(const Topo& T, uint64_t i) {
+  if (is_branch_value(T, i)) return false;
+  const uint32_t a = (uint32_t)(T.lf_pd[i] + 1);
+  return !(el_cached(T, i, a) || (el_subtree(T, i) && el_ext_nibbles(T, i, a) == 0));
+}
+__global__ void __launch_bounds__(BS) k_leaf_prep(Topo T, uint32_t* list, unsigned long long* nlist) {
   __shared__ uint64_t stage[BS * STAGE_WORDS];
+  __shared__ unsigned long long claim[BS / 64 + 1];
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (zero && i == 0) *zero = 0;  // (a counter of the next kernel)
   const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u;
   uint64_t off = 0;
   uint32_t vlen = 0;
@@ -624,33 +634,7 @@ __global__ void __launch_bounds__(BS) k_leaf_prep(Topo T, unsigned long long* ze
     else
       op_leaf_prep(T, i, T.vals + off, vlen);
   }
-}
-
-__global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  unsigned long long perms = 0, hashes = 0, inl = 0;
-  if (i < T.m) {
-    uint32_t in1 = 0;
-    perms = op_leaf_hash(T, i, &in1);
-    hashes = perms ? 1 : 0;
-    inl = in1;
-  }
-  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
-             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
-}
-// Element builds (a block commit): most elements are unchanged subtrees or leaves whose
-// reference is only handed to the new parent; the few that are re-encoded (the block's
-// upserts, moved leaves, new extensions) sit scattered among them, so a thread-per-element
-// hash pass runs a permutation in nearly every wave.  k_leaf_pub publishes the cheap ones
-// and lists the others (one claim per block); k_leaf_hash_list hashes the list in full waves.
-__device__ __forceinline__ bool leaf_listed(const Topo& T, uint64_t i) {
-  if (is_branch_value(T, i)) return false;
-  const uint32_t a = (uint32_t)(T.lf_pd[i] + 1);
-  return !(el_cached(T, i, a) || (el_subtree(T, i) && el_ext_nibbles(T, i, a) == 0));
-}
-__global__ void __launch_bounds__(BS) k_leaf_pub(Topo T, uint32_t* list, unsigned long long* nlist) {
-  __shared__ unsigned long long claim[BS / 64 + 1];
-  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (!list) return;  // (block-uniform) element builds: publish the kept references, list the rest
   const bool live = i < T.m;
   const bool listed = live && leaf_listed(T, i);
   unsigned long long perms = 0, hashes = 0, inl = 0;
@@ -662,6 +646,19 @@ __global__ void __launch_bounds__(BS) k_leaf_pub(Topo T, uint32_t* list, unsigne
   }
   const uint64_t e = block_claim(nlist, listed, claim);
   if (listed) list[e] = (uint32_t)i;
+  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
+             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
+}
+
+__global__ void __launch_bounds__(BS) k_leaf_hash(Topo T) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  unsigned long long perms = 0, hashes = 0, inl = 0;
+  if (i < T.m) {
+    uint32_t in1 = 0;
+    perms = op_leaf_hash(T, i, &in1);
+    hashes = perms ? 1 : 0;
+    inl = in1;
+  }
   block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
              ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
 }
@@ -1569,7 +1566,7 @@ static size_t carve_size(const std::vector<size_t>& items) {
 struct BuildInfo {  // the last build's sizes, for build_stats
   uint64_t n = 0, m = 0, B = 0, key_perms = 0, arena = 0;
   uint32_t levels = 0;
-  bool full_sort = false, early = false;
+  bool full_sort = false, early = false, stage_ev = true;
 };
 struct kh_ctx {
   int dev = 0;
@@ -1578,7 +1575,7 @@ struct kh_ctx {
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // leaf hashing, concurrent with the branch topology
   std::mutex mu;
-  DevBuf ws_list;  // element builds: the list of leaves to hash (k_leaf_pub)
+  DevBuf ws_list;  // element builds: the list of leaves to hash (k_leaf_prep -> k_leaf_hash_list)
   DevBuf ws_inject;                    // kh_block_commit: the injection's error word
   unsigned long long inject_tok = 0;   //   and the token the last call writes there on error
   DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, in_kn, in_aux, in_block, out_emit, emit_dev;
@@ -1999,6 +1996,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // results, counters, depth histogram and level bounds are carved back to back: one memset
   HIPCHK(hipMemsetAsync(T.res_hash, 0, (size_t)((char*)(lb + 80) - (char*)T.res_hash), st));
 
+  // stage events (kh_stats' t_keys / t_sort / t_topo / t_leaf / t_branch): not for a forest's
+  // element builds, whose host is the bottleneck (the block-commit HIP API trace: every API
+  // call of a commit counts); their stats keep t_total only
+  const bool stage_ev = !A.el;
   HIPCHK(hipEventRecord(c->ev[0], st));
   // ---- 1. keys (the plain path takes its 32-bit sort keys from the hashing pass)
   // plain root builds sort 32-bit words (segment id | leading key bits) with the input
@@ -2028,7 +2029,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   } else if (own_keys) {
     HIPCHK(hipMemcpyAsync(K32, A.keys, n * 32, hipMemcpyDeviceToDevice, st));
   }
-  HIPCHK(hipEventRecord(c->ev[1], st));
+  if (stage_ev) HIPCHK(hipEventRecord(c->ev[1], st));
 
   // ---- 2. sort + dedup
   uint64_t m = n;
@@ -2093,7 +2094,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     T.el_cref = ecref;
     T.el_crl = ecrl;
   }
-  HIPCHK(hipEventRecord(c->ev[2], st));
+  if (stage_ev) HIPCHK(hipEventRecord(c->ev[2], st));
 
   // ---- 3. topology
   const uint64_t nb = m - 1;
@@ -2294,7 +2295,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     T.ex_rlen = ce.take<uint32_t>(B);
     T.emit_sel = nullptr;  // the forest sets its write-back selection after the build
   }
-  if (!early) HIPCHK(hipEventRecord(c->ev[3], st));
+  if (!early && stage_ev) HIPCHK(hipEventRecord(c->ev[3], st));
 
   // ---- 4. leaves: encode + hash in LDS (root only), or encode into message slots
   //         that the node-set emitter reads back, then hash
@@ -2340,18 +2341,18 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       LAUNCH_CHECK();
     }
   } else {  // write-back and element builds: encodings kept in message slots, then hashed
-    unsigned long long* nlist = nullptr;  // element builds: the re-encoded leaves' list (k_leaf_pub)
+    // element builds: k_leaf_prep also publishes the elements that keep their reference and
+    // lists the re-encoded ones (counter CTR_LIST, zero since the build's counter memset),
+    // which k_leaf_hash_list hashes in full waves
+    unsigned long long* nlist = A.el ? T.ctr + CTR_LIST : nullptr;
     uint32_t* list = nullptr;
     if (A.el) {
-      c->ws_list.ensure(carve_size({64, m * 4}));
-      Carver cl{(char*)c->ws_list.p, 0, c->ws_list.cap};
-      nlist = cl.take<unsigned long long>(8);
-      list = cl.take<uint32_t>(m);
+      c->ws_list.ensure(carve_size({m * 4}));
+      list = (uint32_t*)c->ws_list.p;
     }
-    hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T, nlist);  // (zeroes *nlist)
+    hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T, list, nlist);
     LAUNCH_CHECK();
-    if (A.el) {  // the re-encoded elements hashed from a list
-      hipLaunchKernelGGL(k_leaf_pub, GRID(m, BS), dim3(BS), 0, st, T, list, nlist);
+    if (A.el) {  // the re-encoded elements hashed from the list
       const uint64_t lblocks = std::min<uint64_t>((uint64_t)c->n_cu * 4, (m + BS - 1) / BS);
       hipLaunchKernelGGL(k_leaf_hash_list, dim3((unsigned)std::max<uint64_t>(lblocks, 1)), dim3(BS), 0, st, T,
                          (const uint32_t*)list, (const unsigned long long*)nlist);
@@ -2360,7 +2361,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     }
     LAUNCH_CHECK();
   }
-  HIPCHK(hipEventRecord(c->ev[4], st));
+  if (stage_ev) HIPCHK(hipEventRecord(c->ev[4], st));
 
   // ---- 5. branch levels, deepest first: encode (gathers the children's refs), then hash
   uint32_t levels = 0;
@@ -2425,6 +2426,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   bi.levels = levels;
   bi.full_sort = ties;
   bi.early = early;
+  bi.stage_ev = stage_ev;
   // A.dev_results (a forest's element build): the results stay on the device and the caller
   // reads the counters at its own next sync (build_stats) -- one host round trip less
   if (A.dev_results) return;
@@ -2470,6 +2472,8 @@ static void build_stats_sums(kh_ctx* c, const unsigned long long* sums, kh_stats
   stats->arena_bytes = bi.arena;
   stats->n_levels = bi.levels;
   stats->full_sort = bi.full_sort ? 1 : 0;
+  stats->t_total_ms = ev_ms(c->ev[0], c->ev[5]);
+  if (!bi.stage_ev) return;
   // split builds: until both halves are hashed (the second half overlaps the first sort)
   stats->t_keys_ms = ev_ms(c->ev[0], c->ev[1]);
   stats->t_sort_ms = ev_ms(c->ev[1], c->ev[2]);
@@ -2478,7 +2482,6 @@ static void build_stats_sums(kh_ctx* c, const unsigned long long* sums, kh_stats
   // publish of its references runs on st after both; t_total_ms holds it)
   stats->t_leaf_ms = bi.early ? ev_ms(c->ev[9], c->ev[10]) : ev_ms(c->ev[3], c->ev[4]);
   stats->t_branch_ms = ev_ms(c->ev[4], c->ev[5]);
-  stats->t_total_ms = ev_ms(c->ev[0], c->ev[5]);
 }
 
 // ---------------------------------------------------------------------------
@@ -2716,6 +2719,20 @@ __global__ void __launch_bounds__(BS) k_f_inputs(const uint64_t* up_keys, uint64
   }
   if (up_trie || del_trie) Tid[o] = up ? up_trie[q] : del_trie[q];
 }
+__device__ __forceinline__ void upsert_elem(const FOps& O, uint64_t o, uint64_t e, uint32_t seg, uint64_t vo,
+                                            uint32_t vl, const Elems& E) {
+  for (int q = 0; q < 4; ++q) E.key[4 * e + q] = O.key[4 * o + q];
+  E.seg[e] = seg;
+  E.db[e] = EL_LEAF;
+  for (int q = 0; q < 4; ++q) E.bref[4 * e + q] = 0;
+  E.brl[e] = 0;
+  E.vo[e] = vo;
+  E.vl[e] = vl;
+  E.src[e] = NONE;
+  E.oldd[e] = EL_NEW;
+  for (int q = 0; q < 4; ++q) E.cref[4 * e + q] = 0;
+  E.crl[e] = 0;
+}
 __global__ void __launch_bounds__(BS) k_f_upsert_elems(FOps O, const uint32_t* tries, uint32_t nt, const uint32_t* ur,
                                                        const uint64_t* uoff, Elems E, uint64_t heap_base,
                                                        uint64_t nups) {
@@ -2723,36 +2740,38 @@ __global__ void __launch_bounds__(BS) k_f_upsert_elems(FOps O, const uint32_t* t
   if (o == 0) *E.n = nups;
   if (o >= O.n || O.kind[o] != FOP_UPSERT) return;
   const uint64_t e = ur[o];
-  for (int q = 0; q < 4; ++q) E.key[4 * e + q] = O.key[4 * o + q];
-  E.seg[e] = seg_of(tries, nt, O.trie[o]);
-  E.db[e] = EL_LEAF;
-  for (int q = 0; q < 4; ++q) E.bref[4 * e + q] = 0;
-  E.brl[e] = 0;
-  E.vo[e] = heap_base + uoff[e];
-  E.vl[e] = (uint32_t)(uoff[e + 1] - uoff[e]);
-  E.src[e] = NONE;
-  E.oldd[e] = EL_NEW;
-  for (int q = 0; q < 4; ++q) E.cref[4 * e + q] = 0;
-  E.crl[e] = 0;
+  upsert_elem(O, o, e, seg_of(tries, nt, O.trie[o]), heap_base + uoff[e], (uint32_t)(uoff[e + 1] - uoff[e]), E);
 }
 // after the counts are known, CG threads per sorted op o: an upsert's value into the heap at
 // its offset uoff[o] (the exclusive scan of the upsert lengths over the sorted ops) and that
 // offset by upsert rank (uo[ur[o]]; uo[nups] = the total); a new trie's id into the list
+// after the counts are known, CG threads per sorted op o: an upsert's value into the heap at
+// its offset uoff[o] (the exclusive scan of the upsert lengths over the sorted ops), that
+// offset by upsert rank (uo[ur[o]]; uo[nups] = the total), and its leaf element (rank
+// ur[o]; E.n = nups: the gather pushes after them); a new trie's id into the list.  The
+// segment of an op is its trie's rank in the sorted list: tpos[o] - 1 + tflag[o].
 __global__ void __launch_bounds__(BS) k_f_ops_post(FOps O, const uint32_t* sidx, const uint32_t* ur,
                                                    const uint8_t* vals, const uint64_t* voff, const uint64_t* uoff,
                                                    uint64_t* uo, uint64_t nups, uint64_t total, uint8_t* heap,
                                                    uint64_t heap_base, const uint32_t* tflag, const uint32_t* tpos,
-                                                   uint32_t* tries) {
+                                                   uint32_t* tries, Elems E) {
   const uint64_t g = (uint64_t)blockIdx.x * BS + threadIdx.x;
   const uint64_t o = g / CG;
   const uint32_t sub = threadIdx.x % CG;
-  if (g == 0) uo[nups] = total;
+  if (g == 0) {
+    uo[nups] = total;
+    *E.n = nups;
+  }
   if (o >= O.n) return;
   if (sub == 0 && tflag[o]) tries[tpos[o]] = O.trie[o];
   if (O.kind[o] != FOP_UPSERT) return;
-  if (sub == 0) uo[ur[o]] = uoff[o];
   const uint64_t s = sidx[o];
-  copy_bytes_group(heap + heap_base + uoff[o], vals + voff[s], voff[s + 1] - voff[s], sub);
+  const uint64_t vl = voff[s + 1] - voff[s];
+  if (sub == 0) {
+    uo[ur[o]] = uoff[o];
+    upsert_elem(O, o, ur[o], tpos[o] + tflag[o] - 1, heap_base + uoff[o], (uint32_t)vl, E);
+  }
+  copy_bytes_group(heap + heap_base + uoff[o], vals + voff[s], vl, sub);
 }
 // sorted op o: its kind, the flag of a new trie (the segments of the element build), and for
 // an upsert its rank flag and value length (the heap copy); one launch over the sorted ops.
@@ -2813,15 +2832,18 @@ __global__ void __launch_bounds__(GATHER_BS) k_f_gather(AMap M, Recs R, const ui
     const uint64_t e = block_claim(E.n, want, claim);  // every thread of the block reaches the claim
     if (want) elem_fill(R, er, seg, E, e);
   }
-}
-__global__ void k_f_gather_roots(AMap M, Recs R, const uint32_t* touched, const uint32_t* tries, uint32_t nt, Elems E) {
-  uint64_t s = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (s >= nt) return;
-  auto push = [&]() { return (uint64_t)atomicAdd(E.n, 1ULL); };
-  const uint64_t zero[4] = {0, 0, 0, 0};
-  const uint32_t r = map_find(M, R, tries[s], 0, zero);
-  if (r == NONE || touched[r]) return;
-  elem_from_record(R, r, (uint32_t)s, E, push);
+  // every trie's untouched root record (a trie no op descended through) -- the same loop form
+  for (uint64_t s0 = (uint64_t)blockIdx.x * GATHER_BS; s0 < nt; s0 += (uint64_t)gridDim.x * GATHER_BS) {
+    const uint64_t s = s0 + threadIdx.x;
+    uint32_t r = NONE;
+    if (s < nt) {
+      const uint64_t zero[4] = {0, 0, 0, 0};
+      r = map_find(M, R, tries[s], 0, zero);
+      if (r != NONE && touched[r]) r = NONE;
+    }
+    const uint64_t e = block_claim(E.n, r != NONE, claim);
+    if (r != NONE) elem_fill(R, r, (uint32_t)s, E, e);
+  }
 }
 
 // after the element build (c->T): one new record per branch (+ extension) at base + j,
@@ -3362,27 +3384,17 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   const uint64_t hb = h->heap_n;
   h->ubuf.ensure(((uint64_t)nups + 1) * 8 + 64);
   uint64_t* uo = (uint64_t*)h->ubuf.p;
-  hipLaunchKernelGGL(k_f_ops_post, GRID(nd * CG, BS), dim3(BS), 0, st, O, (const uint32_t*)S.sidx, (const uint32_t*)ur,
-                     F.up_vals, F.up_voff, (const uint64_t*)uoff, uo, (uint64_t)nups, ubytes, (uint8_t*)h->heap.p, hb,
-                     (const uint32_t*)tflag, (const uint32_t*)tpos, tries);
-  LAUNCH_CHECK();
-  // ---- 2. descent: opened branches and touched leaves
-  recs_reserve(h, h->rn + 16);
-  if (h->mcap == 0) map_rebuild(h, nops + 1024);
-  hipLaunchKernelGGL(k_f_descend, GRID(nd, BS), dim3(BS), 0, st, O, map_of(h), recs_of(h), (uint32_t*)h->touched.p,
-                     (uint8_t*)h->replaced.p, tlist, fctr);
-  LAUNCH_CHECK();
-  // ---- 3. elements: upserts (values in the heap already), untouched children, kept leaves,
-  // roots.  No host round trip after the descent: the element capacity is sized from the
-  // last commit's touched count (or 4 per op), and a short buffer is grown to the exact
-  // size and gathered again after the one sync below.
+  // ---- the elements' buffer: upserts (values in the heap), untouched children, kept
+  // leaves, roots.  Sized from the last commit's touched count (or 4 per op) so the descent
+  // and the gather need no host round trip between them; a short buffer is grown to the
+  // exact size and gathered again after the one sync below.  (Touched records are live
+  // records: at most rn - rdead; a guess past 1M touched records -- 16M elements -- is left
+  // to the exact second pass.)
   const uint64_t tl_cap = nd * 70 + 16;
-  // (touched records are live records: at most rn - rdead; a guess past 1M touched records
-  // -- 16M elements -- is left to the exact second pass)
   uint64_t ntl_guess = std::max<uint64_t>(4 * nd, h->ntl_hint + h->ntl_hint / 4);
   ntl_guess = std::min({ntl_guess, tl_cap, h->rn - h->rdead + 16, (uint64_t)1 << 20});
   Elems E{};
-  auto gather = [&](uint64_t ntl_cap) {
+  auto carve_elems = [&](uint64_t ntl_cap) {
     const uint64_t ecap = (uint64_t)nups + 16 * ntl_cap + nt + 16;
     h->ebuf.ensure(
         carve_size({ecap * 32, ecap * 4, ecap, ecap * 32, ecap, ecap * 8, ecap * 4, ecap * 4, ecap, ecap * 32, ecap, 64}));
@@ -3401,22 +3413,33 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     E.crl = ce.take<uint8_t>(ecap);
     E.n = fctr + 5;
     E.cap = ecap;
-    // (the record elements are pushed after the upserts: k_f_upsert_elems sets E.n = nups)
-    hipLaunchKernelGGL(k_f_upsert_elems, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)tries, nt,
-                       (const uint32_t*)ur, (const uint64_t*)uo, E, hb, (uint64_t)nups);
-    LAUNCH_CHECK();
+    return ecap;
+  };
+  uint64_t ecap = carve_elems(ntl_guess);
+  hipLaunchKernelGGL(k_f_ops_post, GRID(nd * CG, BS), dim3(BS), 0, st, O, (const uint32_t*)S.sidx, (const uint32_t*)ur,
+                     F.up_vals, F.up_voff, (const uint64_t*)uoff, uo, (uint64_t)nups, ubytes, (uint8_t*)h->heap.p, hb,
+                     (const uint32_t*)tflag, (const uint32_t*)tpos, tries, E);
+  LAUNCH_CHECK();
+  // ---- 2. descent: opened branches and touched leaves
+  recs_reserve(h, h->rn + 16);
+  if (h->mcap == 0) map_rebuild(h, nops + 1024);
+  hipLaunchKernelGGL(k_f_descend, GRID(nd, BS), dim3(BS), 0, st, O, map_of(h), recs_of(h), (uint32_t*)h->touched.p,
+                     (uint8_t*)h->replaced.p, tlist, fctr);
+  LAUNCH_CHECK();
+  // ---- 3. elements: the gather (grid-stride over the device's touched count), one sync
+  auto gather = [&](bool redo) {
+    if (redo)  // the upserts' elements again, into the grown buffer
+      hipLaunchKernelGGL(k_f_upsert_elems, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)tries, nt,
+                         (const uint32_t*)ur, (const uint64_t*)uo, E, hb, (uint64_t)nups);
     const uint64_t gblocks = std::min<uint64_t>((uint64_t)c->n_cu * 2, (nd * 16 * 8 + GATHER_BS - 1) / GATHER_BS);
     hipLaunchKernelGGL(k_f_gather, dim3((unsigned)std::max<uint64_t>(gblocks, 1)), dim3(GATHER_BS), 0, st, map_of(h),
                        recs_of(h), (const uint32_t*)h->touched.p, (const uint8_t*)h->replaced.p,
                        (const uint32_t*)tlist, (const unsigned long long*)fctr, (const uint32_t*)tries, nt, E, fctr);
-    hipLaunchKernelGGL(k_f_gather_roots, GRID(nt, BS), dim3(BS), 0, st, map_of(h), recs_of(h),
-                       (const uint32_t*)h->touched.p, (const uint32_t*)tries, nt, E);
     LAUNCH_CHECK();
     HIPCHK(hipMemcpyAsync(c->h_pinned, fctr, 48, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    return ecap;
   };
-  uint64_t ecap = gather(ntl_guess);
+  gather(false);
   const uint64_t ntl = c->h_pinned[0], nrep = c->h_pinned[1];
   if (c->h_pinned[2] == 3) throw KhError{KH_EINTERNAL, "forest descent: corrupt anchor map"};
   if (c->h_pinned[3]) {  // nothing has changed yet: clear the descent's flags and refuse the batch
@@ -3434,7 +3457,8 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   if (c->h_pinned[2]) throw KhError{KH_EINTERNAL, "forest gather: corrupt anchor map"};
   uint64_t ne = c->h_pinned[5];
   if (ne > ecap) {  // the guess was short: the exact capacity, gathered again
-    ecap = gather(ntl);
+    ecap = carve_elems(ntl);
+    gather(true);
     ne = c->h_pinned[5];
     if (c->h_pinned[2]) throw KhError{KH_EINTERNAL, "forest gather: corrupt anchor map"};
   }

@@ -258,6 +258,7 @@ enum {
 constexpr int CTR_SHARDS = 64;
 constexpr int CTR_LONGN = 16 + 7;  // longlist length (row 1, index 7: unused by the stat shards)
 constexpr int CTR_PYR = 16 + 8;    // k_pyramid's finished-block count (row 1, index 8)
+constexpr int CTR_LIST = 16 + 9;   // element builds: the re-encoded leaves listed by k_leaf_prep
 // counter add returning the old value (the host replay is single-threaded)
 KH_HD unsigned long long ctr_add(unsigned long long* p, unsigned long long v) {
 #ifdef __HIP_DEVICE_COMPILE__

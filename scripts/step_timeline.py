@@ -1,6 +1,6 @@
-"""Kernel timeline of the last 100M step in a rocprofv3 --kernel-trace of bench.py
-(measurement only): the step is the last window of kernels separated by an idle gap
-> --gap ms; every kernel with its start offset, duration and queue (stream).
+"""Kernel timeline of a 100M step in a rocprofv3 --kernel-trace of bench.py (measurement
+only): the kernels from one key-hashing launch to the next; every kernel with its start
+offset, duration and queue (stream).
 
   python scripts/step_timeline.py gpurun_out/st [--gap 2] > timeline.json
 """
@@ -21,15 +21,14 @@ def main():
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                  r["Kernel_Name"].replace("void ", "").replace("khst::", "").split("(")[0].split("<")[0][:36],
                  r.get("Queue_Id", r.get("Stream_Id", "?"))) for r in rows)
-    wins, cur = [], []
-    for e in ev:
-        if cur and e[0] - max(x[1] for x in cur[-16:]) > a.gap * 1e6:
-            wins.append(cur)
-            cur = []
-        cur.append(e)
-    if cur:
-        wins.append(cur)
-    w = max(wins[-3:], key=len)  # the last full step (the self-check build follows the timed steps)
+    # a step starts at its key-hashing kernel: the last full step is the window between the
+    # last two such starts that are followed by a whole step (the self-check build follows)
+    starts = [i for i, e in enumerate(ev) if e[2].startswith("k_hash_keys")]
+    if len(starts) >= 2:
+        i0, i1 = starts[-2], starts[-1]
+        w = ev[i0:i1]
+    else:
+        w = ev
     t0 = w[0][0]
     out = [[k, q, round((s - t0) / 1e6, 3), round((e - s) / 1e6, 3)] for s, e, k, q in w]
     print(json.dumps({"span_ms": round((max(x[1] for x in w) - t0) / 1e6, 3), "launches": len(w),
