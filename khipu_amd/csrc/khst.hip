@@ -413,19 +413,21 @@ __global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb, bool ties_u) {
   if (ties_u && T.sck[b] == T.sck[b + 1]) return;
   op_lcp(T, b);
 }
-// the 64-ary min pyramid over the boundary values: level 1 by the whole grid, the (small)
-// upper levels by the last block to finish (the counter *done starts at zero)
-__global__ void __launch_bounds__(BS) k_pyramid(Pyr P, unsigned int* done) {
+// the 64-ary min pyramid over the boundary values: level `from` by the whole grid, the
+// (small) upper levels by the last block to finish (the counter *done starts at zero;
+// done == nullptr: level `from` only)
+__global__ void __launch_bounds__(BS) k_pyramid(Pyr P, int from, unsigned int* done) {
   __shared__ bool last;
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i < P.sz[1]) op_min64(P.lv[0], P.sz[0], (uint8_t*)P.lv[1], i);
+  if (i < P.sz[from]) op_min64(P.lv[from - 1], P.sz[from - 1], (uint8_t*)P.lv[from], i);
+  if (!done) return;
   __threadfence();
   __syncthreads();
   if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
   __threadfence();
-  for (int l = 2; l < P.nl; ++l) {
+  for (int l = from + 1; l < P.nl; ++l) {
     for (uint64_t k = threadIdx.x; k < P.sz[l]; k += BS) op_min64(P.lv[l - 1], P.sz[l - 1], (uint8_t*)P.lv[l], k);
     __threadfence_block();
     __syncthreads();
@@ -533,7 +535,7 @@ __global__ void __launch_bounds__(BS) k_level_scatter(Topo T, const uint32_t* Bp
 
 // the branch tables k_branch_topo wrote in key-order ids (J), moved to level order
 struct BrTab {
-  uint32_t *k, *parent, *first;
+  uint32_t *k, *parent, *first, *end;  // (end: leaf positions only)
   uint8_t *depth, *ext, *pord;
 };
 __global__ void __launch_bounds__(BS) k_branch_permute(Topo T, BrTab J, const uint32_t* pos, const uint32_t* Bp) {
@@ -545,6 +547,7 @@ __global__ void __launch_bounds__(BS) k_branch_permute(Topo T, BrTab J, const ui
     T.br_ext[g] = J.ext[j];
     T.br_pord[g] = J.pord[j];
     T.br_first[g] = J.first[j];
+    if (T.br_end) T.br_end[g] = J.end[j];
     T.br_parent[g] = p == NONE ? NONE : pos[p];  // parents of neighbouring branches are neighbours
   }
 }
@@ -834,6 +837,13 @@ __global__ void __launch_bounds__(BS) k_leaf_move_part(Topo T, const uint32_t* t
     op_leaf_move(T, i, [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); });
 }
 
+// leaf positions, before a small level (k_branch_xl / k_branch_small copy every child
+// record of a branch at once): the level's leaf children's records from their stashes
+__global__ void __launch_bounds__(BS) k_level_leafrecs(Topo T, uint64_t first, uint64_t cnt) {
+  const uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (t < cnt) op_leaf_children(T, (uint32_t)(first + t));
+}
+
 __global__ void __launch_bounds__(BS) k_leaf_long(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long perms = 0, hashes = 0, inl = 0;
@@ -876,7 +886,8 @@ __global__ void __launch_bounds__(BS) k_branch_hash(Topo T, uint64_t first, uint
 // bank-conflict-free within each 16-lane group (stride 34 dwords).
 // V: 0 variable-length keys (op_branch_fused), 1 direct window assembly re-scanning the
 // children per window (op_branch_direct), 2 the children streamed once with the next
-// record prefetched (op_branch_stream)
+// record prefetched (op_branch_stream), 4 the same reading leaf children at their sorted
+// positions (leaf positions), 5 following link records (KHST_LEAF_LINKS=1)
 // WB: threads per block.  WB = 64 (KHST_BRANCH_BS=64, measurement switch): one wave per
 // block, 8,704 B of LDS, so a CU holds 18 waves instead of the 16 that 35 KB blocks of 256
 // threads allow (4.5 per SIMD instead of 4); the counters are summed per wave.
@@ -891,9 +902,11 @@ __global__ void __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(4, 8)))
     // fixed-length keys: direct window assembly; variable-length keys (branch values):
     // the byte stream through the windowed writer
     uint64_t* sl = slots + threadIdx.x * LEAF_WORDS;
-    perms = V == 0 ? op_branch_fused(T, j, sl, 1, &in1)
+    perms = V == 0   ? op_branch_fused(T, j, sl, 1, &in1)
             : V == 1 ? op_branch_direct(T, j, sl, 1, &in1)
-                     : op_branch_stream(T, j, sl, 1, &in1);
+            : V == 2 ? op_branch_stream_t<SRC_REC>(T, j, sl, 1, &in1, ChildSrc{})
+            : V == 4 ? op_branch_stream_t<SRC_POS>(T, j, sl, 1, &in1, ChildSrc{})
+                     : op_branch_stream_t<SRC_LINK>(T, j, sl, 1, &in1, ChildSrc{});
     hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
   }
@@ -953,7 +966,7 @@ __global__ void __launch_bounds__(64) k_branch_small(Topo T, uint64_t first, uin
       }
     }
     uint32_t in1 = 0;
-    perms = op_branch_stream(T, j, slots + tid * LEAF_WORDS, 1, &in1, ChildSrc{cms + tid, crs + tid, WB});
+    perms = op_branch_stream_t<SRC_LDS>(T, j, slots + tid * LEAF_WORDS, 1, &in1, ChildSrc{cms + tid, crs + tid, WB});
     hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
   }
@@ -1885,6 +1898,14 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   const bool rescan = bv && strcmp(bv, "rescan") == 0;          // op_branch_direct
   const bool links = early && split_publish && !leaf_move && !coop && !rescan;
   const uint64_t cbound = links ? 2 * n + 16 : 0;
+  // Leaf positions (trie_ops.h Topo::lpos; unsegmented plain root builds): no leaf child
+  // records at all -- the branch kernels read each leaf child's stash at its sorted position.
+  // KHST_LEAF_POS=0 (measurement switch): the copy pass k_leaf_move instead.
+  static const bool leaf_pos_env = !getenv("KHST_LEAF_POS") || atoi(getenv("KHST_LEAF_POS")) != 0;
+  // (not with the round-2 leaf kernel, KHST_LEAF=v2, which does not publish a top leaf)
+  const bool leaf_v2_env = getenv("KHST_LEAF") && !strcmp(getenv("KHST_LEAF"), "v2");
+  const bool lpos =
+      early && split_publish && !links && !coop && !rescan && !segmented && leaf_pos_env && !leaf_v2_env;
 
   O.res_hash.assign(nres * 4, 0);
   O.res_len.assign(nres, 0);
@@ -1916,6 +1937,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       A.kn ? n : 0,                           // sorted key lengths
       nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1, nb1,  // branch tables in key-order ids (BrTab J)
       cbound * 32, cbound * 2, links ? n * 4 : 0, links ? n * 4 : 0,  // link mode: child records, fix / long lists
+      lpos ? nb1 * 4 : 0, lpos ? nb1 * 4 : 0, lpos ? n * 4 : 0,  // leaf positions: range ends (J, T), long list
   };
   c->ws1.ensure(carve_size(sz));
   Carver cv{(char*)c->ws1.p, 0, c->ws1.cap};
@@ -1986,6 +2008,12 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     T.cmeta = cv.take<uint16_t>(cbound);
     T.fixlist = cv.take<uint32_t>(n);
     T.longlist = cv.take<uint32_t>(n);
+  }
+  if (lpos) {
+    J.end = cv.take<uint32_t>(nb1);
+    T.br_end = cv.take<uint32_t>(nb1);
+    T.longlist = cv.take<uint32_t>(n);
+    T.lpos = 1;
   }
   T.depth0 = A.depth0;
   T.segmented = segmented ? 1 : 0;
@@ -2173,8 +2201,15 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       P.nl++;
       pp += (nout + 255) & ~(uint64_t)255;
     }
-    if (P.nl > 1) {  // every level in one launch (the last block to finish level 1 does the rest)
-      hipLaunchKernelGGL(k_pyramid, GRID(P.sz[1], BS), dim3(BS), 0, st, P, (unsigned int*)(ctr + CTR_PYR));
+    if (P.nl > 1) {  // the levels in one launch (the last block to finish the first does the rest),
+                     // after a launch per level while the next one is too big for one block
+                     // (100M keys: level 2 has 24k entries, ~0.9 ms for a lone block)
+      int from = 1;
+      for (; from + 1 < P.nl && P.sz[from + 1] > 4 * BS; ++from) {
+        hipLaunchKernelGGL(k_pyramid, GRID(P.sz[from], BS), dim3(BS), 0, st, P, from, (unsigned int*)nullptr);
+        LAUNCH_CHECK();
+      }
+      hipLaunchKernelGGL(k_pyramid, GRID(P.sz[from], BS), dim3(BS), 0, st, P, from, (unsigned int*)(ctr + CTR_PYR));
       LAUNCH_CHECK();
     }
     HIPCHK(hipMemsetAsync(T.glast, 1, (nb + 15) & ~(uint64_t)15, st));  // (whole 16-byte words: one fill kernel)
@@ -2212,6 +2247,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     TJ.br_depth = J.depth;
     TJ.br_ext = J.ext;
     TJ.br_pord = J.pord;
+    TJ.br_end = J.end;
     hipLaunchKernelGGL(k_branch_topo, topo_grid(nb), dim3(BS), 0, st, TJ, P, nb);
     LAUNCH_CHECK();
     // level order (grids sized by nb; threads past B exit), then every branch id
@@ -2238,7 +2274,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   if (links) {  // the leaves' child records as links, while they are still being hashed
     hipLaunchKernelGGL(k_leaf_link_rec, topo_grid(m), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
-  } else if (early && split_publish) {  // the leaves' slots, while they are still being hashed
+  } else if (early && split_publish && !lpos) {  // the leaves' slots, while they are still being hashed
     hipLaunchKernelGGL(k_leaf_link, topo_grid(m), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
   }
@@ -2263,7 +2299,12 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   std::vector<uint32_t> lbh(65, 0);
   memcpy(lbh.data(), (const char*)hc + ((char*)lb - (char*)ctr), 65 * 4);
   if (nb == 0) std::fill(lbh.begin(), lbh.end(), 0u);
-  const uint64_t nfix = links ? hc[CTR_FIXN] : 0, nlong = links ? hc[CTR_LONGN] : 0;
+  const uint64_t nfix = links ? hc[CTR_FIXN] : 0, nlong = (links || lpos) ? hc[CTR_LONGN] : 0;
+  if (lpos) {  // every leaf is hashed by now: is any of them inline?
+    unsigned long long ninl = 0;
+    for (int sh = 0; sh < CTR_SHARDS; ++sh) ninl += hc[sh * CTR_N + CTR_INLINE];
+    T.lf_inline = ninl ? 1 : 0;
+  }
 
   // ---- phase-2 workspace: child records + node arena
   // leaf encodings are kept (transposed message slots) for the write-back, element and
@@ -2273,7 +2314,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   const uint64_t bmsg_words = A.emit ? (uint64_t)BR_WORDS * B : 0, xmsg_words = A.emit ? (uint64_t)EXT_WORDS * B : 0;
   if (links && C > cbound) throw KhError{KH_EINTERNAL, "child records exceed their bound"};
   c->ws2.ensure(carve_size({links ? 0 : C * 32, links ? 0 : C * 2, lmsg_words * 8, lf_bytes + 64, bmsg_words * 8,
-                            xmsg_words * 8}));
+                            xmsg_words * 8, lpos ? C * 4 : 0}));
   Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
   if (!links) {
     T.cref = cv2.take<uint64_t>(C * 4);
@@ -2284,6 +2325,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   T.arena = cv2.take<uint8_t>(lf_bytes + 64);  // long leaves
   T.bmsg = A.emit ? cv2.take<uint64_t>(bmsg_words) : nullptr;
   T.xmsg = A.emit ? cv2.take<uint64_t>(xmsg_words) : nullptr;
+  if (lpos) {  // a record without CM_BR is a leaf child's: the metas start at zero
+    T.cend = cv2.take<uint32_t>(C);
+    HIPCHK(hipMemsetAsync(T.cmeta, 0, C * 2, st));
+  }
   T.lb = lb;
   if (A.el) {  // element build: every capped reference kept for the forest's records
     ElemArgs& E = *A.el;
@@ -2308,7 +2353,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint32_t move_d = 0;
   {
     static const bool msplit = getenv("KHST_MOVE_SPLIT") && atoi(getenv("KHST_MOVE_SPLIT")) != 0;
-    if (early && split_publish && !links && msplit && m >= (1u << 18) && nb > 0) {
+    if (early && split_publish && !links && !lpos && msplit && m >= (1u << 18) && nb > 0) {
       uint32_t best = 0, dbest = 0;
       for (uint32_t d = 0; d < 64; ++d)
         if (lbh[d + 1] - lbh[d] > best) best = lbh[d + 1] - lbh[d], dbest = d;
@@ -2316,7 +2361,12 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     }
   }
   if (early) {  // hashed already: publish into the child records; long leaves now
-    if (links) {  // only the listed leaves: the top one, those under deep parents, long ones
+    if (lpos) {  // leaf positions: only the long leaves' parents and arena slots
+      if (nlong) {
+        hipLaunchKernelGGL(k_leaf_fix, GRID(nlong, BS), dim3(BS), 0, st, T, (uint64_t)0, nlong);
+        LAUNCH_CHECK();
+      }
+    } else if (links) {  // only the listed leaves: the top one, those under deep parents, long ones
       if (nfix + nlong) {
         hipLaunchKernelGGL(k_leaf_fix, GRID(nfix + nlong, BS), dim3(BS), 0, st, T, nfix, nlong);
         LAUNCH_CHECK();
@@ -2391,16 +2441,29 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     } else if (coop) {
       hipLaunchKernelGGL(k_branch_coop, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     } else {
+      const bool small = !A.kn && !rescan && small_levels && cnt <= small_level;
+      const bool pos = T.cend && !small && pos_level_ok(T, (uint32_t)d);  // leaf children from their stashes
+      if (T.cend && !pos) {  // leaf positions elsewhere: the level's leaf child records first
+        hipLaunchKernelGGL(k_level_leafrecs, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+        LAUNCH_CHECK();
+      }
       if (A.kn)
         hipLaunchKernelGGL(k_branch_fused<0>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
       else if (rescan)
         hipLaunchKernelGGL(k_branch_fused<1>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
-      else if (small_levels && !T.links && cnt <= xl_level)
+      else if (small && !T.links && cnt <= xl_level)
         hipLaunchKernelGGL(k_branch_xl, dim3((unsigned)((cnt + 1) / 2)), dim3(64), 0, st, T, (uint64_t)lbh[d],
                            (uint64_t)cnt);
-      else if (small_levels && cnt <= small_level)
+      else if (small)
         hipLaunchKernelGGL(k_branch_small, dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, T, (uint64_t)lbh[d],
                            (uint64_t)cnt);
+      else if (pos) {
+        Topo TL = T;
+        TL.lvl_nsh = 28 - 4 * (uint32_t)d;
+        hipLaunchKernelGGL(k_branch_fused<4>, GRID(cnt, BS), dim3(BS), 0, st, TL, (uint64_t)lbh[d], (uint64_t)cnt);
+      }
+      else if (T.links)
+        hipLaunchKernelGGL(k_branch_fused<5>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
       else if (branch_bs64)
         hipLaunchKernelGGL((k_branch_fused<2, 64>), dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, T,
                            (uint64_t)lbh[d], (uint64_t)cnt);

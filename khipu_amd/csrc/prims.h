@@ -304,11 +304,18 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const K* keys, uint64_t 
   for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
   __syncthreads();
   uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)w * WSLICE;
-#pragma unroll 4
+  // every key of the slice loaded before the first LDS atomic (the atomics would otherwise
+  // hold each load back to its own round trip)
+  uint32_t dg[WSLICE / 64];
+#pragma unroll
   for (int it = 0; it < WSLICE / 64; ++it) {
     uint64_t i = base + (uint64_t)it * 64 + lane;
-    if (i < n) atomicAdd(&h[w][(keys[i] >> shift) & 0xFF], 1u);
+    const K kk = keys[i < n ? i : n - 1];  // (unconditional: no branch between the loads)
+    dg[it] = i < n ? (uint32_t)(kk >> shift) & 0xFF : 256u;
   }
+#pragma unroll
+  for (int it = 0; it < WSLICE / 64; ++it)
+    if (dg[it] < 256) atomicAdd(&h[w][dg[it]], 1u);
   __syncthreads();
   for (int d = threadIdx.x; d < 256; d += RS_THREADS) {
     uint32_t s = 0;
@@ -333,6 +340,9 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const 
   __shared__ K sk[TILE];
   __shared__ uint32_t sv[TILE];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // this tile's global base of digit threadIdx.x: loaded now, used after the ranking (one
+  // HBM round trip less in the middle of the tile)
+  const uint32_t gb_pre = fused ? 0u : offs[(uint64_t)threadIdx.x * ntiles + blockIdx.x];
   for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&wc[0][0])[i] = 0;
   __syncthreads();
   const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
@@ -341,12 +351,19 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const 
   uint32_t v[IT];
   uint32_t r[IT];
   const uint64_t lt = lanemask_lt();
+  // the whole slice loaded first: the ranking's LDS traffic and wave barriers would otherwise
+  // hold each load back to its own HBM round trip (16 in a row per tile)
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     uint64_t i = base + (uint64_t)it * 64 + lane;
     bool valid = i < n;
     k[it] = valid ? keys[i] : 0;
     v[it] = valid ? vals[i] : 0;
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    uint64_t i = base + (uint64_t)it * 64 + lane;
+    bool valid = i < n;
     uint32_t d = (uint32_t)(k[it] >> shift) & 0xFF;
     uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -385,7 +402,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const 
       }
       gbase[d] = block_exclusive_scan<uint32_t>(all, lw, &tot) + pre;
     } else {
-      gbase[d] = offs[(uint64_t)d * ntiles + blockIdx.x];
+      gbase[d] = gb_pre;
     }
   }
   __syncthreads();

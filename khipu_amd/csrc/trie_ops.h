@@ -222,6 +222,15 @@ struct Topo {
   uint32_t links;      // child records may be leaf LINKS (CM_LINK: cref holds the sorted position whose
                        // stash lf_eref is the reference; op_leaf_link_rec, op_branch_stream)
   uint32_t* fixlist;   // [m] sorted leaves the post-join pass publishes (top, or parent depth >= LINK_PD_MAX)
+  // leaf positions (default for unsegmented plain root builds): the leaves write no child
+  // records.  A branch child's record carries CM_BR and the end of its key range (cend), so
+  // the parent walks its range and finds each leaf child at the next sorted position, whose
+  // stash (lf_eref / lf_emeta) is the reference (op_branch_stream, op_leaf_children)
+  uint32_t lpos;       // set before the leaf kernel: a top leaf publishes its result itself
+  uint32_t lf_inline;  // some leaf is inline (else every leaf child is a 32-byte hash)
+  uint32_t* br_end;    // [B] one past the last sorted key of the branch's range (nullable)
+  uint32_t* cend;      // [C] at a branch child's record: that branch's br_end (nullable: no positions)
+  uint32_t lvl_nsh;    // per level launch: 28 - 4 * the level's depth (a leaf child's nibble in sck)
   uint32_t* longlist;  // [m] sorted leaves longer than one Keccak block (the leaf kernel lists them)
   // element builds (resident commits, forest.h; all nullable): an element is a leaf, or
   // a SUBTREE standing for an unchanged branch at depth el_db[i] whose capped reference
@@ -557,6 +566,7 @@ KH_HD void op_branch_topo(const Topo& T, const Pyr& P, uint64_t nb, uint64_t b) 
   T.br_parent[j] = Pp.bid;
   T.br_pord[j] = (uint8_t)Pp.pord;
   T.br_first[j] = (uint32_t)(a + 1);
+  if (T.br_end) T.br_end[j] = c < 0 ? (uint32_t)T.m : (uint32_t)c + 1;  // boundary c follows key c
 }
 
 // ---- leaf geometry
@@ -623,8 +633,9 @@ KH_HD void op_leaf_topo(const Topo& T, uint64_t i, AllocFn alloc) {
 
 // ---- publishing a finished node's reference into its parent's child record or
 // the segment result.  enc: the node's encoding in the arena (used when L < 32).
+constexpr uint16_t CM_BR = 0x4000;  // leaf positions: the record is a branch child's (cend holds its end)
 KH_HD void publish_ref(const Topo& T, uint32_t parent, uint32_t pord, uint32_t nib, uint64_t first_key,
-                       const uint64_t* enc, uint32_t L, const uint64_t h[4]) {
+                       const uint64_t* enc, uint32_t L, const uint64_t h[4], uint16_t mflag = 0) {
   uint64_t w[4];
   for (int j = 0; j < 4; ++j) {
     uint32_t base = 8u * (uint32_t)j;
@@ -640,7 +651,7 @@ KH_HD void publish_ref(const Topo& T, uint32_t parent, uint32_t pord, uint32_t n
   } else {
     uint64_t slot = (uint64_t)T.br_cbase[parent] + pord;
     for (int j = 0; j < 4; ++j) T.cref[4 * slot + j] = w[j];
-    T.cmeta[slot] = (uint16_t)((L >= 32 ? 32u : L) | (nib << 8));
+    T.cmeta[slot] = (uint16_t)((L >= 32 ? 32u : L) | (nib << 8) | mflag);
   }
 }
 
@@ -796,9 +807,17 @@ KH_HD void leaf_publish_at(const Topo& T, uint64_t i, uint32_t L, const uint64_t
     }
     T.lf_rlen[i] = L;
   }
+  *inl = (L < 32 && !top) ? 1 : 0;
+  if (T.cend && !top) {  // leaf positions (a long leaf): the stash, where the parent reads it
+    for (int q = 0; q < 4; ++q) {
+      uint32_t base = 8u * (uint32_t)q;
+      T.lf_eref[4 * i + q] = L >= 32 ? hh[q] : (base < L ? head[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0);
+    }
+    T.lf_emeta[i] = (uint8_t)(L >= 32 ? 32 : L);
+    return;
+  }
   uint32_t nib = top ? 0 : leaf_nibble(T, i);
   publish_ref(T, parent, T.lf_pord[i], nib, i, head, L, hh);
-  *inl = (L < 32 && !top) ? 1 : 0;
 }
 
 // hash + publish of leaf i whose encoding (L bytes) sits at w, words `stride` apart
@@ -1218,6 +1237,7 @@ KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, u
   // a top leaf is >= 35 B, so its stash is always the hash; the preset 32 stands for every
   // hashed leaf (one scattered byte write less per leaf)
   if (L < 32) T.lf_emeta[si] = (uint8_t)L;
+  if (top && T.lpos) publish_ref(T, NONE, 0, 0, si, r, 32, r);  // leaf positions: no post-join pass
   return perms;
 }
 // input order (k_leaf_in): the parent depth and sorted position scattered by k_ansv_pd
@@ -1462,8 +1482,10 @@ KH_HD uint32_t branch_publish(const Topo& T, uint32_t j, uint32_t L, const uint6
   bool top = parent == NONE;
   const Key4 key = sorted_key(T, first, d);
   uint32_t nib = top ? 0 : key_nibble(key, pd);
+  const uint16_t mf = T.cend ? CM_BR : 0;
+  if (T.cend && !top) T.cend[(uint64_t)T.br_cbase[parent] + T.br_pord[j]] = T.br_end[j];
   if (ext == 0) {
-    publish_ref(T, parent, T.br_pord[j], nib, first, bhead, L, hb);
+    publish_ref(T, parent, T.br_pord[j], nib, first, bhead, L, hb, mf);
     return 0;
   }
   uint32_t s = (uint32_t)(pd + 1);
@@ -1502,7 +1524,7 @@ KH_HD uint32_t branch_publish(const Topo& T, uint32_t j, uint32_t L, const uint6
     T.ex_rlen[j] = XL;
   }
   *ninl += (XL < 32 && !top) ? 1 : 0;
-  publish_ref(T, parent, T.br_pord[j], nib, first, xhead, XL, hx);
+  publish_ref(T, parent, T.br_pord[j], nib, first, xhead, XL, hx, mf);
   return perms;
 }
 
@@ -1707,13 +1729,46 @@ KH_HD uint32_t op_branch_direct(const Topo& T, uint32_t j, uint64_t* slot, uint6
 // The child records: by default the level's records in HBM (cm / cr at the branch's child
 // base, word q of child c at cr[4c + q]); k_branch_fused<3> (small levels) passes a copy in
 // LDS, lane-interleaved: child c's meta at cm[c * cs], word q at cr[(4c + q) * cs].
+// leaf positions: the branch kernel reads a leaf child's nibble from the sorted 32-bit
+// prefixes (unsegmented: 8 nibbles), so levels below depth 8 take it; the deeper (small)
+// levels take their records from op_leaf_children
+KH_HD bool pos_level_ok(const Topo& T, uint32_t d) { return T.sck && T.ck_sb == 0 && d < 8; }
+// the meta of the leaf child at sorted position pos of a branch of the level being built
+// (pos_level_ok; T.lvl_nsh set for the level: a kernel argument, not a register per lane)
+KH_HD uint32_t leaf_child_meta(const Topo& T, uint64_t pos) {
+  const uint32_t len = T.lf_inline ? T.lf_emeta[pos] : 32u;
+  return len | (((T.sck[pos] >> T.lvl_nsh) & 0xF) << 8);
+}
+// ... and its child records written out (the small levels, whose kernels copy every record
+// of a branch at once): the branch's range walked child by child
+KH_HD void op_leaf_children(const Topo& T, uint32_t j) {
+  const uint32_t k = T.br_k[j], d = T.br_depth[j];
+  const uint64_t cb = T.br_cbase[j];
+  uint64_t pos = T.br_first[j];
+  for (uint32_t c = 0; c < k; ++c) {
+    const uint16_t mc = T.cmeta[cb + c];
+    if (mc & CM_BR) {
+      pos = T.cend[cb + c];
+      continue;
+    }
+    const uint64_t* r = T.lf_eref + 4 * pos;
+    for (int q = 0; q < 4; ++q) T.cref[4 * (cb + c) + q] = r[q];
+    T.cmeta[cb + c] = (uint16_t)(T.lf_emeta[pos] | (key_nibble(sorted_key(T, pos, d + 1), (int)d) << 8));
+    ++pos;
+  }
+}
+
 struct ChildSrc {
   const uint16_t* cm = nullptr;
   const uint64_t* cr = nullptr;
   uint32_t cs = 1;
 };
-KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl,
-                                ChildSrc src = ChildSrc{}) {
+// where op_branch_stream reads the children (one instantiation each, so that a kernel
+// carries no dead path: the branch kernels sit at the VGPR limit of 4 waves per SIMD)
+enum { SRC_REC = 0, SRC_LDS = 1, SRC_LINK = 2, SRC_POS = 3 };
+template <int SRC>
+KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl,
+                                  ChildSrc src) {
   const uint32_t ext = T.br_ext[j];
   const bool top = T.br_parent[j] == NONE;
   *inl = 0;
@@ -1721,19 +1776,37 @@ KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint6
   uint32_t L, perms = 0, ninl = 0;
   {
     const uint32_t k = T.br_k[j];
-    const uint32_t cs = src.cs;
-    const uint16_t* cm = src.cm;
-    const uint64_t* cr = src.cr;
-    if (!cm) {
-      const uint64_t cb = T.br_cbase[j];
-      cm = T.cmeta + cb;
-      cr = T.cref + 4 * cb;
-    }
+    // global records are addressed from the branch's child base (one register, not three pointers)
+    const uint32_t cb = SRC == SRC_LDS ? 0u : T.br_cbase[j];
+    const uint32_t cs = SRC == SRC_LDS ? src.cs : 1u;
+    auto cmeta_at = [&](uint32_t c) -> uint32_t { return SRC == SRC_LDS ? src.cm[c * cs] : T.cmeta[cb + c]; };
+    auto cref_at = [&](uint32_t c) -> const uint64_t* {
+      return SRC == SRC_LDS ? src.cr + 4 * c * cs : T.cref + 4 * (uint64_t)(cb + c);
+    };
     uint32_t payload = 1 + (16 - k);  // terminator "" + empty slots
+    uint32_t brm = 0;                 // leaf positions: bit c = child c is a branch
+    if (SRC == SRC_POS) {  // a leaf child's length from its stash meta (32 unless some leaf is inline)
+      uint32_t pos = T.br_first[j];
 #pragma unroll
-    for (uint32_t c = 0; c < 16; ++c) {
-      const uint32_t len = c < k ? (uint32_t)(cm[c * cs] & 0xFF) : 0;
-      payload += len == 32 ? 33 : len;
+      for (uint32_t c = 0; c < 16; ++c) {
+        if (c < k) {
+          const uint32_t mc = cmeta_at(c);
+          const bool br = mc & CM_BR;
+          brm |= br ? 1u << c : 0u;
+          uint32_t len = br ? mc & 0xFF : 32u;
+          if (T.lf_inline) {  // (the positions are walked only when some leaf may be inline)
+            if (!br) len = T.lf_emeta[pos];
+            pos = br ? T.cend[cb + c] : pos + 1;
+          }
+          payload += len == 32 ? 33 : len;
+        }
+      }
+    } else {
+#pragma unroll
+      for (uint32_t c = 0; c < 16; ++c) {
+        const uint32_t len = c < k ? (cmeta_at(c) & 0xFF) : 0;
+        payload += len == 32 ? 33 : len;
+      }
     }
     const uint32_t hh = rlp_hdr_len(payload);
     L = hh + payload;
@@ -1767,11 +1840,20 @@ KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint6
     uint64_t I[5] = {0, 0, 0, 0, 0};
     uint64_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
     uint32_t nm = 0;
-    // child c's reference: its record, or the stash a LINK record points at (op_leaf_link_rec)
+    uint32_t lpn = SRC == SRC_POS ? T.br_first[j] : 0;  // leaf positions: sorted position of child cc
+    // child c's reference: its record, or the stash a LINK record points at (op_leaf_link_rec),
+    // or (leaf positions) a leaf child's stash at the next position of the range
     auto load_child = [&](uint32_t cc) {
-      nm = cm[cc * cs];
-      const uint64_t* p = cr + 4 * cc * cs;
-      if (T.links && (nm & CM_LINK)) {
+      nm = cmeta_at(cc);
+      const uint64_t* p = cref_at(cc);
+      if (SRC == SRC_POS) {  // every address known up front (the kind from brm): one round trip
+        const bool br = (brm >> cc) & 1;
+        const uint32_t lm = leaf_child_meta(T, lpn), e = T.cend[cb + cc];  // (e: unset for a leaf slot)
+        if (!br) p = T.lf_eref + 4 * (uint64_t)lpn;
+        nm = br ? nm : lm;
+        lpn = br ? e : lpn + 1;
+        n0 = p[0], n1 = p[1], n2 = p[2], n3 = p[3];
+      } else if (SRC == SRC_LINK && (nm & CM_LINK)) {
         p = T.lf_eref + 4 * p[0];
         n0 = p[0], n1 = p[1], n2 = p[2], n3 = p[3];
       } else {
@@ -1841,6 +1923,23 @@ KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint6
   perms += branch_publish(T, j, L, hb, bhead, Slot{slot, stride}, &ninl);
   *inl = ninl;
   return perms;
+}
+
+// runtime choice of the child source (the host replay; the kernels instantiate theirs)
+KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl,
+                                ChildSrc src = ChildSrc{}) {
+  if (src.cm) return op_branch_stream_t<SRC_LDS>(T, j, slot, stride, inl, src);
+  if (T.cend) {
+    if (pos_level_ok(T, T.br_depth[j])) {
+      Topo TL = T;
+      TL.lvl_nsh = 28 - 4 * T.br_depth[j];
+      return op_branch_stream_t<SRC_POS>(TL, j, slot, stride, inl, src);
+    }
+    op_leaf_children(T, j);  // (as the device runs a deep level: the records, then the stream)
+    return op_branch_stream_t<SRC_REC>(T, j, slot, stride, inl, src);
+  }
+  if (T.links) return op_branch_stream_t<SRC_LINK>(T, j, slot, stride, inl, src);
+  return op_branch_stream_t<SRC_REC>(T, j, slot, stride, inl, src);
 }
 
 // node hashes op_branch_hash(T, j, ...) spent `perms` on: the branch if it was

@@ -26,7 +26,10 @@ using namespace khst;
 static int g_leaf_mode = 0;
 // 1: the leaves' child records as links (op_leaf_link_rec, KHST_LEAF_LINKS=1) with the
 // post-join fix pass and op_branch_stream on every branch; 0: link slots + the copy pass
-// (the device default)
+// (KHST_LEAF_POS=0); 2: leaf positions (the device default for unsegmented builds): no leaf
+// child records, the branches read each leaf child's stash at its sorted position, on
+// alternate branches straight from the stash (op_branch_stream) and through the records a
+// small level writes first (op_leaf_children)
 static int g_link_mode = 0;
 
 // keys: n*32 (already keccak'd), vals/voff packed; seg nullable.
@@ -118,6 +121,12 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.ctr = ctr.data();
   T.depth_hist = hist.data();
   uint64_t B = 0;
+  const bool lpos = g_link_mode == 2 && !segmented && g_leaf_mode != 2;  // (as on the device: not with v2)
+  std::vector<uint32_t> br_end(nbb, 0);
+  if (lpos) {
+    T.br_end = br_end.data();
+    T.lpos = 1;
+  }
   std::vector<std::vector<uint8_t>> pyr;
   Pyr P{};
   // unsegmented builds take the device's ck path: boundary values from the sorted first
@@ -176,7 +185,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.lf_emeta = emeta.data();
   T.pdinv = pdinv.data();
   std::vector<uint32_t> longlist(m + 1);
-  T.longlist = g_link_mode ? longlist.data() : nullptr;
+  T.longlist = (g_link_mode == 1 || lpos) ? longlist.data() : nullptr;
   T.svoff = nullptr;  // as on the device: no sorted spans in early builds
   T.svlen = nullptr;
   for (uint64_t i = 0; i < m; ++i) op_pd_scatter(T, i);
@@ -242,8 +251,12 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   };
   std::vector<uint64_t> dst(m + 1);
   T.lf_dst = dst.data();
-  const bool links = early && g_link_mode;
-  if (links) {  // the device default: link records, then the fix pass over the listed leaves
+  const bool links = early && g_link_mode == 1;
+  std::vector<uint32_t> cend(C + 1, 0);
+  if (lpos) {  // only the long leaves' parents and arena slots
+    T.lf_inline = inl ? 1 : 0;
+    for (uint64_t q = 0; q < ctr[CTR_LONGN]; ++q) op_leaf_topo_early(T, longlist[q], bump);
+  } else if (links) {  // the device default: link records, then the fix pass over the listed leaves
     std::vector<uint32_t> fix;
     for (uint64_t i = 0; i < m; ++i)
       if (op_leaf_link_rec(T, i)) fix.push_back((uint32_t)i);
@@ -281,6 +294,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.arena = (uint8_t*)arena.data();
   if (!early)
     for (uint64_t i = 0; i < m; ++i) op_leaf_prep(T, i, T.vals + T.svoff[i], T.svlen[i]);
+  if (lpos) T.cend = cend.data();  // (set after the leaf kernel, as on the device)
   for (uint64_t i = 0; i < m; ++i) {
     uint32_t in1 = 0;
     uint32_t p = early ? op_leaf_long(T, i, &in1) : op_leaf_hash(T, i, &in1);
@@ -296,9 +310,16 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       uint32_t in1 = 0;
       uint64_t slot[LEAF_WORDS + 1];
       // fixed-length keys: both device assemblies, on alternate branches
-      uint32_t p = T.kn                  ? op_branch_fused(T, j, slot, 1, &in1)
-                   : ((j & 1) && !T.links) ? op_branch_direct(T, j, slot, 1, &in1)
-                                           : op_branch_stream(T, j, slot, 1, &in1);
+      uint32_t p;
+      if (lpos && (j & 1)) {  // a small level's path: records written, then read as a copy
+        op_leaf_children(T, j);
+        const uint64_t cb = T.br_cbase[j];
+        p = op_branch_stream(T, j, slot, 1, &in1, ChildSrc{T.cmeta + cb, T.cref + 4 * cb, 1});
+      } else {
+        p = T.kn                            ? op_branch_fused(T, j, slot, 1, &in1)
+            : ((j & 1) && !T.links && !lpos) ? op_branch_direct(T, j, slot, 1, &in1)
+                                             : op_branch_stream(T, j, slot, 1, &in1);
+      }
       perms += p;
       hashes += branch_hash_count(T, j, p);
       inl += in1;

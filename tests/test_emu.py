@@ -24,7 +24,7 @@ def leaf_mode(request):
     E.set_leaf_mode(0)
 
 
-@pytest.fixture(params=[0, 1], ids=["move", "links"])
+@pytest.fixture(params=[0, 1, 2], ids=["move", "links", "positions"])
 def link_mode(request):
     """How the early leaves reach their parents' child records (g_link_mode)."""
     E.set_link_mode(request.param)
