@@ -887,7 +887,8 @@ __global__ void __launch_bounds__(BS) k_branch_hash(Topo T, uint64_t first, uint
 // V: 0 variable-length keys (op_branch_fused), 1 direct window assembly re-scanning the
 // children per window (op_branch_direct), 2 the children streamed once with the next
 // record prefetched (op_branch_stream), 4 the same reading leaf children at their sorted
-// positions (leaf positions), 5 following link records (KHST_LEAF_LINKS=1)
+// positions (leaf positions), 6 the same below depth 8 (the nibble from the input key), 5
+// following link records (KHST_LEAF_LINKS=1)
 // WB: threads per block.  WB = 64 (KHST_BRANCH_BS=64, measurement switch): one wave per
 // block, 8,704 B of LDS, so a CU holds 18 waves instead of the 16 that 35 KB blocks of 256
 // threads allow (4.5 per SIMD instead of 4); the counters are summed per wave.
@@ -906,6 +907,7 @@ __global__ void __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(4, 8)))
             : V == 1 ? op_branch_direct(T, j, sl, 1, &in1)
             : V == 2 ? op_branch_stream_t<SRC_REC>(T, j, sl, 1, &in1, ChildSrc{})
             : V == 4 ? op_branch_stream_t<SRC_POS>(T, j, sl, 1, &in1, ChildSrc{})
+            : V == 6 ? op_branch_stream_t<SRC_POSK>(T, j, sl, 1, &in1, ChildSrc{})
                      : op_branch_stream_t<SRC_LINK>(T, j, sl, 1, &in1, ChildSrc{});
     hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
@@ -2442,8 +2444,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       hipLaunchKernelGGL(k_branch_coop, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     } else {
       const bool small = !A.kn && !rescan && small_levels && cnt <= small_level;
-      const bool pos = T.cend && !small && pos_level_ok(T, (uint32_t)d);  // leaf children from their stashes
-      if (T.cend && !pos) {  // leaf positions elsewhere: the level's leaf child records first
+      const bool pos = T.cend && !small;  // leaf children from their stashes
+      if (T.cend && small) {  // leaf positions, a small level: the level's leaf child records first
         hipLaunchKernelGGL(k_level_leafrecs, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
         LAUNCH_CHECK();
       }
@@ -2459,8 +2461,12 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
                            (uint64_t)cnt);
       else if (pos) {
         Topo TL = T;
-        TL.lvl_nsh = 28 - 4 * (uint32_t)d;
-        hipLaunchKernelGGL(k_branch_fused<4>, GRID(cnt, BS), dim3(BS), 0, st, TL, (uint64_t)lbh[d], (uint64_t)cnt);
+        TL.lvl_depth = (uint32_t)d;
+        TL.lvl_nsh = 28 - 4 * ((uint32_t)d & 7);
+        if (pos_level_ok(T, (uint32_t)d))
+          hipLaunchKernelGGL(k_branch_fused<4>, GRID(cnt, BS), dim3(BS), 0, st, TL, (uint64_t)lbh[d], (uint64_t)cnt);
+        else
+          hipLaunchKernelGGL(k_branch_fused<6>, GRID(cnt, BS), dim3(BS), 0, st, TL, (uint64_t)lbh[d], (uint64_t)cnt);
       }
       else if (T.links)
         hipLaunchKernelGGL(k_branch_fused<5>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);

@@ -231,6 +231,7 @@ struct Topo {
   uint32_t* br_end;    // [B] one past the last sorted key of the branch's range (nullable)
   uint32_t* cend;      // [C] at a branch child's record: that branch's br_end (nullable: no positions)
   uint32_t lvl_nsh;    // per level launch: 28 - 4 * the level's depth (a leaf child's nibble in sck)
+  uint32_t lvl_depth;  //   and the depth itself (deeper levels: the nibble from the input key)
   uint32_t* longlist;  // [m] sorted leaves longer than one Keccak block (the leaf kernel lists them)
   // element builds (resident commits, forest.h; all nullable): an element is a leaf, or
   // a SUBTREE standing for an unchanged branch at depth el_db[i] whose capped reference
@@ -1730,14 +1731,18 @@ KH_HD uint32_t op_branch_direct(const Topo& T, uint32_t j, uint64_t* slot, uint6
 // base, word q of child c at cr[4c + q]); k_branch_fused<3> (small levels) passes a copy in
 // LDS, lane-interleaved: child c's meta at cm[c * cs], word q at cr[(4c + q) * cs].
 // leaf positions: the branch kernel reads a leaf child's nibble from the sorted 32-bit
-// prefixes (unsegmented: 8 nibbles), so levels below depth 8 take it; the deeper (small)
-// levels take their records from op_leaf_children
+// prefixes (unsegmented: 8 nibbles) for levels below depth 8 (pos_level_ok), and from the
+// input key through the sort index below that (SRC_POSK); small levels take their records
+// from op_leaf_children
 KH_HD bool pos_level_ok(const Topo& T, uint32_t d) { return T.sck && T.ck_sb == 0 && d < 8; }
 // the meta of the leaf child at sorted position pos of a branch of the level being built
-// (pos_level_ok; T.lvl_nsh set for the level: a kernel argument, not a register per lane)
+// (T.lvl_nsh / lvl_depth set for the level: kernel arguments, not registers per lane)
+template <bool DEEP>
 KH_HD uint32_t leaf_child_meta(const Topo& T, uint64_t pos) {
   const uint32_t len = T.lf_inline ? T.lf_emeta[pos] : 32u;
-  return len | (((T.sck[pos] >> T.lvl_nsh) & 0xF) << 8);
+  const uint32_t nib = DEEP ? key_nibble(sorted_key(T, pos, T.lvl_depth + 1), (int)T.lvl_depth)
+                            : (T.sck[pos] >> T.lvl_nsh) & 0xF;
+  return len | (nib << 8);
 }
 // ... and its child records written out (the small levels, whose kernels copy every record
 // of a branch at once): the branch's range walked child by child
@@ -1765,7 +1770,7 @@ struct ChildSrc {
 };
 // where op_branch_stream reads the children (one instantiation each, so that a kernel
 // carries no dead path: the branch kernels sit at the VGPR limit of 4 waves per SIMD)
-enum { SRC_REC = 0, SRC_LDS = 1, SRC_LINK = 2, SRC_POS = 3 };
+enum { SRC_REC = 0, SRC_LDS = 1, SRC_LINK = 2, SRC_POS = 3, SRC_POSK = 4 };
 template <int SRC>
 KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl,
                                   ChildSrc src) {
@@ -1785,7 +1790,8 @@ KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uin
     };
     uint32_t payload = 1 + (16 - k);  // terminator "" + empty slots
     uint32_t brm = 0;                 // leaf positions: bit c = child c is a branch
-    if (SRC == SRC_POS) {  // a leaf child's length from its stash meta (32 unless some leaf is inline)
+    constexpr bool POS = SRC == SRC_POS || SRC == SRC_POSK;
+    if (POS) {  // a leaf child's length from its stash meta (32 unless some leaf is inline)
       uint32_t pos = T.br_first[j];
 #pragma unroll
       for (uint32_t c = 0; c < 16; ++c) {
@@ -1840,15 +1846,15 @@ KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uin
     uint64_t I[5] = {0, 0, 0, 0, 0};
     uint64_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
     uint32_t nm = 0;
-    uint32_t lpn = SRC == SRC_POS ? T.br_first[j] : 0;  // leaf positions: sorted position of child cc
+    uint32_t lpn = POS ? T.br_first[j] : 0;  // leaf positions: sorted position of child cc
     // child c's reference: its record, or the stash a LINK record points at (op_leaf_link_rec),
     // or (leaf positions) a leaf child's stash at the next position of the range
     auto load_child = [&](uint32_t cc) {
       nm = cmeta_at(cc);
       const uint64_t* p = cref_at(cc);
-      if (SRC == SRC_POS) {  // every address known up front (the kind from brm): one round trip
+      if (POS) {  // every address known up front (the kind from brm): one round trip
         const bool br = (brm >> cc) & 1;
-        const uint32_t lm = leaf_child_meta(T, lpn), e = T.cend[cb + cc];  // (e: unset for a leaf slot)
+        const uint32_t lm = leaf_child_meta<SRC == SRC_POSK>(T, lpn), e = T.cend[cb + cc];  // (e: unset for a leaf slot)
         if (!br) p = T.lf_eref + 4 * (uint64_t)lpn;
         nm = br ? nm : lm;
         lpn = br ? e : lpn + 1;
@@ -1930,13 +1936,11 @@ KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint6
                                 ChildSrc src = ChildSrc{}) {
   if (src.cm) return op_branch_stream_t<SRC_LDS>(T, j, slot, stride, inl, src);
   if (T.cend) {
-    if (pos_level_ok(T, T.br_depth[j])) {
-      Topo TL = T;
-      TL.lvl_nsh = 28 - 4 * T.br_depth[j];
-      return op_branch_stream_t<SRC_POS>(TL, j, slot, stride, inl, src);
-    }
-    op_leaf_children(T, j);  // (as the device runs a deep level: the records, then the stream)
-    return op_branch_stream_t<SRC_REC>(T, j, slot, stride, inl, src);
+    Topo TL = T;
+    TL.lvl_depth = T.br_depth[j];
+    TL.lvl_nsh = 28 - 4 * (TL.lvl_depth & 7);
+    if (pos_level_ok(T, T.br_depth[j])) return op_branch_stream_t<SRC_POS>(TL, j, slot, stride, inl, src);
+    return op_branch_stream_t<SRC_POSK>(TL, j, slot, stride, inl, src);
   }
   if (T.links) return op_branch_stream_t<SRC_LINK>(T, j, slot, stride, inl, src);
   return op_branch_stream_t<SRC_REC>(T, j, slot, stride, inl, src);
