@@ -449,6 +449,66 @@ __global__ void __launch_bounds__(BS) k_ansv(Topo T, Pyr P, uint64_t nb) {
 __global__ void __launch_bounds__(BS) k_chain(Topo T, uint64_t nb) {
   GRID_STRIDE(b, nb) op_chain(T, b);
 }
+// The same with TOPO_ILP boundaries per thread walked in lockstep (one load per live chain
+// and step, all issued together): the same memory parallelism from a quarter of the waves,
+// which the leaf kernel beside it keeps (KHST_TOPO_ILP, with the grid cap KHST_TOPO_BPC)
+constexpr int TOPO_ILP = 4;
+__global__ void __launch_bounds__(BS) k_chain_ilp(Topo T, uint64_t nb) {
+  const uint64_t S = (uint64_t)gridDim.x * BS;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * BS + threadIdx.x; b0 < nb; b0 += TOPO_ILP * S) {
+    uint64_t b[TOPO_ILP];
+    uint32_t t[TOPO_ILP], o[TOPO_ILP];
+    int64_t j[TOPO_ILP];
+    bool live[TOPO_ILP];
+#pragma unroll
+    for (int q = 0; q < TOPO_ILP; ++q) {
+      b[q] = b0 + q * S;
+      t[q] = b[q] < nb ? T.u[b[q]] : 0;
+      j[q] = (int64_t)b[q];
+      o[q] = 0;
+      live[q] = t[q] != 0;
+    }
+    for (int step = 0; step < 16; ++step) {  // (a chain has at most 15 steps: op_chain)
+      int32_t nx[TOPO_ILP];
+#pragma unroll
+      for (int q = 0; q < TOPO_ILP; ++q) nx[q] = live[q] ? T.pse[j[q]] : -1;
+      bool any = false;
+#pragma unroll
+      for (int q = 0; q < TOPO_ILP; ++q) {
+        if (live[q]) {
+          if (nx[q] < 0) {
+            live[q] = false;
+          } else {
+            j[q] = nx[q];
+            if (++o[q] > 15) {  // impossible for a 16-ary trie: flag corruption
+              T.ctr[CTR_ERR] = 1;
+              live[q] = false;
+            }
+          }
+        }
+        any |= live[q];
+      }
+      if (!any) break;
+    }
+    uint8_t gl[TOPO_ILP];
+#pragma unroll
+    for (int q = 0; q < TOPO_ILP; ++q) gl[q] = (b[q] < nb && t[q] != 0) ? T.glast[b[q]] : 0;
+#pragma unroll
+    for (int q = 0; q < TOPO_ILP; ++q) {
+      if (b[q] >= nb) continue;
+      if (t[q] == 0) {
+        T.rep[b[q]] = NONE;
+        T.ord[b[q]] = 0;
+        T.isrep_bid[b[q]] = 0;
+        continue;
+      }
+      T.rep[b[q]] = (uint32_t)j[q];
+      T.ord[b[q]] = (uint8_t)o[q];
+      T.isrep_bid[b[q]] = (o[q] == 0) ? 1u : 0u;
+      if (gl[q]) T.gk[j[q]] = (uint8_t)(o[q] + 2);  // the group's last member: o + 2 children
+    }
+  }
+}
 // k_ansv with the early leaves' parent-depth scatter folded in (thread i also scatters
 // leaf i; grid over the m leaves): the leaf kernel waits for this kernel instead of a
 // separate k_pd_scatter racing the topology for the memory system (run_build)
@@ -480,6 +540,83 @@ __device__ __forceinline__ void block_add3(unsigned long long* c0, unsigned long
   }
 }
 
+// op_branch_topo with TOPO_ILP boundaries per thread, each load round issued for all of them
+// together (k_chain_ilp)
+__global__ void __launch_bounds__(BS) k_branch_topo_ilp(Topo T, uint64_t nb) {
+  const uint64_t S = (uint64_t)gridDim.x * BS;
+  unsigned long long ext = 0;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * BS + threadIdx.x; b0 < nb; b0 += TOPO_ILP * S) {
+    uint64_t b[TOPO_ILP];
+    bool rep[TOPO_ILP];
+    uint32_t t[TOPO_ILP];
+#pragma unroll
+    for (int q = 0; q < TOPO_ILP; ++q) {
+      b[q] = b0 + q * S;
+      const uint64_t bb = b[q] < nb ? b[q] : 0;
+      t[q] = T.u[bb];
+      const uint32_t r = T.rep[bb];
+      rep[q] = b[q] < nb && t[q] != 0 && r == (uint32_t)b[q];
+    }
+    uint32_t j[TOPO_ILP], gk[TOPO_ILP];
+    int64_t a[TOPO_ILP], c[TOPO_ILP];
+#pragma unroll
+    for (int q = 0; q < TOPO_ILP; ++q) {
+      const uint64_t bb = rep[q] ? b[q] : 0;
+      j[q] = T.isrep_bid[bb];
+      a[q] = T.psv[bb];
+      c[q] = T.nsv[bb];
+      gk[q] = T.gk[bb];
+    }
+    // resolve_parent for every boundary at once: both sides, then the reps' branch ids
+    uint32_t va[TOPO_ILP], vc[TOPO_ILP], ra[TOPO_ILP], rc[TOPO_ILP], oa[TOPO_ILP], oc[TOPO_ILP];
+#pragma unroll
+    for (int q = 0; q < TOPO_ILP; ++q) {
+      const bool ha = rep[q] && a[q] >= 0, hc = rep[q] && c[q] >= 0;
+      const uint64_t ia = ha ? (uint64_t)a[q] : 0, ic = hc ? (uint64_t)c[q] : 0;
+      va[q] = ha ? T.u[ia] : 0;
+      vc[q] = hc ? T.u[ic] : 0;
+      ra[q] = ha ? T.rep[ia] : NONE;
+      rc[q] = hc ? T.rep[ic] : NONE;
+      oa[q] = ha ? T.ord[ia] : 0;
+      oc[q] = hc ? T.ord[ic] : 0;
+    }
+    uint32_t ba[TOPO_ILP], bc[TOPO_ILP];
+#pragma unroll
+    for (int q = 0; q < TOPO_ILP; ++q) {
+      ba[q] = (va[q] && ra[q] != NONE) ? T.isrep_bid[ra[q]] : NONE;
+      bc[q] = (vc[q] && rc[q] != NONE) ? T.isrep_bid[rc[q]] : NONE;
+    }
+#pragma unroll
+    for (int q = 0; q < TOPO_ILP; ++q) {
+      if (!rep[q]) continue;
+      Parent Pp;
+      if (va[q] == 0 && vc[q] == 0) {
+        Pp.bid = NONE;
+        Pp.pd = (int32_t)T.depth0 - 1;
+        Pp.pord = 0;
+      } else if (va[q] >= vc[q]) {
+        Pp.bid = ba[q];
+        Pp.pd = (int32_t)va[q] - 1;
+        Pp.pord = oa[q] + 1u;
+      } else {
+        Pp.bid = bc[q];
+        Pp.pd = (int32_t)vc[q] - 1;
+        Pp.pord = oc[q];
+      }
+      const uint32_t d = t[q] - 1u, e = (uint32_t)((int32_t)d - Pp.pd - 1);
+      const uint32_t jj = j[q];
+      T.br_k[jj] = gk[q];
+      T.br_depth[jj] = (uint8_t)d;
+      T.br_ext[jj] = (uint8_t)e;
+      T.br_parent[jj] = Pp.bid;
+      T.br_pord[jj] = (uint8_t)Pp.pord;
+      T.br_first[jj] = (uint32_t)(a[q] + 1);
+      if (T.br_end) T.br_end[jj] = c[q] < 0 ? (uint32_t)T.m : (uint32_t)c[q] + 1;
+      ext += e ? 1 : 0;
+    }
+  }
+  block_add3(ctr_stat(T.ctr, CTR_EXT, blockIdx.x), ext, nullptr, 0, nullptr, 0);
+}
 __global__ void __launch_bounds__(BS) k_branch_topo(Topo T, Pyr P, uint64_t nb) {
   unsigned long long ext = 0;
   GRID_STRIDE(b, nb) {
@@ -2140,6 +2277,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // 8 per CU slow the leaf kernel (18.8 ms, step 48.5).  KHST_TOPO_BPC: blocks per CU
   // (measurement switch; 0 = one thread per element).
   static const int topo_bpc = getenv("KHST_TOPO_BPC") ? atoi(getenv("KHST_TOPO_BPC")) : 4;
+  // KHST_TOPO_ILP=1 (measurement switch): k_chain / k_branch_topo walk TOPO_ILP boundaries
+  // per thread in lockstep (early builds, beside the leaf kernel)
+  static const bool topo_ilp_env = getenv("KHST_TOPO_ILP") && atoi(getenv("KHST_TOPO_ILP")) != 0;
+  const bool topo_ilp = topo_ilp_env && early;
   const uint32_t topo_cap = topo_bpc > 0 ? (uint32_t)(topo_bpc * c->n_cu) : 0u;
   auto topo_grid = [&](uint64_t cnt) {
     const uint64_t g = (cnt + BS - 1) / BS;
@@ -2238,7 +2379,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       }
     }
     if (pd_mode == 1) launch_leaves(false);
-    hipLaunchKernelGGL(k_chain, topo_grid(nb), dim3(BS), 0, st, T, nb);
+    if (topo_ilp)
+      hipLaunchKernelGGL(k_chain_ilp, topo_grid(nb), dim3(BS), 0, st, T, nb);
+    else
+      hipLaunchKernelGGL(k_chain, topo_grid(nb), dim3(BS), 0, st, T, nb);
     LAUNCH_CHECK();
     scan_exclusive<uint32_t>(T.isrep_bid, T.isrep_bid, nb, Bp, scan_scratch, st);
     // branch tables in key-order ids first (k_branch_topo writes them, thread per boundary)
@@ -2250,7 +2394,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     TJ.br_ext = J.ext;
     TJ.br_pord = J.pord;
     TJ.br_end = J.end;
-    hipLaunchKernelGGL(k_branch_topo, topo_grid(nb), dim3(BS), 0, st, TJ, P, nb);
+    if (topo_ilp)
+      hipLaunchKernelGGL(k_branch_topo_ilp, topo_grid(nb), dim3(BS), 0, st, TJ, nb);
+    else
+      hipLaunchKernelGGL(k_branch_topo, topo_grid(nb), dim3(BS), 0, st, TJ, P, nb);
     LAUNCH_CHECK();
     // level order (grids sized by nb; threads past B exit), then every branch id
     // becomes its level position
