@@ -32,6 +32,18 @@ __device__ __forceinline__ void op(uint32_t& a, uint32_t b, uint32_t c) {
   if constexpr (K == 7) asm("v_not_b32_e32 %0, %0" : "+v"(a));
   if constexpr (K == 8) asm("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(a) : "v"(b));
   if constexpr (K == 9) asm("v_alignbit_b32 %0, %0, %0, %1" : "+v"(a) : "v"(b));
+  if constexpr (K == 10) asm("v_perm_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+  if constexpr (K == 11) asm("v_lshlrev_b32_e32 %0, 7, %0" : "+v"(a));
+  if constexpr (K == 13) asm("v_alignbyte_b32 %0, %0, %1, 3" : "+v"(a) : "v"(b));
+}
+// 64-bit kinds (Keccak lanes as whole 64-bit registers: rotations as two 64-bit shifts
+// merged by v_lshl_add_u64, whose two parts never overlap)
+template <int K>
+__device__ __forceinline__ void op64(uint64_t& a, uint64_t b) {
+  if constexpr (K == 20) asm("v_lshlrev_b64 %0, 7, %0" : "+v"(a));
+  if constexpr (K == 21) asm("v_lshrrev_b64 %0, 7, %0" : "+v"(a));
+  if constexpr (K == 22) asm("v_lshl_add_u64 %0, %0, 7, %1" : "+v"(a) : "v"(b));
+  if constexpr (K == 24) asm("v_pk_mov_b32 %0, %0, %1 op_sel:[1,0]" : "+v"(a) : "v"(b));
 }
 
 template <int K>
@@ -53,6 +65,32 @@ __global__ void __launch_bounds__(256) k_peak(uint32_t* out, uint32_t seed) {
 }
 
 template <int K>
+__global__ void __launch_bounds__(256) k_peak64(uint32_t* out, uint32_t seed) {
+  uint64_t a[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) a[j] = (uint64_t)(seed * (threadIdx.x + 1)) * 0x9e3779b97f4a7c15ull + j;
+  const uint64_t b = ((uint64_t)seed << 32) ^ (threadIdx.x * 7);
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < CH; ++j) op64<K>(a[j], b);
+  }
+  uint64_t x = 0;
+#pragma unroll
+  for (int j = 0; j < CH; ++j) x ^= a[j];
+  if ((uint32_t)x == 0x12345678u) out[blockIdx.x] = (uint32_t)(x >> 32);
+}
+
+template <int K>
+static void launch(int blocks, uint32_t* out, uint32_t seed) {
+  if constexpr (K < 20)
+    k_peak<K><<<blocks, 256>>>(out, seed);
+  else
+    k_peak64<K><<<blocks, 256>>>(out, seed);
+}
+
+template <int K>
 static int run(const char* name) {
   int dev = 0, ncu = 0, clk = 0;
   CHK(hipGetDevice(&dev));
@@ -64,10 +102,10 @@ static int run(const char* name) {
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0));
   CHK(hipEventCreate(&e1));
-  k_peak<K><<<blocks, 256>>>(out, 1);
+  launch<K>(blocks, out, 1);
   CHK(hipDeviceSynchronize());
   CHK(hipEventRecord(e0));
-  for (int r = 0; r < 5; ++r) k_peak<K><<<blocks, 256>>>(out, 2 + r);
+  for (int r = 0; r < 5; ++r) launch<K>(blocks, out, 2 + r);
   CHK(hipEventRecord(e1));
   CHK(hipEventSynchronize(e1));
   float ms = 0;
@@ -91,5 +129,13 @@ int main() {
   if (run<6>("v_and_b32_e32")) return 1;
   if (run<7>("v_not_b32_e32")) return 1;
   if (run<8>("v_lshl_or_b32")) return 1;
+  if (run<10>("v_perm_b32")) return 1;
+  if (run<11>("v_lshlrev_b32")) return 1;
+  if (run<13>("v_alignbyte_b32")) return 1;
+  // 64-bit kinds: lane-ops counted as one per lane (a 64-bit op does two 32-bit lanes' work)
+  if (run<20>("v_lshlrev_b64")) return 1;
+  if (run<21>("v_lshrrev_b64")) return 1;
+  if (run<22>("v_lshl_add_u64")) return 1;
+  if (run<24>("v_pk_mov_b32")) return 1;
   return 0;
 }
