@@ -3011,9 +3011,7 @@ __global__ void __launch_bounds__(BS) k_f_prep(const uint32_t* sidx, uint64_t n,
   ulen[o] = up ? voff[s + 1] - voff[s] : 0;
 }
 constexpr uint32_t GATHER_BS = 1024;
-// The previous form (KHST_GATHER=nibble, measurement switch): one thread per (touched
-// record, child nibble), 16 threads a record whatever its mask.
-__global__ void __launch_bounds__(GATHER_BS) k_f_gather_nib(AMap M, Recs R, const uint32_t* touched, const uint8_t* replaced,
+__global__ void __launch_bounds__(GATHER_BS) k_f_gather(AMap M, Recs R, const uint32_t* touched, const uint8_t* replaced,
                                                  const uint32_t* tlist, const unsigned long long* ntl_p,
                                                  const uint32_t* tries, uint32_t nt, Elems E, unsigned long long* ctr) {
   // one thread per (touched record, child nibble v): the 16 child lookups of an opened
@@ -3053,85 +3051,6 @@ __global__ void __launch_bounds__(GATHER_BS) k_f_gather_nib(AMap M, Recs R, cons
   // every trie's untouched root record (a trie no op descended through) -- the same loop form
   for (uint64_t s0 = (uint64_t)blockIdx.x * GATHER_BS; s0 < nt; s0 += (uint64_t)gridDim.x * GATHER_BS) {
     const uint64_t s = s0 + threadIdx.x;
-    uint32_t r = NONE;
-    if (s < nt) {
-      const uint64_t zero[4] = {0, 0, 0, 0};
-      r = map_find(M, R, tries[s], 0, zero);
-      if (r != NONE && touched[r]) r = NONE;
-    }
-    const uint64_t e = block_claim(E.n, r != NONE, claim);
-    if (r != NONE) elem_fill(R, r, (uint32_t)s, E, e);
-  }
-}
-
-// One round per GATHER_CH touched records and block: a thread per record reads it (one
-// line) and lists its (record, child nibble) pairs in LDS -- a branch's set mask bits, a
-// leaf's one -- then the block's threads take the pairs, so a deep branch of 2-3 children
-// costs 2-3 lookups instead of 16 threads' worth of rounds: each round is a chain of
-// dependent HBM trips (record, map tag, map record, touched flag, element fill) ended by
-// the block-wide claim.  The trie list (a forest commit's segments) is searched in LDS.
-constexpr uint32_t GATHER_CH = 256;
-constexpr uint32_t GATHER_TRIES_LDS = 4096;
-__global__ void __launch_bounds__(GATHER_BS) k_f_gather(AMap M, Recs R, const uint32_t* touched, const uint8_t* replaced,
-                                                 const uint32_t* tlist, const unsigned long long* ntl_p,
-                                                 const uint32_t* tries, uint32_t nt, Elems E, unsigned long long* ctr) {
-  __shared__ unsigned long long claim[GATHER_BS / 64 + 1];
-  __shared__ uint32_t s_r[GATHER_CH], s_seg[GATHER_CH];
-  __shared__ uint8_t s_db[GATHER_CH];
-  __shared__ uint16_t s_pair[GATHER_CH * 16];  // record slot << 4 | child nibble
-  __shared__ uint32_t s_np;
-  __shared__ uint32_t s_tries[GATHER_TRIES_LDS];
-  const uint32_t tid = threadIdx.x;
-  const uint64_t ntl = *ntl_p;
-  const bool tries_lds = nt <= GATHER_TRIES_LDS;
-  if (tries_lds)
-    for (uint32_t i = tid; i < nt; i += GATHER_BS) s_tries[i] = tries[i];
-  for (uint64_t c0 = (uint64_t)blockIdx.x * GATHER_CH; c0 < ntl; c0 += (uint64_t)gridDim.x * GATHER_CH) {
-    if (tid == 0) s_np = 0;
-    __syncthreads();  // (also: s_tries loaded, the last round's pairs consumed)
-    if (tid < GATHER_CH && c0 + tid < ntl) {
-      const uint32_t r = tlist[c0 + tid];
-      uint32_t mask = 0;
-      if (R.rlive[r] == REC_LIVE) {
-        const uint32_t t = R.rt[r], db = R.rdb[r];
-        s_r[tid] = r;
-        s_db[tid] = (uint8_t)db;
-        s_seg[tid] = tries_lds ? seg_of(s_tries, nt, t) : seg_of(tries, nt, t);
-        mask = db == EL_LEAF ? 1u : (uint32_t)R.rmask[r];
-      }
-      if (mask) {
-        uint32_t o = atomicAdd(&s_np, (uint32_t)__popc(mask));
-        for (uint32_t mm = mask; mm; mm &= mm - 1) s_pair[o++] = (uint16_t)((tid << 4) | (uint32_t)__builtin_ctz(mm));
-      }
-    }
-    __syncthreads();
-    const uint32_t np = s_np;
-    for (uint32_t p0 = 0; p0 < np; p0 += GATHER_BS) {  // the same trip count in every thread (the claim)
-      const uint32_t p = p0 + tid;
-      bool want = false;
-      uint32_t er = NONE, seg = 0;
-      if (p < np) {
-        const uint32_t q = s_pair[p], slot = q >> 4, v = q & 15;
-        const uint32_t r = s_r[slot], db = s_db[slot];
-        seg = s_seg[slot];
-        if (db == EL_LEAF) {
-          want = !replaced[r];
-          er = r;
-        } else {
-          uint64_t ck[4] = {R.rk[4ull * r], R.rk[4ull * r + 1], R.rk[4ull * r + 2], R.rk[4ull * r + 3]};
-          set_nibble(ck, db, v);
-          er = map_find(M, R, R.rt[r], db + 1, ck);
-          if (er == NONE) ctr[2] = 4;
-          want = er != NONE && !touched[er];
-        }
-      }
-      const uint64_t e = block_claim(E.n, want, claim);  // every thread of the block reaches the claim
-      if (want) elem_fill(R, er, seg, E, e);
-    }
-  }
-  // every trie's untouched root record (a trie no op descended through) -- the same loop form
-  for (uint64_t s0 = (uint64_t)blockIdx.x * GATHER_BS; s0 < nt; s0 += (uint64_t)gridDim.x * GATHER_BS) {
-    const uint64_t s = s0 + tid;
     uint32_t r = NONE;
     if (s < nt) {
       const uint64_t zero[4] = {0, 0, 0, 0};
@@ -3728,10 +3647,8 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     if (redo)  // the upserts' elements again, into the grown buffer
       hipLaunchKernelGGL(k_f_upsert_elems, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)tries, nt,
                          (const uint32_t*)ur, (const uint64_t*)uo, E, hb, (uint64_t)nups);
-    static const bool gather_nib = getenv("KHST_GATHER") && !strcmp(getenv("KHST_GATHER"), "nibble");  // measurement switch
     const uint64_t gblocks = std::min<uint64_t>((uint64_t)c->n_cu * 2, (nd * 16 * 8 + GATHER_BS - 1) / GATHER_BS);
-    hipLaunchKernelGGL(gather_nib ? k_f_gather_nib : k_f_gather, dim3((unsigned)std::max<uint64_t>(gblocks, 1)),
-                       dim3(GATHER_BS), 0, st, map_of(h),
+    hipLaunchKernelGGL(k_f_gather, dim3((unsigned)std::max<uint64_t>(gblocks, 1)), dim3(GATHER_BS), 0, st, map_of(h),
                        recs_of(h), (const uint32_t*)h->touched.p, (const uint8_t*)h->replaced.p,
                        (const uint32_t*)tlist, (const unsigned long long*)fctr, (const uint32_t*)tries, nt, E, fctr);
     LAUNCH_CHECK();
