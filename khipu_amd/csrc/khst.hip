@@ -1566,6 +1566,9 @@ __global__ void __launch_bounds__(BS) k_hash_keys_owner_l(const uint8_t* keys, u
                                                           uint32_t* hist) {
   hash_keys_owner<false>(keys, klen, n, out, nparts, ntile, hist);
 }
+// V16: keys in and out 16-byte aligned -- each key moved as two 16-byte loads issued before
+// the round's ranking and two 16-byte stores (8-byte words otherwise)
+template <bool V16>
 __global__ void __launch_bounds__(BS) k_part_place(const uint64_t* K, const uint64_t* voff, uint64_t n,
                                                    uint32_t nparts, uint32_t ntile, const uint32_t* base,
                                                    uint64_t* okeys, uint64_t* olen, uint32_t* pos) {
@@ -1579,7 +1582,19 @@ __global__ void __launch_bounds__(BS) k_part_place(const uint64_t* K, const uint
     __syncthreads();
     const uint64_t i = t0 + r * BS + threadIdx.x;
     const bool ok = i < n;
-    const uint32_t o = ok ? nibble_owner(K[4 * i], nparts) : 0;
+    ulonglong2 k0 = make_ulonglong2(0, 0), k1 = make_ulonglong2(0, 0);
+    uint64_t len = 0;
+    if (ok) {
+      if (V16) {
+        k0 = ((const ulonglong2*)K)[2 * i];
+        k1 = ((const ulonglong2*)K)[2 * i + 1];
+      } else {
+        k0 = make_ulonglong2(K[4 * i], K[4 * i + 1]);
+        k1 = make_ulonglong2(K[4 * i + 2], K[4 * i + 3]);
+      }
+      len = voff[i + 1] - voff[i];
+    }
+    const uint32_t o = ok ? nibble_owner(k0.x, nparts) : 0;
     const uint64_t mask = owner_match(ok, o);
     const uint32_t rk = (uint32_t)__popcll(mask & lanemask_lt());
     if (ok && rk == 0) wc[wv][o] = (uint32_t)__popcll(mask);
@@ -1588,8 +1603,16 @@ __global__ void __launch_bounds__(BS) k_part_place(const uint64_t* K, const uint
       uint32_t d = run[o] + rk;
       for (uint32_t w = 0; w < wv; ++w) d += wc[w][o];
       pos[i] = d;
-      for (int q = 0; q < 4; ++q) okeys[4 * (uint64_t)d + q] = K[4 * i + q];
-      olen[d] = voff[i + 1] - voff[i];
+      if (V16) {
+        ((ulonglong2*)okeys)[2 * (uint64_t)d] = k0;
+        ((ulonglong2*)okeys)[2 * (uint64_t)d + 1] = k1;
+      } else {
+        okeys[4 * (uint64_t)d] = k0.x;
+        okeys[4 * (uint64_t)d + 1] = k0.y;
+        okeys[4 * (uint64_t)d + 2] = k1.x;
+        okeys[4 * (uint64_t)d + 3] = k1.y;
+      }
+      olen[d] = len;
     }
     __syncthreads();
     if (threadIdx.x < nparts) {
@@ -4229,8 +4252,12 @@ static void partition_impl(kh_ctx* c, void* vals_done, const uint8_t* d_addr, ui
       LAUNCH_CHECK();
     }
     scan_exclusive<uint32_t>(hist, hist, nh, (uint32_t*)nullptr, sc, st);
-    hipLaunchKernelGGL(k_part_place, dim3(ntile), dim3(BS), 0, st, K, d_voff, n, nparts, ntile,
-                       (const uint32_t*)hist, (uint64_t*)d_out_keys, d_out_vlen, pos);
+    if (!(((uintptr_t)K | (uintptr_t)d_out_keys) & 15))
+      hipLaunchKernelGGL(k_part_place<true>, dim3(ntile), dim3(BS), 0, st, K, d_voff, n, nparts, ntile,
+                         (const uint32_t*)hist, (uint64_t*)d_out_keys, d_out_vlen, pos);
+    else
+      hipLaunchKernelGGL(k_part_place<false>, dim3(ntile), dim3(BS), 0, st, K, d_voff, n, nparts, ntile,
+                         (const uint32_t*)hist, (uint64_t*)d_out_keys, d_out_vlen, pos);
     LAUNCH_CHECK();
     scan_exclusive<uint64_t>(d_out_vlen, ooff, n, (uint64_t*)(tot + 32), sc, st);
     auto vcopy = [&] {
