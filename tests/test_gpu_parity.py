@@ -299,6 +299,36 @@ def test_partition_vs_host(khst, nparts):
         assert np.array_equal(pv[:len(want)].cpu().numpy(), want)
 
 
+def test_partition_keys_8byte_aligned(khst):
+    """Keys at an 8-byte but not 16-byte aligned address take k_part_place's 8-byte word
+    moves (16-byte aligned keys and outputs take the 16-byte ones): same stable partition."""
+    import torch
+    from khipu_amd import sharded
+    rng = np.random.default_rng(7)
+    be = sharded.GpuBackend(0)
+    be.overlap = False
+    n, nparts = 50_001, 8
+    lens = rng.integers(0, 90, n).astype(np.int64)
+    vo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    v = rng.integers(0, 256, int(vo[-1]) + 64, dtype=np.uint8)
+    k = rng.integers(0, 256, n * 32 + 64, dtype=np.uint8)
+    kbuf = torch.zeros(n * 32 + 128, dtype=torch.uint8, device="cuda:0")
+    kd = kbuf[8:8 + n * 32 + 64]
+    kd.copy_(torch.from_numpy(k))
+    assert kd.data_ptr() % 16 == 8
+    vd, od = (torch.from_numpy(x).to("cuda:0") for x in (v, vo))
+    pk, pv, pl, cnt, nb = be.partition(kd, vd, od, n, nparts)
+    torch.cuda.synchronize()
+    kk = k[:n * 32].reshape(n, 32)
+    owner = ((kk[:, 0] >> 4).astype(np.int64) * nparts) >> 4
+    order = np.argsort(owner, kind="stable")
+    assert np.array_equal(cnt, np.bincount(owner, minlength=nparts)[:nparts])
+    assert np.array_equal(pk[:n * 32].cpu().numpy(), kk[order].reshape(-1))
+    assert np.array_equal(pl[:n].cpu().numpy(), lens[order])
+    want = np.concatenate([v[vo[i]:vo[i + 1]] for i in order])
+    assert np.array_equal(pv[:len(want)].cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("nparts", [2, 8, 16])
 def test_hash_partition_vs_host(khst, oracle, nparts):
     """kh_dev_hash_partition_ev (the keys kec256'd in the pass that counts the owners) ==
