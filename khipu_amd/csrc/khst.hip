@@ -2313,7 +2313,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     const char* l = getenv("KHST_LEAF");  // measurement switch: leaves hashed in sorted order
     if (l && strcmp(l, "sorted") == 0) return 2;
     const char* e = getenv("KHST_PD");  // measurement switch
-    return !e ? PD_DEFAULT : strcmp(e, "ansv") == 0 ? 1 : 0;
+    return !e ? PD_DEFAULT : strcmp(e, "ansv") == 0 ? 1 : strcmp(e, "first") == 0 ? 3 : 0;
   }();
   const int pd_mode = (early && nb > 0) ? pd_env : 0;
   if (pd_mode == 2) {  // sorted leaves: no scatter, the stash is written in sorted order
@@ -2389,6 +2389,12 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       HIPCHK(hipEventRecord(c->ev[10], c->st2));
     }
     static const uint32_t pd_chunks = getenv("KHST_PD_CHUNKS") ? (uint32_t)atoi(getenv("KHST_PD_CHUNKS")) : 1u;
+    if (pd_mode == 3) {  // KHST_PD=first: the scatter alone on st, then the leaves; the plain
+                         // ANSV runs beside them on st
+      hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, st, T);
+      LAUNCH_CHECK();
+      launch_leaves(false);
+    }
     if (pd_mode == 1 && pd_chunks <= 1)
       hipLaunchKernelGGL(k_ansv_pd, GRID(m, BS), dim3(BS), 0, st, T, P, nb);
     else
