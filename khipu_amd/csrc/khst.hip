@@ -1848,6 +1848,9 @@ struct SortIO {
   const uint8_t* kn;  // variable-length keys: nibble counts (input order; nullable)
   bool ck_ready = false;  // ck_path: ck0/idx0 already hold the 32-bit sort keys (k_hash_keys_ck)
   bool ck_path = false;   // unsegmented plain build: sort (32-bit prefix, idx) only, never gather the keys
+  // a device word copied to the host with the first sync's flags (c->h_pinned[1]): the
+  // caller's check of earlier stream work, read without a sync of its own (nullable)
+  const unsigned long long* chk = nullptr;
   // out
   uint8_t* u = nullptr;  // ck_path: boundary values, written for the tie runs' inner boundaries
   uint32_t depth0 = 0;
@@ -1859,6 +1862,7 @@ struct SortIO {
 };
 static void sort_dedup(kh_ctx* c, SortIO& S) {
   hipStream_t st = c->st;
+  if (S.chk && S.ck_path) throw KhError{KH_EINTERNAL, "sort: a check word on the prefix path"};
   const uint64_t n = S.n;
   const uint64_t* K32 = S.K32;
   const uint32_t* seg = S.seg;
@@ -1956,6 +1960,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
                        T.ctr + CTR_TIE);
     LAUNCH_CHECK();
     HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
+    if (S.chk) HIPCHK(hipMemcpyAsync(c->h_pinned + 1, S.chk, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     tie_flags = c->h_pinned[0];
   }
@@ -3506,6 +3511,11 @@ struct FCommit {  // one commit's inputs (device buffers)
   const uint8_t* del_keys = nullptr;
   uint64_t ndel = 0;
   uint32_t klen = 32;
+  // an error word of earlier stream work (kh_block_commit's injection) checked at the sort's
+  // sync, before the commit changes anything: equal to chk_tok -> KH_EINVAL chk_msg
+  const unsigned long long* chk = nullptr;
+  unsigned long long chk_tok = 0;
+  const char* chk_msg = nullptr;
 };
 
 static int emit_nodes_dev(kh_ctx* c, DevBuf& out, uint64_t* n_nodes, uint64_t* rlp_len);
@@ -3549,6 +3559,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   S.rs_scratch = cv.take<char>(radix_scratch_bytes(nops));
   S.scan_scratch = cv.take<char>(scan_scratch_bytes(nops + 1, 8));
   S.ctr = cv.take<unsigned long long>(CTR_N);
+  S.chk = F.chk;
   uint8_t* kind = cv.take<uint8_t>(nops);
   uint32_t* tflag = cv.take<uint32_t>(nops);
   uint32_t* tpos = cv.take<uint32_t>(nops);
@@ -3585,6 +3596,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                      segd ? F.del_trie : nullptr, K, Tid, S.ctr);
   LAUNCH_CHECK();
   sort_dedup(c, S);
+  if (F.chk && c->h_pinned[1] == F.chk_tok) throw KhError{KH_EINVAL, F.chk_msg};
   const uint64_t nd = S.m;
   uint32_t* otrie = segd ? S.sseg : sseg;  // the compaction of duplicates moves the sorted ids
   // the descent's touched list and the commit's flags (fctr, zeroed by k_f_prep): [0] touched
@@ -4834,6 +4846,7 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     S.klen = s_klen;
     forest_commit(storage, S, &sst);
     // 2. account.withStateRoot: the new storage roots into the account bodies
+    FCommit A;
     const uint32_t nt = (uint32_t)storage->tries.size();
     if (nt && na_up && d_a_up_trie) {
       // the forest's trie list and roots are still on the device (its commit's tbuf)
@@ -4847,12 +4860,12 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
       hipLaunchKernelGGL(k_inject_roots, GRID(na_up, BS), dim3(BS), 0, st, d_a_up_vals, d_a_up_voff, d_a_up_trie,
                          na_up, (const uint32_t*)storage->d_tries, nt, (const uint64_t*)storage->d_roots, err, tok);
       LAUNCH_CHECK();
-      HIPCHK(hipMemcpyAsync(c->h_pinned, err, 8, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      if (c->h_pinned[0] == tok) throw KhError{KH_EINVAL, "an account upsert with a storage trie is not an account body"};
+      // (read back with the account commit's first sync, before it changes anything)
+      A.chk = err;
+      A.chk_tok = tok;
+      A.chk_msg = "an account upsert with a storage trie is not an account body";
     }
     // 3. the accounts (TrieAccounts.flush, TrieAccounts.scala:22-28)
-    FCommit A;
     A.up_keys = d_a_up_keys;
     A.up_vals = d_a_up_vals;
     A.up_voff = d_a_up_voff;

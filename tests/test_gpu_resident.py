@@ -338,6 +338,54 @@ def test_host_handles_pair_on_the_shared_context(khst, oracle):
     lib().kh_trie_free(fo_h)
 
 
+def test_block_commit_refuses_non_account_body(khst, oracle):
+    """An account upsert naming a storage trie whose body is not an account (no stateRoot
+    field to write, Account.withStateRoot): kh_block_commit refuses the block with KH_EINVAL
+    (the injection's error word is read with the account commit's first sync), the state
+    trie unchanged -- the next block commits onto the old state as the oracle fold says."""
+    import ctypes
+    import random
+    import numpy as np
+    from khipu_amd import _lib
+    from khipu_amd._lib import check, lib
+    from khipu_amd.device import block_commit_host
+    from khipu_amd import codec
+    r = random.Random(22)
+    keys = [bytes(r.getrandbits(8) for _ in range(32)) for _ in range(200)]
+    vals = [codec.account_rlp(i, 10 ** 18 + i) for i in range(200)]
+    kb = np.frombuffer(b"".join(keys), np.uint8)
+    vb = np.frombuffer(b"".join(vals) + bytes(8), np.uint8)
+    vo = np.concatenate([[0], np.cumsum([len(v) for v in vals])]).astype(np.uint64)
+    root = np.zeros(32, np.uint8)
+    st_h, fo_h = ctypes.c_void_p(), ctypes.c_void_p()
+    check(lib().kh_trie_open_host(kb.ctypes.data, 32, vb.ctypes.data, vo.ctypes.data, 200, 0, root.ctypes.data,
+                                  ctypes.byref(st_h)))
+    check(lib().kh_forest_open(None, _lib.KH_HASH_KEYS, ctypes.byref(fo_h)))
+
+    class H:
+        def __init__(self, h):
+            self.h = h
+            self.ctx = type("C", (), {"_sync": staticmethod(lambda: None)})()
+    state, forest = H(st_h), H(fo_h)
+    sk = np.frombuffer(bytes(31) + b"\x02", np.uint8)
+    sv = np.frombuffer(b"\x07" + bytes(8), np.uint8)
+    so = np.array([0, 1], np.uint64)
+    ak = np.frombuffer(keys[0], np.uint8)
+    av = np.frombuffer(b"\x82\x01\x02" + bytes(8), np.uint8).copy()  # an RLP string, not an account
+    ao = np.array([0, 3], np.uint64)
+    at = np.array([0], np.uint32)
+    with pytest.raises(Exception, match="not an account body"):
+        block_commit_host(state, forest, np.array([0], np.uint32), sk, sv, so, None, None, ak, av, ao, at, None)
+    # the next block: a plain account update onto the unchanged state
+    body = codec.account_rlp(9, 99)
+    got = block_commit_host(state, forest, None, None, None, None, None, None, np.frombuffer(keys[1], np.uint8),
+                            np.frombuffer(body + bytes(8), np.uint8).copy(), np.array([0, len(body)], np.uint64),
+                            np.array([_lib.KH_NO_TRIE], np.uint32), None)
+    assert got == oracle.seq_root(keys, [vals[0], body] + vals[2:])
+    lib().kh_trie_free(st_h)
+    lib().kh_trie_free(fo_h)
+
+
 def test_update_of_empty_path_leaf_is_refused(khst, oracle):
     """A later block updating a key whose leaf hangs under a depth-63 branch (its remaining
     path is empty): khipu's putInLeafNode turns that leaf into a childless value-only branch
