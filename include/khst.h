@@ -317,6 +317,39 @@ int kh_block_commit_host(kh_trie* state, kh_trie* storage, const uint32_t* s_up_
                          const uint32_t* a_up_trie, uint64_t na_up, const uint8_t* a_del_keys, uint64_t na_del,
                          uint32_t a_klen, uint8_t state_root32[32], kh_stats* stats);
 
+/* ---- versioned commits ----
+ * Ledger.executeBlock flushes the parallel attempt's world state and, when its root does not
+ * validate, re-executes the block sequentially from the SAME parent state
+ * (khipu-eth/.../ledger/Ledger.scala:237-271); validateBlockAfterExecution rejects a block whose
+ * root or gas does not match (:603-620); TrieAccounts.rootHash flushes a COPY of the trie and
+ * leaves the trie itself untouched (khipu-eth/.../ledger/TrieAccounts.scala:73-80, called per
+ * transaction at Ledger.scala:576; MerklePatriciaTrie.copy, MerklePatriciaTrie.scala:556).
+ *
+ * kh_trie_savepoint opens a savepoint on a trie or forest (they nest; *depth = the number now
+ * open).  Commits after it are journaled: each saves the records it rewrites and logs the
+ * anchor-map slots it changes, O(changed nodes).  kh_trie_rollback returns the handle to the
+ * innermost savepoint's version -- root, records, value heap, the last commit's trie list and
+ * roots (kh_forest_last_roots) and write-back set (kh_trie_emit_nodes) -- and closes it;
+ * kh_trie_release keeps the commits and closes it.  kh_block_commit is all or nothing on both
+ * handles: a refusal or failure in either phase leaves both at the parent version. */
+int kh_trie_savepoint(kh_trie* h, uint32_t* depth);
+int kh_trie_rollback(kh_trie* h);
+int kh_trie_release(kh_trie* h);
+int kh_trie_savepoint_depth(const kh_trie* h, uint32_t* depth);
+
+/* TrieAccounts.rootHash (TrieAccounts.scala:73-80): the root that kh_trie_apply of this batch
+ * would give, the handle left unchanged (a commit between a savepoint and its rollback). */
+int kh_trie_root_of(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals, const uint64_t* d_up_voff,
+                    uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
+                    uint8_t root32[32], kh_stats* stats);
+int kh_trie_root_of_host(kh_trie* h, const uint8_t* up_keys, const uint8_t* up_vals, const uint64_t* up_voff,
+                         uint64_t nup, const uint8_t* del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
+                         uint8_t root32[32], kh_stats* stats);
+
+/* MerklePatriciaTrie.copy (MerklePatriciaTrie.scala:556): an independent handle holding the
+ * current version of h in HBM (no savepoints); free it with kh_trie_free. */
+int kh_trie_copy(kh_trie* h, kh_trie** out);
+
 /* Storage write-back hand-off of the LAST commit (open or apply) of a
  * trie opened with KH_EMIT_NODES: exactly the nodes that commit created -- every node
  * reachable from a new root whose encoding is >= 32 B and that the previous version did

@@ -31,7 +31,8 @@ EXPORTS = (
     "kh_forest_apply_host", "kh_block_commit", "kh_forest_last_roots", "kh_trie_open_nodes",
     "kh_trie_open_nodes_host", "kh_trie_roots_varkeys", "kh_list_roots",
     "kh_trie_root_sharded", "kh_block_commit_host", "kh_dev_list_roots", "kh_trie_get", "kh_trie_get_host",
-    "kh_dev_synth_storage", "kh_trie_roots_segmented_sharded",
+    "kh_dev_synth_storage", "kh_trie_roots_segmented_sharded", "kh_trie_savepoint", "kh_trie_rollback",
+    "kh_trie_release", "kh_trie_savepoint_depth", "kh_trie_root_of", "kh_trie_root_of_host", "kh_trie_copy",
 )
 
 
@@ -133,6 +134,13 @@ def lib():
     L.kh_dev_synth_storage.argtypes = [vp, u32, u64, u64, vp, ctypes.POINTER(u64), ctypes.POINTER(u64), vp, vp, vp, vp]
     L.kh_trie_roots_segmented_sharded.argtypes = [vp, i32, vp, u32, vp, vp, vp, u64, u32, vp, vp]
     L.kh_trie_get_host.argtypes = [vp, vp, vp, u32, u64, vp, u64, vp, vp, ctypes.POINTER(u64)]
+    L.kh_trie_savepoint.argtypes = [vp, ctypes.POINTER(u32)]
+    L.kh_trie_rollback.argtypes = [vp]
+    L.kh_trie_release.argtypes = [vp]
+    L.kh_trie_savepoint_depth.argtypes = [vp, ctypes.POINTER(u32)]
+    L.kh_trie_root_of.argtypes = L.kh_trie_apply.argtypes
+    L.kh_trie_root_of_host.argtypes = L.kh_trie_apply_host.argtypes
+    L.kh_trie_copy.argtypes = [vp, ctypes.POINTER(vp)]
     for name in EXPORTS:
         fn = getattr(L, name)
         if fn.restype is ctypes.c_int or name not in ("kh_last_error", "kh_version"):

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -3192,14 +3193,23 @@ __global__ void __launch_bounds__(BS) k_f_elem_recs(Topo T, Elems E, const uint3
 // map maintenance: delete records' current anchors (two lists in one launch: the touched
 // records, then the element sources), mark dead, insert
 // (the first list's records -- the touched ones -- also die here: marked dead, flags cleared)
+// (mlog, when journaling: entry i = (slot, its old tag, its old record) of the slot this thread
+// changed, slot ~0 for none)
 __global__ void __launch_bounds__(BS) k_map_delete(AMap M, Recs R, const uint32_t* list, uint64_t n,
                                                    const uint32_t* list2, uint64_t n2, uint32_t* touched,
-                                                   uint8_t* replaced) {
+                                                   uint8_t* replaced, uint64_t* mlog) {
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n + n2) return;
   const uint32_t r = i < n ? list[i] : list2[i - n];
+  const uint64_t sl = r == NONE ? ~0ULL : map_slot_of(M, R, r);
+  if (mlog) {
+    mlog[3 * i] = sl;
+    if (sl != ~0ULL) {
+      mlog[3 * i + 1] = M.tag[sl];
+      mlog[3 * i + 2] = r;
+    }
+  }
   if (r == NONE) return;
-  const uint64_t sl = map_slot_of(M, R, r);
   if (sl != ~0ULL) M.tag[sl] = 1;  // tombstone
   if (i < n) {
     R.rlive[r] = REC_DEAD;
@@ -3220,28 +3230,70 @@ __global__ void __launch_bounds__(BS) k_f_untouch(const uint32_t* list, uint64_t
 // (list entries NONE are skipped; used, when given, counts the inserts that took an empty
 // slot: the table's load, live + tombstones)
 __global__ void __launch_bounds__(BS) k_map_insert(AMap M, Recs R, uint64_t base, uint64_t nb, const uint32_t* list,
-                                                   uint64_t n, unsigned long long* err, unsigned long long* used) {
+                                                   uint64_t n, unsigned long long* err, unsigned long long* used,
+                                                   uint64_t* mlog) {
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   bool fresh = false;
   if (i < nb + n) {
     const uint32_t r = i < nb ? (uint32_t)(base + i) : list[i - nb];
+    uint64_t ls = ~0ULL, lt = 0, lr = 0;  // the slot taken, its old tag and record (journal)
     if (r != NONE && R.rlive[r] == REC_LIVE) {
       const unsigned long long h = anchor_tag(R.rt[r], R.rd[r], R.key(r));
       bool done = false;
       for (uint64_t s = h & M.mask, k = 0; k <= M.mask; s = (s + 1) & M.mask, ++k) {
         unsigned long long g = M.tag[s];
         if (g > 1) continue;
+        const uint32_t orec = M.rec[s];  // an empty / tombstone slot's record changes only with its tag
         if (atomicCAS(&M.tag[s], g, h) == g) {
           M.rec[s] = r;
           fresh = g == 0;
           done = true;
+          ls = s;
+          lt = g;
+          lr = orec;
           break;
         }
       }
       if (!done) *err = 5;  // full table
     }
+    if (mlog) {
+      mlog[3 * i] = ls;
+      mlog[3 * i + 1] = lt;
+      mlog[3 * i + 2] = lr;
+    }
   }
   if (used) wave_atomic_add(used, fresh ? 1ULL : 0ULL);
+}
+// journal (versioned commits): the records a commit rewrites in place -- the touched records
+// (they die) and the element sources (re-anchored) -- saved whole before the first change, and
+// restored by a rollback; 8 lanes per record, one 16-byte word each
+__global__ void __launch_bounds__(BS) k_rec_save(const uint8_t* recs, const uint32_t* l1, uint64_t n1, const uint32_t* l2,
+                                                 uint64_t n2, uint32_t* jidx, uint8_t* jrec) {
+  const uint64_t g = (uint64_t)blockIdx.x * BS + threadIdx.x, i = g >> 3;
+  const uint32_t w = (uint32_t)(g & 7);
+  if (i >= n1 + n2) return;
+  const uint32_t r = i < n1 ? l1[i] : l2[i - n1];
+  if (w == 0) jidx[i] = r;
+  if (r == NONE) return;
+  ((ulonglong2*)(jrec + i * REC_BYTES))[w] = ((const ulonglong2*)(recs + (uint64_t)r * REC_BYTES))[w];
+}
+__global__ void __launch_bounds__(BS) k_rec_restore(uint8_t* recs, const uint32_t* jidx, const uint8_t* jrec,
+                                                    uint64_t n) {
+  const uint64_t g = (uint64_t)blockIdx.x * BS + threadIdx.x, i = g >> 3;
+  if (i >= n) return;
+  const uint32_t r = jidx[i];
+  if (r == NONE) return;
+  ((ulonglong2*)(recs + (uint64_t)r * REC_BYTES))[g & 7] = ((const ulonglong2*)(jrec + i * REC_BYTES))[g & 7];
+}
+// undo one map log (the slots of one launch are distinct: a delete tombstones its record's own
+// slot, an insert owns the slot its CAS won)
+__global__ void __launch_bounds__(BS) k_map_undo(AMap M, const uint64_t* mlog, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t s = mlog[3 * i];
+  if (s == ~0ULL) return;
+  M.tag[s] = mlog[3 * i + 1];
+  M.rec[s] = (uint32_t)mlog[3 * i + 2];
 }
 // per touched trie: its new root (segment result), EMPTY when no element remained
 // (block 0 also leaves the commit's final flags in tail: the element build's counters summed
@@ -3286,6 +3338,36 @@ __global__ void __launch_bounds__(BS) k_inject_roots(uint8_t* vals, const uint64
   for (int q = 0; q < 32; ++q) vals[e - 65 + q] = rb[q];
 }
 
+// ---- versioned commits (Ledger.executeBlock flushes a parallel attempt and, when
+// its root does not validate, re-executes sequentially from the SAME parent state,
+// Ledger.scala:237-271; validateBlockAfterExecution rejects a block, :603-620; TrieAccounts.rootHash
+// flushes a COPY, TrieAccounts.scala:73-80).  A savepoint opens an undo journal: every commit
+// after it saves the records it rewrites in place and logs the anchor-map slots it changes, so a
+// rollback restores the version of the savepoint in O(changed records), not O(resident trie).
+// New records, heap bytes and node ids are appended past the savepoint's ends and simply cut off.
+struct JSeg {  // one journaled commit: its saved records and map-slot log ranges (entries)
+  uint64_t rpos = 0, rn = 0;  // saved records [rpos, rpos + rn) of jidx / jrec
+  uint64_t dpos = 0, dn = 0;  // map log: the deletes (tombstones) ...
+  uint64_t ipos = 0, in = 0;  // ... and the inserts, 3 words per entry (slot, old tag, old record)
+};
+struct Savepoint {
+  uint64_t rn = 0, heap_n = 0, nleaves = 0, mused = 0, rdead = 0, map_epoch = 0;
+  uint8_t root[32] = {};
+  std::vector<uint32_t> tries;  // the last commit's touched tries and roots (kh_forest_last_roots)
+  std::vector<uint8_t> roots;
+  size_t seg0 = 0;              // journal fill at the savepoint
+  uint64_t jrec0 = 0, jmap0 = 0;
+  bool em_saved = false;        // the write-back set of the savepoint's version, kept when a later
+  bool em_valid = false;        // commit replaced it (kh_trie_emit_nodes after a rollback)
+  DevBuf em;
+  uint64_t em_n = 0, em_bytes = 0;
+};
+static void swap_buf(DevBuf& a, DevBuf& b) {
+  std::swap(a.p, b.p);
+  std::swap(a.cap, b.cap);
+  std::swap(a.dev, b.dev);
+}
+
 struct kh_trie {
   kh_ctx* c = nullptr;
   uint32_t flags = 0;  // KH_HASH_KEYS: the trie's key encoder; KH_EMIT_NODES: keep each commit's write-back set
@@ -3308,6 +3390,15 @@ struct kh_trie {
   std::vector<uint8_t> roots;
   uint32_t* d_tries = nullptr;  // ... the same on the device (in tbuf; the block commit's injection reads them)
   uint64_t* d_roots = nullptr;
+  // versioned commits: open savepoints (innermost last) and the journal of the commits since the
+  // outermost one
+  std::vector<std::unique_ptr<Savepoint>> sps;
+  std::vector<JSeg> jsegs;
+  DevBuf jidx, jrec, jmap;  // saved record ids (u32), saved records (128 B), map-slot log (3 u64)
+  uint64_t jrec_n = 0, jmap_n = 0;
+  uint64_t map_epoch = 0;   // anchor-map rebuilds so far (a rebuild voids the slot log)
+  bool flags_dirty = false; // a descent marked records and its commit did not finish
+  DevBuf em_spare;          // the write-back buffer a savepoint's saved set rotates with
 };
 
 static Recs recs_of(kh_trie* h) {
@@ -3354,13 +3445,14 @@ static void map_rebuild(kh_trie* h, uint64_t headroom) {
   while (cap < 2 * (h->rn + headroom) + 1024) cap <<= 1;
   h->mslots.ensure(cap * 16);
   h->mcap = cap;
+  ++h->map_epoch;  // the journal's slot log no longer applies: a rollback rebuilds the map
   HIPCHK(hipMemsetAsync(h->mslots.p, 0, cap * 16, st));
   h->merr.ensure(64);
   unsigned long long* err = (unsigned long long*)h->merr.p;
   HIPCHK(hipMemsetAsync(err, 0, 16, st));
   if (h->rn) {
     hipLaunchKernelGGL(k_map_insert, GRID(h->rn, BS), dim3(BS), 0, st, map_of(h), recs_of(h), (uint64_t)0, h->rn,
-                       (const uint32_t*)nullptr, (uint64_t)0, err, (unsigned long long*)nullptr);
+                       (const uint32_t*)nullptr, (uint64_t)0, err, (unsigned long long*)nullptr, (uint64_t*)nullptr);
     hipLaunchKernelGGL(k_rec_count_live, GRID(h->rn, BS), dim3(BS), 0, st, recs_of(h), h->rn, err + 1);
   }
   LAUNCH_CHECK();
@@ -3520,17 +3612,49 @@ struct FCommit {  // one commit's inputs (device buffers)
 
 static int emit_nodes_dev(kh_ctx* c, DevBuf& out, uint64_t* n_nodes, uint64_t* rlp_len);
 
+// a commit is about to replace the write-back set: the innermost savepoint keeps the set of its
+// version (once), and the commit writes into the spare buffer
+static void em_save(kh_trie* h) {
+  if (h->sps.empty()) return;
+  Savepoint& sp = *h->sps.back();
+  if (sp.em_saved) return;
+  sp.em_saved = true;
+  sp.em_valid = h->em_valid;
+  sp.em_n = h->em_n;
+  sp.em_bytes = h->em_bytes;
+  swap_buf(sp.em, h->em);
+  swap_buf(h->em, h->em_spare);
+}
+// journal room for one more commit: nrec saved records, nmap map-log entries
+static JSeg journal_reserve(kh_trie* h, uint64_t nrec, uint64_t nmap) {
+  hipStream_t st = h->c->st;
+  JSeg s;
+  s.rpos = h->jrec_n;
+  s.rn = nrec;
+  const uint64_t rneed = h->jrec_n + nrec + 16, mneed = h->jmap_n + nmap + 16;
+  regrow(h->jidx, h->jrec_n * 4, (rneed + rneed / 2) * 4, st);
+  regrow(h->jrec, h->jrec_n * REC_BYTES, (rneed + rneed / 2) * REC_BYTES, st);
+  regrow(h->jmap, h->jmap_n * 24, (mneed + mneed / 2) * 24, st);
+  return s;
+}
+
 // One commit of a block's ops into the forest: upserts then deletes, the last op on a
-// key winning; deleting an absent key is a no-op.  Fills h->tries / h->roots.
+// key winning; deleting an absent key is a no-op.  Fills h->tries / h->roots.  A refused
+// batch (KH_EINVAL) leaves the handle as it was, its last roots and write-back set included;
+// with a savepoint open (h->sps) every change is journaled for kh_trie_rollback.
 static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   kh_ctx* c = h->c;
   hipStream_t st = c->st;
   if (stats) memset(stats, 0, sizeof(*stats));
-  h->tries.clear();
-  h->roots.clear();
-  h->em_valid = false;
+  const bool journal = !h->sps.empty();
   const uint64_t nops = F.nup + F.ndel;
-  if (nops == 0) return;
+  if (nops == 0) {
+    em_save(h);
+    h->tries.clear();
+    h->roots.clear();
+    h->em_valid = false;
+    return;
+  }
   if (nops >= (1ULL << 30)) throw KhError{KH_EINVAL, "batch too large"};
   if (!(h->flags & KH_HASH_KEYS) && F.klen != 32) throw KhError{KH_EINVAL, "keys must be 32 bytes unless KH_HASH_KEYS"};
   if (F.klen == 0 || F.klen > 4096) throw KhError{KH_EINVAL, "bad key length"};
@@ -3680,6 +3804,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   // ---- 2. descent: opened branches and touched leaves
   recs_reserve(h, h->rn + 16);
   if (h->mcap == 0) map_rebuild(h, nops + 1024);
+  h->flags_dirty = true;  // until the touched records die (k_map_delete) or are untouched
   hipLaunchKernelGGL(k_f_descend, GRID(nd, BS), dim3(BS), 0, st, O, map_of(h), recs_of(h), (uint32_t*)h->touched.p,
                      (uint8_t*)h->replaced.p, tlist, fctr);
   LAUNCH_CHECK();
@@ -3706,6 +3831,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
       LAUNCH_CHECK();
       HIPCHK(hipStreamSynchronize(st));
     }
+    h->flags_dirty = false;
     throw KhError{KH_EINVAL,
                   "put of a key whose leaf has an empty remaining path (63 nibbles shared with another key): khipu "
                   "turns that leaf into a value-only branch (MerklePatriciaTrie.scala:187-199), which this engine "
@@ -3751,6 +3877,29 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   bool count_fresh = false;  // fctr[4] holds this commit's fresh map slots
   uint32_t *isnew = nullptr, *nrank = nullptr, *eid = nullptr, *esrc = nullptr;
   uint8_t* sel = nullptr;
+  // journal (a savepoint is open): the records rewritten in place -- the touched ones and the
+  // element sources -- saved before the first change; the map deletes' and inserts' slot logs.
+  // The segment is listed before the first change, so a failure past it still rolls back.
+  uint64_t *dlog = nullptr, *ilog = nullptr;
+  auto journal_begin = [&](uint64_t ndel_log, uint64_t nins_log) {
+    if (!journal) return;
+    JSeg js = journal_reserve(h, ntl + m, ndel_log + nins_log);
+    js.dpos = h->jmap_n;
+    js.dn = ndel_log;
+    js.ipos = js.dpos + ndel_log;
+    js.in = 0;  // set once the inserts are launched
+    const uint64_t nsave = ntl + m;
+    if (nsave)
+      hipLaunchKernelGGL(k_rec_save, GRID(nsave * 8, BS), dim3(BS), 0, st, (const uint8_t*)h->recs.p,
+                         (const uint32_t*)tlist, ntl, (const uint32_t*)E.src, m, (uint32_t*)h->jidx.p + js.rpos,
+                         (uint8_t*)h->jrec.p + js.rpos * REC_BYTES);
+    LAUNCH_CHECK();
+    dlog = (uint64_t*)h->jmap.p + 3 * js.dpos;
+    ilog = (uint64_t*)h->jmap.p + 3 * js.ipos;
+    h->jsegs.push_back(js);
+    h->jrec_n += nsave;
+    h->jmap_n += ndel_log + nins_log;
+  };
   if (ne) {
     h->selb.ensure(carve_size({m + 2 * B, m * 4, m * 4, m * 4, m * 4, m, scan_scratch_bytes(m + 1, 4), 64}));
     Carver cs{(char*)h->selb.p, 0, h->selb.cap};
@@ -3771,10 +3920,12 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                        esrc, rein);
     LAUNCH_CHECK();
     scan_exclusive<uint32_t>(isnew, nrank, m, tot, sscr, st);
+    journal_begin(ntl + m, B + m);
     // old anchors out of the map (touched records, element sources), then touched records die
     hipLaunchKernelGGL(k_map_delete, GRID(ntl + m, BS), dim3(BS), 0, st, M, R, (const uint32_t*)tlist, ntl,
-                       (const uint32_t*)esrc, m, (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p);
+                       (const uint32_t*)esrc, m, (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p, dlog);
     LAUNCH_CHECK();
+    h->flags_dirty = false;
     hipLaunchKernelGGL(k_f_elem_recs, GRID(m, BS), dim3(BS), 0, st, T, E, (const uint32_t*)tries,
                        (const uint32_t*)nrank, (const uint8_t*)rein, R, base_e, eid);
     LAUNCH_CHECK();
@@ -3786,8 +3937,9 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
       // (the table's load grows by the inserts that took an empty slot: fctr[4], read at the
       // final sync; B + m bounds it for the rebuild test above)
       hipLaunchKernelGGL(k_map_insert, GRID(B + m, BS), dim3(BS), 0, st, M, R, base_b, B, (const uint32_t*)eid, m,
-                         fctr + 3, fctr + 4);
+                         fctr + 3, fctr + 4, ilog);
       LAUNCH_CHECK();
+      if (ilog) h->jsegs.back().in = B + m;
       count_fresh = true;
     }
     hipLaunchKernelGGL(k_f_roots, GRID(nt, BS), dim3(BS), 0, st, (const uint64_t*)T.res_hash,
@@ -3795,9 +3947,12 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                        (const unsigned long long*)fctr, tail);
     LAUNCH_CHECK();
   } else {
+    journal_begin(ntl, 0);
     if (ntl)
       hipLaunchKernelGGL(k_map_delete, GRID(ntl, BS), dim3(BS), 0, st, M, R, (const uint32_t*)tlist, ntl,
-                         (const uint32_t*)nullptr, (uint64_t)0, (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p);
+                         (const uint32_t*)nullptr, (uint64_t)0, (uint32_t*)h->touched.p, (uint8_t*)h->replaced.p,
+                         dlog);
+    h->flags_dirty = false;
     hipLaunchKernelGGL(k_f_roots, GRID(nt, BS), dim3(BS), 0, st, (const uint64_t*)nullptr, (const uint32_t*)nullptr,
                        nt, roots, (const unsigned long long*)nullptr, (const unsigned long long*)fctr, tail);
     LAUNCH_CHECK();
@@ -3805,6 +3960,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   h->rn = base_e + nnew;
   h->nleaves = h->nleaves + nups - nrep;
   // ---- 6. this commit's write-back set (kept on the device for kh_trie_emit_nodes)
+  em_save(h);
   if (keep_em && ne) {
     c->T.emit_sel = sel;
     uint64_t en = 0, eb2 = 0;
@@ -3843,6 +3999,172 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     stats->t_sort_ms = merge_ms;  // batch sort + descent + element gather
     stats->t_total_ms += merge_ms;
   }
+}
+
+// ---- versioned commits: savepoint / rollback / release (see Savepoint)
+static void trie_savepoint(kh_trie* h) {
+  auto sp = std::make_unique<Savepoint>();
+  sp->rn = h->rn;
+  sp->heap_n = h->heap_n;
+  sp->nleaves = h->nleaves;
+  sp->mused = h->mused;
+  sp->rdead = h->rdead;
+  sp->map_epoch = h->map_epoch;
+  memcpy(sp->root, h->root, 32);
+  sp->tries = h->tries;
+  sp->roots = h->roots;
+  sp->seg0 = h->jsegs.size();
+  sp->jrec0 = h->jrec_n;
+  sp->jmap0 = h->jmap_n;
+  h->sps.push_back(std::move(sp));
+}
+// back to the innermost savepoint's version: the journaled commits undone newest first (map
+// inserts, map deletes, then the records they rewrote), the appended records cut off (and
+// cleared), the host-side fields restored; the anchor map is rebuilt instead when it was
+// rebuilt (resized) after the savepoint
+static void trie_rollback(kh_trie* h) {
+  if (h->sps.empty()) throw KhError{KH_EINVAL, "no open savepoint"};
+  hipStream_t st = h->c->st;
+  Savepoint& sp = *h->sps.back();
+  const bool remap = h->map_epoch != sp.map_epoch;
+  if (h->flags_dirty) {  // a commit failed between its descent and its map update
+    if (h->rn) {
+      HIPCHK(hipMemsetAsync(h->touched.p, 0, h->rn * 4, st));
+      HIPCHK(hipMemsetAsync(h->replaced.p, 0, h->rn, st));
+    }
+    h->flags_dirty = false;
+  }
+  const AMap M = map_of(h);
+  for (size_t k = h->jsegs.size(); k-- > sp.seg0;) {
+    const JSeg& s = h->jsegs[k];
+    const uint64_t* jm = (const uint64_t*)h->jmap.p;
+    if (!remap && s.in) hipLaunchKernelGGL(k_map_undo, GRID(s.in, BS), dim3(BS), 0, st, M, jm + 3 * s.ipos, s.in);
+    if (!remap && s.dn) hipLaunchKernelGGL(k_map_undo, GRID(s.dn, BS), dim3(BS), 0, st, M, jm + 3 * s.dpos, s.dn);
+    if (s.rn)
+      hipLaunchKernelGGL(k_rec_restore, GRID(s.rn * 8, BS), dim3(BS), 0, st, (uint8_t*)h->recs.p,
+                         (const uint32_t*)h->jidx.p + s.rpos, (const uint8_t*)h->jrec.p + s.rpos * REC_BYTES, s.rn);
+    LAUNCH_CHECK();
+  }
+  if (h->rn > sp.rn)
+    HIPCHK(hipMemsetAsync((uint8_t*)h->recs.p + sp.rn * REC_BYTES, 0, (h->rn - sp.rn) * REC_BYTES, st));
+  h->rn = sp.rn;
+  h->heap_n = sp.heap_n;
+  h->nleaves = sp.nleaves;
+  h->mused = sp.mused;
+  h->rdead = sp.rdead;
+  memcpy(h->root, sp.root, 32);
+  h->tries = sp.tries;
+  h->roots = sp.roots;
+  h->d_tries = nullptr;
+  h->d_roots = nullptr;
+  h->jsegs.resize(sp.seg0);
+  h->jrec_n = sp.jrec0;
+  h->jmap_n = sp.jmap0;
+  if (sp.em_saved) {
+    swap_buf(h->em_spare, h->em);
+    swap_buf(h->em, sp.em);
+    h->em_valid = sp.em_valid;
+    h->em_n = sp.em_n;
+    h->em_bytes = sp.em_bytes;
+  }
+  h->sps.pop_back();
+  if (remap) map_rebuild(h, 1024);  // (syncs)
+  HIPCHK(hipStreamSynchronize(st));
+}
+// keep the commits since the innermost savepoint: it is dropped (its saved write-back set
+// passes to the enclosing savepoint when that one has none); the journal is emptied when the
+// last savepoint goes
+static void trie_release(kh_trie* h) {
+  if (h->sps.empty()) throw KhError{KH_EINVAL, "no open savepoint"};
+  std::unique_ptr<Savepoint> sp = std::move(h->sps.back());
+  h->sps.pop_back();
+  if (!h->sps.empty()) {
+    Savepoint& outer = *h->sps.back();
+    if (sp->em_saved && !outer.em_saved) {
+      outer.em_saved = true;
+      outer.em_valid = sp->em_valid;
+      outer.em_n = sp->em_n;
+      outer.em_bytes = sp->em_bytes;
+      swap_buf(outer.em, sp->em);
+    }
+  } else {
+    h->jsegs.clear();
+    h->jrec_n = h->jmap_n = 0;
+  }
+  if (sp->em.p && !h->em_spare.p) swap_buf(h->em_spare, sp->em);
+}
+// an all-or-nothing section over one or two handles (kh_block_commit, kh_trie_root_of): a
+// savepoint on each; rolled back unless released
+struct Txn {
+  kh_trie* h[2] = {nullptr, nullptr};
+  bool open = false;
+  Txn(kh_trie* a, kh_trie* b) {
+    trie_savepoint(a);
+    h[0] = a;
+    if (b) {
+      try {
+        trie_savepoint(b);
+      } catch (...) {
+        h[0]->sps.pop_back();
+        throw;
+      }
+      h[1] = b;
+    }
+    open = true;
+  }
+  void release() {
+    for (int i = 1; i >= 0; --i)
+      if (h[i]) trie_release(h[i]);
+    open = false;
+  }
+  void rollback() {
+    for (int i = 1; i >= 0; --i)
+      if (h[i]) trie_rollback(h[i]);
+    open = false;
+  }
+  ~Txn() {
+    if (!open) return;
+    try {
+      rollback();
+    } catch (...) {  // a failed rollback leaves the handle as the failure left it (KH_EDEVICE)
+    }
+  }
+};
+// MerklePatriciaTrie.copy (MerklePatriciaTrie.scala:556): an independent handle holding the
+// current version (records, anchor map, value heap, last roots and write-back set) in HBM
+static kh_trie* trie_copy(kh_trie* h) {
+  std::unique_ptr<kh_trie> n(new kh_trie());
+  n->c = h->c;
+  n->flags = h->flags;
+  n->forest = h->forest;
+  hipStream_t st = h->c->st;
+  recs_reserve(n.get(), h->rn + 16);
+  if (h->rn) HIPCHK(hipMemcpyAsync(n->recs.p, h->recs.p, h->rn * REC_BYTES, hipMemcpyDeviceToDevice, st));
+  n->rn = h->rn;
+  n->rdead = h->rdead;
+  if (h->mcap) {
+    n->mslots.ensure(h->mcap * 16);
+    HIPCHK(hipMemcpyAsync(n->mslots.p, h->mslots.p, h->mcap * 16, hipMemcpyDeviceToDevice, st));
+    n->mcap = h->mcap;
+    n->mused = h->mused;
+  }
+  n->heap.ensure(h->heap_n + 64);
+  if (h->heap_n) HIPCHK(hipMemcpyAsync(n->heap.p, h->heap.p, h->heap_n, hipMemcpyDeviceToDevice, st));
+  n->heap_n = h->heap_n;
+  n->nleaves = h->nleaves;
+  memcpy(n->root, h->root, 32);
+  n->tries = h->tries;
+  n->roots = h->roots;
+  n->ntl_hint = h->ntl_hint;
+  if (h->em_valid && h->em.p) {
+    n->em.ensure(h->em.cap);
+    HIPCHK(hipMemcpyAsync(n->em.p, h->em.p, h->em.cap, hipMemcpyDeviceToDevice, st));
+  }
+  n->em_valid = h->em_valid;
+  n->em_n = h->em_n;
+  n->em_bytes = h->em_bytes;
+  HIPCHK(hipStreamSynchronize(st));
+  return n.release();
 }
 
 // ---------------------------------------------------------------------------
@@ -4820,6 +5142,77 @@ int kh_forest_last_roots(kh_trie* f, uint32_t* h_tries, uint8_t* h_roots32, uint
   API_TRY({ return forest_out(f, h_tries, h_roots32, cap, n_tries); })
 }
 
+int kh_trie_savepoint(kh_trie* h, uint32_t* depth) {
+  if (!h) return set_err(KH_EINVAL, "null handle");
+  API_TRY({
+    trie_savepoint(h);
+    if (depth) *depth = (uint32_t)h->sps.size();
+  })
+}
+int kh_trie_rollback(kh_trie* h) {
+  if (!h) return set_err(KH_EINVAL, "null handle");
+  API_TRY({
+    std::lock_guard<std::mutex> g(h->c->mu);
+    HIPCHK(hipSetDevice(h->c->dev));
+    trie_rollback(h);
+  })
+}
+int kh_trie_release(kh_trie* h) {
+  if (!h) return set_err(KH_EINVAL, "null handle");
+  API_TRY({ trie_release(h); })
+}
+int kh_trie_savepoint_depth(const kh_trie* h, uint32_t* depth) {
+  if (!h || !depth) return set_err(KH_EINVAL, "null handle or output");
+  *depth = (uint32_t)h->sps.size();
+  return KH_OK;
+}
+
+int kh_trie_root_of(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals, const uint64_t* d_up_voff,
+                    uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
+                    uint8_t root32[32], kh_stats* stats) {
+  if (!h || h->forest) return set_err(KH_EINVAL, "null handle or a forest");
+  API_TRY({
+    HIPCHK(hipSetDevice(h->c->dev));
+    check_flags(h, flags);
+    FCommit F;
+    F.up_keys = d_up_keys;
+    F.up_vals = d_up_vals;
+    F.up_voff = d_up_voff;
+    F.nup = nup;
+    F.del_keys = d_del_keys;
+    F.ndel = ndel;
+    F.klen = klen;
+    Txn txn(h, nullptr);
+    forest_commit(h, F, stats);
+    if (root32) memcpy(root32, h->root, 32);
+    txn.rollback();
+  })
+}
+int kh_trie_root_of_host(kh_trie* h, const uint8_t* up_keys, const uint8_t* up_vals, const uint64_t* up_voff,
+                         uint64_t nup, const uint8_t* del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
+                         uint8_t root32[32], kh_stats* stats) {
+  if (!h || h->forest) return set_err(KH_EINVAL, "null handle or a forest");
+  API_TRY({
+    std::lock_guard<std::mutex> g(h->c->mu);
+    HIPCHK(hipSetDevice(h->c->dev));
+    check_flags(h, flags);
+    FCommit F = stage_commit(h->c, nullptr, up_keys, up_vals, up_voff, nup, nullptr, del_keys, ndel, klen);
+    Txn txn(h, nullptr);
+    forest_commit(h, F, stats);
+    if (root32) memcpy(root32, h->root, 32);
+    txn.rollback();
+  })
+}
+
+int kh_trie_copy(kh_trie* h, kh_trie** out) {
+  if (!h || !out) return set_err(KH_EINVAL, "null handle");
+  API_TRY({
+    std::lock_guard<std::mutex> g(h->c->mu);
+    HIPCHK(hipSetDevice(h->c->dev));
+    *out = trie_copy(h);
+  })
+}
+
 int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_trie, const uint8_t* d_s_up_keys,
                     const uint8_t* d_s_up_vals, const uint64_t* d_s_up_voff, uint64_t ns_up,
                     const uint32_t* d_s_del_trie, const uint8_t* d_s_del_keys, uint64_t ns_del, uint32_t s_klen,
@@ -4833,6 +5226,9 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     HIPCHK(hipSetDevice(c->dev));
     hipStream_t st = c->st;
     kh_stats sst{}, ast{};
+    // all or nothing: a refusal in either phase (or a device failure) rolls both handles back
+    // to the parent version (Ledger.scala:237-271 discards the world state of a failed attempt)
+    Txn txn(storage, state);
     // 1. every storage trie of the block (BlockWorldState.scala:243-252 -> TrieStorage.flush)
     FCommit S;
     S.up_trie = d_s_up_trie;
@@ -4874,6 +5270,7 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     A.ndel = na_del;
     A.klen = a_klen;
     forest_commit(state, A, &ast);
+    txn.release();
     memcpy(state_root32, state->root, 32);
     if (stats) {
       *stats = ast;

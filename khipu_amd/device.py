@@ -142,7 +142,37 @@ def _pack_dev(items, device):
     return data.to(device), off.to(device)
 
 
-class ResidentTrie:
+class _Versioned:
+    """Versioned commits shared by ResidentTrie and ResidentForest (kh_trie_savepoint /
+    kh_trie_rollback / kh_trie_release; Ledger.executeBlock's retry from the parent state,
+    Ledger.scala:237-271, and the rejection of validateBlockAfterExecution, :603-620)."""
+
+    def savepoint(self):
+        """Open a savepoint (they nest); returns the number now open."""
+        d = ctypes.c_uint32()
+        check(lib().kh_trie_savepoint(self.h, ctypes.byref(d)))
+        return int(d.value)
+
+    def rollback(self):
+        """Back to the innermost savepoint's version (root, records, last roots, write-back set)."""
+        self.ctx._sync()
+        check(lib().kh_trie_rollback(self.h))
+        self._after_rollback()
+
+    def release(self):
+        """Keep the commits since the innermost savepoint and close it."""
+        check(lib().kh_trie_release(self.h))
+
+    def savepoint_depth(self):
+        d = ctypes.c_uint32()
+        check(lib().kh_trie_savepoint_depth(self.h, ctypes.byref(d)))
+        return int(d.value)
+
+    def _after_rollback(self):
+        pass
+
+
+class ResidentTrie(_Versioned):
     """A trie kept in HBM between commits (kh_trie_open / kh_trie_apply).
 
     commit(upserts, deletes) folds a block's dirty set the way TrieAccounts.flush /
@@ -234,6 +264,43 @@ class ResidentTrie:
         created, every one reachable from the new root with an encoding >= 32 B, plus a changed root."""
         return emitted_nodes(lambda *a: lib().kh_trie_emit_nodes(self.h, *a))
 
+    def root_of(self, upserts=(), deletes=(), stats=None):
+        """TrieAccounts.rootHash (TrieAccounts.scala:73-80): the root commit(upserts, deletes)
+        would give; the trie is left unchanged (kh_trie_root_of)."""
+        ups = list(upserts.items()) if isinstance(upserts, dict) else list(upserts)
+        dels = list(deletes)
+        klen = len(ups[0][0]) if ups else (len(dels[0]) if dels else 32)
+        uk, _ = _pack_dev([k for k, _ in ups], self.dev)
+        uv, uo = _pack_dev([v for _, v in ups], self.dev)
+        dk, _ = _pack_dev(dels, self.dev)
+        root = np.zeros(32, np.uint8)
+        st = stats if stats is not None else KhStats()
+        flags = _lib.KH_HASH_KEYS if self.hash_keys else 0
+        self.ctx._sync()
+        check(lib().kh_trie_root_of(self.h, _ptr(uk), _ptr(uv), _ptr(uo), len(ups), _ptr(dk), len(dels), klen, flags,
+                                    root.ctypes.data, ctypes.byref(st)))
+        return root.tobytes()
+
+    def copy(self):
+        """MerklePatriciaTrie.copy (MerklePatriciaTrie.scala:556): an independent resident trie
+        holding the current version (kh_trie_copy)."""
+        h = ctypes.c_void_p()
+        self.ctx._sync()
+        check(lib().kh_trie_copy(self.h, ctypes.byref(h)))
+        t = ResidentTrie.__new__(ResidentTrie)
+        t.ctx, t.dev, t.h, t.hash_keys, t.root = self.ctx, self.dev, h, self.hash_keys, self.root
+        return t
+
+    def _after_rollback(self):
+        self.root = self.get_root()
+
+    def get_root(self):
+        """The handle's current root (kh_trie_root_of of an empty batch)."""
+        root = np.zeros(32, np.uint8)
+        check(lib().kh_trie_root_of(self.h, None, None, None, 0, None, 0, 32,
+                                    _lib.KH_HASH_KEYS if self.hash_keys else 0, root.ctypes.data, None))
+        return root.tobytes()
+
     def get(self, keys):
         """Batched get (kh_trie_get): [value or None] per key (raw keys with hash_keys)."""
         return trie_get(self.h, keys)
@@ -300,7 +367,7 @@ def emitted_nodes(call):
     raise RuntimeError("kh_trie_emit_nodes: size negotiation failed")
 
 
-class ResidentForest:
+class ResidentForest(_Versioned):
     """Many tries in one handle (contract storage tries; kh_forest_open / kh_forest_apply,
     SURVEY §8 a12): each op names its trie id; one commit re-roots every touched trie."""
 

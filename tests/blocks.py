@@ -75,7 +75,7 @@ def spans(vals, voff, idx):
 
 
 class BlockWorkload:
-    def __init__(self, ctx, n, nblocks, seed=3, nc=2000, ns=1000, dirty=20_000):
+    def __init__(self, ctx, n, nblocks, seed=3, nc=2000, ns=1000, dirty=20_000, emit=False):
         self.ctx, self.n, self.nblocks, self.nc, self.ns = ctx, n, nblocks, nc, ns
         self.dev = f"cuda:{ctx.device}"
         self.g = torch.Generator(device=self.dev)
@@ -88,8 +88,8 @@ class BlockWorkload:
         del addr
         self.state = ResidentTrie.__new__(ResidentTrie)
         self.state.ctx, self.state.dev, self.state.h = ctx, self.dev, None
-        self.state._open(self.keys, 32, self.vals, self.voff, n, False, emit=False)
-        self.forest = ResidentForest(ctx, hash_keys=True)
+        self.state._open(self.keys, 32, self.vals, self.voff, n, False, emit=emit)
+        self.forest = ResidentForest(ctx, hash_keys=True, emit=emit)
         self.ups = []        # every block's account upserts (keys, bodies, offsets) in order
         self.ups_pristine = []  # the same bodies as handed in, before kh_block_commit patched
                                 # the contracts' stateRoot fields in place

@@ -56,8 +56,9 @@ def test_config3_100k_storage_tries(khst, oracle):
         assert gpu[s] == oracle.seq_root(ks, vs), s
 
 
-def test_config2_block_commits(khst, oracle):
-    """configs[2] shape at 1M resident accounts (tests/blocks.py): 3 blocks of 20k dirty
+@pytest.mark.parametrize("n", [1_000_000, 50_000_000], ids=["1m", "50m"])
+def test_config2_block_commits(khst, oracle, n):
+    """configs[2] (tests/blocks.py) at 1M and at its configured 50M resident accounts: 3 blocks of 20k dirty
     accounts (90% updates, 5% inserts, 5% deletes) and 2,000 resident 1k-slot storage tries
     with 10 dirty slots each (10% deletes), storage roots injected into the account bodies,
     one kh_block_commit per block.  Checks: every storage root against a from-scratch
@@ -69,7 +70,7 @@ def test_config2_block_commits(khst, oracle):
     from tests.blocks import BlockWorkload
     ctx = Ctx(0)
     nb = 3
-    w = BlockWorkload(ctx, 1_000_000, nb)
+    w = BlockWorkload(ctx, n, nb)
     for b in range(nb):
         root = w.block(b)
     # storage tries
@@ -109,7 +110,7 @@ def test_config2_block_commits(khst, oracle):
     bodies[-1] = torch.from_numpy(expect).to(bodies[-1].device)
     K, V, O, N = w.final_accounts(bodies=bodies)
     vo = O.cpu().numpy().astype(np.uint64)
-    cpu, cst = oracle.batch_roots(K.cpu().numpy(), (V[:int(vo[-1])].cpu().numpy(), vo), klen=32)
+    cpu, cst = oracle.batch_roots(K.cpu().numpy(), (V[:int(vo[-1])].cpu().numpy(), vo), klen=32, nthreads=16)
     assert cpu[0] == root
     assert len(w.state) == cst["distinct"]
     K, V, O, N = w.final_accounts()

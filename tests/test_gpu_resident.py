@@ -144,13 +144,18 @@ def test_forest_vs_oracle(khst, oracle):
     """A forest (kh_forest_apply): storage tries of many contracts in one
     handle, blocks touching some of them; every touched trie's root equals the oracle's
     trie of that contract folded put-by-put / remove-by-remove; a trie deleted to empty has
-    EMPTY_TRIE_HASH; identical keys in different tries stay apart."""
+    EMPTY_TRIE_HASH; identical keys in different tries stay apart.  The block's write-back
+    delta (the storageNodeStorage.update half of BlockWorldState.scala:320-324) is held to
+    the strict f2 contract (tests/writeback.py): every emitted pair an Updated entry of a
+    touched trie's log, reachable from its new root, and no new reachable node missing."""
     from khipu_amd.device import Ctx, ResidentForest
+    from tests.writeback import check_delta, settle
     r = random.Random(77)
     f = ResidentForest(Ctx(0), hash_keys=True, emit=True)
     tries = {}
+    store = {}
     ids = [r.randrange(1 << 32) for _ in range(60)]
-    for blk in range(6):
+    for blk in range(8):
         ups, dels = [], []
         for t in r.sample(ids, 25):
             o = tries.setdefault(t, oracle.Trie())
@@ -177,11 +182,9 @@ def test_forest_vs_oracle(khst, oracle):
         for t in touched:
             assert got[t] == tries[t].root_hash(), (blk, t)
         delta = f.nodes()
-        for t in touched:
-            want = tries[t].reachable() if tries[t]._live else {}
-            for h, e in delta.items():
-                if h in want:
-                    assert want[h] == e
+        check_delta(delta, [tries[t] for t in touched], store, ("forest block", blk))
+        store.update(delta)
+        settle(tries.values())
     f.close()
 
 
