@@ -81,6 +81,9 @@ typedef struct kh_stats {
   double t_topo_ms;        /* LCP + topology */
   double t_leaf_ms;        /* leaf encode + hash */
   double t_branch_ms;      /* all branch levels */
+  uint32_t n_groups;       /* top-nibble groups of a grouped build (0 or 1: one plain build); the
+                              stage times are then sums over the groups' builds */
+  uint32_t reserved;
 } kh_stats;
 
 const char* kh_last_error(void);

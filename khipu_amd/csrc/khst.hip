@@ -18,8 +18,12 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <exception>
+#include <functional>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -902,6 +906,31 @@ __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
   wave_count(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl != 0);
   if (lb) atomicAdd(&T.ctr[CTR_LONGB], (unsigned long long)lb);
 }
+// The same over one group of a grouped build: thread t takes input list[t] (ascending input
+// indices), reading the keys and values of the whole build in place (n_all bounds them)
+__global__ void __launch_bounds__(BS) k_leaf_in_list(Topo T, const uint32_t* list, uint64_t ng, uint64_t n_all) {
+  const uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  const uint64_t j = t < ng ? list[t] : n_all;  // past the group: a neutral lane
+  auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {
+    WaveBounds b;
+    b.emax = wave_max_u32(use ? e : 0u);
+    b.emin = 255u - wave_max_u32(use ? 255u - e : 0u);
+    b.Lmax = wave_max_u32(use ? lhi : 0u);
+    b.Lmin = 255u - wave_max_u32(use ? 255u - llo : 0u);
+    return b;
+  };
+  uint32_t inl = 0, lb = 0;
+  const uint32_t perms = op_leaf_in3(T, j, n_all, wave, &inl, &lb);
+  wave_count(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms != 0);
+  wave_count(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), perms != 0);
+  wave_count(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl != 0);
+  if (lb) atomicAdd(&T.ctr[CTR_LONGB], (unsigned long long)lb);
+}
+// a group's dropped duplicates (earlier puts of a key put again): no parent-depth record
+__global__ void __launch_bounds__(BS) k_pdinv_skip(const uint32_t* list, uint64_t ng, uint64_t* pdinv) {
+  const uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (t < ng) pdinv[list[t]] = PDINV_SKIP;
+}
 
 // The same leaves in SORTED order (KHST_LEAF=sorted, measurement switch): the parent depth
 // comes from the two adjacent boundaries, so the kernel starts right after k_lcp with no
@@ -1760,6 +1789,11 @@ struct kh_ctx {
   unsigned long long* h_pinned = nullptr;  // small pinned staging for syncs
   uint8_t* h_res = nullptr;                // pinned staging of the per-result outputs (grown; a pageable
   size_t h_res_cap = 0;                    // copy of 100k roots cost 20-30 ms of page pinning per build)
+  // grouped builds (grouped_build): the hashed keys, sort words, group lists and parent-depth
+  // records of the whole build; the second context the odd groups run on; per-group events
+  DevBuf gws;
+  kh_ctx* gsub = nullptr;
+  hipEvent_t gev[18] = {};
   // last build (for emission)
   Topo T{};
   uint64_t last_B = 0;
@@ -1770,6 +1804,17 @@ struct kh_ctx {
 // ---------------------------------------------------------------------------
 // the build
 // ---------------------------------------------------------------------------
+// One top-nibble group of a grouped build (grouped_build): the caller hashed every key and
+// partitioned the sort words by group; the group's build sorts, derives the topology and
+// hashes only its own keys, reading the keys and values of the whole build in place.
+struct GroupArgs {
+  const uint32_t* ck = nullptr;    // [ng] the group's 32-bit sort words, in input order
+  const uint32_t* list = nullptr;  // [ng] their input indices, ascending (the leaf kernel's order)
+  uint64_t n_all = 0;              // inputs of the whole build: the key / value buffers' bounds
+  uint64_t* pdinv = nullptr;       // [n_all] parent depth | sorted position per input, shared by the groups
+  hipEvent_t start_after = nullptr;  // the build's stream waits on it before its first launch
+  std::function<void()> on_topo;     // called once the group's branch topology is enqueued
+};
 struct BuildArgs {
   const uint8_t* keys;
   uint32_t klen;
@@ -1786,6 +1831,8 @@ struct BuildArgs {
   struct ElemArgs* el = nullptr;   // element build of a resident forest commit (forest.h; nullable)
   hipEvent_t vals_ready = nullptr; // the values / offsets land later (multi-GPU exchange): wait before reading them
   bool dev_results = false;        // results and counters stay on the device (no host sync at the end)
+  const GroupArgs* grp = nullptr;  // a group of a grouped build (depth0 = 1, keys = the hashed keys of all groups)
+  bool no_groups = false;          // never split into a grouped build (its own fallback)
 };
 // element build (forest.h): inputs are leaves and subtree elements; the capped reference
 // of every element node, branch and extension is kept for the forest's records
@@ -1826,6 +1873,10 @@ static uint8_t* pinned_stage(kh_ctx* c, size_t bytes) {
   return c->h_res;
 }
 
+// a grouped build met a run of > TIE_RUN_MAX keys with equal 32-bit prefixes (adversarial
+// keys): the build is redone as one plain build, which takes the full 256-bit sort
+struct GroupFallback {};
+
 static float ev_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0;
   if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
@@ -1852,6 +1903,7 @@ struct SortIO {
   // a device word copied to the host with the first sync's flags (c->h_pinned[1]): the
   // caller's check of earlier stream work, read without a sync of its own (nullable)
   const unsigned long long* chk = nullptr;
+  bool no_full_sort = false;  // a group of a grouped build (input indices are not 0..n-1): no 256-bit sort
   // out
   uint8_t* u = nullptr;  // ck_path: boundary values, written for the tie runs' inner boundaries
   uint32_t depth0 = 0;
@@ -1968,6 +2020,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
   const bool fallback = tie_flags & 1, dups = tie_flags & 2;
   uint64_t m = n;
   uint32_t* sidx = idxs;
+  if (fallback && S.no_full_sort) throw GroupFallback{};
   if (fallback) {
     // full 256-bit (+segment) LSD sort from the input order
     uint32_t* ia = idx0;
@@ -2033,7 +2086,13 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
 }
 
 static void build_stats(kh_ctx* c, const unsigned long long* hc, kh_stats* stats);
+static uint32_t group_count(const BuildArgs& A);
+static void grouped_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats, uint32_t G);
 static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats) {
+  if (const uint32_t ng = group_count(A); ng > 1) {  // a large plain root: pipelined over top-nibble groups
+    grouped_build(c, A, O, stats, ng);
+    return;
+  }
   hipStream_t st = c->st;
   const uint64_t n = A.n;
   const bool segmented = A.seg != nullptr;
@@ -2041,6 +2100,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   if (n >= (1ULL << 31)) throw KhError{KH_EINVAL, "n must be < 2^31 per device"};
   if (A.depth0 > 1) throw KhError{KH_EINVAL, "depth0 must be 0 or 1"};
   if (segmented && A.depth0 != 0) throw KhError{KH_EINVAL, "segmented builds use depth0 = 0"};
+  const GroupArgs* G = A.grp;
+  if (G && (segmented || A.depth0 != 1 || A.emit || A.el || A.kn || (A.flags & KH_HASH_KEYS) || A.klen != 32 ||
+            ((uintptr_t)A.keys & 15)))
+    throw KhError{KH_EINTERNAL, "grouped build: a plain depth-1 build over 32-byte hashed keys"};
   if (!(A.flags & KH_HASH_KEYS) && A.klen != 32) throw KhError{KH_EINVAL, "keys must be 32 bytes unless KH_HASH_KEYS"};
   if (A.klen == 0 || A.klen > 4096) throw KhError{KH_EINVAL, "bad key length"};
   const uint32_t sb = segmented ? bits_for(A.nseg) : 0;
@@ -2183,6 +2246,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     T.longlist = cv.take<uint32_t>(n);
     T.lpos = 1;
   }
+  if (G) T.pdinv = G->pdinv;  // indexed by input: shared by the groups (each writes its own inputs')
   T.depth0 = A.depth0;
   T.segmented = segmented ? 1 : 0;
   T.vals = A.vals;
@@ -2206,8 +2270,12 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   static const bool seg_ck = !getenv("KHST_SEG_CK") || strcmp(getenv("KHST_SEG_CK"), "0") != 0;
   const bool seg_words_ok = segmented && sb + CK_KEY_BITS <= 32 && (n / A.nseg) <= (1ULL << (32 - sb - 2));
   const bool ck_path = early && !A.kn && (!segmented || (seg_ck && seg_words_ok));
-  const bool ck_ready = ck_path && (A.flags & KH_HASH_KEYS);
-  if (ck_ready) {
+  const bool ck_ready = ck_path && ((A.flags & KH_HASH_KEYS) || G);
+  if (G) {  // the group's sort words and input indices (input order), copied: the sort overwrites them
+    if (G->start_after) HIPCHK(hipStreamWaitEvent(st, G->start_after, 0));
+    HIPCHK(hipMemcpyAsync(ck0, G->ck, n * 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(idx0, G->list, n * 4, hipMemcpyDeviceToDevice, st));
+  } else if (ck_ready) {
     uint32_t* c0 = (uint32_t*)ck0;
     if (A.klen <= 135)
       hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, c0, idx0, A.seg,
@@ -2236,6 +2304,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr,
              A.kn, ck_ready};
     S.ck_path = ck_path;
+    S.no_full_sort = G != nullptr;
     S.u = T.u;
     S.depth0 = A.depth0;
     sort_dedup(c, S);
@@ -2321,12 +2390,20 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     const char* e = getenv("KHST_PD");  // measurement switch
     return !e ? PD_DEFAULT : strcmp(e, "ansv") == 0 ? 1 : strcmp(e, "first") == 0 ? 3 : 0;
   }();
-  const int pd_mode = (early && nb > 0) ? pd_env : 0;
+  const int pd_mode = (early && nb > 0) ? (G ? PD_DEFAULT : pd_env) : 0;
+  auto pdinv_skip = [&](hipStream_t s) {  // every input of the build without a record (its own inputs only)
+    if (G) {
+      hipLaunchKernelGGL(k_pdinv_skip, GRID(n, BS), dim3(BS), 0, s, G->list, n, T.pdinv);
+      LAUNCH_CHECK();
+    } else {
+      HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, s));
+    }
+  };
   if (pd_mode == 2) {  // sorted leaves: no scatter, the stash is written in sorted order
     HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));
   } else if (pd_mode) {  // presets for the scatter folded into k_ansv (on st)
-    if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, st));  // dropped duplicates: PDINV_SKIP
-    HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));                  // every leaf a hash unless it says otherwise
+    if (m < n) pdinv_skip(st);                      // dropped duplicates: PDINV_SKIP
+    HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));  // every leaf a hash unless it says otherwise
   }
   if (nb > 0) {
     hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb, ties_u);
@@ -2344,15 +2421,17 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
     hipStream_t s2 = c->st2;
     if (scatter) {
-      if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, s2));  // dropped duplicates: PDINV_SKIP
-      HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, s2));                  // every leaf a hash unless it says otherwise
+      if (m < n) pdinv_skip(s2);                      // dropped duplicates: PDINV_SKIP
+      HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, s2));  // every leaf a hash unless it says otherwise
       hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, s2, T);
       LAUNCH_CHECK();
     }
     if (A.vals_ready) HIPCHK(hipStreamWaitEvent(s2, A.vals_ready, 0));  // the topology need not wait
     HIPCHK(hipEventRecord(c->ev[9], s2));
     static const bool leaf_v2 = getenv("KHST_LEAF") && !strcmp(getenv("KHST_LEAF"), "v2");  // measurement switch
-    if (leaf_v2)
+    if (G)
+      hipLaunchKernelGGL(k_leaf_in_list, GRID(n, BS), dim3(BS), 0, s2, T, G->list, n, G->n_all);
+    else if (leaf_v2)
       hipLaunchKernelGGL(k_leaf_in_v2, GRID(n, BS), dim3(BS), 0, s2, T, n);
     else
       hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, s2, T, n);
@@ -2464,6 +2543,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   }
   if (early) {
     HIPCHK(hipEventRecord(c->ev[3], st));      // topology done (the leaves may still run)
+    if (G && G->on_topo) G->on_topo();             // (the next group's sort may start behind it)
     HIPCHK(hipStreamWaitEvent(st, c->ev[10], 0));  // ... and the leaves: their long-leaf bytes
   } else {
     hipLaunchKernelGGL(k_leaf_topo, GRID(m, BS), dim3(BS), 0, st, T);
@@ -2766,6 +2846,230 @@ static kh_ctx* ctx_new(int dev) {
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipHostMalloc((void**)&c->h_pinned, 16384, hipHostMallocDefault));  // >= CTR_N * CTR_SHARDS words
   return c;
+}
+
+// ---------------------------------------------------------------------------
+// Grouped build: one large plain root pipelined over top-nibble groups on one GPU.
+//
+// A plain build's critical path is key hashing -> sort -> boundaries -> ANSV with the
+// parent-depth scatter -> the leaf kernel -> the branch levels; the sort and the topology
+// leave the VALU idle (~8.5 ms at 100M).  Here every key is hashed once, the
+// (sort word, input index) pairs are split stably into G groups by their top key bits
+// (G = 2^gb; group g holds the top nibbles [16g/G, 16(g+1)/G)), and group g is an ordinary
+// depth-1 build of its own keys -- sort, topology, leaves (its inputs in input order,
+// k_leaf_in_list), branch levels -- reading the keys and values of the whole build in
+// place.  Groups alternate between two contexts (four streams: the HIP hardware queue
+// count), driven by two host threads; group g + 1's sort waits only for group g's topology,
+// so it and group g + 1's topology run beside group g's leaves and branch levels.  The 16
+// top-nibble references are folded into the root branch on the host (kh_fold_root16's
+// encoding, MerklePatriciaTrie.scala:169).  Adversarial keys (a run of > TIE_RUN_MAX equal
+// 32-bit prefixes, or fewer than two occupied top nibbles) redo the build as one plain build.
+// Measured at 100M accounts (profiles/r4c_groups_ab_100m.json, one box): 42.97 ms plain against
+// 43.93 / 45.26 / 47.26 ms with 2 / 4 / 8 groups (roots equal).  The groups' topology chains
+// (sort, ANSV, chain, branch records, level order: ~11 ms of latency-bound kernels per 100M keys
+// alone) become the critical path: group g + 1's sort waits for group g's topology, and the
+// topology runs no faster beside the leaf and branch kernels than it does beside the leaf kernel
+// in the plain build.  So the plain build stays the default; KHST_GROUPS=2|4|8|16 (read per call,
+// a measurement switch) selects the grouped build, which tests/test_gpu_grouped.py keeps
+// parity-checked.
+constexpr uint64_t GROUP_MIN_N = 1ULL << 23;  // below ~8M inputs the per-group fixed costs dominate
+static uint32_t group_count(const BuildArgs& A) {
+  const char* e = getenv("KHST_GROUPS");
+  const int env = e ? atoi(e) : 1;
+  if (env <= 1 || A.grp || A.no_groups || A.seg || A.depth0 || A.emit || A.el || A.kn || A.vlen || A.vals_ready ||
+      A.n < GROUP_MIN_N)
+    return 1;
+  uint32_t g = 2;
+  while (g < (uint32_t)env && g < 16) g <<= 1;
+  return g;
+}
+__global__ void k_group_offsets(const uint32_t* counts, uint32_t tiles, uint32_t G, uint64_t n, uint64_t* gofs) {
+  const uint32_t g = threadIdx.x;  // the exclusive scan of the digit-major counts: digit g starts at tile 0
+  if (g < G) gofs[g] = counts[(uint64_t)g * tiles];
+  if (g == G) gofs[G] = n;
+}
+static kh_ctx* ctx_new(int dev);
+static void grouped_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats, uint32_t G) {
+  hipStream_t st = c->st;
+  const uint64_t n = A.n;
+  uint32_t gb = 0;
+  while ((1u << gb) < G) ++gb;
+  if (!c->gsub) c->gsub = ctx_new(c->dev);
+  for (auto& e : c->gev)
+    if (!e) HIPCHK(hipEventCreate(&e));
+  // ---- the whole build's keys, sort words, group lists and parent-depth records
+  const uint32_t tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+  const bool hashed = A.flags & KH_HASH_KEYS;
+  const bool own_keys = hashed || ((uintptr_t)A.keys & 15);
+  if (!hashed && A.klen != 32) throw KhError{KH_EINVAL, "keys must be 32 bytes unless KH_HASH_KEYS"};
+  c->gws.ensure(carve_size({own_keys ? n * 32 : 0, n * 4, n * 4, n * 4, n * 4, n * 8, (size_t)tiles * 256 * 4,
+                            scan_scratch_bytes((uint64_t)tiles * 256, 4), 64 * 8}));
+  Carver cv{(char*)c->gws.p, 0, c->gws.cap};
+  uint64_t* K32 = own_keys ? cv.take<uint64_t>(n * 4) : (uint64_t*)A.keys;
+  uint32_t* ck = cv.take<uint32_t>(n);
+  uint32_t* idx = cv.take<uint32_t>(n);
+  uint32_t* gck = cv.take<uint32_t>(n);
+  uint32_t* gidx = cv.take<uint32_t>(n);
+  uint64_t* pdinv = cv.take<uint64_t>(n);
+  uint32_t* counts = cv.take<uint32_t>((size_t)tiles * 256);
+  void* scan_ws = cv.take<char>(scan_scratch_bytes((uint64_t)tiles * 256, 4));
+  uint64_t* gofs = cv.take<uint64_t>(64);
+  HIPCHK(hipEventRecord(c->gev[16], st));
+  if (hashed) {
+    if (A.klen <= 135)
+      hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, ck, idx,
+                         (const uint32_t*)nullptr, 0u);
+    else
+      hipLaunchKernelGGL(k_hash_keys_ck<false>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, ck, idx,
+                         (const uint32_t*)nullptr, 0u);
+  } else {
+    if (own_keys) HIPCHK(hipMemcpyAsync(K32, A.keys, n * 32, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_make_ck32, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, n, ck, idx,
+                       (const uint32_t*)nullptr, 0u);
+  }
+  LAUNCH_CHECK();
+  HIPCHK(hipEventRecord(c->gev[17], st));
+  // ---- the stable split by the top gb bits: one radix pass (only G of its 256 digits occur),
+  // input order kept inside a group
+  const int sh = 32 - (int)gb;
+  hipLaunchKernelGGL(k_rs_hist<uint32_t>, dim3(tiles), dim3(RS_THREADS), 0, st, (const uint32_t*)ck, n, sh, counts,
+                     tiles);
+  scan_exclusive<uint32_t>(counts, counts, (uint64_t)tiles * 256, (uint32_t*)nullptr, scan_ws, st);
+  hipLaunchKernelGGL(k_rs_scatter<uint32_t>, dim3(tiles), dim3(RS_THREADS), 0, st, (const uint32_t*)ck,
+                     (const uint32_t*)idx, gck, gidx, n, sh, (const uint32_t*)counts, tiles, false);
+  hipLaunchKernelGGL(k_group_offsets, dim3(1), dim3(64), 0, st, (const uint32_t*)counts, tiles, G, n, gofs);
+  LAUNCH_CHECK();
+  HIPCHK(hipMemcpyAsync(c->h_pinned, gofs, (G + 1) * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  std::vector<uint64_t> go(c->h_pinned, c->h_pinned + G + 1);
+  // ---- the groups: two host threads, group g on context g & 1
+  kh_ctx* ctxs[2] = {c, c->gsub};
+  std::mutex mu;
+  std::condition_variable cvar;
+  std::vector<char> topo(G, 0);
+  bool abort = false, fallback = false;
+  std::exception_ptr err;
+  std::vector<BuildOut> outs(G);
+  std::vector<kh_stats> gst(G);
+  std::vector<double> t_end(G, 0.0);
+  auto fail = [&](bool fb, std::exception_ptr e) {
+    std::lock_guard<std::mutex> lk(mu);
+    abort = true;
+    if (fb) fallback = true;
+    if (e && !err) err = e;
+    cvar.notify_all();
+  };
+  auto worker = [&](int w) {
+    try {
+      HIPCHK(hipSetDevice(c->dev));
+      kh_ctx* x = ctxs[w];
+      for (uint32_t g = (uint32_t)w; g < G; g += 2) {
+        hipEvent_t after = c->gev[17];
+        if (g > 0) {
+          std::unique_lock<std::mutex> lk(mu);
+          cvar.wait(lk, [&] { return topo[g - 1] || abort; });
+          if (abort) return;
+          after = c->gev[g - 1];
+        }
+        bool signalled = false;
+        auto signal = [&, g, x] {
+          HIPCHK(hipEventRecord(c->gev[g], x->st));
+          std::lock_guard<std::mutex> lk(mu);
+          topo[g] = 1;
+          signalled = true;
+          cvar.notify_all();
+        };
+        const uint64_t g0 = go[g], ng = go[g + 1] - go[g];
+        if (ng == 0) {
+          HIPCHK(hipStreamWaitEvent(x->st, after, 0));
+          signal();
+          continue;
+        }
+        GroupArgs GA;
+        GA.ck = gck + g0;
+        GA.list = gidx + g0;
+        GA.n_all = n;
+        GA.pdinv = pdinv;
+        GA.start_after = after;
+        GA.on_topo = signal;
+        BuildArgs B{(const uint8_t*)K32, 32, A.vals, A.voff, ng, nullptr, 1, 1, 0, false};
+        B.grp = &GA;
+        run_build(x, B, outs[g], &gst[g]);
+        if (!signalled) signal();
+        t_end[g] = ev_ms(c->gev[16], x->ev[5]);
+      }
+    } catch (GroupFallback&) {
+      fail(true, nullptr);
+    } catch (...) {
+      fail(false, std::current_exception());
+    }
+  };
+  std::thread t1(worker, 1);
+  worker(0);
+  t1.join();
+  if (err) std::rethrow_exception(err);
+  // ---- the 16 top-nibble references folded into the root branch
+  uint64_t refs[64] = {};
+  uint32_t lens[16] = {};
+  int nonempty = 0, inl_tops = 0;
+  for (uint32_t q = 0; q < 16 && !fallback; ++q) {
+    const BuildOut& R = outs[q >> (4 - gb)];
+    const uint32_t L = R.res_len.size() > q ? R.res_len[q] : 0;
+    if (!L) continue;
+    ++nonempty;
+    lens[q] = L >= 32 ? 32 : L;
+    memcpy(refs + 4 * q, L >= 32 ? &R.res_hash[4 * q] : &R.res_inl[4 * q], 32);
+    if (L < 32) ++inl_tops;
+  }
+  if (fallback || nonempty < 2) {  // adversarial keys: one plain build (full sort / a root that is not a branch)
+    for (kh_ctx* x : ctxs) {
+      HIPCHK(hipStreamSynchronize(x->st));
+      HIPCHK(hipStreamSynchronize(x->st2));
+    }
+    BuildArgs P = A;
+    P.no_groups = true;
+    run_build(c, P, O, stats);
+    return;
+  }
+  uint64_t enc[80];
+  const uint32_t L = encode_branch16(refs, lens, (uint8_t*)enc);
+  uint64_t h[4];
+  kec256_msg<true>((const uint8_t*)enc, L, h);
+  O.res_hash.assign(h, h + 4);
+  O.res_len.assign(1, L);
+  O.res_inl.assign(4, 0);
+  if (L < 32) memcpy(O.res_inl.data(), enc, 32);
+  if (stats) {
+    kh_stats s{};
+    s.n_inputs = n;
+    for (uint32_t g = 0; g < G; ++g) {
+      const kh_stats& x = gst[g];
+      s.n_leaves += x.n_leaves;
+      s.n_branches += x.n_branches;
+      s.n_extensions += x.n_extensions;
+      s.n_inline += x.n_inline;
+      s.n_node_hashes += x.n_node_hashes;
+      s.n_node_perms += x.n_node_perms;
+      s.arena_bytes += x.arena_bytes;
+      s.n_levels = std::max(s.n_levels, x.n_levels);
+      s.full_sort |= x.full_sort;
+      s.t_sort_ms += x.t_sort_ms;
+      s.t_topo_ms += x.t_topo_ms;
+      s.t_leaf_ms += x.t_leaf_ms;
+      s.t_branch_ms += x.t_branch_ms;
+      s.t_total_ms = std::max(s.t_total_ms, t_end[g]);
+    }
+    // the subtrie tops were hashed as tops; in the whole trie a top shorter than 32 bytes is
+    // embedded in the root branch instead; the root branch itself is one more node
+    s.n_node_hashes = s.n_node_hashes - inl_tops + 1;
+    s.n_node_perms = s.n_node_perms - inl_tops + (L / 136 + 1);
+    s.n_inline += inl_tops;
+    s.n_branches += 1;
+    s.n_key_perms = hashed ? n * (uint64_t)(A.klen / 136 + 1) : 0;
+    s.t_keys_ms = ev_ms(c->gev[16], c->gev[17]);
+    s.n_groups = G;
+    *stats = s;
+  }
 }
 
 static kh_ctx* shared_ctx(int dev) {
@@ -4095,6 +4399,9 @@ static void trie_release(kh_trie* h) {
 }
 // an all-or-nothing section over one or two handles (kh_block_commit, kh_trie_root_of): a
 // savepoint on each; rolled back unless released
+#ifndef KHST_BLOCK_TXN  // measurement builds only (-DKHST_BLOCK_TXN=0: a block commit without its journal)
+#define KHST_BLOCK_TXN 1
+#endif
 struct Txn {
   kh_trie* h[2] = {nullptr, nullptr};
   bool open = false;
@@ -4187,10 +4494,13 @@ int kh_ctx_destroy(kh_ctx* c) {
   API_TRY({
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->st);
+    if (c->gsub) (void)kh_ctx_destroy(c->gsub);
     for (DevBuf* b : {&c->ws_inject, &c->ws_list, &c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->in_kn, &c->in_aux, &c->in_block, &c->out_emit,
-                      &c->emit_dev})
+                      &c->emit_dev, &c->gws})
       b->release();
     for (auto& e : c->ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->gev)
       if (e) (void)hipEventDestroy(e);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->h_res) (void)hipHostFree(c->h_res);
@@ -5228,7 +5538,9 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     kh_stats sst{}, ast{};
     // all or nothing: a refusal in either phase (or a device failure) rolls both handles back
     // to the parent version (Ledger.scala:237-271 discards the world state of a failed attempt)
+#if KHST_BLOCK_TXN
     Txn txn(storage, state);
+#endif
     // 1. every storage trie of the block (BlockWorldState.scala:243-252 -> TrieStorage.flush)
     FCommit S;
     S.up_trie = d_s_up_trie;
@@ -5270,7 +5582,9 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     A.ndel = na_del;
     A.klen = a_klen;
     forest_commit(state, A, &ast);
+#if KHST_BLOCK_TXN
     txn.release();
+#endif
     memcpy(state_root32, state->root, 32);
     if (stats) {
       *stats = ast;

@@ -35,27 +35,33 @@ static int g_link_mode = 0;
 // keys: n*32 (already keccak'd), vals/voff packed; seg nullable.
 // Outputs per result r: hash (32 B), enc length, inline bytes (32 B).
 // stats_out[0..5] = m, B, node hashes, node perms, inline nodes, extensions.
+// list (nullable): one group of a grouped build (khst.hip grouped_build): the build covers
+// only the inputs list[0 .. ng) (ascending input indices) of the n inputs, sorts their global
+// indices, and hashes its leaves in list order (k_leaf_in_list) against the whole buffers
 static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, uint64_t n, const uint32_t* seg,
                       uint64_t nseg, uint32_t depth0, uint8_t* out_hash, uint32_t* out_len, uint8_t* out_inl,
-                      uint64_t* stats_out) {
+                      uint64_t* stats_out, const uint32_t* list = nullptr, uint64_t ng = 0) {
   const bool segmented = seg != nullptr;
   const uint64_t nres = segmented ? nseg : (depth0 == 1 ? 16 : 1);
   std::vector<uint64_t> res_hash(nres * 4, 0), res_inl(nres * 4, 0);
   std::vector<uint32_t> res_len(nres, 0);
-  if (n == 0) {
+  if (n == 0 || (list && ng == 0)) {
     memset(out_len, 0, nres * 4);
     return 0;
   }
   // sort (stable, by segment then key bytes), keep the last duplicate
-  std::vector<uint32_t> order(n);
-  std::iota(order.begin(), order.end(), 0u);
+  std::vector<uint32_t> order(list ? ng : n);
+  if (list)
+    std::copy(list, list + ng, order.begin());
+  else
+    std::iota(order.begin(), order.end(), 0u);
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
     if (segmented && seg[a] != seg[b]) return seg[a] < seg[b];
     return memcmp(keys + 32ull * a, keys + 32ull * b, 32) < 0;
   });
   std::vector<uint32_t> sidx;
-  for (uint64_t i = 0; i < n; ++i) {
-    bool dup_next = i + 1 < n && memcmp(keys + 32ull * order[i], keys + 32ull * order[i + 1], 32) == 0 &&
+  for (uint64_t i = 0; i < order.size(); ++i) {
+    bool dup_next = i + 1 < order.size() && memcmp(keys + 32ull * order[i], keys + 32ull * order[i + 1], 32) == 0 &&
                     (!segmented || seg[order[i]] == seg[order[i + 1]]);
     if (!dup_next) sidx.push_back(order[i]);
   }
@@ -225,8 +231,10 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
     };
     const bool sorted_order = g_leaf_mode == 3;  // KHST_LEAF=sorted (k_leaf_sorted)
     if (sorted_order) std::fill(emeta.begin(), emeta.end(), (uint8_t)32);
-    for (uint64_t j = 0; j < (sorted_order ? m : n) + 3; ++j) {  // lanes past the end take part as on the device
+    const uint64_t nlanes = list ? ng : sorted_order ? m : n;
+    for (uint64_t t = 0; t < nlanes + 3; ++t) {  // lanes past the end take part as on the device
       uint32_t in1 = 0, lb = 0;
+      const uint64_t j = list ? (t < ng ? list[t] : n) : t;  // k_leaf_in_list: the group's inputs
       uint32_t p = sorted_order ? op_leaf_sorted(T, j, n, wave, &in1, &lb) : op_leaf_in3(T, j, n, wave, &in1, &lb);
       perms += p;
       hashes += p ? 1 : 0;
@@ -348,6 +356,48 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
               uint64_t nseg, uint32_t depth0, uint8_t* out_hash, uint32_t* out_len, uint8_t* out_inl,
               uint64_t* stats_out) {
   return build_core(keys, vals, voff, n, seg, nseg, depth0, out_hash, out_len, out_inl, stats_out);
+}
+
+// a grouped build (khst.hip grouped_build): the inputs split stably by the top gb bits of
+// their keys, each group a depth-1 build over its own inputs (list order), the 16 top-nibble
+// references folded into the root (kh_fold_root16's encoding)
+int emu_build_grouped(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, uint64_t n, uint32_t gb,
+                      uint8_t* root32, uint64_t* stats_out) {
+  const uint32_t G = 1u << gb;
+  std::vector<std::vector<uint32_t>> lists(G);
+  for (uint64_t i = 0; i < n; ++i) lists[keys[32 * i] >> (8 - gb)].push_back((uint32_t)i);
+  uint64_t refs[64] = {}, st[6] = {}, tot[6] = {};
+  uint32_t lens[16] = {};
+  int nonempty = 0, inl_tops = 0;
+  for (uint32_t g = 0; g < G; ++g) {
+    uint8_t h[16 * 32], in[16 * 32];
+    uint32_t len[16];
+    int rc = build_core(keys, vals, voff, n, nullptr, 1, 1, h, len, in, st, lists[g].data(), lists[g].size());
+    if (rc) return rc;
+    if (!lists[g].empty())
+      for (int k = 0; k < 6; ++k) tot[k] += st[k];
+    for (uint32_t q = g * (16 / G); q < (g + 1) * (16 / G); ++q) {
+      if (!len[q]) continue;
+      ++nonempty;
+      lens[q] = len[q] >= 32 ? 32 : len[q];
+      memcpy(refs + 4 * q, len[q] >= 32 ? h + 32 * q : in + 32 * q, 32);
+      if (len[q] < 32) ++inl_tops;
+    }
+  }
+  if (nonempty < 2) return -9;  // the device redoes such a build as one plain build
+  uint64_t enc[80];
+  const uint32_t L = encode_branch16(refs, lens, (uint8_t*)enc);
+  uint64_t hh[4];
+  kec256_msg<true>((const uint8_t*)enc, L, hh);
+  memcpy(root32, hh, 32);
+  if (stats_out) {
+    tot[1] += 1;                    // the root branch
+    tot[2] = tot[2] - inl_tops + 1;  // node hashes: an inline top is embedded, the root is hashed
+    tot[3] = tot[3] - inl_tops + (L / 136 + 1);
+    tot[4] += inl_tops;
+    memcpy(stats_out, tot, sizeof(tot));
+  }
+  return 0;
 }
 
 int emu_node_children(const uint8_t* v, uint64_t len, int kind, uint8_t* out32, uint8_t* kinds, uint32_t* n) {

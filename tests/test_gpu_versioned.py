@@ -285,9 +285,8 @@ def test_refused_block_leaves_both_handles_at_parent(khst, oracle):
     b0 = bytearray(body0)
     b0[len(b0) - 65:len(b0) - 33] = t.root_hash()
     assert got == oracle.seq_root(keys, [bytes(b0), body] + vals[2:])
-    from khipu_amd._lib import lib
-    lib().kh_trie_free(state.h)
-    lib().kh_trie_free(forest.h)
+    state.close()
+    forest.close()
 
 
 def test_refused_account_descent_rolls_back_storage(khst, oracle):
@@ -313,9 +312,8 @@ def test_refused_account_descent_rolls_back_storage(khst, oracle):
                           np.array([0xFFFFFFFF], np.uint32), None)
     assert state.get_root() == parent_state and forest.last_roots() == parent_last
     assert forest.get([(5, bytes(31) + b"\x03")]) == [None]
-    from khipu_amd._lib import lib
-    lib().kh_trie_free(state.h)
-    lib().kh_trie_free(forest.h)
+    state.close()
+    forest.close()
 
 
 def test_block_rollback_and_sequential_retry(khst, oracle):
