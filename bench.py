@@ -63,9 +63,13 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-cpu-batch", action="store_true", help="skip the all-core full-size CPU root")
     p.add_argument("--sharded", action="store_true", help="force the nibble-sharded RCCL path (any N)")
-    p.add_argument("--workload", choices=("state", "lists", "storage"), default="state",
+    p.add_argument("--workload", choices=("state", "lists", "storage", "verify"), default="state",
                    help="state: the BASELINE metric (default); lists: transactions roots (SURVEY §8 f4); "
-                        "storage: configs[3], 100k storage tries (trie-id shards over --gpus N)")
+                        "storage: configs[3], 100k storage tries (trie-id shards over --gpus N); "
+                        "verify: fast-sync NodeData verification (SURVEY §8 f3)")
+    p.add_argument("--nodes-accounts", type=int, default=1_000_000,
+                   help="verify: the NodeData batch is every node of a trie of this many accounts")
+    p.add_argument("--no-host-path", action="store_true", help="state: skip the host-buffer (PCIe) drop-in timing")
     p.add_argument("--tries", type=int, default=100_000, help="storage: storage tries per step")
     p.add_argument("--blocks", type=int, default=10_000, help="lists: blocks per step")
     return p.parse_args()
@@ -139,6 +143,100 @@ def cpu_baseline(ctx, cfg, addr, vals, voff, samples):
                                                 "residual_us_per_put": res},
             "state_root_s_extrapolated_100M": round(est, 1),
             "extrapolation": "100M x (a + b log16 100M) us from the fitted samples (not run)"}
+
+
+def host_path(addr, vals, voff, n, gpu_root, reps=2):
+    """The JNI drop-in path: kh_trie_root from HOST buffers -- the addresses,
+    the packed account bodies and their offsets staged over PCIe by the library, keys hashed on
+    the GPU, the root back -- timed end to end on the wall clock (never `value`)."""
+    from khipu_amd import trie as ktrie
+    a, vb, vo = host_inputs(addr, vals, voff, n)
+    times = []
+    for _ in range(reps + 1):  # the first call also sizes the shared context's buffers
+        t0 = time.perf_counter()
+        root = ktrie.trie_root(a, (vb, vo), hash_keys=True, klen=20)
+        times.append(time.perf_counter() - t0)
+    assert root == gpu_root, "host-buffer root differs from the device-buffer root"
+    h2d = a.nbytes + vb.nbytes + vo.nbytes
+    best = min(times[1:])
+    return {"ms": round(best * 1e3, 2), "ms_all": [round(t * 1e3, 2) for t in times], "h2d_bytes": int(h2d),
+            "h2d_gb_per_s_if_all_copy": round(h2d / best / 1e9, 2), "state_root_match": True,
+            "note": "kh_trie_root over pageable host arrays (the JVM's direct buffers): PCIe staging + the build; "
+                    "not the bench value, whose inputs are already in HBM"}
+
+
+def verify(args):
+    """f3: fast-sync NodeData verification (kh_verify_nodes; NodeDatasRequest.processResponse,
+    sync/package.scala:81-165) of one peer batch: every node of a synthetic state trie of
+    --nodes-accounts accounts (kh_trie_root_nodes), requested as StateMptNodeHash, answered in
+    a shuffled order.  One step = one kh_verify_nodes call from host buffers (PCIe staging
+    included).  CPU leg: the oracle's restatement (or_verify_nodes) on one core over the same
+    batch; every output is asserted equal."""
+    import ctypes
+    import torch
+    from khipu_amd.device import Ctx
+    from khipu_amd.trie import trie_root_nodes
+    from khipu_amd._lib import check, lib
+    ctx = Ctx(0)
+    na = args.nodes_accounts
+    addr, vals, voff = ctx.synth_accounts(args.cfg, 0, na)
+    a, vb, vo = host_inputs(addr, vals, voff, na)
+    _, nodes = trie_root_nodes([a[20 * i:20 * i + 20].tobytes() for i in range(na)],
+                               [vb[vo[i]:vo[i + 1]].tobytes() for i in range(na)], hash_keys=True)
+    rng = np.random.default_rng(7)
+    hashes = list(nodes.keys())
+    order = rng.permutation(len(hashes))
+    values = [nodes[hashes[i]] for i in order]
+    n = len(values)
+    data = np.frombuffer(b"".join(values) + bytes(16), np.uint8)
+    off = np.concatenate([[0], np.cumsum([len(v) for v in values])]).astype(np.uint64)
+    req = np.frombuffer(b"".join(hashes), np.uint8)
+    kinds = np.zeros(n, np.uint8)  # StateMptNodeHash
+    hh = np.zeros((n, 32), np.uint8)
+    match = np.zeros(n, np.int64)
+    status = np.zeros(n, np.uint8)
+    coff = np.zeros(n + 1, np.uint64)
+    cap = 16 * n
+    child = np.zeros((cap, 32), np.uint8)
+    ckind = np.zeros(cap, np.uint8)
+    total = ctypes.c_uint64()
+
+    def call():  # kh_verify_nodes_packed: the children concatenated as processResponse lists them
+        check(lib().kh_verify_nodes_packed(data.ctypes.data, off.ctypes.data, n, req.ctypes.data, kinds.ctypes.data,
+                                           n, hh.ctypes.data, match.ctypes.data, status.ctypes.data,
+                                           coff.ctypes.data, child.ctypes.data, ckind.ctypes.data, cap,
+                                           ctypes.byref(total)))
+    for _ in range(args.warmup):
+        call()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        call()
+    dt = (time.perf_counter() - t0) / args.steps
+    out = {"metric": "fast-sync NodeData values verified/s (kec256 + request match + PV63 decode)", "value": n / dt,
+           "unit": "nodes/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt * 1e3,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+           "data": "synthetic (every node of a state trie of synthetic accounts, shuffled)",
+           "config": {"workload": f"{n} NodeData values ({int(off[-1])} B) of a {na}-account state trie, one "
+                                  f"kh_verify_nodes call from host buffers", "nodes": n, "bytes": int(off[-1]),
+                      "parallelism": "single GPU"},
+           "children_listed": int(total.value)}
+    assert (match >= 0).all() and (status == 0).all()
+    nchild = np.diff(coff).astype(np.uint8)
+    if not args.no_cpu:
+        from oracle import oracle
+        t1 = time.perf_counter()
+        ch, cm, cs, cn, cc, ck = oracle.verify_nodes_batch(data, off, req, kinds)
+        tc = time.perf_counter() - t1
+        assert (ch == hh).all() and (cm == match).all() and (cs == status).all() and (cn == nchild).all()
+        mask = np.arange(16)[None, :] < nchild[:, None]
+        t = int(total.value)
+        assert (cc[mask] == child[:t]).all() and (ck[mask] == ckind[:t]).all()  # row-major = concatenation order
+        out["cpu_baseline"] = {"value": n / tc, "unit": "nodes/s", "cores": 1, "kind": "port",
+                               "sample": f"the same {n} values, or_verify_nodes (NodeDatasRequest.processResponse "
+                                         f"restated, one core); every output asserted equal; CPU: {cpu_model()}",
+                               "seconds": round(tc, 3)}
+    print(json.dumps(out), flush=True)
 
 
 def cpu_batch(addr, vals, voff, n, gpu_root, threads):
@@ -241,6 +339,8 @@ def single(args):
                                        "n_node_perms", "n_key_perms", "arena_bytes", "n_levels")},
         "roofline": roof,
     }
+    if not args.no_host_path:
+        out["drop_in_host_path"] = host_path(addr, vals, voff, n, root)
     if not args.no_cpu:
         samples = [int(x) for x in args.seq_samples.split(",") if x and int(x) <= n]
         if samples:
@@ -517,6 +617,8 @@ def main():
         lists(args)
     elif args.workload == "storage":
         storage(args)
+    elif args.workload == "verify":
+        verify(args)
     elif world > 1 or args.gpus > 1 or args.sharded:
         from khipu_amd import sharded
         sharded.bench_main(args)

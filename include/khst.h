@@ -241,6 +241,15 @@ int kh_dev_hash_partition_ev(kh_ctx* ctx, void* vals_done, const uint8_t* d_keys
 int kh_verify_nodes(const uint8_t* data, const uint64_t* off, uint64_t n, const uint8_t* req32, const uint8_t* req_kind,
                     uint64_t nreq, uint8_t* hash32, int64_t* match, uint8_t* status, uint8_t* nchild, uint8_t* child32,
                     uint8_t* child_kind);
+/* The same with the children packed, as processResponse concatenates them (childHashes :::
+ * hashes): value i's children are child32[32k..) / child_kind[k] for k in
+ * [child_off[i], child_off[i+1]) (child_off has n+1 entries); *n_children = the total.  When
+ * the total exceeds child_cap (16 n always suffices) the call returns KH_ENOSPC after writing
+ * every other output, child_off and *n_children. */
+int kh_verify_nodes_packed(const uint8_t* data, const uint64_t* off, uint64_t n, const uint8_t* req32,
+                           const uint8_t* req_kind, uint64_t nreq, uint8_t* hash32, int64_t* match, uint8_t* status,
+                           uint64_t* child_off, uint8_t* child32, uint8_t* child_kind, uint64_t child_cap,
+                           uint64_t* n_children);
 
 /* ---- resident tries and forests: incremental commit ----
  * A trie kept in HBM between commits as node records found by their anchor (trie id,

@@ -33,6 +33,7 @@ EXPORTS = (
     "kh_trie_root_sharded", "kh_block_commit_host", "kh_dev_list_roots", "kh_trie_get", "kh_trie_get_host",
     "kh_dev_synth_storage", "kh_trie_roots_segmented_sharded", "kh_trie_savepoint", "kh_trie_rollback",
     "kh_trie_release", "kh_trie_savepoint_depth", "kh_trie_root_of", "kh_trie_root_of_host", "kh_trie_copy",
+    "kh_verify_nodes_packed",
 )
 
 
@@ -142,6 +143,7 @@ def lib():
     L.kh_trie_root_of.argtypes = L.kh_trie_apply.argtypes
     L.kh_trie_root_of_host.argtypes = L.kh_trie_apply_host.argtypes
     L.kh_trie_copy.argtypes = [vp, ctypes.POINTER(vp)]
+    L.kh_verify_nodes_packed.argtypes = [vp, vp, u64, vp, vp, u64, vp, vp, vp, vp, vp, vp, u64, ctypes.POINTER(u64)]
     for name in EXPORTS:
         fn = getattr(L, name)
         if fn.restype is ctypes.c_int or name not in ("kh_last_error", "kh_version"):

@@ -83,8 +83,10 @@ __global__ void __launch_bounds__(BS) k_kec_batch(const uint8_t* data, const uin
 __global__ void __launch_bounds__(BS) k_verify_nodes(const uint8_t* data, const uint64_t* off, uint64_t n,
                                                      const uint64_t* req, const uint8_t* req_kind,
                                                      const uint32_t* req_idx, uint64_t nreq, uint64_t* hash_out,
-                                                     int64_t* match, uint8_t* status, uint8_t* nchild,
+                                                     int64_t* match, uint8_t* status, uint32_t* nchild,
                                                      uint8_t* child32, uint8_t* child_kind) {
+  // req: the distinct requested hashes in key order, req_idx: the request each stands for (the
+  // last of equal hashes: requestNodeHashes.toMap, sync/package.scala:85); req_kind by request
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
   const uint64_t o = off[i];
@@ -92,16 +94,36 @@ __global__ void __launch_bounds__(BS) k_verify_nodes(const uint8_t* data, const 
   uint64_t h[4];
   kec256_msg<false>(data + o, len, h);
   for (int j = 0; j < 4; ++j) hash_out[4 * i + j] = h[j];
-  uint64_t p = key_lower_bound(req, nreq, h);
+  const uint64_t p = key_lower_bound(req, nreq, h);
   int64_t mi = -1;
   uint8_t kind = NK_NONE;
   if (p < nreq && key_cmp(req + 4 * p, h) == 0) {
-    while (p + 1 < nreq && key_cmp(req + 4 * (p + 1), h) == 0) ++p;
     mi = req_idx[p];
-    kind = req_kind[p];
+    kind = req_kind[mi];
   }
   match[i] = mi;
-  status[i] = op_node_children(data + o, len, kind, child32 + 512 * i, child_kind + 16 * i, nchild + i);
+  uint8_t nc = 0;
+  status[i] = op_node_children(data + o, len, kind, child32 + 512 * i, child_kind + 16 * i, &nc);
+  nchild[i] = nc;
+}
+__global__ void __launch_bounds__(BS) k_u32_to_u64(const uint32_t* in, uint64_t n, uint64_t* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < n) out[i] = in[i];
+}
+__global__ void k_set_last(uint64_t* dst, const uint64_t* src) { *dst = *src; }
+// the children of value i packed at coff[i] (the exclusive scan of the counts)
+__global__ void __launch_bounds__(BS) k_pack_children(const uint32_t* nchild, const uint64_t* coff, uint64_t n,
+                                                      const uint8_t* child32, const uint8_t* child_kind,
+                                                      uint8_t* out32, uint8_t* out_kind) {
+  const uint64_t g = (uint64_t)blockIdx.x * BS + threadIdx.x, i = g >> 4;
+  const uint32_t c = (uint32_t)(g & 15);  // 16 threads per value: one child each
+  if (i >= n || c >= nchild[i]) return;
+  const uint64_t d = coff[i] + c;
+  const ulonglong2* src = (const ulonglong2*)(child32 + 512 * i + 32 * c);
+  ulonglong2* dst = (ulonglong2*)(out32 + 32 * d);
+  dst[0] = src[0];
+  dst[1] = src[1];
+  out_kind[d] = child_kind[16 * i + c];
 }
 
 template <bool SHORT>
@@ -1773,6 +1795,47 @@ struct BuildInfo {  // the last build's sizes, for build_stats
   uint32_t levels = 0;
   bool full_sort = false, early = false, stage_ev = true;
 };
+// A host thread kept for a context (kh_block_commit's storage phase): post() hands it one job,
+// join() waits for the job; no thread is started per call.
+struct Worker {
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::function<void()> job;
+  bool has_job = false, stop = false;
+  void post(std::function<void()> f) {
+    std::unique_lock<std::mutex> lk(mu);
+    if (!th.joinable()) th = std::thread([this] { loop(); });
+    job = std::move(f);
+    has_job = true;
+    cv.notify_all();
+  }
+  void join() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [this] { return !has_job; });
+  }
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [this] { return has_job || stop; });
+      if (stop) return;
+      std::function<void()> f = std::move(job);
+      lk.unlock();
+      f();  // (the job catches its own exceptions)
+      lk.lock();
+      has_job = false;
+      cv.notify_all();
+    }
+  }
+  ~Worker() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    if (th.joinable()) th.join();
+  }
+};
 struct kh_ctx {
   int dev = 0;
   int n_cu = 256;  // compute units of the device
@@ -1794,6 +1857,11 @@ struct kh_ctx {
   DevBuf gws;
   kh_ctx* gsub = nullptr;
   hipEvent_t gev[18] = {};
+  // kh_block_commit: the second context its storage phase runs on, beside the account phase on
+  // this one, and the event of the storage roots' injection into the account bodies
+  kh_ctx* bsub = nullptr;
+  hipEvent_t bev = nullptr;
+  std::unique_ptr<Worker> bworker;
   // last build (for emission)
   Topo T{};
   uint64_t last_B = 0;
@@ -1833,6 +1901,7 @@ struct BuildArgs {
   bool dev_results = false;        // results and counters stay on the device (no host sync at the end)
   const GroupArgs* grp = nullptr;  // a group of a grouped build (depth0 = 1, keys = the hashed keys of all groups)
   bool no_groups = false;          // never split into a grouped build (its own fallback)
+  std::function<void()> before_leaves;  // element builds: called (host) right before the leaves are encoded
 };
 // element build (forest.h): inputs are leaves and subtree elements; the capped reference
 // of every element node, branch and extension is kept for the forest's records
@@ -2664,6 +2733,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       c->ws_list.ensure(carve_size({m * 4}));
       list = (uint32_t*)c->ws_list.p;
     }
+    if (A.before_leaves) A.before_leaves();  // (a block commit's account values arrive here)
     hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T, list, nlist);
     LAUNCH_CHECK();
     if (A.el) {  // the re-encoded elements hashed from the list
@@ -3309,24 +3379,27 @@ __global__ void __launch_bounds__(BS) k_f_ops_post(FOps O, const uint32_t* sidx,
                                                    const uint8_t* vals, const uint64_t* voff, const uint64_t* uoff,
                                                    uint64_t* uo, uint64_t nups, uint64_t total, uint8_t* heap,
                                                    uint64_t heap_base, const uint32_t* tflag, const uint32_t* tpos,
-                                                   uint32_t* tries, Elems E) {
+                                                   uint32_t* tries, Elems E, bool meta, bool copy) {
+  // meta: the trie list, the offsets by rank, the upserts' leaf elements (no value bytes read);
+  // copy: the value bytes into the heap (kh_block_commit defers it until the storage roots are
+  // injected into the account bodies)
   const uint64_t g = (uint64_t)blockIdx.x * BS + threadIdx.x;
   const uint64_t o = g / CG;
   const uint32_t sub = threadIdx.x % CG;
-  if (g == 0) {
+  if (meta && g == 0) {
     uo[nups] = total;
     *E.n = nups;
   }
   if (o >= O.n) return;
-  if (sub == 0 && tflag[o]) tries[tpos[o]] = O.trie[o];
+  if (meta && sub == 0 && tflag[o]) tries[tpos[o]] = O.trie[o];
   if (O.kind[o] != FOP_UPSERT) return;
   const uint64_t s = sidx[o];
   const uint64_t vl = voff[s + 1] - voff[s];
-  if (sub == 0) {
+  if (meta && sub == 0) {
     uo[ur[o]] = uoff[o];
     upsert_elem(O, o, ur[o], tpos[o] + tflag[o] - 1, heap_base + uoff[o], (uint32_t)vl, E);
   }
-  copy_bytes_group(heap + heap_base + uoff[o], vals + voff[s], vl, sub);
+  if (copy) copy_bytes_group(heap + heap_base + uoff[o], vals + voff[s], vl, sub);
 }
 // sorted op o: its kind, the flag of a new trie (the segments of the element build), and for
 // an upsert its rank flag and value length (the heap copy); one launch over the sorted ops.
@@ -3476,6 +3549,10 @@ __global__ void __launch_bounds__(BS) k_f_elem_recs(Topo T, Elems E, const uint3
   const uint32_t s = T.sidx[i], src = E.src[s];
   const uint64_t r = src == NONE ? base + newrank[i] : src;
   eid[i] = rein[i] ? (uint32_t)r : NONE;
+  // an element keeping its source record at the same anchor, untouched (most of them: the
+  // unchanged children of the opened branches): the record would be rewritten byte for byte
+  // (its key, anchor, references and value span are the element's, copied from it)
+  if (src != NONE && !rein[i]) return;
   RecVal v;
   for (int q = 0; q < 4; ++q) {
     v.k[q] = T.skey[4 * i + q];
@@ -3912,6 +3989,13 @@ struct FCommit {  // one commit's inputs (device buffers)
   const unsigned long long* chk = nullptr;
   unsigned long long chk_tok = 0;
   const char* chk_msg = nullptr;
+  // deferred values (kh_block_commit's account phase, run beside the storage phase): the
+  // key-only work -- hashing, sort, descent, gather -- is enqueued first; before_values (host)
+  // returns once vals_ready has been recorded (the storage roots' injection into up_vals), the
+  // stream waits on it, and only then are the values copied into the heap and `chk` read (at
+  // the gather's sync, still before the commit changes anything)
+  std::function<void()> before_values;
+  hipEvent_t vals_ready = nullptr;
 };
 
 static int emit_nodes_dev(kh_ctx* c, DevBuf& out, uint64_t* n_nodes, uint64_t* rlp_len);
@@ -3987,7 +4071,8 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   S.rs_scratch = cv.take<char>(radix_scratch_bytes(nops));
   S.scan_scratch = cv.take<char>(scan_scratch_bytes(nops + 1, 8));
   S.ctr = cv.take<unsigned long long>(CTR_N);
-  S.chk = F.chk;
+  const bool defer = (bool)F.before_values;
+  S.chk = defer ? nullptr : F.chk;
   uint8_t* kind = cv.take<uint8_t>(nops);
   uint32_t* tflag = cv.take<uint32_t>(nops);
   uint32_t* tpos = cv.take<uint32_t>(nops);
@@ -4024,7 +4109,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                      segd ? F.del_trie : nullptr, K, Tid, S.ctr);
   LAUNCH_CHECK();
   sort_dedup(c, S);
-  if (F.chk && c->h_pinned[1] == F.chk_tok) throw KhError{KH_EINVAL, F.chk_msg};
+  if (!defer && F.chk && c->h_pinned[1] == F.chk_tok) throw KhError{KH_EINVAL, F.chk_msg};
   const uint64_t nd = S.m;
   uint32_t* otrie = segd ? S.sseg : sseg;  // the compaction of duplicates moves the sorted ids
   // the descent's touched list and the commit's flags (fctr, zeroed by k_f_prep): [0] touched
@@ -4103,7 +4188,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   uint64_t ecap = carve_elems(ntl_guess);
   hipLaunchKernelGGL(k_f_ops_post, GRID(nd * CG, BS), dim3(BS), 0, st, O, (const uint32_t*)S.sidx, (const uint32_t*)ur,
                      F.up_vals, F.up_voff, (const uint64_t*)uoff, uo, (uint64_t)nups, ubytes, (uint8_t*)h->heap.p, hb,
-                     (const uint32_t*)tflag, (const uint32_t*)tpos, tries, E);
+                     (const uint32_t*)tflag, (const uint32_t*)tpos, tries, E, true, !defer);
   LAUNCH_CHECK();
   // ---- 2. descent: opened branches and touched leaves
   recs_reserve(h, h->rn + 16);
@@ -4150,6 +4235,20 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     if (c->h_pinned[2]) throw KhError{KH_EINTERNAL, "forest gather: corrupt anchor map"};
   }
   if (ne > ecap) throw KhError{KH_EINTERNAL, "forest gather: element overflow"};
+  // deferred values: once their producer is done (the host waits for its event to be recorded,
+  // the stream for the event), the values into the heap -- right before the element build's
+  // leaves read them, so the element sort and topology run beside the producer too
+  bool values_in = !defer;
+  auto values_now = [&] {
+    if (values_in) return;
+    values_in = true;
+    F.before_values();
+    if (F.vals_ready) HIPCHK(hipStreamWaitEvent(st, F.vals_ready, 0));
+    hipLaunchKernelGGL(k_f_ops_post, GRID(nd * CG, BS), dim3(BS), 0, st, O, (const uint32_t*)S.sidx,
+                       (const uint32_t*)ur, F.up_vals, F.up_voff, (const uint64_t*)uoff, uo, (uint64_t)nups, ubytes,
+                       (uint8_t*)h->heap.p, hb, (const uint32_t*)tflag, (const uint32_t*)tpos, tries, E, false, true);
+    LAUNCH_CHECK();
+  };
   h->ntl_hint = ntl;
   h->heap_n = hb + ubytes;
   HIPCHK(hipEventRecord(c->ev[7], st));
@@ -4167,11 +4266,13 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     A.vlen = E.vl;
     A.el = &EA;
     A.dev_results = true;  // the counters come back with the roots (build_stats below)
+    if (defer) A.before_leaves = values_now;
     run_build(c, A, O2, &bst);
     B = c->last_B;
     m = c->T.m;
     if (m != ne) throw KhError{KH_EINTERNAL, "forest: duplicate elements"};
   }
+  values_now();  // (no element build: the producer still finishes before the commit does)
   // ---- 5. records: new branches, re-anchored / new elements; the anchor map follows
   const uint64_t nnew = nups;  // every upsert is a new leaf record
   recs_reserve(h, h->rn + B + nnew + 16);
@@ -4192,10 +4293,12 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     js.dn = ndel_log;
     js.ipos = js.dpos + ndel_log;
     js.in = 0;  // set once the inserts are launched
+    // (the records rewritten in place: the touched ones and the element sources that move --
+    // k_f_elem_recs leaves every other source record as it is)
     const uint64_t nsave = ntl + m;
     if (nsave)
       hipLaunchKernelGGL(k_rec_save, GRID(nsave * 8, BS), dim3(BS), 0, st, (const uint8_t*)h->recs.p,
-                         (const uint32_t*)tlist, ntl, (const uint32_t*)E.src, m, (uint32_t*)h->jidx.p + js.rpos,
+                         (const uint32_t*)tlist, ntl, (const uint32_t*)esrc, m, (uint32_t*)h->jidx.p + js.rpos,
                          (uint8_t*)h->jrec.p + js.rpos * REC_BYTES);
     LAUNCH_CHECK();
     dlog = (uint64_t*)h->jmap.p + 3 * js.dpos;
@@ -4287,7 +4390,11 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   const size_t o_roots = (size_t)((char*)roots - (char*)tries), o_tail = (size_t)((char*)tail - (char*)tries);
   uint8_t* hs = pinned_stage(c, o_tail + 64);
   HIPCHK(hipMemcpyAsync(hs, tries, o_tail + 64, hipMemcpyDeviceToHost, st));
+  if (defer && F.chk) HIPCHK(hipMemcpyAsync(c->h_pinned + 8, F.chk, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  // a deferred producer's error word, read at the last sync: the commit has changed the handle
+  // by now, so the caller's savepoint takes it back (kh_block_commit always holds one)
+  if (defer && F.chk && c->h_pinned[8] == F.chk_tok) throw KhError{KH_EINVAL, F.chk_msg};
   const unsigned long long* ht = (const unsigned long long*)(hs + o_tail);
   if (count_fresh) h->mused += ht[6];
   memcpy(h->tries.data(), hs, (uint64_t)nt * 4);
@@ -4495,6 +4602,8 @@ int kh_ctx_destroy(kh_ctx* c) {
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->st);
     if (c->gsub) (void)kh_ctx_destroy(c->gsub);
+    if (c->bsub) (void)kh_ctx_destroy(c->bsub);
+    if (c->bev) (void)hipEventDestroy(c->bev);
     for (DevBuf* b : {&c->ws_inject, &c->ws_list, &c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->in_kn, &c->in_aux, &c->in_block, &c->out_emit,
                       &c->emit_dev, &c->gws})
       b->release();
@@ -5056,62 +5165,155 @@ int kh_dev_synth_accounts(kh_ctx* c, uint32_t cfg, uint64_t first, uint64_t n, u
   })
 }
 
+// NodeDatasRequest.processResponse over one batch: the values and requests staged,
+// the requests sorted and deduplicated on the device (the last of equal hashes wins), every value
+// hashed, matched and decoded by k_verify_nodes, the children packed; one host sync.  Outputs
+// through the context's pinned staging.  packed: child_off[n+1] + packed children; else the
+// 16-slot rows of kh_verify_nodes.
+static int verify_nodes_impl(const uint8_t* data, const uint64_t* off, uint64_t n, const uint8_t* req32,
+                             const uint8_t* req_kind, uint64_t nreq, uint8_t* hash32, int64_t* match, uint8_t* status,
+                             uint8_t* nchild_rows, uint8_t* child_rows, uint8_t* kind_rows, uint64_t* child_off,
+                             uint8_t* child32, uint8_t* child_kind, uint64_t child_cap, uint64_t* n_children) {
+  if (n_children) *n_children = 0;
+  if (n == 0) {
+    if (child_off) child_off[0] = 0;
+    return KH_OK;
+  }
+  if (!data || !off || (nreq && (!req32 || !req_kind))) throw KhError{KH_EINVAL, "null buffer"};
+  if (n >= (1ULL << 31) || nreq >= (1ULL << 31)) throw KhError{KH_EINVAL, "batch too large"};
+  kh_ctx* c = shared_ctx(current_device());
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  hipStream_t st = c->st;
+  const uint64_t v0 = off[0], vbytes = off[n] - v0;
+  std::vector<uint64_t> rel(off, off + n + 1);
+  for (auto& x : rel) x -= v0;
+  c->in_vals.ensure(vbytes + 64);
+  c->in_voff.ensure((n + 1) * 8 + 64);
+  const uint64_t nr = nreq ? nreq : 1;
+  c->in_keys.ensure(carve_size({32 * nr + 32, nr + 1}));
+  Carver ci{(char*)c->in_keys.p, 0, c->in_keys.cap};
+  uint64_t* dreq = ci.take<uint64_t>(4 * nr + 4);
+  uint8_t* dkind = ci.take<uint8_t>(nr + 1);
+  if (vbytes) HIPCHK(hipMemcpyAsync(c->in_vals.p, data + v0, vbytes, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c->in_voff.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+  if (nreq) {
+    HIPCHK(hipMemcpyAsync(dreq, req32, 32 * nreq, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dkind, req_kind, nreq, hipMemcpyHostToDevice, st));
+  }
+  // the requests in key order, one per distinct hash (sort_dedup: the last duplicate kept)
+  c->ws1.ensure(carve_size({nr * 8, nr * 8, nr * 4, nr * 4, nr * 32, radix_scratch_bytes(nr),
+                            scan_scratch_bytes(nr, 8), CTR_N * 8}));
+  Carver cs{(char*)c->ws1.p, 0, c->ws1.cap};
+  SortIO S{(const uint64_t*)dreq, nullptr, 0, nreq, cs.take<uint64_t>(nr), cs.take<uint64_t>(nr),
+           cs.take<uint32_t>(nr), cs.take<uint32_t>(nr), cs.take<uint64_t>(nr * 4), nullptr,
+           cs.take<char>(radix_scratch_bytes(nr)), cs.take<char>(scan_scratch_bytes(nr, 8)),
+           cs.take<unsigned long long>(CTR_N), nullptr, false};
+  uint64_t m = 0;
+  const uint64_t* skey = dreq;
+  const uint32_t* sidx = nullptr;
+  if (nreq) {
+    HIPCHK(hipMemsetAsync(S.ctr, 0, CTR_N * 8, st));
+    if (nreq == 1) {  // (nothing to sort)
+      HIPCHK(hipMemsetAsync(S.idx0, 0, 4, st));
+      m = 1;
+      sidx = S.idx0;
+    } else {
+      sort_dedup(c, S);
+      m = S.m;
+      skey = S.skey;
+      sidx = S.sidx;
+    }
+  }
+  // per value: hash, match, decode (16-slot rows), then the children packed
+  c->out_emit.ensure(carve_size({32 * n, 8 * n, n, 4 * n, 512 * n, 16 * n, 8 * (n + 1), scan_scratch_bytes(n + 1, 8),
+                                 32 * 16 * n, 16 * n, 64}));
+  Carver co{(char*)c->out_emit.p, 0, c->out_emit.cap};
+  uint64_t* dh = co.take<uint64_t>(4 * n);
+  int64_t* dm = co.take<int64_t>(n);
+  uint8_t* ds = co.take<uint8_t>(n);
+  uint32_t* dn = co.take<uint32_t>(n);
+  uint8_t* dc = co.take<uint8_t>(512 * n);
+  uint8_t* dk = co.take<uint8_t>(16 * n);
+  uint64_t* coff = co.take<uint64_t>(n + 1);
+  void* sscr = co.take<char>(scan_scratch_bytes(n + 1, 8));
+  uint8_t* pc = co.take<uint8_t>(32 * 16 * n);
+  uint8_t* pk = co.take<uint8_t>(16 * n);
+  uint64_t* tot = co.take<uint64_t>(8);
+  hipLaunchKernelGGL(k_verify_nodes, GRID(n, BS), dim3(BS), 0, st, (const uint8_t*)c->in_vals.p,
+                     (const uint64_t*)c->in_voff.p, n, skey, (const uint8_t*)dkind, sidx, m, dh, dm, ds, dn, dc, dk);
+  LAUNCH_CHECK();
+  // (counts widened: scan_exclusive sums 64-bit offsets from 32-bit counts through a copy)
+  hipLaunchKernelGGL(k_u32_to_u64, GRID(n, BS), dim3(BS), 0, st, (const uint32_t*)dn, n, coff);
+  LAUNCH_CHECK();
+  scan_exclusive<uint64_t>(coff, coff, n, tot, sscr, st);
+  hipLaunchKernelGGL(k_set_last, dim3(1), dim3(1), 0, st, coff + n, (const uint64_t*)tot);
+  hipLaunchKernelGGL(k_pack_children, GRID(16 * n, BS), dim3(BS), 0, st, (const uint32_t*)dn, (const uint64_t*)coff, n,
+                     (const uint8_t*)dc, (const uint8_t*)dk, pc, pk);
+  LAUNCH_CHECK();
+  HIPCHK(hipMemcpyAsync(c->h_pinned, tot, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint64_t total = c->h_pinned[0];
+  if (n_children) *n_children = total;
+  // outputs through pinned staging: hashes, matches, statuses, counts / offsets, children
+  const uint64_t bytes = 32 * n + 8 * n + n + 8 * (n + 1) + 4 * n + 33 * total + 64;
+  uint8_t* hs = pinned_stage(c, bytes);
+  uint8_t* hp = hs;
+  auto back = [&](void* dst, const void* src, uint64_t b) {
+    if (!dst || !b) return;
+    HIPCHK(hipMemcpyAsync(hp, src, b, hipMemcpyDeviceToHost, st));
+    hp += b;
+  };
+  uint8_t *h_hash = hp;
+  back(hash32, dh, 32 * n);
+  uint8_t* h_match = hp;
+  back(match, dm, 8 * n);
+  uint8_t* h_status = hp;
+  back(status, ds, n);
+  uint8_t* h_coff = hp;
+  back((void*)1, coff, 8 * (n + 1));
+  uint8_t* h_pc = hp;
+  back((void*)1, pc, 32 * total);
+  uint8_t* h_pk = hp;
+  back((void*)1, pk, total);
+  HIPCHK(hipStreamSynchronize(st));
+  if (hash32) memcpy(hash32, h_hash, 32 * n);
+  if (match) memcpy(match, h_match, 8 * n);
+  if (status) memcpy(status, h_status, n);
+  const uint64_t* hco = (const uint64_t*)h_coff;
+  if (child_off) {  // packed
+    memcpy(child_off, hco, 8 * (n + 1));
+    if (total > child_cap || (total && (!child32 || !child_kind)))
+      return set_err(KH_ENOSPC, "children output too small");
+    memcpy(child32, h_pc, 32 * total);
+    memcpy(child_kind, h_pk, total);
+  } else {  // the 16-slot rows of kh_verify_nodes
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint64_t a = hco[i], k = hco[i + 1] - a;
+      if (nchild_rows) nchild_rows[i] = (uint8_t)k;
+      if (k && child_rows) memcpy(child_rows + 512 * i, h_pc + 32 * a, 32 * k);
+      if (k && kind_rows) memcpy(kind_rows + 16 * i, h_pk + a, k);
+    }
+  }
+  return KH_OK;
+}
+
 int kh_verify_nodes(const uint8_t* data, const uint64_t* off, uint64_t n, const uint8_t* req32, const uint8_t* req_kind,
                     uint64_t nreq, uint8_t* hash32, int64_t* match, uint8_t* status, uint8_t* nchild, uint8_t* child32,
                     uint8_t* child_kind) {
   API_TRY({
-    if (n == 0) return KH_OK;
-    if (!data || !off || (nreq && (!req32 || !req_kind))) throw KhError{KH_EINVAL, "null buffer"};
-    kh_ctx* c = shared_ctx(current_device());
-    std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(hipSetDevice(c->dev));
-    hipStream_t st = c->st;
-    // requests sorted by hash on the host (stable: the last duplicate ends last)
-    std::vector<uint32_t> ord(nreq);
-    for (uint64_t r = 0; r < nreq; ++r) ord[r] = (uint32_t)r;
-    std::stable_sort(ord.begin(), ord.end(),
-                     [&](uint32_t a, uint32_t b) { return memcmp(req32 + 32ull * a, req32 + 32ull * b, 32) < 0; });
-    std::vector<uint8_t> rs(32 * nreq + 32), rk(nreq + 1);
-    for (uint64_t r = 0; r < nreq; ++r) {
-      memcpy(&rs[32 * r], req32 + 32ull * ord[r], 32);
-      rk[r] = req_kind[ord[r]];
-    }
-    uint64_t v0 = off[0], vbytes = off[n] - v0;
-    std::vector<uint64_t> rel(off, off + n + 1);
-    for (auto& x : rel) x -= v0;
-    c->in_vals.ensure(vbytes + 64);
-    c->in_voff.ensure((n + 1) * 8 + 64);
-    c->in_keys.ensure(carve_size({32 * nreq + 32, nreq + 1, 4 * nreq + 4}));
-    c->out_emit.ensure(carve_size({32 * n, 8 * n, n, n, 512 * n, 16 * n}));
-    Carver ci{(char*)c->in_keys.p, 0, c->in_keys.cap};
-    uint64_t* dreq = ci.take<uint64_t>(4 * nreq + 4);
-    uint8_t* dkind = ci.take<uint8_t>(nreq + 1);
-    uint32_t* didx = ci.take<uint32_t>(nreq + 1);
-    Carver co{(char*)c->out_emit.p, 0, c->out_emit.cap};
-    uint64_t* dh = co.take<uint64_t>(4 * n);
-    int64_t* dm = co.take<int64_t>(n);
-    uint8_t* ds = co.take<uint8_t>(n);
-    uint8_t* dn = co.take<uint8_t>(n);
-    uint8_t* dc = co.take<uint8_t>(512 * n);
-    uint8_t* dk = co.take<uint8_t>(16 * n);
-    if (vbytes) HIPCHK(hipMemcpyAsync(c->in_vals.p, data + v0, vbytes, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->in_voff.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-    if (nreq) {
-      HIPCHK(hipMemcpyAsync(dreq, rs.data(), 32 * nreq, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(dkind, rk.data(), nreq, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(didx, ord.data(), 4 * nreq, hipMemcpyHostToDevice, st));
-    }
-    hipLaunchKernelGGL(k_verify_nodes, GRID(n, BS), dim3(BS), 0, st, (const uint8_t*)c->in_vals.p,
-                       (const uint64_t*)c->in_voff.p, n, (const uint64_t*)dreq, (const uint8_t*)dkind,
-                       (const uint32_t*)didx, nreq, dh, dm, ds, dn, dc, dk);
-    LAUNCH_CHECK();
-    if (hash32) HIPCHK(hipMemcpyAsync(hash32, dh, 32 * n, hipMemcpyDeviceToHost, st));
-    if (match) HIPCHK(hipMemcpyAsync(match, dm, 8 * n, hipMemcpyDeviceToHost, st));
-    if (status) HIPCHK(hipMemcpyAsync(status, ds, n, hipMemcpyDeviceToHost, st));
-    if (nchild) HIPCHK(hipMemcpyAsync(nchild, dn, n, hipMemcpyDeviceToHost, st));
-    if (child32) HIPCHK(hipMemcpyAsync(child32, dc, 512 * n, hipMemcpyDeviceToHost, st));
-    if (child_kind) HIPCHK(hipMemcpyAsync(child_kind, dk, 16 * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    return verify_nodes_impl(data, off, n, req32, req_kind, nreq, hash32, match, status, nchild, child32, child_kind,
+                             nullptr, nullptr, nullptr, 0, nullptr);
+  })
+}
+int kh_verify_nodes_packed(const uint8_t* data, const uint64_t* off, uint64_t n, const uint8_t* req32,
+                           const uint8_t* req_kind, uint64_t nreq, uint8_t* hash32, int64_t* match, uint8_t* status,
+                           uint64_t* child_off, uint8_t* child32, uint8_t* child_kind, uint64_t child_cap,
+                           uint64_t* n_children) {
+  if (!child_off) return set_err(KH_EINVAL, "null child offsets");
+  API_TRY({
+    return verify_nodes_impl(data, off, n, req32, req_kind, nreq, hash32, match, status, nullptr, nullptr, nullptr,
+                             child_off, child32, child_kind, child_cap, n_children);
   })
 }
 
@@ -5523,6 +5725,21 @@ int kh_trie_copy(kh_trie* h, kh_trie** out) {
   })
 }
 
+// The storage phase of a block runs on a second context of the device (its own streams and
+// workspaces) on a host thread of its own, beside the account phase: the account keys are
+// hashed, sorted and descended, and their elements gathered, while the storage tries commit;
+// the account values are read only after the storage roots are injected into them
+// (FCommit::before_values / vals_ready).  KHST_BLOCK_OVERLAP=0 (measurement builds): one phase
+// after the other on one stream.
+#ifndef KHST_BLOCK_OVERLAP
+#define KHST_BLOCK_OVERLAP 1
+#endif
+struct CtxSwap {  // a handle's commits on another context of the same device, for a scope
+  kh_trie* h;
+  kh_ctx* old;
+  CtxSwap(kh_trie* t, kh_ctx* x) : h(t), old(t->c) { t->c = x; }
+  ~CtxSwap() { h->c = old; }
+};
 int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_trie, const uint8_t* d_s_up_keys,
                     const uint8_t* d_s_up_vals, const uint64_t* d_s_up_voff, uint64_t ns_up,
                     const uint32_t* d_s_del_trie, const uint8_t* d_s_del_keys, uint64_t ns_del, uint32_t s_klen,
@@ -5552,28 +5769,8 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     S.del_keys = d_s_del_keys;
     S.ndel = ns_del;
     S.klen = s_klen;
-    forest_commit(storage, S, &sst);
-    // 2. account.withStateRoot: the new storage roots into the account bodies
-    FCommit A;
-    const uint32_t nt = (uint32_t)storage->tries.size();
-    if (nt && na_up && d_a_up_trie) {
-      // the forest's trie list and roots are still on the device (its commit's tbuf)
-      // (the error word is never cleared: a failing call writes its own token into it)
-      if (!c->ws_inject.p) {
-        c->ws_inject.ensure(64);
-        HIPCHK(hipMemsetAsync(c->ws_inject.p, 0, 64, st));
-      }
-      unsigned long long* err = (unsigned long long*)c->ws_inject.p;
-      const unsigned long long tok = ++c->inject_tok;
-      hipLaunchKernelGGL(k_inject_roots, GRID(na_up, BS), dim3(BS), 0, st, d_a_up_vals, d_a_up_voff, d_a_up_trie,
-                         na_up, (const uint32_t*)storage->d_tries, nt, (const uint64_t*)storage->d_roots, err, tok);
-      LAUNCH_CHECK();
-      // (read back with the account commit's first sync, before it changes anything)
-      A.chk = err;
-      A.chk_tok = tok;
-      A.chk_msg = "an account upsert with a storage trie is not an account body";
-    }
     // 3. the accounts (TrieAccounts.flush, TrieAccounts.scala:22-28)
+    FCommit A;
     A.up_keys = d_a_up_keys;
     A.up_vals = d_a_up_vals;
     A.up_voff = d_a_up_voff;
@@ -5581,7 +5778,76 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     A.del_keys = d_a_del_keys;
     A.ndel = na_del;
     A.klen = a_klen;
-    forest_commit(state, A, &ast);
+    A.chk_msg = "an account upsert with a storage trie is not an account body";
+    // the injection's error word (never cleared: a failing call writes its own token into it)
+    if (!c->ws_inject.p) {
+      c->ws_inject.ensure(64);
+      HIPCHK(hipMemsetAsync(c->ws_inject.p, 0, 64, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    unsigned long long* err = (unsigned long long*)c->ws_inject.p;
+    const unsigned long long tok = ++c->inject_tok;
+    // 2. account.withStateRoot: the new storage roots into the account bodies (the forest's trie
+    // list and roots are still on the device: its commit's tbuf)
+    auto inject = [&](hipStream_t s) {
+      const uint32_t nt = (uint32_t)storage->tries.size();
+      if (!(nt && na_up && d_a_up_trie)) return false;
+      hipLaunchKernelGGL(k_inject_roots, GRID(na_up, BS), dim3(BS), 0, s, d_a_up_vals, d_a_up_voff, d_a_up_trie,
+                         na_up, (const uint32_t*)storage->d_tries, nt, (const uint64_t*)storage->d_roots, err, tok);
+      LAUNCH_CHECK();
+      return true;
+    };
+    const bool overlap = KHST_BLOCK_OVERLAP && (ns_up + ns_del) && (na_up + na_del);
+    if (!overlap) {
+      forest_commit(storage, S, &sst);
+      if (inject(st)) {  // (read back with the account commit's first sync, before it changes anything)
+        A.chk = err;
+        A.chk_tok = tok;
+      }
+      forest_commit(state, A, &ast);
+    } else {
+      if (!c->bsub) c->bsub = ctx_new(c->dev);
+      if (!c->bev) HIPCHK(hipEventCreateWithFlags(&c->bev, hipEventDisableTiming));
+      kh_ctx* aux = c->bsub;
+      std::mutex mu;
+      std::condition_variable cv;
+      bool done = false;
+      std::exception_ptr serr, aerr;
+      if (!c->bworker) c->bworker.reset(new Worker());
+      c->bworker->post([&] {
+        try {
+          HIPCHK(hipSetDevice(c->dev));
+          CtxSwap sw(storage, aux);
+          forest_commit(storage, S, &sst);
+          inject(aux->st);
+          HIPCHK(hipEventRecord(c->bev, aux->st));
+        } catch (...) {
+          serr = std::current_exception();
+        }
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          done = true;
+        }
+        cv.notify_all();
+        (void)hipStreamSynchronize(aux->st);  // nothing of the phase is left in flight
+      });
+      A.chk = err;  // (only an injection that failed writes this call's token)
+      A.chk_tok = tok;
+      A.vals_ready = c->bev;
+      A.before_values = [&] {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return done; });
+        if (serr) throw KhError{KH_EINTERNAL, "the block's storage phase failed"};
+      };
+      try {
+        forest_commit(state, A, &ast);
+      } catch (...) {
+        aerr = std::current_exception();
+      }
+      c->bworker->join();
+      if (serr) std::rethrow_exception(serr);
+      if (aerr) std::rethrow_exception(aerr);
+    }
 #if KHST_BLOCK_TXN
     txn.release();
 #endif

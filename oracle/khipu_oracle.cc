@@ -1073,4 +1073,35 @@ int or_node_children(const uint8_t* v, uint64_t len, int kind, uint8_t* out32, u
   return st;
 }
 
+// NodeDatasRequest.processResponse (sync/package.scala:81-125) over one batch, one core: kec256
+// of every value, the request it answers (requestNodeHashes.map(...).toMap: the last request of
+// equal hashes wins), and for a matched trie node its PV63 decode and child list
+// (getStateNodeChildren / getContractMptNodeChildren, :127-165).  Outputs laid out as
+// kh_verify_nodes' (include/khst.h): the CPU leg of bench.py --workload verify.
+int or_verify_nodes(const uint8_t* data, const uint64_t* off, uint64_t n, const uint8_t* req32, const uint8_t* req_kind,
+                    uint64_t nreq, uint8_t* hash32, int64_t* match, uint8_t* status, uint8_t* nchild, uint8_t* child32,
+                    uint8_t* child_kind) {
+  std::unordered_map<std::string, int64_t> req;
+  req.reserve(nreq * 2 + 1);
+  for (uint64_t r = 0; r < nreq; ++r) req[std::string((const char*)req32 + 32 * r, 32)] = (int64_t)r;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint8_t* v = data + off[i];
+    const uint64_t len = off[i + 1] - off[i];
+    uint8_t h[32];
+    keccak256_pad(v, (size_t)len, 0x01, h);
+    memcpy(hash32 + 32 * i, h, 32);
+    auto it = req.find(std::string((const char*)h, 32));
+    match[i] = it == req.end() ? -1 : it->second;
+    status[i] = 0;
+    nchild[i] = 0;
+    if (it == req.end()) continue;
+    const int kind = req_kind[it->second];
+    if (kind == 3) continue;  // EvmcodeHash: no decoding
+    uint32_t nc = 0;
+    status[i] = (uint8_t)or_node_children(v, len, kind, child32 + 512 * i, child_kind + 16 * i, &nc);
+    nchild[i] = (uint8_t)nc;
+  }
+  return 0;
+}
+
 }  // extern "C"

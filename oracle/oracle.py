@@ -62,6 +62,7 @@ def lib():
         L.or_batch_roots.argtypes = [vp, vp, u64, vp, vp, u64, vp, u64, ctypes.c_int, ctypes.c_int, vp, vp]
         L.or_batch_last_error.restype = ctypes.c_char_p
         L.or_batch_kec256.argtypes = [u8p, u64, vp]
+        L.or_verify_nodes.argtypes = [vp, vp, u64, vp, vp, u64, vp, vp, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -285,3 +286,27 @@ def node_children(value: bytes, kind: int):
     n = ctypes.c_uint32()
     st = lib().or_node_children(value, len(value), kind, out, kinds, ctypes.byref(n))
     return st, [(out.raw[32 * i:32 * i + 32], kinds.raw[i]) for i in range(n.value)]
+
+
+def verify_nodes_batch(data, off, req32, req_kind):
+    """NodeDatasRequest.processResponse over one batch on one core (or_verify_nodes): numpy
+    inputs as kh_verify_nodes takes them; returns (hash32 [n,32], match [n], status [n],
+    nchild [n], child32 [n,16,32], child_kind [n,16])."""
+    import numpy as np
+    n = len(off) - 1
+    nreq = len(req_kind)
+    data = np.ascontiguousarray(data, np.uint8)
+    off = np.ascontiguousarray(off, np.uint64)
+    req32 = np.ascontiguousarray(req32, np.uint8)
+    req_kind = np.ascontiguousarray(req_kind, np.uint8)
+    hh = np.zeros((max(n, 1), 32), np.uint8)
+    match = np.zeros(max(n, 1), np.int64)
+    status = np.zeros(max(n, 1), np.uint8)
+    nchild = np.zeros(max(n, 1), np.uint8)
+    child = np.zeros((max(n, 1), 16, 32), np.uint8)
+    ckind = np.zeros((max(n, 1), 16), np.uint8)
+    rc = lib().or_verify_nodes(data.ctypes.data, off.ctypes.data, n, req32.ctypes.data, req_kind.ctypes.data, nreq,
+                               hh.ctypes.data, match.ctypes.data, status.ctypes.data, nchild.ctypes.data,
+                               child.ctypes.data, ckind.ctypes.data)
+    assert rc == 0
+    return hh[:n], match[:n], status[:n], nchild[:n], child[:n], ckind[:n]

@@ -132,3 +132,36 @@ def test_truncated_items_reference_behaviour(oracle):
         for kind in (0, 2):
             st_o = oracle.node_children(v, kind)[0]
             assert st_o != 0 and emu.node_children(v, kind)[0] == st_o
+
+
+def test_batch_verify_matches_per_node_decode(oracle):
+    """or_verify_nodes (the CPU leg of bench.py --workload verify) equals the per-node
+    restatement: kec256 of each value, the last request of a hash wins
+    (requestNodeHashes.toMap, sync/package.scala:85), children of matched trie nodes only."""
+    import numpy as np
+    r = random.Random(4)
+    values, reqs, kinds = [], [], []
+    for name, kind, nodes in _sets(oracle):
+        for h, enc in nodes.items():
+            values.append(enc)
+            reqs.append(h)
+            kinds.append(kind)
+            if r.random() < 0.1:
+                values.append(C.mutate(r, enc))  # not requested
+    reqs.append(reqs[0])  # a duplicate request: the later kind (EvmcodeHash) wins
+    kinds.append(3)
+    data = np.frombuffer(b"".join(values) + bytes(16), np.uint8)
+    off = np.concatenate([[0], np.cumsum([len(v) for v in values])]).astype(np.uint64)
+    req = np.frombuffer(b"".join(reqs), np.uint8)
+    hh, match, status, nchild, child, ckind = oracle.verify_nodes_batch(data, off, req, np.array(kinds, np.uint8))
+    last = {h: i for i, h in enumerate(reqs)}
+    for i, v in enumerate(values):
+        h = oracle.kec256(v)
+        assert hh[i].tobytes() == h
+        assert match[i] == last.get(h, -1)
+        if match[i] < 0 or kinds[match[i]] == 3:
+            assert nchild[i] == 0 and status[i] == 0
+            continue
+        st, ch = oracle.node_children(v, kinds[match[i]])
+        assert status[i] == st
+        assert [(child[i, j].tobytes(), int(ckind[i, j])) for j in range(nchild[i])] == ch
