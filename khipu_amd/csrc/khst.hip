@@ -476,65 +476,88 @@ __global__ void __launch_bounds__(BS) k_ansv(Topo T, Pyr P, uint64_t nb) {
 __global__ void __launch_bounds__(BS) k_chain(Topo T, uint64_t nb) {
   GRID_STRIDE(b, nb) op_chain(T, b);
 }
-// The same with TOPO_ILP boundaries per thread walked in lockstep (one load per live chain
-// and step, all issued together): the same memory parallelism from a quarter of the waves,
-// which the leaf kernel beside it keeps (KHST_TOPO_ILP, with the grid cap KHST_TOPO_BPC)
-constexpr int TOPO_ILP = 4;
-__global__ void __launch_bounds__(BS) k_chain_ilp(Topo T, uint64_t nb) {
-  const uint64_t S = (uint64_t)gridDim.x * BS;
-  for (uint64_t b0 = (uint64_t)blockIdx.x * BS + threadIdx.x; b0 < nb; b0 += TOPO_ILP * S) {
-    uint64_t b[TOPO_ILP];
-    uint32_t t[TOPO_ILP], o[TOPO_ILP];
-    int64_t j[TOPO_ILP];
-    bool live[TOPO_ILP];
+// ANSV and chains tile by tile in LDS (trie_ops.h op_tile_ansv / op_tile_chain), the boundaries
+// whose answers leave the tile listed for k_ansv_list / k_chain_list; with pd, the early
+// leaves' parent-depth scatter of the tile's sorted positions too (op_pd_scatter)
+constexpr int TT_THREADS = 256;
+// a tile's listed boundaries from its per-wave ballots (one 64-bit word per 64 boundaries):
+// one wave, one global claim per list and tile
+__device__ __forceinline__ void tile_list_out(const uint64_t* mask, uint64_t t0, unsigned long long* cnt, uint32_t* list) {
+  const uint32_t lane = __lane_id();
+  const uint64_t m = mask[lane];
+  const uint32_t c = (uint32_t)__popcll(m);
+  uint32_t x = c;
 #pragma unroll
-    for (int q = 0; q < TOPO_ILP; ++q) {
-      b[q] = b0 + q * S;
-      t[q] = b[q] < nb ? T.u[b[q]] : 0;
-      j[q] = (int64_t)b[q];
-      o[q] = 0;
-      live[q] = t[q] != 0;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if ((int)lane >= o) x += y;
+  }
+  const uint32_t tot = __shfl(x, 63);
+  if (tot == 0) return;
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(cnt, (unsigned long long)tot);
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)base, 0), hi = (uint32_t)__shfl((int)(uint32_t)(base >> 32), 0);
+  uint64_t s = (((uint64_t)hi << 32) | lo) + (x - c);
+  for (uint64_t r = m; r; r &= r - 1) list[s++] = (uint32_t)(t0 + 64 * lane + (uint32_t)__ffsll((long long)r) - 1);
+}
+__global__ void __launch_bounds__(TT_THREADS) k_topo_tile(Topo T, uint64_t nb, bool pd, unsigned long long* nlist,
+                                                         uint32_t* alist, uint32_t* clist) {
+  __shared__ __align__(16) uint8_t su[TOPO_TILE + 16];
+  __shared__ __align__(16) uint8_t sl1[64 + 16];
+  __shared__ int16_t lpse[TOPO_TILE];
+  __shared__ __align__(16) uint8_t lnext[TOPO_TILE];
+  __shared__ uint8_t lrin[TOPO_TILE];
+  __shared__ uint64_t amask[TOPO_TILE / 64], cmask[TOPO_TILE / 64];
+  const uint64_t t0 = (uint64_t)blockIdx.x * TOPO_TILE;
+  const uint32_t tn = (uint32_t)(nb - t0 < TOPO_TILE ? nb - t0 : TOPO_TILE);
+  for (uint32_t w = threadIdx.x; w < TOPO_TILE / 16; w += TT_THREADS) {
+    const uint32_t o = 16 * w;
+    if (o + 16 <= tn) {
+      *(ulonglong2*)(su + o) = *(const ulonglong2*)(T.u + t0 + o);  // (u is carved 256-byte aligned)
+    } else {
+      for (uint32_t q = 0; q < 16; ++q) su[o + q] = o + q < tn ? T.u[t0 + o + q] : (uint8_t)0x7F;
     }
-    for (int step = 0; step < 16; ++step) {  // (a chain has at most 15 steps: op_chain)
-      int32_t nx[TOPO_ILP];
-#pragma unroll
-      for (int q = 0; q < TOPO_ILP; ++q) nx[q] = live[q] ? T.pse[j[q]] : -1;
-      bool any = false;
-#pragma unroll
-      for (int q = 0; q < TOPO_ILP; ++q) {
-        if (live[q]) {
-          if (nx[q] < 0) {
-            live[q] = false;
-          } else {
-            j[q] = nx[q];
-            if (++o[q] > 15) {  // impossible for a 16-ary trie: flag corruption
-              T.ctr[CTR_ERR] = 1;
-              live[q] = false;
-            }
-          }
-        }
-        any |= live[q];
-      }
-      if (!any) break;
-    }
-    uint8_t gl[TOPO_ILP];
-#pragma unroll
-    for (int q = 0; q < TOPO_ILP; ++q) gl[q] = (b[q] < nb && t[q] != 0) ? T.glast[b[q]] : 0;
-#pragma unroll
-    for (int q = 0; q < TOPO_ILP; ++q) {
-      if (b[q] >= nb) continue;
-      if (t[q] == 0) {
-        T.rep[b[q]] = NONE;
-        T.ord[b[q]] = 0;
-        T.isrep_bid[b[q]] = 0;
-        continue;
-      }
-      T.rep[b[q]] = (uint32_t)j[q];
-      T.ord[b[q]] = (uint8_t)o[q];
-      T.isrep_bid[b[q]] = (o[q] == 0) ? 1u : 0u;
-      if (gl[q]) T.gk[j[q]] = (uint8_t)(o[q] + 2);  // the group's last member: o + 2 children
+    *(ulonglong2*)(lnext + o) = ulonglong2{0, 0};
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    uint32_t mn = 0x7F;
+    for (uint32_t q = 0; q < 64; ++q) mn = min(mn, (uint32_t)su[64 * threadIdx.x + q]);
+    sl1[threadIdx.x] = (uint8_t)mn;
+  }
+  __syncthreads();
+  const TilePyr P{su, sl1, tn, (tn + 63) / 64};
+  const uint32_t wv = threadIdx.x >> 6;
+  for (uint32_t k = 0; k < TOPO_TILE / TT_THREADS; ++k) {
+    const uint32_t i = k * TT_THREADS + threadIdx.x;
+    const uint64_t m = __ballot(i < tn && op_tile_ansv(T, P, t0, i, lpse, lnext, lrin));
+    if (__lane_id() == 0) amask[k * (TT_THREADS / 64) + wv] = m;
+  }
+  __syncthreads();
+  for (uint32_t k = 0; k < TOPO_TILE / TT_THREADS; ++k) {
+    const uint32_t i = k * TT_THREADS + threadIdx.x;
+    const uint64_t m = __ballot(i < tn && op_tile_chain(T, P, t0, i, lpse, lnext, lrin));
+    if (__lane_id() == 0) cmask[k * (TT_THREADS / 64) + wv] = m;
+  }
+  __syncthreads();
+  if (wv == 0) tile_list_out(amask, t0, &nlist[0], alist);
+  if (wv == 1) tile_list_out(cmask, t0, &nlist[1], clist);
+  if (pd) {  // sorted leaves [t0, t0 + TOPO_TILE) (the last tile: through m - 1 = nb)
+    const uint64_t lend = blockIdx.x + 1 == gridDim.x ? T.m : t0 + TOPO_TILE;
+    for (uint64_t i = t0 + threadIdx.x; i < lend; i += TT_THREADS) {  // (the tile's values from LDS)
+      const uint32_t q = (uint32_t)(i - t0);
+      pd_scatter_vals(T, i, q > 0 ? su[q - 1] : i > 0 ? T.u[i - 1] : 0, q < tn ? su[q] : 0);
     }
   }
+}
+// the listed boundaries (grid-stride over the device's list count)
+__global__ void __launch_bounds__(BS) k_ansv_list(Topo T, Pyr P, const uint32_t* list, const unsigned long long* cnt) {
+  const uint64_t n = *cnt;
+  for (uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BS) op_ansv(T, P, list[i]);
+}
+__global__ void __launch_bounds__(BS) k_chain_list(Topo T, const uint32_t* list, const unsigned long long* cnt) {
+  const uint64_t n = *cnt;
+  for (uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BS) op_chain(T, list[i]);
 }
 // k_ansv with the early leaves' parent-depth scatter folded in (thread i also scatters
 // leaf i; grid over the m leaves): the leaf kernel waits for this kernel instead of a
@@ -567,83 +590,6 @@ __device__ __forceinline__ void block_add3(unsigned long long* c0, unsigned long
   }
 }
 
-// op_branch_topo with TOPO_ILP boundaries per thread, each load round issued for all of them
-// together (k_chain_ilp)
-__global__ void __launch_bounds__(BS) k_branch_topo_ilp(Topo T, uint64_t nb) {
-  const uint64_t S = (uint64_t)gridDim.x * BS;
-  unsigned long long ext = 0;
-  for (uint64_t b0 = (uint64_t)blockIdx.x * BS + threadIdx.x; b0 < nb; b0 += TOPO_ILP * S) {
-    uint64_t b[TOPO_ILP];
-    bool rep[TOPO_ILP];
-    uint32_t t[TOPO_ILP];
-#pragma unroll
-    for (int q = 0; q < TOPO_ILP; ++q) {
-      b[q] = b0 + q * S;
-      const uint64_t bb = b[q] < nb ? b[q] : 0;
-      t[q] = T.u[bb];
-      const uint32_t r = T.rep[bb];
-      rep[q] = b[q] < nb && t[q] != 0 && r == (uint32_t)b[q];
-    }
-    uint32_t j[TOPO_ILP], gk[TOPO_ILP];
-    int64_t a[TOPO_ILP], c[TOPO_ILP];
-#pragma unroll
-    for (int q = 0; q < TOPO_ILP; ++q) {
-      const uint64_t bb = rep[q] ? b[q] : 0;
-      j[q] = T.isrep_bid[bb];
-      a[q] = T.psv[bb];
-      c[q] = T.nsv[bb];
-      gk[q] = T.gk[bb];
-    }
-    // resolve_parent for every boundary at once: both sides, then the reps' branch ids
-    uint32_t va[TOPO_ILP], vc[TOPO_ILP], ra[TOPO_ILP], rc[TOPO_ILP], oa[TOPO_ILP], oc[TOPO_ILP];
-#pragma unroll
-    for (int q = 0; q < TOPO_ILP; ++q) {
-      const bool ha = rep[q] && a[q] >= 0, hc = rep[q] && c[q] >= 0;
-      const uint64_t ia = ha ? (uint64_t)a[q] : 0, ic = hc ? (uint64_t)c[q] : 0;
-      va[q] = ha ? T.u[ia] : 0;
-      vc[q] = hc ? T.u[ic] : 0;
-      ra[q] = ha ? T.rep[ia] : NONE;
-      rc[q] = hc ? T.rep[ic] : NONE;
-      oa[q] = ha ? T.ord[ia] : 0;
-      oc[q] = hc ? T.ord[ic] : 0;
-    }
-    uint32_t ba[TOPO_ILP], bc[TOPO_ILP];
-#pragma unroll
-    for (int q = 0; q < TOPO_ILP; ++q) {
-      ba[q] = (va[q] && ra[q] != NONE) ? T.isrep_bid[ra[q]] : NONE;
-      bc[q] = (vc[q] && rc[q] != NONE) ? T.isrep_bid[rc[q]] : NONE;
-    }
-#pragma unroll
-    for (int q = 0; q < TOPO_ILP; ++q) {
-      if (!rep[q]) continue;
-      Parent Pp;
-      if (va[q] == 0 && vc[q] == 0) {
-        Pp.bid = NONE;
-        Pp.pd = (int32_t)T.depth0 - 1;
-        Pp.pord = 0;
-      } else if (va[q] >= vc[q]) {
-        Pp.bid = ba[q];
-        Pp.pd = (int32_t)va[q] - 1;
-        Pp.pord = oa[q] + 1u;
-      } else {
-        Pp.bid = bc[q];
-        Pp.pd = (int32_t)vc[q] - 1;
-        Pp.pord = oc[q];
-      }
-      const uint32_t d = t[q] - 1u, e = (uint32_t)((int32_t)d - Pp.pd - 1);
-      const uint32_t jj = j[q];
-      T.br_k[jj] = gk[q];
-      T.br_depth[jj] = (uint8_t)d;
-      T.br_ext[jj] = (uint8_t)e;
-      T.br_parent[jj] = Pp.bid;
-      T.br_pord[jj] = (uint8_t)Pp.pord;
-      T.br_first[jj] = (uint32_t)(a[q] + 1);
-      if (T.br_end) T.br_end[jj] = c[q] < 0 ? (uint32_t)T.m : (uint32_t)c[q] + 1;
-      ext += e ? 1 : 0;
-    }
-  }
-  block_add3(ctr_stat(T.ctr, CTR_EXT, blockIdx.x), ext, nullptr, 0, nullptr, 0);
-}
 __global__ void __launch_bounds__(BS) k_branch_topo(Topo T, Pyr P, uint64_t nb) {
   unsigned long long ext = 0;
   GRID_STRIDE(b, nb) {
@@ -2238,6 +2184,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1, nb1,  // branch tables in key-order ids (BrTab J)
       cbound * 32, cbound * 2, links ? n * 4 : 0, links ? n * 4 : 0,  // link mode: child records, fix / long lists
       lpos ? nb1 * 4 : 0, lpos ? nb1 * 4 : 0, lpos ? n * 4 : 0,  // leaf positions: range ends (J, T), long list
+      nb1 * 4, nb1 * 4,                       // tile topology: boundaries left to the whole-array ANSV / chain
   };
   c->ws1.ensure(carve_size(sz));
   Carver cv{(char*)c->ws1.p, 0, c->ws1.cap};
@@ -2315,6 +2262,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     T.longlist = cv.take<uint32_t>(n);
     T.lpos = 1;
   }
+  uint32_t* tlist_a = cv.take<uint32_t>(nb1);
+  uint32_t* tlist_c = cv.take<uint32_t>(nb1);
   if (G) T.pdinv = G->pdinv;  // indexed by input: shared by the groups (each writes its own inputs')
   T.depth0 = A.depth0;
   T.segmented = segmented ? 1 : 0;
@@ -2444,15 +2393,14 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // 8 per CU slow the leaf kernel (18.8 ms, step 48.5).  KHST_TOPO_BPC: blocks per CU
   // (measurement switch; 0 = one thread per element).
   static const int topo_bpc = getenv("KHST_TOPO_BPC") ? atoi(getenv("KHST_TOPO_BPC")) : 4;
-  // KHST_TOPO_ILP=1 (measurement switch): k_chain / k_branch_topo walk TOPO_ILP boundaries
-  // per thread in lockstep (early builds, beside the leaf kernel)
-  static const bool topo_ilp_env = getenv("KHST_TOPO_ILP") && atoi(getenv("KHST_TOPO_ILP")) != 0;
-  const bool topo_ilp = topo_ilp_env && early;
   const uint32_t topo_cap = topo_bpc > 0 ? (uint32_t)(topo_bpc * c->n_cu) : 0u;
   auto topo_grid = [&](uint64_t cnt) {
     const uint64_t g = (cnt + BS - 1) / BS;
     return dim3((unsigned)(early && topo_cap && g > topo_cap ? topo_cap : (g ? g : 1)));
   };
+  // KHST_TOPO_TILE=0 (measurement switch, read per call): the whole-array ANSV and chain walk
+  // (k_ansv / k_ansv_pd, k_chain) instead of the tile-local ones (k_topo_tile)
+  const char* tte = getenv("KHST_TOPO_TILE");
   static const int pd_env = [] {
     const char* l = getenv("KHST_LEAF");  // measurement switch: leaves hashed in sorted order
     if (l && strcmp(l, "sorted") == 0) return 2;
@@ -2460,6 +2408,10 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     return !e ? PD_DEFAULT : strcmp(e, "ansv") == 0 ? 1 : strcmp(e, "first") == 0 ? 3 : 0;
   }();
   const int pd_mode = (early && nb > 0) ? (G ? PD_DEFAULT : pd_env) : 0;
+  // (=2: the parent-depth scatter as its own kernel after k_topo_tile; =3: the scatter first,
+  // the leaves right after it and k_topo_tile beside them)
+  const int tile_mode = (pd_mode == 0 || pd_mode == 1) ? (tte ? atoi(tte) : 1) : 0;
+  const bool topo_tile = tile_mode != 0;
   auto pdinv_skip = [&](hipStream_t s) {  // every input of the build without a record (its own inputs only)
     if (G) {
       hipLaunchKernelGGL(k_pdinv_skip, GRID(n, BS), dim3(BS), 0, s, G->list, n, T.pdinv);
@@ -2521,52 +2473,70 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
       P.nl++;
       pp += (nout + 255) & ~(uint64_t)255;
     }
-    if (P.nl > 1) {  // the levels in one launch (the last block to finish the first does the rest),
-                     // after a launch per level while the next one is too big for one block
-                     // (100M keys: level 2 has 24k entries, ~0.9 ms for a lone block)
-      int from = 1;
-      for (; from + 1 < P.nl && P.sz[from + 1] > 4 * BS; ++from) {
-        hipLaunchKernelGGL(k_pyramid, GRID(P.sz[from], BS), dim3(BS), 0, st, P, from, (unsigned int*)nullptr);
+    auto pyramid = [&] {
+      if (P.nl > 1) {  // the levels in one launch (the last block to finish the first does the rest),
+                       // after a launch per level while the next one is too big for one block
+                       // (100M keys: level 2 has 24k entries, ~0.9 ms for a lone block)
+        int from = 1;
+        for (; from + 1 < P.nl && P.sz[from + 1] > 4 * BS; ++from) {
+          hipLaunchKernelGGL(k_pyramid, GRID(P.sz[from], BS), dim3(BS), 0, st, P, from, (unsigned int*)nullptr);
+          LAUNCH_CHECK();
+        }
+        hipLaunchKernelGGL(k_pyramid, GRID(P.sz[from], BS), dim3(BS), 0, st, P, from, (unsigned int*)(ctr + CTR_PYR));
         LAUNCH_CHECK();
       }
-      hipLaunchKernelGGL(k_pyramid, GRID(P.sz[from], BS), dim3(BS), 0, st, P, from, (unsigned int*)(ctr + CTR_PYR));
-      LAUNCH_CHECK();
-    }
+    };
     HIPCHK(hipMemsetAsync(T.glast, 1, (nb + 15) & ~(uint64_t)15, st));  // (whole 16-byte words: one fill kernel)
-    if (pd_mode == 2) {  // the leaves need only u: they start here, beside the whole topology
-      HIPCHK(hipEventRecord(c->ev[8], st));
-      HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
-      if (A.vals_ready) HIPCHK(hipStreamWaitEvent(c->st2, A.vals_ready, 0));
-      HIPCHK(hipEventRecord(c->ev[9], c->st2));
-      hipLaunchKernelGGL(k_leaf_sorted, GRID(m, BS), dim3(BS), 0, c->st2, T, n);
+    if (topo_tile) {
+      // ANSV and chains tile by tile in LDS (k_topo_tile, the early leaves' parent depths with
+      // them); the leaves start right after it; the few boundaries whose answers leave their
+      // tile (k_ansv_list / k_chain_list over the whole pyramid) run beside the leaves
+      unsigned long long* tcnt = ctr + CTR_TLIST;
+      if (pd_mode == 1 && tile_mode == 3) {
+        hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, st, T);
+        LAUNCH_CHECK();
+        launch_leaves(false);
+      }
+      hipLaunchKernelGGL(k_topo_tile, dim3((unsigned)((nb + TOPO_TILE - 1) / TOPO_TILE)), dim3(TT_THREADS), 0, st, T,
+                         nb, pd_mode == 1 && tile_mode == 1, tcnt, tlist_a, tlist_c);
       LAUNCH_CHECK();
-      HIPCHK(hipEventRecord(c->ev[10], c->st2));
-    }
-    static const uint32_t pd_chunks = getenv("KHST_PD_CHUNKS") ? (uint32_t)atoi(getenv("KHST_PD_CHUNKS")) : 1u;
-    if (pd_mode == 3) {  // KHST_PD=first: the scatter alone on st, then the leaves; the plain
-                         // ANSV runs beside them on st
-      hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, st, T);
-      LAUNCH_CHECK();
-      launch_leaves(false);
-    }
-    if (pd_mode == 1 && pd_chunks <= 1)
-      hipLaunchKernelGGL(k_ansv_pd, GRID(m, BS), dim3(BS), 0, st, T, P, nb);
-    else
-      hipLaunchKernelGGL(k_ansv, GRID(nb, BS), dim3(BS), 0, st, T, P, nb);
-    LAUNCH_CHECK();
-    if (pd_mode == 1 && pd_chunks > 1) {
-      const uint64_t step = (n + pd_chunks - 1) / pd_chunks;
-      for (uint64_t lo = 0; lo < n; lo += step) {
-        hipLaunchKernelGGL(k_pd_scatter_rng, GRID(m, BS), dim3(BS), 0, st, T, lo, lo + step);
+      if (pd_mode == 1 && tile_mode == 2) {
+        hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, st, T);
         LAUNCH_CHECK();
       }
-    }
-    if (pd_mode == 1) launch_leaves(false);
-    if (topo_ilp)
-      hipLaunchKernelGGL(k_chain_ilp, topo_grid(nb), dim3(BS), 0, st, T, nb);
-    else
+      if (pd_mode == 1 && tile_mode != 3) launch_leaves(false);
+      pyramid();
+      hipLaunchKernelGGL(k_ansv_list, topo_grid(nb / 16 + 1), dim3(BS), 0, st, T, P, (const uint32_t*)tlist_a,
+                         (const unsigned long long*)tcnt);
+      hipLaunchKernelGGL(k_chain_list, topo_grid(nb / 16 + 1), dim3(BS), 0, st, T, (const uint32_t*)tlist_c,
+                         (const unsigned long long*)(tcnt + 1));
+      LAUNCH_CHECK();
+    } else {
+      pyramid();
+      if (pd_mode == 2) {  // the leaves need only u: they start here, beside the whole topology
+        HIPCHK(hipEventRecord(c->ev[8], st));
+        HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
+        if (A.vals_ready) HIPCHK(hipStreamWaitEvent(c->st2, A.vals_ready, 0));
+        HIPCHK(hipEventRecord(c->ev[9], c->st2));
+        hipLaunchKernelGGL(k_leaf_sorted, GRID(m, BS), dim3(BS), 0, c->st2, T, n);
+        LAUNCH_CHECK();
+        HIPCHK(hipEventRecord(c->ev[10], c->st2));
+      }
+      if (pd_mode == 3) {  // KHST_PD=first: the scatter alone on st, then the leaves; the plain
+                           // ANSV runs beside them on st
+        hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, st, T);
+        LAUNCH_CHECK();
+        launch_leaves(false);
+      }
+      if (pd_mode == 1)
+        hipLaunchKernelGGL(k_ansv_pd, GRID(m, BS), dim3(BS), 0, st, T, P, nb);
+      else
+        hipLaunchKernelGGL(k_ansv, GRID(nb, BS), dim3(BS), 0, st, T, P, nb);
+      LAUNCH_CHECK();
+      if (pd_mode == 1) launch_leaves(false);
       hipLaunchKernelGGL(k_chain, topo_grid(nb), dim3(BS), 0, st, T, nb);
-    LAUNCH_CHECK();
+      LAUNCH_CHECK();
+    }
     scan_exclusive<uint32_t>(T.isrep_bid, T.isrep_bid, nb, Bp, scan_scratch, st);
     // branch tables in key-order ids first (k_branch_topo writes them, thread per boundary)
     Topo TJ = T;
@@ -2577,10 +2547,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     TJ.br_ext = J.ext;
     TJ.br_pord = J.pord;
     TJ.br_end = J.end;
-    if (topo_ilp)
-      hipLaunchKernelGGL(k_branch_topo_ilp, topo_grid(nb), dim3(BS), 0, st, TJ, nb);
-    else
-      hipLaunchKernelGGL(k_branch_topo, topo_grid(nb), dim3(BS), 0, st, TJ, P, nb);
+    hipLaunchKernelGGL(k_branch_topo, topo_grid(nb), dim3(BS), 0, st, TJ, P, nb);
     LAUNCH_CHECK();
     // level order (grids sized by nb; threads past B exit), then every branch id
     // becomes its level position

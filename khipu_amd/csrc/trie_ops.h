@@ -269,6 +269,7 @@ constexpr int CTR_SHARDS = 64;
 constexpr int CTR_LONGN = 16 + 7;  // longlist length (row 1, index 7: unused by the stat shards)
 constexpr int CTR_PYR = 16 + 8;    // k_pyramid's finished-block count (row 1, index 8)
 constexpr int CTR_LIST = 16 + 9;   // element builds: the re-encoded leaves listed by k_leaf_prep
+constexpr int CTR_TLIST = 16 + 10; // k_topo_tile's two list lengths (row 1, indices 10 and 11)
 // counter add returning the old value (the host replay is single-threaded)
 KH_HD unsigned long long ctr_add(unsigned long long* p, unsigned long long v) {
 #ifdef __HIP_DEVICE_COMPILE__
@@ -519,6 +520,112 @@ KH_HD void op_chain(const Topo& T, uint64_t b) {
   T.ord[b] = (uint8_t)o;
   T.isrep_bid[b] = (o == 0) ? 1u : 0u;
   if (T.glast[b]) T.gk[j] = (uint8_t)(o + 2);  // the group's last member: the branch has o + 2 children
+}
+
+// ---- stage: ANSV and chains tile by tile (k_topo_tile).  op_ansv / op_chain above take one
+// dependent HBM round trip per pyramid level and per chain step for every boundary.  Here a
+// workgroup holds a tile of consecutive boundaries in LDS (with its own 64-ary level) and
+// answers every query whose answer lies in the tile.  Listed for op_ansv / op_chain over the
+// whole array: the boundaries with no smaller-or-equal one before them in the tile (the tile's
+// prefix minima), the representatives whose next strictly smaller boundary lies past it, and
+// the members whose chain passes such a boundary or that have no later member in the tile
+// while their group's range leaves it.  A link op_ansv makes across tiles always ends at a
+// listed boundary, so the global pass sees the same links op_ansv / op_chain would: the
+// results are theirs on every boundary (tests/test_emu.py checks it with tiles of 1..4096).
+// The tile's two levels (its tn values and the mins of 64 of them) are a fixed-shape TilePyr:
+// a Pyr indexed by level would live in scratch memory.
+struct TilePyr {
+  const uint8_t* l0;
+  const uint8_t* l1;
+  uint32_t sz0, sz1;
+};
+// ansv_left / ansv_right over the two levels
+KH_HD int64_t tile_left(const TilePyr& P, uint32_t b, uint32_t t) {
+  int64_t f = scan_left(P.l0, P.sz0, b & ~63u, b, t);
+  if (f >= 0) return f;
+  f = scan_left(P.l1, P.sz1, 0, b >> 6, t);
+  if (f < 0) return -1;
+  const uint32_t lo = (uint32_t)f * 64, hi = lo + 64 < P.sz0 ? lo + 64 : P.sz0;
+  return scan_left(P.l0, P.sz0, lo, hi, t);
+}
+KH_HD int64_t tile_right(const TilePyr& P, uint32_t b, uint32_t t) {
+  const uint32_t end = (b | 63u) + 1 < P.sz0 ? (b | 63u) + 1 : P.sz0;
+  int64_t f = scan_right(P.l0, P.sz0, b + 1, end, t);
+  if (f >= 0) return f;
+  f = scan_right(P.l1, P.sz1, (b >> 6) + 1, P.sz1, t);
+  if (f < 0) return -1;
+  const uint32_t lo = (uint32_t)f * 64, hi = lo + 64 < P.sz0 ? lo + 64 : P.sz0;
+  return scan_right(P.l0, P.sz0, lo, hi, t);
+}
+constexpr uint32_t TOPO_TILE = 4096;
+constexpr int16_t LP_OPEN = -2;  // lpse: the link leaves the tile
+// phase 1, tile boundary i (global t0 + i): local ANSV; returns true when op_ansv must redo it.
+// lnext[j] = 1 marks j as having a later member of its group in the tile (zeroed before the
+// phase); lrin[i] = 1 marks a representative whose next strictly smaller boundary is in it.
+KH_HD bool op_tile_ansv(const Topo& T, const TilePyr& P, uint64_t t0, uint32_t i, int16_t* lpse, uint8_t* lnext,
+                        uint8_t* lrin) {
+  const uint64_t b = t0 + i;
+  const uint32_t t = P.l0[i];
+  if (t == 0) {
+    T.psv[b] = T.nsv[b] = T.pse[b] = -1;
+    lpse[i] = -1;
+    return false;
+  }
+  const int64_t j = tile_left(P, i, t + 1);  // previous smaller-or-equal in the tile
+  if (j < 0) {
+    lpse[i] = LP_OPEN;
+    return true;
+  }
+  if (P.l0[j] == t) {  // the previous member of b's group
+    lpse[i] = (int16_t)j;
+    lnext[j] = 1;
+    T.pse[b] = (int32_t)(t0 + j);
+    T.glast[t0 + j] = 0;
+    return false;
+  }
+  // the group's first member: its range ends at the next strictly smaller boundary
+  lpse[i] = -1;
+  T.pse[b] = -1;
+  T.psv[b] = (int32_t)(t0 + j);
+  const int64_t q = tile_right(P, i, t);
+  if (q < 0) {
+    lrin[i] = 0;
+    return true;  // beyond the tile
+  }
+  T.nsv[b] = (int32_t)(t0 + q);
+  lrin[i] = 1;
+  return false;
+}
+// phase 2 (after phase 1 on the whole tile): the chain walk over the tile's links; returns true
+// when op_chain must redo it: the walk leaves the tile, or b has no later member in the tile
+// while its group's range does (it may be the group's last or not)
+KH_HD bool op_tile_chain(const Topo& T, const TilePyr& P, uint64_t t0, uint32_t i, const int16_t* lpse,
+                         const uint8_t* lnext, const uint8_t* lrin) {
+  const uint64_t b = t0 + i;
+  if (P.l0[i] == 0) {
+    T.rep[b] = NONE;
+    T.ord[b] = 0;
+    T.isrep_bid[b] = 0;
+    return false;
+  }
+  uint32_t j = i, o = 0;
+  for (;;) {
+    const int16_t p = lpse[j];
+    if (p == LP_OPEN) return true;
+    if (p < 0) break;
+    j = (uint32_t)p;
+    if (++o > 15) {  // impossible for a 16-ary trie: flag corruption
+      T.ctr[CTR_ERR] = 1;
+      break;
+    }
+  }
+  const bool last = !lnext[i];
+  if (last && !lrin[j]) return true;
+  T.rep[b] = (uint32_t)(t0 + j);
+  T.ord[b] = (uint8_t)o;
+  T.isrep_bid[b] = o == 0 ? 1u : 0u;
+  if (last) T.gk[t0 + j] = (uint8_t)(o + 2);  // the group's last member: o + 2 children
+  return false;
 }
 
 // parent resolution for a node whose key range is [s, e]: boundaries s-1 and e

@@ -8,6 +8,8 @@
 // never calls it; the GPU parity tests (tests/test_gpu_parity.py) exercise the
 // real kernels.
 #include <algorithm>
+#include <array>
+#include <random>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -23,6 +25,34 @@ using namespace khst;
 // which form of the early leaf kernel the replay runs: 0 / 1 = op_leaf_in3 with the
 // loosest / the lane's own wave bounds, 2 = op_leaf_in (KHST_LEAF=v2), 3 = op_leaf_sorted
 // (KHST_LEAF=sorted) with the loosest bounds
+// The device's tile-local topology (khst.hip k_topo_tile, then k_ansv_list / k_chain_list
+// after the whole-array pyramid P) replayed tile by tile with tiles of `tile` boundaries
+static void topo_tiles(const Topo& T, const Pyr& P, uint64_t nb, uint32_t tile) {
+  std::vector<uint32_t> alist, clist;
+  std::vector<uint8_t> su(TOPO_TILE + 16), sl1(64 + 16);
+  std::vector<int16_t> lpse(TOPO_TILE);
+  std::vector<uint8_t> lnext(TOPO_TILE), lrin(TOPO_TILE);
+  for (uint64_t t0 = 0; t0 < nb; t0 += tile) {
+    const uint32_t tn = (uint32_t)(nb - t0 < tile ? nb - t0 : tile);
+    std::fill(su.begin(), su.end(), (uint8_t)0x7F);
+    memcpy(su.data(), T.u + t0, tn);
+    std::fill(lnext.begin(), lnext.end(), (uint8_t)0);
+    std::fill(lrin.begin(), lrin.end(), (uint8_t)0x5A);  // (set by phase 1 wherever phase 2 reads it)
+    for (uint32_t w = 0; w < 64; ++w) {
+      uint32_t mn = 0x7F;
+      for (uint32_t q = 0; q < 64 && 64 * w + q < TOPO_TILE; ++q) mn = std::min(mn, (uint32_t)su[64 * w + q]);
+      sl1[w] = (uint8_t)mn;
+    }
+    const TilePyr L{su.data(), sl1.data(), tn, (tn + 63) / 64};
+    for (uint32_t i = 0; i < tn; ++i)
+      if (op_tile_ansv(T, L, t0, i, lpse.data(), lnext.data(), lrin.data())) alist.push_back((uint32_t)(t0 + i));
+    for (uint32_t i = 0; i < tn; ++i)
+      if (op_tile_chain(T, L, t0, i, lpse.data(), lnext.data(), lrin.data())) clist.push_back((uint32_t)(t0 + i));
+  }
+  for (uint32_t b : alist) op_ansv(T, P, b);
+  for (uint32_t b : clist) op_chain(T, b);
+}
+
 static int g_leaf_mode = 0;
 // 1: the leaves' child records as links (op_leaf_link_rec, KHST_LEAF_LINKS=1) with the
 // post-join fix pass and op_branch_stream on every branch; 0: link slots + the copy pass
@@ -160,8 +190,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       P.sz[P.nl] = nout;
       P.nl++;
     }
-    for (uint64_t b = 0; b < nb; ++b) op_ansv(T, P, b);
-    for (uint64_t b = 0; b < nb; ++b) op_chain(T, b);
+    topo_tiles(T, P, nb, TOPO_TILE);  // (as on the device)
     if (ctr[CTR_ERR]) return -5;
     uint32_t run = 0;
     for (uint64_t b = 0; b < nb; ++b) {
@@ -441,6 +470,82 @@ int emu_fold16(const uint8_t* hash32x16, const uint32_t* len16, const uint8_t* i
 }
 
 }  // extern "C"
+
+// The tile-local topology (topo_tiles: op_tile_ansv / op_tile_chain + the listed boundaries)
+// against op_ansv + op_chain on every boundary, with small and full tiles, on the boundary
+// values of sorted distinct keys (deep and shallow tries, segment breaks).  Returns 0 if
+// pse, psv / nsv of the representatives, rep, ord, isrep, glast and gk all agree.
+extern "C" int emu_topo_tile_check(uint64_t seed, int iters) {
+  std::mt19937_64 r(seed);
+  const uint32_t tiles[] = {1, 7, 16, 64, 100, 1000, TOPO_TILE};
+  for (int it = 0; it < iters; ++it) {
+    const uint64_t n = 2 + r() % 20000;
+    const int mode = it % 3;
+    std::vector<std::array<uint8_t, 24>> keys(n);
+    for (auto& k : keys)
+      for (int d = 0; d < 24; ++d)  // mode 0: uniform nibbles; 1: narrow alphabets (deep); 2: mixed
+        k[d] = (uint8_t)(mode == 0 ? r() % 16 : mode == 1 ? r() % (d < 8 ? 2 : 16) : r() % (1 + (d * 7 + r() % 3) % 16));
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    const uint64_t nb = keys.size() - 1;
+    if (nb == 0) continue;
+    std::vector<uint8_t> u(nb + 16);
+    for (uint64_t b = 0; b < nb; ++b) {
+      int d = 0;
+      while (d < 24 && keys[b][d] == keys[b + 1][d]) ++d;
+      u[b] = (uint8_t)(d + 1);
+      if (mode == 2 && r() % 500 == 0) u[b] = 0;  // a segment break
+    }
+    std::vector<std::vector<uint8_t>> lv;
+    lv.reserve(8);
+    Pyr P{};
+    P.lv[0] = u.data();
+    P.sz[0] = nb;
+    P.nl = 1;
+    while (P.sz[P.nl - 1] > 64) {
+      uint64_t nin = P.sz[P.nl - 1], nout = (nin + 63) / 64;
+      lv.emplace_back(nout + 16);
+      for (uint64_t i = 0; i < nout; ++i) op_min64(P.lv[P.nl - 1], nin, lv.back().data(), i);
+      P.lv[P.nl] = lv.back().data();
+      P.sz[P.nl] = nout;
+      P.nl++;
+    }
+    struct Arr {
+      std::vector<int32_t> psv, nsv, pse;
+      std::vector<uint32_t> rep, isrep;
+      std::vector<uint8_t> ord, glast, gk;
+      std::vector<unsigned long long> ctr;
+      Topo T{};
+      Arr(uint64_t nb, uint8_t* u)
+          : psv(nb, 7), nsv(nb, 7), pse(nb, 7), rep(nb, 7), isrep(nb, 7), ord(nb, 7), glast(nb, 1), gk(nb, 0),
+            ctr(CTR_N * CTR_SHARDS, 0) {
+        T.u = u;
+        T.psv = psv.data();
+        T.nsv = nsv.data();
+        T.pse = pse.data();
+        T.rep = rep.data();
+        T.isrep_bid = isrep.data();
+        T.ord = ord.data();
+        T.glast = glast.data();
+        T.gk = gk.data();
+        T.ctr = ctr.data();
+      }
+    };
+    Arr G(nb, u.data()), L(nb, u.data());
+    for (uint64_t b = 0; b < nb; ++b) op_ansv(G.T, P, b);
+    for (uint64_t b = 0; b < nb; ++b) op_chain(G.T, b);
+    topo_tiles(L.T, P, nb, tiles[it % 7]);
+    if (G.ctr[CTR_ERR] || L.ctr[CTR_ERR]) return 1;
+    for (uint64_t b = 0; b < nb; ++b) {
+      if (u[b] == 0) continue;
+      if (G.pse[b] != L.pse[b]) return 2;
+      if (G.rep[b] != L.rep[b] || G.ord[b] != L.ord[b] || G.isrep[b] != L.isrep[b]) return 3;
+      if (G.glast[b] != L.glast[b]) return 4;
+      if (G.rep[b] == b && (G.psv[b] != L.psv[b] || G.nsv[b] != L.nsv[b] || G.gk[b] != L.gk[b])) return 5;
+    }
+  }
+  return 0;
+}
 
 // Brute-force check of the pyramid + SWAR nearest-smaller-value searches (trie_ops.h)
 // against their naive definitions on random, shallow and almost-flat value arrays.

@@ -111,6 +111,17 @@ def test_nearest_smaller_value_searches():
     assert L.emu_ansv_check(7, 150) == 0
 
 
+def test_tile_topology_matches_whole_array():
+    """k_topo_tile (op_tile_ansv / op_tile_chain per tile, the listed boundaries through
+    op_ansv / op_chain after it) == op_ansv + op_chain on every boundary: tiles of 1..4096
+    boundaries over the boundary values of sorted random keys (uniform, deep, with segment
+    breaks).  The emulated builds above run the same tile replay."""
+    import ctypes
+    L = E.lib()
+    L.emu_topo_tile_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    assert L.emu_topo_tile_check(11, 84) == 0
+
+
 def test_lane_spread_keccak():
     """keccak_xlane.h (the N1 small-level permutation: 25 lanes per state, two LDS steps per
     round), replayed lane by lane, == keccak.h's one-thread Keccak-f[1600] (which the oracle
