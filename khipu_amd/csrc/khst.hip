@@ -798,15 +798,6 @@ __global__ void __launch_bounds__(BS) k_pd_scatter(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i < T.m) op_pd_scatter(T, i);
 }
-// The same scatter restricted to the inputs [lo, hi) (KHST_PD_CHUNKS=c, measurement switch:
-// c launches after a plain k_ansv, each scattering into a 1/c slice of pdinv, so that the
-// partial-line writes of one launch may merge in the memory-side cache)
-__global__ void __launch_bounds__(BS) k_pd_scatter_rng(Topo T, uint64_t lo, uint64_t hi) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i >= T.m) return;
-  const uint64_t t = T.sidx ? T.sidx[i] : i;
-  if (t >= lo && t < hi) op_pd_scatter(T, i);
-}
 // Round-2 form (KHST_LEAF=v2, measurement switch): every load up front at addresses that
 // do not depend on the parent depth, the message moved into place by 64-bit byte funnels
 // and word-select networks.  82 VGPRs, 5 waves per SIMD; 5,472 VALU instructions per wave
@@ -1961,7 +1952,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
     const bool flip = radix_sort_pairs<uint32_t>(c0, idx0, c1, idx1, n, 0, 32, rs_scratch, st);
     uint32_t* c32 = flip ? c1 : c0;
     idxs = flip ? idx1 : idx0;
-    static const bool tie_one = getenv("KHST_TIE_ONE") != nullptr;  // measurement switch
+    const bool tie_one = getenv("KHST_TIE_ONE") != nullptr;  // measurement switch
     if (tie_one) {
       hipLaunchKernelGGL(k_tie_fix_ck, GRID(n, BS), dim3(BS), 0, st, c32, idxs, n, (const uint64_t*)K32,
                          T.ctr + CTR_TIE);
@@ -2137,8 +2128,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // at 100M, 50.9 ms against 43.5 (profiles/r3j_leaf_links_ab_100m.json): 100M scattered
   // 10-byte record writes cost the topology stream 10 ms beside the leaf kernel.
   // Other switches: KHST_PUBLISH_ONE (one publish pass after the join), KHST_BRANCH=coop|rescan.
-  static const bool split_publish = !getenv("KHST_PUBLISH_ONE");
-  static const bool leaf_move = !getenv("KHST_LEAF_LINKS") || strcmp(getenv("KHST_LEAF_LINKS"), "1") != 0;
+  const bool split_publish = !getenv("KHST_PUBLISH_ONE");
+  const bool leaf_move = !getenv("KHST_LEAF_LINKS") || strcmp(getenv("KHST_LEAF_LINKS"), "1") != 0;
   const char* bv = getenv("KHST_BRANCH");
   const bool coop = bv && strcmp(bv, "coop") == 0 && !A.kn;  // (the coop assembly has no branch values)
   const bool rescan = bv && strcmp(bv, "rescan") == 0;          // op_branch_direct
@@ -2147,7 +2138,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // Leaf positions (trie_ops.h Topo::lpos; unsegmented plain root builds): no leaf child
   // records at all -- the branch kernels read each leaf child's stash at its sorted position.
   // KHST_LEAF_POS=0 (measurement switch): the copy pass k_leaf_move instead.
-  static const bool leaf_pos_env = !getenv("KHST_LEAF_POS") || atoi(getenv("KHST_LEAF_POS")) != 0;
+  const bool leaf_pos_env = !getenv("KHST_LEAF_POS") || atoi(getenv("KHST_LEAF_POS")) != 0;
   // (not with the round-2 leaf kernel, KHST_LEAF=v2, which does not publish a top leaf)
   const bool leaf_v2_env = getenv("KHST_LEAF") && !strcmp(getenv("KHST_LEAF"), "v2");
   const bool lpos =
@@ -2285,7 +2276,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // beside the segment id keep runs of equal words short (the block-local tie fix orders
   // them; one longer than TIE_RUN_MAX falls back to the full sort): at most one key per
   // four word values on average.  KHST_SEG_CK=0: the 64-bit composite sort (measurement switch).
-  static const bool seg_ck = !getenv("KHST_SEG_CK") || strcmp(getenv("KHST_SEG_CK"), "0") != 0;
+  const bool seg_ck = !getenv("KHST_SEG_CK") || strcmp(getenv("KHST_SEG_CK"), "0") != 0;
   const bool seg_words_ok = segmented && sb + CK_KEY_BITS <= 32 && (n / A.nseg) <= (1ULL << (32 - sb - 2));
   const bool ck_path = early && !A.kn && (!segmented || (seg_ck && seg_words_ok));
   const bool ck_ready = ck_path && ((A.flags & KH_HASH_KEYS) || G);
@@ -2392,7 +2383,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // (one thread per element); 2 blocks per CU starve the topology (23.7 ms, step 49.2),
   // 8 per CU slow the leaf kernel (18.8 ms, step 48.5).  KHST_TOPO_BPC: blocks per CU
   // (measurement switch; 0 = one thread per element).
-  static const int topo_bpc = getenv("KHST_TOPO_BPC") ? atoi(getenv("KHST_TOPO_BPC")) : 4;
+  const int topo_bpc = getenv("KHST_TOPO_BPC") ? atoi(getenv("KHST_TOPO_BPC")) : 4;
   const uint32_t topo_cap = topo_bpc > 0 ? (uint32_t)(topo_bpc * c->n_cu) : 0u;
   auto topo_grid = [&](uint64_t cnt) {
     const uint64_t g = (cnt + BS - 1) / BS;
@@ -2401,7 +2392,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // KHST_TOPO_TILE=0 (measurement switch, read per call): the whole-array ANSV and chain walk
   // (k_ansv / k_ansv_pd, k_chain) instead of the tile-local ones (k_topo_tile)
   const char* tte = getenv("KHST_TOPO_TILE");
-  static const int pd_env = [] {
+  const int pd_env = [] {
     const char* l = getenv("KHST_LEAF");  // measurement switch: leaves hashed in sorted order
     if (l && strcmp(l, "sorted") == 0) return 2;
     const char* e = getenv("KHST_PD");  // measurement switch
@@ -2449,7 +2440,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     }
     if (A.vals_ready) HIPCHK(hipStreamWaitEvent(s2, A.vals_ready, 0));  // the topology need not wait
     HIPCHK(hipEventRecord(c->ev[9], s2));
-    static const bool leaf_v2 = getenv("KHST_LEAF") && !strcmp(getenv("KHST_LEAF"), "v2");  // measurement switch
+    const bool leaf_v2 = getenv("KHST_LEAF") && !strcmp(getenv("KHST_LEAF"), "v2");  // measurement switch
     if (G)
       hipLaunchKernelGGL(k_leaf_in_list, GRID(n, BS), dim3(BS), 0, s2, T, G->list, n, G->n_all);
     else if (leaf_v2)
@@ -2652,7 +2643,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   // it takes off the join (branch levels 7.76 -> 8.9 ms), so it stays off.
   uint32_t move_d = 0;
   {
-    static const bool msplit = getenv("KHST_MOVE_SPLIT") && atoi(getenv("KHST_MOVE_SPLIT")) != 0;
+    const bool msplit = getenv("KHST_MOVE_SPLIT") && atoi(getenv("KHST_MOVE_SPLIT")) != 0;
     if (early && split_publish && !links && !lpos && msplit && m >= (1u << 18) && nb > 0) {
       uint32_t best = 0, dbest = 0;
       for (uint32_t d = 0; d < 64; ++d)
@@ -2718,14 +2709,14 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   uint32_t levels = 0;
   // N1 variant: one thread per branch assembling its own window (default) or the
   // wave-cooperative DPP assembly (KHST_BRANCH=coop; DESIGN.md §5 has the measurement)
-  static const bool branch_bs64 = getenv("KHST_BRANCH_BS") && atoi(getenv("KHST_BRANCH_BS")) == 64;
+  const bool branch_bs64 = getenv("KHST_BRANCH_BS") && atoi(getenv("KHST_BRANCH_BS")) == 64;
   // levels of at most XL_LEVEL branches: k_branch_xl (32 lanes per branch, the permutation
   // spread over them); of at most SMALL_LEVEL: k_branch_small (every child record loaded at
   // once); KHST_BRANCH_SMALL=0 (measurement switch) keeps them all on k_branch_fused
-  static const bool small_levels = !getenv("KHST_BRANCH_SMALL") || atoi(getenv("KHST_BRANCH_SMALL")) != 0;
+  const bool small_levels = !getenv("KHST_BRANCH_SMALL") || atoi(getenv("KHST_BRANCH_SMALL")) != 0;
   // (measurement switches: the level sizes below which the two small-level kernels run)
-  static const uint32_t xl_level = getenv("KHST_XL_LEVEL") ? (uint32_t)atoi(getenv("KHST_XL_LEVEL")) : XL_LEVEL;
-  static const uint32_t small_level =
+  const uint32_t xl_level = getenv("KHST_XL_LEVEL") ? (uint32_t)atoi(getenv("KHST_XL_LEVEL")) : XL_LEVEL;
+  const uint32_t small_level =
       getenv("KHST_SMALL_LEVEL") ? (uint32_t)atoi(getenv("KHST_SMALL_LEVEL")) : SMALL_LEVEL;
   bool moved = move_d == 0;
   for (int d = 63; d >= 0; --d) {
@@ -2742,7 +2733,8 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
     } else if (coop) {
       hipLaunchKernelGGL(k_branch_coop, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     } else {
-      const bool small = !A.kn && !rescan && small_levels && cnt <= small_level;
+      // (link records, KHST_LEAF_LINKS=1, only through k_branch_fused<5>, which follows them)
+      const bool small = !A.kn && !rescan && !T.links && small_levels && cnt <= small_level;
       const bool pos = T.cend && !small;  // leaf children from their stashes
       if (T.cend && small) {  // leaf positions, a small level: the level's leaf child records first
         hipLaunchKernelGGL(k_level_leafrecs, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
@@ -2752,7 +2744,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
         hipLaunchKernelGGL(k_branch_fused<0>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
       else if (rescan)
         hipLaunchKernelGGL(k_branch_fused<1>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
-      else if (small && !T.links && cnt <= xl_level)
+      else if (small && cnt <= xl_level)
         hipLaunchKernelGGL(k_branch_xl, dim3((unsigned)((cnt + 1) / 2)), dim3(64), 0, st, T, (uint64_t)lbh[d],
                            (uint64_t)cnt);
       else if (small)
