@@ -386,6 +386,20 @@ int kh_trie_get_host(kh_trie* h, const uint32_t* trie, const uint8_t* keys, uint
                      uint8_t* vals, uint64_t val_cap, uint64_t* voff, uint8_t* found, uint64_t* val_bytes);
 
 /* Leaves of a trie (of all tries of a forest). */
+/* HBM held by a resident trie or forest.  Records and the value heap are append-only between
+ * compactions: a commit appends the records and values it makes and leaves the ones it
+ * replaces dead (~18 MB per configs[2] block).  records / heap_bytes: in use; live_records /
+ * live_heap_bytes: the current version's (counted on the device); map_slots: anchor-map
+ * capacity; hbm_bytes: every buffer the handle holds. */
+typedef struct kh_trie_usage_t {
+  uint64_t records, live_records, heap_bytes, live_heap_bytes, map_slots, hbm_bytes;
+} kh_trie_usage_t;
+int kh_trie_usage(kh_trie* h, kh_trie_usage_t* u);
+/* Rewrite the live records and their values densely and rebuild the anchor map (O(records)
+ * on the device; the version -- roots, last roots, write-back set -- is unchanged).  The JVM
+ * calls it between blocks when dead records pass a budget.  KH_EINVAL while a savepoint is
+ * open (the journal holds record indices).  before (nullable): records / heap bytes before. */
+int kh_trie_compact(kh_trie* h, kh_trie_usage_t* before);
 int kh_trie_size(const kh_trie* h, uint64_t* n);
 int kh_trie_free(kh_trie* h);
 

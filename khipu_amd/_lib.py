@@ -33,7 +33,7 @@ EXPORTS = (
     "kh_trie_root_sharded", "kh_block_commit_host", "kh_dev_list_roots", "kh_trie_get", "kh_trie_get_host",
     "kh_dev_synth_storage", "kh_trie_roots_segmented_sharded", "kh_trie_savepoint", "kh_trie_rollback",
     "kh_trie_release", "kh_trie_savepoint_depth", "kh_trie_root_of", "kh_trie_root_of_host", "kh_trie_copy",
-    "kh_verify_nodes_packed",
+    "kh_verify_nodes_packed", "kh_trie_usage", "kh_trie_compact",
 )
 
 
@@ -56,6 +56,12 @@ class MPTNodeMissingException(KhError):
 
 class DeviceError(KhError):
     """KH_EDEVICE / KH_ENOMEM: the GPU path failed."""
+
+
+class KhTrieUsage(ctypes.Structure):
+    """kh_trie_usage_t: a resident handle's records, value heap and HBM (include/khst.h)."""
+    _fields_ = [(f, ctypes.c_uint64) for f in
+                ("records", "live_records", "heap_bytes", "live_heap_bytes", "map_slots", "hbm_bytes")]
 
 
 class KhStats(ctypes.Structure):
@@ -143,6 +149,8 @@ def lib():
     L.kh_trie_root_of.argtypes = L.kh_trie_apply.argtypes
     L.kh_trie_root_of_host.argtypes = L.kh_trie_apply_host.argtypes
     L.kh_trie_copy.argtypes = [vp, ctypes.POINTER(vp)]
+    L.kh_trie_usage.argtypes = [vp, ctypes.POINTER(KhTrieUsage)]
+    L.kh_trie_compact.argtypes = [vp, ctypes.POINTER(KhTrieUsage)]
     L.kh_verify_nodes_packed.argtypes = [vp, vp, u64, vp, vp, u64, vp, vp, vp, vp, vp, vp, u64, ctypes.POINTER(u64)]
     for name in EXPORTS:
         fn = getattr(L, name)

@@ -3778,6 +3778,12 @@ __global__ void __launch_bounds__(BS) k_rec_count_live(Recs R, uint64_t n, unsig
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(cnt, v);
 }
+__global__ void __launch_bounds__(BS) k_heap_live(Recs R, uint64_t n, unsigned long long* cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  unsigned long long v = (i < n && R.rlive[i] == REC_LIVE) ? R.rvl[i] : 0;
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(cnt, v);
+}
 // (re)build the anchor map with capacity >= 2 * (records + headroom), inserting every live record
 static void map_rebuild(kh_trie* h, uint64_t headroom) {
   hipStream_t st = h->c->st;
@@ -4538,6 +4544,123 @@ static kh_trie* trie_copy(kh_trie* h) {
   n->em_bytes = h->em_bytes;
   HIPCHK(hipStreamSynchronize(st));
   return n.release();
+}
+
+// ---- compaction: records and the value heap are append-only between compactions (a commit
+// appends the records and values it makes and leaves the ones it replaces dead); trie_compact
+// rewrites the live records densely, each with its value moved into a dense heap, and rebuilds
+// the anchor map.  Nothing outside the records and the map refers to a record index (roots,
+// last roots and the write-back set are hashes and encodings), so the version is unchanged.
+__global__ void __launch_bounds__(BS) k_compact_in(Recs R, uint64_t n, uint32_t* live, uint64_t* vlen) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  const bool l = R.rlive[i] == REC_LIVE;
+  live[i] = l ? 1u : 0u;
+  vlen[i] = l ? R.rvl[i] : 0;
+}
+// 8 threads per record: one 16-byte quarter-line each, then the value's bytes strided over them
+__global__ void __launch_bounds__(BS) k_compact_move(Recs R, uint64_t n, const uint32_t* pos, const uint64_t* hoff,
+                                                     const uint8_t* heap, uint8_t* recs2, uint8_t* heap2) {
+  const uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x, i = t >> 3;
+  const uint32_t q = (uint32_t)(t & 7);
+  if (i >= n || R.rlive[i] != REC_LIVE) return;
+  const uint64_t ho = hoff[i];
+  ulonglong2 w = ((const ulonglong2*)(R.rk.b + i * REC_BYTES))[q];
+  if (q == 3) w.x = ho;  // rvo: bytes 48..55
+  ((ulonglong2*)(recs2 + (uint64_t)pos[i] * REC_BYTES))[q] = w;
+  const uint32_t vl = R.rvl[i];
+  const uint64_t vo = R.rvo[i];
+  for (uint32_t b = q; b < vl; b += 8) heap2[ho + b] = heap[vo + b];
+}
+static void trie_compact(kh_trie* h, kh_trie_usage_t* before) {
+  if (!h->sps.empty()) throw KhError{KH_EINVAL, "kh_trie_compact: a savepoint is open"};
+  kh_ctx* c = h->c;
+  hipStream_t st = c->st;
+  const uint64_t n = h->rn;
+  if (before) {
+    before->records = n;
+    before->heap_bytes = h->heap_n;
+  }
+  if (n == 0) return;
+  DevBuf wsb;
+  const size_t scr = scan_scratch_bytes(n, 8);
+  wsb.ensure(n * 4 + n * 8 + scr + 256);
+  uint64_t* vlen = (uint64_t*)wsb.p;
+  uint32_t* live = (uint32_t*)((char*)wsb.p + n * 8);
+  void* scratch = (char*)wsb.p + n * 12 + 64;
+  h->merr.ensure(64);
+  uint64_t* tot = (uint64_t*)h->merr.p, *tot64 = tot + 1;
+  hipLaunchKernelGGL(k_compact_in, GRID(n, BS), dim3(BS), 0, st, recs_of(h), n, live, vlen);
+  LAUNCH_CHECK();
+  scan_exclusive<uint32_t>(live, live, n, (uint32_t*)tot, scratch, st);
+  scan_exclusive<uint64_t>(vlen, vlen, n, tot64, scratch, st);
+  HIPCHK(hipMemcpyAsync(c->h_pinned, tot, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const uint64_t nlive = (uint32_t)c->h_pinned[0], hbytes = c->h_pinned[1];
+  const uint64_t cap = std::max<uint64_t>(nlive + nlive / 2, 4096);
+  DevBuf recs2, touched2, replaced2, heap2;
+  recs2.ensure(cap * REC_BYTES);
+  touched2.ensure(cap * 4);
+  replaced2.ensure(cap);
+  heap2.ensure(hbytes + hbytes / 4 + 64);
+  HIPCHK(hipMemsetAsync((uint8_t*)recs2.p + nlive * REC_BYTES, 0, recs2.cap - nlive * REC_BYTES, st));
+  HIPCHK(hipMemsetAsync(touched2.p, 0, touched2.cap, st));
+  HIPCHK(hipMemsetAsync(replaced2.p, 0, replaced2.cap, st));
+  hipLaunchKernelGGL(k_compact_move, GRID(n * 8, BS), dim3(BS), 0, st, recs_of(h), n, (const uint32_t*)live,
+                     (const uint64_t*)vlen, (const uint8_t*)h->heap.p, (uint8_t*)recs2.p, (uint8_t*)heap2.p);
+  LAUNCH_CHECK();
+  HIPCHK(hipStreamSynchronize(st));
+  swap_buf(h->recs, recs2);
+  swap_buf(h->touched, touched2);
+  swap_buf(h->replaced, replaced2);
+  swap_buf(h->heap, heap2);
+  h->rcap = std::min({h->recs.cap / REC_BYTES, h->touched.cap / 4, h->replaced.cap});
+  h->rn = nlive;
+  h->heap_n = hbytes;
+  h->flags_dirty = false;
+  // the per-commit scratch keeps the size of the largest commit so far (the open's build
+  // above all): released here, the next commit sizes it again; the write-back set is moved
+  // to a buffer of its own size
+  for (DevBuf* b : {&h->ws, &h->elout, &h->eloutb, &h->tlb, &h->ebuf, &h->tbuf, &h->ubuf, &h->selb, &h->gbuf,
+                    &h->em_spare})
+    b->release();
+  h->d_tries = nullptr;  // (they lived in tbuf; the block commit's injection uploads them again)
+  h->d_roots = nullptr;
+  if (h->em.p && h->em_valid && h->em_n) {
+    const size_t need = ((h->em_n * 32 + 255) & ~(size_t)255) + ((h->em_bytes + 255) & ~(size_t)255) + (h->em_n + 1) * 8;
+    if (need < h->em.cap / 2) {
+      DevBuf e2;
+      e2.ensure(need);
+      HIPCHK(hipMemcpyAsync(e2.p, h->em.p, need, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipStreamSynchronize(st));
+      swap_buf(h->em, e2);
+    }
+  } else {
+    h->em.release();
+  }
+  map_rebuild(h, 1024);  // (syncs; recounts the live records: rdead = 0)
+}
+static void trie_usage(kh_trie* h, kh_trie_usage_t* u) {
+  kh_ctx* c = h->c;
+  hipStream_t st = c->st;
+  memset(u, 0, sizeof(*u));
+  u->records = h->rn;
+  u->heap_bytes = h->heap_n;
+  u->map_slots = h->mcap;
+  u->hbm_bytes = h->recs.cap + h->touched.cap + h->replaced.cap + h->mslots.cap + h->heap.cap + h->ws.cap +
+                 h->elout.cap + h->eloutb.cap + h->em.cap + h->em_spare.cap + h->jidx.cap + h->jrec.cap +
+                 h->jmap.cap + h->tlb.cap + h->ebuf.cap + h->tbuf.cap + h->ubuf.cap + h->selb.cap + h->gbuf.cap;
+  if (!h->rn) return;
+  h->merr.ensure(64);
+  unsigned long long* cnt = (unsigned long long*)h->merr.p;
+  HIPCHK(hipMemsetAsync(cnt, 0, 16, st));
+  hipLaunchKernelGGL(k_rec_count_live, GRID(h->rn, BS), dim3(BS), 0, st, recs_of(h), h->rn, cnt);
+  hipLaunchKernelGGL(k_heap_live, GRID(h->rn, BS), dim3(BS), 0, st, recs_of(h), h->rn, cnt + 1);
+  LAUNCH_CHECK();
+  HIPCHK(hipMemcpyAsync(c->h_pinned, cnt, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  u->live_records = c->h_pinned[0];
+  u->live_heap_bytes = c->h_pinned[1];
 }
 
 // ---------------------------------------------------------------------------
@@ -5750,7 +5873,7 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     // list and roots are still on the device: its commit's tbuf)
     auto inject = [&](hipStream_t s) {
       const uint32_t nt = (uint32_t)storage->tries.size();
-      if (!(nt && na_up && d_a_up_trie)) return false;
+      if (!(nt && na_up && d_a_up_trie && storage->d_tries)) return false;  // (set by this call's storage commit)
       hipLaunchKernelGGL(k_inject_roots, GRID(na_up, BS), dim3(BS), 0, s, d_a_up_vals, d_a_up_voff, d_a_up_trie,
                          na_up, (const uint32_t*)storage->d_tries, nt, (const uint64_t*)storage->d_roots, err, tok);
       LAUNCH_CHECK();
@@ -6018,6 +6141,24 @@ int kh_trie_get_host(kh_trie* h, const uint32_t* trie, const uint8_t* keys, uint
     const uint64_t total = n ? voff[n] : tot;
     if (total) HIPCHK(hipMemcpyAsync(vals, dv, total, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+  })
+}
+
+int kh_trie_compact(kh_trie* h, kh_trie_usage_t* before) {
+  if (!h) return set_err(KH_EINVAL, "null handle");
+  API_TRY({
+    std::lock_guard<std::mutex> g(h->c->mu);
+    HIPCHK(hipSetDevice(h->c->dev));
+    trie_compact(h, before);
+  })
+}
+
+int kh_trie_usage(kh_trie* h, kh_trie_usage_t* u) {
+  if (!h || !u) return set_err(KH_EINVAL, "null handle");
+  API_TRY({
+    std::lock_guard<std::mutex> g(h->c->mu);
+    HIPCHK(hipSetDevice(h->c->dev));
+    trie_usage(h, u);
   })
 }
 

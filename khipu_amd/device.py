@@ -171,6 +171,21 @@ class _Versioned:
     def _after_rollback(self):
         pass
 
+    def usage(self):
+        """{records, live_records, heap_bytes, live_heap_bytes, map_slots, hbm_bytes} (kh_trie_usage)."""
+        u = _lib.KhTrieUsage()
+        self.ctx._sync()
+        check(lib().kh_trie_usage(self.h, ctypes.byref(u)))
+        return {f: int(getattr(u, f)) for f, _ in u._fields_}
+
+    def compact(self):
+        """Rewrite the live records and values densely (kh_trie_compact); the version is unchanged.
+        Returns {records, heap_bytes} before it."""
+        u = _lib.KhTrieUsage()
+        self.ctx._sync()
+        check(lib().kh_trie_compact(self.h, ctypes.byref(u)))
+        return {"records": int(u.records), "heap_bytes": int(u.heap_bytes)}
+
 
 class ResidentTrie(_Versioned):
     """A trie kept in HBM between commits (kh_trie_open / kh_trie_apply).

@@ -103,12 +103,32 @@ def cfg3(args):
     ctx = Ctx(0)
     nb = args.warmup + args.steps
     t0 = time.perf_counter()
-    w = BlockWorkload(ctx, args.resident, nb)
+    w = BlockWorkload(ctx, args.resident, nb + 1)
     open_s = time.perf_counter() - t0
+    u_open = {"state": w.state.usage(), "storage": w.forest.usage()}
     for b in range(nb):
         root = w.block(b)
     blocks = w.t_commit[args.warmup:]
     ms = np.array([x[0] for x in blocks])
+    # record / heap growth over the blocks, then one compaction of each handle (kh_trie_compact)
+    # and one more block on the compacted records
+    u_blocks = {"state": w.state.usage(), "storage": w.forest.usage()}
+    torch.cuda.synchronize()
+    tc0 = time.perf_counter()
+    w.state.compact()
+    tc1 = time.perf_counter()
+    w.forest.compact()
+    tc2 = time.perf_counter()
+    u_compact = {"state": w.state.usage(), "storage": w.forest.usage()}
+    root = w.block(nb)
+    compaction = {
+        "usage_after_open": u_open, "usage_after_blocks": u_blocks, "usage_after_compaction": u_compact,
+        "dead_record_bytes_per_block": {k: (u_blocks[k]["records"] - u_blocks[k]["live_records"]
+                                            - (u_open[k]["records"] - u_open[k]["live_records"])) * 128 // nb
+                                        for k in u_open},
+        "compact_ms": {"state": (tc1 - tc0) * 1e3, "storage": (tc2 - tc1) * 1e3},
+        "block_ms_after_compaction": w.t_commit[-1][0],
+    }
     K, V, O, N = w.final_accounts()
     hf, _, _, _ = ctx.build(K, 32, V, O, N)
     assert hf[0].tobytes() == root, "block-commit state root != full build of the final state"
@@ -140,7 +160,7 @@ def cfg3(args):
             "open_s": open_s, "block_ms_median": float(np.median(ms)), "block_ms_all": ms.tolist(),
             "rehashed_nodes_median": int(np.median([x[1] for x in blocks])),
             "ops_per_block": int(blocks[0][2]), "resident_accounts_after": len(w.state),
-            "state_root_after": root.hex(), "checked": checked}
+            "state_root_after": root.hex(), "checked": checked, "compaction": compaction}
 
 
 def cfg4(args):
