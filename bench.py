@@ -278,6 +278,35 @@ def pmc_traffic(kernel, n):
     return None
 
 
+def pmc_traffic_per_unit(kernel, units_per_launch):
+    """HBM bytes per launch of `kernel` for a launch of `units_per_launch` units, scaled from the
+    newest committed 100M PMC summary (the leaf kernel's bytes per leaf do not depend on the
+    size: input-order reads, one scattered 32-byte stash per leaf).  The sharded lines use it
+    for their per-rank launches; None without a summary."""
+    full = pmc_traffic(kernel, 100_000_000)
+    if full is None:
+        return None
+    return full / 100_000_000 * units_per_launch
+
+
+def committed_cpu_baseline():
+    """The cpu_baseline of the newest committed N = 1 bench line (profiles/r*_bench*.json):
+    the sequential port is timed on rank 0 at N = 1 only (its 4-sample fit up to 1M accounts);
+    the N > 1 lines report that measurement, named by its file, instead of timing it again."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench*.json")), key=round_key):
+        try:
+            with open(f) as fh:
+                row = json.loads(fh.read().strip().splitlines()[-1])
+        except (OSError, ValueError, IndexError):
+            continue
+        cb = row.get("cpu_baseline")
+        if row.get("n_gpus") == 1 and cb and row.get("metric", "").startswith("node-hashes/sec (full state root"):
+            best = dict(cb, source=f"{os.path.relpath(f, ROOT)} (timed at N = 1 on rank 0; not re-run at N > 1)")
+    return best
+
+
 def roofline(stats, n):
     """Dominant single kernel of the step (the larger of the two one-launch hash kernels),
     from the HIP events the library records on the stream each kernel runs on."""

@@ -2401,7 +2401,11 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   const int pd_mode = (early && nb > 0) ? (G ? PD_DEFAULT : pd_env) : 0;
   // (=2: the parent-depth scatter as its own kernel after k_topo_tile; =3: the scatter first,
   // the leaves right after it and k_topo_tile beside them)
-  const int tile_mode = (pd_mode == 0 || pd_mode == 1) ? (tte ? atoi(tte) : 1) : 0;
+  // Default: tiles from TOPO_TILE_MIN boundaries; below it the extra launches cost more than the
+  // dependent loads they save (configs[2] element builds of ~100k: 1.95 against 2.04 ms per
+  // block, profiles/r4w_topo_tile_block_ab_50m.json)
+  constexpr uint64_t TOPO_TILE_MIN = 1u << 21;
+  const int tile_mode = (pd_mode == 0 || pd_mode == 1) ? (tte ? atoi(tte) : (nb >= TOPO_TILE_MIN ? 1 : 0)) : 0;
   const bool topo_tile = tile_mode != 0;
   auto pdinv_skip = [&](hipStream_t s) {  // every input of the build without a record (its own inputs only)
     if (G) {

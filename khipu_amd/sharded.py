@@ -352,9 +352,12 @@ def bench_main(args):
     slow = max(leaf_all, key=lambda x: x[0])
     VALU_PEAK, OPS = 256 * 4 * 32 * 2.4e9, 5760
     achieved = slow[1] * OPS / max(slow[0] * 1e-3, 1e-12)
+    import bench
     roof = {"kernel": "k_leaf_in", "bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK / 1e12,
-            "unit": "T int32-lane-ops/s", "frac": achieved / VALU_PEAK, "traffic": None, "avg_ms": slow[0],
-            "perms_per_launch": int(slow[1]), "rank": "slowest of the ranks"}
+            "unit": "T int32-lane-ops/s", "frac": achieved / VALU_PEAK,
+            "traffic": bench.pmc_traffic_per_unit("k_leaf_in", slow[1]),
+            "traffic_note": "HBM bytes per launch: the committed 100M PMC summary's bytes per leaf x this launch's leaves",
+            "avg_ms": slow[0], "perms_per_launch": int(slow[1]), "rank": "slowest of the ranks"}
     # one more (untimed) step with a device sync after every phase: where the time goes
     phases = {}
     sharded_root(be, addr, vals, voff, n, phases=phases)
@@ -393,14 +396,17 @@ def bench_main(args):
             "roofline": roof,
         }
         if not getattr(args, "no_cpu", False):
-            # the khipu-faithful sequential CPU trie on prefixes of rank 0's slice (its first
-            # accounts are the workload's first accounts), asserted against this GPU's root of
-            # the same prefix; the full-size all-core CPU root check runs in the N = 1 line
-            import bench
-            samples = [int(x) for x in str(getattr(args, "seq_samples", "20000,50000")).split(",")
-                       if x and int(x) <= min(n, 50_000)]
-            if samples:
-                out["cpu_baseline"] = bench.cpu_baseline(be.ctx, args.cfg, addr, vals, voff, samples)
+            # the khipu-faithful sequential CPU trie is timed at N = 1 only (rank 0; its 4-sample
+            # fit up to 1M accounts, each sample's root asserted against the GPU's); an N > 1 line
+            # reports the newest committed N = 1 measurement, named by its file.  A world-1 run of
+            # this path (no committed line) times the small samples itself.
+            cb = bench.committed_cpu_baseline() if world > 1 else None
+            if cb is None:
+                samples = [int(x) for x in str(getattr(args, "seq_samples", "20000,50000")).split(",")
+                           if x and int(x) <= min(n, 50_000)]
+                cb = bench.cpu_baseline(be.ctx, args.cfg, addr, vals, voff, samples) if samples else None
+            if cb:
+                out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
     dist.barrier()
     dist.destroy_process_group()

@@ -10,7 +10,7 @@ N=${PMC_ACCOUNTS:-100000000}
 run() {
   local p=$1; shift
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d gpurun_out/${TAG}_$p -o pmc \
-    -- python3 bench.py --accounts $N --steps 1 --warmup 1 --no-cpu > gpurun_out/${TAG}_$p.log 2>&1
+    -- python3 bench.py --accounts $N --steps 1 --warmup 1 --no-cpu --no-host-path > gpurun_out/${TAG}_$p.log 2>&1
   local rc=$?; echo "PMC_${p}_RC=$rc"; [ $rc -eq 0 ] || exit $rc
 }
 run p1 FETCH_SIZE

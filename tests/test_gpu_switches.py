@@ -28,6 +28,7 @@ SWITCHES = [
     "KHST_TOPO_BPC=0",
     "KHST_TOPO_BPC=2",
     "KHST_TOPO_TILE=0",
+    "KHST_TOPO_TILE=1",
     "KHST_TOPO_TILE=2",
     "KHST_TOPO_TILE=3",
     "KHST_PD=sep",
