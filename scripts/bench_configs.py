@@ -103,7 +103,7 @@ def cfg3(args):
     ctx = Ctx(0)
     nb = args.warmup + args.steps
     t0 = time.perf_counter()
-    w = BlockWorkload(ctx, args.resident, nb + 1)
+    w = BlockWorkload(ctx, args.resident, nb + 1, nc=args.contracts, dirty=args.dirty)
     open_s = time.perf_counter() - t0
     u_open = {"state": w.state.usage(), "storage": w.forest.usage()}
     for b in range(nb):
@@ -132,7 +132,7 @@ def cfg3(args):
     K, V, O, N = w.final_accounts()
     hf, _, _, _ = ctx.build(K, 32, V, O, N)
     assert hf[0].tobytes() == root, "block-commit state root != full build of the final state"
-    checked = "state root and all 2,000 storage roots == full GPU builds"
+    checked = f"state root and all {w.nc} storage roots == full GPU builds"
     if not args.no_cpu:  # the independent CPU batch builder over the whole final state
         from oracle import oracle
         vo = O.cpu().numpy().astype(np.uint64)
@@ -153,10 +153,10 @@ def cfg3(args):
                                    hash_keys=True, nthreads=args.cpu_threads)
         bad = [c for c in range(w.nc) if cs[c] != w.roots[c]]
         assert not bad, f"storage roots differ from the CPU batch builder: {bad[:5]}"
-        checked = (f"state root and all 2,000 storage roots == full GPU builds AND == the CPU batch builder "
+        checked = (f"state root and all {w.nc} storage roots == full GPU builds AND == the CPU batch builder "
                    f"(oracle/batch_root.cc, {args.cpu_threads} threads, state root {cpu_s:.1f} s)")
-    return {"config": f"configs[2]: 20k dirty accounts + 2,000 storage tries x 10 dirty slots per block over a "
-                      f"{args.resident // 10**6}M-account resident trie (kh_block_commit)",
+    return {"config": f"configs[2]: {args.dirty} dirty accounts + {args.contracts} storage tries x 10 dirty slots per "
+                      f"block over a {args.resident / 10**6:g}M-account resident trie (kh_block_commit)",
             "open_s": open_s, "block_ms_median": float(np.median(ms)), "block_ms_all": ms.tolist(),
             "rehashed_nodes_median": int(np.median([x[1] for x in blocks])),
             "ops_per_block": int(blocks[0][2]), "resident_accounts_after": len(w.state),
@@ -224,6 +224,8 @@ def main():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--resident", type=int, default=50_000_000)
+    p.add_argument("--dirty", type=int, default=20_000, help="configs[2]: dirty accounts per block")
+    p.add_argument("--contracts", type=int, default=2_000, help="configs[2]: storage tries (10 dirty slots each)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU batch-builder checks")
     p.add_argument("--cpu-threads", type=int, default=16)
     args = p.parse_args()
