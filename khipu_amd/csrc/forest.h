@@ -67,6 +67,36 @@ KH_HD void set_nibble(uint64_t* key, uint32_t i, uint32_t v) {
   key[q] = (key[q] & ~(0xFULL << sh)) | ((uint64_t)v << sh);
 }
 
+// ---- khipu's value-only branch.  A re-put of a 32-byte key whose leaf hangs under a
+// depth-63 branch (its remaining path empty) goes through putInLeafNode with ml == 0 and an
+// empty existing key: BranchNode.withValueOnly, then putInBranchNode with an empty key sets
+// the value (MerklePatriciaTrie.scala:187-199, 258-262).  The leaf becomes a branch at depth 64
+// with no children and the new value -- not the canonical trie of the same keys, but khipu's.
+// Here it is a record with db = VB_DEPTH (no branch of 32-byte keys sits at depth 64), mask 0
+// and its value span; in an element build it is a subtree element whose capped reference is
+// that of its encoding [0x80 x 16, value].  Removing its key throws in khipu (fix of a branch
+// with no children and no value, :430-477): the commit is refused.
+constexpr uint32_t VB_DEPTH = 64;
+KH_HD uint32_t vb_put_len(uint8_t* out, uint32_t p, uint64_t len, uint32_t base) {  // RLP length prefix
+  if (len < 56) {
+    out[p++] = (uint8_t)(base + len);
+    return p;
+  }
+  const uint32_t nb = be_nbytes(len);
+  out[p++] = (uint8_t)(base + 55 + nb);
+  for (uint32_t i = nb; i-- > 0;) out[p++] = (uint8_t)(len >> (8 * i));
+  return p;
+}
+// the encoding of a value-only branch holding val (<= vl + 26 bytes); returns its length
+KH_HD uint32_t vb_encode(const uint8_t* val, uint32_t vl, uint8_t* out) {
+  const uint32_t v0 = vl ? val[0] : 0;
+  uint32_t p = vb_put_len(out, 0, 16 + rlp_str_len(vl, v0), 0xC0);
+  for (int c = 0; c < 16; ++c) out[p++] = 0x80;
+  if (!(vl == 1 && v0 < 0x80)) p = vb_put_len(out, p, vl, 0x80);
+  for (uint32_t i = 0; i < vl; ++i) out[p++] = val[i];
+  return p;
+}
+
 constexpr uint8_t REC_DEAD = 0, REC_LIVE = 1;
 
 // Node records: one 128-byte record per node (array of structures), so a probe's check
@@ -189,7 +219,7 @@ KH_HD uint32_t forest_get(const AMap& M, const Recs& R, uint32_t t, const uint64
     const uint32_t r = map_find(M, R, t, d, key);
     if (r == NONE) return NONE;
     const uint32_t db = R.rdb[r];
-    if (db == EL_LEAF) {
+    if (db == EL_LEAF || db == VB_DEPTH) {  // a leaf, or a value-only branch: it holds one key
       const uint64_t* L = R.key(r);
       return (L[0] == key[0] && L[1] == key[1] && L[2] == key[2] && L[3] == key[3]) ? r : NONE;
     }
@@ -248,7 +278,7 @@ KH_HD void elem_fill(const Recs& R, uint32_t r, uint32_t seg, const Elems& E, ui
   for (int q = 0; q < 4; ++q) E.bref[4 * e + q] = R.rbref[4ull * r + q];
   E.brl[e] = R.rbrl[r];
   E.vo[e] = R.rvo[r];
-  E.vl[e] = R.rdb[r] == EL_LEAF ? R.rvl[r] : 0;
+  E.vl[e] = (R.rdb[r] == EL_LEAF || R.rdb[r] == VB_DEPTH) ? R.rvl[r] : 0;  // (a value-only branch keeps its value)
   E.src[e] = r;
   E.oldd[e] = R.rd[r];
   for (int q = 0; q < 4; ++q) E.cref[4 * e + q] = R.rref[4ull * r + q];

@@ -3228,9 +3228,10 @@ static void copy_root(const BuildOut& O, uint64_t r, uint8_t* out32) {
 // value heap in HBM; a commit rebuilds only the nodes on its dirty paths
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32_t* touched, uint8_t* replaced,
-                                                  uint32_t* tlist, unsigned long long* ctr) {
+                                                  uint32_t* tlist, unsigned long long* ctr, uint8_t* vbf) {
   const uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  // ctr[0] touched list size, [1] replaced leaves, [2] error.  Every op of a commit passes
+  // ctr[0] touched list size, [1] replaced leaves, [2] error, [3] refusal, [6] value-only
+  // branches made (vbf[o]: op o puts a value-only branch, forest.h VB_DEPTH).  Every op of a commit passes
   // through its trie's top records: the touched flag is read before it is exchanged, so
   // only the first few ops contend for a hot record's atomic (a stale 0 from the vector
   // cache costs one extra exchange, never a wrong mark), and the replacements are counted
@@ -3253,7 +3254,7 @@ __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32
   const uint64_t* K = O.key + 4 * (live ? o : 0);
   const uint32_t t = live ? O.trie[o] : 0;
   uint32_t d = 0;
-  bool active = live, repl = false, lost = live;
+  bool active = live, repl = false, lost = live, vb = false;
   for (int step = 0; step < 70 && __ballot(active); ++step) {
     uint32_t r = NONE;
     bool leaf = false;
@@ -3269,11 +3270,21 @@ __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32
           if (L[0] == K[0] && L[1] == K[1] && L[2] == K[2] && L[3] == K[3]) {
             replaced[r] = 1;  // keys are unique in the batch: one op per leaf
             repl = true;
-            // khipu's put into a leaf whose remaining path is EMPTY (it hangs under a depth-63
-            // branch) turns it into a childless value-only branch (putInLeafNode, ml == 0 with
-            // an empty existingKey: MerklePatriciaTrie.scala:187-199 -> putInBranchNode
-            // :258-262), a non-canonical node this engine does not build: refused, not diverged
-            if (d == 64 && O.kind[o] == FOP_UPSERT) atomicOr(&ctr[3], 1ULL);
+            // a put into a leaf whose remaining path is EMPTY (it hangs under a depth-63 branch)
+            // makes khipu's value-only branch (forest.h VB_DEPTH)
+            vb = d == VB_DEPTH && O.kind[o] == FOP_UPSERT;
+          }
+          active = lost = false;
+        } else if (db == VB_DEPTH) {  // a value-only branch: only its own key reaches it
+          const uint64_t* L = R.key(r);
+          if (L[0] == K[0] && L[1] == K[1] && L[2] == K[2] && L[3] == K[3]) {
+            if (O.kind[o] == FOP_UPSERT) {  // putInBranchNode with an empty key: the new value
+              vb = repl = true;
+            } else {  // removeFromBranchNode, then fix: "Branch with no subvalues" (MPTException)
+              atomicOr(&ctr[3], 1ULL);
+            }
+          } else {
+            r = NONE;  // (cannot happen: another key leaves the extension above it)
           }
           active = lost = false;
         } else if (lcp_nibbles(load_key(K, 0), load_key(R.key(r), 0)) < (int)db) {
@@ -3287,7 +3298,35 @@ __global__ void __launch_bounds__(BS) k_f_descend(FOps O, AMap M, Recs R, uint32
     mark(r != NONE, r);
   }
   wave_count(&ctr[1], repl);
+  wave_count(&ctr[6], vb);
+  if (live) vbf[o] = vb ? 1 : 0;
   if (lost) ctr[2] = 3;
+}
+// value-only branches (k_f_descend's vbf): upsert o's element (rank ur[o], its value in the
+// heap) becomes the subtree element of its encoding; hashed encodings (>= 32 B) are listed for
+// the write-back set (vbl: encoding offset in enc, length; vbh: hash), count in cnt
+__global__ void __launch_bounds__(BS) k_f_vb_elems(FOps O, const uint8_t* vbf, const uint32_t* ur, const uint64_t* uoff,
+                                                   const uint8_t* heap, Elems E, uint8_t* enc, uint64_t* vbl,
+                                                   uint64_t* vbh, unsigned long long* cnt) {
+  const uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (o >= O.n || !vbf[o]) return;
+  const uint64_t e = ur[o], eo = uoff[o] + 32 * e;
+  const uint32_t L = vb_encode(heap + E.vo[e], E.vl[e], enc + eo);
+  uint64_t w[4];
+  if (L >= 32) {
+    kec256_msg<false>(enc + eo, L, w);
+  } else {
+    words_of(enc + eo, L, w);
+  }
+  for (int q = 0; q < 4; ++q) E.bref[4 * e + q] = w[q];
+  E.brl[e] = (uint8_t)(L >= 32 ? 32 : L);
+  E.db[e] = (uint8_t)VB_DEPTH;
+  if (L >= 32) {
+    const unsigned long long s = atomicAdd(cnt, 1ULL);
+    vbl[2 * s] = eo;
+    vbl[2 * s + 1] = L;
+    for (int q = 0; q < 4; ++q) vbh[4 * s + q] = w[q];
+  }
 }
 
 // upsert op o (its rank among the batch's upserts = ur[o]) -> leaf element; value into the heap
@@ -3871,7 +3910,32 @@ __global__ void __launch_bounds__(BS) k_open_level(OItems I, uint64_t ni, OItems
     N.prl[t] = (uint8_t)(pr ? prl : (is_hash ? 32 : crl));
   };
   if (k == 17) {  // branch [ref_0 .. ref_15, value]
-    if (it[16].list || it[16].len) return bad(OPEN_VALUE);  // a secure trie never stores a branch value
+    if (it[16].list || it[16].len) {
+      // a secure trie stores a branch value only in khipu's value-only branch (forest.h VB_DEPTH):
+      // no children, at depth 64
+      bool none = !it[16].list && d == VB_DEPTH;
+      for (int c = 0; c < 16 && none; ++c) none = !it[c].list && it[c].len == 0;
+      if (!none) return bad(OPEN_VALUE);
+      const uint64_t vo = atomicAdd(heap_n, (unsigned long long)it[16].len);
+      for (uint32_t q = 0; q < it[16].len; ++q) heap[vo + q] = e[it[16].off + q];
+      const uint64_t r = rbase + atomicAdd(rcount, 1ULL);
+      for (int q = 0; q < 4; ++q) {
+        R.rk[4 * r + q] = pre[q];
+        R.rbref[4 * r + q] = own[q];
+        R.rref[4 * r + q] = I.pref[4 * i + q];
+      }
+      R.rt[r] = trie;
+      R.rd[r] = (uint8_t)a;
+      R.rdb[r] = (uint8_t)VB_DEPTH;
+      R.rvo[r] = vo;
+      R.rvl[r] = it[16].len;
+      R.rbrl[r] = (uint8_t)ownl;
+      R.rrl[r] = I.prl[i];
+      R.rmask[r] = 0;
+      R.rlive[r] = REC_LIVE;
+      atomicAdd(leaves, 1ULL);  // (its key counts as one of the trie's keys)
+      return;
+    }
     uint32_t mask = 0;
     for (int c = 0; c < 16; ++c) {
       if (!it[c].list && it[c].len == 0) continue;
@@ -3968,6 +4032,8 @@ struct FCommit {  // one commit's inputs (device buffers)
 };
 
 static int emit_nodes_dev(kh_ctx* c, DevBuf& out, uint64_t* n_nodes, uint64_t* rlp_len);
+static void em_append(kh_ctx* c, DevBuf& em, uint64_t& tn, uint64_t& tb, const uint64_t* d_hashes, const uint8_t* src,
+                      const std::vector<uint64_t>& list);
 
 // a commit is about to replace the write-back set: the innermost savepoint keeps the set of its
 // version (once), and the commit writes into the spare buffer
@@ -4083,11 +4149,12 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   uint32_t* otrie = segd ? S.sseg : sseg;  // the compaction of duplicates moves the sorted ids
   // the descent's touched list and the commit's flags (fctr, zeroed by k_f_prep): [0] touched
   // count, [1] replaced leaves, [2] anchor-map error, [3] refusal / map insert error,
-  // [4] fresh map slots, [5] element count
-  h->tlb.ensure(carve_size({nd * 70 * 4 + 64, 64}));
+  // [4] fresh map slots, [5] element count, [6] value-only branches made, [7] the hashed ones
+  h->tlb.ensure(carve_size({nd * 70 * 4 + 64, 64, nd + 64}));
   Carver c3{(char*)h->tlb.p, 0, h->tlb.cap};
   uint32_t* tlist = c3.take<uint32_t>(nd * 70 + 16);
   unsigned long long* fctr = c3.take<unsigned long long>(8);
+  uint8_t* vbf = c3.take<uint8_t>(nd + 64);  // ops that make a value-only branch
   // kinds, the distinct tries of the batch (sorted: the segments of the element build), and
   // the upserts' ranks and value offsets (their values go to the heap)
   hipLaunchKernelGGL(k_f_prep, GRID(nd, BS), dim3(BS), 0, st, (const uint32_t*)S.sidx, nd, F.nup, segd, otrie,
@@ -4164,7 +4231,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   if (h->mcap == 0) map_rebuild(h, nops + 1024);
   h->flags_dirty = true;  // until the touched records die (k_map_delete) or are untouched
   hipLaunchKernelGGL(k_f_descend, GRID(nd, BS), dim3(BS), 0, st, O, map_of(h), recs_of(h), (uint32_t*)h->touched.p,
-                     (uint8_t*)h->replaced.p, tlist, fctr);
+                     (uint8_t*)h->replaced.p, tlist, fctr, vbf);
   LAUNCH_CHECK();
   // ---- 3. elements: the gather (grid-stride over the device's touched count), one sync
   auto gather = [&](bool redo) {
@@ -4176,7 +4243,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                        recs_of(h), (const uint32_t*)h->touched.p, (const uint8_t*)h->replaced.p,
                        (const uint32_t*)tlist, (const unsigned long long*)fctr, (const uint32_t*)tries, nt, E, fctr);
     LAUNCH_CHECK();
-    HIPCHK(hipMemcpyAsync(c->h_pinned, fctr, 48, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned, fctr, 56, hipMemcpyDeviceToHost, st));  // [0..6]
     HIPCHK(hipStreamSynchronize(st));
   };
   gather(false);
@@ -4191,9 +4258,9 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     }
     h->flags_dirty = false;
     throw KhError{KH_EINVAL,
-                  "put of a key whose leaf has an empty remaining path (63 nibbles shared with another key): khipu "
-                  "turns that leaf into a value-only branch (MerklePatriciaTrie.scala:187-199), which this engine "
-                  "does not reproduce; the trie is unchanged"};
+                  "remove of a key held by a value-only branch: khipu's fix of the emptied branch throws "
+                  "MPTException(\"Branch with no subvalues\") (MerklePatriciaTrie.scala:323-370,430-477); the trie "
+                  "is unchanged"};
   }
   if (c->h_pinned[2]) throw KhError{KH_EINTERNAL, "forest gather: corrupt anchor map"};
   uint64_t ne = c->h_pinned[5];
@@ -4218,6 +4285,30 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                        (uint8_t*)h->heap.p, hb, (const uint32_t*)tflag, (const uint32_t*)tpos, tries, E, false, true);
     LAUNCH_CHECK();
   };
+  // value-only branches (rare: a re-put of a key sharing 63 nibbles with another): their
+  // encodings need the values, so a deferred producer is waited for here
+  const uint64_t nvb = c->h_pinned[6];
+  std::vector<uint64_t> vb_list;  // (encoding offset, length) of the hashed ones
+  DevBuf vbenc;
+  uint64_t* vbh = nullptr;
+  if (nvb) {
+    values_now();
+    vbenc.ensure(ubytes + 32 * (uint64_t)nups + 64 + nvb * 48 + 64);
+    uint8_t* enc = (uint8_t*)vbenc.p;
+    uint64_t* vbl = (uint64_t*)(enc + ((ubytes + 32 * (uint64_t)nups + 64 + 15) & ~(uint64_t)15));
+    vbh = vbl + 2 * nvb;
+    unsigned long long* vcnt = fctr + 7;
+    hipLaunchKernelGGL(k_f_vb_elems, GRID(nd, BS), dim3(BS), 0, st, O, (const uint8_t*)vbf, (const uint32_t*)ur,
+                       (const uint64_t*)uoff, (const uint8_t*)h->heap.p, E, enc, vbl, vbh, vcnt);
+    LAUNCH_CHECK();
+    if (h->flags & KH_EMIT_NODES) {
+      HIPCHK(hipMemcpyAsync(c->h_pinned, vcnt, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      const uint64_t nh = c->h_pinned[0];
+      vb_list.resize(2 * nh);
+      if (nh) HIPCHK(hipMemcpy(vb_list.data(), vbl, 16 * nh, hipMemcpyDeviceToHost));
+    }
+  }
   h->ntl_hint = ntl;
   h->heap_n = hb + ubytes;
   HIPCHK(hipEventRecord(c->ev[7], st));
@@ -4342,6 +4433,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     uint64_t en = 0, eb2 = 0;
     emit_nodes_dev(c, h->em, &en, &eb2);
     c->T.emit_sel = nullptr;
+    if (!vb_list.empty()) em_append(c, h->em, en, eb2, vbh, (const uint8_t*)vbenc.p, vb_list);
     h->em_n = en;
     h->em_bytes = eb2;
     h->em_valid = true;
@@ -4906,6 +4998,38 @@ static EmitLayout emit_layout(DevBuf& out, uint64_t tn, uint64_t tb) {
   uint8_t* orlp = oh + ((tn * 32 + 255) & ~255ULL);
   uint64_t* ooff = (uint64_t*)(orlp + ((tb + 255) & ~255ULL));
   return EmitLayout{oh, orlp, ooff};
+}
+// nodes that are not nodes of the element build appended to a write-back set (the value-only
+// branches a commit made): hashes (device, 4 words each), encodings in src at the (offset,
+// length) pairs of list (host)
+static void em_append(kh_ctx* c, DevBuf& em, uint64_t& tn, uint64_t& tb, const uint64_t* d_hashes, const uint8_t* src,
+                      const std::vector<uint64_t>& list) {
+  const uint64_t n = list.size() / 2;
+  if (!n) return;
+  hipStream_t st = c->st;
+  uint64_t add = 0;
+  for (uint64_t j = 0; j < n; ++j) add += list[2 * j + 1];
+  const uint64_t tn2 = tn + n, tb2 = tb + add;
+  DevBuf e2;
+  e2.ensure(tn2 * 32 + tb2 + (tn2 + 1) * 8 + 1024);
+  const EmitLayout A = emit_layout(em, tn, tb), N = emit_layout(e2, tn2, tb2);
+  if (tn) HIPCHK(hipMemcpyAsync(N.hashes, A.hashes, tn * 32, hipMemcpyDeviceToDevice, st));
+  if (tn) HIPCHK(hipMemcpyAsync(N.off, A.off, tn * 8, hipMemcpyDeviceToDevice, st));
+  if (tb) HIPCHK(hipMemcpyAsync(N.rlp, A.rlp, tb, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync(N.hashes + tn * 32, d_hashes, n * 32, hipMemcpyDeviceToDevice, st));
+  std::vector<uint64_t> offs(n + 1);
+  uint64_t at = tb;
+  for (uint64_t j = 0; j < n; ++j) {
+    HIPCHK(hipMemcpyAsync(N.rlp + at, src + list[2 * j], list[2 * j + 1], hipMemcpyDeviceToDevice, st));
+    offs[j] = at;
+    at += list[2 * j + 1];
+  }
+  offs[n] = at;
+  HIPCHK(hipMemcpyAsync(N.off + tn, offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));  // (offs is a host temporary)
+  swap_buf(em, e2);
+  tn = tn2;
+  tb = tb2;
 }
 static int emit_nodes_dev(kh_ctx* c, DevBuf& out, uint64_t* n_nodes, uint64_t* rlp_len) {
   Topo& T = c->T;

@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 from tests import cases as C
+from tests.writeback import check_delta
 
 pytestmark = pytest.mark.gpu
 
@@ -389,43 +390,180 @@ def test_block_commit_refuses_non_account_body(khst, oracle):
     lib().kh_trie_free(fo_h)
 
 
-def test_update_of_empty_path_leaf_is_refused(khst, oracle):
-    """A later block updating a key whose leaf hangs under a depth-63 branch (its remaining
-    path is empty): khipu's putInLeafNode turns that leaf into a childless value-only branch
-    (MerklePatriciaTrie.scala:187-199 -> :258-262; tests/test_oracle.py pins the quirk), a
-    node the canonical builder never makes.  The resident commit refuses the batch with
-    MPTException and leaves the trie unchanged instead of returning a root that differs
-    from the JVM's; batches that do not hit the shape still match the oracle fold, including
-    the same key once its sibling is gone (its leaf then has a path again)."""
-    from khipu_amd.device import Ctx, ResidentTrie
-    from khipu_amd._lib import MPTException
-    r = random.Random(63)
+def _pair(r):
+    """Two keys sharing 63 nibbles: they hang under a depth-63 branch, their leaves' paths empty."""
     k1 = bytearray(C._rk(r))
     k2 = bytearray(k1)
-    k2[31] ^= 0x01  # 63 shared nibbles: k1 and k2 hang under a depth-63 branch
-    k1, k2 = bytes(k1), bytes(k2)
-    others = [C._rk(r) for _ in range(200)]
+    k2[31] ^= 0x01
+    return bytes(k1), bytes(k2)
+
+
+@pytest.mark.parametrize("small", [False, True], ids=["hashed", "inline"])
+def test_value_only_branch_vs_oracle(khst, oracle, small):
+    """khipu's value-only branch (forest.h VB_DEPTH): a re-put of a key whose leaf hangs under
+    a depth-63 branch goes through putInLeafNode with ml == 0 and an empty existing key and
+    leaves a childless branch holding the new value (MerklePatriciaTrie.scala:187-199 ->
+    putInBranchNode :258-262; tests/test_oracle.py pins the shape).  Every block equals the
+    oracle's fold and its write-back delta the oracle's Updated log (tests/writeback.py):
+    making it, updating it, its sibling removed (an extension above it, then merged with the
+    one above that), a new branch above it, get() of its key; removing its key is refused like
+    khipu's MPTException ("Branch with no subvalues") with the trie unchanged; a node store of
+    every emitted node reopens it (kh_trie_open_nodes).  small: 1-byte values (the branch is
+    embedded in its parent, < 32 B) instead of account bodies."""
+    from khipu_amd.device import Ctx, ResidentTrie
+    from khipu_amd._lib import MPTException
+    r = random.Random(64 if small else 63)
+    val = (lambda: bytes([r.randrange(1, 0x80)])) if small else (lambda: C.account_value(r))
+    k1, k2 = _pair(r)
+    k3 = bytearray(k1)
+    k3[31] = (k3[31] & 0x0F) | (((k3[31] >> 4) ^ 0x3) << 4)  # 62 nibbles shared with k1 and k2
+    k3 = bytes(k3)
+    q1, q2 = _pair(r)  # a second pair whose value-only branch is made and kept
+    others = [C._rk(r) for _ in range(300)]
+    ks = others + [k1, k2, q1, q2]
+    vs = [val() for _ in ks]
+    o = oracle.Trie()
+    for k, v in zip(ks, vs):
+        o.put(k, v)
+    ctx = Ctx(0)
+    t = ResidentTrie(ctx, ks, vs)
+    assert t.root == o.root_hash()
+    store = dict(t.nodes())
+    o.persist().reopen()
+    live = dict(zip(ks, vs))
+
+    def block(ups, dels, what):
+        for k, v in ups:
+            o.put(k, v)
+            live[k] = v
+        for k in dels:
+            o.remove(k)
+            live.pop(k, None)
+        root = t.commit(ups, dels)
+        assert root == o.root_hash(), what
+        delta = t.nodes()
+        check_delta(delta, [o], store, what)
+        store.update(delta)
+        o.persist().reopen()
+        probe = [k1, k2, k3, q1, q2] + others[:20]
+        assert t.get(probe) == [live.get(k) for k in probe], what
+
+    block([(k1, val()), (others[0], val()), (q1, val())], [], "value-only branches made")
+    block([(k1, val())], [others[1]], "value-only branch updated")
+    size = len(t)
+    with pytest.raises(MPTException, match="value-only branch"):
+        t.commit([(others[2], val())], [k1])
+    assert t.get_root() == o.root_hash() and len(t) == size
+    block([(others[3], val())], [k2], "its sibling removed: an extension above it")
+    block([(k3, val())], [], "a new branch above it")
+    block([(k1, val()), (q1, val())], [others[4]], "updated under the new branch")
+    block([], [k3], "the branch above it removed again")
+    # reopen from the node store: the value-only branches decode into records
+    t2 = ResidentTrie.from_nodes(ctx, t.root, store)
+    assert t2.root == t.root and len(t2) == len(t)
+    probe = [k1, q1, q2] + others[:10]
+    assert t2.get(probe) == [live.get(k) for k in probe]
+    v = val()
+    o.put(q1, v)
+    assert t2.commit([(q1, v)], []) == o.root_hash()
+    t2.close()
+    t.close()
+
+
+def test_value_only_branch_in_block_commit(khst, oracle):
+    """kh_block_commit with value-only branches made in both phases of one block: in a storage
+    trie (raw slot keys) and in the state trie, whose account phase runs beside the storage
+    phase and reads its values only after the storage roots are injected (the branch's
+    encoding needs them).  Two blocks; the state root equals the oracle's fold with the
+    injected storageRoot, the storage root the oracle's."""
+    import ctypes
+    from khipu_amd import _lib, codec
+    from khipu_amd._lib import check, lib
+    from khipu_amd.device import block_commit_host
+    r = random.Random(66)
+    a1, a2 = _pair(r)
+    s1, s2 = _pair(r)
+    akeys = [C._rk(r) for _ in range(300)] + [a1, a2]
+    avals = [codec.account_rlp(i, 10 ** 18 + i) for i in range(len(akeys))]
+    kb = np.frombuffer(b"".join(akeys), np.uint8)
+    vb = np.frombuffer(b"".join(avals) + bytes(8), np.uint8)
+    vo = np.concatenate([[0], np.cumsum([len(v) for v in avals])]).astype(np.uint64)
+    root = np.zeros(32, np.uint8)
+    st_h, fo_h = ctypes.c_void_p(), ctypes.c_void_p()
+    check(lib().kh_trie_open_host(kb.ctypes.data, 32, vb.ctypes.data, vo.ctypes.data, len(akeys), 0,
+                                  root.ctypes.data, ctypes.byref(st_h)))
+    check(lib().kh_forest_open(None, 0, ctypes.byref(fo_h)))
+
+    class H:
+        def __init__(self, h):
+            self.h = h
+            self.ctx = type("C", (), {"_sync": staticmethod(lambda: None)})()
+    state, forest = H(st_h), H(fo_h)
+    so_t = oracle.Trie()  # storage trie 0
+    st_t = oracle.Trie()  # the state trie
+    for k, v in zip(akeys, avals):
+        st_t.put(k, v)
+    slots = [C._rk(r) for _ in range(40)] + [s1, s2]
+
+    def block(sups, aups):
+        for k, v in sups:
+            so_t.put(k, v)
+        sroot = so_t.root_hash()
+        sk = np.frombuffer(b"".join(k for k, _ in sups), np.uint8)
+        sv = np.frombuffer(b"".join(v for _, v in sups) + bytes(8), np.uint8)
+        so = np.concatenate([[0], np.cumsum([len(v) for _, v in sups])]).astype(np.uint64)
+        bodies = [codec.account_rlp(n, b) for _, (n, b) in aups]
+        av = np.frombuffer(b"".join(bodies) + bytes(8), np.uint8).copy()
+        ao = np.concatenate([[0], np.cumsum([len(b) for b in bodies])]).astype(np.uint64)
+        at = np.array([0] + [_lib.KH_NO_TRIE] * (len(aups) - 1), np.uint32)  # the first names trie 0
+        ak = np.frombuffer(b"".join(k for k, _ in aups), np.uint8)
+        got = block_commit_host(state, forest, np.zeros(len(sups), np.uint32), sk, sv, so, None, None, ak, av, ao,
+                                at, None)
+        b0 = bytearray(bodies[0])
+        b0[len(b0) - 65:len(b0) - 33] = sroot
+        for (k, _), b in zip(aups, [bytes(b0)] + bodies[1:]):
+            st_t.put(k, b)
+        assert got == st_t.root_hash()
+
+    block([(k, bytes([r.randrange(1, 256)]) * r.choice([1, 3, 33])) for k in slots],
+          [(akeys[0], (1, 5)), (akeys[1], (2, 6))])
+    # the second block re-puts s1 (a storage value-only branch) and a1 (a state one, naming trie 0)
+    block([(s1, b"\x07" * 33), (slots[0], b"\x09")], [(a1, (3, 7)), (akeys[2], (4, 8))])
+    block([(s1, b"\x08"), (slots[1], b"\x0a" * 5)], [(a1, (5, 9))])
+    lib().kh_trie_free(st_h)
+    lib().kh_trie_free(fo_h)
+
+
+def test_value_only_branch_versions_and_compaction(khst, oracle):
+    """A value-only branch through a savepoint (rolled back, then made again), a copy, and a
+    compaction (its value moves to the dense heap): roots and get() stay the oracle's."""
+    from khipu_amd.device import Ctx, ResidentTrie
+    r = random.Random(65)
+    k1, k2 = _pair(r)
+    others = [C._rk(r) for _ in range(100)]
     ks = others + [k1, k2]
     vs = [C.account_value(r) for _ in ks]
     o = oracle.Trie()
     for k, v in zip(ks, vs):
         o.put(k, v)
     t = ResidentTrie(Ctx(0), ks, vs)
-    assert t.root == o.root_hash()
-    before = t.root
-    with pytest.raises(MPTException, match="value-only branch"):
-        t.commit([(others[0], C.account_value(r)), (k1, C.account_value(r))], [])
-    assert t.root_hash == before
-    # the trie is intact: a valid batch (removing the sibling) matches the oracle fold ...
-    ups = [(others[1], C.account_value(r))]
-    for k, v in ups:
-        o.put(k, v)
-    o.remove(k2)
-    assert t.commit(ups, [k2]) == o.root_hash()
-    # ... and k1 (now a leaf with a path under a shallower branch) updates normally
+    parent = t.root
+    t.savepoint()
+    t.commit([(k1, C.account_value(r))], [])
+    t.rollback()
+    assert t.get_root() == parent == o.root_hash()
     v1 = C.account_value(r)
     o.put(k1, v1)
     assert t.commit([(k1, v1)], []) == o.root_hash()
+    c = t.copy()
+    t.compact()
+    assert t.get_root() == o.root_hash() and t.get([k1, k2]) == [v1, vs[-1]]
+    v2 = C.account_value(r)
+    o.put(k1, v2)
+    o.remove(others[0])
+    assert t.commit([(k1, v2)], [others[0]]) == o.root_hash()
+    assert c.get([k1]) == [v1]
+    c.close()
     t.close()
 
 

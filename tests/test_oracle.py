@@ -158,7 +158,7 @@ def test_reference_value_branch_quirk(oracle):
     remaining path: putInLeafNode with ml == 0 and an empty existingKey builds
     BranchNode.withValueOnly and puts into it (MerklePatriciaTrie.scala:187-199,258-262),
     so the root differs from the canonical trie of the same (key, value) set.  The GPU
-    resident commit refuses such a batch (tests/test_gpu_resident.py)."""
+    resident commit reproduces it (tests/test_gpu_resident.py::test_value_only_branch_*)."""
     import random
     r = random.Random(63)
     k1 = bytearray(r.getrandbits(8) for _ in range(32))
