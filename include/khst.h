@@ -284,7 +284,10 @@ int kh_trie_open_nodes(kh_ctx* ctx, const uint8_t root32[32], const uint8_t* d_e
 int kh_trie_open_nodes_host(const uint8_t root32[32], const uint8_t* enc, const uint64_t* off, uint64_t n,
                             uint32_t flags, uint8_t missing32[32], kh_trie** out);
 
-/* One commit; root32 receives the new root.  stats: n_node_hashes counts the nodes re-hashed. */
+/* One commit; root32 receives the new root.  stats: n_node_hashes counts the nodes re-hashed.
+ * A handle without KH_EMIT_NODES returns once the new roots are on the host: the commit's
+ * record and anchor-map writes finish on the library's stream after it (every later call on
+ * the handle is ordered after them; an internal failure there surfaces at the next call). */
 int kh_trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals, const uint64_t* d_up_voff,
                   uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
                   uint8_t root32[32], kh_stats* stats);

@@ -720,7 +720,9 @@ __global__ void __launch_bounds__(BS) k_leaf_prep(Topo T, uint32_t* list, unsign
   const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u;
   uint64_t off = 0;
   uint32_t vlen = 0;
-  if (i < T.m) {
+  // (an element build's cached nodes and subtrees are not re-encoded: their values are not
+  // staged -- most elements of a block commit, the unchanged siblings on the dirty paths)
+  if (i < T.m && !(T.el_db && (el_subtree(T, i) || el_cached(T, i, (uint32_t)(T.lf_pd[i] + 1))))) {
     off = T.svoff[i];
     vlen = T.svlen[i];
   }
@@ -1799,6 +1801,10 @@ struct kh_ctx {
   kh_ctx* bsub = nullptr;
   hipEvent_t bev = nullptr;
   std::unique_ptr<Worker> bworker;
+  // plain builds on the 32-bit-prefix path do not wait for the tie kernel's flags (SortIO::
+  // speculate); a build whose flags were set (repeated keys, a long run) is redone without, and
+  // the next spec_off builds do not speculate
+  uint32_t spec_off = 0;
   // last build (for emission)
   Topo T{};
   uint64_t last_B = 0;
@@ -1838,6 +1844,7 @@ struct BuildArgs {
   bool dev_results = false;        // results and counters stay on the device (no host sync at the end)
   const GroupArgs* grp = nullptr;  // a group of a grouped build (depth0 = 1, keys = the hashed keys of all groups)
   bool no_groups = false;          // never split into a grouped build (its own fallback)
+  bool no_spec = false;            // no speculative sort (SortIO::speculate): the retry of one that failed
   std::function<void()> before_leaves;  // element builds: called (host) right before the leaves are encoded
 };
 // element build (forest.h): inputs are leaves and subtree elements; the capped reference
@@ -1882,6 +1889,8 @@ static uint8_t* pinned_stage(kh_ctx* c, size_t bytes) {
 // a grouped build met a run of > TIE_RUN_MAX keys with equal 32-bit prefixes (adversarial
 // keys): the build is redone as one plain build, which takes the full 256-bit sort
 struct GroupFallback {};
+// a speculative sort (SortIO::speculate) met repeated keys or a long run: the build is redone
+struct SpecRetry {};
 
 static float ev_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0;
@@ -1910,6 +1919,10 @@ struct SortIO {
   // caller's check of earlier stream work, read without a sync of its own (nullable)
   const unsigned long long* chk = nullptr;
   bool no_full_sort = false;  // a group of a grouped build (input indices are not 0..n-1): no 256-bit sort
+  // ck_path: no sync for the tie kernel's flags: the sort proceeds as if no key repeats and no
+  // run is too long (hashed keys: the rule); the caller reads the flags at its next sync
+  // (CTR_TIE) and redoes the build without speculating if either is set
+  bool speculate = false;
   // out
   uint8_t* u = nullptr;  // ck_path: boundary values, written for the tie runs' inner boundaries
   uint32_t depth0 = 0;
@@ -1961,9 +1974,12 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
                          (const uint64_t*)K32, T.ctr + CTR_TIE, S.u, S.depth0);
     }
     LAUNCH_CHECK();
-    HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    const uint64_t tf = c->h_pinned[0];
+    uint64_t tf = 0;
+    if (!S.speculate) {
+      HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      tf = c->h_pinned[0];
+    }
     long_run = tf & 1;
     if (!long_run) {
       uint64_t m = n;
@@ -2094,7 +2110,17 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
 static void build_stats(kh_ctx* c, const unsigned long long* hc, kh_stats* stats);
 static uint32_t group_count(const BuildArgs& A);
 static void grouped_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats, uint32_t G);
+static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats);
 static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats) {
+  try {
+    run_build_once(c, A, O, stats);
+  } catch (SpecRetry&) {
+    BuildArgs B = A;
+    B.no_spec = true;
+    run_build_once(c, B, O, stats);
+  }
+}
+static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats) {
   if (const uint32_t ng = group_count(A); ng > 1) {  // a large plain root: pipelined over top-nibble groups
     grouped_build(c, A, O, stats, ng);
     return;
@@ -2305,6 +2331,9 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   if (stage_ev) HIPCHK(hipEventRecord(c->ev[1], st));
 
   // ---- 2. sort + dedup
+  // (KHST_SPEC=0, measurement switch: the tie flags' sync as before)
+  const bool spec = ck_path && !G && !A.no_spec && c->spec_off == 0 && !(getenv("KHST_SPEC") && atoi(getenv("KHST_SPEC")) == 0);
+  if (c->spec_off) --c->spec_off;
   uint64_t m = n;
   uint32_t* sidx = nullptr;
   bool fallback = false;
@@ -2314,6 +2343,7 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
              A.kn, ck_ready};
     S.ck_path = ck_path;
     S.no_full_sort = G != nullptr;
+    S.speculate = spec;
     S.u = T.u;
     S.depth0 = A.depth0;
     sort_dedup(c, S);
@@ -2587,6 +2617,11 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   HIPCHK(hipMemcpyAsync(c->h_pinned, ctr, tcopy, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const unsigned long long* hc = c->h_pinned;
+  if (spec && hc[CTR_TIE]) {  // repeated keys or a long run after all: redo without speculating
+    HIPCHK(hipStreamSynchronize(c->st2));
+    c->spec_off = 8;
+    throw SpecRetry{};
+  }
   const uint64_t B = (uint32_t)hc[CTR_B];
   const uint64_t lf_bytes = early ? hc[CTR_LONGB] : hc[CTR_B + 2];
   const uint64_t C = (uint32_t)hc[CTR_B + 3];
@@ -3782,7 +3817,29 @@ struct kh_trie {
   uint64_t map_epoch = 0;   // anchor-map rebuilds so far (a rebuild voids the slot log)
   bool flags_dirty = false; // a descent marked records and its commit did not finish
   DevBuf em_spare;          // the write-back buffer a savepoint's saved set rotates with
+  // a commit's tail left in flight (forest_commit, no write-back set): its records and anchor
+  // map are written after the call returned; pend (pinned) gets the map's error flag and fresh
+  // slot count, read by trie_settle before the host next needs them
+  hipEvent_t ev_roots = nullptr, pend_ev = nullptr;
+  unsigned long long* pend = nullptr;
+  bool pend_valid = false, pend_fresh = false;
+  kh_trie() = default;
+  kh_trie(const kh_trie&) = delete;
+  kh_trie& operator=(const kh_trie&) = delete;
+  ~kh_trie() {
+    if (ev_roots) (void)hipEventDestroy(ev_roots);
+    if (pend_ev) (void)hipEventDestroy(pend_ev);
+    if (pend) (void)hipHostFree(pend);
+  }
 };
+// the in-flight tail of the last commit: its map error and fresh slots (before mused is read)
+static void trie_settle(kh_trie* h) {
+  if (!h->pend_valid) return;
+  HIPCHK(hipEventSynchronize(h->pend_ev));
+  h->pend_valid = false;
+  if (h->pend[0]) throw KhError{KH_EINTERNAL, "anchor map insert failed"};
+  if (h->pend_fresh) h->mused += h->pend[1];
+}
 
 static Recs recs_of(kh_trie* h) {
   return recs_at((uint8_t*)h->recs.p);
@@ -3829,6 +3886,7 @@ __global__ void __launch_bounds__(BS) k_heap_live(Recs R, uint64_t n, unsigned l
 }
 // (re)build the anchor map with capacity >= 2 * (records + headroom), inserting every live record
 static void map_rebuild(kh_trie* h, uint64_t headroom) {
+  h->pend_valid = false;  // (the rebuild counts the table afresh; the stream has run the tail by its sync)
   hipStream_t st = h->c->st;
   uint64_t cap = 1024;
   while (cap < 2 * (h->rn + headroom) + 1024) cap <<= 1;
@@ -4029,6 +4087,10 @@ struct FCommit {  // one commit's inputs (device buffers)
   // the gather's sync, still before the commit changes anything)
   std::function<void()> before_values;
   hipEvent_t vals_ready = nullptr;
+  // the new roots are on the device (d_tries / d_roots, right after the element build; the
+  // records and the anchor map still follow): kh_block_commit's storage phase injects them
+  // into the account bodies here, so the account phase need not wait for the rest
+  std::function<void(hipStream_t, uint32_t)> after_roots;  // (the stream, the commit's trie count)
 };
 
 static int emit_nodes_dev(kh_ctx* c, DevBuf& out, uint64_t* n_nodes, uint64_t* rlp_len);
@@ -4332,6 +4394,30 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     m = c->T.m;
     if (m != ne) throw KhError{KH_EINTERNAL, "forest: duplicate elements"};
   }
+  // Without a write-back set or a map rebuild, the commit returns as soon as its roots are on
+  // the host; the records and the anchor map follow on the stream (the next call is ordered
+  // after them, trie_settle reads their flags): configs[2]'s account phase ends 0.1 ms sooner
+  trie_settle(h);  // (the previous commit's tail: done by now, stream order)
+  const bool rebuild = ne && 2 * (h->mused + B + m + 1024) > h->mcap;
+  const bool lazy = ne && !keep_em && !rebuild;
+  const size_t o_roots = (size_t)((char*)roots - (char*)tries), o_tail = (size_t)((char*)tail - (char*)tries);
+  uint8_t* hs = nullptr;
+  if (ne && (lazy || F.after_roots)) {  // the roots now (k_f_roots runs again with the final flags below)
+    hipLaunchKernelGGL(k_f_roots, GRID(nt, BS), dim3(BS), 0, st, (const uint64_t*)c->T.res_hash,
+                       (const uint32_t*)c->T.res_len, nt, roots, (const unsigned long long*)c->T.ctr,
+                       (const unsigned long long*)fctr, tail);
+    LAUNCH_CHECK();
+    if (F.after_roots) F.after_roots(st, nt);
+    if (lazy) {
+      if (!h->ev_roots) HIPCHK(hipEventCreateWithFlags(&h->ev_roots, hipEventDisableTiming));
+      if (!h->pend_ev) HIPCHK(hipEventCreateWithFlags(&h->pend_ev, hipEventDisableTiming));
+      if (!h->pend) HIPCHK(hipHostMalloc((void**)&h->pend, 64, hipHostMallocDefault));
+      hs = pinned_stage(c, o_tail + 64);
+      HIPCHK(hipMemcpyAsync(hs, tries, o_tail + 64, hipMemcpyDeviceToHost, st));
+      if (defer && F.chk) HIPCHK(hipMemcpyAsync(c->h_pinned + 8, F.chk, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipEventRecord(h->ev_roots, st));
+    }
+  }
   values_now();  // (no element build: the producer still finishes before the commit does)
   // ---- 5. records: new branches, re-anchored / new elements; the anchor map follows
   const uint64_t nnew = nups;  // every upsert is a new leaf record
@@ -4398,7 +4484,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     LAUNCH_CHECK();
     // map capacity: rebuild when live + tombstones would pass half the table
     h->rn = base_e + nnew;
-    if (2 * (h->mused + B + m + 1024) > h->mcap) {
+    if (rebuild) {
       map_rebuild(h, B + m);
     } else {
       // (the table's load grows by the inserts that took an empty slot: fctr[4], read at the
@@ -4409,10 +4495,17 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
       if (ilog) h->jsegs.back().in = B + m;
       count_fresh = true;
     }
-    hipLaunchKernelGGL(k_f_roots, GRID(nt, BS), dim3(BS), 0, st, (const uint64_t*)T.res_hash,
-                       (const uint32_t*)T.res_len, nt, roots, (const unsigned long long*)T.ctr,
-                       (const unsigned long long*)fctr, tail);
-    LAUNCH_CHECK();
+    if (lazy) {  // the map's flags to the handle's pinned word pair, read by trie_settle
+      HIPCHK(hipMemcpyAsync(h->pend, fctr + 3, 16, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipEventRecord(h->pend_ev, st));
+      h->pend_valid = true;
+      h->pend_fresh = count_fresh;
+    } else {
+      hipLaunchKernelGGL(k_f_roots, GRID(nt, BS), dim3(BS), 0, st, (const uint64_t*)T.res_hash,
+                         (const uint32_t*)T.res_len, nt, roots, (const unsigned long long*)T.ctr,
+                         (const unsigned long long*)fctr, tail);
+      LAUNCH_CHECK();
+    }
   } else {
     journal_begin(ntl, 0);
     if (ntl)
@@ -4448,20 +4541,23 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   h->tries.resize(nt);
   h->roots.resize((uint64_t)nt * 32);
   // (k_f_roots left the final flags in the tail after the roots: one copy)
-  const size_t o_roots = (size_t)((char*)roots - (char*)tries), o_tail = (size_t)((char*)tail - (char*)tries);
-  uint8_t* hs = pinned_stage(c, o_tail + 64);
-  HIPCHK(hipMemcpyAsync(hs, tries, o_tail + 64, hipMemcpyDeviceToHost, st));
-  if (defer && F.chk) HIPCHK(hipMemcpyAsync(c->h_pinned + 8, F.chk, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  if (lazy) {
+    HIPCHK(hipEventSynchronize(h->ev_roots));
+  } else {
+    hs = pinned_stage(c, o_tail + 64);
+    HIPCHK(hipMemcpyAsync(hs, tries, o_tail + 64, hipMemcpyDeviceToHost, st));
+    if (defer && F.chk) HIPCHK(hipMemcpyAsync(c->h_pinned + 8, F.chk, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   // a deferred producer's error word, read at the last sync: the commit has changed the handle
   // by now, so the caller's savepoint takes it back (kh_block_commit always holds one)
   if (defer && F.chk && c->h_pinned[8] == F.chk_tok) throw KhError{KH_EINVAL, F.chk_msg};
   const unsigned long long* ht = (const unsigned long long*)(hs + o_tail);
-  if (count_fresh) h->mused += ht[6];
+  if (!lazy && count_fresh) h->mused += ht[6];
   memcpy(h->tries.data(), hs, (uint64_t)nt * 4);
   memcpy(h->roots.data(), hs + o_roots, (uint64_t)nt * 32);
   if (ne) build_stats_sums(c, ht, &bst);
-  if (ht[5]) throw KhError{KH_EINTERNAL, "anchor map insert failed"};
+  if (!lazy && ht[5]) throw KhError{KH_EINTERNAL, "anchor map insert failed"};
   if (!h->forest) memcpy(h->root, nt ? h->roots.data() : h->root, 32);
   float merge_ms = ev_ms(c->ev[6], c->ev[7]);
   if (stats) {
@@ -4475,6 +4571,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
 
 // ---- versioned commits: savepoint / rollback / release (see Savepoint)
 static void trie_savepoint(kh_trie* h) {
+  trie_settle(h);
   auto sp = std::make_unique<Savepoint>();
   sp->rn = h->rn;
   sp->heap_n = h->heap_n;
@@ -4496,6 +4593,10 @@ static void trie_savepoint(kh_trie* h) {
 // rebuilt (resized) after the savepoint
 static void trie_rollback(kh_trie* h) {
   if (h->sps.empty()) throw KhError{KH_EINVAL, "no open savepoint"};
+  try {
+    trie_settle(h);
+  } catch (const KhError&) {  // (the journal undoes that commit's map writes all the same)
+  }
   hipStream_t st = h->c->st;
   Savepoint& sp = *h->sps.back();
   const bool remap = h->map_epoch != sp.map_epoch;
@@ -4608,6 +4709,7 @@ struct Txn {
 // MerklePatriciaTrie.copy (MerklePatriciaTrie.scala:556): an independent handle holding the
 // current version (records, anchor map, value heap, last roots and write-back set) in HBM
 static kh_trie* trie_copy(kh_trie* h) {
+  trie_settle(h);
   std::unique_ptr<kh_trie> n(new kh_trie());
   n->c = h->c;
   n->flags = h->flags;
@@ -4670,6 +4772,7 @@ __global__ void __launch_bounds__(BS) k_compact_move(Recs R, uint64_t n, const u
 }
 static void trie_compact(kh_trie* h, kh_trie_usage_t* before) {
   if (!h->sps.empty()) throw KhError{KH_EINVAL, "kh_trie_compact: a savepoint is open"};
+  trie_settle(h);
   kh_ctx* c = h->c;
   hipStream_t st = c->st;
   const uint64_t n = h->rn;
@@ -4737,6 +4840,7 @@ static void trie_compact(kh_trie* h, kh_trie_usage_t* before) {
   map_rebuild(h, 1024);  // (syncs; recounts the live records: rdead = 0)
 }
 static void trie_usage(kh_trie* h, kh_trie_usage_t* u) {
+  trie_settle(h);
   kh_ctx* c = h->c;
   hipStream_t st = c->st;
   memset(u, 0, sizeof(*u));
@@ -5999,8 +6103,7 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     const unsigned long long tok = ++c->inject_tok;
     // 2. account.withStateRoot: the new storage roots into the account bodies (the forest's trie
     // list and roots are still on the device: its commit's tbuf)
-    auto inject = [&](hipStream_t s) {
-      const uint32_t nt = (uint32_t)storage->tries.size();
+    auto inject = [&](hipStream_t s, uint32_t nt) {  // nt: the storage commit's touched tries
       if (!(nt && na_up && d_a_up_trie && storage->d_tries)) return false;  // (set by this call's storage commit)
       hipLaunchKernelGGL(k_inject_roots, GRID(na_up, BS), dim3(BS), 0, s, d_a_up_vals, d_a_up_voff, d_a_up_trie,
                          na_up, (const uint32_t*)storage->d_tries, nt, (const uint64_t*)storage->d_roots, err, tok);
@@ -6010,7 +6113,7 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     const bool overlap = KHST_BLOCK_OVERLAP && (ns_up + ns_del) && (na_up + na_del);
     if (!overlap) {
       forest_commit(storage, S, &sst);
-      if (inject(st)) {  // (read back with the account commit's first sync, before it changes anything)
+      if (inject(st, (uint32_t)storage->tries.size())) {  // (read back with the account commit's first sync, before it changes anything)
         A.chk = err;
         A.chk_tok = tok;
       }
@@ -6021,16 +6124,29 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
       kh_ctx* aux = c->bsub;
       std::mutex mu;
       std::condition_variable cv;
-      bool done = false;
+      bool done = false, injected = false;
       std::exception_ptr serr, aerr;
       if (!c->bworker) c->bworker.reset(new Worker());
+      // the injection as soon as the storage roots are on the device (FCommit::after_roots),
+      // before the storage phase's records and anchor map; once, and at the end if the phase
+      // had no element build
+      auto inject_once = [&](hipStream_t s, uint32_t nt) {
+        if (injected) return;
+        inject(s, nt);
+        HIPCHK(hipEventRecord(c->bev, s));
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          injected = true;
+        }
+        cv.notify_all();
+      };
+      S.after_roots = inject_once;
       c->bworker->post([&] {
         try {
           HIPCHK(hipSetDevice(c->dev));
           CtxSwap sw(storage, aux);
           forest_commit(storage, S, &sst);
-          inject(aux->st);
-          HIPCHK(hipEventRecord(c->bev, aux->st));
+          inject_once(aux->st, (uint32_t)storage->tries.size());
         } catch (...) {
           serr = std::current_exception();
         }
@@ -6046,8 +6162,8 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
       A.vals_ready = c->bev;
       A.before_values = [&] {
         std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return done; });
-        if (serr) throw KhError{KH_EINTERNAL, "the block's storage phase failed"};
+        cv.wait(lk, [&] { return injected || done; });
+        if (!injected) throw KhError{KH_EINTERNAL, "the block's storage phase failed"};
       };
       try {
         forest_commit(state, A, &ast);

@@ -6,7 +6,7 @@ tag=$1; shift
 for rep in 1 2; do
 for spec in "$@"; do
   label=${spec%%:*}; envs=${spec#*:}
-  env $envs timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu > gpurun_out/ab_${tag}_${label}_$rep.json 2>/dev/null || exit 1
+  env $envs timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu --no-host-path > gpurun_out/ab_${tag}_${label}_$rep.json 2>/dev/null || exit 1
   python -c "import json;d=json.load(open('gpurun_out/ab_${tag}_${label}_$rep.json'));print('$label', round(d['ms_per_step'],2), d['state_root'][:12], {k: round(v,2) for k,v in d['stage_ms'].items()})"
 done
 done

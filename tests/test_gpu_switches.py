@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
 
 SWITCHES = [
     "KHST_TIE_ONE=1",
+    "KHST_SPEC=0",
     "KHST_PUBLISH_ONE=1",
     "KHST_LEAF_LINKS=1",
     "KHST_LEAF_LINKS=1,KHST_TOPO_TILE=0",

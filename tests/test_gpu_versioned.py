@@ -290,28 +290,32 @@ def test_refused_block_leaves_both_handles_at_parent(khst, oracle):
 
 
 def test_refused_account_descent_rolls_back_storage(khst, oracle):
-    """The account phase's own refusal (an update of a leaf with an empty remaining path,
-    MerklePatriciaTrie.scala:187-199) comes after the storage phase: the forest is rolled
-    back with the state trie."""
+    """The account phase's own refusal (removing a key held by khipu's value-only branch: its
+    fix throws MPTException("Branch with no subvalues"), MerklePatriciaTrie.scala:323-370,
+    430-477) comes after the storage phase: the forest is rolled back with the state trie."""
     from khipu_amd import codec
     from khipu_amd.device import block_commit_host
     keys, vals, state, forest = _host_pair(khst, 150, 23)
     k1 = bytearray(keys[0])
     k1[31] ^= 0x01  # 63 nibbles shared with keys[0]
     body = codec.account_rlp(3, 3)
-    # put k1 (a sibling of keys[0] under a depth-63 branch) in an accepted block
-    block_commit_host(state, forest, None, None, None, None, None, None, np.frombuffer(bytes(k1), np.uint8),
-                      np.frombuffer(body + bytes(8), np.uint8).copy(), np.array([0, len(body)], np.uint64),
-                      np.array([0xFFFFFFFF], np.uint32), None)
+    nt = np.array([0xFFFFFFFF], np.uint32)
+    # put k1 (a sibling of keys[0] under a depth-63 branch), then re-put keys[0]: its leaf
+    # (remaining path empty) becomes a value-only branch
+    for k in (bytes(k1), keys[0]):
+        block_commit_host(state, forest, None, None, None, None, None, None, np.frombuffer(k, np.uint8),
+                          np.frombuffer(body + bytes(8), np.uint8).copy(), np.array([0, len(body)], np.uint64),
+                          nt, None)
     parent_state, parent_last = state.get_root(), forest.last_roots()
     sk = np.frombuffer(bytes(31) + b"\x03", np.uint8)
     with pytest.raises(Exception, match="value-only branch"):
         block_commit_host(state, forest, np.array([5], np.uint32), sk, np.frombuffer(b"\x11" + bytes(8), np.uint8),
-                          np.array([0, 1], np.uint64), None, None, np.frombuffer(keys[0], np.uint8),
+                          np.array([0, 1], np.uint64), None, None, np.frombuffer(keys[1], np.uint8),
                           np.frombuffer(body + bytes(8), np.uint8).copy(), np.array([0, len(body)], np.uint64),
-                          np.array([0xFFFFFFFF], np.uint32), None)
+                          nt, np.frombuffer(keys[0], np.uint8))
     assert state.get_root() == parent_state and forest.last_roots() == parent_last
     assert forest.get([(5, bytes(31) + b"\x03")]) == [None]
+    assert state.get([keys[0]]) == [body]
     state.close()
     forest.close()
 
