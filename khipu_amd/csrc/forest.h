@@ -251,6 +251,7 @@ struct Elems {
   uint8_t* oldd;    // the source record's anchor depth (EL_NEW for an upsert)
   uint64_t* cref;   // [cap*4] the source record's capped reference (rref)
   uint8_t* crl;
+  uint8_t* late;    // its value arrives late (FCommit::late; upserts only)
   unsigned long long* n;  // counter
   uint64_t cap;
 };
@@ -283,6 +284,7 @@ KH_HD void elem_fill(const Recs& R, uint32_t r, uint32_t seg, const Elems& E, ui
   E.oldd[e] = R.rd[r];
   for (int q = 0; q < 4; ++q) E.cref[4 * e + q] = R.rref[4ull * r + q];
   E.crl[e] = R.rrl[r];
+  E.late[e] = 0;
 }
 
 

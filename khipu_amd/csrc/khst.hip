@@ -713,16 +713,20 @@ __device__ __forceinline__ bool leaf_listed(const Topo& T, uint64_t i) {
   const uint32_t a = (uint32_t)(T.lf_pd[i] + 1);
   return !(el_cached(T, i, a) || (el_subtree(T, i) && el_ext_nibbles(T, i, a) == 0));
 }
-__global__ void __launch_bounds__(BS) k_leaf_prep(Topo T, uint32_t* list, unsigned long long* nlist) {
+// pass (element builds with late values, ElemArgs::late): 0 every element; 1 all but the late
+// ones (before their values arrive); 2 only the late ones
+__global__ void __launch_bounds__(BS) k_leaf_prep(Topo T, uint32_t* list, unsigned long long* nlist, int pass) {
   __shared__ uint64_t stage[BS * STAGE_WORDS];
   __shared__ unsigned long long claim[BS / 64 + 1];
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  bool mine = i < T.m;
+  if (pass && mine) mine = (T.el_late[T.sidx[i]] != 0) == (pass == 2);
   const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u;
   uint64_t off = 0;
   uint32_t vlen = 0;
   // (an element build's cached nodes and subtrees are not re-encoded: their values are not
   // staged -- most elements of a block commit, the unchanged siblings on the dirty paths)
-  if (i < T.m && !(T.el_db && (el_subtree(T, i) || el_cached(T, i, (uint32_t)(T.lf_pd[i] + 1))))) {
+  if (mine && !(T.el_db && (el_subtree(T, i) || el_cached(T, i, (uint32_t)(T.lf_pd[i] + 1))))) {
     off = T.svoff[i];
     vlen = T.svlen[i];
   }
@@ -743,14 +747,14 @@ __global__ void __launch_bounds__(BS) k_leaf_prep(Topo T, uint32_t* list, unsign
     }
   }
   __syncthreads();
-  if (i < T.m) {
+  if (mine) {
     if (nw <= STAGE_WORDS)  // two call sites so each keeps its address space (ds_read vs global_load)
       op_leaf_prep(T, i, (const uint8_t*)(stage + threadIdx.x * STAGE_WORDS) + ((off + vmis) & 7), vlen);
     else
       op_leaf_prep(T, i, T.vals + off, vlen);
   }
   if (!list) return;  // (block-uniform) element builds: publish the kept references, list the rest
-  const bool live = i < T.m;
+  const bool live = mine;
   const bool listed = live && leaf_listed(T, i);
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (live && !listed) {
@@ -1846,6 +1850,7 @@ struct BuildArgs {
   bool no_groups = false;          // never split into a grouped build (its own fallback)
   bool no_spec = false;            // no speculative sort (SortIO::speculate): the retry of one that failed
   std::function<void()> before_leaves;  // element builds: called (host) right before the leaves are encoded
+  std::function<bool()> late_ready;     // ... late values (ElemArgs::late) already on their way: one leaf pass
 };
 // element build (forest.h): inputs are leaves and subtree elements; the capped reference
 // of every element node, branch and extension is kept for the forest's records
@@ -1856,6 +1861,9 @@ struct ElemArgs {
   const uint8_t* oldd;   // [n] previous anchor depth (EL_NEW: none)
   const uint64_t* cref;  // [n*4] previous capped reference
   const uint8_t* crl;    // [n]
+  // [n] nullable: the element's value arrives late (kh_block_commit: an account body that gets
+  // its storage root): the other leaves are encoded and hashed before before_leaves
+  const uint8_t* late = nullptr;
   DevBuf* out;           // sorted el_db / el_bref / el_brl and lf_ref / lf_rlen (sized by m)
   DevBuf* outb;          // br_ref / br_rlen, ex_ref / ex_rlen (sized by B)
 };
@@ -2397,6 +2405,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     T.el_oldd = eoldd;
     T.el_cref = ecref;
     T.el_crl = ecrl;
+    T.el_late = E.late;
   }
   if (stage_ev) HIPCHK(hipEventRecord(c->ev[2], st));
 
@@ -2726,17 +2735,28 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     // which k_leaf_hash_list hashes in full waves
     unsigned long long* nlist = A.el ? T.ctr + CTR_LIST : nullptr;
     uint32_t* list = nullptr;
+    // late values still to come: the other leaves first, the late ones after them (when they are
+    // on their way already, one pass: a second costs ~60 us of latency)
+    const bool split = A.el && T.el_late && !(A.late_ready && A.late_ready());
     if (A.el) {
-      c->ws_list.ensure(carve_size({m * 4}));
+      c->ws_list.ensure(carve_size({m * 4, split ? m * 4 : 0}));
       list = (uint32_t*)c->ws_list.p;
     }
+    const uint64_t lblocks = std::max<uint64_t>(std::min<uint64_t>((uint64_t)c->n_cu * 4, (m + BS - 1) / BS), 1);
+    if (split) {
+      hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T, list, nlist, 1);
+      hipLaunchKernelGGL(k_leaf_hash_list, dim3((unsigned)lblocks), dim3(BS), 0, st, T, (const uint32_t*)list,
+                         (const unsigned long long*)nlist);
+      LAUNCH_CHECK();
+      list += m;
+      nlist = T.ctr + CTR_LIST2;
+    }
     if (A.before_leaves) A.before_leaves();  // (a block commit's account values arrive here)
-    hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T, list, nlist);
+    hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T, list, nlist, split ? 2 : 0);
     LAUNCH_CHECK();
     if (A.el) {  // the re-encoded elements hashed from the list
-      const uint64_t lblocks = std::min<uint64_t>((uint64_t)c->n_cu * 4, (m + BS - 1) / BS);
-      hipLaunchKernelGGL(k_leaf_hash_list, dim3((unsigned)std::max<uint64_t>(lblocks, 1)), dim3(BS), 0, st, T,
-                         (const uint32_t*)list, (const unsigned long long*)nlist);
+      hipLaunchKernelGGL(k_leaf_hash_list, dim3((unsigned)lblocks), dim3(BS), 0, st, T, (const uint32_t*)list,
+                         (const unsigned long long*)nlist);
     } else {
       hipLaunchKernelGGL(k_leaf_hash, GRID(m, BS), dim3(BS), 0, st, T);
     }
@@ -3382,7 +3402,8 @@ __global__ void __launch_bounds__(BS) k_f_inputs(const uint64_t* up_keys, uint64
   if (up_trie || del_trie) Tid[o] = up ? up_trie[q] : del_trie[q];
 }
 __device__ __forceinline__ void upsert_elem(const FOps& O, uint64_t o, uint64_t e, uint32_t seg, uint64_t vo,
-                                            uint32_t vl, const Elems& E) {
+                                            uint32_t vl, const Elems& E, bool late = false) {
+  E.late[e] = late ? 1 : 0;
   for (int q = 0; q < 4; ++q) E.key[4 * e + q] = O.key[4 * o + q];
   E.seg[e] = seg;
   E.db[e] = EL_LEAF;
@@ -3397,12 +3418,13 @@ __device__ __forceinline__ void upsert_elem(const FOps& O, uint64_t o, uint64_t 
 }
 __global__ void __launch_bounds__(BS) k_f_upsert_elems(FOps O, const uint32_t* tries, uint32_t nt, const uint32_t* ur,
                                                        const uint64_t* uoff, Elems E, uint64_t heap_base,
-                                                       uint64_t nups) {
+                                                       uint64_t nups, const uint32_t* sidx, const uint32_t* late) {
   uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (o == 0) *E.n = nups;
   if (o >= O.n || O.kind[o] != FOP_UPSERT) return;
   const uint64_t e = ur[o];
-  upsert_elem(O, o, e, seg_of(tries, nt, O.trie[o]), heap_base + uoff[e], (uint32_t)(uoff[e + 1] - uoff[e]), E);
+  upsert_elem(O, o, e, seg_of(tries, nt, O.trie[o]), heap_base + uoff[e], (uint32_t)(uoff[e + 1] - uoff[e]), E,
+              late && late[sidx[o]] != 0xFFFFFFFFu);
 }
 // after the counts are known, CG threads per sorted op o: an upsert's value into the heap at
 // its offset uoff[o] (the exclusive scan of the upsert lengths over the sorted ops) and that
@@ -3416,10 +3438,11 @@ __global__ void __launch_bounds__(BS) k_f_ops_post(FOps O, const uint32_t* sidx,
                                                    const uint8_t* vals, const uint64_t* voff, const uint64_t* uoff,
                                                    uint64_t* uo, uint64_t nups, uint64_t total, uint8_t* heap,
                                                    uint64_t heap_base, const uint32_t* tflag, const uint32_t* tpos,
-                                                   uint32_t* tries, Elems E, bool meta, bool copy) {
+                                                   uint32_t* tries, Elems E, bool meta, int copy,
+                                                   const uint32_t* late) {
   // meta: the trie list, the offsets by rank, the upserts' leaf elements (no value bytes read);
-  // copy: the value bytes into the heap (kh_block_commit defers it until the storage roots are
-  // injected into the account bodies)
+  // copy: the value bytes into the heap -- 1 all, 2 those not late, 3 the late ones (late[s] !=
+  // ~0: kh_block_commit's account bodies that get a storage root; the rest are copied early)
   const uint64_t g = (uint64_t)blockIdx.x * BS + threadIdx.x;
   const uint64_t o = g / CG;
   const uint32_t sub = threadIdx.x % CG;
@@ -3432,11 +3455,13 @@ __global__ void __launch_bounds__(BS) k_f_ops_post(FOps O, const uint32_t* sidx,
   if (O.kind[o] != FOP_UPSERT) return;
   const uint64_t s = sidx[o];
   const uint64_t vl = voff[s + 1] - voff[s];
+  const bool is_late = late && late[s] != 0xFFFFFFFFu;
   if (meta && sub == 0) {
     uo[ur[o]] = uoff[o];
-    upsert_elem(O, o, ur[o], tpos[o] + tflag[o] - 1, heap_base + uoff[o], (uint32_t)vl, E);
+    upsert_elem(O, o, ur[o], tpos[o] + tflag[o] - 1, heap_base + uoff[o], (uint32_t)vl, E, is_late);
   }
-  if (copy) copy_bytes_group(heap + heap_base + uoff[o], vals + voff[s], vl, sub);
+  if (copy == 1 || (copy == 2 && !is_late) || (copy == 3 && is_late))
+    copy_bytes_group(heap + heap_base + uoff[o], vals + voff[s], vl, sub);
 }
 // sorted op o: its kind, the flag of a new trie (the segments of the element build), and for
 // an upsert its rank flag and value length (the heap copy); one launch over the sorted ops.
@@ -4087,6 +4112,11 @@ struct FCommit {  // one commit's inputs (device buffers)
   // the gather's sync, still before the commit changes anything)
   std::function<void()> before_values;
   hipEvent_t vals_ready = nullptr;
+  // deferred values: the upserts whose bodies the producer changes (late[i] != ~0, by upsert
+  // index; kh_block_commit: those naming a storage trie); the rest are copied and their leaves
+  // encoded and hashed before before_values (nullable: every value waits)
+  const uint32_t* late = nullptr;
+  std::function<bool()> late_ready;  // (host) the producer has enqueued the late values already
   // the new roots are on the device (d_tries / d_roots, right after the element build; the
   // records and the anchor map still follow): kh_block_commit's storage phase injects them
   // into the account bodies here, so the account phase need not wait for the rest
@@ -4265,7 +4295,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   auto carve_elems = [&](uint64_t ntl_cap) {
     const uint64_t ecap = (uint64_t)nups + 16 * ntl_cap + nt + 16;
     h->ebuf.ensure(
-        carve_size({ecap * 32, ecap * 4, ecap, ecap * 32, ecap, ecap * 8, ecap * 4, ecap * 4, ecap, ecap * 32, ecap, 64}));
+        carve_size({ecap * 32, ecap * 4, ecap, ecap * 32, ecap, ecap * 8, ecap * 4, ecap * 4, ecap, ecap * 32, ecap, ecap, 64}));
     Carver ce{(char*)h->ebuf.p, 0, h->ebuf.cap};
     E = Elems{};
     E.key = ce.take<uint64_t>(ecap * 4);
@@ -4279,6 +4309,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     E.oldd = ce.take<uint8_t>(ecap);
     E.cref = ce.take<uint64_t>(ecap * 4);
     E.crl = ce.take<uint8_t>(ecap);
+    E.late = ce.take<uint8_t>(ecap);
     E.n = fctr + 5;
     E.cap = ecap;
     return ecap;
@@ -4286,7 +4317,8 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   uint64_t ecap = carve_elems(ntl_guess);
   hipLaunchKernelGGL(k_f_ops_post, GRID(nd * CG, BS), dim3(BS), 0, st, O, (const uint32_t*)S.sidx, (const uint32_t*)ur,
                      F.up_vals, F.up_voff, (const uint64_t*)uoff, uo, (uint64_t)nups, ubytes, (uint8_t*)h->heap.p, hb,
-                     (const uint32_t*)tflag, (const uint32_t*)tpos, tries, E, true, !defer);
+                     (const uint32_t*)tflag, (const uint32_t*)tpos, tries, E, true, !defer ? 1 : F.late ? 2 : 0,
+                     F.late);
   LAUNCH_CHECK();
   // ---- 2. descent: opened branches and touched leaves
   recs_reserve(h, h->rn + 16);
@@ -4299,7 +4331,8 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   auto gather = [&](bool redo) {
     if (redo)  // the upserts' elements again, into the grown buffer
       hipLaunchKernelGGL(k_f_upsert_elems, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)tries, nt,
-                         (const uint32_t*)ur, (const uint64_t*)uo, E, hb, (uint64_t)nups);
+                         (const uint32_t*)ur, (const uint64_t*)uo, E, hb, (uint64_t)nups, (const uint32_t*)S.sidx,
+                         F.late);
     const uint64_t gblocks = std::min<uint64_t>((uint64_t)c->n_cu * 2, (nd * 16 * 8 + GATHER_BS - 1) / GATHER_BS);
     hipLaunchKernelGGL(k_f_gather, dim3((unsigned)std::max<uint64_t>(gblocks, 1)), dim3(GATHER_BS), 0, st, map_of(h),
                        recs_of(h), (const uint32_t*)h->touched.p, (const uint8_t*)h->replaced.p,
@@ -4344,7 +4377,8 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     if (F.vals_ready) HIPCHK(hipStreamWaitEvent(st, F.vals_ready, 0));
     hipLaunchKernelGGL(k_f_ops_post, GRID(nd * CG, BS), dim3(BS), 0, st, O, (const uint32_t*)S.sidx,
                        (const uint32_t*)ur, F.up_vals, F.up_voff, (const uint64_t*)uoff, uo, (uint64_t)nups, ubytes,
-                       (uint8_t*)h->heap.p, hb, (const uint32_t*)tflag, (const uint32_t*)tpos, tries, E, false, true);
+                       (uint8_t*)h->heap.p, hb, (const uint32_t*)tflag, (const uint32_t*)tpos, tries, E, false,
+                       F.late ? 3 : 1, F.late);
     LAUNCH_CHECK();
   };
   // value-only branches (rare: a re-put of a key sharing 63 nibbles with another): their
@@ -4380,7 +4414,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   uint64_t B = 0, m = 0;
   const bool keep_em = h->flags & KH_EMIT_NODES;
   if (ne) {
-    ElemArgs EA{E.db, E.bref, E.brl, E.oldd, E.cref, E.crl, &h->elout, &h->eloutb};
+    ElemArgs EA{E.db, E.bref, E.brl, E.oldd, E.cref, E.crl, (defer && F.late) ? E.late : nullptr, &h->elout, &h->eloutb};
     // encodings are kept (emit path) only when the handle hands out its write-back set;
     // otherwise the fused branch levels (one launch per level, no message arena)
     BuildArgs A{(const uint8_t*)E.key, 32, (const uint8_t*)h->heap.p, (const uint64_t*)E.vo, ne,
@@ -4389,6 +4423,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
     A.el = &EA;
     A.dev_results = true;  // the counters come back with the roots (build_stats below)
     if (defer) A.before_leaves = values_now;
+    if (defer) A.late_ready = F.late_ready;
     run_build(c, A, O2, &bst);
     B = c->last_B;
     m = c->T.m;
@@ -6160,6 +6195,11 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
       A.chk = err;  // (only an injection that failed writes this call's token)
       A.chk_tok = tok;
       A.vals_ready = c->bev;
+      A.late = d_a_up_trie;  // the bodies that get a storage root; the rest are hashed before it
+      A.late_ready = [&] {
+        std::lock_guard<std::mutex> lk(mu);
+        return injected;
+      };
       A.before_values = [&] {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return injected || done; });

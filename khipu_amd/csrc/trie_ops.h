@@ -237,6 +237,7 @@ struct Topo {
   // a SUBTREE standing for an unchanged branch at depth el_db[i] whose capped reference
   // is el_bref / el_brl (its keys all share key i's first el_db nibbles)
   const uint8_t* el_db;     // [m] EL_LEAF or the subtree's branch depth
+  const uint8_t* el_late;   // [n] nullable, INPUT order (via sidx): the element's value arrives late (two leaf passes)
   const uint64_t* el_bref;  // [m*4]
   const uint8_t* el_brl;    // [m]
   const uint8_t* el_oldd;   // [m] anchor depth of the element's node in the previous version (EL_NEW: none)
@@ -270,6 +271,7 @@ constexpr int CTR_LONGN = 16 + 7;  // longlist length (row 1, index 7: unused by
 constexpr int CTR_PYR = 16 + 8;    // k_pyramid's finished-block count (row 1, index 8)
 constexpr int CTR_LIST = 16 + 9;   // element builds: the re-encoded leaves listed by k_leaf_prep
 constexpr int CTR_TLIST = 16 + 10; // k_topo_tile's two list lengths (row 1, indices 10 and 11)
+constexpr int CTR_LIST2 = 16 + 12; // element builds with late values: the late leaves' list (row 1, index 12)
 // counter add returning the old value (the host replay is single-threaded)
 KH_HD unsigned long long ctr_add(unsigned long long* p, unsigned long long v) {
 #ifdef __HIP_DEVICE_COMPILE__
