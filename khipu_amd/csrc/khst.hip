@@ -969,12 +969,6 @@ __global__ void __launch_bounds__(BS) k_leaf_move_part(Topo T, const uint32_t* t
     op_leaf_move(T, i, [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); });
 }
 
-// leaf positions, before a small level (k_branch_xl / k_branch_small copy every child
-// record of a branch at once): the level's leaf children's records from their stashes
-__global__ void __launch_bounds__(BS) k_level_leafrecs(Topo T, uint64_t first, uint64_t cnt) {
-  const uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (t < cnt) op_leaf_children(T, (uint32_t)(first + t));
-}
 
 __global__ void __launch_bounds__(BS) k_leaf_long(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -1079,16 +1073,43 @@ __global__ void __launch_bounds__(64) k_branch_small(Topo T, uint64_t first, uin
     const uint64_t cb = T.br_cbase[j];
     uint64_t r[64];
     uint32_t mm[16];
+    if (T.cend) {  // leaf positions: the leaf children straight from their stashes (op_leaf_children)
+      uint32_t ce[16];
 #pragma unroll
-    for (uint32_t c = 0; c < 16; ++c) {
-      if (c < k) {
-        const ulonglong2* p = (const ulonglong2*)(T.cref + 4 * (cb + c));
-        const ulonglong2 a = p[0], b = p[1];
-        r[4 * c] = a.x;
-        r[4 * c + 1] = a.y;
-        r[4 * c + 2] = b.x;
-        r[4 * c + 3] = b.y;
-        mm[c] = T.cmeta[cb + c];
+      for (uint32_t c = 0; c < 16; ++c) {
+        if (c < k) {
+          mm[c] = T.cmeta[cb + c];
+          ce[c] = T.cend[cb + c];
+        }
+      }
+      const uint32_t d = T.br_depth[j];
+      uint64_t pos = T.br_first[j];
+#pragma unroll
+      for (uint32_t c = 0; c < 16; ++c) {
+        if (c < k) {
+          const bool br = mm[c] & CM_BR;
+          const uint64_t* src = br ? T.cref + 4 * (cb + c) : T.lf_eref + 4 * pos;
+          const ulonglong2 a = ((const ulonglong2*)src)[0], b = ((const ulonglong2*)src)[1];
+          r[4 * c] = a.x;
+          r[4 * c + 1] = a.y;
+          r[4 * c + 2] = b.x;
+          r[4 * c + 3] = b.y;
+          if (!br) mm[c] = (T.lf_inline ? T.lf_emeta[pos] : 32u) | (key_nibble(sorted_key(T, pos, d + 1), (int)d) << 8);
+          pos = br ? ce[c] : pos + 1;
+        }
+      }
+    } else {
+#pragma unroll
+      for (uint32_t c = 0; c < 16; ++c) {
+        if (c < k) {
+          const ulonglong2* p = (const ulonglong2*)(T.cref + 4 * (cb + c));
+          const ulonglong2 a = p[0], b = p[1];
+          r[4 * c] = a.x;
+          r[4 * c + 1] = a.y;
+          r[4 * c + 2] = b.x;
+          r[4 * c + 3] = b.y;
+          mm[c] = T.cmeta[cb + c];
+        }
       }
     }
 #pragma unroll
@@ -1155,13 +1176,31 @@ __global__ void __launch_bounds__(64) k_branch_xl(Topo T, uint64_t first, uint64
   const bool top = T.br_parent[j] == NONE;
   uint32_t len = 0, nib = 0;
   uint64_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  uint32_t mc = 0, ce = 0;
   if (sub < k) {
-    const uint32_t mc = T.cmeta[cb + sub];
-    len = mc & 0xFF;
-    nib = (mc >> 8) & 0xF;
-    const ulonglong2* p = (const ulonglong2*)(T.cref + 4 * (cb + sub));
+    mc = T.cmeta[cb + sub];
+    if (T.cend) ce = T.cend[cb + sub];
+  }
+  // leaf positions: a leaf child's stash is read where it lies -- child c sits right after the
+  // last branch child b before it (at that branch's end, plus c - b - 1), or at the branch's
+  // first key plus c (op_leaf_children, here one lane per child)
+  const bool leafpos = T.cend && sub < k && !(mc & CM_BR);
+  const uint32_t bm = (uint32_t)(__ballot(T.cend && sub < k && (mc & CM_BR)) >> gbase) & 0xFFFFu;
+  const uint32_t below = sub < 16 ? bm & ((1u << sub) - 1) : 0;
+  const int bl = below ? 31 - __builtin_clz(below) : -1;
+  const uint32_t ceb = (uint32_t)__shfl((int)ce, (int)(gbase + (bl < 0 ? 0 : bl)));
+  if (sub < k) {
+    uint64_t pos = 0;
+    if (leafpos) pos = bl < 0 ? (uint64_t)T.br_first[j] + sub : (uint64_t)ceb + (sub - (uint32_t)bl - 1);
+    const ulonglong2* p = (const ulonglong2*)(leafpos ? T.lf_eref + 4 * pos : T.cref + 4 * (cb + sub));
     const ulonglong2 a = p[0], b = p[1];
     r0 = a.x, r1 = a.y, r2 = b.x, r3 = b.y;
+    if (leafpos) {
+      const uint32_t d = T.br_depth[j];
+      mc = (T.lf_inline ? T.lf_emeta[pos] : 32u) | (key_nibble(sorted_key(T, pos, d + 1), (int)d) << 8);
+    }
+    len = mc & 0xFF;
+    nib = (mc >> 8) & 0xF;
   }
   const uint32_t ilen = len == 32 ? 33 : len;
   const uint32_t incl = row16_scan(ilen ? ilen - 1 : 0);  // lanes 0..15 of the group: one DPP row
@@ -2795,10 +2834,9 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
       // (link records, KHST_LEAF_LINKS=1, only through k_branch_fused<5>, which follows them)
       const bool small = !A.kn && !rescan && !T.links && small_levels && cnt <= small_level;
       const bool pos = T.cend && !small;  // leaf children from their stashes
-      if (T.cend && small) {  // leaf positions, a small level: the level's leaf child records first
-        hipLaunchKernelGGL(k_level_leafrecs, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
-        LAUNCH_CHECK();
-      }
+      // (leaf positions, a small level: k_branch_xl / k_branch_small read the leaf children's
+      // stashes themselves, as op_leaf_children restates -- a separate pass writing the level's leaf
+      // child records first cost 5-12 us + a launch per level)
       if (A.kn)
         hipLaunchKernelGGL(k_branch_fused<0>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
       else if (rescan)
