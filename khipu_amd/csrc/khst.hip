@@ -1560,6 +1560,27 @@ __global__ void __launch_bounds__(BS) k_part_count(const uint64_t* K, uint64_t n
   __syncthreads();
   if (threadIdx.x < nparts) hist[(uint64_t)threadIdx.x * ntile + blockIdx.x] = c[threadIdx.x];
 }
+// the owners' record counts (the scanned tile table) and value bytes (the sum of the tiles'
+// byte sums, k_part_place's hbytes): block p for owner p
+__global__ void __launch_bounds__(BS) k_part_bounds_t(const uint32_t* base, const unsigned long long* hbytes,
+                                                      uint32_t ntile, uint64_t n, uint32_t nparts,
+                                                      unsigned long long* cnt, unsigned long long* bytes) {
+  __shared__ unsigned long long part[PT_WAVES];
+  const uint32_t p = blockIdx.x;
+  unsigned long long v = 0;
+  for (uint32_t t = threadIdx.x; t < ntile; t += BS) v += hbytes[(uint64_t)p * ntile + t];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tot = 0;
+    for (uint32_t w = 0; w < PT_WAVES; ++w) tot += part[w];
+    bytes[p] = tot;
+    const uint64_t a = base[(uint64_t)p * ntile];
+    const uint64_t b = p + 1 < nparts ? base[(uint64_t)(p + 1) * ntile] : n;
+    cnt[p] = b - a;
+  }
+}
 // Key hashing with k_part_count folded in (kh_dev_hash_partition_ev): each block hashes
 // BS keys and adds its owner counts into the (owner, tile) table, zeroed beforehand; a tile
 // is PT_R consecutive blocks, as k_part_place reads it
@@ -1605,11 +1626,19 @@ __global__ void __launch_bounds__(BS) k_hash_keys_owner_l(const uint8_t* keys, u
 template <bool V16>
 __global__ void __launch_bounds__(BS) k_part_place(const uint64_t* K, const uint64_t* voff, uint64_t n,
                                                    uint32_t nparts, uint32_t ntile, const uint32_t* base,
-                                                   uint64_t* okeys, uint64_t* olen, uint32_t* pos) {
+                                                   uint64_t* okeys, uint64_t* olen, uint32_t* pos,
+                                                   unsigned long long* hbytes) {
+  // (hbytes, when given: the tile's value bytes per owner -- the owners' byte totals without
+  // a scan of the placed lengths, which then runs after the counts are back)
   __shared__ uint32_t run[16];
   __shared__ uint32_t wc[PT_WAVES][16];
+  __shared__ unsigned long long cb[16];
   const uint32_t wv = threadIdx.x >> 6;
   if (threadIdx.x < 16) run[threadIdx.x] = threadIdx.x < nparts ? base[(uint64_t)threadIdx.x * ntile + blockIdx.x] : 0;
+  if (threadIdx.x < 16) cb[threadIdx.x] = 0;
+  uint64_t acc[16];
+#pragma unroll
+  for (uint32_t q = 0; q < 16; ++q) acc[q] = 0;
   const uint64_t t0 = (uint64_t)blockIdx.x * PT_TILE;
   for (uint32_t r = 0; r < PT_R; ++r) {
     if (threadIdx.x < PT_WAVES * 16) wc[threadIdx.x >> 4][threadIdx.x & 15] = 0;
@@ -1648,6 +1677,8 @@ __global__ void __launch_bounds__(BS) k_part_place(const uint64_t* K, const uint
       }
       olen[d] = len;
     }
+#pragma unroll
+    for (uint32_t q = 0; q < 16; ++q) acc[q] += o == q ? len : 0ull;
     __syncthreads();
     if (threadIdx.x < nparts) {
       uint32_t t = 0;
@@ -1655,6 +1686,16 @@ __global__ void __launch_bounds__(BS) k_part_place(const uint64_t* K, const uint
       run[threadIdx.x] += t;
     }
     __syncthreads();
+  }
+  if (hbytes) {
+#pragma unroll
+    for (uint32_t q = 0; q < 16; ++q) {
+      if (q >= nparts) break;
+      const unsigned long long v = wave_sum((unsigned long long)acc[q]);
+      if ((threadIdx.x & 63) == 0 && v) atomicAdd(&cb[q], v);
+    }
+    __syncthreads();
+    if (threadIdx.x < nparts) hbytes[(uint64_t)threadIdx.x * ntile + blockIdx.x] = cb[threadIdx.x];
   }
 }
 // Value spans to their placed offsets, in source order: one CG-lane group per record
@@ -5374,7 +5415,7 @@ static void partition_impl(kh_ctx* c, void* vals_done, const uint8_t* d_addr, ui
     const uint32_t ntile = (uint32_t)((n + PT_TILE - 1) / PT_TILE);
     const uint64_t nh = (uint64_t)nparts * ntile;
     c->ws3.ensure(carve_size({nh * 4, n * 4, n * 8, scan_scratch_bytes(std::max<uint64_t>(n, nh), 8), 40 * 8,
-                              d_addr ? n * 32 : 0}));
+                              d_addr ? n * 32 : 0, nh * 8}));
     Carver cv{(char*)c->ws3.p, 0, c->ws3.cap};
     uint32_t* hist = cv.take<uint32_t>(nh);
     uint32_t* pos = cv.take<uint32_t>(n);
@@ -5382,6 +5423,11 @@ static void partition_impl(kh_ctx* c, void* vals_done, const uint8_t* d_addr, ui
     void* sc = cv.take<char>(scan_scratch_bytes(std::max<uint64_t>(n, nh), 8));
     unsigned long long* tot = cv.take<unsigned long long>(40);  // counts | bytes | byte total
     const uint64_t* K = (const uint64_t*)d_keys32;
+    // the place pass sums the tiles' value bytes per owner: the counts and bytes go back to the
+    // host before the scan of the placed lengths (that scan, and with vals_done the value copy,
+    // run after the return); the hashing variant counts in its hashing pass and scans first
+    const bool tbytes = d_addr == nullptr;
+    unsigned long long* hbytes = tbytes ? cv.take<unsigned long long>(nh) : nullptr;
     if (d_addr) {  // hashed here, the owners counted in the same pass (no k_part_count re-read)
       uint64_t* hk = cv.take<uint64_t>(n * 4);
       HIPCHK(hipMemsetAsync(hist, 0, nh * 4, st));
@@ -5400,21 +5446,26 @@ static void partition_impl(kh_ctx* c, void* vals_done, const uint8_t* d_addr, ui
     scan_exclusive<uint32_t>(hist, hist, nh, (uint32_t*)nullptr, sc, st);
     if (!(((uintptr_t)K | (uintptr_t)d_out_keys) & 15))
       hipLaunchKernelGGL(k_part_place<true>, dim3(ntile), dim3(BS), 0, st, K, d_voff, n, nparts, ntile,
-                         (const uint32_t*)hist, (uint64_t*)d_out_keys, d_out_vlen, pos);
+                         (const uint32_t*)hist, (uint64_t*)d_out_keys, d_out_vlen, pos, hbytes);
     else
       hipLaunchKernelGGL(k_part_place<false>, dim3(ntile), dim3(BS), 0, st, K, d_voff, n, nparts, ntile,
-                         (const uint32_t*)hist, (uint64_t*)d_out_keys, d_out_vlen, pos);
+                         (const uint32_t*)hist, (uint64_t*)d_out_keys, d_out_vlen, pos, hbytes);
     LAUNCH_CHECK();
-    scan_exclusive<uint64_t>(d_out_vlen, ooff, n, (uint64_t*)(tot + 32), sc, st);
     auto vcopy = [&] {
+      if (tbytes) scan_exclusive<uint64_t>(d_out_vlen, ooff, n, (uint64_t*)(tot + 32), sc, st);
       hipLaunchKernelGGL(k_part_vcopy, GRID(n * CG, BS), dim3(BS), 0, st, d_vals, d_voff, (const uint32_t*)pos,
                          (const uint64_t*)ooff, n, d_out_vals);
       LAUNCH_CHECK();
     };
+    if (!tbytes) scan_exclusive<uint64_t>(d_out_vlen, ooff, n, (uint64_t*)(tot + 32), sc, st);
     if (!vals_done) vcopy();
-    HIPCHK(hipMemsetAsync(tot, 0, 256, st));
-    hipLaunchKernelGGL(k_part_bounds, dim3(1), dim3(64), 0, st, (const uint32_t*)hist, ntile, (const uint64_t*)ooff,
-                       (const uint64_t*)(tot + 32), n, nparts, tot, tot + 16);
+    if (!tbytes) HIPCHK(hipMemsetAsync(tot, 0, 256, st));  // (k_part_bounds_t writes every owner's pair)
+    if (tbytes)
+      hipLaunchKernelGGL(k_part_bounds_t, dim3(nparts), dim3(BS), 0, st, (const uint32_t*)hist,
+                         (const unsigned long long*)hbytes, ntile, n, nparts, tot, tot + 16);
+    else
+      hipLaunchKernelGGL(k_part_bounds, dim3(1), dim3(64), 0, st, (const uint32_t*)hist, ntile, (const uint64_t*)ooff,
+                         (const uint64_t*)(tot + 32), n, nparts, tot, tot + 16);
     LAUNCH_CHECK();
     HIPCHK(hipMemcpyAsync(c->h_pinned, tot, 256, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
