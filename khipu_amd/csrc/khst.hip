@@ -1690,9 +1690,10 @@ __global__ void __launch_bounds__(BS) k_part_place(const uint64_t* K, const uint
   if (hbytes) {
 #pragma unroll
     for (uint32_t q = 0; q < 16; ++q) {
-      if (q >= nparts) break;
-      const unsigned long long v = wave_sum((unsigned long long)acc[q]);
-      if ((threadIdx.x & 63) == 0 && v) atomicAdd(&cb[q], v);
+      if (q < nparts) {
+        const unsigned long long v = wave_sum((unsigned long long)acc[q]);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&cb[q], v);
+      }
     }
     __syncthreads();
     if (threadIdx.x < nparts) hbytes[(uint64_t)threadIdx.x * ntile + blockIdx.x] = cb[threadIdx.x];
