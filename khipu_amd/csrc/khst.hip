@@ -1581,45 +1581,64 @@ __global__ void __launch_bounds__(BS) k_part_bounds_t(const uint32_t* base, cons
     cnt[p] = b - a;
   }
 }
-// Key hashing with k_part_count folded in (kh_dev_hash_partition_ev): each block hashes
-// BS keys and adds its owner counts into the (owner, tile) table, zeroed beforehand; a tile
-// is PT_R consecutive blocks, as k_part_place reads it
+// Key hashing for kh_dev_hash_partition_ev: each key's owner also goes out as one byte, so
+// the count pass (k_part_count_o) reads 1 byte per record instead of the keys' lines
 template <bool SHORT>
 __device__ __forceinline__ void hash_keys_owner(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out,
-                                                uint32_t nparts, uint32_t ntile, uint32_t* hist) {
+                                                uint32_t nparts, uint8_t* owner) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h[4];
+  if (SHORT)
+    kec256_short(keys + i * klen, klen, h);
+  else
+    kec256_msg<false>(keys + i * klen, klen, h);
+  for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
+  owner[i] = (uint8_t)nibble_owner(h[0], nparts);
+}
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(7)))
+k_hash_keys_owner_s(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out, uint32_t nparts, uint8_t* owner) {
+  hash_keys_owner<true>(keys, klen, n, out, nparts, owner);
+}
+__global__ void __launch_bounds__(BS) k_hash_keys_owner_l(const uint8_t* keys, uint32_t klen, uint64_t n,
+                                                          uint64_t* out, uint32_t nparts, uint8_t* owner) {
+  hash_keys_owner<false>(keys, klen, n, out, nparts, owner);
+}
+// k_part_count from the owner bytes: PT_R consecutive records per thread (one 8-byte load),
+// counted per owner in registers, one wave sum and LDS add per owner
+__global__ void __launch_bounds__(BS) k_part_count_o(const uint8_t* owner, uint64_t n, uint32_t nparts, uint32_t ntile,
+                                                     uint32_t* hist) {
+  static_assert(PT_R == 8, "one 8-byte load per thread");
   __shared__ uint32_t c[16];
   if (threadIdx.x < 16) c[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  const bool ok = i < n;
-  uint32_t o = 0;
-  if (ok) {
-    uint64_t h[4];
-    if (SHORT)
-      kec256_short(keys + i * klen, klen, h);
-    else
-      kec256_msg<false>(keys + i * klen, klen, h);
-    for (int j = 0; j < 4; ++j) out[4 * i + j] = h[j];
-    o = nibble_owner(h[0], nparts);
+  const uint64_t i0 = (uint64_t)blockIdx.x * PT_TILE + (uint64_t)threadIdx.x * PT_R;
+  uint64_t w = 0;
+  if (i0 + PT_R <= n) {
+    w = *(const uint64_t*)(owner + i0);
+  } else {
+    for (uint32_t r = 0; r < PT_R; ++r)
+      if (i0 + r < n) w |= (uint64_t)owner[i0 + r] << (8 * r);
   }
-  const uint64_t mask = owner_match(ok, o);
-  if (ok && (mask & lanemask_lt()) == 0) atomicAdd(&c[o], (uint32_t)__popcll(mask));  // one add per group
+  const uint32_t valid = i0 >= n ? 0u : (uint32_t)min<uint64_t>(PT_R, n - i0);
+  uint32_t acc[16];
+#pragma unroll
+  for (uint32_t q = 0; q < 16; ++q) acc[q] = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < PT_R; ++r) {
+    const uint32_t o = (uint32_t)(w >> (8 * r)) & 0xFF;
+#pragma unroll
+    for (uint32_t q = 0; q < 16; ++q) acc[q] += (r < valid && o == q) ? 1u : 0u;
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < 16; ++q) {
+    if (q < nparts) {
+      const uint32_t v = wave_sum(acc[q]);
+      if ((threadIdx.x & 63) == 0 && v) atomicAdd(&c[q], v);
+    }
+  }
   __syncthreads();
-  if (threadIdx.x < nparts && c[threadIdx.x])
-    atomicAdd(&hist[(uint64_t)threadIdx.x * ntile + blockIdx.x / PT_R], c[threadIdx.x]);
-}
-// single-block keys (addresses) held to 7 waves per SIMD, as k_hash_keys runs: the owner
-// count adds 5 VGPRs, which at 77 left it at 6 and made the fused call 0.1-0.5 ms slower
-// than hashing + k_part_count
-__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(7)))
-k_hash_keys_owner_s(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out, uint32_t nparts, uint32_t ntile,
-                    uint32_t* hist) {
-  hash_keys_owner<true>(keys, klen, n, out, nparts, ntile, hist);
-}
-__global__ void __launch_bounds__(BS) k_hash_keys_owner_l(const uint8_t* keys, uint32_t klen, uint64_t n,
-                                                          uint64_t* out, uint32_t nparts, uint32_t ntile,
-                                                          uint32_t* hist) {
-  hash_keys_owner<false>(keys, klen, n, out, nparts, ntile, hist);
+  if (threadIdx.x < nparts) hist[(uint64_t)threadIdx.x * ntile + blockIdx.x] = c[threadIdx.x];
 }
 // V16: keys in and out 16-byte aligned -- each key moved as two 16-byte loads issued before
 // the round's ranking and two 16-byte stores (8-byte words otherwise)
@@ -1628,8 +1647,8 @@ __global__ void __launch_bounds__(BS) k_part_place(const uint64_t* K, const uint
                                                    uint32_t nparts, uint32_t ntile, const uint32_t* base,
                                                    uint64_t* okeys, uint64_t* olen, uint32_t* pos,
                                                    unsigned long long* hbytes) {
-  // (hbytes, when given: the tile's value bytes per owner -- the owners' byte totals without
-  // a scan of the placed lengths, which then runs after the counts are back)
+  // (hbytes: the tile's value bytes per owner -- the owners' byte totals without a scan of
+  // the placed lengths, which then runs after the counts are back)
   __shared__ uint32_t run[16];
   __shared__ uint32_t wc[PT_WAVES][16];
   __shared__ unsigned long long cb[16];
@@ -1687,17 +1706,15 @@ __global__ void __launch_bounds__(BS) k_part_place(const uint64_t* K, const uint
     }
     __syncthreads();
   }
-  if (hbytes) {
 #pragma unroll
-    for (uint32_t q = 0; q < 16; ++q) {
-      if (q < nparts) {
-        const unsigned long long v = wave_sum((unsigned long long)acc[q]);
-        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&cb[q], v);
-      }
+  for (uint32_t q = 0; q < 16; ++q) {
+    if (q < nparts) {
+      const unsigned long long v = wave_sum((unsigned long long)acc[q]);
+      if ((threadIdx.x & 63) == 0 && v) atomicAdd(&cb[q], v);
     }
-    __syncthreads();
-    if (threadIdx.x < nparts) hbytes[(uint64_t)threadIdx.x * ntile + blockIdx.x] = cb[threadIdx.x];
   }
+  __syncthreads();
+  if (threadIdx.x < nparts) hbytes[(uint64_t)threadIdx.x * ntile + blockIdx.x] = cb[threadIdx.x];
 }
 // Value spans to their placed offsets, in source order: one CG-lane group per record
 // (consecutive groups read consecutive source bytes)
@@ -1709,18 +1726,6 @@ __global__ void __launch_bounds__(BS) k_part_vcopy(const uint8_t* vals, const ui
   const uint64_t o = voff[i];
   copy_bytes_group(ovals + ooff[pos[i]], vals + o, voff[i + 1] - o, lane);
 }
-// records and value bytes per owner, from the owner-major scanned tile table (base) and
-// the byte offsets of the placed records (ooff, *tot their total)
-__global__ void k_part_bounds(const uint32_t* base, uint32_t ntile, const uint64_t* ooff, const uint64_t* tot,
-                              uint64_t n, uint32_t nparts, unsigned long long* cnt, unsigned long long* bytes) {
-  const uint32_t p = threadIdx.x;
-  if (p >= nparts) return;
-  const uint64_t a = base[(uint64_t)p * ntile];
-  const uint64_t b = p + 1 < nparts ? base[(uint64_t)(p + 1) * ntile] : n;
-  cnt[p] = b - a;
-  bytes[p] = (b < n ? ooff[b] : *tot) - (a < n ? ooff[a] : *tot);
-}
-
 __global__ void __launch_bounds__(BS) k_synth_len(uint32_t cfg, uint64_t first, uint64_t n, uint64_t* voff) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i > n) return;
@@ -5416,7 +5421,7 @@ static void partition_impl(kh_ctx* c, void* vals_done, const uint8_t* d_addr, ui
     const uint32_t ntile = (uint32_t)((n + PT_TILE - 1) / PT_TILE);
     const uint64_t nh = (uint64_t)nparts * ntile;
     c->ws3.ensure(carve_size({nh * 4, n * 4, n * 8, scan_scratch_bytes(std::max<uint64_t>(n, nh), 8), 40 * 8,
-                              d_addr ? n * 32 : 0, nh * 8}));
+                              d_addr ? n * 32 : 0, nh * 8, d_addr ? n + 16 : 0}));
     Carver cv{(char*)c->ws3.p, 0, c->ws3.cap};
     uint32_t* hist = cv.take<uint32_t>(nh);
     uint32_t* pos = cv.take<uint32_t>(n);
@@ -5426,18 +5431,17 @@ static void partition_impl(kh_ctx* c, void* vals_done, const uint8_t* d_addr, ui
     const uint64_t* K = (const uint64_t*)d_keys32;
     // the place pass sums the tiles' value bytes per owner: the counts and bytes go back to the
     // host before the scan of the placed lengths (that scan, and with vals_done the value copy,
-    // run after the return); the hashing variant counts in its hashing pass and scans first
-    const bool tbytes = d_addr == nullptr;
-    unsigned long long* hbytes = tbytes ? cv.take<unsigned long long>(nh) : nullptr;
-    if (d_addr) {  // hashed here, the owners counted in the same pass (no k_part_count re-read)
+    // run after the return)
+    unsigned long long* hbytes = cv.take<unsigned long long>(nh);
+    if (d_addr) {  // hashed here, each owner written as a byte that the count pass reads
       uint64_t* hk = cv.take<uint64_t>(n * 4);
-      HIPCHK(hipMemsetAsync(hist, 0, nh * 4, st));
+      uint8_t* ob = cv.take<uint8_t>(n + 16);
       if (klen <= 135)
-        hipLaunchKernelGGL(k_hash_keys_owner_s, GRID(n, BS), dim3(BS), 0, st, d_addr, klen, n, hk, nparts, ntile,
-                           hist);
+        hipLaunchKernelGGL(k_hash_keys_owner_s, GRID(n, BS), dim3(BS), 0, st, d_addr, klen, n, hk, nparts, ob);
       else
-        hipLaunchKernelGGL(k_hash_keys_owner_l, GRID(n, BS), dim3(BS), 0, st, d_addr, klen, n, hk, nparts, ntile,
-                           hist);
+        hipLaunchKernelGGL(k_hash_keys_owner_l, GRID(n, BS), dim3(BS), 0, st, d_addr, klen, n, hk, nparts, ob);
+      LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_part_count_o, dim3(ntile), dim3(BS), 0, st, (const uint8_t*)ob, n, nparts, ntile, hist);
       LAUNCH_CHECK();
       K = hk;
     } else {
@@ -5453,20 +5457,14 @@ static void partition_impl(kh_ctx* c, void* vals_done, const uint8_t* d_addr, ui
                          (const uint32_t*)hist, (uint64_t*)d_out_keys, d_out_vlen, pos, hbytes);
     LAUNCH_CHECK();
     auto vcopy = [&] {
-      if (tbytes) scan_exclusive<uint64_t>(d_out_vlen, ooff, n, (uint64_t*)(tot + 32), sc, st);
+      scan_exclusive<uint64_t>(d_out_vlen, ooff, n, (uint64_t*)(tot + 32), sc, st);
       hipLaunchKernelGGL(k_part_vcopy, GRID(n * CG, BS), dim3(BS), 0, st, d_vals, d_voff, (const uint32_t*)pos,
                          (const uint64_t*)ooff, n, d_out_vals);
       LAUNCH_CHECK();
     };
-    if (!tbytes) scan_exclusive<uint64_t>(d_out_vlen, ooff, n, (uint64_t*)(tot + 32), sc, st);
     if (!vals_done) vcopy();
-    if (!tbytes) HIPCHK(hipMemsetAsync(tot, 0, 256, st));  // (k_part_bounds_t writes every owner's pair)
-    if (tbytes)
-      hipLaunchKernelGGL(k_part_bounds_t, dim3(nparts), dim3(BS), 0, st, (const uint32_t*)hist,
-                         (const unsigned long long*)hbytes, ntile, n, nparts, tot, tot + 16);
-    else
-      hipLaunchKernelGGL(k_part_bounds, dim3(1), dim3(64), 0, st, (const uint32_t*)hist, ntile, (const uint64_t*)ooff,
-                         (const uint64_t*)(tot + 32), n, nparts, tot, tot + 16);
+    hipLaunchKernelGGL(k_part_bounds_t, dim3(nparts), dim3(BS), 0, st, (const uint32_t*)hist,
+                       (const unsigned long long*)hbytes, ntile, n, nparts, tot, tot + 16);
     LAUNCH_CHECK();
     HIPCHK(hipMemcpyAsync(c->h_pinned, tot, 256, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));

@@ -70,9 +70,10 @@ class GpuBackend:
         return pk, pv, pl, cnt[:nparts].astype(np.int64), nb[:nparts].astype(np.int64)
 
     def hash_partition(self, addr, vals, voff, n, nparts, klen=20):
-        """hash_keys + partition in one library call (kh_dev_hash_partition_ev: the owners
-        are counted in the hashing pass); same outputs and overlap as partition().  Not what
-        the step runs: measured slower than the two calls (scripts/shard_rank_sim.py)."""
+        """hash_keys + partition in one library call (kh_dev_hash_partition_ev: the hashing
+        pass writes each key's owner as a byte, which the count pass reads instead of the
+        keys' lines); same outputs and overlap as partition().  What the step runs at N > 1
+        (scripts/shard_rank_sim.py times both forms)."""
         from ._lib import check, lib
         from .device import _ptr
         pk = torch.empty(n * 32 + 64, dtype=torch.uint8, device=self.device)
@@ -238,16 +239,22 @@ def sharded_root(be, addr, vals, voff, n, klen=20, keys_prehashed=False, phases=
             be.sync()
             t.append(time.perf_counter())
 
-    keys32 = addr if keys_prehashed else be.hash_keys(addr, n, klen)
-    mark()
     if world == 1:  # nothing to route: the build reads the records where they are
+        keys32 = addr if keys_prehashed else be.hash_keys(addr, n, klen)
+        mark()
         rk, rv, ro, m, ready = keys32, vals, voff, n, None
         mark()
         mark()
     else:
-        # (hashing and partition as two calls: the fused kh_dev_hash_partition_ev measured
-        # 0.1-0.3 ms slower per rank, profiles/r3t_shard_rank_sim_world*.json)
-        pk, pv, pl, cnt, nb = be.partition(keys32, vals, voff, n, world)
+        if keys_prehashed:
+            mark()
+            pk, pv, pl, cnt, nb = be.partition(addr, vals, voff, n, world)
+        else:
+            # hashing and partition in one call (kh_dev_hash_partition_ev: the hashing pass
+            # writes each key's owner byte, the count pass reads those instead of the keys;
+            # profiles/r4aw_hash_partition_ab_world8.json)
+            pk, pv, pl, cnt, nb = be.hash_partition(addr, vals, voff, n, world, klen)
+            mark()
         mark()
         rk, rv, ro, m, ready = exchange(be, pk, pv, pl, cnt, nb)
         mark()

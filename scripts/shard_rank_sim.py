@@ -3,8 +3,8 @@
   hash      kec256 of the rank's 100M/N slice of the addresses;
   partition the slice into N owners (kh_dev_partition_ev: keys, lengths, counts; the value
             copy, which the step overlaps with the key exchange, is timed on its own); and
-            both in one call (kh_dev_hash_partition_ev, the owners counted in the hashing
-            pass; measured slower, so the step does not use it);
+            both in one call (kh_dev_hash_partition_ev: the hashing pass writes each key's
+            owner byte for the count pass -- what the step runs since round 4);
   build     the OWNER-SHAPED shard from nibble 1 (depth0 = 1): the records of all 100M
             accounts whose top key nibble q has q * N >> 4 == 0 -- exactly what rank 0
             receives (100M/N records under 16/N root nibbles), not the rank's own slice.
@@ -69,7 +69,7 @@ def main():
         hh, ll, ii = be.build(sk, sv, so, m, depth0=1)
         be.sync()
         t4 = time.perf_counter()
-        be.hash_partition(addr, vals, voff, n, N)  # hashing + partition in one call (measured, not run by the step)
+        be.hash_partition(addr, vals, voff, n, N)  # hashing + partition in one call (the step's form)
         t5 = time.perf_counter()
         be.vals_done.synchronize()
         be.sync()
@@ -83,8 +83,10 @@ def main():
     out = {"world": N, "records_per_rank": n, "shard_records": m,
            "shard_nibbles": [q for q in range(16) if (q * N) >> 4 == 0],
            "ms": med,
-           "critical_path_ms_excl_exchange": round(med["hash_keys"] + med["partition_keys"] + med["build"], 3),
-           "critical_path_ms_excl_exchange_fused": round(med["hash_partition_keys"] + med["build"], 3),
+           # the step's form (sharded.sharded_root: one hash + partition call), and the two calls
+           "critical_path_ms_excl_exchange": round(med["hash_partition_keys"] + med["build"], 3),
+           "critical_path_ms_excl_exchange_two_calls": round(med["hash_keys"] + med["partition_keys"] + med["build"],
+                                                             3),
            "build_stages_ms": {"sort": st.t_sort_ms, "topology": st.t_topo_ms, "leaves": st.t_leaf_ms,
                                "branches": st.t_branch_ms, "total": st.t_total_ms},
            "subtrie_refs_occupied": int((ll > 0).sum()),

@@ -331,7 +331,7 @@ def test_partition_keys_8byte_aligned(khst):
 
 @pytest.mark.parametrize("nparts", [2, 8, 16])
 def test_hash_partition_vs_host(khst, oracle, nparts):
-    """kh_dev_hash_partition_ev (the keys kec256'd in the pass that counts the owners) ==
+    """kh_dev_hash_partition_ev (the keys kec256'd in a pass that writes each owner byte) ==
     the oracle's kec256 of every address, partitioned stably by top-nibble owner: keys,
     lengths, value bytes, counts and bytes per owner; 20-byte addresses (the short
     single-block hash), 200-byte keys (multi-block), n not a multiple of the 2,048-record

@@ -34,6 +34,10 @@ class CpuBackend:
                 np.frombuffer(self.emu.kec256(a[klen * i:klen * i + klen].tobytes()), np.uint8).copy())
         return out
 
+    def hash_partition(self, addr, vals, voff, n, nparts, klen=20):
+        """GpuBackend.hash_partition's outputs: the two calls in turn"""
+        return self.partition(self.hash_keys(addr, n, klen), vals, voff, n, nparts)
+
     def partition(self, keys32, vals, voff, n, nparts):
         k = keys32[:n * 32].numpy().reshape(n, 32)
         vo = voff.numpy()
