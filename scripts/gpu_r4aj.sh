@@ -2,7 +2,7 @@
 # Round 4 final measurement set: the N = 1 bench line (CPU legs, host path), its kernel trace,
 # configs[1..3] (scripts/bench_configs.py), lists / storage / verify lines, world-8 simulation
 export TMPDIR=/tmp
-tag=${1:-r4aj}
+tag=${1:-r4ay}
 step() { local name=$1; shift; "$@"; local rc=$?; echo "${name}_RC=$rc" >&2; [ $rc -eq 0 ] || exit $rc; }
 step BENCH timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err
 cut -c1-300 gpurun_out/${tag}_bench.json
