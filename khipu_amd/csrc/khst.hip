@@ -1272,17 +1272,59 @@ __global__ void __launch_bounds__(64) k_branch_xl(Topo T, uint64_t first, uint64
     const uint32_t l = (uint32_t)__shfl((int)lo, (int)(gbase + q)), h = (uint32_t)__shfl((int)hi, (int)(gbase + q));
     hb[q] = hashit ? ((uint64_t)h << 32) | l : 0;
   }
-  if (sub != 0) return;
-  T.br_len[j] = L;
   uint64_t bhead[4] = {0, 0, 0, 0};
-  if (L < 32)
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t base = 8u * (uint32_t)q;
-      bhead[q] = base < L ? E[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0;
+  uint32_t ninl = hashit ? 0 : 1, perms = hashit ? nfull + 1 : 0;
+  if (sub == 0) {
+    T.br_len[j] = L;
+    if (L < 32)
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t base = 8u * (uint32_t)q;
+        bhead[q] = base < L ? E[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0;
+      }
+    branch_keep(T, j, L, hb, bhead);
+  }
+  if (ext == 0) {
+    if (sub != 0) return;
+    perms += branch_publish(T, j, L, hb, bhead, Slot{E, 1}, &ninl);
+  } else {
+    // the extension above it: lane 0 encodes it into the group's (zeroed) LDS words and the
+    // permutation runs spread over the group too, as the branch's did (one lane's
+    // permutation here was the level's longest step)
+    PubCtx P;
+    uint32_t XL = 0;
+    xl_sync();  // (lane 0 has read the branch encoding's head)
+    if (sub < 17) E[sub] = 0;
+    xl_sync();
+    if (sub == 0) {
+      P = pub_ctx(T, j);
+      pub_cend(T, j, P);
+      XL = ext_encode(T, j, P, L, hb, bhead, Slot{E, 1});
     }
-  uint32_t ninl = hashit ? 0 : 1;
-  branch_keep(T, j, L, hb, bhead);
-  const uint32_t perms = (hashit ? nfull + 1 : 0) + branch_publish(T, j, L, hb, bhead, Slot{E, 1}, &ninl);
+    XL = (uint32_t)__shfl((int)XL, (int)gbase);
+    xl_sync();
+    const bool xhash = XL >= 32 || top;
+    uint32_t xlo = 0, xhi = 0;
+    if (xhash) {
+      const XLane X = xlane_setup(sub);
+      if (sub < 17) {
+        uint64_t w = E[sub];
+        if ((XL >> 3) == sub) w ^= 0x01ULL << (8 * (XL & 7));
+        if (sub == 16) w ^= 0x80ULL << 56;
+        xlo = (uint32_t)w;
+        xhi = (uint32_t)(w >> 32);
+      }
+      keccakf_xlane(xlo, xhi, kb[g], X);
+    }
+    uint64_t hx[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t l = (uint32_t)__shfl((int)xlo, (int)(gbase + q)), h = (uint32_t)__shfl((int)xhi, (int)(gbase + q));
+      hx[q] = xhash ? ((uint64_t)h << 32) | l : 0;
+    }
+    if (sub != 0) return;
+    ext_finish(T, j, P, XL, hx, Slot{E, 1}, &ninl);
+    perms += xhash ? 1 : 0;
+  }
   atomicAdd(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), (unsigned long long)perms);
   atomicAdd(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), (unsigned long long)branch_hash_count(T, j, perms));
   if (ninl) atomicAdd(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), (unsigned long long)ninl);

@@ -1582,24 +1582,39 @@ struct WinBW {
 // ---- extension (if any) + publish of branch j whose reference is (L, hb, bhead): an
 // extension [HP(nibbles pd+1 .. d-1, ext), ref(branch)] is encoded into xs and hashed.
 // Returns the permutations spent on the extension; *ninl counts inline nodes.
-KH_HD uint32_t branch_publish(const Topo& T, uint32_t j, uint32_t L, const uint64_t hb[4], const uint64_t bhead[4],
-                              Slot xs, uint32_t* ninl) {
-  uint32_t ext = T.br_ext[j];
-  uint32_t parent = T.br_parent[j];
-  uint64_t first = T.br_first[j];
-  uint32_t d = T.br_depth[j];
-  int32_t pd = (int32_t)d - (int32_t)ext - 1;
-  bool top = parent == NONE;
-  const Key4 key = sorted_key(T, first, d);
-  uint32_t nib = top ? 0 : key_nibble(key, pd);
-  const uint16_t mf = T.cend ? CM_BR : 0;
-  if (T.cend && !top) T.cend[(uint64_t)T.br_cbase[parent] + T.br_pord[j]] = T.br_end[j];
-  if (ext == 0) {
-    publish_ref(T, parent, T.br_pord[j], nib, first, bhead, L, hb, mf);
-    return 0;
-  }
-  uint32_t s = (uint32_t)(pd + 1);
-  uint32_t hl = ext / 2 + 1;  // HP bytes
+// where branch j's reference goes: its parent (or the result slot), its nibble there, and
+// the extension above it (branch_publish, and k_branch_xl's split form)
+struct PubCtx {
+  uint32_t ext, parent, d;
+  int32_t pd;
+  bool top;
+  uint64_t first;
+  Key4 key;
+  uint32_t nib;
+  uint16_t mf;
+};
+KH_HD PubCtx pub_ctx(const Topo& T, uint32_t j) {
+  PubCtx P;
+  P.ext = T.br_ext[j];
+  P.parent = T.br_parent[j];
+  P.first = T.br_first[j];
+  P.d = T.br_depth[j];
+  P.pd = (int32_t)P.d - (int32_t)P.ext - 1;
+  P.top = P.parent == NONE;
+  P.key = sorted_key(T, P.first, P.d);
+  P.nib = P.top ? 0 : key_nibble(P.key, P.pd);
+  P.mf = T.cend ? CM_BR : 0;
+  return P;
+}
+// leaf positions: the branch's end position beside its record in the parent
+KH_HD void pub_cend(const Topo& T, uint32_t j, const PubCtx& P) {
+  if (T.cend && !P.top) T.cend[(uint64_t)T.br_cbase[P.parent] + T.br_pord[j]] = T.br_end[j];
+}
+// the extension's encoding (HP path + the branch's reference) into xs; its length (T.ex_len)
+KH_HD uint32_t ext_encode(const Topo& T, uint32_t j, const PubCtx& P, uint32_t L, const uint64_t hb[4],
+                          const uint64_t bhead[4], Slot xs) {
+  uint32_t s = (uint32_t)(P.pd + 1);
+  uint32_t hl = P.ext / 2 + 1;  // HP bytes
   uint32_t refl = L >= 32 ? 33 : L;
   uint32_t hpl = hl == 1 ? 1 : 1 + hl;  // first HP byte 0x00 / 0x1_ < 0x80
   uint32_t xpay = hpl + refl;
@@ -1607,21 +1622,25 @@ KH_HD uint32_t branch_publish(const Topo& T, uint32_t j, uint32_t L, const uint6
   x.len_prefix(xpay, 0xC0);
   if (hl > 1) x.put1(0x80 + hl);
   uint32_t q = s;
-  if (ext & 1) {
-    x.put1(0x10u | key_nibble(key, (int)q));
+  if (P.ext & 1) {
+    x.put1(0x10u | key_nibble(P.key, (int)q));
     ++q;
   } else {
     x.put1(0x00);
   }
-  for (; q < d; q += 2) x.put1((key_nibble(key, (int)q) << 4) | key_nibble(key, (int)q + 1));
+  for (; q < P.d; q += 2) x.put1((key_nibble(P.key, (int)q) << 4) | key_nibble(P.key, (int)q + 1));
   uint64_t bref[4];
   for (int t = 0; t < 4; ++t) bref[t] = L >= 32 ? hb[t] : bhead[t];
   bw_ref(x, bref, L >= 32 ? 32 : L);
   x.flush();
   uint32_t XL = rlp_hdr_len(xpay) + xpay;
   T.ex_len[j] = XL;
-  uint64_t hx[4], xhead[4];
-  uint32_t perms = hash_slot(xs, XL, top, hx);
+  return XL;
+}
+// the extension's hash hx (or its inline encoding, read from xs) kept and published
+KH_HD void ext_finish(const Topo& T, uint32_t j, const PubCtx& P, uint32_t XL, const uint64_t hx[4], Slot xs,
+                      uint32_t* ninl) {
+  uint64_t xhead[4];
   slot_head(xs, XL, xhead);
   if (T.ex_hash)
     for (int q2 = 0; q2 < 4; ++q2) T.ex_hash[4 * j + q2] = hx[q2];
@@ -1633,8 +1652,21 @@ KH_HD uint32_t branch_publish(const Topo& T, uint32_t j, uint32_t L, const uint6
     }
     T.ex_rlen[j] = XL;
   }
-  *ninl += (XL < 32 && !top) ? 1 : 0;
-  publish_ref(T, parent, T.br_pord[j], nib, first, xhead, XL, hx, mf);
+  *ninl += (XL < 32 && !P.top) ? 1 : 0;
+  publish_ref(T, P.parent, T.br_pord[j], P.nib, P.first, xhead, XL, hx, P.mf);
+}
+KH_HD uint32_t branch_publish(const Topo& T, uint32_t j, uint32_t L, const uint64_t hb[4], const uint64_t bhead[4],
+                              Slot xs, uint32_t* ninl) {
+  const PubCtx P = pub_ctx(T, j);
+  pub_cend(T, j, P);
+  if (P.ext == 0) {
+    publish_ref(T, P.parent, T.br_pord[j], P.nib, P.first, bhead, L, hb, P.mf);
+    return 0;
+  }
+  const uint32_t XL = ext_encode(T, j, P, L, hb, bhead, xs);
+  uint64_t hx[4];
+  const uint32_t perms = hash_slot(xs, XL, P.top, hx);
+  ext_finish(T, j, P, XL, hx, xs, ninl);
   return perms;
 }
 
