@@ -1,5 +1,5 @@
 #!/bin/bash
-# k_branch_xl hashes a branch's extension with the lane-spread permutation (it was one lane's):
+# k_branch_xl: the extension hashed lane-spread (r4bc) and the publish context loaded up front (r4bd):
 # GPU suite, then configs[2] block commits, the world-8 simulation and the 100M step, alternated
 # with the HEAD build (scripts/build_ab_base.sh)
 export TMPDIR=/tmp
