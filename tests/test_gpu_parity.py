@@ -335,12 +335,12 @@ def test_hash_partition_vs_host(khst, oracle, nparts):
     the oracle's kec256 of every address, partitioned stably by top-nibble owner: keys,
     lengths, value bytes, counts and bytes per owner; 20-byte addresses (the short
     single-block hash), 200-byte keys (multi-block), n not a multiple of the 2,048-record
-    tile, and the empty batch."""
+    tile nor of the count pass's 8 owner bytes per thread (1, 7, 2,049), and the empty batch."""
     import torch
     from khipu_amd import sharded
     rng = np.random.default_rng(100 + nparts)
     be = sharded.GpuBackend(0)
-    for klen, n in ((20, 0), (20, 5_000), (20, 70_001), (200, 3_001)):
+    for klen, n in ((20, 0), (20, 1), (20, 7), (20, 2_049), (20, 5_000), (20, 70_001), (200, 3_001)):
         lens = rng.integers(0, 120, n).astype(np.int64)
         vo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
         v = rng.integers(0, 256, int(vo[-1]) + 64, dtype=np.uint8)
