@@ -715,12 +715,27 @@ __device__ __forceinline__ bool leaf_listed(const Topo& T, uint64_t i) {
 }
 // pass (element builds with late values, ElemArgs::late): 0 every element; 1 all but the late
 // ones (before their values arrive); 2 only the late ones
-__global__ void __launch_bounds__(BS) k_leaf_prep(Topo T, uint32_t* list, unsigned long long* nlist, int pass) {
+// pass 0: every element; 1: those whose value is not late, the late ones listed into (late,
+// *nlate); 2: the listed late ones only (thread t: late[t]), each hashed here rather than
+// listed for k_leaf_hash_list -- the late values arrive last, and a pass over every element
+// plus a hash launch after them was ~60 us on the block commit's critical path
+__global__ void __launch_bounds__(BS) k_leaf_prep(Topo T, uint32_t* list, unsigned long long* nlist, int pass,
+                                                  uint32_t* late, unsigned long long* nlate) {
   __shared__ uint64_t stage[BS * STAGE_WORDS];
-  __shared__ unsigned long long claim[BS / 64 + 1];
+  __shared__ unsigned long long claim[BS / 64 + 1], claim2[BS / 64 + 1];
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (pass == 2) {
+    const uint64_t nl = *nlate;
+    if ((uint64_t)blockIdx.x * BS >= nl) return;  // (block-uniform)
+    i = i < nl ? late[i] : T.m;
+  }
   bool mine = i < T.m;
-  if (pass && mine) mine = (T.el_late[T.sidx[i]] != 0) == (pass == 2);
+  if (pass == 1) {
+    const bool is_late = mine && T.el_late[T.sidx[i]] != 0;
+    const uint64_t e = block_claim(nlate, is_late, claim2);
+    if (is_late) late[e] = (uint32_t)i;
+    mine = mine && !is_late;
+  }
   const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u;
   uint64_t off = 0;
   uint32_t vlen = 0;
@@ -755,7 +770,7 @@ __global__ void __launch_bounds__(BS) k_leaf_prep(Topo T, uint32_t* list, unsign
   }
   if (!list) return;  // (block-uniform) element builds: publish the kept references, list the rest
   const bool live = mine;
-  const bool listed = live && leaf_listed(T, i);
+  const bool listed = live && pass != 2 && leaf_listed(T, i);
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (live && !listed) {
     uint32_t in1 = 0;
@@ -2872,17 +2887,17 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     }
     const uint64_t lblocks = std::max<uint64_t>(std::min<uint64_t>((uint64_t)c->n_cu * 4, (m + BS - 1) / BS), 1);
     if (split) {
-      hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T, list, nlist, 1);
+      hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T, list, nlist, 1, list + m, T.ctr + CTR_LIST2);
       hipLaunchKernelGGL(k_leaf_hash_list, dim3((unsigned)lblocks), dim3(BS), 0, st, T, (const uint32_t*)list,
                          (const unsigned long long*)nlist);
       LAUNCH_CHECK();
-      list += m;
-      nlist = T.ctr + CTR_LIST2;
     }
     if (A.before_leaves) A.before_leaves();  // (a block commit's account values arrive here)
-    hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T, list, nlist, split ? 2 : 0);
+    hipLaunchKernelGGL(k_leaf_prep, GRID(m, BS), dim3(BS), 0, st, T, list, nlist, split ? 2 : 0, list + m,
+                       T.ctr + CTR_LIST2);
     LAUNCH_CHECK();
-    if (A.el) {  // the re-encoded elements hashed from the list
+    if (split) {  // (the late leaves were hashed by the pass itself)
+    } else if (A.el) {  // the re-encoded elements hashed from the list
       hipLaunchKernelGGL(k_leaf_hash_list, dim3((unsigned)lblocks), dim3(BS), 0, st, T, (const uint32_t*)list,
                          (const unsigned long long*)nlist);
     } else {
