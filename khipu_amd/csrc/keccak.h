@@ -132,8 +132,19 @@ KH_HD void keccak_round(KState& S, uint64_t rc) {
   S.hi[0] ^= (uint32_t)(rc >> 32);
 }
 
+// U rounds per loop iteration.  8 (3 iterations; the pi renaming costs ~5 moves per round, 42
+// per back-edge) by default: the branch kernels inline several permutations, and at 24 their
+// code outgrows the instruction cache (58 -> 129 KB; branch levels 1.0 ms longer at 100M).
+// 24, straight-line, in the leaf kernel (op_leaf_core): no moves, 78 -> 69 VGPRs, 7 waves per
+// SIMD, 15.6 -> 14.8 ms at 100M.  Key hashing measured no faster straight-line (8 waves per
+// SIMD at 61 VGPRs; profiles/r4bp_keccak_unroll_ab_100m.json)
+#ifndef KECCAK_LOOP_ROUNDS
+#define KECCAK_LOOP_ROUNDS 8  // (measurement builds: -DKECCAK_LOOP_ROUNDS=24 unrolls every permutation)
+#endif
+constexpr int KECCAK_LOOP = KECCAK_LOOP_ROUNDS, KECCAK_FULL = 24;
+template <int U = KECCAK_LOOP>
 KH_HD void keccakf(KState& s) {
-#pragma unroll 8  // 3 iterations: the pi renaming costs ~5 moves/round (42 per back-edge)
+#pragma unroll U
   for (int r = 0; r < 24; ++r) keccak_round(s, round_constant(r));
 }
 

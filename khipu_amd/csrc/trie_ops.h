@@ -1331,7 +1331,7 @@ KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, u
   uint64_t* r = T.lf_eref + 4 * si;
   uint32_t perms = 0;
   if (L >= 32 || top) {  // a leaf embedded in its parent is never hashed (Node.scala:114)
-    keccakf(S);
+    keccakf<KECCAK_FULL>(S);
     for (int q = 0; q < 4; ++q) r[q] = lane(S, q);
     perms = 1;
   } else {  // the encoding itself: the message words without the padding byte at L (< 32);
