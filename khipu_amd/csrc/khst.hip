@@ -867,8 +867,11 @@ __device__ __forceinline__ void wave_count(unsigned long long* dst, bool f) {
 // their message shifts, and the message is assembled dword by dword (v_perm_b32) straight
 // into the Keccak state.  Every lane of a wave runs the wave-bound reductions, so threads
 // past n take part with neutral values.
-// 78 VGPRs, 6 waves per SIMD.  Forced to 7 waves (72 VGPRs, no spills) it runs 1.0 ms slower
-// in the step (profiles/r3l_occupancy_ab_100m.json), as key hashing forced to 8 (+2 ms).
+// 69 VGPRs, 7 waves per SIMD, with its permutation straight-line (keccakf<KECCAK_FULL>: no
+// pi-renaming moves at loop back-edges; 78 VGPRs and 6 waves with the 3-iteration loop, 0.9 ms
+// slower in the step, profiles/r4bp_keccak_unroll_ab_100m.json).  Forced to 7 waves by the
+// register limit instead (72 VGPRs, no spills) it had run 1.0 ms slower
+// (profiles/r3l_occupancy_ab_100m.json).
 __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
   const uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
   auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {
