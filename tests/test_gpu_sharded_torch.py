@@ -61,7 +61,7 @@ class HostStagedDist:
         t.copy_(c)
 
 
-def _worker(rank, world, port, n_total, chunk, q):
+def _worker(rank, world, port, n_total, chunk, q, cpu=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import sys
@@ -85,6 +85,7 @@ def _worker(rank, world, port, n_total, chunk, q):
             ok, rep = sharded.self_check(be, 5, n_total, roots[-1])
             out["self_check"] = ok
             out["single"] = rep["single_gpu_root"]
+        if rank == 0 and cpu:
             from oracle import oracle as O
             a, v, o = be.ctx.synth_accounts(5, 0, n_total)
             a, v, o = a.cpu().numpy(), v.cpu().numpy(), o.cpu().numpy()
