@@ -17,8 +17,8 @@ call) and exits with its status.
 
 CPU legs (rank 0, N = 1, after the timed region):
   cpu_baseline       the khipu-faithful sequential trie (oracle/khipu_oracle.cc, 1 core)
-                     on the first 20k/50k/100k accounts of the same workload; every
-                     sample's root is asserted equal to the GPU root of the same prefix;
+                     on the first 20k/50k/100k/1M accounts of the same workload (--seq-samples);
+                     every sample's root is asserted equal to the GPU root of the same prefix;
                      the 100M state-root time is extrapolated from the fitted per-put cost
   cpu_batch_allcore  the independent batch builder (oracle/batch_root.cc) on ALL cores
                      over the full workload; its root is asserted equal to the GPU root
@@ -314,19 +314,14 @@ def roofline(stats, n):
               "sort": "t_sort_ms", "topology": "t_topo_ms"}
     avg = {k: float(np.mean([x[v] for x in stats])) for k, v in stages.items()}
     s = stats[-1]
-    # a grouped build (n_groups > 1) launches the leaf kernel once per top-nibble group
-    # (k_leaf_in_list); its stage time is the sum over the launches
-    groups = max(1, int(s.get("n_groups", 0)))
-    leaf = "k_leaf_in_list" if groups > 1 else "k_leaf_in"
-    total = {"k_hash_keys_ck": avg["k_hash_keys_ck"], leaf: avg["k_leaf_in"]}
+    total = {"k_hash_keys_ck": avg["k_hash_keys_ck"], "k_leaf_in": avg["k_leaf_in"]}
     dom = max(total, key=total.get)
-    launches = groups if dom == leaf else 1
-    perms = {"k_hash_keys_ck": s["n_key_perms"], leaf: s["n_leaves"]}[dom] / launches
-    launch_ms = total[dom] / launches
+    perms = {"k_hash_keys_ck": s["n_key_perms"], "k_leaf_in": s["n_leaves"]}[dom]
+    launch_ms = total[dom]
     achieved = perms * OPS_PER_PERM / (launch_ms * 1e-3)
     return avg, {"kernel": dom, "bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
                  "unit": "T int32-lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS,
-                 "traffic": pmc_traffic(dom, n), "avg_ms": launch_ms, "launches_per_step": launches,
+                 "traffic": pmc_traffic(dom, n), "avg_ms": launch_ms, "launches_per_step": 1,
                  "perms_per_launch": perms}
 
 

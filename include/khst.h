@@ -37,8 +37,14 @@
  *
  * Errors: int status; message via kh_last_error() (thread-local).  KH_EDEVICE means
  * the GPU path failed; the caller decides what to do (there is no silent fallback).
- * Threading: every call is reentrant; host entry points share one lazily created,
- * mutex-guarded device context per device.
+ * Threading: every call is reentrant.  Host entry points share one lazily created
+ * device context per device; every call that uses a context holds its (recursive) mutex
+ * for the call, and every call on a resident handle (kh_trie / forest) holds the mutex of
+ * the context the handle was opened on, so calls on handles of one context from many
+ * threads are serialised (a thread reading one handle's write-back set waits for another
+ * thread's commit on the same context to finish, never for anything else).  A commit
+ * whose in-flight tail (records, anchor map) fails leaves its handle refusing every call
+ * but kh_trie_rollback (to a savepoint opened before it) and kh_trie_free.
  */
 #ifndef KHST_H
 #define KHST_H
@@ -81,8 +87,7 @@ typedef struct kh_stats {
   double t_topo_ms;        /* LCP + topology */
   double t_leaf_ms;        /* leaf encode + hash */
   double t_branch_ms;      /* all branch levels */
-  uint32_t n_groups;       /* top-nibble groups of a grouped build (0 or 1: one plain build); the
-                              stage times are then sums over the groups' builds */
+  uint32_t reserved0;      /* 0 (kept for the layout the JNI shim and ctypes mirror) */
   uint32_t reserved;
 } kh_stats;
 

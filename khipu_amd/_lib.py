@@ -71,7 +71,7 @@ class KhStats(ctypes.Structure):
         ("n_node_perms", ctypes.c_uint64), ("n_key_perms", ctypes.c_uint64), ("arena_bytes", ctypes.c_uint64),
         ("n_levels", ctypes.c_uint32), ("full_sort", ctypes.c_uint32), ("t_total_ms", ctypes.c_double),
         ("t_keys_ms", ctypes.c_double), ("t_sort_ms", ctypes.c_double), ("t_topo_ms", ctypes.c_double),
-        ("t_leaf_ms", ctypes.c_double), ("t_branch_ms", ctypes.c_double), ("n_groups", ctypes.c_uint32),
+        ("t_leaf_ms", ctypes.c_double), ("t_branch_ms", ctypes.c_double), ("reserved0", ctypes.c_uint32),
         ("reserved", ctypes.c_uint32),
     ]
 

@@ -293,17 +293,10 @@ __device__ __forceinline__ bool tie_run_start(const uint32_t* ck, uint64_t n, ui
   const uint32_t hi = ck[i];
   return ck[i + 1] == hi && !(i > 0 && ck[i - 1] == hi);
 }
-// one thread per sorted position: the thread at a run's start orders the run
-__global__ void __launch_bounds__(BS) k_tie_fix_ck(uint32_t* ck, uint32_t* idx, uint64_t n, const uint64_t* K,
-                                                   unsigned long long* flags) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (tie_run_start(ck, n, i)) tie_run_ck(ck, idx, n, K, flags, i);
-}
-// Block-local run list (default): a block covers TF_ITEMS * BS sorted positions, lists
-// its run starts in LDS, and its first threads order the runs (wave 0 for the ~1 % of
-// starting positions of random keys), so one wave per TF_ITEMS * 4 waves' worth of
-// positions waits on a run's dependent key reads instead of nearly every wave (the
-// one-thread-per-position kernel above).  A global list with one atomic per wave was
+// Block-local run list: a block covers TF_ITEMS * BS sorted positions, lists its run
+// starts in LDS, and its first threads order the runs (wave 0 for the ~1 % of starting
+// positions of random keys), so one wave per TF_ITEMS * 4 waves' worth of positions waits
+// on a run's dependent key reads instead of nearly every wave (one thread per position).  A global list with one atomic per wave was
 // measured far slower (a single contended counter: +9 ms at 100M).
 constexpr int TF_ITEMS = 4;
 __global__ void __launch_bounds__(BS) k_tie_fix_ck_blk(uint32_t* ck, uint32_t* idx, uint64_t n, const uint64_t* K,
@@ -810,42 +803,12 @@ __global__ void __launch_bounds__(BS) k_leaf_hash_list(Topo T, const uint32_t* l
              ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
 }
 
-// Early leaves (plain root builds; trie_ops.h op_leaf_in): one thread per INPUT,
-// launched on the second stream right after op_pd_scatter, beside the branch topology.
-// The keys and packed values are read in input order (sequential), the message, header
-// included, is assembled in registers straight into the Keccak state.
-constexpr int PD_DEFAULT = 1;  // where the early leaves' parent depths are scattered (run_build)
+// the early leaves' parent depths and sorted positions for a trie too small for a topology
+// (one key: no boundaries, no ANSV to fold the scatter into)
 __global__ void __launch_bounds__(BS) k_pd_scatter(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i < T.m) op_pd_scatter(T, i);
 }
-// Round-2 form (KHST_LEAF=v2, measurement switch): every load up front at addresses that
-// do not depend on the parent depth, the message moved into place by 64-bit byte funnels
-// and word-select networks.  82 VGPRs, 5 waves per SIMD; 5,472 VALU instructions per wave
-// (profiles/r2zs_pmc_instmix_100m.json).
-__global__ void __launch_bounds__(BS) k_leaf_in_v2(Topo T, uint64_t n) {
-  const uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  typedef const __attribute__((address_space(1))) u64x2 gpair;  // global (not flat) 16-byte loads
-  const uint32_t vmis = (uint32_t)((uintptr_t)T.vals & 15);
-  gpair* vp = (gpair*)(T.vals - vmis);
-  unsigned long long perms = 0, inl = 0, longb = 0;
-  if (j < n) {
-    uint32_t in1 = 0, lb = 0;
-    auto ld2 = [vp](int64_t p, uint64_t& lo, uint64_t& hi) {
-      const u64x2 v = vp[p];
-      lo = v.x;
-      hi = v.y;
-    };
-    perms = op_leaf_in(T, j, ld2, vmis, &in1, &lb);
-    inl = in1;
-    longb = lb;
-  }
-  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), perms,
-             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
-  __syncthreads();  // block_add3's LDS slots are reused
-  block_add3(&T.ctr[CTR_LONGB], longb, nullptr, 0, nullptr, 0);
-}
-
 // max over the wave's 64 lanes (DPP row shifts + row broadcasts), returned to every lane
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true));  // row_shr:1
@@ -889,104 +852,23 @@ __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
   wave_count(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl != 0);
   if (lb) atomicAdd(&T.ctr[CTR_LONGB], (unsigned long long)lb);
 }
-// The same over one group of a grouped build: thread t takes input list[t] (ascending input
-// indices), reading the keys and values of the whole build in place (n_all bounds them)
-__global__ void __launch_bounds__(BS) k_leaf_in_list(Topo T, const uint32_t* list, uint64_t ng, uint64_t n_all) {
-  const uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  const uint64_t j = t < ng ? list[t] : n_all;  // past the group: a neutral lane
-  auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {
-    WaveBounds b;
-    b.emax = wave_max_u32(use ? e : 0u);
-    b.emin = 255u - wave_max_u32(use ? 255u - e : 0u);
-    b.Lmax = wave_max_u32(use ? lhi : 0u);
-    b.Lmin = 255u - wave_max_u32(use ? 255u - llo : 0u);
-    return b;
-  };
-  uint32_t inl = 0, lb = 0;
-  const uint32_t perms = op_leaf_in3(T, j, n_all, wave, &inl, &lb);
-  wave_count(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms != 0);
-  wave_count(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), perms != 0);
-  wave_count(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl != 0);
-  if (lb) atomicAdd(&T.ctr[CTR_LONGB], (unsigned long long)lb);
-}
-// a group's dropped duplicates (earlier puts of a key put again): no parent-depth record
-__global__ void __launch_bounds__(BS) k_pdinv_skip(const uint32_t* list, uint64_t ng, uint64_t* pdinv) {
-  const uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (t < ng) pdinv[list[t]] = PDINV_SKIP;
-}
-
-// The same leaves in SORTED order (KHST_LEAF=sorted, measurement switch): the parent depth
-// comes from the two adjacent boundaries, so the kernel starts right after k_lcp with no
-// scatter (k_ansv_pd becomes k_ansv); keys and values are read through the sorted input
-// index (random 32-byte key and value-span reads) and the stash is written in order.
-__global__ void __launch_bounds__(BS) k_leaf_sorted(Topo T, uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {
-    WaveBounds b;
-    b.emax = wave_max_u32(use ? e : 0u);
-    b.emin = 255u - wave_max_u32(use ? 255u - e : 0u);
-    b.Lmax = wave_max_u32(use ? lhi : 0u);
-    b.Lmin = 255u - wave_max_u32(use ? 255u - llo : 0u);
-    return b;
-  };
-  uint32_t inl = 0, lb = 0;
-  const uint32_t perms = op_leaf_sorted(T, i, n, wave, &inl, &lb);
-  wave_count(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms != 0);
-  wave_count(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), perms != 0);
-  wave_count(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl != 0);
-  if (lb) atomicAdd(&T.ctr[CTR_LONGB], (unsigned long long)lb);
-}
-
-// after the branch topology (plain root builds): stashed leaf references into the
-// parents' child records, arena slots for long leaves
-__global__ void __launch_bounds__(BS) k_leaf_topo_early(Topo T) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i < T.m)
-    op_leaf_topo_early(T, i,
-                       [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); });
-}
 // the same publish split in two (trie_ops.h op_leaf_link / op_leaf_move)
 __global__ void __launch_bounds__(BS) k_leaf_link(Topo T) {
   GRID_STRIDE(i, T.m) op_leaf_link(T, i);
 }
-__global__ void __launch_bounds__(BS) k_leaf_link_rec(Topo T) {
-  GRID_STRIDE_WAVE(i, T.m) {  // every lane of a wave runs the ballot (threads past m list nothing)
-    const bool listed = i < T.m && op_leaf_link_rec(T, i);
-    const uint64_t slot = wave_claim(&T.ctr[CTR_FIXN], listed);
-    if (listed) T.fixlist[slot] = (uint32_t)i;
-  }
-}
-// after the join: fix-list leaves (unless long) take the copy pass; long leaves their arena
-// slot and parent (op_leaf_topo_early), for k_leaf_long
-__global__ void __launch_bounds__(BS) k_leaf_fix(Topo T, uint64_t nfix, uint64_t nlong) {
+// after the join (leaf positions): the long leaves' arena slots and parents
+// (op_leaf_topo_early), for k_leaf_long
+__global__ void __launch_bounds__(BS) k_leaf_fix(Topo T, uint64_t nlong) {
   const uint64_t q = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  auto alloc = [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); };
-  if (q < nfix) {
-    const uint32_t i = T.fixlist[q];
-    if (T.lf_emeta[i] != EMETA_LONG) op_leaf_move(T, i, alloc);
-  } else if (q < nfix + nlong) {
-    op_leaf_topo_early(T, T.longlist[q - nfix], alloc);
-  }
+  if (q < nlong)
+    op_leaf_topo_early(T, T.longlist[q],
+                       [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); });
 }
 __global__ void __launch_bounds__(BS) k_leaf_move(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i < T.m)
     op_leaf_move(T, i, [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); });
 }
-
-// The copy pass in two parts split at a child-record slot (*thr: the first child record
-// of the branches at depth >= D, run_build): the leaves under parents of depth >= D, and
-// every top or long leaf, before the branch levels (upper = 1); the others on the second
-// stream beside the levels deeper than D - 1, which never read their records (upper = 0)
-__global__ void __launch_bounds__(BS) k_leaf_move_part(Topo T, const uint32_t* thr, int upper) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  if (i >= T.m) return;
-  const uint64_t d = T.lf_dst[i];
-  const bool hi = T.lf_emeta[i] == EMETA_LONG || d == LINK_TOP || (d & LINK_SLOT) >= *thr;
-  if (hi == (upper != 0))
-    op_leaf_move(T, i, [&](uint64_t b) { return (uint64_t)atomicAdd(&T.ctr[CTR_LFBYTES], (unsigned long long)b); });
-}
-
 
 __global__ void __launch_bounds__(BS) k_leaf_long(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
@@ -1028,18 +910,13 @@ __global__ void __launch_bounds__(BS) k_branch_hash(Topo T, uint64_t first, uint
 // HBM: the level reads its contiguous child records once and writes one 34-byte
 // reference per node.  Slot layout [thread][word]: a wave's 8-byte slot accesses are
 // bank-conflict-free within each 16-lane group (stride 34 dwords).
-// V: 0 variable-length keys (op_branch_fused), 1 direct window assembly re-scanning the
-// children per window (op_branch_direct), 2 the children streamed once with the next
+// V: 0 variable-length keys (op_branch_fused), 2 the children streamed once with the next
 // record prefetched (op_branch_stream), 4 the same reading leaf children at their sorted
-// positions (leaf positions), 6 the same below depth 8 (the nibble from the input key), 5
-// following link records (KHST_LEAF_LINKS=1)
-// WB: threads per block.  WB = 64 (KHST_BRANCH_BS=64, measurement switch): one wave per
-// block, 8,704 B of LDS, so a CU holds 18 waves instead of the 16 that 35 KB blocks of 256
-// threads allow (4.5 per SIMD instead of 4); the counters are summed per wave.
-template <int V, int WB = BS>
-__global__ void __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(4, 8))) k_branch_fused(Topo T, uint64_t first, uint64_t cnt) {
-  __shared__ uint64_t slots[WB * LEAF_WORDS];
-  uint64_t t = (uint64_t)blockIdx.x * WB + threadIdx.x;
+// positions (leaf positions), 6 the same below depth 8 (the nibble from the input key)
+template <int V>
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8))) k_branch_fused(Topo T, uint64_t first, uint64_t cnt) {
+  __shared__ uint64_t slots[BS * LEAF_WORDS];
+  uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (t < cnt) {
     uint32_t j = (uint32_t)(first + t);
@@ -1048,27 +925,14 @@ __global__ void __launch_bounds__(WB) __attribute__((amdgpu_waves_per_eu(4, 8)))
     // the byte stream through the windowed writer
     uint64_t* sl = slots + threadIdx.x * LEAF_WORDS;
     perms = V == 0   ? op_branch_fused(T, j, sl, 1, &in1)
-            : V == 1 ? op_branch_direct(T, j, sl, 1, &in1)
             : V == 2 ? op_branch_stream_t<SRC_REC>(T, j, sl, 1, &in1, ChildSrc{})
             : V == 4 ? op_branch_stream_t<SRC_POS>(T, j, sl, 1, &in1, ChildSrc{})
-            : V == 6 ? op_branch_stream_t<SRC_POSK>(T, j, sl, 1, &in1, ChildSrc{})
-                     : op_branch_stream_t<SRC_LINK>(T, j, sl, 1, &in1, ChildSrc{});
+                     : op_branch_stream_t<SRC_POSK>(T, j, sl, 1, &in1, ChildSrc{});
     hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
   }
-  if (WB == BS) {
-    block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
-               ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
-  } else {
-    perms = wave_sum(perms);
-    hashes = wave_sum(hashes);
-    inl = wave_sum(inl);
-    if ((threadIdx.x & 63) == 0) {
-      if (perms) atomicAdd(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms);
-      if (hashes) atomicAdd(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes);
-      if (inl) atomicAdd(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
-    }
-  }
+  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
+             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
 }
 
 // Small levels (a block commit's dirty paths, the few branches at the top of a full build):
@@ -1346,150 +1210,6 @@ __global__ void __launch_bounds__(64) k_branch_xl(Topo T, uint64_t first, uint64
   atomicAdd(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), (unsigned long long)perms);
   atomicAdd(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), (unsigned long long)branch_hash_count(T, j, perms));
   if (ninl) atomicAdd(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), (unsigned long long)ninl);
-}
-
-// Wave-cooperative variant of k_branch_fused (row N1, measured against it: see
-// DESIGN.md §5).  Each thread still owns one branch and its Keccak state, but the
-// encoding window of block b is assembled by a 16-lane group (one DPP row) per branch:
-// lane c takes child record c (one coalesced 32-byte load per lane; the level's records
-// are contiguous), its byte offset in the encoding is hdr + nibble + the row's exclusive
-// DPP prefix sum of (item length - 1), and it XORs its bytes (^ 0x80) into the window,
-// which the row first fills with 0x80 (every empty slot and the terminator are 0x80).
-// The 4 rows of a wave assemble the 64 windows in 16 steps; then every lane absorbs its
-// own window and the permutation runs on all 64 lanes.
-__global__ void __launch_bounds__(BS) k_branch_coop(Topo T, uint64_t first, uint64_t cnt) {
-  __shared__ uint64_t win[BS * LEAF_WORDS];
-  __shared__ uint32_t s_L[BS], s_cb[BS], s_kh[BS];  // per owner: length, child base, k | hdr << 8 | nblk << 16
-  const uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
-  const uint32_t ln = threadIdx.x & 63, wbase = threadIdx.x & ~63u, c = ln & 15, row = ln >> 4;
-  const uint32_t j = (uint32_t)(first + t);
-  const bool valid = t < cnt;
-  const bool top = valid && T.br_parent[j] == NONE;
-  const uint32_t ext = valid ? T.br_ext[j] : 0;
-  uint32_t L = 0, payload = 0, k = 0, nblk = 0;
-  bool hashit = false;
-  if (valid) {
-    payload = branch_payload(T, j);
-    L = rlp_hdr_len(payload) + payload;
-    k = T.br_k[j];
-    hashit = L >= 32 || (top && ext == 0);
-    nblk = hashit ? L / 136 + 1 : 1;
-    T.br_len[j] = L;
-  }
-  s_L[threadIdx.x] = L;
-  s_cb[threadIdx.x] = valid ? T.br_cbase[j] : 0;
-  s_kh[threadIdx.x] = k | (rlp_hdr_len(payload) << 8) | (nblk << 16);
-  const uint32_t nb_wave = wave_max_u32(nblk);
-  wave_lds_sync();
-  KState S = {};
-  for (uint32_t b = 0; b < nb_wave; ++b) {
-    for (uint32_t sidx = 0; sidx < 16; ++sidx) {
-      const uint32_t o = wbase + row * 16 + sidx;  // the owner whose window this row builds
-      const uint32_t kh = s_kh[o], kk = kh & 0xFF, hh = (kh >> 8) & 0xFF, onb = kh >> 16;
-      if (b >= onb) continue;  // row-uniform
-      const uint32_t LL = s_L[o], w0 = 136u * b;
-      uint64_t* wb = win + (uint64_t)o * LEAF_WORDS;
-      // 1. 0x80 fill of the window's message bytes (lane c: word c; lane 0 also word 16)
-      for (uint32_t w = c; w < 17; w += 16) {
-        const uint32_t a = w0 + 8 * w;
-        const uint32_t n80 = LL > a ? (LL - a < 8 ? LL - a : 8) : 0;
-        wb[w] = low_bytes_mask(n80) & 0x8080808080808080ULL;
-      }
-      // 2. child c: its item bytes (0xa0 + hash, or the inline encoding) at its offset
-      uint32_t len = 0, nib = 0;
-      uint64_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-      const uint64_t rec = (uint64_t)s_cb[o] + c;
-      if (c < kk) {
-        const uint32_t mc = T.cmeta[rec];
-        len = mc & 0xFF;
-        nib = mc >> 8;
-        r0 = T.cref[4 * rec];
-        r1 = T.cref[4 * rec + 1];
-        r2 = T.cref[4 * rec + 2];
-        r3 = T.cref[4 * rec + 3];
-      }
-      const uint32_t ilen = len == 32 ? 33 : len;
-      const uint32_t incl = row16_scan(ilen ? ilen - 1 : 0);
-      const uint32_t off = hh + nib + incl - (ilen ? ilen - 1 : 0);
-      wave_lds_sync();  // the fill lands before any XOR
-      if (ilen && off < w0 + 136 && off + ilen > w0) {
-        uint64_t I[5];
-        if (len == 32) {
-          I[0] = 0xA0 | (r0 << 8);
-          I[1] = (r0 >> 56) | (r1 << 8);
-          I[2] = (r1 >> 56) | (r2 << 8);
-          I[3] = (r2 >> 56) | (r3 << 8);
-          I[4] = r3 >> 56;
-        } else {
-          I[0] = r0; I[1] = r1; I[2] = r2; I[3] = r3; I[4] = 0;  // zero beyond len (capped refs)
-        }
-        const uint32_t sh = off & 7, wfirst = off >> 3;
-#pragma unroll
-        for (uint32_t q = 0; q < 6; ++q) {
-          const uint64_t cur = q < 5 ? I[q] : 0, prv = q ? I[q - 1] : 0;
-          const uint64_t y = sh ? (cur << (8 * sh)) | (prv >> (64 - 8 * sh)) : cur;
-          const uint32_t W = wfirst + q;  // absolute word
-          // item bytes of this word: [max(off, 8W), min(off + ilen, 8W + 8)) relative to 8W
-          const int32_t lo = (int32_t)off - 8 * (int32_t)W, hi = (int32_t)(off + ilen) - 8 * (int32_t)W;
-          const uint32_t blo = lo > 0 ? (uint32_t)lo : 0, bhi = hi < 8 ? (hi > 0 ? (uint32_t)hi : 0) : 8;
-          if (bhi <= blo || W < w0 / 8 || W >= w0 / 8 + 17) continue;
-          const uint64_t m = low_bytes_mask(bhi) & ~low_bytes_mask(blo);
-          atomicXor((unsigned long long*)(wb + (W - w0 / 8)), (unsigned long long)((y ^ 0x8080808080808080ULL) & m));
-        }
-      }
-      // 3. the list header (window 0), lane 0
-      if (c == 0 && b == 0) {
-        const uint32_t pl = LL - hh;
-        uint64_t hdr = hh == 1 ? (0xC0 + pl) : hh == 2 ? (0xF8 | ((uint64_t)pl << 8))
-                                                        : (0xF9 | ((uint64_t)(pl >> 8) << 8) | ((uint64_t)(pl & 0xFF) << 16));
-        atomicXor((unsigned long long*)wb, (unsigned long long)((hdr ^ 0x8080808080808080ULL) & low_bytes_mask(hh)));
-      }
-      wave_lds_sync();
-    }
-    // absorb my window (one Keccak block) and permute
-    if (b < nblk && hashit) {
-      const uint32_t nfull = L / 136, rem = b < nfull ? 136 : L - 136 * nfull;
-      const uint64_t* my = win + (uint64_t)threadIdx.x * LEAF_WORDS;
-#pragma unroll
-      for (int q = 0; q < 17; ++q) {
-        const uint32_t base = 8u * (uint32_t)q;
-        uint64_t x = base < rem ? my[q] & low_bytes_mask(rem - base < 8 ? rem - base : 8) : 0;
-        if (b == nfull) {
-          if ((rem >> 3) == (uint32_t)q) x ^= 0x01ULL << (8 * (rem & 7));
-          if (q == 16) x ^= 0x80ULL << 56;
-        }
-        kxor(S, q, x);
-      }
-      keccakf(S);
-    }
-    wave_lds_sync();  // the next window reuses the slots
-  }
-  unsigned long long perms = 0, hashes = 0, inl = 0;
-  if (valid) {
-    uint64_t hb[4] = {0, 0, 0, 0}, bhead[4] = {0, 0, 0, 0};
-    uint32_t ninl = 0, p = 0;
-    {
-      if (hashit) {
-        for (int q = 0; q < 4; ++q) hb[q] = lane(S, q);
-        p = L / 136 + 1;
-      }
-      if (L < 32) {  // one window, still in the slot
-        const uint64_t* my = win + (uint64_t)threadIdx.x * LEAF_WORDS;
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t base = 8u * (uint32_t)q;
-          bhead[q] = base < L ? my[q] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0;
-        }
-      }
-      ninl = hashit ? 0 : 1;
-      branch_keep(T, j, L, hb, bhead);
-    }
-    p += branch_publish(T, j, L, hb, bhead, Slot{win + (uint64_t)threadIdx.x * LEAF_WORDS, 1}, &ninl);
-    perms = p;
-    hashes = branch_hash_count(T, j, p);
-    inl = ninl;
-  }
-  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
-             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
 }
 
 // write-back emission: node q in [0, m + 2B): leaf q, or branch / extension of branch (q-m)/2.
@@ -1931,21 +1651,19 @@ struct kh_ctx {
   hipStream_t own = nullptr;
   hipStream_t st = nullptr;
   hipStream_t st2 = nullptr;  // leaf hashing, concurrent with the branch topology
-  std::mutex mu;
+  // every entry point that uses the context holds it (recursive: a *_host entry point locks,
+  // then calls its device variant, which locks again); a resident handle's calls lock the
+  // context the handle was opened on (kh_trie::home)
+  std::recursive_mutex mu;
   DevBuf ws_list;  // element builds: the list of leaves to hash (k_leaf_prep -> k_leaf_hash_list)
   DevBuf ws_inject;                    // kh_block_commit: the injection's error word
   unsigned long long inject_tok = 0;   //   and the token the last call writes there on error
   DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, in_kn, in_aux, in_block, out_emit, emit_dev;
-  hipEvent_t ev[13] = {};  // [8] boundaries ready (st), [9] / [10] leaf kernel start / end (st2),
-                          // [11] second part of the leaf copy pass done (st2), [12] unused
+  hipEvent_t ev[11] = {};  // [0..5] build stages (st), [6] / [7] forest commit marks, [8] boundaries
+                          // ready (st), [9] / [10] leaf kernel start / end (st2)
   unsigned long long* h_pinned = nullptr;  // small pinned staging for syncs
   uint8_t* h_res = nullptr;                // pinned staging of the per-result outputs (grown; a pageable
   size_t h_res_cap = 0;                    // copy of 100k roots cost 20-30 ms of page pinning per build)
-  // grouped builds (grouped_build): the hashed keys, sort words, group lists and parent-depth
-  // records of the whole build; the second context the odd groups run on; per-group events
-  DevBuf gws;
-  kh_ctx* gsub = nullptr;
-  hipEvent_t gev[18] = {};
   // kh_block_commit: the second context its storage phase runs on, beside the account phase on
   // this one, and the event of the storage roots' injection into the account bodies
   kh_ctx* bsub = nullptr;
@@ -1965,17 +1683,6 @@ struct kh_ctx {
 // ---------------------------------------------------------------------------
 // the build
 // ---------------------------------------------------------------------------
-// One top-nibble group of a grouped build (grouped_build): the caller hashed every key and
-// partitioned the sort words by group; the group's build sorts, derives the topology and
-// hashes only its own keys, reading the keys and values of the whole build in place.
-struct GroupArgs {
-  const uint32_t* ck = nullptr;    // [ng] the group's 32-bit sort words, in input order
-  const uint32_t* list = nullptr;  // [ng] their input indices, ascending (the leaf kernel's order)
-  uint64_t n_all = 0;              // inputs of the whole build: the key / value buffers' bounds
-  uint64_t* pdinv = nullptr;       // [n_all] parent depth | sorted position per input, shared by the groups
-  hipEvent_t start_after = nullptr;  // the build's stream waits on it before its first launch
-  std::function<void()> on_topo;     // called once the group's branch topology is enqueued
-};
 struct BuildArgs {
   const uint8_t* keys;
   uint32_t klen;
@@ -1992,8 +1699,6 @@ struct BuildArgs {
   struct ElemArgs* el = nullptr;   // element build of a resident forest commit (forest.h; nullable)
   hipEvent_t vals_ready = nullptr; // the values / offsets land later (multi-GPU exchange): wait before reading them
   bool dev_results = false;        // results and counters stay on the device (no host sync at the end)
-  const GroupArgs* grp = nullptr;  // a group of a grouped build (depth0 = 1, keys = the hashed keys of all groups)
-  bool no_groups = false;          // never split into a grouped build (its own fallback)
   bool no_spec = false;            // no speculative sort (SortIO::speculate): the retry of one that failed
   std::function<void()> before_leaves;  // element builds: called (host) right before the leaves are encoded
   std::function<bool()> late_ready;     // ... late values (ElemArgs::late) already on their way: one leaf pass
@@ -2040,9 +1745,6 @@ static uint8_t* pinned_stage(kh_ctx* c, size_t bytes) {
   return c->h_res;
 }
 
-// a grouped build met a run of > TIE_RUN_MAX keys with equal 32-bit prefixes (adversarial
-// keys): the build is redone as one plain build, which takes the full 256-bit sort
-struct GroupFallback {};
 // a speculative sort (SortIO::speculate) met repeated keys or a long run: the build is redone
 struct SpecRetry {};
 
@@ -2072,7 +1774,6 @@ struct SortIO {
   // a device word copied to the host with the first sync's flags (c->h_pinned[1]): the
   // caller's check of earlier stream work, read without a sync of its own (nullable)
   const unsigned long long* chk = nullptr;
-  bool no_full_sort = false;  // a group of a grouped build (input indices are not 0..n-1): no 256-bit sort
   // ck_path: no sync for the tie kernel's flags: the sort proceeds as if no key repeats and no
   // run is too long (hashed keys: the rule); the caller reads the flags at its next sync
   // (CTR_TIE) and redoes the build without speculating if either is set
@@ -2119,14 +1820,8 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
     const bool flip = radix_sort_pairs<uint32_t>(c0, idx0, c1, idx1, n, 0, 32, rs_scratch, st);
     uint32_t* c32 = flip ? c1 : c0;
     idxs = flip ? idx1 : idx0;
-    const bool tie_one = getenv("KHST_TIE_ONE") != nullptr;  // measurement switch
-    if (tie_one) {
-      hipLaunchKernelGGL(k_tie_fix_ck, GRID(n, BS), dim3(BS), 0, st, c32, idxs, n, (const uint64_t*)K32,
-                         T.ctr + CTR_TIE);
-    } else {
-      hipLaunchKernelGGL(k_tie_fix_ck_blk, GRID(n, TF_ITEMS * BS), dim3(BS), 0, st, c32, idxs, n,
-                         (const uint64_t*)K32, T.ctr + CTR_TIE, S.u, S.depth0);
-    }
+    hipLaunchKernelGGL(k_tie_fix_ck_blk, GRID(n, TF_ITEMS * BS), dim3(BS), 0, st, c32, idxs, n,
+                       (const uint64_t*)K32, T.ctr + CTR_TIE, S.u, S.depth0);
     LAUNCH_CHECK();
     uint64_t tf = 0;
     if (!S.speculate) {
@@ -2167,7 +1862,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
       S.sck = ock;
       S.sseg = sseg;
       S.fallback = false;
-      S.ties_u = !tie_one && S.u && m == n;  // no dedup: the run boundaries' values stand
+      S.ties_u = S.u && m == n;  // no dedup: the run boundaries' values stand
       return;
     }
   } else {
@@ -2196,7 +1891,6 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
   const bool fallback = tie_flags & 1, dups = tie_flags & 2;
   uint64_t m = n;
   uint32_t* sidx = idxs;
-  if (fallback && S.no_full_sort) throw GroupFallback{};
   if (fallback) {
     // full 256-bit (+segment) LSD sort from the input order
     uint32_t* ia = idx0;
@@ -2262,8 +1956,6 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
 }
 
 static void build_stats(kh_ctx* c, const unsigned long long* hc, kh_stats* stats);
-static uint32_t group_count(const BuildArgs& A);
-static void grouped_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats, uint32_t G);
 static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats);
 static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats) {
   try {
@@ -2275,10 +1967,6 @@ static void run_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stat
   }
 }
 static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats) {
-  if (const uint32_t ng = group_count(A); ng > 1) {  // a large plain root: pipelined over top-nibble groups
-    grouped_build(c, A, O, stats, ng);
-    return;
-  }
   hipStream_t st = c->st;
   const uint64_t n = A.n;
   const bool segmented = A.seg != nullptr;
@@ -2286,10 +1974,6 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   if (n >= (1ULL << 31)) throw KhError{KH_EINVAL, "n must be < 2^31 per device"};
   if (A.depth0 > 1) throw KhError{KH_EINVAL, "depth0 must be 0 or 1"};
   if (segmented && A.depth0 != 0) throw KhError{KH_EINVAL, "segmented builds use depth0 = 0"};
-  const GroupArgs* G = A.grp;
-  if (G && (segmented || A.depth0 != 1 || A.emit || A.el || A.kn || (A.flags & KH_HASH_KEYS) || A.klen != 32 ||
-            ((uintptr_t)A.keys & 15)))
-    throw KhError{KH_EINTERNAL, "grouped build: a plain depth-1 build over 32-byte hashed keys"};
   if (!(A.flags & KH_HASH_KEYS) && A.klen != 32) throw KhError{KH_EINVAL, "keys must be 32 bytes unless KH_HASH_KEYS"};
   if (A.klen == 0 || A.klen > 4096) throw KhError{KH_EINVAL, "bad key length"};
   const uint32_t sb = segmented ? bits_for(A.nseg) : 0;
@@ -2300,29 +1984,11 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   const bool early = !A.emit && !A.el && !A.kn;
   if (A.kn && (A.emit || A.el || (A.flags & KH_HASH_KEYS)))
     throw KhError{KH_EINVAL, "variable-length keys: root-only builds of unhashed keys"};
-  // The early leaves reach their parents' child records by a link pass on the topology
-  // stream (slot of each sorted leaf) and a copy pass after the join (k_leaf_move).
-  // KHST_LEAF_LINKS=1 (measurement switch) writes the child records themselves during the
-  // hashing as LINKS to the stashes, which the branch kernel follows (trie_ops.h
-  // op_leaf_link_rec; records in the phase-1 workspace, sized by the bound C <= 2n): measured
-  // at 100M, 50.9 ms against 43.5 (profiles/r3j_leaf_links_ab_100m.json): 100M scattered
-  // 10-byte record writes cost the topology stream 10 ms beside the leaf kernel.
-  // Other switches: KHST_PUBLISH_ONE (one publish pass after the join), KHST_BRANCH=coop|rescan.
-  const bool split_publish = !getenv("KHST_PUBLISH_ONE");
-  const bool leaf_move = !getenv("KHST_LEAF_LINKS") || strcmp(getenv("KHST_LEAF_LINKS"), "1") != 0;
-  const char* bv = getenv("KHST_BRANCH");
-  const bool coop = bv && strcmp(bv, "coop") == 0 && !A.kn;  // (the coop assembly has no branch values)
-  const bool rescan = bv && strcmp(bv, "rescan") == 0;          // op_branch_direct
-  const bool links = early && split_publish && !leaf_move && !coop && !rescan;
-  const uint64_t cbound = links ? 2 * n + 16 : 0;
   // Leaf positions (trie_ops.h Topo::lpos; unsegmented plain root builds): no leaf child
   // records at all -- the branch kernels read each leaf child's stash at its sorted position.
-  // KHST_LEAF_POS=0 (measurement switch): the copy pass k_leaf_move instead.
-  const bool leaf_pos_env = !getenv("KHST_LEAF_POS") || atoi(getenv("KHST_LEAF_POS")) != 0;
-  // (not with the round-2 leaf kernel, KHST_LEAF=v2, which does not publish a top leaf)
-  const bool leaf_v2_env = getenv("KHST_LEAF") && !strcmp(getenv("KHST_LEAF"), "v2");
-  const bool lpos =
-      early && split_publish && !links && !coop && !rescan && !segmented && leaf_pos_env && !leaf_v2_env;
+  // Segmented early builds reach their parents' child records by a link pass on the topology
+  // stream (slot of each sorted leaf) and a copy pass after the join (k_leaf_move).
+  const bool lpos = early && !segmented;
 
   O.res_hash.assign(nres * 4, 0);
   O.res_len.assign(nres, 0);
@@ -2349,11 +2015,10 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
       A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
       nres * 32, nres * 4, nres * 32,         // results
       CTR_N * CTR_SHARDS * 8, 64 * 4, 80 * 4, 512 * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
-      early ? n * 32 : 0, early ? n : 0, early ? n * 8 : 0, early ? n * 8 : 0,  // early leaves: stashed references,
-                                                                  // meta, pd|position, link slots
+      early ? n * 32 : 0, early ? n : 0, early ? n * 8 : 0,  // early leaves: stashed references, meta, pd|position
+      early && !lpos ? n * 8 : 0,                                 // link slots (segmented early builds)
       A.kn ? n : 0,                           // sorted key lengths
       nb1 * 4, nb1 * 4, nb1 * 4, nb1, nb1, nb1,  // branch tables in key-order ids (BrTab J)
-      cbound * 32, cbound * 2, links ? n * 4 : 0, links ? n * 4 : 0,  // link mode: child records, fix / long lists
       lpos ? nb1 * 4 : 0, lpos ? nb1 * 4 : 0, lpos ? n * 4 : 0,  // leaf positions: range ends (J, T), long list
       nb1 * 4, nb1 * 4,                       // tile topology: boundaries left to the whole-array ANSV / chain
   };
@@ -2411,7 +2076,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   T.lf_eref = early ? cv.take<uint64_t>(n * 4) : nullptr;
   T.lf_emeta = early ? cv.take<uint8_t>(n) : nullptr;
   T.pdinv = early ? cv.take<uint64_t>(n) : nullptr;
-  T.lf_dst = early ? cv.take<uint64_t>(n) : nullptr;
+  T.lf_dst = early && !lpos ? cv.take<uint64_t>(n) : nullptr;
   T.kin = K32;
   uint8_t* skn = A.kn ? cv.take<uint8_t>(n) : nullptr;
   BrTab J{};
@@ -2421,12 +2086,6 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   J.depth = cv.take<uint8_t>(nb1);
   J.ext = cv.take<uint8_t>(nb1);
   J.pord = cv.take<uint8_t>(nb1);
-  if (links) {
-    T.cref = cv.take<uint64_t>(cbound * 4);
-    T.cmeta = cv.take<uint16_t>(cbound);
-    T.fixlist = cv.take<uint32_t>(n);
-    T.longlist = cv.take<uint32_t>(n);
-  }
   if (lpos) {
     J.end = cv.take<uint32_t>(nb1);
     T.br_end = cv.take<uint32_t>(nb1);
@@ -2435,7 +2094,6 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   }
   uint32_t* tlist_a = cv.take<uint32_t>(nb1);
   uint32_t* tlist_c = cv.take<uint32_t>(nb1);
-  if (G) T.pdinv = G->pdinv;  // indexed by input: shared by the groups (each writes its own inputs')
   T.depth0 = A.depth0;
   T.segmented = segmented ? 1 : 0;
   T.vals = A.vals;
@@ -2455,16 +2113,11 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   // index and never gather the sorted keys.  Segmented builds too while the key bits left
   // beside the segment id keep runs of equal words short (the block-local tie fix orders
   // them; one longer than TIE_RUN_MAX falls back to the full sort): at most one key per
-  // four word values on average.  KHST_SEG_CK=0: the 64-bit composite sort (measurement switch).
-  const bool seg_ck = !getenv("KHST_SEG_CK") || strcmp(getenv("KHST_SEG_CK"), "0") != 0;
+  // four word values on average.  Otherwise the 64-bit composite sort.
   const bool seg_words_ok = segmented && sb + CK_KEY_BITS <= 32 && (n / A.nseg) <= (1ULL << (32 - sb - 2));
-  const bool ck_path = early && !A.kn && (!segmented || (seg_ck && seg_words_ok));
-  const bool ck_ready = ck_path && ((A.flags & KH_HASH_KEYS) || G);
-  if (G) {  // the group's sort words and input indices (input order), copied: the sort overwrites them
-    if (G->start_after) HIPCHK(hipStreamWaitEvent(st, G->start_after, 0));
-    HIPCHK(hipMemcpyAsync(ck0, G->ck, n * 4, hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemcpyAsync(idx0, G->list, n * 4, hipMemcpyDeviceToDevice, st));
-  } else if (ck_ready) {
+  const bool ck_path = early && !A.kn && (!segmented || seg_words_ok);
+  const bool ck_ready = ck_path && (A.flags & KH_HASH_KEYS);
+  if (ck_ready) {
     uint32_t* c0 = (uint32_t*)ck0;
     if (A.klen <= 135)
       hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, c0, idx0, A.seg,
@@ -2485,8 +2138,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   if (stage_ev) HIPCHK(hipEventRecord(c->ev[1], st));
 
   // ---- 2. sort + dedup
-  // (KHST_SPEC=0, measurement switch: the tie flags' sync as before)
-  const bool spec = ck_path && !G && !A.no_spec && c->spec_off == 0 && !(getenv("KHST_SPEC") && atoi(getenv("KHST_SPEC")) == 0);
+  const bool spec = ck_path && !A.no_spec && c->spec_off == 0;
   if (c->spec_off) --c->spec_off;
   uint64_t m = n;
   uint32_t* sidx = nullptr;
@@ -2496,7 +2148,6 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr,
              A.kn, ck_ready};
     S.ck_path = ck_path;
-    S.no_full_sort = G != nullptr;
     S.speculate = spec;
     S.u = T.u;
     S.depth0 = A.depth0;
@@ -2566,80 +2217,52 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   // 4 blocks per CU, so they leave the leaf kernel more of the machine and still finish
   // first.  Measured at 100M (profiles/r2zg_cap_ab_100m.json): 46.5 ms against 47.4 uncapped
   // (one thread per element); 2 blocks per CU starve the topology (23.7 ms, step 49.2),
-  // 8 per CU slow the leaf kernel (18.8 ms, step 48.5).  KHST_TOPO_BPC: blocks per CU
-  // (measurement switch; 0 = one thread per element).
-  const int topo_bpc = getenv("KHST_TOPO_BPC") ? atoi(getenv("KHST_TOPO_BPC")) : 4;
-  const uint32_t topo_cap = topo_bpc > 0 ? (uint32_t)(topo_bpc * c->n_cu) : 0u;
+  // 8 per CU slow the leaf kernel (18.8 ms, step 48.5).
+  const uint32_t topo_cap = 4u * (uint32_t)c->n_cu;
   auto topo_grid = [&](uint64_t cnt) {
     const uint64_t g = (cnt + BS - 1) / BS;
-    return dim3((unsigned)(early && topo_cap && g > topo_cap ? topo_cap : (g ? g : 1)));
+    return dim3((unsigned)(early && g > topo_cap ? topo_cap : (g ? g : 1)));
   };
-  // KHST_TOPO_TILE=0 (measurement switch, read per call): the whole-array ANSV and chain walk
-  // (k_ansv / k_ansv_pd, k_chain) instead of the tile-local ones (k_topo_tile)
-  const char* tte = getenv("KHST_TOPO_TILE");
-  const int pd_env = [] {
-    const char* l = getenv("KHST_LEAF");  // measurement switch: leaves hashed in sorted order
-    if (l && strcmp(l, "sorted") == 0) return 2;
-    const char* e = getenv("KHST_PD");  // measurement switch
-    return !e ? PD_DEFAULT : strcmp(e, "ansv") == 0 ? 1 : strcmp(e, "first") == 0 ? 3 : 0;
-  }();
-  const int pd_mode = (early && nb > 0) ? (G ? PD_DEFAULT : pd_env) : 0;
-  // (=2: the parent-depth scatter as its own kernel after k_topo_tile; =3: the scatter first,
-  // the leaves right after it and k_topo_tile beside them)
-  // Default: tiles from TOPO_TILE_MIN boundaries; below it the extra launches cost more than the
+  // Early leaves (plain root builds) need only the boundaries: they are hashed in input
+  // order on st2 beside the topology.  Their parent depths (and sorted positions) are
+  // scattered by the ANSV kernel on st (k_topo_tile, or k_ansv_pd below TOPO_TILE_MIN) and
+  // the leaf kernel starts after it (pd_scan); a trie of one key has no topology: a
+  // separate k_pd_scatter on st2.  Measured at 100M (profiles/r2y_pd_ab_100m.json): 49.9 ms
+  // (in the ANSV) against 52.2 (separate); folded into k_chain 50.6; into k_lcp, the leaf
+  // kernel starting right after it, 50.7 (it then runs beside the whole topology: 19.7 ms
+  // instead of 14.9).  The later alternatives (the scatter in two passes, before the tile
+  // kernel, after it, the leaves in sorted order): DESIGN.md §5.
+  const bool pd_scan = early && nb > 0;
+  // Tiles from TOPO_TILE_MIN boundaries; below it the extra launches cost more than the
   // dependent loads they save (configs[2] element builds of ~100k: 1.95 against 2.04 ms per
   // block, profiles/r4w_topo_tile_block_ab_50m.json)
   constexpr uint64_t TOPO_TILE_MIN = 1u << 21;
-  const int tile_mode = (pd_mode == 0 || pd_mode == 1) ? (tte ? atoi(tte) : (nb >= TOPO_TILE_MIN ? 1 : 0)) : 0;
-  const bool topo_tile = tile_mode != 0;
-  auto pdinv_skip = [&](hipStream_t s) {  // every input of the build without a record (its own inputs only)
-    if (G) {
-      hipLaunchKernelGGL(k_pdinv_skip, GRID(n, BS), dim3(BS), 0, s, G->list, n, T.pdinv);
-      LAUNCH_CHECK();
-    } else {
-      HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, s));
-    }
-  };
-  if (pd_mode == 2) {  // sorted leaves: no scatter, the stash is written in sorted order
-    HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));
-  } else if (pd_mode) {  // presets for the scatter folded into k_ansv (on st)
-    if (m < n) pdinv_skip(st);                      // dropped duplicates: PDINV_SKIP
+  const bool topo_tile = nb >= TOPO_TILE_MIN;
+  if (pd_scan) {  // presets for the scatter folded into the ANSV (on st)
+    if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, st));  // dropped duplicates: PDINV_SKIP
     HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));  // every leaf a hash unless it says otherwise
   }
   if (nb > 0) {
     hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb, ties_u);
     LAUNCH_CHECK();
   }
-  // Early leaves (plain root builds) need only the boundaries: they are hashed in input
-  // order on st2 beside the topology.  Their parent depths are scattered inside k_ansv on
-  // st and the leaf kernel starts after it (pd_mode 1), or by a separate k_pd_scatter on
-  // st2 right after k_lcp (pd_mode 0; KHST_PD=sep, and tries too small for a topology).
-  // Measured at 100M (profiles/r2y_pd_ab_100m.json): 49.9 ms (ansv) against 52.2 (sep);
-  // folded into k_chain 50.6; into k_lcp, the leaf kernel starting right after it, 50.7
-  // (it then runs beside the whole topology: 19.7 ms instead of 14.9).
   auto launch_leaves = [&](bool scatter) {  // on st2, after everything enqueued on st so far
     HIPCHK(hipEventRecord(c->ev[8], st));
     HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
     hipStream_t s2 = c->st2;
     if (scatter) {
-      if (m < n) pdinv_skip(s2);                      // dropped duplicates: PDINV_SKIP
+      if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, s2));  // dropped duplicates: PDINV_SKIP
       HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, s2));  // every leaf a hash unless it says otherwise
       hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, s2, T);
       LAUNCH_CHECK();
     }
     if (A.vals_ready) HIPCHK(hipStreamWaitEvent(s2, A.vals_ready, 0));  // the topology need not wait
     HIPCHK(hipEventRecord(c->ev[9], s2));
-    const bool leaf_v2 = getenv("KHST_LEAF") && !strcmp(getenv("KHST_LEAF"), "v2");  // measurement switch
-    if (G)
-      hipLaunchKernelGGL(k_leaf_in_list, GRID(n, BS), dim3(BS), 0, s2, T, G->list, n, G->n_all);
-    else if (leaf_v2)
-      hipLaunchKernelGGL(k_leaf_in_v2, GRID(n, BS), dim3(BS), 0, s2, T, n);
-    else
-      hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, s2, T, n);
+    hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, s2, T, n);
     LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[10], s2));
   };
-  if (early && pd_mode == 0) launch_leaves(true);
+  if (early && !pd_scan) launch_leaves(true);
   if (nb > 0) {
     P.lv[0] = T.u;
     P.sz[0] = nb;
@@ -2672,19 +2295,10 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
       // them); the leaves start right after it; the few boundaries whose answers leave their
       // tile (k_ansv_list / k_chain_list over the whole pyramid) run beside the leaves
       unsigned long long* tcnt = ctr + CTR_TLIST;
-      if (pd_mode == 1 && tile_mode == 3) {
-        hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, st, T);
-        LAUNCH_CHECK();
-        launch_leaves(false);
-      }
       hipLaunchKernelGGL(k_topo_tile, dim3((unsigned)((nb + TOPO_TILE - 1) / TOPO_TILE)), dim3(TT_THREADS), 0, st, T,
-                         nb, pd_mode == 1 && tile_mode == 1, tcnt, tlist_a, tlist_c);
+                         nb, pd_scan, tcnt, tlist_a, tlist_c);
       LAUNCH_CHECK();
-      if (pd_mode == 1 && tile_mode == 2) {
-        hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, st, T);
-        LAUNCH_CHECK();
-      }
-      if (pd_mode == 1 && tile_mode != 3) launch_leaves(false);
+      if (pd_scan) launch_leaves(false);
       pyramid();
       hipLaunchKernelGGL(k_ansv_list, topo_grid(nb / 16 + 1), dim3(BS), 0, st, T, P, (const uint32_t*)tlist_a,
                          (const unsigned long long*)tcnt);
@@ -2693,27 +2307,12 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
       LAUNCH_CHECK();
     } else {
       pyramid();
-      if (pd_mode == 2) {  // the leaves need only u: they start here, beside the whole topology
-        HIPCHK(hipEventRecord(c->ev[8], st));
-        HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
-        if (A.vals_ready) HIPCHK(hipStreamWaitEvent(c->st2, A.vals_ready, 0));
-        HIPCHK(hipEventRecord(c->ev[9], c->st2));
-        hipLaunchKernelGGL(k_leaf_sorted, GRID(m, BS), dim3(BS), 0, c->st2, T, n);
-        LAUNCH_CHECK();
-        HIPCHK(hipEventRecord(c->ev[10], c->st2));
-      }
-      if (pd_mode == 3) {  // KHST_PD=first: the scatter alone on st, then the leaves; the plain
-                           // ANSV runs beside them on st
-        hipLaunchKernelGGL(k_pd_scatter, GRID(m, BS), dim3(BS), 0, st, T);
-        LAUNCH_CHECK();
-        launch_leaves(false);
-      }
-      if (pd_mode == 1)
+      if (pd_scan)
         hipLaunchKernelGGL(k_ansv_pd, GRID(m, BS), dim3(BS), 0, st, T, P, nb);
       else
         hipLaunchKernelGGL(k_ansv, GRID(nb, BS), dim3(BS), 0, st, T, P, nb);
       LAUNCH_CHECK();
-      if (pd_mode == 1) launch_leaves(false);
+      if (pd_scan) launch_leaves(false);
       hipLaunchKernelGGL(k_chain, topo_grid(nb), dim3(BS), 0, st, T, nb);
       LAUNCH_CHECK();
     }
@@ -2750,16 +2349,12 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     // child record bases
     scan_exclusive<uint32_t>(T.br_k, T.br_cbase, nb, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
   }
-  if (links) {  // the leaves' child records as links, while they are still being hashed
-    hipLaunchKernelGGL(k_leaf_link_rec, topo_grid(m), dim3(BS), 0, st, T);
-    LAUNCH_CHECK();
-  } else if (early && split_publish && !lpos) {  // the leaves' slots, while they are still being hashed
+  if (early && !lpos) {  // the leaves' slots, while they are still being hashed
     hipLaunchKernelGGL(k_leaf_link, topo_grid(m), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
   }
   if (early) {
     HIPCHK(hipEventRecord(c->ev[3], st));      // topology done (the leaves may still run)
-    if (G && G->on_topo) G->on_topo();             // (the next group's sort may start behind it)
     HIPCHK(hipStreamWaitEvent(st, c->ev[10], 0));  // ... and the leaves: their long-leaf bytes
   } else {
     hipLaunchKernelGGL(k_leaf_topo, GRID(m, BS), dim3(BS), 0, st, T);
@@ -2784,7 +2379,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   std::vector<uint32_t> lbh(65, 0);
   memcpy(lbh.data(), (const char*)hc + ((char*)lb - (char*)ctr), 65 * 4);
   if (nb == 0) std::fill(lbh.begin(), lbh.end(), 0u);
-  const uint64_t nfix = links ? hc[CTR_FIXN] : 0, nlong = (links || lpos) ? hc[CTR_LONGN] : 0;
+  const uint64_t nlong = lpos ? hc[CTR_LONGN] : 0;
   if (lpos) {  // every leaf is hashed by now: is any of them inline?
     unsigned long long ninl = 0;
     for (int sh = 0; sh < CTR_SHARDS; ++sh) ninl += hc[sh * CTR_N + CTR_INLINE];
@@ -2797,14 +2392,11 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   const bool lmsgs = A.emit || A.kn || A.el;
   const uint64_t lmsg_words = lmsgs ? (uint64_t)LEAF_WORDS * m : 0;
   const uint64_t bmsg_words = A.emit ? (uint64_t)BR_WORDS * B : 0, xmsg_words = A.emit ? (uint64_t)EXT_WORDS * B : 0;
-  if (links && C > cbound) throw KhError{KH_EINTERNAL, "child records exceed their bound"};
-  c->ws2.ensure(carve_size({links ? 0 : C * 32, links ? 0 : C * 2, lmsg_words * 8, lf_bytes + 64, bmsg_words * 8,
-                            xmsg_words * 8, lpos ? C * 4 : 0}));
+  c->ws2.ensure(carve_size({C * 32, C * 2, lmsg_words * 8, lf_bytes + 64, bmsg_words * 8, xmsg_words * 8,
+                            lpos ? C * 4 : 0}));
   Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
-  if (!links) {
-    T.cref = cv2.take<uint64_t>(C * 4);
-    T.cmeta = cv2.take<uint16_t>(C);
-  }
+  T.cref = cv2.take<uint64_t>(C * 4);
+  T.cmeta = cv2.take<uint16_t>(C);
   T.lmsg = lmsgs ? cv2.take<uint64_t>(lmsg_words) : nullptr;
   T.lstride = m;
   T.arena = cv2.take<uint8_t>(lf_bytes + 64);  // long leaves
@@ -2829,46 +2421,14 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
 
   // ---- 4. leaves: encode + hash in LDS (root only), or encode into message slots
   //         that the node-set emitter reads back, then hash
-  // KHST_MOVE_SPLIT=1 (measurement switch): the copy pass of the early leaves split at
-  // depth move_d (0: not split), D = one below the busiest branch level, so the records of
-  // the leaves under the busiest levels' branches are written beside the deeper levels.
-  // Measured at 100M (profiles/r3n_move_split_ab_100m.json): 44.86 ms against 45.00 in one
-  // pass, within the noise -- the second part slows the levels it runs beside by as much as
-  // it takes off the join (branch levels 7.76 -> 8.9 ms), so it stays off.
-  uint32_t move_d = 0;
-  {
-    const bool msplit = getenv("KHST_MOVE_SPLIT") && atoi(getenv("KHST_MOVE_SPLIT")) != 0;
-    if (early && split_publish && !links && !lpos && msplit && m >= (1u << 18) && nb > 0) {
-      uint32_t best = 0, dbest = 0;
-      for (uint32_t d = 0; d < 64; ++d)
-        if (lbh[d + 1] - lbh[d] > best) best = lbh[d + 1] - lbh[d], dbest = d;
-      if (dbest + 1 < 64 && lbh[dbest + 1] < lbh[64]) move_d = dbest + 1;  // levels >= D exist
-    }
-  }
   if (early) {  // hashed already: publish into the child records; long leaves now
     if (lpos) {  // leaf positions: only the long leaves' parents and arena slots
       if (nlong) {
-        hipLaunchKernelGGL(k_leaf_fix, GRID(nlong, BS), dim3(BS), 0, st, T, (uint64_t)0, nlong);
+        hipLaunchKernelGGL(k_leaf_fix, GRID(nlong, BS), dim3(BS), 0, st, T, nlong);
         LAUNCH_CHECK();
       }
-    } else if (links) {  // only the listed leaves: the top one, those under deep parents, long ones
-      if (nfix + nlong) {
-        hipLaunchKernelGGL(k_leaf_fix, GRID(nfix + nlong, BS), dim3(BS), 0, st, T, nfix, nlong);
-        LAUNCH_CHECK();
-      }
-      T.links = 1;
-    } else if (split_publish && move_d) {
-      const uint32_t* thr = T.br_cbase + lbh[move_d];
-      hipLaunchKernelGGL(k_leaf_move_part, GRID(m, BS), dim3(BS), 0, c->st2, T, thr, 0);
-      LAUNCH_CHECK();
-      HIPCHK(hipEventRecord(c->ev[11], c->st2));
-      hipLaunchKernelGGL(k_leaf_move_part, GRID(m, BS), dim3(BS), 0, st, T, thr, 1);
-      LAUNCH_CHECK();
-    } else if (split_publish) {
+    } else {  // segmented: the stashed references copied into the parents' child records
       hipLaunchKernelGGL(k_leaf_move, GRID(m, BS), dim3(BS), 0, st, T);
-      LAUNCH_CHECK();
-    } else {
-      hipLaunchKernelGGL(k_leaf_topo_early, GRID(m, BS), dim3(BS), 0, st, T);
       LAUNCH_CHECK();
     }
     if (lf_bytes) {
@@ -2912,49 +2472,30 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
 
   // ---- 5. branch levels, deepest first: encode (gathers the children's refs), then hash
   uint32_t levels = 0;
-  // N1 variant: one thread per branch assembling its own window (default) or the
-  // wave-cooperative DPP assembly (KHST_BRANCH=coop; DESIGN.md §5 has the measurement)
-  const bool branch_bs64 = getenv("KHST_BRANCH_BS") && atoi(getenv("KHST_BRANCH_BS")) == 64;
   // levels of at most XL_LEVEL branches: k_branch_xl (32 lanes per branch, the permutation
   // spread over them); of at most SMALL_LEVEL: k_branch_small (every child record loaded at
-  // once); KHST_BRANCH_SMALL=0 (measurement switch) keeps them all on k_branch_fused
-  const bool small_levels = !getenv("KHST_BRANCH_SMALL") || atoi(getenv("KHST_BRANCH_SMALL")) != 0;
-  // (measurement switches: the level sizes below which the two small-level kernels run)
-  const uint32_t xl_level = getenv("KHST_XL_LEVEL") ? (uint32_t)atoi(getenv("KHST_XL_LEVEL")) : XL_LEVEL;
-  const uint32_t small_level =
-      getenv("KHST_SMALL_LEVEL") ? (uint32_t)atoi(getenv("KHST_SMALL_LEVEL")) : SMALL_LEVEL;
-  bool moved = move_d == 0;
+  // once); larger ones k_branch_fused (one thread per branch)
   for (int d = 63; d >= 0; --d) {
     uint32_t cnt = lbh[d + 1] - lbh[d];
     if (!cnt) continue;
-    if (!moved && d < (int)move_d) {  // this level reads the second part's records
-      HIPCHK(hipStreamWaitEvent(st, c->ev[11], 0));
-      moved = true;
-    }
     if (A.emit) {  // the write-back build keeps every encoding in its message slot for emission
       hipLaunchKernelGGL(k_branch_prep, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
       LAUNCH_CHECK();
       hipLaunchKernelGGL(k_branch_hash, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
-    } else if (coop) {
-      hipLaunchKernelGGL(k_branch_coop, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
     } else {
-      // (link records, KHST_LEAF_LINKS=1, only through k_branch_fused<5>, which follows them)
-      const bool small = !A.kn && !rescan && !T.links && small_levels && cnt <= small_level;
-      const bool pos = T.cend && !small;  // leaf children from their stashes
+      const bool small = !A.kn && cnt <= SMALL_LEVEL;
       // (leaf positions, a small level: k_branch_xl / k_branch_small read the leaf children's
       // stashes themselves, as op_leaf_children restates -- a separate pass writing the level's leaf
       // child records first cost 5-12 us + a launch per level)
       if (A.kn)
         hipLaunchKernelGGL(k_branch_fused<0>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
-      else if (rescan)
-        hipLaunchKernelGGL(k_branch_fused<1>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
-      else if (small && cnt <= xl_level)
+      else if (small && cnt <= XL_LEVEL)
         hipLaunchKernelGGL(k_branch_xl, dim3((unsigned)((cnt + 1) / 2)), dim3(64), 0, st, T, (uint64_t)lbh[d],
                            (uint64_t)cnt);
       else if (small)
         hipLaunchKernelGGL(k_branch_small, dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, T, (uint64_t)lbh[d],
                            (uint64_t)cnt);
-      else if (pos) {
+      else if (T.cend) {  // leaf children from their stashes
         Topo TL = T;
         TL.lvl_depth = (uint32_t)d;
         TL.lvl_nsh = 28 - 4 * ((uint32_t)d & 7);
@@ -2962,19 +2503,13 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
           hipLaunchKernelGGL(k_branch_fused<4>, GRID(cnt, BS), dim3(BS), 0, st, TL, (uint64_t)lbh[d], (uint64_t)cnt);
         else
           hipLaunchKernelGGL(k_branch_fused<6>, GRID(cnt, BS), dim3(BS), 0, st, TL, (uint64_t)lbh[d], (uint64_t)cnt);
-      }
-      else if (T.links)
-        hipLaunchKernelGGL(k_branch_fused<5>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
-      else if (branch_bs64)
-        hipLaunchKernelGGL((k_branch_fused<2, 64>), dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, T,
-                           (uint64_t)lbh[d], (uint64_t)cnt);
-      else
+      } else {
         hipLaunchKernelGGL(k_branch_fused<2>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
+      }
     }
     LAUNCH_CHECK();
     ++levels;
   }
-  if (!moved) HIPCHK(hipStreamWaitEvent(st, c->ev[11], 0));
   HIPCHK(hipEventRecord(c->ev[5], st));
 
   // ---- results
@@ -3069,240 +2604,14 @@ static kh_ctx* ctx_new(int dev) {
   // The topology stream (st) has the priority over the leaf stream (st2): the leaf kernel
   // then shares the CUs with the topology (18 ms instead of 14.7 alone) but the topology
   // stays off the critical path.  Measured (profiles/r2za_*, r2zc_*): the leaf stream first
-  // (KHST_LEAF_PRIO=hi) or equal priorities starve the topology (22.3 ms) and cost 0.5 ms;
+  // or equal priorities starve the topology (22.3 ms) and cost 0.5 ms;
   // restricting the topology stream to 1/2 or 3/4 of the CUs changes nothing.
-  const char* lp = getenv("KHST_LEAF_PRIO");  // measurement switch
-  const bool leaf_hi = lp && strcmp(lp, "hi") == 0;
-  HIPCHK(hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, leaf_hi ? prio_lo : prio_hi));
-  HIPCHK(hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, leaf_hi ? prio_hi : prio_lo));
+  HIPCHK(hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, prio_hi));
+  HIPCHK(hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, prio_lo));
   c->st = c->own;
   for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipHostMalloc((void**)&c->h_pinned, 16384, hipHostMallocDefault));  // >= CTR_N * CTR_SHARDS words
   return c;
-}
-
-// ---------------------------------------------------------------------------
-// Grouped build: one large plain root pipelined over top-nibble groups on one GPU.
-//
-// A plain build's critical path is key hashing -> sort -> boundaries -> ANSV with the
-// parent-depth scatter -> the leaf kernel -> the branch levels; the sort and the topology
-// leave the VALU idle (~8.5 ms at 100M).  Here every key is hashed once, the
-// (sort word, input index) pairs are split stably into G groups by their top key bits
-// (G = 2^gb; group g holds the top nibbles [16g/G, 16(g+1)/G)), and group g is an ordinary
-// depth-1 build of its own keys -- sort, topology, leaves (its inputs in input order,
-// k_leaf_in_list), branch levels -- reading the keys and values of the whole build in
-// place.  Groups alternate between two contexts (four streams: the HIP hardware queue
-// count), driven by two host threads; group g + 1's sort waits only for group g's topology,
-// so it and group g + 1's topology run beside group g's leaves and branch levels.  The 16
-// top-nibble references are folded into the root branch on the host (kh_fold_root16's
-// encoding, MerklePatriciaTrie.scala:169).  Adversarial keys (a run of > TIE_RUN_MAX equal
-// 32-bit prefixes, or fewer than two occupied top nibbles) redo the build as one plain build.
-// Measured at 100M accounts (profiles/r4c_groups_ab_100m.json, one box): 42.97 ms plain against
-// 43.93 / 45.26 / 47.26 ms with 2 / 4 / 8 groups (roots equal).  The groups' topology chains
-// (sort, ANSV, chain, branch records, level order: ~11 ms of latency-bound kernels per 100M keys
-// alone) become the critical path: group g + 1's sort waits for group g's topology, and the
-// topology runs no faster beside the leaf and branch kernels than it does beside the leaf kernel
-// in the plain build.  So the plain build stays the default; KHST_GROUPS=2|4|8|16 (read per call,
-// a measurement switch) selects the grouped build, which tests/test_gpu_grouped.py keeps
-// parity-checked.
-constexpr uint64_t GROUP_MIN_N = 1ULL << 23;  // below ~8M inputs the per-group fixed costs dominate
-static uint32_t group_count(const BuildArgs& A) {
-  const char* e = getenv("KHST_GROUPS");
-  const int env = e ? atoi(e) : 1;
-  if (env <= 1 || A.grp || A.no_groups || A.seg || A.depth0 || A.emit || A.el || A.kn || A.vlen || A.vals_ready ||
-      A.n < GROUP_MIN_N)
-    return 1;
-  uint32_t g = 2;
-  while (g < (uint32_t)env && g < 16) g <<= 1;
-  return g;
-}
-__global__ void k_group_offsets(const uint32_t* counts, uint32_t tiles, uint32_t G, uint64_t n, uint64_t* gofs) {
-  const uint32_t g = threadIdx.x;  // the exclusive scan of the digit-major counts: digit g starts at tile 0
-  if (g < G) gofs[g] = counts[(uint64_t)g * tiles];
-  if (g == G) gofs[G] = n;
-}
-static kh_ctx* ctx_new(int dev);
-static void grouped_build(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats* stats, uint32_t G) {
-  hipStream_t st = c->st;
-  const uint64_t n = A.n;
-  uint32_t gb = 0;
-  while ((1u << gb) < G) ++gb;
-  if (!c->gsub) c->gsub = ctx_new(c->dev);
-  for (auto& e : c->gev)
-    if (!e) HIPCHK(hipEventCreate(&e));
-  // ---- the whole build's keys, sort words, group lists and parent-depth records
-  const uint32_t tiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
-  const bool hashed = A.flags & KH_HASH_KEYS;
-  const bool own_keys = hashed || ((uintptr_t)A.keys & 15);
-  if (!hashed && A.klen != 32) throw KhError{KH_EINVAL, "keys must be 32 bytes unless KH_HASH_KEYS"};
-  c->gws.ensure(carve_size({own_keys ? n * 32 : 0, n * 4, n * 4, n * 4, n * 4, n * 8, (size_t)tiles * 256 * 4,
-                            scan_scratch_bytes((uint64_t)tiles * 256, 4), 64 * 8}));
-  Carver cv{(char*)c->gws.p, 0, c->gws.cap};
-  uint64_t* K32 = own_keys ? cv.take<uint64_t>(n * 4) : (uint64_t*)A.keys;
-  uint32_t* ck = cv.take<uint32_t>(n);
-  uint32_t* idx = cv.take<uint32_t>(n);
-  uint32_t* gck = cv.take<uint32_t>(n);
-  uint32_t* gidx = cv.take<uint32_t>(n);
-  uint64_t* pdinv = cv.take<uint64_t>(n);
-  uint32_t* counts = cv.take<uint32_t>((size_t)tiles * 256);
-  void* scan_ws = cv.take<char>(scan_scratch_bytes((uint64_t)tiles * 256, 4));
-  uint64_t* gofs = cv.take<uint64_t>(64);
-  HIPCHK(hipEventRecord(c->gev[16], st));
-  if (hashed) {
-    if (A.klen <= 135)
-      hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, ck, idx,
-                         (const uint32_t*)nullptr, 0u);
-    else
-      hipLaunchKernelGGL(k_hash_keys_ck<false>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, ck, idx,
-                         (const uint32_t*)nullptr, 0u);
-  } else {
-    if (own_keys) HIPCHK(hipMemcpyAsync(K32, A.keys, n * 32, hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_make_ck32, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, n, ck, idx,
-                       (const uint32_t*)nullptr, 0u);
-  }
-  LAUNCH_CHECK();
-  HIPCHK(hipEventRecord(c->gev[17], st));
-  // ---- the stable split by the top gb bits: one radix pass (only G of its 256 digits occur),
-  // input order kept inside a group
-  const int sh = 32 - (int)gb;
-  hipLaunchKernelGGL(k_rs_hist<uint32_t>, dim3(tiles), dim3(RS_THREADS), 0, st, (const uint32_t*)ck, n, sh, counts,
-                     tiles);
-  scan_exclusive<uint32_t>(counts, counts, (uint64_t)tiles * 256, (uint32_t*)nullptr, scan_ws, st);
-  hipLaunchKernelGGL(k_rs_scatter<uint32_t>, dim3(tiles), dim3(RS_THREADS), 0, st, (const uint32_t*)ck,
-                     (const uint32_t*)idx, gck, gidx, n, sh, (const uint32_t*)counts, tiles, false);
-  hipLaunchKernelGGL(k_group_offsets, dim3(1), dim3(64), 0, st, (const uint32_t*)counts, tiles, G, n, gofs);
-  LAUNCH_CHECK();
-  HIPCHK(hipMemcpyAsync(c->h_pinned, gofs, (G + 1) * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  std::vector<uint64_t> go(c->h_pinned, c->h_pinned + G + 1);
-  // ---- the groups: two host threads, group g on context g & 1
-  kh_ctx* ctxs[2] = {c, c->gsub};
-  std::mutex mu;
-  std::condition_variable cvar;
-  std::vector<char> topo(G, 0);
-  bool abort = false, fallback = false;
-  std::exception_ptr err;
-  std::vector<BuildOut> outs(G);
-  std::vector<kh_stats> gst(G);
-  std::vector<double> t_end(G, 0.0);
-  auto fail = [&](bool fb, std::exception_ptr e) {
-    std::lock_guard<std::mutex> lk(mu);
-    abort = true;
-    if (fb) fallback = true;
-    if (e && !err) err = e;
-    cvar.notify_all();
-  };
-  auto worker = [&](int w) {
-    try {
-      HIPCHK(hipSetDevice(c->dev));
-      kh_ctx* x = ctxs[w];
-      for (uint32_t g = (uint32_t)w; g < G; g += 2) {
-        hipEvent_t after = c->gev[17];
-        if (g > 0) {
-          std::unique_lock<std::mutex> lk(mu);
-          cvar.wait(lk, [&] { return topo[g - 1] || abort; });
-          if (abort) return;
-          after = c->gev[g - 1];
-        }
-        bool signalled = false;
-        auto signal = [&, g, x] {
-          HIPCHK(hipEventRecord(c->gev[g], x->st));
-          std::lock_guard<std::mutex> lk(mu);
-          topo[g] = 1;
-          signalled = true;
-          cvar.notify_all();
-        };
-        const uint64_t g0 = go[g], ng = go[g + 1] - go[g];
-        if (ng == 0) {
-          HIPCHK(hipStreamWaitEvent(x->st, after, 0));
-          signal();
-          continue;
-        }
-        GroupArgs GA;
-        GA.ck = gck + g0;
-        GA.list = gidx + g0;
-        GA.n_all = n;
-        GA.pdinv = pdinv;
-        GA.start_after = after;
-        GA.on_topo = signal;
-        BuildArgs B{(const uint8_t*)K32, 32, A.vals, A.voff, ng, nullptr, 1, 1, 0, false};
-        B.grp = &GA;
-        run_build(x, B, outs[g], &gst[g]);
-        if (!signalled) signal();
-        t_end[g] = ev_ms(c->gev[16], x->ev[5]);
-      }
-    } catch (GroupFallback&) {
-      fail(true, nullptr);
-    } catch (...) {
-      fail(false, std::current_exception());
-    }
-  };
-  std::thread t1(worker, 1);
-  worker(0);
-  t1.join();
-  if (err) std::rethrow_exception(err);
-  // ---- the 16 top-nibble references folded into the root branch
-  uint64_t refs[64] = {};
-  uint32_t lens[16] = {};
-  int nonempty = 0, inl_tops = 0;
-  for (uint32_t q = 0; q < 16 && !fallback; ++q) {
-    const BuildOut& R = outs[q >> (4 - gb)];
-    const uint32_t L = R.res_len.size() > q ? R.res_len[q] : 0;
-    if (!L) continue;
-    ++nonempty;
-    lens[q] = L >= 32 ? 32 : L;
-    memcpy(refs + 4 * q, L >= 32 ? &R.res_hash[4 * q] : &R.res_inl[4 * q], 32);
-    if (L < 32) ++inl_tops;
-  }
-  if (fallback || nonempty < 2) {  // adversarial keys: one plain build (full sort / a root that is not a branch)
-    for (kh_ctx* x : ctxs) {
-      HIPCHK(hipStreamSynchronize(x->st));
-      HIPCHK(hipStreamSynchronize(x->st2));
-    }
-    BuildArgs P = A;
-    P.no_groups = true;
-    run_build(c, P, O, stats);
-    return;
-  }
-  uint64_t enc[80];
-  const uint32_t L = encode_branch16(refs, lens, (uint8_t*)enc);
-  uint64_t h[4];
-  kec256_msg<true>((const uint8_t*)enc, L, h);
-  O.res_hash.assign(h, h + 4);
-  O.res_len.assign(1, L);
-  O.res_inl.assign(4, 0);
-  if (L < 32) memcpy(O.res_inl.data(), enc, 32);
-  if (stats) {
-    kh_stats s{};
-    s.n_inputs = n;
-    for (uint32_t g = 0; g < G; ++g) {
-      const kh_stats& x = gst[g];
-      s.n_leaves += x.n_leaves;
-      s.n_branches += x.n_branches;
-      s.n_extensions += x.n_extensions;
-      s.n_inline += x.n_inline;
-      s.n_node_hashes += x.n_node_hashes;
-      s.n_node_perms += x.n_node_perms;
-      s.arena_bytes += x.arena_bytes;
-      s.n_levels = std::max(s.n_levels, x.n_levels);
-      s.full_sort |= x.full_sort;
-      s.t_sort_ms += x.t_sort_ms;
-      s.t_topo_ms += x.t_topo_ms;
-      s.t_leaf_ms += x.t_leaf_ms;
-      s.t_branch_ms += x.t_branch_ms;
-      s.t_total_ms = std::max(s.t_total_ms, t_end[g]);
-    }
-    // the subtrie tops were hashed as tops; in the whole trie a top shorter than 32 bytes is
-    // embedded in the root branch instead; the root branch itself is one more node
-    s.n_node_hashes = s.n_node_hashes - inl_tops + 1;
-    s.n_node_perms = s.n_node_perms - inl_tops + (L / 136 + 1);
-    s.n_inline += inl_tops;
-    s.n_branches += 1;
-    s.n_key_perms = hashed ? n * (uint64_t)(A.klen / 136 + 1) : 0;
-    s.t_keys_ms = ev_ms(c->gev[16], c->gev[17]);
-    s.n_groups = G;
-    *stats = s;
-  }
 }
 
 static kh_ctx* shared_ctx(int dev) {
@@ -3957,7 +3266,8 @@ static void swap_buf(DevBuf& a, DevBuf& b) {
 }
 
 struct kh_trie {
-  kh_ctx* c = nullptr;
+  kh_ctx* c = nullptr;     // the context its commits run on (kh_block_commit moves the storage phase for a call)
+  kh_ctx* home = nullptr;  // the context it was opened on: every call on the handle holds home->mu
   uint32_t flags = 0;  // KH_HASH_KEYS: the trie's key encoder; KH_EMIT_NODES: keep each commit's write-back set
   bool forest = false;
   DevBuf recs, touched, replaced;  // node records (forest.h Recs: 128 B each), per-commit flags
@@ -3993,6 +3303,9 @@ struct kh_trie {
   hipEvent_t ev_roots = nullptr, pend_ev = nullptr;
   unsigned long long* pend = nullptr;
   bool pend_valid = false, pend_fresh = false;
+  // such a tail failed (its anchor map is not trustworthy): every later call refuses the
+  // handle (KH_EINTERNAL) except kh_trie_free
+  bool broken = false;
   kh_trie() = default;
   kh_trie(const kh_trie&) = delete;
   kh_trie& operator=(const kh_trie&) = delete;
@@ -4004,12 +3317,21 @@ struct kh_trie {
 };
 // the in-flight tail of the last commit: its map error and fresh slots (before mused is read)
 static void trie_settle(kh_trie* h) {
+  if (h->broken) throw KhError{KH_EINTERNAL, "handle unusable: an earlier commit's anchor-map update failed"};
   if (!h->pend_valid) return;
-  HIPCHK(hipEventSynchronize(h->pend_ev));
+  const hipError_t e = hipEventSynchronize(h->pend_ev);
+  if (e != hipSuccess || h->pend[0]) {
+    h->broken = true;  // sticky: the map may hold part of that commit
+    h->pend_valid = false;
+    if (e != hipSuccess) throw KhError{KH_EDEVICE, std::string("commit tail: ") + hipGetErrorString(e)};
+    throw KhError{KH_EINTERNAL, "anchor map insert failed"};
+  }
   h->pend_valid = false;
-  if (h->pend[0]) throw KhError{KH_EINTERNAL, "anchor map insert failed"};
   if (h->pend_fresh) h->mused += h->pend[1];
 }
+
+// every entry point on a resident handle serialises on its home context (khst.h: reentrant)
+#define HANDLE_LOCK(h) std::lock_guard<std::recursive_mutex> handle_lock_((h)->home->mu)
 
 static Recs recs_of(kh_trie* h) {
   return recs_at((uint8_t*)h->recs.p);
@@ -4318,6 +3640,9 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   if (nops >= (1ULL << 30)) throw KhError{KH_EINVAL, "batch too large"};
   if (!(h->flags & KH_HASH_KEYS) && F.klen != 32) throw KhError{KH_EINVAL, "keys must be 32 bytes unless KH_HASH_KEYS"};
   if (F.klen == 0 || F.klen > 4096) throw KhError{KH_EINVAL, "bad key length"};
+  // the previous commit's in-flight tail (records, anchor map): its flags before this
+  // commit's descent reads the map (done by now, stream order; a failure refuses the handle)
+  trie_settle(h);
   HIPCHK(hipEventRecord(c->ev[6], st));
   // ---- 1. op keys (the trie's key encoder), trie ids, sort by (trie, key), last op wins
   const bool segd = h->forest;
@@ -4577,7 +3902,6 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   // Without a write-back set or a map rebuild, the commit returns as soon as its roots are on
   // the host; the records and the anchor map follow on the stream (the next call is ordered
   // after them, trie_settle reads their flags): configs[2]'s account phase ends 0.1 ms sooner
-  trie_settle(h);  // (the previous commit's tail: done by now, stream order)
   const bool rebuild = ne && 2 * (h->mused + B + m + 1024) > h->mcap;
   const bool lazy = ne && !keep_em && !rebuild;
   const size_t o_roots = (size_t)((char*)roots - (char*)tries), o_tail = (size_t)((char*)tail - (char*)tries);
@@ -4777,6 +4101,7 @@ static void trie_rollback(kh_trie* h) {
     trie_settle(h);
   } catch (const KhError&) {  // (the journal undoes that commit's map writes all the same)
   }
+  // (a savepoint is opened only on a settled, usable handle: a broken tail came after it)
   hipStream_t st = h->c->st;
   Savepoint& sp = *h->sps.back();
   const bool remap = h->map_epoch != sp.map_epoch;
@@ -4823,12 +4148,14 @@ static void trie_rollback(kh_trie* h) {
   h->sps.pop_back();
   if (remap) map_rebuild(h, 1024);  // (syncs)
   HIPCHK(hipStreamSynchronize(st));
+  h->broken = false;  // back before any failed tail
 }
 // keep the commits since the innermost savepoint: it is dropped (its saved write-back set
 // passes to the enclosing savepoint when that one has none); the journal is emptied when the
 // last savepoint goes
 static void trie_release(kh_trie* h) {
   if (h->sps.empty()) throw KhError{KH_EINVAL, "no open savepoint"};
+  trie_settle(h);  // a commit kept only once its in-flight tail checked out
   std::unique_ptr<Savepoint> sp = std::move(h->sps.back());
   h->sps.pop_back();
   if (!h->sps.empty()) {
@@ -4848,9 +4175,6 @@ static void trie_release(kh_trie* h) {
 }
 // an all-or-nothing section over one or two handles (kh_block_commit, kh_trie_root_of): a
 // savepoint on each; rolled back unless released
-#ifndef KHST_BLOCK_TXN  // measurement builds only (-DKHST_BLOCK_TXN=0: a block commit without its journal)
-#define KHST_BLOCK_TXN 1
-#endif
 struct Txn {
   kh_trie* h[2] = {nullptr, nullptr};
   bool open = false;
@@ -4892,6 +4216,7 @@ static kh_trie* trie_copy(kh_trie* h) {
   trie_settle(h);
   std::unique_ptr<kh_trie> n(new kh_trie());
   n->c = h->c;
+  n->home = h->home;
   n->flags = h->flags;
   n->forest = h->forest;
   hipStream_t st = h->c->st;
@@ -5063,15 +4388,12 @@ int kh_ctx_destroy(kh_ctx* c) {
   API_TRY({
     (void)hipSetDevice(c->dev);
     (void)hipStreamSynchronize(c->st);
-    if (c->gsub) (void)kh_ctx_destroy(c->gsub);
     if (c->bsub) (void)kh_ctx_destroy(c->bsub);
     if (c->bev) (void)hipEventDestroy(c->bev);
     for (DevBuf* b : {&c->ws_inject, &c->ws_list, &c->ws1, &c->ws2, &c->ws3, &c->in_keys, &c->in_vals, &c->in_voff, &c->in_seg, &c->in_kn, &c->in_aux, &c->in_block, &c->out_emit,
-                      &c->emit_dev, &c->gws})
+                      &c->emit_dev})
       b->release();
     for (auto& e : c->ev)
-      if (e) (void)hipEventDestroy(e);
-    for (auto& e : c->gev)
       if (e) (void)hipEventDestroy(e);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->h_res) (void)hipHostFree(c->h_res);
@@ -5101,7 +4423,7 @@ int kh_dev_kec256_batch(kh_ctx* c, const uint8_t* d_data, const uint64_t* d_off,
 int kh_kec256_batch(const uint8_t* data, const uint64_t* off, uint64_t n, uint8_t* out32) {
   API_TRY({
     kh_ctx* c = shared_ctx(current_device());
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->dev));
     if (n == 0) return KH_OK;
     uint64_t o0 = off[0], bytes = off[n] - o0;
@@ -5130,7 +4452,7 @@ int kh_trie_root(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const 
       return KH_OK;
     }
     kh_ctx* c = shared_ctx(current_device());
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->dev));
     Staged S = stage_inputs(c, keys, klen, vals, voff, n, nullptr);
     BuildArgs A{S.keys, klen, S.vals, S.voff, n, nullptr, 1, 0, flags, false};
@@ -5157,7 +4479,7 @@ int kh_trie_roots_segmented(const uint8_t* keys, uint32_t klen, const uint8_t* v
       return KH_OK;
     }
     kh_ctx* c = shared_ctx(current_device());
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->dev));
     const uint64_t* vo = voff + seg_off[0];
     Staged S = stage_inputs(c, keys + seg_off[0] * klen, klen, vals, vo, n, &seg);
@@ -5190,7 +4512,7 @@ int kh_trie_roots_varkeys(const uint8_t* keys, const uint64_t* koff, const uint8
       kn[i] = (uint8_t)(2 * (b - a));
     }
     kh_ctx* c = shared_ctx(current_device());
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->dev));
     c->in_kn.ensure(n + 64);
     HIPCHK(hipMemcpyAsync(c->in_kn.p, kn.data(), n, hipMemcpyHostToDevice, c->st));
@@ -5217,7 +4539,7 @@ int kh_list_roots(const uint8_t* items, const uint64_t* off, const uint64_t* seg
       return KH_OK;
     }
     kh_ctx* c = shared_ctx(current_device());
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->dev));
     c->in_aux.ensure((nseg + 1) * 8 + 64);
     HIPCHK(hipMemcpyAsync(c->in_aux.p, seg_off, (nseg + 1) * 8, hipMemcpyHostToDevice, c->st));
@@ -5354,6 +4676,10 @@ static int emit_to_host(kh_ctx* c, DevBuf& src, uint64_t tn, uint64_t tb, uint8_
                         uint8_t* rlp, uint64_t rlp_cap, uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len) {
   *n_nodes = tn;
   *rlp_len = tb;
+  if (tn == 0) {  // (no buffer needed: kh_trie_compact may have released it)
+    if (off) off[0] = 0;
+    return KH_OK;
+  }
   if (tn > node_cap || tb > rlp_cap || !hashes32 || !rlp || !off) {
     if (tn == 0 && off) off[0] = 0;
     return (tn == 0) ? KH_OK : set_err(KH_ENOSPC, "output too small");
@@ -5380,7 +4706,7 @@ int kh_trie_root_nodes(const uint8_t* keys, uint32_t klen, const uint8_t* vals, 
       return KH_OK;
     }
     kh_ctx* c = shared_ctx(current_device());
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->dev));
     Staged S = stage_inputs(c, keys, klen, vals, voff, n, nullptr);
     BuildArgs A{S.keys, klen, S.vals, S.voff, n, nullptr, 1, 0, flags, true};
@@ -5679,7 +5005,7 @@ static int verify_nodes_impl(const uint8_t* data, const uint64_t* off, uint64_t 
   if (!data || !off || (nreq && (!req32 || !req_kind))) throw KhError{KH_EINVAL, "null buffer"};
   if (n >= (1ULL << 31) || nreq >= (1ULL << 31)) throw KhError{KH_EINVAL, "batch too large"};
   kh_ctx* c = shared_ctx(current_device());
-  std::lock_guard<std::mutex> g(c->mu);
+  std::lock_guard<std::recursive_mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->dev));
   hipStream_t st = c->st;
   const uint64_t v0 = off[0], vbytes = off[n] - v0;
@@ -5927,6 +5253,7 @@ static void trie_open_nodes(kh_trie* h, const uint8_t* root32, const uint8_t* d_
 static kh_trie* trie_new(kh_ctx* c, uint32_t flags, bool forest) {
   kh_trie* h = new kh_trie();
   h->c = c;
+  h->home = c;
   h->flags = flags;
   h->forest = forest;
   memcpy(h->root, EMPTY_TRIE_HASH, 32);
@@ -5940,6 +5267,7 @@ static void check_flags(const kh_trie* h, uint32_t flags) {
 int kh_trie_open(kh_ctx* c, const uint8_t* d_keys, uint32_t klen, const uint8_t* d_vals, const uint64_t* d_voff,
                  uint64_t n, uint32_t flags, uint8_t root32[32], kh_trie** out) {
   if (!c || !out) return set_err(KH_EINVAL, "null context or handle");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
   kh_trie* h = nullptr;
   API_TRY({
     HIPCHK(hipSetDevice(c->dev));
@@ -5965,6 +5293,7 @@ int kh_trie_open(kh_ctx* c, const uint8_t* d_keys, uint32_t klen, const uint8_t*
 int kh_trie_open_nodes(kh_ctx* c, const uint8_t root32[32], const uint8_t* d_enc, const uint64_t* d_off, uint64_t n,
                        uint32_t flags, uint8_t missing32[32], kh_trie** out) {
   if (!c || !out || !root32) return set_err(KH_EINVAL, "null context, root or handle");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
   kh_trie* h = nullptr;
   API_TRY({
     HIPCHK(hipSetDevice(c->dev));
@@ -5985,7 +5314,7 @@ int kh_trie_open_nodes_host(const uint8_t root32[32], const uint8_t* enc, const 
   if (!out || !root32 || (n && (!enc || !off))) return set_err(KH_EINVAL, "null input");
   API_TRY({
     kh_ctx* c = shared_ctx(current_device());
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->dev));
     const uint64_t o0 = n ? off[0] : 0, bytes = n ? off[n] - o0 : 0;
     c->in_vals.ensure(bytes + 64);
@@ -6006,7 +5335,7 @@ int kh_trie_open_host(const uint8_t* keys, uint32_t klen, const uint8_t* vals, c
   if (!out || (n && (!keys || !voff))) return set_err(KH_EINVAL, "null input");
   API_TRY({
     kh_ctx* c = shared_ctx(current_device());
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->dev));
     Staged S = stage_inputs(c, keys, klen, vals, voff, n, nullptr);
     int rc = kh_trie_open(c, S.keys, klen, S.vals, S.voff, n, flags, root32, out);
@@ -6018,6 +5347,7 @@ int kh_trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals
                   uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
                   uint8_t root32[32], kh_stats* stats) {
   if (!h || h->forest) return set_err(KH_EINVAL, "null handle or a forest (use kh_forest_apply)");
+  HANDLE_LOCK(h);
   API_TRY({
     HIPCHK(hipSetDevice(h->c->dev));
     check_flags(h, flags);
@@ -6081,7 +5411,7 @@ int kh_trie_apply_host(kh_trie* h, const uint8_t* up_keys, const uint8_t* up_val
                        uint8_t root32[32], kh_stats* stats) {
   if (!h || h->forest) return set_err(KH_EINVAL, "null handle or a forest (use kh_forest_apply_host)");
   API_TRY({
-    std::lock_guard<std::mutex> g(h->c->mu);
+    HANDLE_LOCK(h);
     HIPCHK(hipSetDevice(h->c->dev));
     check_flags(h, flags);
     FCommit F = stage_commit(h->c, nullptr, up_keys, up_vals, up_voff, nup, nullptr, del_keys, ndel, klen);
@@ -6114,6 +5444,7 @@ int kh_forest_apply(kh_trie* f, const uint32_t* d_up_trie, const uint8_t* d_up_k
                     uint64_t ndel, uint32_t klen, uint32_t* h_tries, uint8_t* h_roots32, uint64_t cap,
                     uint64_t* n_tries, kh_stats* stats) {
   if (!f || !f->forest) return set_err(KH_EINVAL, "null handle or not a forest");
+  HANDLE_LOCK(f);
   API_TRY({
     HIPCHK(hipSetDevice(f->c->dev));
     FCommit F;
@@ -6138,7 +5469,7 @@ int kh_forest_apply_host(kh_trie* f, const uint32_t* up_trie, const uint8_t* up_
   if (!f || !f->forest) return set_err(KH_EINVAL, "null handle or not a forest");
   if ((nup && !up_trie) || (ndel && !del_trie)) return set_err(KH_EINVAL, "forest ops need trie ids");
   API_TRY({
-    std::lock_guard<std::mutex> g(f->c->mu);
+    HANDLE_LOCK(f);
     HIPCHK(hipSetDevice(f->c->dev));
     FCommit F = stage_commit(f->c, up_trie, up_keys, up_vals, up_voff, nup, del_trie, del_keys, ndel, klen);
     forest_commit(f, F, stats);
@@ -6148,12 +5479,15 @@ int kh_forest_apply_host(kh_trie* f, const uint32_t* up_trie, const uint8_t* up_
 
 int kh_forest_last_roots(kh_trie* f, uint32_t* h_tries, uint8_t* h_roots32, uint64_t cap, uint64_t* n_tries) {
   if (!f) return set_err(KH_EINVAL, "null handle");
+  HANDLE_LOCK(f);
   API_TRY({ return forest_out(f, h_tries, h_roots32, cap, n_tries); })
 }
 
 int kh_trie_savepoint(kh_trie* h, uint32_t* depth) {
   if (!h) return set_err(KH_EINVAL, "null handle");
+  HANDLE_LOCK(h);
   API_TRY({
+    HIPCHK(hipSetDevice(h->c->dev));
     trie_savepoint(h);
     if (depth) *depth = (uint32_t)h->sps.size();
   })
@@ -6161,17 +5495,22 @@ int kh_trie_savepoint(kh_trie* h, uint32_t* depth) {
 int kh_trie_rollback(kh_trie* h) {
   if (!h) return set_err(KH_EINVAL, "null handle");
   API_TRY({
-    std::lock_guard<std::mutex> g(h->c->mu);
+    HANDLE_LOCK(h);
     HIPCHK(hipSetDevice(h->c->dev));
     trie_rollback(h);
   })
 }
 int kh_trie_release(kh_trie* h) {
   if (!h) return set_err(KH_EINVAL, "null handle");
-  API_TRY({ trie_release(h); })
+  HANDLE_LOCK(h);
+  API_TRY({
+    HIPCHK(hipSetDevice(h->c->dev));
+    trie_release(h);
+  })
 }
 int kh_trie_savepoint_depth(const kh_trie* h, uint32_t* depth) {
   if (!h || !depth) return set_err(KH_EINVAL, "null handle or output");
+  HANDLE_LOCK(h);
   *depth = (uint32_t)h->sps.size();
   return KH_OK;
 }
@@ -6180,6 +5519,7 @@ int kh_trie_root_of(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_va
                     uint64_t nup, const uint8_t* d_del_keys, uint64_t ndel, uint32_t klen, uint32_t flags,
                     uint8_t root32[32], kh_stats* stats) {
   if (!h || h->forest) return set_err(KH_EINVAL, "null handle or a forest");
+  HANDLE_LOCK(h);
   API_TRY({
     HIPCHK(hipSetDevice(h->c->dev));
     check_flags(h, flags);
@@ -6202,7 +5542,7 @@ int kh_trie_root_of_host(kh_trie* h, const uint8_t* up_keys, const uint8_t* up_v
                          uint8_t root32[32], kh_stats* stats) {
   if (!h || h->forest) return set_err(KH_EINVAL, "null handle or a forest");
   API_TRY({
-    std::lock_guard<std::mutex> g(h->c->mu);
+    HANDLE_LOCK(h);
     HIPCHK(hipSetDevice(h->c->dev));
     check_flags(h, flags);
     FCommit F = stage_commit(h->c, nullptr, up_keys, up_vals, up_voff, nup, nullptr, del_keys, ndel, klen);
@@ -6216,7 +5556,7 @@ int kh_trie_root_of_host(kh_trie* h, const uint8_t* up_keys, const uint8_t* up_v
 int kh_trie_copy(kh_trie* h, kh_trie** out) {
   if (!h || !out) return set_err(KH_EINVAL, "null handle");
   API_TRY({
-    std::lock_guard<std::mutex> g(h->c->mu);
+    HANDLE_LOCK(h);
     HIPCHK(hipSetDevice(h->c->dev));
     *out = trie_copy(h);
   })
@@ -6226,11 +5566,7 @@ int kh_trie_copy(kh_trie* h, kh_trie** out) {
 // workspaces) on a host thread of its own, beside the account phase: the account keys are
 // hashed, sorted and descended, and their elements gathered, while the storage tries commit;
 // the account values are read only after the storage roots are injected into them
-// (FCommit::before_values / vals_ready).  KHST_BLOCK_OVERLAP=0 (measurement builds): one phase
-// after the other on one stream.
-#ifndef KHST_BLOCK_OVERLAP
-#define KHST_BLOCK_OVERLAP 1
-#endif
+// (FCommit::before_values / vals_ready).
 struct CtxSwap {  // a handle's commits on another context of the same device, for a scope
   kh_trie* h;
   kh_ctx* old;
@@ -6244,7 +5580,8 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
                     const uint32_t* d_a_up_trie, uint64_t na_up, const uint8_t* d_a_del_keys, uint64_t na_del,
                     uint32_t a_klen, uint8_t state_root32[32], kh_stats* stats) {
   if (!state || state->forest || !storage || !storage->forest) return set_err(KH_EINVAL, "need a state trie and a forest");
-  if (state->c != storage->c) return set_err(KH_EINVAL, "state trie and forest on different contexts");
+  if (state->home != storage->home) return set_err(KH_EINVAL, "state trie and forest on different contexts");
+  HANDLE_LOCK(state);
   API_TRY({
     kh_ctx* c = state->c;
     HIPCHK(hipSetDevice(c->dev));
@@ -6252,9 +5589,7 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     kh_stats sst{}, ast{};
     // all or nothing: a refusal in either phase (or a device failure) rolls both handles back
     // to the parent version (Ledger.scala:237-271 discards the world state of a failed attempt)
-#if KHST_BLOCK_TXN
     Txn txn(storage, state);
-#endif
     // 1. every storage trie of the block (BlockWorldState.scala:243-252 -> TrieStorage.flush)
     FCommit S;
     S.up_trie = d_s_up_trie;
@@ -6293,7 +5628,7 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
       LAUNCH_CHECK();
       return true;
     };
-    const bool overlap = KHST_BLOCK_OVERLAP && (ns_up + ns_del) && (na_up + na_del);
+    const bool overlap = (ns_up + ns_del) && (na_up + na_del);
     if (!overlap) {
       forest_commit(storage, S, &sst);
       if (inject(st, (uint32_t)storage->tries.size())) {  // (read back with the account commit's first sync, before it changes anything)
@@ -6362,9 +5697,11 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
       if (serr) std::rethrow_exception(serr);
       if (aerr) std::rethrow_exception(aerr);
     }
-#if KHST_BLOCK_TXN
+    // all or nothing, also for the lazy tails (records, anchor maps) still in flight: a failure
+    // there rolls both handles back (~Txn) instead of surfacing on a later call
+    trie_settle(storage);
+    trie_settle(state);
     txn.release();
-#endif
     memcpy(state_root32, state->root, 32);
     if (stats) {
       *stats = ast;
@@ -6390,7 +5727,7 @@ int kh_block_commit_host(kh_trie* state, kh_trie* storage, const uint32_t* s_up_
   if ((ns_up && (!s_up_trie || !s_up_voff)) || (ns_del && !s_del_trie) || (na_up && !a_up_voff))
     return set_err(KH_EINVAL, "null input");
   kh_ctx* c = state->c;
-  std::lock_guard<std::mutex> g(c->mu);
+  HANDLE_LOCK(state);
   int rc = KH_OK;
   try {
     HIPCHK(hipSetDevice(c->dev));
@@ -6442,6 +5779,7 @@ int kh_block_commit_host(kh_trie* state, kh_trie* storage, const uint32_t* s_up_
 int kh_trie_emit_nodes(kh_trie* h, uint8_t* hashes32, uint64_t node_cap, uint8_t* rlp, uint64_t rlp_cap,
                        uint64_t* off, uint64_t* n_nodes, uint64_t* rlp_len) {
   if (!h || !n_nodes || !rlp_len) return set_err(KH_EINVAL, "null handle or size outputs");
+  HANDLE_LOCK(h);
   API_TRY({
     if (!(h->flags & KH_EMIT_NODES)) throw KhError{KH_EINVAL, "trie opened without KH_EMIT_NODES"};
     HIPCHK(hipSetDevice(h->c->dev));
@@ -6537,6 +5875,7 @@ int kh_trie_get(kh_trie* h, const uint32_t* d_trie, const uint8_t* d_keys, uint3
                 uint64_t val_cap, uint64_t* d_voff, uint8_t* d_found, uint64_t* val_bytes) {
   if (!h) return set_err(KH_EINVAL, "null handle");
   if (!d_voff || (n && (!d_keys || !d_found))) return set_err(KH_EINVAL, "null buffer");
+  HANDLE_LOCK(h);
   API_TRY({
     HIPCHK(hipSetDevice(h->c->dev));
     return trie_get(h, d_trie, d_keys, klen, n, d_vals, val_cap, d_voff, d_found, val_bytes);
@@ -6548,7 +5887,7 @@ int kh_trie_get_host(kh_trie* h, const uint32_t* trie, const uint8_t* keys, uint
   if (!h) return set_err(KH_EINVAL, "null handle");
   if (!voff || (n && (!keys || !found))) return set_err(KH_EINVAL, "null buffer");
   API_TRY({
-    std::lock_guard<std::mutex> g(h->c->mu);
+    HANDLE_LOCK(h);
     kh_ctx* c = h->c;
     HIPCHK(hipSetDevice(c->dev));
     hipStream_t st = c->st;
@@ -6579,7 +5918,7 @@ int kh_trie_get_host(kh_trie* h, const uint32_t* trie, const uint8_t* keys, uint
 int kh_trie_compact(kh_trie* h, kh_trie_usage_t* before) {
   if (!h) return set_err(KH_EINVAL, "null handle");
   API_TRY({
-    std::lock_guard<std::mutex> g(h->c->mu);
+    HANDLE_LOCK(h);
     HIPCHK(hipSetDevice(h->c->dev));
     trie_compact(h, before);
   })
@@ -6588,7 +5927,7 @@ int kh_trie_compact(kh_trie* h, kh_trie_usage_t* before) {
 int kh_trie_usage(kh_trie* h, kh_trie_usage_t* u) {
   if (!h || !u) return set_err(KH_EINVAL, "null handle");
   API_TRY({
-    std::lock_guard<std::mutex> g(h->c->mu);
+    HANDLE_LOCK(h);
     HIPCHK(hipSetDevice(h->c->dev));
     trie_usage(h, u);
   })
@@ -6596,12 +5935,14 @@ int kh_trie_usage(kh_trie* h, kh_trie_usage_t* u) {
 
 int kh_trie_size(const kh_trie* h, uint64_t* n) {
   if (!h || !n) return set_err(KH_EINVAL, "null handle");
+  HANDLE_LOCK(h);
   *n = h->nleaves;
   return KH_OK;
 }
 
 int kh_trie_free(kh_trie* h) {
   if (!h) return KH_OK;
+  HANDLE_LOCK(h);  // (the lock is the home context's, which outlives the handle)
   API_TRY({
     (void)hipSetDevice(h->c->dev);
     (void)hipStreamSynchronize(h->c->st);

@@ -218,10 +218,8 @@ struct Topo {
   const uint64_t* kin; // [n*4] the keys in input order (the early leaf kernel reads them sequentially)
   uint64_t* pdinv;     // [n] per INPUT position: parent depth << 32 | sorted position; PDINV_SKIP for
                        //     a dropped duplicate
-  uint64_t* lf_dst;    // [m] nibble << 56 | parent child-record slot, LINK_TOP for a top leaf (op_leaf_link)
-  uint32_t links;      // child records may be leaf LINKS (CM_LINK: cref holds the sorted position whose
-                       // stash lf_eref is the reference; op_leaf_link_rec, op_branch_stream)
-  uint32_t* fixlist;   // [m] sorted leaves the post-join pass publishes (top, or parent depth >= LINK_PD_MAX)
+  uint64_t* lf_dst;    // [m] nibble << 56 | parent child-record slot, LINK_TOP for a top leaf (op_leaf_link;
+                       //     segmented builds)
   // leaf positions (default for unsegmented plain root builds): the leaves write no child
   // records.  A branch child's record carries CM_BR and the end of its key range (cend), so
   // the parent walks its range and finds each leaf child at the next sorted position, whose
@@ -257,7 +255,7 @@ struct Topo {
 
 enum {
   CTR_HASHES = 0, CTR_PERMS = 1, CTR_INLINE = 2, CTR_ARENA = 3, CTR_ERR = 4, CTR_EXT = 5, CTR_LONGB = 6,
-  CTR_FIXN = 7,  // fixlist length (row 0; the stat shards use indices 0-2 and 5 of their rows)
+  // (row 0; the stat shards use indices 0-2 and 5 of their rows)
   // scratch slots for device-side totals read back by the host
   CTR_TIE = 8, CTR_M = 9, CTR_B = 10, CTR_BRBYTES = 11, CTR_LFBYTES = 12, CTR_C = 13, CTR_E0 = 14, CTR_E1 = 15,
   CTR_N = 16
@@ -982,57 +980,9 @@ KH_HD uint32_t op_leaf_hash(const Topo& T, uint64_t i, uint32_t* inl) {
   return leaf_hash_at(T, i, (const uint64_t*)(T.arena + T.lf_aoff[i]), 1, L, inl);
 }
 
-// Leaf header of a 32-byte key (leaf_header's bytes, <= 38 B) built in 5 registers, no
-// byte stream: [list prefix][0x80 + h if h > 1][HP first byte] at bytes [0, o1), the key
-// bytes [kb0, 32) at [o1, o1 + h - 1) (the key shifted by o1 - kb0 bytes: a byte funnel
-// and a word shift of 0..4), then the value's string prefix (0, 1 or 2 bytes).  Bytes
-// past the header are zero.
-KH_HD void leaf_header_regs(const Key4& k, const LeafGeom& g, uint64_t vlen, uint64_t hw[5]) {
-  const uint32_t lhl = g.payload < 56 ? 1u : 2u;  // short leaf: payload <= 133
-  const uint64_t lh = lhl == 1 ? (0xC0 + g.payload) : (0xF8 | (g.payload << 8));
-  const uint32_t o1 = lhl + (g.h > 1 ? 1u : 0u) + 1u;
-  uint64_t pw = lh;
-  if (g.h > 1) pw |= (uint64_t)(0x80 + g.h) << (8 * lhl);
-  pw |= (uint64_t)g.hp0 << (8 * (o1 - 1));
-  const uint32_t kb0 = (g.s + 1) / 2;
-  const int32_t dl = (int32_t)o1 - (int32_t)kb0;  // message byte x holds key byte x - dl
-  const uint32_t rb = (uint32_t)dl & 7u;
-  const uint32_t sw = (uint32_t)(-(dl >> 3));  // 0..4: word q = Y[q + sw]
-  const uint64_t K[4] = {k.w0, k.w1, k.w2, k.w3};
-  uint64_t A[9];  // Y[t] = bytes [8t - rb, 8t - rb + 8) of the key
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const uint64_t cur = t < 4 ? K[t] : 0, prv = (t >= 1 && t <= 4) ? K[t - 1] : 0;
-    A[t] = rb ? (cur << (8 * rb)) | (prv >> (64 - 8 * rb)) : cur;
-  }
-#pragma unroll
-  for (int st = 0; st < 3; ++st) {  // A[v] <- A[v + sw]
-    const int d = 1 << st;
-    const bool on = (sw >> st) & 1;
-#pragma unroll
-    for (int v = 0; v < 9; ++v) A[v] = on ? (v + d < 9 ? A[v + d] : 0) : A[v];
-  }
-  const uint32_t e = o1 + g.h - 1;  // the value prefix's first byte
-  const bool vh_on = !(vlen == 1 && g.v0 < 0x80);
-  const uint64_t vh = !vh_on ? 0 : vlen < 56 ? (0x80 + vlen) : (0xB8 | (vlen << 8));
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    uint64_t x = q == 0 ? (A[0] & ~low_bytes_mask(o1)) | pw : A[q];
-    const int32_t d = (int32_t)e - 8 * q;
-    if (d >= 0 && d < 8) x |= vh << (8 * d);
-    else if (d == -1) x |= vh >> 8;
-    hw[q] = x;
-  }
-}
-
 // ---- early leaves: parent depth from the two adjacent boundaries (= resolve_parent's pd)
 constexpr uint8_t EMETA_LONG = 0xFF;
 constexpr uint64_t PDINV_SKIP = ~0ULL;
-KH_HD int32_t leaf_pd_early(const Topo& T, uint64_t i) {
-  uint32_t va = i > 0 ? T.u[i - 1] : 0, vc = i + 1 < T.m ? T.u[i] : 0;
-  uint32_t v = va > vc ? va : vc;
-  return v == 0 ? (int32_t)T.depth0 - 1 : (int32_t)v - 1;
-}
 // Plain root builds hash their leaves in INPUT order right after op_lcp, on a second
 // stream, while the branch topology is computed.  Input order reads the keys and the
 // packed values sequentially (the sorted order would gather every value span at random:
@@ -1042,108 +992,6 @@ KH_HD int32_t leaf_pd_early(const Topo& T, uint64_t i) {
 // fire-and-forget); op_leaf_topo_early then moves it into the parent's child record.
 KH_HD void op_pd_scatter(const Topo& T, uint64_t i) {
   pd_scatter_vals(T, i, i > 0 ? T.u[i - 1] : 0, i + 1 < T.m ? T.u[i] : 0);
-}
-// One input j.  Every load is issued up front, independent of each other's results
-// except the span offsets: the scatter record, the key, the value span's offsets, then
-// the 16-byte pairs of the value buffer that hold the span (`ld2(p, lo, hi)` loads pair
-// p of the buffer whose byte `vmis` is value byte 0; only pairs overlapping the span are
-// read).  The addresses do not depend on the parent depth or on the header length, so
-// the value reads overlap the other loads (one dependent round trip, not three).
-// The message (<= 135 B) is then assembled in registers straight into the Keccak
-// state: header bytes [0, P) from leaf_header_regs, value bytes [P, L) moved into place
-// by a byte funnel and a 3-stage word shift.  Returns permutations; *inl / *longb count inline leaves and long-leaf
-// arena bytes.
-constexpr int LEAF_IN_PAIRS = 10;  // covers any span of a short leaf (<= 132 B) at any alignment
-template <typename LD2>
-KH_HD uint32_t op_leaf_in(const Topo& T, uint64_t j, LD2 ld2, uint32_t vmis, uint32_t* inl, uint32_t* longb) {
-  *inl = 0;
-  *longb = 0;
-  const uint64_t pv = T.pdinv[j];
-  const Key4 k = load_key(T.kin, j);
-  const uint64_t off = T.voff[j];
-  const uint32_t vlen = (uint32_t)(T.voff[j + 1] - off);
-  const uint64_t vb = off + vmis;  // buffer byte of value byte 0
-  const uint32_t mis = (uint32_t)(vb & 15);
-  const int64_t pf = (int64_t)(vb >> 4);
-  const uint64_t np = vlen ? ((vb + vlen - 1) >> 4) - (vb >> 4) + 1 : 0;  // pairs under the span
-  uint64_t W[2 * LEAF_IN_PAIRS];
-#pragma unroll
-  for (int p = 0; p < LEAF_IN_PAIRS; ++p) {
-    uint64_t lo = 0, hi = 0;
-    if ((uint64_t)p < np) ld2(pf + p, lo, hi);
-    W[2 * p] = lo;
-    W[2 * p + 1] = hi;
-  }
-  if (pv == PDINV_SKIP) return 0;  // an earlier put of a key put again later
-  const int32_t pd = (int8_t)(uint8_t)(pv >> 32);
-  const uint64_t si = (uint32_t)pv;  // sorted position: where the reference is stashed
-  const uint32_t v0 = vlen == 1 ? (uint32_t)(((mis & 8) ? W[1] : W[0]) >> (8 * (mis & 7))) & 0xFF : 0;
-  const LeafGeom g = leaf_geom(k, pd, vlen, v0);
-  if (g.L > LEAF_SHORT_MAX) {  // encoded + hashed by op_leaf_long into its arena slot
-    T.lf_emeta[si] = EMETA_LONG;
-    *longb = (g.L + 7) & ~7u;
-    if (T.longlist) T.longlist[ctr_add(&T.ctr[CTR_LONGN], 1)] = si;
-    return 0;
-  }
-  const bool top = pd == (int32_t)T.depth0 - 1;
-  uint64_t hw[5];
-  leaf_header_regs(k, g, vlen, hw);
-  const uint32_t L = g.L, P = L - vlen;
-  // message byte x in [P, L) is byte x - P + mis of W.  With P - mis = 8a + r (0 <= r < 8;
-  // a 32-byte key's header is <= 38 B, so -2 <= a <= 4): message word q is bytes
-  // [8(q - a) - r, +8) of W = Y[q - a], Y[t] = bytes [8t - r, 8t - r + 8) of W (rb = r).
-  const int32_t D = (int32_t)P - (int32_t)mis;
-  const uint32_t rb = (uint32_t)D & 7u;
-  const uint32_t s = (uint32_t)((D >> 3) + 2);  // word shift, 0..6: message word q = Y[q + 2 - s]
-  uint64_t A[2 * LEAF_IN_PAIRS - 1];
-#pragma unroll
-  for (int t = 0; t < 2 * LEAF_IN_PAIRS - 1; ++t) {
-    const uint64_t lo = t ? W[t - 1] : 0;
-    A[t] = rb ? (W[t] << (8 * rb)) | (lo >> (64 - 8 * rb)) : W[t];
-  }
-#pragma unroll
-  for (int st = 0; st < 3; ++st) {  // A[v] <- A[v - s] (zeros shifted in)
-    const int d = 1 << st;
-    const bool on = (s >> st) & 1;
-#pragma unroll
-    for (int v = 2 * LEAF_IN_PAIRS - 2; v >= 0; --v) A[v] = on ? (v >= d ? A[v - d] : 0) : A[v];
-  }
-  KState S = {};
-  uint64_t head[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int q = 0; q < 17; ++q) {
-    uint64_t x = A[q + 2];
-    const uint32_t b0 = 8u * (uint32_t)q;
-    if (b0 + 8 <= P || b0 >= L) x = 0;  // header-only or past the end
-    else {
-      if (b0 < P) x &= ~low_bytes_mask(P - b0);
-      if (b0 + 8 > L) x &= low_bytes_mask(L - b0);
-    }
-    if (q < 5) x |= hw[q];
-    if (q < 4) head[q] = x;
-    if ((L >> 3) == (uint32_t)q) x ^= 0x01ULL << (8 * (L & 7));
-    if (q == 16) x ^= 0x80ULL << 56;
-    S.lo[q] = (uint32_t)x;
-    S.hi[q] = (uint32_t)(x >> 32);
-  }
-  uint64_t* r = T.lf_eref + 4 * si;
-  uint32_t perms = 0;
-  if (L >= 32 || top) {  // a leaf embedded in its parent is never hashed (Node.scala:114)
-    keccakf(S);
-    for (int q = 0; q < 4; ++q) r[q] = lane(S, q);
-    perms = 1;
-  } else {
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t b = 8u * (uint32_t)q;
-      r[q] = b < L ? head[q] & low_bytes_mask(L - b < 8 ? L - b : 8) : 0;
-    }
-    *inl = 1;
-  }
-  // a top leaf is >= 35 B (its path is >= 63 nibbles: an HP of >= 33 B), so its stash is
-  // always the hash
-  if (L < 32) T.lf_emeta[si] = (uint8_t)L;  // the preset 32 stands for every hashed leaf (one scattered
-                                           // byte write less per leaf)
-  return perms;
 }
 // ---- leaf message assembly on 32-bit dwords (k_leaf_in).  The message of a short
 // account leaf is prefix [0, o1) | key bytes [kb0, 32) at [o1, e) | value prefix [e, P) |
@@ -1230,7 +1078,7 @@ KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, u
   if (live && lng) {  // encoded + hashed by op_leaf_long into its arena slot
     T.lf_emeta[si] = EMETA_LONG;
     *longb = (Lnr + 7) & ~7u;
-    if (T.longlist) T.longlist[ctr_add(&T.ctr[CTR_LONGN], 1)] = si;  // link mode: the post-join pass finds it
+    if (T.longlist) T.longlist[ctr_add(&T.ctr[CTR_LONGN], 1)] = si;  // leaf positions: the post-join pass finds it
   }
   if (!use) return 0;
   // ---- second round trip: the value's first byte, the key and the value at their shifts
@@ -1357,15 +1205,6 @@ KH_HD uint32_t op_leaf_in3(const Topo& T, uint64_t j, uint64_t n, WAVE wave, uin
   const bool live = pv != PDINV_SKIP;  // not an earlier put of a key put again later
   return op_leaf_core(T, live, (int32_t)(int8_t)(uint8_t)(pv >> 32), (uint32_t)pv, j, n, wave, inl, longb);
 }
-// sorted order (k_leaf_sorted, KHST_LEAF=sorted): the parent depth straight from the two
-// adjacent boundaries, the key and value through the sorted input index (random reads)
-template <typename WAVE>
-KH_HD uint32_t op_leaf_sorted(const Topo& T, uint64_t i, uint64_t n, WAVE wave, uint32_t* inl, uint32_t* longb) {
-  const bool live = i < T.m;
-  const uint64_t j = live ? (T.sidx ? T.sidx[i] : i) : 0;
-  return op_leaf_core(T, live, live ? leaf_pd_early(T, i) : 0, (uint32_t)i, j, n, wave, inl, longb);
-}
-
 // value span of sorted leaf i (early builds gather no spans: through the input index)
 KH_HD void leaf_span_early(const Topo& T, uint64_t i, uint64_t* off, uint32_t* len) {
   if (T.svoff) {
@@ -1393,33 +1232,6 @@ KH_HD void op_leaf_link(const Topo& T, uint64_t i) {
   }
   const Key4 k = sorted_key(T, i, (uint32_t)P.pd + 1);
   T.lf_dst[i] = ((uint64_t)key_nibble(k, P.pd) << 56) | ((uint64_t)T.br_cbase[P.bid] + P.pord);
-}
-// Link records (default for plain root builds): a leaf under a parent of depth < LINK_PD_MAX
-// has a path of >= 56 nibbles, so its encoding is >= 32 B and its reference is its hash (a
-// long leaf's hash is published over the link later by op_leaf_long).  Its child record is
-// written right here, while it is still being hashed, as a LINK to its stash: length 32,
-// the nibble, and the sorted position, which the branch kernel follows (op_branch_stream).
-// Every other leaf (the top one, and those under deeper parents, which may be inline) goes
-// on the fix list for the post-join pass (op_leaf_move).  Returns true when listed.
-constexpr int32_t LINK_PD_MAX = 8;
-constexpr uint16_t CM_LINK = 0x8000;
-KH_HD bool op_leaf_link_rec(const Topo& T, uint64_t i) {
-  const int64_t a = (int64_t)i - 1, c = (i + 1 < T.m) ? (int64_t)i : -1;
-  const Parent P = resolve_parent(T, a, c);
-  if (P.bid == NONE) {
-    T.lf_dst[i] = LINK_TOP;
-    return true;
-  }
-  const Key4 k = sorted_key(T, i, (uint32_t)P.pd + 1);
-  const uint32_t nib = key_nibble(k, P.pd);
-  const uint64_t slot = (uint64_t)T.br_cbase[P.bid] + P.pord;
-  if (P.pd >= LINK_PD_MAX) {
-    T.lf_dst[i] = ((uint64_t)nib << 56) | slot;
-    return true;
-  }
-  T.cref[4 * slot] = i;
-  T.cmeta[slot] = (uint16_t)(32u | (nib << 8) | CM_LINK);
-  return false;
 }
 template <typename AllocFn>
 KH_HD void op_leaf_topo_early(const Topo& T, uint64_t i, AllocFn alloc);
@@ -1776,94 +1588,7 @@ KH_HD void window_place(uint64_t* slot, uint64_t stride, uint32_t w0, uint32_t o
     slot[(W - w0 / 8) * stride] ^= (y ^ 0x8080808080808080ULL) & m;
   }
 }
-KH_HD uint32_t op_branch_direct(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl) {
-  const uint32_t ext = T.br_ext[j];
-  const bool top = T.br_parent[j] == NONE;
-  *inl = 0;
-  uint64_t hb[4] = {0, 0, 0, 0}, bhead[4] = {0, 0, 0, 0};
-  uint32_t L, perms = 0, ninl = 0;
-  {
-    const uint32_t k = T.br_k[j];
-    const uint64_t cb = T.br_cbase[j];
-    const uint16_t* cm = T.cmeta + cb;
-    const uint64_t* cr = T.cref + 4 * cb;
-    const uint32_t payload = branch_payload(T, j);
-    const uint32_t hh = rlp_hdr_len(payload);
-    L = hh + payload;
-    T.br_len[j] = L;
-    const bool hashit = L >= 32 || (top && ext == 0);
-    const uint32_t nfull = L / 136;
-    KState S = {};
-    for (uint32_t b = 0; b <= nfull; ++b) {
-      const uint32_t w0 = 136u * b;
-#pragma unroll
-      for (int q = 0; q < 17; ++q) {  // 0x80 over the encoding's bytes of this window
-        const uint32_t a = w0 + 8u * (uint32_t)q;
-        const uint32_t n80 = L > a ? (L - a < 8 ? L - a : 8) : 0;
-        slot[q * stride] = low_bytes_mask(n80) & 0x8080808080808080ULL;
-      }
-      if (b == 0) {  // the list header
-        const uint32_t pl = payload;
-        const uint64_t hdr = hh == 1 ? (0xC0 + pl)
-                             : hh == 2 ? (0xF8 | ((uint64_t)pl << 8))
-                                       : (0xF9 | ((uint64_t)(pl >> 8) << 8) | ((uint64_t)(pl & 0xFF) << 16));
-        slot[0] ^= (hdr ^ 0x8080808080808080ULL) & low_bytes_mask(hh);
-      }
-      uint32_t run = 0;  // sum of (item length - 1) over the children placed so far
-      for (uint32_t c = 0; c < k; ++c) {
-        const uint32_t mc = cm[c], len = mc & 0xFF, ilen = len == 32 ? 33 : len;
-        const uint32_t off = hh + (mc >> 8) + run;
-        run += ilen - 1;
-        if (off + ilen <= w0) continue;
-        if (off >= w0 + 136) break;
-        const uint64_t r0 = cr[4 * c], r1 = cr[4 * c + 1], r2 = cr[4 * c + 2], r3 = cr[4 * c + 3];
-        uint64_t I[5];
-        if (len == 32) {
-          I[0] = 0xA0 | (r0 << 8);
-          I[1] = (r0 >> 56) | (r1 << 8);
-          I[2] = (r1 >> 56) | (r2 << 8);
-          I[3] = (r2 >> 56) | (r3 << 8);
-          I[4] = r3 >> 56;
-        } else {  // an embedded child: its bytes (the capped reference is zero past len)
-          I[0] = r0;
-          I[1] = r1;
-          I[2] = r2;
-          I[3] = r3;
-          I[4] = 0;
-        }
-        window_place(slot, stride, w0, off, ilen, I);
-      }
-      if (!hashit) break;  // embedded in its parent: never hashed (Node.scala:114)
-      const uint32_t rem = b < nfull ? 136 : L - 136 * nfull;
-#pragma unroll
-      for (int q = 0; q < 17; ++q) {
-        uint64_t x = slot[q * stride];  // zero past the encoding already
-        if (b == nfull) {
-          if ((rem >> 3) == (uint32_t)q) x ^= 0x01ULL << (8 * (rem & 7));
-          if (q == 16) x ^= 0x80ULL << 56;
-        }
-        kxor(S, q, x);
-      }
-      keccakf(S);
-    }
-    if (hashit) {
-      for (int q = 0; q < 4; ++q) hb[q] = lane(S, q);
-      perms = nfull + 1;
-    }
-    if (L < 32)
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t base = 8u * (uint32_t)q;
-        bhead[q] = base < L ? slot[q * stride] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0;
-      }
-    ninl = hashit ? 0 : 1;
-    branch_keep(T, j, L, hb, bhead);
-  }
-  perms += branch_publish(T, j, L, hb, bhead, Slot{slot, stride}, &ninl);
-  *inl = ninl;
-  return perms;
-}
-
-// The same direct assembly with the children streamed ONCE in order: the window loop
+// Direct window assembly with the children streamed ONCE in order: the window loop
 // resumes at the first child not yet placed (an item crossing a window edge is placed
 // again, its tail, in the next window), the next child's record is loaded while the
 // current one is placed, and the child lengths for the payload are loaded as one batch
@@ -1911,7 +1636,7 @@ struct ChildSrc {
 };
 // where op_branch_stream reads the children (one instantiation each, so that a kernel
 // carries no dead path: the branch kernels sit at the VGPR limit of 4 waves per SIMD)
-enum { SRC_REC = 0, SRC_LDS = 1, SRC_LINK = 2, SRC_POS = 3, SRC_POSK = 4 };
+enum { SRC_REC = 0, SRC_LDS = 1, SRC_POS = 3, SRC_POSK = 4 };
 template <int SRC>
 KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl,
                                   ChildSrc src) {
@@ -1988,8 +1713,8 @@ KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uin
     uint64_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
     uint32_t nm = 0;
     uint32_t lpn = POS ? T.br_first[j] : 0;  // leaf positions: sorted position of child cc
-    // child c's reference: its record, or the stash a LINK record points at (op_leaf_link_rec),
-    // or (leaf positions) a leaf child's stash at the next position of the range
+    // child c's reference: its record, or (leaf positions) a leaf child's stash at the next
+    // position of the range
     auto load_child = [&](uint32_t cc) {
       nm = cmeta_at(cc);
       const uint64_t* p = cref_at(cc);
@@ -1999,9 +1724,6 @@ KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uin
         if (!br) p = T.lf_eref + 4 * (uint64_t)lpn;
         nm = br ? nm : lm;
         lpn = br ? e : lpn + 1;
-        n0 = p[0], n1 = p[1], n2 = p[2], n3 = p[3];
-      } else if (SRC == SRC_LINK && (nm & CM_LINK)) {
-        p = T.lf_eref + 4 * p[0];
         n0 = p[0], n1 = p[1], n2 = p[2], n3 = p[3];
       } else {
         n0 = p[0], n1 = p[cs], n2 = p[2 * cs], n3 = p[3 * cs];
@@ -2083,7 +1805,6 @@ KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint6
     if (pos_level_ok(T, T.br_depth[j])) return op_branch_stream_t<SRC_POS>(TL, j, slot, stride, inl, src);
     return op_branch_stream_t<SRC_POSK>(TL, j, slot, stride, inl, src);
   }
-  if (T.links) return op_branch_stream_t<SRC_LINK>(T, j, slot, stride, inl, src);
   return op_branch_stream_t<SRC_REC>(T, j, slot, stride, inl, src);
 }
 

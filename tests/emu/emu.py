@@ -25,18 +25,17 @@ def lib():
         L.emu_set_leaf_mode.argtypes = [ctypes.c_int]
         L.emu_set_link_mode.argtypes = [ctypes.c_int]
         L.emu_xlane_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
-        L.emu_build_grouped.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, vp]
         _lib = L
     return _lib
 
 
 def set_leaf_mode(mode):
-    """0 / 1: op_leaf_in3 with the loosest / the lane's own wave bounds; 2: op_leaf_in."""
+    """0 / 1: op_leaf_in3 with the loosest / the lane's own wave bounds."""
     lib().emu_set_leaf_mode(mode)
 
 
 def set_link_mode(mode):
-    """1: leaf link records + fix pass (KHST_LEAF_LINKS=1); 0: link slots + copy pass (default)."""
+    """0: link slots + copy pass (segmented builds); 2: leaf positions (unsegmented builds)."""
     lib().emu_set_link_mode(mode)
 
 
@@ -70,23 +69,6 @@ def build(keys32, vals, seg=None, nseg=1, depth0=0):
     res = [(oh[32 * r:32 * r + 32].tobytes(), int(ol[r]), oi[32 * r:32 * r + int(ol[r])].tobytes() if ol[r] < 32 else b"")
            for r in range(nres)]
     return res, st
-
-
-def build_grouped(keys32, vals, gb):
-    """The grouped build's replay (2^gb top-nibble groups, khst.hip grouped_build): (root, stats
-    [m, B, node hashes, perms, inline, extensions]) or (None, rc) when the device would redo it
-    as a plain build."""
-    n = len(keys32)
-    kb = _buf(b"".join(keys32) + b"\0" * 16)
-    vb, off = pack(vals)
-    root = np.zeros(32, np.uint8)
-    st = np.zeros(6, np.uint64)
-    rc = lib().emu_build_grouped(kb.ctypes.data, vb.ctypes.data, off.ctypes.data, n, gb, root.ctypes.data,
-                                 st.ctypes.data)
-    if rc == -9:
-        return None, rc
-    assert rc == 0, rc
-    return root.tobytes(), st
 
 
 def kec256(b: bytes) -> bytes:

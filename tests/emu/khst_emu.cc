@@ -22,9 +22,6 @@
 
 using namespace khst;
 
-// which form of the early leaf kernel the replay runs: 0 / 1 = op_leaf_in3 with the
-// loosest / the lane's own wave bounds, 2 = op_leaf_in (KHST_LEAF=v2), 3 = op_leaf_sorted
-// (KHST_LEAF=sorted) with the loosest bounds
 // The device's tile-local topology (khst.hip k_topo_tile, then k_ansv_list / k_chain_list
 // after the whole-array pyramid P) replayed tile by tile with tiles of `tile` boundaries
 static void topo_tiles(const Topo& T, const Pyr& P, uint64_t nb, uint32_t tile) {
@@ -53,38 +50,33 @@ static void topo_tiles(const Topo& T, const Pyr& P, uint64_t nb, uint32_t tile) 
   for (uint32_t b : clist) op_chain(T, b);
 }
 
+// which form of the early leaf kernel the replay runs: 0 / 1 = op_leaf_in3 with the
+// loosest / the lane's own wave bounds (every dword masked / every dword classified)
 static int g_leaf_mode = 0;
-// 1: the leaves' child records as links (op_leaf_link_rec, KHST_LEAF_LINKS=1) with the
-// post-join fix pass and op_branch_stream on every branch; 0: link slots + the copy pass
-// (KHST_LEAF_POS=0); 2: leaf positions (the device default for unsegmented builds): no leaf
-// child records, the branches read each leaf child's stash at its sorted position, on
-// alternate branches straight from the stash (op_branch_stream) and through the records a
-// small level writes first (op_leaf_children)
+// 0: link slots + the copy pass (op_leaf_link / op_leaf_move: the device's segmented
+// builds); 2: leaf positions (the device's unsegmented builds): no leaf child records, the
+// branches read each leaf child's stash at its sorted position, on alternate branches
+// straight from the stash (op_branch_stream) and through the records a small level writes
+// first (op_leaf_children)
 static int g_link_mode = 0;
 
 // keys: n*32 (already keccak'd), vals/voff packed; seg nullable.
 // Outputs per result r: hash (32 B), enc length, inline bytes (32 B).
 // stats_out[0..5] = m, B, node hashes, node perms, inline nodes, extensions.
-// list (nullable): one group of a grouped build (khst.hip grouped_build): the build covers
-// only the inputs list[0 .. ng) (ascending input indices) of the n inputs, sorts their global
-// indices, and hashes its leaves in list order (k_leaf_in_list) against the whole buffers
 static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, uint64_t n, const uint32_t* seg,
                       uint64_t nseg, uint32_t depth0, uint8_t* out_hash, uint32_t* out_len, uint8_t* out_inl,
-                      uint64_t* stats_out, const uint32_t* list = nullptr, uint64_t ng = 0) {
+                      uint64_t* stats_out) {
   const bool segmented = seg != nullptr;
   const uint64_t nres = segmented ? nseg : (depth0 == 1 ? 16 : 1);
   std::vector<uint64_t> res_hash(nres * 4, 0), res_inl(nres * 4, 0);
   std::vector<uint32_t> res_len(nres, 0);
-  if (n == 0 || (list && ng == 0)) {
+  if (n == 0) {
     memset(out_len, 0, nres * 4);
     return 0;
   }
   // sort (stable, by segment then key bytes), keep the last duplicate
-  std::vector<uint32_t> order(list ? ng : n);
-  if (list)
-    std::copy(list, list + ng, order.begin());
-  else
-    std::iota(order.begin(), order.end(), 0u);
+  std::vector<uint32_t> order(n);
+  std::iota(order.begin(), order.end(), 0u);
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
     if (segmented && seg[a] != seg[b]) return seg[a] < seg[b];
     return memcmp(keys + 32ull * a, keys + 32ull * b, 32) < 0;
@@ -157,7 +149,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.ctr = ctr.data();
   T.depth_hist = hist.data();
   uint64_t B = 0;
-  const bool lpos = g_link_mode == 2 && !segmented && g_leaf_mode != 2;  // (as on the device: not with v2)
+  const bool lpos = g_link_mode == 2 && !segmented;
   std::vector<uint32_t> br_end(nbb, 0);
   if (lpos) {
     T.br_end = br_end.data();
@@ -210,8 +202,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   }
   // plain builds replay the device's early-leaf path: parent depths scattered to input
   // order (k_pd_scatter), leaves hashed in input order (k_leaf_in), references stashed
-  // per input and published after the topology (k_leaf_topo_early)
-  const bool early = true;
+  // per input and published after the topology
   std::vector<uint64_t> eref(4 * m + 4);
   std::vector<uint8_t> emeta(m + 1, 32);  // preset as on the device
   std::vector<uint64_t> pdinv(n + 1, PDINV_SKIP);
@@ -220,7 +211,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.lf_emeta = emeta.data();
   T.pdinv = pdinv.data();
   std::vector<uint32_t> longlist(m + 1);
-  T.longlist = (g_link_mode == 1 || lpos) ? longlist.data() : nullptr;
+  T.longlist = lpos ? longlist.data() : nullptr;
   T.svoff = nullptr;  // as on the device: no sorted spans in early builds
   T.svlen = nullptr;
   for (uint64_t i = 0; i < m; ++i) op_pd_scatter(T, i);
@@ -236,35 +227,16 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   std::vector<uint64_t> kbuf(4 * n + 16, 0);
   if (n) memcpy(kbuf.data(), T.kin, 32 * n);
   T.kin = kbuf.data();
-  if (g_leaf_mode == 2) {  // the round-2 kernel's form (KHST_LEAF=v2)
-    const uint32_t vmis = (uint32_t)((uintptr_t)T.vals & 15);
-    const uint8_t* vp = T.vals - vmis;
-    auto ld2 = [vp](int64_t p, uint64_t& lo, uint64_t& hi) {
-      memcpy(&lo, vp + 16 * p, 8);
-      memcpy(&hi, vp + 16 * p + 8, 8);
-    };
-    for (uint64_t j = 0; j < n; ++j) {
-      uint32_t in1 = 0, lb = 0;
-      uint32_t p = op_leaf_in(T, j, ld2, vmis, &in1, &lb);
-      perms += p;
-      hashes += p ? 1 : 0;
-      inl += in1;
-      longb += lb;
-    }
-  } else {
+  {
     // op_leaf_in3 with the loosest wave bounds (mode 0: every dword takes its masked form)
     // or the lane's own values (mode 1: every dword takes its classified form)
     auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {
       if (g_leaf_mode == 0 || !use) return WaveBounds{0, 255, 0, 255};
       return WaveBounds{e, e, llo, lhi};
     };
-    const bool sorted_order = g_leaf_mode == 3;  // KHST_LEAF=sorted (k_leaf_sorted)
-    if (sorted_order) std::fill(emeta.begin(), emeta.end(), (uint8_t)32);
-    const uint64_t nlanes = list ? ng : sorted_order ? m : n;
-    for (uint64_t t = 0; t < nlanes + 3; ++t) {  // lanes past the end take part as on the device
+    for (uint64_t j = 0; j < n + 3; ++j) {  // lanes past the end take part as on the device
       uint32_t in1 = 0, lb = 0;
-      const uint64_t j = list ? (t < ng ? list[t] : n) : t;  // k_leaf_in_list: the group's inputs
-      uint32_t p = sorted_order ? op_leaf_sorted(T, j, n, wave, &in1, &lb) : op_leaf_in3(T, j, n, wave, &in1, &lb);
+      uint32_t p = op_leaf_in3(T, j, n, wave, &in1, &lb);
       perms += p;
       hashes += p ? 1 : 0;
       inl += in1;
@@ -288,30 +260,15 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   };
   std::vector<uint64_t> dst(m + 1);
   T.lf_dst = dst.data();
-  const bool links = early && g_link_mode == 1;
   std::vector<uint32_t> cend(C + 1, 0);
   if (lpos) {  // only the long leaves' parents and arena slots
     T.lf_inline = inl ? 1 : 0;
     for (uint64_t q = 0; q < ctr[CTR_LONGN]; ++q) op_leaf_topo_early(T, longlist[q], bump);
-  } else if (links) {  // the device default: link records, then the fix pass over the listed leaves
-    std::vector<uint32_t> fix;
-    for (uint64_t i = 0; i < m; ++i)
-      if (op_leaf_link_rec(T, i)) fix.push_back((uint32_t)i);
-    for (uint32_t i : fix)
-      if (T.lf_emeta[i] != EMETA_LONG) op_leaf_move(T, i, bump);
-    for (uint64_t q = 0; q < ctr[CTR_LONGN]; ++q) op_leaf_topo_early(T, longlist[q], bump);
-    T.links = 1;
-  } else {
-    if (early)  // the device's split publish: slots during the hashing, then the copy
-      for (uint64_t i = 0; i < m; ++i) op_leaf_link(T, i);
-    for (uint64_t i = 0; i < m; ++i) {
-      if (early)
-        op_leaf_move(T, i, bump);
-      else
-        op_leaf_topo(T, i, bump);
-    }
+  } else {  // the device's split publish: slots during the hashing, then the copy
+    for (uint64_t i = 0; i < m; ++i) op_leaf_link(T, i);
+    for (uint64_t i = 0; i < m; ++i) op_leaf_move(T, i, bump);
   }
-  if (early && lfb != longb) return -7;  // the arena is sized by the early count
+  if (lfb != longb) return -7;  // the arena is sized by the early count
   std::vector<uint64_t> arena((lfb + 64) / 8 + 1), lmsg(LEAF_WORDS * m + 1), bmsg(BR_WORDS * B + 1),
       xmsg(EXT_WORDS * B + 1);
   T.lmsg = lmsg.data();
@@ -329,12 +286,10 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.lb = lbv.data();
   std::vector<uint8_t> br_dirty(B + 1, 1);
   T.arena = (uint8_t*)arena.data();
-  if (!early)
-    for (uint64_t i = 0; i < m; ++i) op_leaf_prep(T, i, T.vals + T.svoff[i], T.svlen[i]);
   if (lpos) T.cend = cend.data();  // (set after the leaf kernel, as on the device)
   for (uint64_t i = 0; i < m; ++i) {
     uint32_t in1 = 0;
-    uint32_t p = early ? op_leaf_long(T, i, &in1) : op_leaf_hash(T, i, &in1);
+    uint32_t p = op_leaf_long(T, i, &in1);
     perms += p;
     hashes += p ? 1 : 0;
     inl += in1;
@@ -346,16 +301,13 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       uint32_t j = lorder[g];
       uint32_t in1 = 0;
       uint64_t slot[LEAF_WORDS + 1];
-      // fixed-length keys: both device assemblies, on alternate branches
       uint32_t p;
       if (lpos && (j & 1)) {  // a small level's path: records written, then read as a copy
         op_leaf_children(T, j);
         const uint64_t cb = T.br_cbase[j];
         p = op_branch_stream(T, j, slot, 1, &in1, ChildSrc{T.cmeta + cb, T.cref + 4 * cb, 1});
       } else {
-        p = T.kn                            ? op_branch_fused(T, j, slot, 1, &in1)
-            : ((j & 1) && !T.links && !lpos) ? op_branch_direct(T, j, slot, 1, &in1)
-                                             : op_branch_stream(T, j, slot, 1, &in1);
+        p = T.kn ? op_branch_fused(T, j, slot, 1, &in1) : op_branch_stream(T, j, slot, 1, &in1);
       }
       perms += p;
       hashes += branch_hash_count(T, j, p);
@@ -385,48 +337,6 @@ int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, ui
               uint64_t nseg, uint32_t depth0, uint8_t* out_hash, uint32_t* out_len, uint8_t* out_inl,
               uint64_t* stats_out) {
   return build_core(keys, vals, voff, n, seg, nseg, depth0, out_hash, out_len, out_inl, stats_out);
-}
-
-// a grouped build (khst.hip grouped_build): the inputs split stably by the top gb bits of
-// their keys, each group a depth-1 build over its own inputs (list order), the 16 top-nibble
-// references folded into the root (kh_fold_root16's encoding)
-int emu_build_grouped(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, uint64_t n, uint32_t gb,
-                      uint8_t* root32, uint64_t* stats_out) {
-  const uint32_t G = 1u << gb;
-  std::vector<std::vector<uint32_t>> lists(G);
-  for (uint64_t i = 0; i < n; ++i) lists[keys[32 * i] >> (8 - gb)].push_back((uint32_t)i);
-  uint64_t refs[64] = {}, st[6] = {}, tot[6] = {};
-  uint32_t lens[16] = {};
-  int nonempty = 0, inl_tops = 0;
-  for (uint32_t g = 0; g < G; ++g) {
-    uint8_t h[16 * 32], in[16 * 32];
-    uint32_t len[16];
-    int rc = build_core(keys, vals, voff, n, nullptr, 1, 1, h, len, in, st, lists[g].data(), lists[g].size());
-    if (rc) return rc;
-    if (!lists[g].empty())
-      for (int k = 0; k < 6; ++k) tot[k] += st[k];
-    for (uint32_t q = g * (16 / G); q < (g + 1) * (16 / G); ++q) {
-      if (!len[q]) continue;
-      ++nonempty;
-      lens[q] = len[q] >= 32 ? 32 : len[q];
-      memcpy(refs + 4 * q, len[q] >= 32 ? h + 32 * q : in + 32 * q, 32);
-      if (len[q] < 32) ++inl_tops;
-    }
-  }
-  if (nonempty < 2) return -9;  // the device redoes such a build as one plain build
-  uint64_t enc[80];
-  const uint32_t L = encode_branch16(refs, lens, (uint8_t*)enc);
-  uint64_t hh[4];
-  kec256_msg<true>((const uint8_t*)enc, L, hh);
-  memcpy(root32, hh, 32);
-  if (stats_out) {
-    tot[1] += 1;                    // the root branch
-    tot[2] = tot[2] - inl_tops + 1;  // node hashes: an inline top is embedded, the root is hashed
-    tot[3] = tot[3] - inl_tops + (L / 136 + 1);
-    tot[4] += inl_tops;
-    memcpy(stats_out, tot, sizeof(tot));
-  }
-  return 0;
 }
 
 int emu_node_children(const uint8_t* v, uint64_t len, int kind, uint8_t* out32, uint8_t* kinds, uint32_t* n) {

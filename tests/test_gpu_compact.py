@@ -85,6 +85,24 @@ def test_compact_refused_with_open_savepoint(khst, oracle):
     t.close()
 
 
+def test_emit_after_delete_only_commit_and_compaction(khst, oracle):
+    """A commit that changes nothing (deletes of absent keys) leaves an empty write-back set;
+    compaction may release its buffer, and reading the set afterwards gives 0 nodes (not a
+    device error from a copy out of a released buffer)."""
+    from khipu_amd.device import Ctx, ResidentTrie
+    r = random.Random(4)
+    ks = [C._rk(r) for _ in range(400)]
+    vs = [C.account_value(r) for _ in ks]
+    t = ResidentTrie(Ctx(0), ks, vs)
+    root = t.root
+    assert t.commit([], [C._rk(r) for _ in range(3)]) == root
+    assert t.nodes() == {}
+    t.compact()
+    assert t.nodes() == {}
+    assert t.get_root() == root == _oracle(oracle, ks, vs).root_hash()
+    t.close()
+
+
 def test_compact_forest(khst, oracle):
     """A storage forest: roots of every trie, last roots and get() unchanged; a later commit
     across tries equals the oracle per trie."""

@@ -364,12 +364,11 @@ def test_hash_partition_vs_host(khst, oracle, nparts):
         assert np.array_equal(pv[:len(want)].cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("variant", ["lane", "coop"])
-def test_branch_variants_vs_oracle(khst, oracle, variant, monkeypatch):
-    """Both N1 branch kernels (KHST_BRANCH: one thread per branch, or the wave-cooperative
-    DPP assembly) give the oracle's roots on every edge case, storage tries with inline
-    children and segmented builds."""
-    monkeypatch.setenv("KHST_BRANCH", variant)
+def test_branch_levels_vs_oracle(khst, oracle):
+    """The N1 branch kernels give the oracle's roots on every edge case, storage tries with
+    inline children and segmented builds, and a 200k device build's root and permutation
+    count equal the CPU batch builder's."""
+    variant = "default"
     for name, keys, vals in C.all_cases(big=False):
         assert khst.trie_root(keys, vals) == oracle.seq_root(keys, vals), (variant, name)
     tries = C.segmented_case()
