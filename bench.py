@@ -117,9 +117,27 @@ def host_inputs(addr, vals, voff, n):
     return a, vb, vo
 
 
+def committed_seq_samples(cfg):
+    """Samples of the same sequential port beyond the default ones (scripts/seq_sample.py,
+    e.g. 10M accounts, ~10 minutes on one core): the newest committed
+    profiles/*_seq_sample_*.json per size, each root asserted against the GPU when it was taken."""
+    import glob
+    out = {}
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_seq_sample_*.json")), key=round_key):
+        try:
+            with open(f) as fh:
+                row = json.loads(fh.read().strip().splitlines()[-1])
+        except (OSError, ValueError, IndexError):
+            continue
+        if row.get("state_root_match") and f"(config {cfg})" in row.get("sample", ""):
+            out[row["accounts"]] = dict(row, source=os.path.relpath(f, ROOT))
+    return [out[k] for k in sorted(out)]
+
+
 def cpu_baseline(ctx, cfg, addr, vals, voff, samples):
     """khipu-faithful sequential trie (oracle, 1 core) on prefixes of the same synthetic
-    workload, key hashing included; unit: node-hashes/s.  Asserts GPU == CPU per sample."""
+    workload, key hashing included; unit: node-hashes/s.  Asserts GPU == CPU per sample.
+    The per-put cost fit also takes the committed larger samples (committed_seq_samples)."""
     from oracle import oracle
     rows = []
     for s in samples:
@@ -135,14 +153,26 @@ def cpu_baseline(ctx, cfg, addr, vals, voff, samples):
     a, b, res = fit_put_cost([(r["accounts"], r["seconds"]) for r in rows])
     big = rows[-1]
     est = 1e8 * (a + b * math.log(1e8, 16)) * 1e-6
-    return {"value": big["node_hashes"] / big["seconds"], "unit": "node-hashes/s", "cores": 1, "kind": "port",
-            "sample": f"first {big['accounts']} accounts of the same synthetic workload, sequential put per account "
-                      f"(MerklePatriciaTrie.scala:157-281 as driven by TrieAccounts.flush), key hashing included; "
-                      f"{big['seconds']:.2f} s; GPU root asserted equal on every sample; CPU: {cpu_model()}",
-            "samples": rows, "fit_us_per_put": {"a": round(a, 4), "b_per_log16n": round(b, 4),
-                                                "residual_us_per_put": res},
-            "state_root_s_extrapolated_100M": round(est, 1),
-            "extrapolation": "100M x (a + b log16 100M) us from the fitted samples (not run)"}
+    out = {"value": big["node_hashes"] / big["seconds"], "unit": "node-hashes/s", "cores": 1, "kind": "port",
+           "sample": f"first {big['accounts']} accounts of the same synthetic workload, sequential put per account "
+                     f"(MerklePatriciaTrie.scala:157-281 as driven by TrieAccounts.flush), key hashing included; "
+                     f"{big['seconds']:.2f} s; GPU root asserted equal on every sample; CPU: {cpu_model()}",
+           "samples": rows, "fit_us_per_put": {"a": round(a, 4), "b_per_log16n": round(b, 4),
+                                               "residual_us_per_put": res},
+           "state_root_s_extrapolated_100M": round(est, 1),
+           "extrapolation": "100M x (a + b log16 100M) us from the fitted samples (not run)"}
+    extra = [r for r in committed_seq_samples(cfg) if r["accounts"] > big["accounts"]]
+    if extra:  # the slope pinned by the larger committed samples (timed on an earlier box)
+        pts = [(r["accounts"], r["seconds"]) for r in rows] + [(r["accounts"], r["seconds"]) for r in extra]
+        a2, b2, res2 = fit_put_cost(pts)
+        est2 = 1e8 * (a2 + b2 * math.log(1e8, 16)) * 1e-6
+        out["with_committed_samples"] = {
+            "samples": [{k: r[k] for k in ("accounts", "seconds", "us_per_put", "source")} for r in extra],
+            "fit_us_per_put": {"a": round(a2, 4), "b_per_log16n": round(b2, 4), "residual_us_per_put": res2},
+            "state_root_s_extrapolated_100M": round(est2, 1),
+            "note": "the same fit with the larger committed samples (derived: their times come from the box that "
+                    "took them, named in source; this run's own samples are the ones above)"}
+    return out
 
 
 def host_path(addr, vals, voff, n, gpu_root, reps=2):

@@ -437,6 +437,7 @@ __global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb, bool ties_u) {
 // (small) upper levels by the last block to finish (the counter *done starts at zero;
 // done == nullptr: level `from` only)
 __global__ void __launch_bounds__(BS) k_pyramid(Pyr P, int from, unsigned int* done) {
+  topo_prio();
   __shared__ bool last;
   const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i < P.sz[from]) op_min64(P.lv[from - 1], P.sz[from - 1], (uint8_t*)P.lv[from], i);
@@ -455,6 +456,7 @@ __global__ void __launch_bounds__(BS) k_pyramid(Pyr P, int from, unsigned int* d
 }
 
 __global__ void __launch_bounds__(BS) k_ansv(Topo T, Pyr P, uint64_t nb) {
+  topo_prio();
   uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (b < nb) op_ansv(T, P, b);
 }
@@ -467,6 +469,7 @@ __global__ void __launch_bounds__(BS) k_ansv(Topo T, Pyr P, uint64_t nb) {
   for (uint64_t i##_b = (uint64_t)blockIdx.x * BS, i = i##_b + threadIdx.x; i##_b < (n);        \
        i##_b += (uint64_t)gridDim.x * BS, i = i##_b + threadIdx.x)
 __global__ void __launch_bounds__(BS) k_chain(Topo T, uint64_t nb) {
+  topo_prio();
   GRID_STRIDE(b, nb) op_chain(T, b);
 }
 // ANSV and chains tile by tile in LDS (trie_ops.h op_tile_ansv / op_tile_chain), the boundaries
@@ -545,10 +548,12 @@ __global__ void __launch_bounds__(TT_THREADS) k_topo_tile(Topo T, uint64_t nb, b
 }
 // the listed boundaries (grid-stride over the device's list count)
 __global__ void __launch_bounds__(BS) k_ansv_list(Topo T, Pyr P, const uint32_t* list, const unsigned long long* cnt) {
+  topo_prio();
   const uint64_t n = *cnt;
   for (uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BS) op_ansv(T, P, list[i]);
 }
 __global__ void __launch_bounds__(BS) k_chain_list(Topo T, const uint32_t* list, const unsigned long long* cnt) {
+  topo_prio();
   const uint64_t n = *cnt;
   for (uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BS) op_chain(T, list[i]);
 }
@@ -584,6 +589,7 @@ __device__ __forceinline__ void block_add3(unsigned long long* c0, unsigned long
 }
 
 __global__ void __launch_bounds__(BS) k_branch_topo(Topo T, Pyr P, uint64_t nb) {
+  topo_prio();
   unsigned long long ext = 0;
   GRID_STRIDE(b, nb) {
     op_branch_topo(T, P, nb, b);
@@ -614,6 +620,7 @@ __device__ __forceinline__ uint32_t branch_bucket(const Topo& T, uint64_t j) {
 }
 constexpr uint32_t LV_TILE = BS * 16;  // branch ids per block: few blocks -> a short [bucket][block] table
 __global__ void __launch_bounds__(BS) k_level_count(Topo T, const uint32_t* Bp, uint32_t* bcnt, uint32_t nblk) {
+  topo_prio();
   __shared__ uint32_t h[NBUCKET];
   for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) h[q] = 0;
   __syncthreads();
@@ -628,6 +635,7 @@ __global__ void __launch_bounds__(BS) k_level_count(Topo T, const uint32_t* Bp, 
 // so a level reads its branches' fields, child records and message slots contiguously
 __global__ void __launch_bounds__(BS) k_level_scatter(Topo T, const uint32_t* Bp, const uint32_t* bbase,
                                                       uint32_t nblk, uint32_t* pos) {
+  topo_prio();
   __shared__ uint32_t base[NBUCKET];
   for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) base[q] = bbase[(uint64_t)q * nblk + blockIdx.x];
   __syncthreads();
@@ -642,6 +650,7 @@ struct BrTab {
   uint8_t *depth, *ext, *pord;
 };
 __global__ void __launch_bounds__(BS) k_branch_permute(Topo T, BrTab J, const uint32_t* pos, const uint32_t* Bp) {
+  topo_prio();
   const uint64_t B = *Bp;
   GRID_STRIDE(j, B) {
     const uint32_t g = pos[j], p = J.parent[j];
@@ -656,11 +665,13 @@ __global__ void __launch_bounds__(BS) k_branch_permute(Topo T, BrTab J, const ui
 }
 // group reps carry level-order branch ids from here on (leaf parents, resident tables)
 __global__ void __launch_bounds__(BS) k_bid_remap(Topo T, const uint32_t* pos, uint64_t nb) {
+  topo_prio();
   GRID_STRIDE(b, nb) if (T.u[b] != 0 && T.rep[b] == (uint32_t)b) T.isrep_bid[b] = pos[T.isrep_bid[b]];
 }
 
 // level bounds: lb[d] = first position of depth d in `order`, lb[64] = B
 __global__ void k_level_bounds(const uint32_t* bbase, uint32_t nblk, const uint32_t* Bp, uint32_t* lb) {
+  topo_prio();
   uint32_t d = threadIdx.x;
   if (d < 64) lb[d] = bbase[(uint64_t)d * 8 * nblk];
   if (d == 0) lb[64] = *Bp;
@@ -824,19 +835,25 @@ __device__ __forceinline__ void wave_count(unsigned long long* dst, bool f) {
   const uint64_t b = __ballot(f);
   if (b && __lane_id() == 0) atomicAdd(dst, (unsigned long long)__popcll(b));
 }
-// Early leaves (plain root builds; trie_ops.h op_leaf_in3): one thread per INPUT, on the
+// Early leaves (plain root builds; trie_ops.h op_leaf_core): one thread per INPUT, on the
 // second stream beside the branch topology.  Keys and packed values are read in input
 // order; the parent depth gives the header geometry, the key and value are then loaded at
 // their message shifts, and the message is assembled dword by dword (v_perm_b32) straight
 // into the Keccak state.  Every lane of a wave runs the wave-bound reductions, so threads
 // past n take part with neutral values.
-// 69 VGPRs, 7 waves per SIMD, with its permutation straight-line (keccakf<KECCAK_FULL>: no
-// pi-renaming moves at loop back-edges; 78 VGPRs and 6 waves with the 3-iteration loop, 0.9 ms
-// slower in the step, profiles/r4bp_keccak_unroll_ab_100m.json).  Forced to 7 waves by the
-// register limit instead (72 VGPRs, no spills) it had run 1.0 ms slower
-// (profiles/r3l_occupancy_ab_100m.json).
+// A block takes LEAF_ITEMS runs of BS consecutive inputs, one after the other: the next run's
+// scatter record and span offsets (the first of the two dependent load rounds) are brought
+// into LDS by LDS-DMA while the current input is assembled and permuted (no registers held
+// across the permutation), and the counters are added once per wave (42.6 -> 41.9 ms in the
+// step against one input per thread, profiles/r5g_leaf_prefetch_ab_100m.json).  Blocks that
+// live for a few runs only keep the wave slots turning over for the topology kernels beside
+// them (a persistent grid starved them: the topology stream 15 -> 22 ms, the step 42.5 -> 45
+// ms, profiles/r5e_leaf_grid_ab_100m.json; forcing 7 waves per SIMD spilled and cost 1.4 ms).
+// The permutation is straight-line (keccakf<KECCAK_FULL>: no pi-renaming moves at loop
+// back-edges; 78 VGPRs and 6 waves with the 3-iteration loop, 0.9 ms slower in the step,
+// profiles/r4bp_keccak_unroll_ab_100m.json).
+constexpr uint32_t LEAF_ITEMS = 4;
 __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
-  const uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
   auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {
     WaveBounds b;
     b.emax = wave_max_u32(use ? e : 0u);
@@ -845,12 +862,52 @@ __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
     b.Lmin = 255u - wave_max_u32(use ? 255u - llo : 0u);
     return b;
   };
-  uint32_t inl = 0, lb = 0;
-  const uint32_t perms = op_leaf_in3(T, j, n, wave, &inl, &lb);
-  wave_count(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms != 0);
-  wave_count(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), perms != 0);
-  wave_count(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl != 0);
-  if (lb) atomicAdd(&T.ctr[CTR_LONGB], (unsigned long long)lb);
+  const uint64_t j0 = (uint64_t)blockIdx.x * LEAF_ITEMS * BS + threadIdx.x, jend = j0 + LEAF_ITEMS * BS;
+  // double-buffered per wave: [slot][wave][pv low / pv high dwords (2 x 64), voff[j], voff[j+1] (64 pairs)]
+  __shared__ uint32_t pbuf[2][BS / 64][64 * 6];
+  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  auto issue = [&](uint32_t slot, uint64_t j) {  // (every lane of the wave: j past n reads a clamped input)
+    typedef __attribute__((address_space(1))) void gv;
+    typedef __attribute__((address_space(3))) void lv;
+    const uint64_t jj = j < n ? j : n - 1;
+    uint32_t* b = pbuf[slot][w];
+    __builtin_amdgcn_global_load_lds((gv*)(T.pdinv + jj), (lv*)b, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((gv*)((const uint32_t*)(T.pdinv + jj) + 1), (lv*)(b + 64), 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((gv*)(T.voff + jj), (lv*)(b + 128), 16, 0, 0);
+  };
+  auto take = [&](uint32_t slot, uint64_t j, uint64_t& pv, uint64_t& off, uint64_t& end) {
+    __builtin_amdgcn_s_waitcnt(0);  // (vmcnt: the slot's LDS-DMA has landed)
+    asm volatile("" ::: "memory");
+    const uint32_t* b = pbuf[slot][w];
+    pv = j < n ? ((uint64_t)b[64 + l] << 32) | b[l] : PDINV_SKIP;
+    off = ((const uint64_t*)(b + 128))[2 * l];
+    end = ((const uint64_t*)(b + 128))[2 * l + 1];
+  };
+  const uintptr_t vend = (uintptr_t)T.vals + T.voff[n];  // (once: see op_leaf_core)
+  uint64_t pv = 0, off = 0, end = 0;
+  issue(0, j0);
+  uint32_t perms = 0, inl = 0, slot = 0;
+#pragma unroll 1
+  for (uint64_t j = j0; j < jend && j - threadIdx.x % 64 < n; j += BS) {  // (wave-uniform: the wave's first input)
+    const uint64_t jn = j + BS < jend ? j + BS : n;
+    take(slot, j, pv, off, end);
+    if (jn - threadIdx.x % 64 < n) issue(slot ^ 1, jn);
+    slot ^= 1;
+    const bool live = pv != PDINV_SKIP;  // not an earlier put of a key put again later
+    uint32_t in1 = 0, lb = 0;
+    perms += op_leaf_core(T, live, (int32_t)(int8_t)(uint8_t)(pv >> 32), (uint32_t)pv, j, n, off,
+                          (uint32_t)(end - off), vend, wave, &in1, &lb);
+    inl += in1;
+    if (lb) atomicAdd(&T.ctr[CTR_LONGB], (unsigned long long)lb);
+  }
+  const unsigned long long sp = wave_sum((unsigned long long)perms), si = wave_sum((unsigned long long)inl);
+  if ((threadIdx.x & 63) == 0) {
+    if (sp) {
+      atomicAdd(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), sp);
+      atomicAdd(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), sp);
+    }
+    if (si) atomicAdd(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), si);
+  }
 }
 // the same publish split in two (trie_ops.h op_leaf_link / op_leaf_move)
 __global__ void __launch_bounds__(BS) k_leaf_link(Topo T) {
@@ -2258,7 +2315,11 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     }
     if (A.vals_ready) HIPCHK(hipStreamWaitEvent(s2, A.vals_ready, 0));  // the topology need not wait
     HIPCHK(hipEventRecord(c->ev[9], s2));
-    hipLaunchKernelGGL(k_leaf_in, GRID(n, BS), dim3(BS), 0, s2, T, n);
+    {
+      const uint64_t runs = (n + BS - 1) / BS;
+      const uint64_t g = (runs + LEAF_ITEMS - 1) / LEAF_ITEMS;
+      hipLaunchKernelGGL(k_leaf_in, dim3((unsigned)std::max<uint64_t>(g, 1)), dim3(BS), 0, s2, T, n);
+    }
     LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[10], s2));
   };

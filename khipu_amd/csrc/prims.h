@@ -15,6 +15,12 @@ namespace khst {
 
 constexpr int WAVE = 64;
 
+// Issue priority of the latency-bound topology kernels that run beside the VALU-bound leaf
+// kernel (scans, pyramid, list kernels, branch records, level order): s_setprio raises their
+// waves over the leaf waves in the SIMD's issue arbitration (priority, then age), so a long-
+// lived leaf wave does not win every issue slot from a younger topology wave.
+__device__ __forceinline__ void topo_prio() { __builtin_amdgcn_s_setprio(2); }
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
   uint32_t lane = __lane_id();
   return lane == 0 ? 0ULL : (~0ULL >> (64 - lane));
@@ -80,6 +86,7 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* lds_waves, T* total) {
 template <typename T>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const T* in, T* out, uint64_t n, T* tile_sums,
                                                              T* last_in) {
+  topo_prio();
   __shared__ T lw[SCAN_THREADS / 64];
   uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
   T v[SCAN_ITEMS];
@@ -102,6 +109,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const T* in, T* out
 
 template <typename T>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_add(T* out, uint64_t n, const T* tile_off) {
+  topo_prio();
   uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
   T add = tile_off[blockIdx.x];
   for (int i = threadIdx.x; i < SCAN_TILE; i += SCAN_THREADS)
@@ -110,6 +118,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_add(T* out, uint64_t n, c
 
 template <typename T>
 __global__ void k_scan_total(const T* in_last, const T* out_last, T* total) {
+  topo_prio();
   *total = *in_last + *out_last;
 }
 
@@ -188,6 +197,7 @@ __device__ __forceinline__ void scan_small_block(const T* in, T* out, uint64_t n
 }
 template <typename T>
 __global__ void __launch_bounds__(SCAN_SMALL_THREADS) k_scan_small(const T* in, T* out, uint64_t n, T* total) {
+  topo_prio();
   scan_small_block<T>(in, out, n, total);
 }
 // Up to three small scans of n elements in one launch, one block each (a commit's per-op
@@ -199,6 +209,7 @@ struct ScanJob {
   bool wide;  // uint64_t elements (else uint32_t)
 };
 __global__ void __launch_bounds__(SCAN_SMALL_THREADS) k_scan_small3(ScanJob a, ScanJob b, ScanJob c, uint64_t n) {
+  topo_prio();
   const ScanJob& j = blockIdx.x == 0 ? a : blockIdx.x == 1 ? b : c;
   if (!j.in) return;
   if (j.wide)
@@ -214,6 +225,7 @@ constexpr uint64_t SCAN_TWO_MAX_TILES = 2048;
 template <typename T>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_add_sums(T* out, uint64_t n, const T* sums, uint32_t tiles,
                                                                 T* total) {
+  topo_prio();
   __shared__ T lw[SCAN_THREADS / 64];
   const uint32_t b = blockIdx.x;
   T s = 0;

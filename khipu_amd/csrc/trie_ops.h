@@ -1053,16 +1053,20 @@ constexpr uint32_t LEAF_KD = 12;  // key dwords (message dwords 0..9 + funnel)
 KH_HD uint32_t rlp_hdr_len32(uint32_t x) {  // rlp_hdr_len of a 32-bit length
   return x < 56 ? 1u : x < 0x100u ? 2u : x < 0x10000u ? 3u : x < 0x1000000u ? 4u : 5u;
 }
-// One leaf: input j (key kin[j], value voff[j]..voff[j+1]) with parent depth pd, stashed at
-// sorted position si.  live = false: a lane that only takes part in the wave reductions.
+// One leaf: input j (key kin[j], value vals[off .. off + vlen) = voff[j]..voff[j+1]) with
+// parent depth pd, stashed at sorted position si.  live = false: a lane that only takes part
+// in the wave reductions.  vend: the end of the value buffer, vals + voff[n] (the caller reads
+// it once: a load inside the kernel's loop would be one more dependent round trip per input).
 template <typename WAVE>
-KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, uint64_t j, uint64_t n, WAVE wave,
-                            uint32_t* inl, uint32_t* longb) {
+KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, uint64_t j, uint64_t n, uint64_t off,
+                            uint32_t vlen, uintptr_t vend, WAVE wave, uint32_t* inl, uint32_t* longb) {
   *inl = 0;
   *longb = 0;
-  const uint64_t off = live ? T.voff[j] : 0;
-  const uint32_t vlen = live ? (uint32_t)(T.voff[j + 1] - off) : 0;
-  if (!live) pd = 0;
+  if (!live) {
+    pd = 0;
+    off = 0;
+    vlen = 0;
+  }
   // geometry (leaf_geom / leaf_header), 32-bit.  A 1-byte value < 0x80 is its own encoding
   // (no prefix): that only shortens L by one and never changes the list-prefix length
   // (the payload stays < 56), so everything up to P is known before the value is read.
@@ -1105,7 +1109,7 @@ KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, u
   const uintptr_t VBa = VB & ~(uintptr_t)3;
   {
     const uintptr_t lo4 = (uintptr_t)T.vals & ~(uintptr_t)3;
-    const uintptr_t hi4 = ((uintptr_t)T.vals + T.voff[n] + 3) & ~(uintptr_t)3;
+    const uintptr_t hi4 = (vend + 3) & ~(uintptr_t)3;
     if (VBa < lo4 || VBa + 4 * LEAF_VD > hi4) {  // the window leaves the value buffer: dword by dword
 #pragma unroll
       for (uint32_t i = 0; i < LEAF_VD; ++i) {
@@ -1195,15 +1199,21 @@ KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, u
   // a top leaf is >= 35 B, so its stash is always the hash; the preset 32 stands for every
   // hashed leaf (one scattered byte write less per leaf)
   if (L < 32) T.lf_emeta[si] = (uint8_t)L;
-  if (top && T.lpos) publish_ref(T, NONE, 0, 0, si, r, 32, r);  // leaf positions: no post-join pass
+  // leaf positions: a top leaf (a trie or subtrie of one key) is published after the join by
+  // k_leaf_fix, with the long leaves (op_leaf_topo_early publishes a top leaf's stash)
+  if (top && T.longlist) T.longlist[ctr_add(&T.ctr[CTR_LONGN], 1)] = si;
   return perms;
 }
-// input order (k_leaf_in): the parent depth and sorted position scattered by k_ansv_pd
+// input order (the emulator's replay of k_leaf_in, which prefetches pdinv/voff itself): the
+// parent depth and sorted position scattered by k_ansv_pd
 template <typename WAVE>
 KH_HD uint32_t op_leaf_in3(const Topo& T, uint64_t j, uint64_t n, WAVE wave, uint32_t* inl, uint32_t* longb) {
   const uint64_t pv = j < n ? T.pdinv[j] : PDINV_SKIP;
   const bool live = pv != PDINV_SKIP;  // not an earlier put of a key put again later
-  return op_leaf_core(T, live, (int32_t)(int8_t)(uint8_t)(pv >> 32), (uint32_t)pv, j, n, wave, inl, longb);
+  const uint64_t off = live ? T.voff[j] : 0;
+  const uint32_t vlen = live ? (uint32_t)(T.voff[j + 1] - off) : 0;
+  return op_leaf_core(T, live, (int32_t)(int8_t)(uint8_t)(pv >> 32), (uint32_t)pv, j, n, off, vlen,
+                      (uintptr_t)T.vals + T.voff[n], wave, inl, longb);
 }
 // value span of sorted leaf i (early builds gather no spans: through the input index)
 KH_HD void leaf_span_early(const Topo& T, uint64_t i, uint64_t* off, uint32_t* len) {
