@@ -178,13 +178,18 @@ __global__ void __launch_bounds__(BS) k_sseg_from_ck(const uint32_t* sck, uint64
 }
 
 // composite sort key: segment id in the top sb bits, then the key's leading bits (big-endian)
+// (flags, nullable: |= 4 when a segment id needs more than sb bits -- a forest commit's sb is
+// a hint from the trie ids seen before; the sort is then redone with 32)
 __global__ void __launch_bounds__(BS) k_make_ck(const uint64_t* K, const uint32_t* seg, uint32_t sb, uint64_t n,
-                                                uint64_t* ck, uint32_t* idx) {
+                                                uint64_t* ck, uint32_t* idx, unsigned long long* flags) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
   uint64_t be = bswap64(K[4 * i]);
   uint64_t c = be;
-  if (sb) c = ((uint64_t)seg[i] << (64 - sb)) | (be >> sb);
+  if (sb) {
+    if (flags && sb < 32 && (seg[i] >> sb)) atomicOr(flags, 4ULL);
+    c = ((uint64_t)seg[i] << (64 - sb)) | (be >> sb);
+  }
   ck[i] = c;
   idx[i] = (uint32_t)i;
 }
@@ -192,8 +197,9 @@ __global__ void __launch_bounds__(BS) k_make_ck(const uint64_t* K, const uint32_
 // Runs of equal 32-bit sort prefixes (same segment, equal leading key bits) are
 // put in full-key order by the thread at the run's start: an insertion sort of
 // (key, index, segment) in place, stable, so among equal keys the input order
-// (later put last) is kept.  flags |= 2 if equal keys exist (dedup needed),
-// |= 1 if a run exceeds TIE_RUN_MAX (take the full-sort path instead).
+// (later put last) is kept.  flags |= 2 if equal keys exist (dedup needed; flags[-1]
+// (CTR_NDUP) counts the keys dropped), |= 1 if a run exceeds TIE_RUN_MAX (take the
+// full-sort path instead).
 constexpr uint32_t TIE_RUN_MAX = 64;
 // variable-length keys (zero padded, kn nibbles): a key sorts before the longer keys it
 // prefixes, i.e. (padded key, length) order
@@ -233,13 +239,18 @@ __global__ void __launch_bounds__(BS) k_tie_fix(const uint64_t* ck, uint64_t n, 
     sidx[b] = ix;
     if (sseg) sseg[b] = sg;
   }
-  bool dup = false;
+  unsigned long long ndup = 0;
   for (uint64_t a = i + 1; a < e; ++a) {
     const uint64_t* x = skey + 4 * (a - 1);
     const uint64_t* y = skey + 4 * a;
-    dup |= x[0] == y[0] && x[1] == y[1] && x[2] == y[2] && x[3] == y[3] && (!kn || kn[sidx[a - 1]] == kn[sidx[a]]);
+    ndup += (x[0] == y[0] && x[1] == y[1] && x[2] == y[2] && x[3] == y[3] && (!kn || kn[sidx[a - 1]] == kn[sidx[a]]))
+                ? 1
+                : 0;
   }
-  if (dup) atomicOr(flags, 2ULL);
+  if (ndup) {
+    atomicOr(flags, 2ULL);
+    atomicAdd(flags - 1, ndup);
+  }
 }
 
 // Unsegmented plain builds sort (leading 32 key bits, index) pairs only; runs of equal
@@ -611,7 +622,11 @@ __global__ void __launch_bounds__(BS) k_leaf_topo(Topo T) {
 // grouped: the waves of a level run the same number of permutations.  Per-block
 // bucket counts are laid out [bucket][block]; one exclusive scan gives every
 // (bucket, block) its base; a second pass ranks inside the block with LDS atomics.
-constexpr uint32_t NBUCKET = 64 * 8;
+// (Bucketed by the exact child count instead -- waves with uniform child loops -- the
+// children ranges of neighbouring branches are no longer adjacent: depth 6 5.06 -> 5.32 ms,
+// 11.8 -> 14.5 GB read, profiles/r5m_level_order_ab_100m.json.)
+constexpr uint32_t LV_PER_DEPTH = 8;
+constexpr uint32_t NBUCKET = 64 * LV_PER_DEPTH;
 __device__ __forceinline__ uint32_t branch_bucket(const Topo& T, uint64_t j) {
   uint32_t k = T.br_k[j];
   uint32_t payload = 32 * k + 17;
@@ -673,7 +688,7 @@ __global__ void __launch_bounds__(BS) k_bid_remap(Topo T, const uint32_t* pos, u
 __global__ void k_level_bounds(const uint32_t* bbase, uint32_t nblk, const uint32_t* Bp, uint32_t* lb) {
   topo_prio();
   uint32_t d = threadIdx.x;
-  if (d < 64) lb[d] = bbase[(uint64_t)d * 8 * nblk];
+  if (d < 64) lb[d] = bbase[(uint64_t)d * LV_PER_DEPTH * nblk];
   if (d == 0) lb[64] = *Bp;
 }
 
@@ -819,16 +834,6 @@ __global__ void __launch_bounds__(BS) k_leaf_hash_list(Topo T, const uint32_t* l
 __global__ void __launch_bounds__(BS) k_pd_scatter(Topo T) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i < T.m) op_pd_scatter(T, i);
-}
-// max over the wave's 64 lanes (DPP row shifts + row broadcasts), returned to every lane
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true));  // row_shr:1
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true));  // row_shr:2
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true));  // row_shr:4
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true));  // row_shr:8
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 // per-wave counter add: the lanes' flags counted by ballot, one atomic per wave
 __device__ __forceinline__ void wave_count(unsigned long long* dst, bool f) {
@@ -1715,6 +1720,7 @@ struct kh_ctx {
   DevBuf ws_list;  // element builds: the list of leaves to hash (k_leaf_prep -> k_leaf_hash_list)
   DevBuf ws_inject;                    // kh_block_commit: the injection's error word
   unsigned long long inject_tok = 0;   //   and the token the last call writes there on error
+  DevBuf ws_arena;  // the build's long leaves (sized once the leaves are hashed)
   DevBuf ws1, ws2, ws3, in_keys, in_vals, in_voff, in_seg, in_kn, in_aux, in_block, out_emit, emit_dev;
   hipEvent_t ev[11] = {};  // [0..5] build stages (st), [6] / [7] forest commit marks, [8] boundaries
                           // ready (st), [9] / [10] leaf kernel start / end (st2)
@@ -1758,7 +1764,7 @@ struct BuildArgs {
   bool dev_results = false;        // results and counters stay on the device (no host sync at the end)
   bool no_spec = false;            // no speculative sort (SortIO::speculate): the retry of one that failed
   std::function<void()> before_leaves;  // element builds: called (host) right before the leaves are encoded
-  std::function<bool()> late_ready;     // ... late values (ElemArgs::late) already on their way: one leaf pass
+  std::function<bool()> late_ready;     // ... late values (ElemArgs::late) already on the device: one leaf pass
 };
 // element build (forest.h): inputs are leaves and subtree elements; the capped reference
 // of every element node, branch and extension is kept for the forest's records
@@ -1922,28 +1928,43 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
       S.ties_u = S.u && m == n;  // no dedup: the run boundaries' values stand
       return;
     }
-  } else {
+  }
+  uint64_t tie_flags = 1;  // long_run: straight to the full sort
+  uint64_t ndup = 0;
+  // the 64-bit composite prefixes sorted on their top 32 bits, the keys gathered and the runs
+  // of equal prefixes put in order; one sync for the flags (and the caller's check word)
+  uint32_t sbu = sb;  // (a forest's hint; 32 if it was short)
+  auto sort_prefix = [&] {
     if (!S.ck_ready) {
-      hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, sb, n, ck0, idx0);
+      hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, sbu, n, ck0, idx0,
+                         T.ctr + CTR_TIE);
       LAUNCH_CHECK();
     }
     bool flip = radix_sort_pairs<uint64_t>(ck0, idx0, ck1, idx1, n, 32, 64, rs_scratch, st);
     cks = flip ? ck1 : ck0;
     idxs = flip ? idx1 : idx0;
     LAUNCH_CHECK();
-  }
-  uint64_t tie_flags = 1;  // long_run: straight to the full sort
-  if (!long_run) {
     hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, (const uint32_t*)idxs, n,
                        skey, sseg);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_tie_fix, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, n, skey, idxs, sseg, S.kn,
                        T.ctr + CTR_TIE);
     LAUNCH_CHECK();
-    HIPCHK(hipMemcpyAsync(c->h_pinned, T.ctr + CTR_TIE, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_pinned + 2, T.ctr + CTR_NDUP, 16, hipMemcpyDeviceToHost, st));  // [2] dups, [3] flags
     if (S.chk) HIPCHK(hipMemcpyAsync(c->h_pinned + 1, S.chk, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    tie_flags = c->h_pinned[0];
+    tie_flags = c->h_pinned[3];
+    ndup = c->h_pinned[2];
+  };
+  if (!S.ck_path) {
+    sort_prefix();
+    if (tie_flags & 4) {  // a trie id past the hinted bits: again with 32
+      if (S.ck_ready) throw KhError{KH_EINTERNAL, "sort: segment bits on prepared prefixes"};
+      HIPCHK(hipMemsetAsync(T.ctr + CTR_NDUP, 0, 16, st));
+      sbu = 32;
+      S.sb = 32;
+      sort_prefix();
+    }
   }
   const bool fallback = tie_flags & 1, dups = tie_flags & 2;
   uint64_t m = n;
@@ -1954,7 +1975,8 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
     uint32_t* ib = idx1;
     uint64_t* ka = ck0;
     uint64_t* kb = ck1;
-    hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, 0u, n, ka, ia);
+    hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, 0u, n, ka, ia,
+                       (unsigned long long*)nullptr);
     LAUNCH_CHECK();
     auto pass = [&](int word, int bits) {
       if (word >= 0)
@@ -1972,24 +1994,31 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
     };
     if (S.kn) pass(-2, 8);  // least significant: the length
     for (int w = 3; w >= 0; --w) pass(w, 64);
-    if (segmented) pass(-1, ((sb + 7) / 8) * 8);
+    if (segmented) pass(-1, ((sbu + 7) / 8) * 8);
     hipLaunchKernelGGL(k_gather, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, (const uint32_t*)ia, n,
                        skey, sseg);
     LAUNCH_CHECK();
     sidx = ia;
   }
   if (fallback || dups) {
-    // keep the LAST of equal keys (later puts win): flags, scan, compaction
+    // keep the LAST of equal keys (later puts win): flags, scan, compaction.  Without the
+    // full sort the count of dropped keys came with the tie flags: no sync of its own, and the
+    // scan in multi-block form (a 1024-thread block waited ~90 us for a CU beside a block
+    // commit's other phase, profiles/r5m_block_commit_timeline_50m.json)
     uint32_t* keep = (uint32_t*)(sidx == idx0 ? ck1 : ck0);  // n*8 free bytes
     uint32_t* keep_pos = sidx == idx0 ? idx1 : idx0;
     hipLaunchKernelGGL(k_dup, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)skey, (const uint32_t*)sseg,
                        (const uint32_t*)sidx, S.kn, n, keep);
     LAUNCH_CHECK();
     uint32_t* mtot = (uint32_t*)(T.ctr + CTR_M);
-    scan_exclusive<uint32_t>(keep, keep_pos, n, mtot, scan_scratch, st);
-    HIPCHK(hipMemcpyAsync(c->h_pinned, mtot, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    m = (uint32_t)c->h_pinned[0];
+    scan_exclusive<uint32_t>(keep, keep_pos, n, mtot, scan_scratch, st, fallback);
+    if (fallback) {
+      HIPCHK(hipMemcpyAsync(c->h_pinned, mtot, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      m = (uint32_t)c->h_pinned[0];
+    } else {
+      m = n - ndup;
+    }
     if (m < n) {
       c->ws3.ensure(carve_size({n * 32, n * 4, n * 4}));
       Carver c3{(char*)c->ws3.p, 0, c->ws3.cap};
@@ -2071,7 +2100,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
       n * 4, n, n, n * 8, n * 4, n * 8, n * 4,  // leaves, svoff, svlen
       A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
       nres * 32, nres * 4, nres * 32,         // results
-      CTR_N * CTR_SHARDS * 8, 64 * 4, 80 * 4, 512 * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
+      CTR_N * CTR_SHARDS * 8, 64 * 4, 80 * 4, NBUCKET * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
       early ? n * 32 : 0, early ? n : 0, early ? n * 8 : 0,  // early leaves: stashed references, meta, pd|position
       early && !lpos ? n * 8 : 0,                                 // link slots (segmented early builds)
       A.kn ? n : 0,                           // sorted key lengths
@@ -2415,14 +2444,15 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     LAUNCH_CHECK();
   }
   if (early) {
-    HIPCHK(hipEventRecord(c->ev[3], st));      // topology done (the leaves may still run)
-    HIPCHK(hipStreamWaitEvent(st, c->ev[10], 0));  // ... and the leaves: their long-leaf bytes
+    HIPCHK(hipEventRecord(c->ev[3], st));  // topology done (the leaves may still run)
   } else {
     hipLaunchKernelGGL(k_leaf_topo, GRID(m, BS), dim3(BS), 0, st, T);
     LAUNCH_CHECK();
   }
   // one host sync for every size the second workspace needs: the counters, the depth
-  // histogram and the level bounds are carved back to back, one copy
+  // histogram and the level bounds are carved back to back, one copy.  Early builds take it
+  // while the leaf kernel still runs (the child records are carved and cleared beside it) and
+  // read the leaves' own counters (long and inline leaves) with a second, short one
   const size_t tcopy = (size_t)((char*)(lb + 65) - (char*)ctr);
   if (tcopy > 16384) throw KhError{KH_EINTERNAL, "counter block exceeds the pinned staging"};
   HIPCHK(hipMemcpyAsync(c->h_pinned, ctr, tcopy, hipMemcpyDeviceToHost, st));
@@ -2434,18 +2464,11 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     throw SpecRetry{};
   }
   const uint64_t B = (uint32_t)hc[CTR_B];
-  const uint64_t lf_bytes = early ? hc[CTR_LONGB] : hc[CTR_B + 2];
   const uint64_t C = (uint32_t)hc[CTR_B + 3];
   if (hc[CTR_ERR]) throw KhError{KH_EINTERNAL, "topology invariant violated (group chain > 15)"};
   std::vector<uint32_t> lbh(65, 0);
   memcpy(lbh.data(), (const char*)hc + ((char*)lb - (char*)ctr), 65 * 4);
   if (nb == 0) std::fill(lbh.begin(), lbh.end(), 0u);
-  const uint64_t nlong = lpos ? hc[CTR_LONGN] : 0;
-  if (lpos) {  // every leaf is hashed by now: is any of them inline?
-    unsigned long long ninl = 0;
-    for (int sh = 0; sh < CTR_SHARDS; ++sh) ninl += hc[sh * CTR_N + CTR_INLINE];
-    T.lf_inline = ninl ? 1 : 0;
-  }
 
   // ---- phase-2 workspace: child records + node arena
   // leaf encodings are kept (transposed message slots) for the write-back, element and
@@ -2453,20 +2476,32 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   const bool lmsgs = A.emit || A.kn || A.el;
   const uint64_t lmsg_words = lmsgs ? (uint64_t)LEAF_WORDS * m : 0;
   const uint64_t bmsg_words = A.emit ? (uint64_t)BR_WORDS * B : 0, xmsg_words = A.emit ? (uint64_t)EXT_WORDS * B : 0;
-  c->ws2.ensure(carve_size({C * 32, C * 2, lmsg_words * 8, lf_bytes + 64, bmsg_words * 8, xmsg_words * 8,
-                            lpos ? C * 4 : 0}));
+  c->ws2.ensure(carve_size({C * 32, C * 2, lmsg_words * 8, bmsg_words * 8, xmsg_words * 8, lpos ? C * 4 : 0}));
   Carver cv2{(char*)c->ws2.p, 0, c->ws2.cap};
   T.cref = cv2.take<uint64_t>(C * 4);
   T.cmeta = cv2.take<uint16_t>(C);
   T.lmsg = lmsgs ? cv2.take<uint64_t>(lmsg_words) : nullptr;
   T.lstride = m;
-  T.arena = cv2.take<uint8_t>(lf_bytes + 64);  // long leaves
-  T.bmsg = A.emit ? cv2.take<uint64_t>(bmsg_words) : nullptr;
-  T.xmsg = A.emit ? cv2.take<uint64_t>(xmsg_words) : nullptr;
   if (lpos) {  // a record without CM_BR is a leaf child's: the metas start at zero
     T.cend = cv2.take<uint32_t>(C);
     HIPCHK(hipMemsetAsync(T.cmeta, 0, C * 2, st));
   }
+  if (early) {  // the leaves' counters: their long-leaf bytes, long and inline leaves
+    HIPCHK(hipStreamWaitEvent(st, c->ev[10], 0));
+    HIPCHK(hipMemcpyAsync(c->h_pinned, ctr, (size_t)CTR_N * CTR_SHARDS * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  const uint64_t lf_bytes = early ? hc[CTR_LONGB] : hc[CTR_B + 2];
+  const uint64_t nlong = lpos ? hc[CTR_LONGN] : 0;
+  if (lpos) {  // every leaf is hashed by now: is any of them inline?
+    unsigned long long ninl = 0;
+    for (int sh = 0; sh < CTR_SHARDS; ++sh) ninl += hc[sh * CTR_N + CTR_INLINE];
+    T.lf_inline = ninl ? 1 : 0;
+  }
+  c->ws_arena.ensure(lf_bytes + 64);
+  T.arena = (uint8_t*)c->ws_arena.p;  // long leaves
+  T.bmsg = A.emit ? cv2.take<uint64_t>(bmsg_words) : nullptr;
+  T.xmsg = A.emit ? cv2.take<uint64_t>(xmsg_words) : nullptr;
   T.lb = lb;
   if (A.el) {  // element build: every capped reference kept for the forest's records
     ElemArgs& E = *A.el;
@@ -2503,7 +2538,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     unsigned long long* nlist = A.el ? T.ctr + CTR_LIST : nullptr;
     uint32_t* list = nullptr;
     // late values still to come: the other leaves first, the late ones after them (when they are
-    // on their way already, one pass: a second costs ~60 us of latency)
+    // on the device already, one pass: a second costs ~60 us of latency)
     const bool split = A.el && T.el_late && !(A.late_ready && A.late_ready());
     if (A.el) {
       c->ws_list.ensure(carve_size({m * 4, split ? m * 4 : 0}));
@@ -3331,6 +3366,7 @@ struct kh_trie {
   kh_ctx* home = nullptr;  // the context it was opened on: every call on the handle holds home->mu
   uint32_t flags = 0;  // KH_HASH_KEYS: the trie's key encoder; KH_EMIT_NODES: keep each commit's write-back set
   bool forest = false;
+  uint32_t tid_bits = 0;  // forests: bits of the trie ids committed so far (+ headroom; 0: none yet)
   DevBuf recs, touched, replaced;  // node records (forest.h Recs: 128 B each), per-commit flags
   uint64_t rcap = 0, rn = 0, rdead = 0;
   DevBuf mslots;  // anchor map: 16-byte (tag, record) slots
@@ -3644,7 +3680,7 @@ struct FCommit {  // one commit's inputs (device buffers)
   // index; kh_block_commit: those naming a storage trie); the rest are copied and their leaves
   // encoded and hashed before before_values (nullable: every value waits)
   const uint32_t* late = nullptr;
-  std::function<bool()> late_ready;  // (host) the producer has enqueued the late values already
+  std::function<bool()> late_ready;  // (host) the late values are already on the device
   // the new roots are on the device (d_tries / d_roots, right after the element build; the
   // records and the anchor map still follow): kh_block_commit's storage phase injects them
   // into the account bodies here, so the account phase need not wait for the rest
@@ -3725,7 +3761,10 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   uint32_t* sseg = cv.take<uint32_t>(nops);
   S.sseg = segd ? sseg : nullptr;
   S.seg = segd ? Tid : nullptr;
-  S.sb = segd ? 32 : 0;
+  // the trie ids' bits: a hint from the ids committed before (two bits of headroom; the sort is
+  // redone with 32 if an id needs more), so the sorted 32-bit prefix holds key bits too and
+  // runs of equal prefixes (one per trie with all 32) stay short
+  S.sb = segd ? (h->tid_bits ? std::max(h->tid_bits, 1u) : 32u) : 0;
   S.rs_scratch = cv.take<char>(radix_scratch_bytes(nops));
   S.scan_scratch = cv.take<char>(scan_scratch_bytes(nops + 1, 8));
   S.ctr = cv.take<unsigned long long>(CTR_N);
@@ -4121,6 +4160,8 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   if (!lazy && count_fresh) h->mused += ht[6];
   memcpy(h->tries.data(), hs, (uint64_t)nt * 4);
   memcpy(h->roots.data(), hs + o_roots, (uint64_t)nt * 32);
+  if (nt && h->forest)  // (sorted: the last is the largest)
+    h->tid_bits = std::max(h->tid_bits, std::min(bits_for((uint64_t)h->tries[nt - 1] + 1) + 2, 32u));
   if (ne) build_stats_sums(c, ht, &bst);
   if (!lazy && ht[5]) throw KhError{KH_EINTERNAL, "anchor map insert failed"};
   if (!h->forest) memcpy(h->root, nt ? h->roots.data() : h->root, 32);
@@ -5740,9 +5781,10 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
       A.chk_tok = tok;
       A.vals_ready = c->bev;
       A.late = d_a_up_trie;  // the bodies that get a storage root; the rest are hashed before it
-      A.late_ready = [&] {
+      A.late_ready = [&] {  // the injection already DONE on the device (merely enqueued, the storage
+                            // phase's queue may still hold ~0.2 ms of work: the other leaves go first)
         std::lock_guard<std::mutex> lk(mu);
-        return injected;
+        return injected && hipEventQuery(c->bev) == hipSuccess;
       };
       A.before_values = [&] {
         std::unique_lock<std::mutex> lk(mu);

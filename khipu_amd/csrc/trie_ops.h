@@ -257,6 +257,7 @@ enum {
   CTR_HASHES = 0, CTR_PERMS = 1, CTR_INLINE = 2, CTR_ARENA = 3, CTR_ERR = 4, CTR_EXT = 5, CTR_LONGB = 6,
   // (row 0; the stat shards use indices 0-2 and 5 of their rows)
   // scratch slots for device-side totals read back by the host
+  CTR_NDUP = 7,  // sorts: repeated keys (k_tie_fix)
   CTR_TIE = 8, CTR_M = 9, CTR_B = 10, CTR_BRBYTES = 11, CTR_LFBYTES = 12, CTR_C = 13, CTR_E0 = 14, CTR_E1 = 15,
   CTR_N = 16
 };
@@ -1598,6 +1599,30 @@ KH_HD void window_place(uint64_t* slot, uint64_t stride, uint32_t w0, uint32_t o
     slot[(W - w0 / 8) * stride] ^= (y ^ 0x8080808080808080ULL) & m;
   }
 }
+// The same for a hashed child's 33-byte item (0xA0 + hash; the common case), branch-free: it
+// covers exactly the 5 words from off / 8; each is funnel-shifted by off % 8 bytes and
+// XOR-ed into the window with one LDS atomic (no read-back), a word outside the window
+// XOR-ing zero into word 0.
+KH_HD void slot_xor(uint64_t* p, uint64_t v) {
+#ifdef __HIP_DEVICE_COMPILE__
+  __hip_atomic_fetch_xor(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#else
+  *p ^= v;
+#endif
+}
+KH_HD void place33(uint64_t* slot, uint64_t stride, uint32_t w0, uint32_t off, const uint64_t I[5]) {
+  const uint32_t sh = off & 7, s = 8 * sh;
+  const int32_t r0 = (int32_t)(off >> 3) - (int32_t)(w0 >> 3);
+#pragma unroll
+  for (uint32_t q = 0; q < 5; ++q) {
+    const uint64_t cur = I[q], prv = q ? I[q - 1] : 0;
+    const uint64_t y = (cur << s) | ((prv >> 1) >> (63 - s));
+    const uint64_t m = q == 0 ? ~0ULL << s : q == 4 ? low_bytes_mask(sh + 1) : ~0ULL;
+    const int32_t rel = r0 + (int32_t)q;
+    const bool in = rel >= 0 && rel < 17;
+    slot_xor(slot + (in ? (uint32_t)rel : 0u) * stride, in ? (y ^ 0x8080808080808080ULL) & m : 0);
+  }
+}
 // Direct window assembly with the children streamed ONCE in order: the window loop
 // resumes at the first child not yet placed (an item crossing a window edge is placed
 // again, its tail, in the next window), the next child's record is loaded while the
@@ -1771,7 +1796,10 @@ KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uin
           take();
         }
         if (off >= w0 + 136) break;  // starts in a later window
-        window_place(slot, stride, w0, off, ilen, I);
+        if (ilen == 33)
+          place33(slot, stride, w0, off, I);
+        else
+          window_place(slot, stride, w0, off, ilen, I);
         if (off + ilen > w0 + 136) break;  // its tail goes into the next window too
         have = false;
         ++c;

@@ -366,10 +366,12 @@ def trie_get(h, keys, trie_ids=None):
 
 
 def emitted_nodes(call):
-    """Size negotiation of kh_trie_emit_nodes (KH_ENOSPC reports the sizes; no re-encoding)."""
+    """Size negotiation of kh_trie_emit_nodes (KH_ENOSPC reports the sizes; no re-encoding).
+    Another thread's commit on the handle may replace the set between the size query and the
+    read (the reader then sees KH_ENOSPC with the new sizes): the query is repeated."""
     nn, nl = ctypes.c_uint64(0), ctypes.c_uint64(0)
     cap_n, cap_b = 0, 0
-    for _ in range(2):
+    for _ in range(16):
         hs = np.zeros(32 * max(cap_n, 1), np.uint8)
         rl = np.zeros(max(cap_b, 1), np.uint8)
         of = np.zeros(cap_n + 1, np.uint64)

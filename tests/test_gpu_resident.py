@@ -189,6 +189,34 @@ def test_forest_vs_oracle(khst, oracle):
     f.close()
 
 
+def test_forest_trie_id_bits(khst, oracle):
+    """The forest's op sort takes the trie ids' bits from the ids committed before (so its
+    32-bit prefix holds key bits too): small ids, then an id past the hint (the sort is redone
+    with 32 bits), ids back inside it, many ops per trie (past the tie kernel's run limit when
+    every op of a trie shared its prefix) and one slot in several tries; every root against
+    the oracle's tries folded put by put."""
+    from khipu_amd.device import Ctx, ResidentForest
+    r = random.Random(5)
+    f = ResidentForest(Ctx(0), hash_keys=True)
+    tries = {}
+    plan = [[0, 1, 2, 3], [1, 5, 7], [6, 5000, 3], [2, 4999, 5000, 70000], [0, 1, 65535, 7]]
+    for blk, ids in enumerate(plan):
+        ups = []
+        for t in ids:
+            for _ in range(r.choice([3, 90, 200])):
+                ups.append((t, bytes(r.getrandbits(8) for _ in range(32)), C.storage_value(r)))
+            ups.append((t, b"\x22" * 32, bytes([blk + 1])))
+        dup = bytes(r.getrandbits(8) for _ in range(32))  # one key put twice: the later put wins
+        ups += [(ids[0], dup, b"\x01"), (ids[0], dup, bytes([0x40 + blk]))]
+        got = f.commit(ups, [])
+        for t, slot, v in ups:
+            tries.setdefault(t, oracle.Trie()).put(oracle.kec256(slot), v)
+        assert set(got) == set(ids), blk
+        for t in ids:
+            assert got[t] == tries[t].root_hash(), (blk, t)
+    f.close()
+
+
 @pytest.mark.parametrize("sc", C.commit_scenarios()[:4], ids=lambda s: s[0])
 def test_open_from_node_store(khst, oracle, sc):
     """kh_trie_open_nodes: a trie opened from its root hash and the
