@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of library builds on the 100M bench plus one FETCH_SIZE pass per build (measurement only):
 #   bash scripts/gpu_ab_fetch.sh TAG label=path ...   (path "" = the default libkhst.so)
-# Summarise the passes with scripts/fetch_by_dispatch.py.
+# Summarise the passes with scripts/fetch_by_dispatch.py; NOFETCH=1 skips them.
 export TMPDIR=/tmp
 tag=$1; shift
 specs=("$@")
@@ -12,6 +12,7 @@ for spec in "${specs[@]}"; do
   python -c "import json;d=json.load(open('gpurun_out/ab_${tag}_${label}_$rep.json'));print('$label', round(d['ms_per_step'],2), d['state_root'][:12], {k: round(v,2) for k,v in d['stage_ms'].items()})"
 done
 done
+[ -n "$NOFETCH" ] && exit 0  # (NOFETCH=1: the timed runs only)
 for spec in "${specs[@]}"; do
   label=${spec%%=*}; lib=${spec#*=}
   export KHST_LIB_AB=$lib
