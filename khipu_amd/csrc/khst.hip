@@ -974,10 +974,17 @@ __global__ void __launch_bounds__(BS) k_branch_hash(Topo T, uint64_t first, uint
 // bank-conflict-free within each 16-lane group (stride 34 dwords).
 // V: 0 variable-length keys (op_branch_fused), 2 the children streamed once with the next
 // record prefetched (op_branch_stream), 4 the same reading leaf children at their sorted
-// positions (leaf positions), 6 the same below depth 8 (the nibble from the input key)
+// positions (leaf positions) through the 12-bit child table (SRC_T12: the children's metas
+// loaded in one round; a wave with a branch spanning 4096+ keys takes SRC_POS), 6 the same
+// below depth 8 (the nibble from the input key).  Child table vs metas loaded child by child:
+// branch levels 7.91-7.95 -> 7.85-7.87 ms, reads 21.0 -> 16.3 GB at 100M
+// (profiles/r5u_branch_table12_ab_100m.json); one more child in flight spills 19 VGPRs and
+// costs 0.5 ms (r5v_branch_table12_queue_ab_100m.json).
 template <int V>
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8))) k_branch_fused(Topo T, uint64_t first, uint64_t cnt) {
   __shared__ uint64_t slots[BS * LEAF_WORDS];
+  constexpr bool TB = V == 4 || V == 6;
+  __shared__ uint32_t tbl[TB ? 6 * BS : 1];  // [dword][thread]: 24 B per lane beside its 136-byte window
   uint64_t t = (uint64_t)blockIdx.x * BS + threadIdx.x;
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (t < cnt) {
@@ -986,15 +993,25 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8)))
     // fixed-length keys: direct window assembly; variable-length keys (branch values):
     // the byte stream through the windowed writer
     uint64_t* sl = slots + threadIdx.x * LEAF_WORDS;
+    // (leaf positions: the table form unless some branch of the wave spans 4096 keys or more)
+    const bool wide = TB && wave_any(T.br_end[j] - T.br_first[j] >= T12_SPAN);
+    const ChildSrc ts{nullptr, nullptr, 1, tbl + threadIdx.x, BS};
     perms = V == 0   ? op_branch_fused(T, j, sl, 1, &in1)
             : V == 2 ? op_branch_stream_t<SRC_REC>(T, j, sl, 1, &in1, ChildSrc{})
-            : V == 4 ? op_branch_stream_t<SRC_POS>(T, j, sl, 1, &in1, ChildSrc{})
-                     : op_branch_stream_t<SRC_POSK>(T, j, sl, 1, &in1, ChildSrc{});
+            : V == 4 ? (TB && !wide ? op_branch_stream_t<SRC_T12>(T, j, sl, 1, &in1, ts)
+                                    : op_branch_stream_t<SRC_POS>(T, j, sl, 1, &in1, ChildSrc{}))
+                     : (TB && !wide ? op_branch_stream_t<SRC_T12K>(T, j, sl, 1, &in1, ts)
+                                    : op_branch_stream_t<SRC_POSK>(T, j, sl, 1, &in1, ChildSrc{}));
     hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
   }
-  block_add3(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), perms, ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), hashes,
-             ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), inl);
+  // one atomic per wave (a block-wide sum would need LDS past the 40 KB that 4 blocks per CU allow)
+  const unsigned long long sp = wave_sum(perms), sh = wave_sum(hashes), si = wave_sum(inl);
+  if ((threadIdx.x & 63) == 0) {
+    if (sp) atomicAdd(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), sp);
+    if (sh) atomicAdd(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), sh);
+    if (si) atomicAdd(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), si);
+  }
 }
 
 // Small levels (a block commit's dirty paths, the few branches at the top of a full build):

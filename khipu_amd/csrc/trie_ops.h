@@ -1599,6 +1599,20 @@ KH_HD void window_place(uint64_t* slot, uint64_t stride, uint32_t w0, uint32_t o
     slot[(W - w0 / 8) * stride] ^= (y ^ 0x8080808080808080ULL) & m;
   }
 }
+// any active lane of the wave (the host replay: the one lane)
+KH_HD bool wave_any(bool p) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __ballot(p) != 0;
+#else
+  return p;
+#endif
+}
+// nibble d of the key at sorted position pos, read as one dword of the input key
+KH_HD uint32_t sorted_nibble_deep(const Topo& T, uint64_t pos, uint32_t d) {
+  const uint32_t* k = (const uint32_t*)(T.kin + 4 * (uint64_t)T.sidx[pos]);
+  const uint32_t b = (k[d >> 3] >> (8 * ((d >> 1) & 3))) & 0xFF;
+  return (d & 1) ? b & 0xF : b >> 4;
+}
 // The same for a hashed child's 33-byte item (0xA0 + hash; the common case), branch-free: it
 // covers exactly the 5 words from off / 8; each is funnel-shifted by off % 8 bytes and
 // XOR-ed into the window with one LDS atomic (no read-back), a word outside the window
@@ -1668,10 +1682,19 @@ struct ChildSrc {
   const uint16_t* cm = nullptr;
   const uint64_t* cr = nullptr;
   uint32_t cs = 1;
+  uint32_t* tb = nullptr;  // SRC_T12*: the branch's child table (6 dwords, tbs apart)
+  uint32_t tbs = 1;
 };
 // where op_branch_stream reads the children (one instantiation each, so that a kernel
-// carries no dead path: the branch kernels sit at the VGPR limit of 4 waves per SIMD)
-enum { SRC_REC = 0, SRC_LDS = 1, SRC_POS = 3, SRC_POSK = 4 };
+// carries no dead path: the branch kernels sit at the VGPR limit of 4 waves per SIMD).
+// SRC_T12 / SRC_T12K (leaf positions, a branch whose key range is < 4096 positions): every
+// child's meta and end are loaded in one round and the leaf children's nibbles in a second,
+// and the child loop reads a per-thread table of 12-bit entries (a leaf child's position
+// relative to the branch's first key, or a branch child's reference length) from 24 bytes of
+// LDS: no dependent metadata load per child, and the table fits beside the window at 4 waves
+// per SIMD (16 entries of 32 bits needed 3).
+enum { SRC_REC = 0, SRC_LDS = 1, SRC_POS = 3, SRC_POSK = 4, SRC_T12 = 5, SRC_T12K = 6 };
+constexpr uint32_t T12_SPAN = 4096;  // key positions a table entry can reach
 template <int SRC>
 KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl,
                                   ChildSrc src) {
@@ -1692,7 +1715,56 @@ KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uin
     uint32_t payload = 1 + (16 - k);  // terminator "" + empty slots
     uint32_t brm = 0;                 // leaf positions: bit c = child c is a branch
     constexpr bool POS = SRC == SRC_POS || SRC == SRC_POSK;
-    if (POS) {  // a leaf child's length from its stash meta (32 unless some leaf is inline)
+    constexpr bool TBL = SRC == SRC_T12 || SRC == SRC_T12K;
+    uint64_t nibs = 0;                                   // TBL: child c's nibble at bits 4c
+    const uint32_t kfirst = TBL ? T.br_first[j] : 0u;  // TBL: the positions' origin
+    if (TBL) {
+      // one round: every child's meta and end (clamped to the last child: no predicated loads;
+      // the loops stop at the wave's largest child count)
+      uint32_t mc[16], ce[16], lp[16], lm[16];
+#pragma unroll
+      for (uint32_t c = 0; c < 16; ++c) {
+        if (!wave_any(c < k)) break;
+        const uint32_t cc = c < k ? c : k - 1;
+        mc[c] = T.cmeta[cb + cc];
+        ce[c] = T.cend[cb + cc];
+      }
+      uint32_t pos = kfirst;
+#pragma unroll
+      for (uint32_t c = 0; c < 16; ++c) {  // the leaf positions (a branch child skips its range)
+        if (!wave_any(c < k)) break;
+        const bool br = c < k && (mc[c] & CM_BR);
+        brm |= br ? 1u << c : 0u;
+        lp[c] = pos;
+        pos = br ? ce[c] : pos + 1;
+      }
+      // second round: the leaf children's nibbles (and lengths when a leaf may be inline)
+#pragma unroll
+      for (uint32_t c = 0; c < 16; ++c) {
+        if (!wave_any(c < k)) break;
+        const uint32_t p = c < k ? lp[c] : lp[0];
+        const uint32_t nib = SRC == SRC_T12K ? sorted_nibble_deep(T, p, T.lvl_depth) : (T.sck[p] >> T.lvl_nsh) & 0xF;
+        lm[c] = (T.lf_inline ? T.lf_emeta[p] : 32u) | nib << 8;
+      }
+      uint32_t tw[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (uint32_t c = 0; c < 16; ++c) {
+        if (!wave_any(c < k)) break;
+        const bool br = (brm >> c) & 1;
+        const uint32_t m = br ? mc[c] : lm[c];
+        const uint32_t len = m & 0xFF;
+        if (c < k) {
+          payload += len == 32 ? 33 : len;
+          nibs |= (uint64_t)((m >> 8) & 0xF) << (4 * c);
+        }
+        const uint32_t e = (br ? len : lp[c] - kfirst) & 0xFFF;
+        const uint32_t bit = 12 * c, d = bit >> 5, sh = bit & 31;
+        tw[d] |= e << sh;
+        if (sh > 20) tw[d + 1] |= e >> (32 - sh);
+      }
+#pragma unroll
+      for (uint32_t d = 0; d < 6; ++d) src.tb[d * src.tbs] = tw[d];
+    } else if (POS) {  // a leaf child's length from its stash meta (32 unless some leaf is inline)
       uint32_t pos = T.br_first[j];
 #pragma unroll
       for (uint32_t c = 0; c < 16; ++c) {
@@ -1751,6 +1823,18 @@ KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uin
     // child c's reference: its record, or (leaf positions) a leaf child's stash at the next
     // position of the range
     auto load_child = [&](uint32_t cc) {
+      if (TBL) {  // the table entry: a leaf's position from the branch's first key, a branch child's length
+        const uint32_t bit = 12 * cc, d = bit >> 5, sh = bit & 31;
+        uint32_t e = src.tb[d * src.tbs] >> sh;
+        if (sh > 20) e |= src.tb[(d + 1) * src.tbs] << (32 - sh);
+        e &= 0xFFF;
+        const bool br = (brm >> cc) & 1;
+        const uint32_t len = br ? e : T.lf_inline ? T.lf_emeta[kfirst + e] : 32u;
+        nm = len | ((uint32_t)(nibs >> (4 * cc)) & 0xF) << 8;
+        const uint64_t* p = br ? T.cref + 4 * (uint64_t)(cb + cc) : T.lf_eref + 4 * (uint64_t)(kfirst + e);
+        n0 = p[0], n1 = p[1], n2 = p[2], n3 = p[3];
+        return;
+      }
       nm = cmeta_at(cc);
       const uint64_t* p = cref_at(cc);
       if (POS) {  // every address known up front (the kind from brm): one round trip
@@ -1840,6 +1924,13 @@ KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint6
     Topo TL = T;
     TL.lvl_depth = T.br_depth[j];
     TL.lvl_nsh = 28 - 4 * (TL.lvl_depth & 7);
+    if (T.br_end && T.br_end[j] - T.br_first[j] < T12_SPAN) {
+      uint32_t tb[6];
+      src.tb = tb;
+      src.tbs = 1;
+      if (pos_level_ok(T, T.br_depth[j])) return op_branch_stream_t<SRC_T12>(TL, j, slot, stride, inl, src);
+      return op_branch_stream_t<SRC_T12K>(TL, j, slot, stride, inl, src);
+    }
     if (pos_level_ok(T, T.br_depth[j])) return op_branch_stream_t<SRC_POS>(TL, j, slot, stride, inl, src);
     return op_branch_stream_t<SRC_POSK>(TL, j, slot, stride, inl, src);
   }
