@@ -437,11 +437,18 @@ __global__ void __launch_bounds__(BS) k_el_gather3(Topo T, const uint8_t* db, co
   obrl2[i] = brl2[s];
 }
 
-// ties_u: boundaries between equal 32-bit prefixes were valued by the tie-run kernel
-__global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb, bool ties_u) {
+// ties_u: boundaries between equal 32-bit prefixes were valued by the tie-run kernel, unless
+// a run was too long for it (tie flag bit 0: a speculative build, redone after its first sync
+// with the full sort).  Such a run is left unordered and unvalued, so its boundaries get 0 (as
+// between repeated keys: each key of the run a trie of its own) -- whatever the buffer held
+// from an earlier build would shape a topology whose leaf depths leave 0..63.
+__global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb, bool ties_u, const unsigned long long* tie) {
   uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (b >= nb) return;
-  if (ties_u && T.sck[b] == T.sck[b + 1]) return;
+  if (ties_u && T.sck[b] == T.sck[b + 1]) {
+    if (*tie & 1) T.u[b] = 0;
+    return;
+  }
   op_lcp(T, b);
 }
 // the 64-ary min pyramid over the boundary values: level `from` by the whole grid, the
@@ -2346,7 +2353,8 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));  // every leaf a hash unless it says otherwise
   }
   if (nb > 0) {
-    hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb, ties_u);
+    hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb, ties_u,
+                       (const unsigned long long*)(ctr + CTR_TIE));
     LAUNCH_CHECK();
   }
   auto launch_leaves = [&](bool scatter) {  // on st2, after everything enqueued on st so far

@@ -1918,13 +1918,13 @@ KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uin
 
 // runtime choice of the child source (the host replay; the kernels instantiate theirs)
 KH_HD uint32_t op_branch_stream(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl,
-                                ChildSrc src = ChildSrc{}) {
+                                ChildSrc src = ChildSrc{}, bool per_child = false) {
   if (src.cm) return op_branch_stream_t<SRC_LDS>(T, j, slot, stride, inl, src);
   if (T.cend) {
     Topo TL = T;
     TL.lvl_depth = T.br_depth[j];
     TL.lvl_nsh = 28 - 4 * (TL.lvl_depth & 7);
-    if (T.br_end && T.br_end[j] - T.br_first[j] < T12_SPAN) {
+    if (!per_child && T.br_end && T.br_end[j] - T.br_first[j] < T12_SPAN) {  // (per_child: the wide waves' form)
       uint32_t tb[6];
       src.tb = tb;
       src.tbs = 1;

@@ -307,7 +307,9 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
         const uint64_t cb = T.br_cbase[j];
         p = op_branch_stream(T, j, slot, 1, &in1, ChildSrc{T.cmeta + cb, T.cref + 4 * cb, 1});
       } else {
-        p = T.kn ? op_branch_fused(T, j, slot, 1, &in1) : op_branch_stream(T, j, slot, 1, &in1);
+        // (leaf positions: the child-table form, and every fourth branch the per-child form that
+        // a wave with a branch spanning 4096+ keys takes on the device)
+        p = T.kn ? op_branch_fused(T, j, slot, 1, &in1) : op_branch_stream(T, j, slot, 1, &in1, ChildSrc{}, (j & 3) == 0);
       }
       perms += p;
       hashes += branch_hash_count(T, j, p);

@@ -408,6 +408,29 @@ def test_tie_runs_across_blocks(khst, oracle):
     assert khst.trie_root(rep, rvals) == oracle.batch_root(rep, rvals, nthreads=4)
 
 
+def test_wide_branches_in_large_levels(khst, oracle):
+    """The large levels' child table reaches 4,096 key positions from a branch's first key;
+    a wave holding a branch that spans more takes the per-child form (k_branch_fused).  3M
+    random raw keys (a 65,536-branch depth-4 level and a ~0.9M-branch depth-5 level) plus
+    a 20k-key cluster under one 5-nibble prefix and a 6k-key cluster under one 6-nibble
+    prefix, whose ancestors in those levels span 6k-20k keys; the root equals the CPU batch
+    builder's."""
+    rng = np.random.default_rng(31)
+    n = 3_000_000
+    keys = rng.integers(0, 256, (n + 26_000, 32), dtype=np.uint8)
+    keys[n:n + 20_000, :2] = [0x12, 0x34]
+    keys[n:n + 20_000, 2] = (keys[n:n + 20_000, 2] & 0x0F) | 0x50  # prefix 0x1234 5
+    keys[n + 20_000:, :3] = [0xAB, 0xCD, 0xEF]                      # prefix 0xABCDEF
+    rng.shuffle(keys)
+    lens = rng.choice([1, 33, 70, 90], len(keys)).astype(np.uint64)
+    off = np.zeros(len(keys) + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    vals = rng.integers(1, 256, int(off[-1]), dtype=np.uint8)
+    flat = np.ascontiguousarray(keys).reshape(-1)
+    roots, _ = oracle.batch_roots(flat, (vals, off), klen=32)
+    assert khst.trie_root(flat, (vals, off), klen=32) == roots[0]
+
+
 def test_hashed_keys_with_repeats(khst, oracle):
     """Hashed-key builds (the plain path: 32-bit sort prefixes from the hashing pass, ties
     ordered by the whole key, the last put of a repeated key kept) over sizes around the
