@@ -150,6 +150,67 @@ KH_HD void keccakf(KState& s) {
 
 KH_HD uint64_t lane(const KState& s, int i) { return ((uint64_t)s.hi[i] << 32) | s.lo[i]; }
 
+// ---- Keccak-f on a lane pair (k_branch_small: levels of 8k-32k branches, a wave or two per
+// SIMD, where one thread's permutation -- 180 dependent VALU a round at 4 cycles each -- is the
+// level's latency).  Lane 2i holds the low halves of the 25 state words, lane 2i + 1 the high
+// halves, in W[25].  Every 64-bit rotation becomes one DPP swap with the partner lane and one
+// funnel shift, the same instruction on both lanes (low lane: (l, h) -> l' = {l:h} >> (32 - n);
+// high lane: (h, l) -> h' = {h:l} >> (32 - n); past 32 the operands trade places); theta's
+// parities and chi stay lane-local.  120 VALU a round per lane.  Both lanes of a pair must be
+// active (the DPP reads the partner).
+KH_HD uint32_t pair_partner(uint32_t x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  // quad_perm [1,0,3,2]; bound_ctrl set, so no "old" operand is materialised (every lane reads
+  // its partner: the v_mov of a zero old value before each DPP move was a fifth of the round)
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);
+#else
+  return x;  // (host code never runs the pair form)
+#endif
+}
+KH_HD bool pair_odd() {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __lane_id() & 1;
+#else
+  return false;
+#endif
+}
+KH_HD uint32_t rotl_pair(uint32_t v, int n) {
+  if (n == 0) return v;
+  const uint32_t p = pair_partner(v);
+  return n < 32 ? funnel(v, p, 32 - n) : n == 32 ? p : funnel(p, v, 64 - n);
+}
+KH_HD void keccak_round_pair(uint32_t* W, uint32_t rc_half) {
+  constexpr int ROT[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+  uint32_t C[5], R[5], B[25];
+#pragma unroll
+  for (int x = 0; x < 5; ++x) C[x] = xor3(xor3(W[x], W[x + 5], W[x + 10]), W[x + 15], W[x + 20]);
+#pragma unroll
+  for (int x = 0; x < 5; ++x) R[x] = funnel(C[x], pair_partner(C[x]), 31);  // this lane's half of rot(C[x], 1)
+#pragma unroll
+  for (int x = 0; x < 5; ++x)
+#pragma unroll
+    for (int y = 0; y < 5; ++y) {
+      const int i = x + 5 * y;
+      B[y + 5 * ((2 * x + 3 * y) % 5)] = rotl_pair(xor3(W[i], C[(x + 4) % 5], R[(x + 1) % 5]), ROT[i]);
+    }
+#pragma unroll
+  for (int y = 0; y < 5; ++y)
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+      const int i = x + 5 * y;
+      W[i] = B[i] ^ (~B[(x + 1) % 5 + 5 * y] & B[(x + 2) % 5 + 5 * y]);
+    }
+  W[0] ^= rc_half;
+}
+template <int U = KECCAK_LOOP>
+KH_HD void keccakf_pair(uint32_t* W, bool odd) {
+#pragma unroll U
+  for (int r = 0; r < 24; ++r) {
+    const uint64_t rc = round_constant(r);
+    keccak_round_pair(W, odd ? (uint32_t)(rc >> 32) : (uint32_t)rc);
+  }
+}
+
 // XOR word w into rate lane i (i compile-time after unrolling).
 KH_HD void kxor(KState& s, int i, uint64_t w) {
   s.lo[i] ^= (uint32_t)w;

@@ -1025,15 +1025,18 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8)))
 // latency-bound, a wave or less per CU.  op_branch_stream prefetches one child record
 // ahead, so a full branch waits for 16 HBM round trips in a row.  Here every child record
 // of the branch is loaded at once (16 x 32 B in flight per thread) and copied to LDS
-// (lane-interleaved, conflict-free), and the stream reads it from there.  One wave per
-// block; the VGPR budget is free at this occupancy.
+// (lane-interleaved, conflict-free), and the stream reads it from there.  A lane pair per
+// branch: both lanes assemble the same encoding and share the permutations (keccakf_pair,
+// 120 instead of 180 dependent VALU a round); one wave per block, the VGPR budget is free at
+// this occupancy.
 constexpr uint32_t SMALL_LEVEL = 32768;  // branches per level below which k_branch_small runs
+constexpr uint32_t SMALL_BPB = 32;       // k_branch_small: branches per 64-lane block
 __global__ void __launch_bounds__(64) k_branch_small(Topo T, uint64_t first, uint64_t cnt) {
   constexpr uint32_t WB = 64;
   __shared__ uint64_t slots[WB * LEAF_WORDS];
   __shared__ uint64_t crs[64 * WB];
   __shared__ uint16_t cms[16 * WB];
-  const uint64_t t = (uint64_t)blockIdx.x * WB + threadIdx.x;
+  const uint64_t t = (uint64_t)blockIdx.x * SMALL_BPB + (threadIdx.x >> 1);  // (a pair is inside or past cnt together)
   unsigned long long perms = 0, hashes = 0, inl = 0;
   if (t < cnt) {
     const uint32_t j = (uint32_t)(first + t), tid = threadIdx.x;
@@ -1089,9 +1092,10 @@ __global__ void __launch_bounds__(64) k_branch_small(Topo T, uint64_t first, uin
       }
     }
     uint32_t in1 = 0;
-    perms = op_branch_stream_t<SRC_LDS>(T, j, slots + tid * LEAF_WORDS, 1, &in1, ChildSrc{cms + tid, crs + tid, WB});
+    perms = op_branch_stream_t<SRC_LDS, true>(T, j, slots + tid * LEAF_WORDS, 1, &in1, ChildSrc{cms + tid, crs + tid, WB});
     hashes = branch_hash_count(T, j, (uint32_t)perms);
     inl = in1;
+    if (tid & 1) perms = hashes = inl = 0;  // (counted once per pair)
   }
   perms = wave_sum(perms);
   hashes = wave_sum(hashes);
@@ -2614,7 +2618,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
         hipLaunchKernelGGL(k_branch_xl, dim3((unsigned)((cnt + 1) / 2)), dim3(64), 0, st, T, (uint64_t)lbh[d],
                            (uint64_t)cnt);
       else if (small)
-        hipLaunchKernelGGL(k_branch_small, dim3((unsigned)((cnt + 63) / 64)), dim3(64), 0, st, T, (uint64_t)lbh[d],
+        hipLaunchKernelGGL(k_branch_small, dim3((unsigned)((cnt + SMALL_BPB - 1) / SMALL_BPB)), dim3(64), 0, st, T, (uint64_t)lbh[d],
                            (uint64_t)cnt);
       else if (T.cend) {  // leaf children from their stashes
         Topo TL = T;

@@ -1,12 +1,12 @@
 // Device primitives for the state-root pipeline: wave reductions, exclusive scan,
 // and a stable LSD radix sort of (uint64 key, uint32 value) pairs.
 //
-// Radix sort: 8-bit digits, one (histogram, scan, scatter) triple per pass.  A
-// tile is 256 threads x 8 items = 2048 keys; each 64-lane wave owns a
-// contiguous 512-key slice of the tile and ranks its keys with a ballot-based
-// wave-level multisplit (8 ballots give the mask of lanes holding the same
-// digit), so the scatter is stable; the tile is then staged in LDS in digit
-// order and written out run by run (coalesced).
+// Radix sort: 8-bit digits; one launch counts the digits of every pass, then one launch per
+// pass (decoupled look-back over the tiles' digit counts).  A tile is 256 threads x 16 keys
+// (4 for small sorts); each 64-lane wave owns a contiguous slice of the tile and ranks its
+// keys with a ballot-based wave-level multisplit (8 ballots give the mask of lanes holding
+// the same digit), so the scatter is stable; the tile is then staged in LDS in digit order
+// and written out run by run (coalesced).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -302,7 +302,12 @@ void scan_exclusive(const T* in, T* out, uint64_t n, T* total, void* scratch, hi
 // ---------------------------------------------------------------------------
 // Radix sort of (key, uint32 val) pairs on key bits [lo_bit, hi_bit); keys are uint64
 // (composite segment | key prefixes) or uint32 (the plain path's 32-bit key prefixes:
-// 8 bytes a pair moved per pass instead of 12).
+// 8 bytes a pair moved per pass instead of 12).  One sweep per pass: one launch counts the
+// digits of every pass at once (a pass's digit totals do not depend on the order the earlier
+// passes leave), then each pass is one launch whose tiles rank their keys, publish their digit
+// counts and take the counts of the tiles before them by decoupled look-back.  (Each pass had
+// been a histogram launch, a scan of the tiles x 256 counts unless the sort was small, and the
+// scatter: 2 to 5 launches.)
 // ---------------------------------------------------------------------------
 constexpr int RS_THREADS = 256;
 // 16 keys per thread: 4096-key tiles, so a digit's run in a tile averages 16 keys (64 B
@@ -314,60 +319,74 @@ constexpr int RS_THREADS = 256;
 constexpr int RS_ITEMS = KHST_RS_ITEMS;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 keys: 36 KiB of LDS staging (32-bit keys)
 constexpr int RS_WAVES = RS_THREADS / 64;
-constexpr int RS_WSLICE = RS_TILE / RS_WAVES;   // 512 keys per wave
-constexpr uint32_t RS_FUSE_TILES = 64;          // radix_sort_pairs: scan-free passes up to 256k keys
+constexpr int RS_MAX_PASSES = 8;
+// Status word of (pass, tile, digit): bits 63:62 are 0 until the tile publishes, 1 for the
+// tile's own count of the digit, 2 for the count over this tile and every tile before it;
+// bits 61:0 hold the count.
+constexpr unsigned long long RS_ST_AGG = 1ull << 62, RS_ST_INC = 2ull << 62, RS_ST_CNT = RS_ST_AGG - 1;
+// scratch header: the digit totals of every pass, then the passes' tile tickets
+constexpr size_t RS_HDR_BYTES = (RS_MAX_PASSES * 256 + RS_MAX_PASSES) * sizeof(uint32_t);
+constexpr size_t RS_HDR_PAD = (RS_HDR_BYTES + 255) / 256 * 256;
 
-template <typename K, int IT = RS_ITEMS>
-__global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const K* keys, uint64_t n, int shift, uint32_t* counts,
-                                                        uint32_t ntiles) {
-  constexpr int TILE = RS_THREADS * IT, WSLICE = TILE / RS_WAVES;
-  __shared__ uint32_t h[RS_WAVES][256];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
+// Digit totals of npass passes (bits lo_bit + 8p .. + 8) over all n keys, added into ghist
+// (zeroed), and the first pass's status words cleared.  Grid-stride over tiles.
+template <typename K, int IT>
+__global__ void __launch_bounds__(RS_THREADS) k_rs_hist_all(const K* keys, uint64_t n, int lo_bit, int npass,
+                                                            uint32_t* ghist, unsigned long long* st0, uint64_t nst) {
+  constexpr int TILE = RS_THREADS * IT;
+  __shared__ uint32_t h[RS_MAX_PASSES][256];
+  for (int i = threadIdx.x; i < RS_MAX_PASSES * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * RS_THREADS + threadIdx.x; i < nst; i += (uint64_t)gridDim.x * RS_THREADS)
+    st0[i] = 0;
   __syncthreads();
-  uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)w * WSLICE;
-  // every key of the slice loaded before the first LDS atomic (the atomics would otherwise
-  // hold each load back to its own round trip)
-  uint32_t dg[WSLICE / 64];
+  for (uint64_t t0 = (uint64_t)blockIdx.x * TILE; t0 < n; t0 += (uint64_t)gridDim.x * TILE) {
+    // every key of the tile loaded before the first LDS atomic (the atomics would otherwise
+    // hold each load back to its own round trip)
+    K kk[IT];
 #pragma unroll
-  for (int it = 0; it < WSLICE / 64; ++it) {
-    uint64_t i = base + (uint64_t)it * 64 + lane;
-    const K kk = keys[i < n ? i : n - 1];  // (unconditional: no branch between the loads)
-    dg[it] = i < n ? (uint32_t)(kk >> shift) & 0xFF : 256u;
+    for (int it = 0; it < IT; ++it) {
+      const uint64_t i = t0 + (uint64_t)it * RS_THREADS + threadIdx.x;
+      kk[it] = keys[i < n ? i : n - 1];
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      if (t0 + (uint64_t)it * RS_THREADS + threadIdx.x < n)
+        for (int p = 0; p < npass; ++p) atomicAdd(&h[p][(uint32_t)(kk[it] >> (lo_bit + 8 * p)) & 0xFF], 1u);
+    }
   }
-#pragma unroll
-  for (int it = 0; it < WSLICE / 64; ++it)
-    if (dg[it] < 256) atomicAdd(&h[w][dg[it]], 1u);
   __syncthreads();
-  for (int d = threadIdx.x; d < 256; d += RS_THREADS) {
-    uint32_t s = 0;
-#pragma unroll
-    for (int q = 0; q < RS_WAVES; ++q) s += h[q][d];
-    counts[(uint64_t)d * ntiles + blockIdx.x] = s;
+  for (int i = threadIdx.x; i < npass * 256; i += RS_THREADS) {
+    const uint32_t v = (&h[0][0])[i];
+    if (v) atomicAdd(&ghist[i], v);
   }
 }
 
-// Scatter of one pass.  Keys are ranked per wave (ballot multisplit), placed in
-// LDS in digit order for the whole tile, then written out so that each digit's
-// run of the tile goes to consecutive global addresses (coalesced stores instead
-// of one scattered 8-byte store per key).
+// One pass.  The tile index comes from a ticket (tiles are taken in launch order, so every
+// tile a look-back waits for is already running).  Keys are ranked per wave (ballot
+// multisplit), the tile's digit counts published, the counts of the tiles before it looked
+// back for, the tile placed in LDS in digit order and written out so that each digit's run of
+// the tile goes to consecutive global addresses (coalesced stores instead of one scattered
+// store per key).  status_next (nullable): the next pass's status words, cleared here.
 template <typename K, int IT = RS_ITEMS>
-__global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const uint32_t* vals, K* okeys,
-                                                           uint32_t* ovals, uint64_t n, int shift,
-                                                           const uint32_t* offs, uint32_t ntiles, bool fused) {
+__global__ void __launch_bounds__(RS_THREADS) k_rs_pass(const K* keys, const uint32_t* vals, K* okeys,
+                                                        uint32_t* ovals, uint64_t n, int shift, const uint32_t* ghist,
+                                                        unsigned long long* status, unsigned long long* status_next,
+                                                        uint32_t* ticket) {
   constexpr int TILE = RS_THREADS * IT, WSLICE = TILE / RS_WAVES;
   __shared__ uint32_t wc[RS_WAVES][256];
   __shared__ uint32_t tstart[256], gbase[256];
   __shared__ uint32_t lw[RS_THREADS / 64];
+  __shared__ uint32_t s_tile;
   __shared__ K sk[TILE];
   __shared__ uint32_t sv[TILE];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // this tile's global base of digit threadIdx.x: loaded now, used after the ranking (one
-  // HBM round trip less in the middle of the tile)
-  const uint32_t gb_pre = fused ? 0u : offs[(uint64_t)threadIdx.x * ntiles + blockIdx.x];
+  if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+  const uint32_t gtot = ghist[threadIdx.x];  // digit threadIdx.x over all tiles (RS_THREADS == 256 digits)
+  if (status_next) status_next[(uint64_t)blockIdx.x * 256 + threadIdx.x] = 0;
   for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_THREADS) (&wc[0][0])[i] = 0;
   __syncthreads();
-  const uint64_t tbase = (uint64_t)blockIdx.x * TILE;
+  const uint32_t tile = s_tile;
+  const uint64_t tbase = (uint64_t)tile * TILE;
   const uint64_t base = tbase + (uint64_t)w * WSLICE;
   K k[IT];
   uint32_t v[IT];
@@ -402,9 +421,10 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const 
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
-  // per digit: wave offsets inside the tile's digit run, tile-local run start, global base
+  // per digit: wave offsets inside the tile's digit run, the count published, tile-local run
+  // start, the digit's global start, the count in earlier tiles (look-back)
   {
-    const int d = threadIdx.x;  // RS_THREADS == 256 digits
+    const int d = threadIdx.x;
     uint32_t run = 0;
 #pragma unroll
     for (int q = 0; q < RS_WAVES; ++q) {
@@ -412,20 +432,27 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const 
       wc[q][d] = run;
       run += t;
     }
+    unsigned long long* my = status + (uint64_t)tile * 256 + d;
+    __hip_atomic_store(my, (tile == 0 ? RS_ST_INC : RS_ST_AGG) | run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t tot;
     tstart[d] = block_exclusive_scan<uint32_t>(run, lw, &tot);
-    if (fused) {  // offs holds the raw tile counts: the digit's total and this tile's share before it
-      uint32_t all = 0, pre = 0;
-      const uint32_t* cd = offs + (uint64_t)d * ntiles;
-      for (uint32_t t = 0; t < ntiles; ++t) {
-        const uint32_t q = cd[t];
-        all += q;
-        pre += t < blockIdx.x ? q : 0u;
+    const uint32_t dbase = block_exclusive_scan<uint32_t>(gtot, lw, &tot);
+    uint64_t excl = 0;
+    if (tile > 0) {
+      for (uint64_t t = tile - 1;;) {
+        const unsigned long long s =
+            __hip_atomic_load(status + t * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((s >> 62) == 0) {  // not published yet (its tile is running: it took an earlier ticket)
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        excl += s & RS_ST_CNT;
+        if ((s >> 62) == 2) break;  // (tile 0 publishes its count as inclusive)
+        --t;
       }
-      gbase[d] = block_exclusive_scan<uint32_t>(all, lw, &tot) + pre;
-    } else {
-      gbase[d] = gb_pre;
+      __hip_atomic_store(my, RS_ST_INC | (excl + run), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    gbase[d] = dbase + (uint32_t)excl;
   }
   __syncthreads();
 #pragma unroll
@@ -453,46 +480,52 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const K* keys, const 
 // (4 keys per thread): 4x the blocks, a quarter of each block's serial ranking -- the passes
 // are latency-bound at these sizes.
 constexpr int RS_SMALL_ITEMS = 4;
-constexpr uint64_t RS_SMALL_N = (uint64_t)RS_FUSE_TILES * RS_THREADS * RS_SMALL_ITEMS;  // 65536
+constexpr uint64_t RS_SMALL_N = 65536;
+inline uint64_t radix_tiles(uint64_t n) {
+  const uint64_t tile = n <= RS_SMALL_N ? (uint64_t)RS_THREADS * RS_SMALL_ITEMS : (uint64_t)RS_TILE;
+  return (n + tile - 1) / tile;
+}
 inline size_t radix_scratch_bytes(uint64_t n) {
-  uint64_t tiles = (n + RS_TILE - 1) / RS_TILE;
-  if (n <= RS_SMALL_N) tiles = (n + RS_THREADS * RS_SMALL_ITEMS - 1) / (RS_THREADS * RS_SMALL_ITEMS);
-  uint64_t c = tiles * 256;
-  return c * sizeof(uint32_t) + 256 + scan_scratch_bytes(c, sizeof(uint32_t));
+  return RS_HDR_PAD + 2 * radix_tiles(n) * 256 * sizeof(unsigned long long) + 256;
 }
 
-// Sorts (k0, v0) on bits [lo_bit, hi_bit) (multiples of 8), using (k1, v1) as
-// ping-pong buffers.  Returns true if the result ended in (k1, v1).
-// n must be < 2^32.
+// Sorts (k0, v0) on bits [lo_bit, hi_bit) (multiples of 8, at most 64 bits), using (k1, v1)
+// as ping-pong buffers.  Returns true if the result ended in (k1, v1).  n must be < 2^32.
+// Launches: a fill of the scratch header, the digit count, one per pass.
 template <typename K>
 inline bool radix_sort_pairs(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n, int lo_bit, int hi_bit,
                              void* scratch, hipStream_t st) {
-  if (n <= 1) return false;
+  if (n <= 1 || hi_bit <= lo_bit) return false;
   const bool small = n <= RS_SMALL_N;
-  const uint32_t tile = small ? RS_THREADS * RS_SMALL_ITEMS : RS_TILE;
-  uint32_t tiles = (uint32_t)((n + tile - 1) / tile);
-  uint32_t* counts = (uint32_t*)scratch;
-  void* scan_ws = (char*)scratch + (((uint64_t)tiles * 256 * sizeof(uint32_t) + 255) / 256) * 256;
+  const uint64_t tiles = radix_tiles(n);
+  const int npass = (hi_bit - lo_bit + 7) / 8;
+  uint32_t* ghist = (uint32_t*)scratch;
+  uint32_t* ticket = ghist + RS_MAX_PASSES * 256;
+  unsigned long long* stat[2] = {(unsigned long long*)((char*)scratch + RS_HDR_PAD), nullptr};
+  stat[1] = stat[0] + tiles * 256;
+  (void)hipMemsetAsync(ghist, 0, RS_HDR_BYTES, st);
+  const unsigned hgrid = (unsigned)(tiles < 1024 ? tiles : 1024);
+  if (small)
+    hipLaunchKernelGGL((k_rs_hist_all<K, RS_SMALL_ITEMS>), dim3(hgrid), dim3(RS_THREADS), 0, st, (const K*)k0, n,
+                       lo_bit, npass, ghist, stat[0], tiles * 256);
+  else
+    hipLaunchKernelGGL((k_rs_hist_all<K, RS_ITEMS>), dim3(hgrid), dim3(RS_THREADS), 0, st, (const K*)k0, n, lo_bit,
+                       npass, ghist, stat[0], tiles * 256);
   bool flip = false;
-  // up to RS_FUSE_TILES tiles (small sorts: a block commit's ops and elements) the scatter
-  // computes its digit bases from the raw counts itself: 2 launches a pass instead of 3-5
-  const bool fused = tiles <= RS_FUSE_TILES;
-  for (int sh = lo_bit; sh < hi_bit; sh += 8) {
+  for (int p = 0; p < npass; ++p) {
     K* ik = flip ? k1 : k0;
     uint32_t* iv = flip ? v1 : v0;
     K* ok = flip ? k0 : k1;
     uint32_t* ov = flip ? v0 : v1;
-    if (small) {
-      hipLaunchKernelGGL((k_rs_hist<K, RS_SMALL_ITEMS>), dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik, n, sh,
-                         counts, tiles);
-      hipLaunchKernelGGL((k_rs_scatter<K, RS_SMALL_ITEMS>), dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik,
-                         (const uint32_t*)iv, ok, ov, n, sh, (const uint32_t*)counts, tiles, true);
-    } else {
-      hipLaunchKernelGGL(k_rs_hist<K>, dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik, n, sh, counts, tiles);
-      if (!fused) scan_exclusive<uint32_t>(counts, counts, (uint64_t)tiles * 256, (uint32_t*)nullptr, scan_ws, st);
-      hipLaunchKernelGGL(k_rs_scatter<K>, dim3(tiles), dim3(RS_THREADS), 0, st, (const K*)ik, (const uint32_t*)iv, ok,
-                         ov, n, sh, (const uint32_t*)counts, tiles, fused);
-    }
+    unsigned long long* nxt = p + 1 < npass ? stat[(p + 1) & 1] : nullptr;
+    if (small)
+      hipLaunchKernelGGL((k_rs_pass<K, RS_SMALL_ITEMS>), dim3((unsigned)tiles), dim3(RS_THREADS), 0, st, (const K*)ik,
+                         (const uint32_t*)iv, ok, ov, n, lo_bit + 8 * p, (const uint32_t*)(ghist + 256 * p), stat[p & 1],
+                         nxt, ticket + p);
+    else
+      hipLaunchKernelGGL((k_rs_pass<K>), dim3((unsigned)tiles), dim3(RS_THREADS), 0, st, (const K*)ik,
+                         (const uint32_t*)iv, ok, ov, n, lo_bit + 8 * p, (const uint32_t*)(ghist + 256 * p), stat[p & 1],
+                         nxt, ticket + p);
     flip = !flip;
   }
   return flip;

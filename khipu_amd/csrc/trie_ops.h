@@ -1695,7 +1695,10 @@ struct ChildSrc {
 // per SIMD (16 entries of 32 bits needed 3).
 enum { SRC_REC = 0, SRC_LDS = 1, SRC_POS = 3, SRC_POSK = 4, SRC_T12 = 5, SRC_T12K = 6 };
 constexpr uint32_t T12_SPAN = 4096;  // key positions a table entry can reach
-template <int SRC>
+// PAIR (k_branch_small): lanes 2i and 2i + 1 both run the stream for the same branch (the same
+// control flow and stores) and share its permutations, each holding one 32-bit half of every
+// state word (keccak.h keccakf_pair); the extension above a branch stays one lane's.
+template <int SRC, bool PAIR = false>
 KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uint64_t stride, uint32_t* inl,
                                   ChildSrc src) {
   const uint32_t ext = T.br_ext[j];
@@ -1895,12 +1898,30 @@ KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uin
         slot[(rem >> 3) * stride] ^= 0x01ULL << (8 * (rem & 7));
         slot[16 * stride] ^= 0x80ULL << 56;
       }
+      if (PAIR) {
+        const bool odd = pair_odd();
 #pragma unroll
-      for (int q = 0; q < 17; ++q) kxor(S, q, slot[q * stride]);  // zero past the encoding already
-      keccakf(S);
+        for (int q = 0; q < 17; ++q) {
+          const uint64_t w = slot[q * stride];
+          S.lo[q] ^= odd ? (uint32_t)(w >> 32) : (uint32_t)w;
+        }
+        keccakf_pair(S.lo, odd);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 17; ++q) kxor(S, q, slot[q * stride]);  // zero past the encoding already
+        keccakf(S);
+      }
     }
     if (hashit) {
-      for (int q = 0; q < 4; ++q) hb[q] = lane(S, q);
+      if (PAIR) {
+        const bool odd = pair_odd();
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t m = S.lo[q], o = pair_partner(m);
+          hb[q] = odd ? ((uint64_t)m << 32) | o : ((uint64_t)o << 32) | m;
+        }
+      } else {
+        for (int q = 0; q < 4; ++q) hb[q] = lane(S, q);
+      }
       perms = nfull + 1;
     }
     if (L < 32)
