@@ -1,49 +1,76 @@
-"""Host side of the last block commit in a rocprofv3 --hip-trace (measurement only): every
-HIP API call of the last window (cut like scripts/block_trace.py: idle gaps > --gap ms
-between kernels), with its duration and the host time since the previous call ended.
+"""Host-side view of configs[2] block commits (measurement only): a rocprofv3 --hip-trace
+--kernel-trace run of scripts/block_commit_prof.py, cut into blocks at the idle gaps, then per
+block and host thread: time inside HIP calls by function, the host time between a
+hipStreamSynchronize returning and the thread's next HIP call, and for every kernel the delay
+from its launch call returning to the kernel starting on the GPU.
 
-  python scripts/api_trace.py gpurun_out/bc_api [--gap 30] [--top 40]
+  python scripts/api_trace.py gpurun_out/bch_r6d > profiles/<tag>_block_commit_host_api_50m.json
 """
-import argparse
+import collections
 import csv
 import glob
 import json
+import sys
+
+
+def rows(d, pat):
+    out = []
+    for f in glob.glob(f"{d}/**/{pat}", recursive=True):
+        out += list(csv.DictReader(open(f)))
+    return out
 
 
 def main():
-    p = argparse.ArgumentParser()
-    p.add_argument("dir")
-    p.add_argument("--gap", type=float, default=30.0)
-    p.add_argument("--top", type=int, default=40)
-    a = p.parse_args()
-    krows, arows = [], []
-    for f in glob.glob(f"{a.dir}/**/*kernel_trace.csv", recursive=True):
-        krows += list(csv.DictReader(open(f)))
-    for f in glob.glob(f"{a.dir}/**/*hip_api_trace.csv", recursive=True):
-        arows += list(csv.DictReader(open(f)))
-    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in krows)
-    wins, cur = [], []
-    for e in ev:
-        if cur and e[0] - max(x[1] for x in cur[-8:]) > a.gap * 1e6:
-            wins.append(cur)
+    d = sys.argv[1]
+    gap_ns = 20e6
+    api = rows(d, "*hip_api_trace.csv")
+    ker = rows(d, "*kernel_trace.csv")
+    ks = sorted(({"name": r["Kernel_Name"].split("(")[0].replace("void ", ""), "corr": r["Correlation_Id"],
+                  "s": int(r["Start_Timestamp"]), "e": int(r["End_Timestamp"])} for r in ker), key=lambda k: k["s"])
+    # blocks: kernels separated by idle gaps
+    blocks, cur = [], []
+    for k in ks:
+        if cur and k["s"] - max(x["e"] for x in cur) > gap_ns:
+            blocks.append(cur)
             cur = []
-        cur.append(e)
-    if cur:
-        wins.append(cur)
-    w = wins[-1]
-    t0, t1 = w[0][0] - 400_000, w[-1][1]  # (the call starts before its first kernel)
-    calls = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Function"]) for r in arows
-                   if t0 <= int(r["Start_Timestamp"]) <= t1)
-    out, prev = [], None
-    for s, e, fn in calls:
-        out.append([fn, round((s - t0) / 1e3, 1), round((e - s) / 1e3, 1), round((s - prev) / 1e3, 1) if prev else 0.0])
-        prev = e
-    tot = {}
-    for fn, _, d, _ in out:
-        tot[fn] = tot.get(fn, 0.0) + d
-    print(json.dumps({"calls": len(out), "api_us_by_function": dict(sorted(tot.items(), key=lambda kv: -kv[1])[:a.top]),
-                      "host_gaps_over_10us": [x for x in out if x[3] > 10][:a.top],
-                      "longest_calls": sorted(out, key=lambda x: -x[2])[:a.top]}, indent=1))
+        cur.append(k)
+    blocks.append(cur)
+    blocks = [b for b in blocks if len(b) > 50][-3:]  # the timed blocks
+    calls = sorted(({"fn": r["Function"], "tid": r["Thread_Id"], "corr": r["Correlation_Id"], "s": int(r["Start_Timestamp"]),
+                     "e": int(r["End_Timestamp"])} for r in api), key=lambda c: c["s"])
+    by_corr = {c["corr"]: c for c in calls}
+    res = []
+    for b in blocks:
+        t0, t1 = b[0]["s"] - 200_000, max(k["e"] for k in b)
+        cs = [c for c in calls if t0 <= c["s"] <= t1]
+        per_thread = collections.defaultdict(list)
+        for c in cs:
+            per_thread[c["tid"]].append(c)
+        threads = {}
+        for tid, lst in per_thread.items():
+            fn_us = collections.Counter()
+            fn_n = collections.Counter()
+            after_sync = []
+            for i, c in enumerate(lst):
+                fn_us[c["fn"]] += (c["e"] - c["s"]) / 1e3
+                fn_n[c["fn"]] += 1
+                if c["fn"] == "hipStreamSynchronize" and i + 1 < len(lst):
+                    after_sync.append(round((lst[i + 1]["s"] - c["e"]) / 1e3, 1))
+            span = (lst[-1]["e"] - lst[0]["s"]) / 1e3
+            threads[tid] = {"calls": len(lst), "span_us": round(span, 1),
+                            "in_hip_us": round(sum(fn_us.values()), 1),
+                            "by_function_us": {k: [fn_n[k], round(v, 1)] for k, v in fn_us.most_common(12)},
+                            "host_us_after_each_sync": after_sync}
+        lat = []
+        for k in b:
+            c = by_corr.get(k["corr"])
+            if c:
+                lat.append((k["s"] - c["e"]) / 1e3)
+        lat.sort()
+        res.append({"kernels": len(b), "gpu_span_us": round((t1 - b[0]["s"]) / 1e3, 1), "threads": threads,
+                    "launch_return_to_kernel_start_us": {"median": round(lat[len(lat) // 2], 1) if lat else None,
+                                                         "p90": round(lat[int(len(lat) * 0.9)], 1) if lat else None}})
+    print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
