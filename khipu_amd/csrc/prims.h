@@ -481,12 +481,25 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_pass(const K* keys, const uin
 // are latency-bound at these sizes.
 constexpr int RS_SMALL_ITEMS = 4;
 constexpr uint64_t RS_SMALL_N = 65536;
-inline uint64_t radix_tiles(uint64_t n) {
-  const uint64_t tile = n <= RS_SMALL_N ? (uint64_t)RS_THREADS * RS_SMALL_ITEMS : (uint64_t)RS_TILE;
+// Large sorts (from RS_BIG_N keys: a full build's) take RS_BIG_ITEMS keys per thread: with the
+// one-sweep passes fewer, longer tiles publish and look back less and store longer digit runs
+// (100M: the 4 passes 3.40 -> 3.00 ms with 8192-key tiles, profiles/r6k_radix_tile_ab_100m.json)
+// at 2 waves per SIMD; below RS_BIG_N they would leave CUs without a tile.
+#ifndef KHST_RS_BIG_ITEMS
+#define KHST_RS_BIG_ITEMS 32
+#endif
+constexpr int RS_BIG_ITEMS = KHST_RS_BIG_ITEMS;
+constexpr uint64_t RS_BIG_N = 1ull << 22;
+// (the big tiles for 32-bit keys only: 64-bit ones would hold 101 KB of LDS a block)
+inline int radix_items(uint64_t n, size_t key_bytes) {
+  return n <= RS_SMALL_N ? RS_SMALL_ITEMS : (n >= RS_BIG_N && key_bytes == 4) ? RS_BIG_ITEMS : RS_ITEMS;
+}
+inline uint64_t radix_tiles(uint64_t n, size_t key_bytes) {
+  const uint64_t tile = (uint64_t)RS_THREADS * (uint64_t)radix_items(n, key_bytes);
   return (n + tile - 1) / tile;
 }
-inline size_t radix_scratch_bytes(uint64_t n) {
-  return RS_HDR_PAD + 2 * radix_tiles(n) * 256 * sizeof(unsigned long long) + 256;
+inline size_t radix_scratch_bytes(uint64_t n) {  // (64-bit keys: the most tiles)
+  return RS_HDR_PAD + 2 * radix_tiles(n, 8) * 256 * sizeof(unsigned long long) + 256;
 }
 
 // Sorts (k0, v0) on bits [lo_bit, hi_bit) (multiples of 8, at most 64 bits), using (k1, v1)
@@ -496,8 +509,8 @@ template <typename K>
 inline bool radix_sort_pairs(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n, int lo_bit, int hi_bit,
                              void* scratch, hipStream_t st) {
   if (n <= 1 || hi_bit <= lo_bit) return false;
-  const bool small = n <= RS_SMALL_N;
-  const uint64_t tiles = radix_tiles(n);
+  const int items = radix_items(n, sizeof(K));
+  const uint64_t tiles = radix_tiles(n, sizeof(K));
   const int npass = (hi_bit - lo_bit + 7) / 8;
   uint32_t* ghist = (uint32_t*)scratch;
   uint32_t* ticket = ghist + RS_MAX_PASSES * 256;
@@ -505,7 +518,8 @@ inline bool radix_sort_pairs(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t 
   stat[1] = stat[0] + tiles * 256;
   (void)hipMemsetAsync(ghist, 0, RS_HDR_BYTES, st);
   const unsigned hgrid = (unsigned)(tiles < 1024 ? tiles : 1024);
-  if (small)
+  // (the digit count's tile is only its loop step: large sorts take RS_ITEMS keys per thread)
+  if (items == RS_SMALL_ITEMS)
     hipLaunchKernelGGL((k_rs_hist_all<K, RS_SMALL_ITEMS>), dim3(hgrid), dim3(RS_THREADS), 0, st, (const K*)k0, n,
                        lo_bit, npass, ghist, stat[0], tiles * 256);
   else
@@ -518,8 +532,12 @@ inline bool radix_sort_pairs(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t 
     K* ok = flip ? k0 : k1;
     uint32_t* ov = flip ? v0 : v1;
     unsigned long long* nxt = p + 1 < npass ? stat[(p + 1) & 1] : nullptr;
-    if (small)
+    if (items == RS_SMALL_ITEMS)
       hipLaunchKernelGGL((k_rs_pass<K, RS_SMALL_ITEMS>), dim3((unsigned)tiles), dim3(RS_THREADS), 0, st, (const K*)ik,
+                         (const uint32_t*)iv, ok, ov, n, lo_bit + 8 * p, (const uint32_t*)(ghist + 256 * p), stat[p & 1],
+                         nxt, ticket + p);
+    else if (sizeof(K) == 4 && items == RS_BIG_ITEMS)
+      hipLaunchKernelGGL((k_rs_pass<K, sizeof(K) == 4 ? RS_BIG_ITEMS : RS_ITEMS>), dim3((unsigned)tiles), dim3(RS_THREADS), 0, st, (const K*)ik,
                          (const uint32_t*)iv, ok, ov, n, lo_bit + 8 * p, (const uint32_t*)(ghist + 256 * p), stat[p & 1],
                          nxt, ticket + p);
     else
