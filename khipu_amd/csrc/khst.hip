@@ -310,8 +310,11 @@ __device__ __forceinline__ bool tie_run_start(const uint32_t* ck, uint64_t n, ui
 // on a run's dependent key reads instead of nearly every wave (one thread per position).  A global list with one atomic per wave was
 // measured far slower (a single contended counter: +9 ms at 100M).
 constexpr int TF_ITEMS = 4;
+// full_u (unsegmented words): the boundaries between different words are valued here too
+// (lcp_value's rule from the words alone), so k_lcp does not read the words again
 __global__ void __launch_bounds__(BS) k_tie_fix_ck_blk(uint32_t* ck, uint32_t* idx, uint64_t n, const uint64_t* K,
-                                                       unsigned long long* flags, uint8_t* u, uint32_t depth0) {
+                                                       unsigned long long* flags, uint8_t* u, uint32_t depth0,
+                                                       bool full_u) {
   __shared__ uint32_t list[TF_ITEMS * BS];
   __shared__ uint32_t cnt;
   if (threadIdx.x == 0) cnt = 0;
@@ -320,7 +323,14 @@ __global__ void __launch_bounds__(BS) k_tie_fix_ck_blk(uint32_t* ck, uint32_t* i
 #pragma unroll
   for (int q = 0; q < TF_ITEMS; ++q) {
     const uint64_t i = base + (uint64_t)q * BS + threadIdx.x;
-    if (tie_run_start(ck, n, i)) list[atomicAdd(&cnt, 1u)] = (uint32_t)(i - base);
+    if (i + 1 >= n) continue;
+    const uint32_t a = ck[i], c = ck[i + 1];
+    if (a == c) {
+      if (!(i > 0 && ck[i - 1] == a)) list[atomicAdd(&cnt, 1u)] = (uint32_t)(i - base);
+    } else if (full_u) {
+      const int l = (int)((uint32_t)clz64((uint64_t)(a ^ c) << 32) >> 2);
+      u[i] = (l < (int)depth0 || l > 63) ? 0 : (uint8_t)(l + 1);
+    }
   }
   __syncthreads();
   const uint32_t nr = cnt;
@@ -450,6 +460,13 @@ __global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb, bool ties_u, co
     return;
   }
   op_lcp(T, b);
+}
+// every boundary was valued by the tie kernel: only a run too long for it (flag bit 0: a
+// speculative build about to be redone) gets its boundaries cleared, as in k_lcp
+__global__ void __launch_bounds__(BS) k_lcp_long_runs(Topo T, uint64_t nb, const unsigned long long* tie) {
+  if (!(*tie & 1)) return;
+  for (uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * BS)
+    if (T.sck[b] == T.sck[b + 1]) T.u[b] = 0;
 }
 // the 64-ary min pyramid over the boundary values: level `from` by the whole grid, the
 // (small) upper levels by the last block to finish (the counter *done starts at zero;
@@ -1874,6 +1891,7 @@ struct SortIO {
   uint32_t depth0 = 0;
   const uint32_t* sck = nullptr;  // ck_path: the sorted 32-bit key prefixes (skey not gathered)
   bool ties_u = false;            // u holds the tie runs' boundaries (k_lcp skips them)
+  bool all_u = false;             // u holds every boundary (k_lcp only clears a too-long run's)
   uint64_t m;
   uint32_t* sidx;
   bool fallback;
@@ -1911,8 +1929,9 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
     const bool flip = radix_sort_pairs<uint32_t>(c0, idx0, c1, idx1, n, 0, 32, rs_scratch, st);
     uint32_t* c32 = flip ? c1 : c0;
     idxs = flip ? idx1 : idx0;
+    const bool full_u = S.u && !segmented;
     hipLaunchKernelGGL(k_tie_fix_ck_blk, GRID(n, TF_ITEMS * BS), dim3(BS), 0, st, c32, idxs, n,
-                       (const uint64_t*)K32, T.ctr + CTR_TIE, S.u, S.depth0);
+                       (const uint64_t*)K32, T.ctr + CTR_TIE, S.u, S.depth0, full_u);
     LAUNCH_CHECK();
     uint64_t tf = 0;
     if (!S.speculate) {
@@ -1954,6 +1973,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
       S.sseg = sseg;
       S.fallback = false;
       S.ties_u = S.u && m == n;  // no dedup: the run boundaries' values stand
+      S.all_u = S.ties_u && full_u;  // and every other boundary's
       return;
     }
   }
@@ -2257,7 +2277,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   uint64_t m = n;
   uint32_t* sidx = nullptr;
   bool fallback = false;
-  bool ties_u = false;
+  bool ties_u = false, all_u = false;
   {
     SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr,
              A.kn, ck_ready};
@@ -2274,6 +2294,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     T.sck = S.sck;  // non-null: no sorted keys materialised (trie_ops.h sorted_key)
     T.ck_sb = S.sck ? sb : 0;
     ties_u = S.ties_u;
+    all_u = S.all_u;
   }
   const bool ties = fallback;
   T.m = m;
@@ -2357,8 +2378,12 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));  // every leaf a hash unless it says otherwise
   }
   if (nb > 0) {
-    hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb, ties_u,
-                       (const unsigned long long*)(ctr + CTR_TIE));
+    if (all_u)
+      hipLaunchKernelGGL(k_lcp_long_runs, dim3((unsigned)std::min<uint64_t>((nb + BS - 1) / BS, 1024)), dim3(BS), 0, st,
+                         T, nb, (const unsigned long long*)(ctr + CTR_TIE));
+    else
+      hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb, ties_u,
+                         (const unsigned long long*)(ctr + CTR_TIE));
     LAUNCH_CHECK();
   }
   auto launch_leaves = [&](bool scatter) {  // on st2, after everything enqueued on st so far
