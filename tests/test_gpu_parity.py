@@ -383,6 +383,22 @@ def test_branch_levels_vs_oracle(khst, oracle):
     assert hh[0].tobytes() == roots[0] and st.n_node_perms == bst["node_perms"], variant
 
 
+def test_radix_tile_thresholds(khst, oracle):
+    """The radix sort's tile size changes with n (prims.h radix_items: 1024-key tiles up to
+    65,536 keys, 4096 above, 8192 for 32-bit words from 4,194,304 keys): hashed-key builds one
+    key either side of both thresholds, with the one-sweep passes' look-back over many tiles;
+    roots and node counts equal the CPU batch builder's."""
+    from khipu_amd.device import Ctx
+    ctx = Ctx(0)
+    for n in (65_535, 65_536, 65_537, (1 << 22) - 1, 1 << 22, (1 << 22) + 1):
+        (hh, _, _, st), (addr, vals, voff) = _device_synth_root(ctx, n, cfg=5)
+        a = addr[:20 * n].cpu().numpy()
+        vo = voff[:n + 1].cpu().numpy().astype(np.uint64)
+        roots, bst = oracle.batch_roots(a, (vals[:int(vo[-1])].cpu().numpy(), vo), klen=20, hash_keys=True)
+        assert hh[0].tobytes() == roots[0], n
+        assert (bst["leaves"], bst["node_hashes"]) == (st.n_leaves, st.n_node_hashes), n
+
+
 def test_tie_runs_across_blocks(khst, oracle):
     """Many runs of equal 32-bit sort prefixes (2..64 keys each, some spanning the tie
     kernel's 1,024-position blocks), raw 32-byte keys: the runs are ordered by the whole
