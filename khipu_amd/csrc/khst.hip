@@ -210,15 +210,17 @@ __device__ __forceinline__ bool key_less(const uint64_t* a, const uint64_t* b, u
   }
   return kna < knb;
 }
+// (tsh: the composite prefixes were sorted on their bits from tsh up; a run is equal there)
 __global__ void __launch_bounds__(BS) k_tie_fix(const uint64_t* ck, uint64_t n, uint64_t* skey, uint32_t* sidx,
-                                                uint32_t* sseg, const uint8_t* kn, unsigned long long* flags) {
+                                                uint32_t* sseg, const uint8_t* kn, unsigned long long* flags,
+                                                uint32_t tsh) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i + 1 >= n) return;
-  uint32_t hi = (uint32_t)(ck[i] >> 32);
-  if ((uint32_t)(ck[i + 1] >> 32) != hi) return;   // no run starting or continuing here
-  if (i > 0 && (uint32_t)(ck[i - 1] >> 32) == hi) return;  // not the run's first element
+  const uint64_t hi = ck[i] >> tsh;
+  if ((ck[i + 1] >> tsh) != hi) return;   // no run starting or continuing here
+  if (i > 0 && (ck[i - 1] >> tsh) == hi) return;  // not the run's first element
   uint64_t e = i + 1;
-  while (e < n && (uint32_t)(ck[e] >> 32) == hi && e - i <= TIE_RUN_MAX) ++e;
+  while (e < n && (ck[e] >> tsh) == hi && e - i <= TIE_RUN_MAX) ++e;
   if (e - i > TIE_RUN_MAX) {
     atomicOr(flags, 1ULL);
     return;
@@ -1879,6 +1881,9 @@ struct SortIO {
   const uint8_t* kn;  // variable-length keys: nibble counts (input order; nullable)
   bool ck_ready = false;  // ck_path: ck0/idx0 already hold the 32-bit sort keys (k_hash_keys_ck)
   bool ck_path = false;   // unsegmented plain build: sort (32-bit prefix, idx) only, never gather the keys
+  // 64-bit composite path: the radix range is bits [rs_lo, 64) -- 40 (the leading 24 bits) where
+  // keys are few per segment, the tie kernel then orders the runs of equal leading 24 bits
+  int rs_lo = 32;
   // a device word copied to the host with the first sync's flags (c->h_pinned[1]): the
   // caller's check of earlier stream work, read without a sync of its own (nullable)
   const unsigned long long* chk = nullptr;
@@ -1988,7 +1993,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
                          T.ctr + CTR_TIE);
       LAUNCH_CHECK();
     }
-    bool flip = radix_sort_pairs<uint64_t>(ck0, idx0, ck1, idx1, n, 32, 64, rs_scratch, st);
+    bool flip = radix_sort_pairs<uint64_t>(ck0, idx0, ck1, idx1, n, S.rs_lo, 64, rs_scratch, st);
     cks = flip ? ck1 : ck0;
     idxs = flip ? idx1 : idx0;
     LAUNCH_CHECK();
@@ -1996,7 +2001,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
                        skey, sseg);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_tie_fix, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, n, skey, idxs, sseg, S.kn,
-                       T.ctr + CTR_TIE);
+                       T.ctr + CTR_TIE, (uint32_t)S.rs_lo);
     LAUNCH_CHECK();
     HIPCHK(hipMemcpyAsync(c->h_pinned + 2, T.ctr + CTR_NDUP, 16, hipMemcpyDeviceToHost, st));  // [2] dups, [3] flags
     if (S.chk) HIPCHK(hipMemcpyAsync(c->h_pinned + 1, S.chk, 8, hipMemcpyDeviceToHost, st));
@@ -2011,6 +2016,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
       HIPCHK(hipMemsetAsync(T.ctr + CTR_NDUP, 0, 16, st));
       sbu = 32;
       S.sb = 32;
+      S.rs_lo = 32;  // (the segment id alone fills the leading 32 bits)
       sort_prefix();
     }
   }
@@ -2282,6 +2288,9 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr,
              A.kn, ck_ready};
     S.ck_path = ck_path;
+    // element builds (hashed paths, few per segment): the leading 24 composite bits suffice
+    if (A.el && !A.kn && sb <= 18 && (segmented ? n / A.nseg : n) <= (1ull << (19 - (segmented ? sb : 0))))
+      S.rs_lo = 40;
     S.speculate = spec;
     S.u = T.u;
     S.depth0 = A.depth0;
@@ -3819,6 +3828,9 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   // redone with 32 if an id needs more), so the sorted 32-bit prefix holds key bits too and
   // runs of equal prefixes (one per trie with all 32) stay short
   S.sb = segd ? (h->tid_bits ? std::max(h->tid_bits, 1u) : 32u) : 0;
+  // keccak'd keys, a few ops per trie: the leading 24 composite bits (the tie kernel orders the
+  // rare runs past them; 2^17 ops over the 2^(sb - 2) tries the hint allows, 2^19 in one trie)
+  if (S.sb <= 18 && nops <= (segd ? (1ull << 17) : (1ull << 19))) S.rs_lo = 40;
   S.rs_scratch = cv.take<char>(radix_scratch_bytes(nops));
   S.scan_scratch = cv.take<char>(scan_scratch_bytes(nops + 1, 8));
   S.ctr = cv.take<unsigned long long>(CTR_N);
