@@ -271,11 +271,13 @@ __device__ __forceinline__ bool ck_equal(uint32_t a, uint32_t b, const uint64_t*
 // the run of equal prefixes starting at i (ck[i] == ck[i + 1], i the run's first)
 // u (nullable): also the boundary values inside the run, from the whole keys (k_lcp then
 // skips boundaries between equal prefixes unless a dedup shifts the positions)
+// (tsh 8: the words were sorted on their top 24 bits only; a run is equal there, its boundaries
+// between different words valued here too -- from the whole keys, as lcp_value would)
 __device__ void tie_run_ck(uint32_t* ck, uint32_t* idx, uint64_t n, const uint64_t* K, unsigned long long* flags,
-                           uint64_t i, uint8_t* u = nullptr, uint32_t depth0 = 0) {
-  const uint32_t hi = ck[i];
+                           uint64_t i, uint8_t* u = nullptr, uint32_t depth0 = 0, uint32_t tsh = 0) {
+  const uint32_t hi = ck[i] >> tsh;
   uint64_t e = i + 1;
-  while (e < n && ck[e] == hi && e - i <= TIE_RUN_MAX) ++e;
+  while (e < n && (ck[e] >> tsh) == hi && e - i <= TIE_RUN_MAX) ++e;
   if (e - i > TIE_RUN_MAX) {
     atomicOr(flags, 1ULL);
     return;
@@ -316,7 +318,7 @@ constexpr int TF_ITEMS = 4;
 // (lcp_value's rule from the words alone), so k_lcp does not read the words again
 __global__ void __launch_bounds__(BS) k_tie_fix_ck_blk(uint32_t* ck, uint32_t* idx, uint64_t n, const uint64_t* K,
                                                        unsigned long long* flags, uint8_t* u, uint32_t depth0,
-                                                       bool full_u) {
+                                                       bool full_u, uint32_t tsh) {
   __shared__ uint32_t list[TF_ITEMS * BS];
   __shared__ uint32_t cnt;
   if (threadIdx.x == 0) cnt = 0;
@@ -327,8 +329,8 @@ __global__ void __launch_bounds__(BS) k_tie_fix_ck_blk(uint32_t* ck, uint32_t* i
     const uint64_t i = base + (uint64_t)q * BS + threadIdx.x;
     if (i + 1 >= n) continue;
     const uint32_t a = ck[i], c = ck[i + 1];
-    if (a == c) {
-      if (!(i > 0 && ck[i - 1] == a)) list[atomicAdd(&cnt, 1u)] = (uint32_t)(i - base);
+    if ((a >> tsh) == (c >> tsh)) {
+      if (!(i > 0 && (ck[i - 1] >> tsh) == (a >> tsh))) list[atomicAdd(&cnt, 1u)] = (uint32_t)(i - base);
     } else if (full_u) {
       const int l = (int)((uint32_t)clz64((uint64_t)(a ^ c) << 32) >> 2);
       u[i] = (l < (int)depth0 || l > 63) ? 0 : (uint8_t)(l + 1);
@@ -336,7 +338,7 @@ __global__ void __launch_bounds__(BS) k_tie_fix_ck_blk(uint32_t* ck, uint32_t* i
   }
   __syncthreads();
   const uint32_t nr = cnt;
-  for (uint32_t t = threadIdx.x; t < nr; t += BS) tie_run_ck(ck, idx, n, K, flags, base + list[t], u, depth0);
+  for (uint32_t t = threadIdx.x; t < nr; t += BS) tie_run_ck(ck, idx, n, K, flags, base + list[t], u, depth0, tsh);
 }
 
 __global__ void __launch_bounds__(BS) k_dup_ck(const uint32_t* ck, const uint32_t* idx, const uint64_t* K, uint64_t n,
@@ -465,10 +467,11 @@ __global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb, bool ties_u, co
 }
 // every boundary was valued by the tie kernel: only a run too long for it (flag bit 0: a
 // speculative build about to be redone) gets its boundaries cleared, as in k_lcp
-__global__ void __launch_bounds__(BS) k_lcp_long_runs(Topo T, uint64_t nb, const unsigned long long* tie) {
+__global__ void __launch_bounds__(BS) k_lcp_long_runs(Topo T, uint64_t nb, const unsigned long long* tie,
+                                                      uint32_t tsh) {
   if (!(*tie & 1)) return;
   for (uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * BS)
-    if (T.sck[b] == T.sck[b + 1]) T.u[b] = 0;
+    if ((T.sck[b] >> tsh) == (T.sck[b + 1] >> tsh)) T.u[b] = 0;
 }
 // the 64-ary min pyramid over the boundary values: level `from` by the whole grid, the
 // (small) upper levels by the last block to finish (the counter *done starts at zero;
@@ -1884,6 +1887,9 @@ struct SortIO {
   // 64-bit composite path: the radix range is bits [rs_lo, 64) -- 40 (the leading 24 bits) where
   // keys are few per segment, the tie kernel then orders the runs of equal leading 24 bits
   int rs_lo = 32;
+  // ck path: the words are sorted on their bits from tsh up (8: hashed keys, few enough that
+  // runs of equal top-24 bits stay rare; the tie kernel orders them)
+  uint32_t tsh = 0;
   // a device word copied to the host with the first sync's flags (c->h_pinned[1]): the
   // caller's check of earlier stream work, read without a sync of its own (nullable)
   const unsigned long long* chk = nullptr;
@@ -1931,12 +1937,12 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
       hipLaunchKernelGGL(k_make_ck32, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, n, c0, idx0, seg, sb);
       LAUNCH_CHECK();
     }
-    const bool flip = radix_sort_pairs<uint32_t>(c0, idx0, c1, idx1, n, 0, 32, rs_scratch, st);
+    const bool flip = radix_sort_pairs<uint32_t>(c0, idx0, c1, idx1, n, S.tsh, 32, rs_scratch, st);
     uint32_t* c32 = flip ? c1 : c0;
     idxs = flip ? idx1 : idx0;
     const bool full_u = S.u && !segmented;
     hipLaunchKernelGGL(k_tie_fix_ck_blk, GRID(n, TF_ITEMS * BS), dim3(BS), 0, st, c32, idxs, n,
-                       (const uint64_t*)K32, T.ctr + CTR_TIE, S.u, S.depth0, full_u);
+                       (const uint64_t*)K32, T.ctr + CTR_TIE, S.u, S.depth0, full_u, S.tsh);
     LAUNCH_CHECK();
     uint64_t tf = 0;
     if (!S.speculate) {
@@ -2257,6 +2263,9 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   const bool seg_words_ok = segmented && sb + CK_KEY_BITS <= 32 && (n / A.nseg) <= (1ULL << (32 - sb - 2));
   const bool ck_path = early && !A.kn && (!segmented || seg_words_ok);
   const bool ck_ready = ck_path && (A.flags & KH_HASH_KEYS);
+  // hashed keys of an unsegmented build up to 2^20 (a run of equal top-24 bits every 32 keys at
+  // most): the words' lowest 8 bits are left to the tie kernel -- one radix pass less
+  const uint32_t tsh = ck_ready && !segmented && n <= (1ull << 20) ? 8u : 0u;
   if (ck_ready) {
     uint32_t* c0 = (uint32_t*)ck0;
     if (A.klen <= 135)
@@ -2288,6 +2297,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     SortIO S{(const uint64_t*)K32, A.seg, sb, n, ck0, ck1, idx0, idx1, skey, sseg, rs_scratch, scan_scratch, T.ctr,
              A.kn, ck_ready};
     S.ck_path = ck_path;
+    S.tsh = tsh;
     // element builds (hashed paths, few per segment): the leading 24 composite bits suffice
     if (A.el && !A.kn && sb <= 18 && (segmented ? n / A.nseg : n) <= (1ull << (19 - (segmented ? sb : 0))))
       S.rs_lo = 40;
@@ -2389,7 +2399,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   if (nb > 0) {
     if (all_u)
       hipLaunchKernelGGL(k_lcp_long_runs, dim3((unsigned)std::min<uint64_t>((nb + BS - 1) / BS, 1024)), dim3(BS), 0, st,
-                         T, nb, (const unsigned long long*)(ctr + CTR_TIE));
+                         T, nb, (const unsigned long long*)(ctr + CTR_TIE), tsh);
     else
       hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb, ties_u,
                          (const unsigned long long*)(ctr + CTR_TIE));
