@@ -546,6 +546,17 @@ __global__ void __launch_bounds__(TT_THREADS) k_topo_tile(Topo T, uint64_t nb, b
   __shared__ uint64_t amask[TOPO_TILE / 64], cmask[TOPO_TILE / 64];
   const uint64_t t0 = (uint64_t)blockIdx.x * TOPO_TILE;
   const uint32_t tn = (uint32_t)(nb - t0 < TOPO_TILE ? nb - t0 : TOPO_TILE);
+  // the presets two fills wrote before this kernel (a fill launch each on the critical path):
+  // glast 1 over the tile's boundaries (whole 16-byte words; this block's phase 1 clears some,
+  // after the barrier below), lf_emeta 32 over its sorted leaves (the last tile: through m - 1)
+  {
+    const uint64_t gend = t0 + ((tn + 15) & ~15u);
+    const uint64_t lend = blockIdx.x + 1 == gridDim.x ? (pd ? T.m : t0) : t0 + TOPO_TILE;
+    const ulonglong2 ones{0x0101010101010101ULL, 0x0101010101010101ULL};
+    for (uint64_t o = t0 + 16 * threadIdx.x; o < gend; o += 16 * TT_THREADS) *(ulonglong2*)(T.glast + o) = ones;
+    if (pd)
+      for (uint64_t o = t0 + threadIdx.x; o < lend; o += TT_THREADS) T.lf_emeta[o] = 32;
+  }
   for (uint32_t w = threadIdx.x; w < TOPO_TILE / 16; w += TT_THREADS) {
     const uint32_t o = 16 * w;
     if (o + 16 <= tn) {
@@ -2394,7 +2405,8 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   const bool topo_tile = nb >= TOPO_TILE_MIN;
   if (pd_scan) {  // presets for the scatter folded into the ANSV (on st)
     if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, st));  // dropped duplicates: PDINV_SKIP
-    HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));  // every leaf a hash unless it says otherwise
+    // every leaf a hash unless it says otherwise (k_topo_tile presets its own tile's leaves)
+    if (!topo_tile) HIPCHK(hipMemsetAsync(T.lf_emeta, 32, m, st));
   }
   if (nb > 0) {
     if (all_u)
@@ -2452,7 +2464,8 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
         LAUNCH_CHECK();
       }
     };
-    HIPCHK(hipMemsetAsync(T.glast, 1, (nb + 15) & ~(uint64_t)15, st));  // (whole 16-byte words: one fill kernel)
+    // (k_topo_tile presets its own tile's boundaries)
+    if (!topo_tile) HIPCHK(hipMemsetAsync(T.glast, 1, (nb + 15) & ~(uint64_t)15, st));  // (whole 16-byte words)
     if (topo_tile) {
       // ANSV and chains tile by tile in LDS (k_topo_tile, the early leaves' parent depths with
       // them); the leaves start right after it; the few boundaries whose answers leave their
