@@ -2520,8 +2520,13 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     hipLaunchKernelGGL(k_branch_permute, topo_grid(nb), dim3(BS), 0, st, T, J, (const uint32_t*)order,
                        (const uint32_t*)Bp);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_bid_remap, topo_grid(nb), dim3(BS), 0, st, T, (const uint32_t*)order, nb);
-    LAUNCH_CHECK();
+    if (lpos) {  // (only the few long and top leaves resolve a parent later: through the order itself,
+                 // not a 100M-boundary remap pass beside the leaf kernel)
+      T.bid_pos = order;
+    } else {
+      hipLaunchKernelGGL(k_bid_remap, topo_grid(nb), dim3(BS), 0, st, T, (const uint32_t*)order, nb);
+      LAUNCH_CHECK();
+    }
     // child record bases
     scan_exclusive<uint32_t>(T.br_k, T.br_cbase, nb, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
   }

@@ -171,6 +171,7 @@ struct Topo {
   uint32_t* rep;          // [m-1] group representative of b
   uint8_t* ord;           // [m-1] ordinal of b within its group
   uint32_t* isrep_bid;     // [m-1] 1 if rep, then (after scan) branch id of rep
+  const uint32_t* bid_pos;  // nullable: isrep_bid holds key-order ids, their level positions (leaf-position builds skip k_bid_remap)
   uint8_t* glast;         // [nb] 1 unless a later boundary of the same group exists (preset 1)
   uint8_t* gk;            // [nb] at a group's representative: its branch's child count
   // branches (B <= m-1)
@@ -641,8 +642,12 @@ KH_HD Parent resolve_parent(const Topo& T, int64_t a, int64_t c) {
   const uint32_t va = a >= 0 ? T.u[a] : 0, vc = c >= 0 ? T.u[c] : 0;
   const uint32_t ra = a >= 0 ? T.rep[a] : NONE, rc = c >= 0 ? T.rep[c] : NONE;
   const uint32_t oa = a >= 0 ? T.ord[a] : 0, oc = c >= 0 ? T.ord[c] : 0;
-  const uint32_t ba = (va && ra != NONE) ? T.isrep_bid[ra] : NONE;
-  const uint32_t bc = (vc && rc != NONE) ? T.isrep_bid[rc] : NONE;
+  uint32_t ba = (va && ra != NONE) ? T.isrep_bid[ra] : NONE;
+  uint32_t bc = (vc && rc != NONE) ? T.isrep_bid[rc] : NONE;
+  if (T.bid_pos) {
+    if (ba != NONE) ba = T.bid_pos[ba];
+    if (bc != NONE) bc = T.bid_pos[bc];
+  }
   Parent P;
   if (va == 0 && vc == 0) {
     P.bid = NONE;
