@@ -2516,7 +2516,6 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     hipLaunchKernelGGL(k_level_bounds, dim3(1), dim3(64), 0, st, (const uint32_t*)bcnt, nblk, (const uint32_t*)Bp,
                        lb);
     LAUNCH_CHECK();
-    HIPCHK(hipMemsetAsync(T.br_k, 0, (nb * 4 + 15) & ~(uint64_t)15, st));  // entries past B must scan as 0
     hipLaunchKernelGGL(k_branch_permute, topo_grid(nb), dim3(BS), 0, st, T, J, (const uint32_t*)order,
                        (const uint32_t*)Bp);
     LAUNCH_CHECK();
@@ -2527,8 +2526,10 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
       hipLaunchKernelGGL(k_bid_remap, topo_grid(nb), dim3(BS), 0, st, T, (const uint32_t*)order, nb);
       LAUNCH_CHECK();
     }
-    // child record bases
-    scan_exclusive<uint32_t>(T.br_k, T.br_cbase, nb, (uint32_t*)(ctr + CTR_C), scan_scratch, st);
+    // child record bases: the first B entries only (B from the device; no clearing of the
+    // entries past it, and a third of the 100M-entry scan's traffic beside the leaf kernel)
+    scan_exclusive<uint32_t>(T.br_k, T.br_cbase, nb, (uint32_t*)(ctr + CTR_C), scan_scratch, st, true,
+                             (const uint32_t*)Bp);
   }
   if (early && !lpos) {  // the leaves' slots, while they are still being hashed
     hipLaunchKernelGGL(k_leaf_link, topo_grid(m), dim3(BS), 0, st, T);

@@ -93,10 +93,17 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* lds_waves, T* total) {
   return wbase + x - v;
 }
 
+// n_dev (nullable): a device count that caps n (the entries past it are neither read nor
+// written; their tiles' sums are 0)
+__device__ __forceinline__ uint64_t scan_n(uint64_t n, const uint32_t* n_dev) {
+  return n_dev && (uint64_t)*n_dev < n ? (uint64_t)*n_dev : n;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const T* in, T* out, uint64_t n, T* tile_sums,
-                                                             T* last_in) {
+                                                             T* last_in, const uint32_t* n_dev) {
   topo_prio();
+  n = scan_n(n, n_dev);
   __shared__ T lw[SCAN_THREADS / 64];
   uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
   T v[SCAN_ITEMS];
@@ -118,18 +125,22 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_tiles(const T* in, T* out
 }
 
 template <typename T>
-__global__ void __launch_bounds__(SCAN_THREADS) k_scan_add(T* out, uint64_t n, const T* tile_off) {
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_add(T* out, uint64_t n, const T* tile_off,
+                                                           const uint32_t* n_dev) {
   topo_prio();
+  n = scan_n(n, n_dev);
   uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+  if (base >= n) return;
   T add = tile_off[blockIdx.x];
   for (int i = threadIdx.x; i < SCAN_TILE; i += SCAN_THREADS)
     if (base + i < n) out[base + i] += add;
 }
 
 template <typename T>
-__global__ void k_scan_total(const T* in_last, const T* out_last, T* total) {
+__global__ void k_scan_total(const T* in_last, const T* out, uint64_t n, T* total, const uint32_t* n_dev) {
   topo_prio();
-  *total = *in_last + *out_last;
+  n = scan_n(n, n_dev);
+  *total = n ? *in_last + out[n - 1] : (T)0;
 }
 
 // Small scans (a block commit's op and element counts): one block walks the tiles in order
@@ -234,8 +245,9 @@ __global__ void __launch_bounds__(SCAN_SMALL_THREADS) k_scan_small3(ScanJob a, S
 constexpr uint64_t SCAN_TWO_MAX_TILES = 2048;
 template <typename T>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_add_sums(T* out, uint64_t n, const T* sums, uint32_t tiles,
-                                                                T* total) {
+                                                                T* total, const uint32_t* n_dev) {
   topo_prio();
+  n = scan_n(n, n_dev);
   __shared__ T lw[SCAN_THREADS / 64];
   const uint32_t b = blockIdx.x;
   T s = 0;
@@ -268,13 +280,16 @@ inline size_t scan_scratch_bytes(uint64_t n, size_t elem) {
 // small_ok = false: never the one-block k_scan_small (the nested scan of a large scan's tile
 // sums, which may run beside the leaf kernel: a 1024-thread block waits for a whole CU to
 // drain there -- the topology stream of a 100M build lost 6 ms to it).
+// n_dev (nullable): a device-side count that caps n (a grid sized by the host's bound; the
+// entries past the count are neither read nor written).
 template <typename T>
-void scan_exclusive(const T* in, T* out, uint64_t n, T* total, void* scratch, hipStream_t st, bool small_ok = true) {
+void scan_exclusive(const T* in, T* out, uint64_t n, T* total, void* scratch, hipStream_t st, bool small_ok = true,
+                    const uint32_t* n_dev = nullptr) {
   if (n == 0) {
     if (total) (void)hipMemsetAsync(total, 0, sizeof(T), st);
     return;
   }
-  if (small_ok && n <= SCAN_SMALL_MAX) {
+  if (small_ok && !n_dev && n <= SCAN_SMALL_MAX) {
     hipLaunchKernelGGL(k_scan_small<T>, dim3(1), dim3(SCAN_SMALL_THREADS), 0, st, in, out, n, total);
     return;
   }
@@ -284,19 +299,21 @@ void scan_exclusive(const T* in, T* out, uint64_t n, T* total, void* scratch, hi
   T* last_in = sums + tiles;  // one slot after the tile sums
   if (tiles <= SCAN_TWO_MAX_TILES) {
     hipLaunchKernelGGL(k_scan_tiles<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, in, out, n, sums,
-                       (T*)nullptr);
+                       (T*)nullptr, n_dev);
     hipLaunchKernelGGL(k_scan_add_sums<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, out, n, (const T*)sums,
-                       (uint32_t)tiles, total);
+                       (uint32_t)tiles, total, n_dev);
     return;
   }
   hipLaunchKernelGGL(k_scan_tiles<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, in, out, n, sums,
-                     total ? last_in : (T*)nullptr);
+                     total ? last_in : (T*)nullptr, n_dev);
   if (tiles > 1) {
     char* next = (char*)scratch + (((tiles + 1) * sizeof(T) + 63) / 64) * 64 + 64;
     scan_exclusive<T>(sums, sums, tiles, (T*)nullptr, next, st, false);
-    hipLaunchKernelGGL(k_scan_add<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, out, n, (const T*)sums);
+    hipLaunchKernelGGL(k_scan_add<T>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, st, out, n, (const T*)sums,
+                       n_dev);
   }
-  if (total) hipLaunchKernelGGL(k_scan_total<T>, dim3(1), dim3(1), 0, st, (const T*)last_in, (const T*)(out + n - 1), total);
+  if (total)
+    hipLaunchKernelGGL(k_scan_total<T>, dim3(1), dim3(1), 0, st, (const T*)last_in, (const T*)out, n, total, n_dev);
 }
 
 // ---------------------------------------------------------------------------
