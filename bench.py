@@ -191,7 +191,9 @@ def host_path(addr, vals, voff, n, gpu_root, reps=2):
     best = min(times[1:])
     return {"ms": round(best * 1e3, 2), "ms_all": [round(t * 1e3, 2) for t in times], "h2d_bytes": int(h2d),
             "h2d_gb_per_s_if_all_copy": round(h2d / best / 1e9, 2), "state_root_match": True,
-            "note": "kh_trie_root over pageable host arrays (the JVM's direct buffers): PCIe staging + the build; "
+            "note": "kh_trie_root over pageable host arrays (the JVM's direct buffers): the library streams them "
+                    "through pinned 64-MB chunks behind the build (keys in parts as hashing starts, then offsets, "
+                    "values last, the leaves launched when they land); PCIe staging + the build on the wall clock; "
                     "not the bench value, whose inputs are already in HBM"}
 
 

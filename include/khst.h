@@ -66,6 +66,8 @@ extern "C" {
 /* flags */
 #define KH_HASH_KEYS 0x1u   /* trie key = kec256(input key) */
 #define KH_EMIT_NODES 0x2u  /* resident tries: keep each commit's write-back set (kh_trie_emit_nodes) */
+#define KH_SHARD_RCCL 0x4u  /* kh_trie_root_sharded: exchange over RCCL even when a device repeats (needs a
+                               communicator that accepts repeats, such as the tests' loopback) */
 typedef struct kh_ctx kh_ctx;
 #define KH_NO_TRIE 0xFFFFFFFFu  /* kh_block_commit: an account upsert without a storage trie */
 

@@ -19,6 +19,7 @@ KH_EINTERNAL = -5
 KH_ENOSPC = -6
 KH_HASH_KEYS = 0x1
 KH_EMIT_NODES = 0x2
+KH_SHARD_RCCL = 0x4  # kh_trie_root_sharded: the RCCL exchange even when a device repeats (tests' loopback)
 KH_NO_TRIE = 0xFFFFFFFF
 
 # every symbol include/khst.h declares

@@ -150,9 +150,11 @@ __device__ __forceinline__ uint32_t ck_word(uint64_t h0, const uint32_t* seg, ui
   return sb ? (seg[i] << (32 - sb)) | (kb >> sb) : kb;
 }
 template <bool SHORT>
-__global__ void __launch_bounds__(BS) KH_KEYS_WAVES k_hash_keys_ck(const uint8_t* keys, uint32_t klen, uint64_t n, uint64_t* out,
-                                                     uint32_t* ck, uint32_t* idx, const uint32_t* seg, uint32_t sb) {
-  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+__global__ void __launch_bounds__(BS) KH_KEYS_WAVES k_hash_keys_ck(const uint8_t* keys, uint32_t klen, uint64_t first,
+                                                                    uint64_t n, uint64_t* out, uint32_t* ck, uint32_t* idx,
+                                                                    const uint32_t* seg, uint32_t sb) {
+  // keys [first, n): one launch over all of them, or one per part of host inputs still arriving
+  uint64_t i = first + (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
   uint64_t h[4];
   if (SHORT)  // keys of <= 135 bytes (addresses, slot words): one block
@@ -936,7 +938,7 @@ __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
   for (uint64_t j = j0; j < jend && j - threadIdx.x % 64 < n; j += BS) {  // (wave-uniform: the wave's first input)
     const uint64_t jn = j + BS < jend ? j + BS : n;
     take(slot, j, pv, off, end);
-    if (jn - threadIdx.x % 64 < n) issue(slot ^ 1, jn);
+    if (j + BS < jend && jn - threadIdx.x % 64 < n) issue(slot ^ 1, jn);  // (wave-uniform: no next run past the block's)
     slot ^= 1;
     const bool live = pv != PDINV_SKIP;  // not an earlier put of a key put again later
     uint32_t in1 = 0, lb = 0;
@@ -1768,6 +1770,73 @@ struct Worker {
     if (th.joinable()) th.join();
   }
 };
+
+// Host memcpy into pinned staging on COPY_THREADS host threads (the caller and COPY_THREADS - 1
+// kept workers): a single thread copies pageable -> pinned at ~22 GB/s on the box, 4 threads at
+// ~80, 8 at ~113, against ~57 GB/s of PCIe (profiles/r8a_h2d_probe.jsonl).  One job at a time,
+// split into one part per thread, so a worker never mixes parts of two jobs.
+constexpr int COPY_THREADS = 8;
+class CopyPool {
+  std::vector<std::thread> th_;
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_;
+  uint8_t* dst_ = nullptr;
+  const uint8_t* src_ = nullptr;
+  size_t bytes_ = 0, part_ = 0;
+  uint64_t gen_ = 0;
+  int left_ = 0;
+  bool stop_ = false;
+  void part(int w) {
+    const size_t a = part_ * (size_t)w;
+    if (a < bytes_) memcpy(dst_ + a, src_ + a, std::min(part_, bytes_ - a));
+  }
+  void loop(int w) {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      lk.unlock();
+      part(w);
+      lk.lock();
+      if (--left_ == 0) done_.notify_all();
+    }
+  }
+
+ public:
+  void copy(void* dst, const void* src, size_t bytes) {
+    if (bytes < (8u << 20)) {  // (a small copy is not worth the hand-off)
+      memcpy(dst, src, bytes);
+      return;
+    }
+    std::lock_guard<std::mutex> jl(job_mu_);
+    std::unique_lock<std::mutex> lk(mu_);
+    for (int w = (int)th_.size() + 1; w < COPY_THREADS; ++w) th_.emplace_back([this, w] { loop(w); });
+    dst_ = (uint8_t*)dst;
+    src_ = (const uint8_t*)src;
+    bytes_ = bytes;
+    part_ = ((bytes + COPY_THREADS - 1) / COPY_THREADS + 4095) & ~(size_t)4095;
+    left_ = COPY_THREADS - 1;
+    ++gen_;
+    cv_.notify_all();
+    lk.unlock();
+    part(0);
+    lk.lock();
+    done_.wait(lk, [&] { return left_ == 0; });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+};
+static CopyPool g_copy_pool;
+constexpr int RING_SLOTS = 4;
+constexpr size_t RING_CHUNK = 64u << 20;  // 64 MB chunks: 56 GB/s end to end in the probe (32-128 MB alike)
 struct kh_ctx {
   int dev = 0;
   int n_cu = 256;  // compute units of the device
@@ -1802,6 +1871,64 @@ struct kh_ctx {
   uint64_t last_B = 0;
   uint64_t last_nres = 0;
   BuildInfo binfo;
+  // host-input staging (HostStage): a copy stream, a ring of pinned chunks with the event of
+  // each chunk's last DMA, the events the stager records (key parts, keys + offsets, values) and
+  // the thread that streams the inputs behind the build (created on first use)
+  hipStream_t cs = nullptr;
+  uint8_t* ring = nullptr;
+  hipEvent_t ring_ev[RING_SLOTS] = {};
+  bool ring_busy[RING_SLOTS] = {};
+  uint32_t ring_next = 0;
+  std::vector<hipEvent_t> part_ev;
+  std::unique_ptr<Worker> hworker;
+};
+
+// Host inputs (keys, value offsets, values of kh_trie_root / kh_trie_root_nodes /
+// kh_trie_open_host) streamed to HBM behind the build instead of before it: the library's
+// worker thread copies them through a ring of pinned 64-MB chunks (g_copy_pool's threads fill a
+// chunk, one DMA on c->cs sends it) in the order the build needs them -- the keys in parts
+// (an event each: key hashing starts on the first part while the others are in flight), then
+// the value offsets (rebased on the device, not in a host copy), then the values.  The build
+// waits for an event only where it first reads those bytes (the keys' parts at hashing, the
+// values at the leaves), and the host waits for the worker to have RECORDED an event before
+// enqueueing a wait on it (a wait on an unrecorded event would be a no-op).  Round 5 staged
+// everything serially before the build: pageable copies plus an 800-MB host rebase of the
+// offsets, 420 ms for 100M accounts (BENCH_r05 drop_in_host_path).
+struct HostStage {
+  kh_ctx* c;
+  std::mutex mu;
+  std::condition_variable cv;
+  uint32_t recorded = 0;  // events recorded: key parts [0, nkp), then keys + offsets (nkp), values (nkp + 1)
+  bool failed = false;
+  int code = KH_OK;
+  std::string msg;
+  uint32_t nkp = 0;
+  std::vector<uint64_t> kend;  // key part p covers inputs [kend[p-1], kend[p])
+  bool posted = false;
+  explicit HostStage(kh_ctx* cc) : c(cc) {}
+  HostStage(const HostStage&) = delete;
+  hipEvent_t ev(uint32_t p) const { return c->part_ev[p]; }
+  // host: block until event p is recorded (throws the stager's error)
+  void wait(uint32_t p) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return recorded > p || failed; });
+    if (recorded <= p) throw KhError{code, msg};
+  }
+  // host + stream: st waits for event p
+  void stream_wait(hipStream_t st, uint32_t p) {
+    wait(p);
+    HIPCHK(hipStreamWaitEvent(st, ev(p), 0));
+  }
+  void publish() {
+    std::lock_guard<std::mutex> lk(mu);
+    ++recorded;
+    cv.notify_all();
+  }
+  void join() {
+    if (posted) c->hworker->join();
+    posted = false;
+  }
+  ~HostStage() { join(); }  // the stager must be done with the staging buffers before the call returns
 };
 
 // ---------------------------------------------------------------------------
@@ -1826,6 +1953,7 @@ struct BuildArgs {
   bool no_spec = false;            // no speculative sort (SortIO::speculate): the retry of one that failed
   std::function<void()> before_leaves;  // element builds: called (host) right before the leaves are encoded
   std::function<bool()> late_ready;     // ... late values (ElemArgs::late) already on the device: one leaf pass
+  HostStage* hs = nullptr;  // host inputs still streaming in (keys in parts, values last; vals_ready unset)
 };
 // element build (forest.h): inputs are leaves and subtree elements; the capped reference
 // of every element node, branch and extension is kept for the forest's records
@@ -2277,15 +2405,23 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   // hashed keys of an unsegmented build up to 2^20 (a run of equal top-24 bits every 32 keys at
   // most): the words' lowest 8 bits are left to the tie kernel -- one radix pass less
   const uint32_t tsh = ck_ready && !segmented && n <= (1ull << 20) ? 8u : 0u;
+  // host inputs still arriving: the hashing of the plain path starts part by part as the keys
+  // land; every other path waits for all keys (and the value offsets)
+  if (A.hs && !ck_ready) A.hs->stream_wait(st, A.hs->nkp);
   if (ck_ready) {
     uint32_t* c0 = (uint32_t*)ck0;
-    if (A.klen <= 135)
-      hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, c0, idx0, A.seg,
-                         sb);
-    else
-      hipLaunchKernelGGL(k_hash_keys_ck<false>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32, c0, idx0, A.seg,
-                         sb);
-    LAUNCH_CHECK();
+    const uint32_t parts = A.hs ? A.hs->nkp : 1;
+    for (uint32_t p = 0; p < parts; ++p) {
+      const uint64_t a = A.hs && p ? A.hs->kend[p - 1] : 0, b = A.hs ? A.hs->kend[p] : n;
+      if (A.hs) A.hs->stream_wait(st, p);
+      if (A.klen <= 135)
+        hipLaunchKernelGGL(k_hash_keys_ck<true>, GRID(b - a, BS), dim3(BS), 0, st, A.keys, A.klen, a, b, K32, c0, idx0,
+                           A.seg, sb);
+      else
+        hipLaunchKernelGGL(k_hash_keys_ck<false>, GRID(b - a, BS), dim3(BS), 0, st, A.keys, A.klen, a, b, K32, c0, idx0,
+                           A.seg, sb);
+      LAUNCH_CHECK();
+    }
   } else if (A.flags & KH_HASH_KEYS) {
     if (A.klen <= 135)
       hipLaunchKernelGGL(k_hash_keys<true>, GRID(n, BS), dim3(BS), 0, st, A.keys, A.klen, n, K32);
@@ -2336,6 +2472,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     T.svlen = nullptr;
   } else {
     if (A.vals_ready) HIPCHK(hipStreamWaitEvent(st, A.vals_ready, 0));
+    if (A.hs) A.hs->stream_wait(st, A.hs->nkp + 1);
     if (!A.el) {  // (element builds gather their spans with the element properties below)
       hipLaunchKernelGGL(k_val_gather, GRID(m, BS), dim3(BS), 0, st, T);
       LAUNCH_CHECK();
@@ -2417,8 +2554,11 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
                          (const unsigned long long*)(ctr + CTR_TIE));
     LAUNCH_CHECK();
   }
-  auto launch_leaves = [&](bool scatter) {  // on st2, after everything enqueued on st so far
-    HIPCHK(hipEventRecord(c->ev[8], st));
+  // host inputs still arriving (A.hs): the leaf launch on st2 waits until the stager has recorded
+  // the values' event, so it is enqueued after the topology (which needs no values), behind the
+  // first host sync below
+  bool leaves_deferred = false;
+  auto start_leaves = [&](bool scatter) {  // on st2, after st's work up to ev[8]
     HIPCHK(hipStreamWaitEvent(c->st2, c->ev[8], 0));
     hipStream_t s2 = c->st2;
     if (scatter) {
@@ -2428,6 +2568,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
       LAUNCH_CHECK();
     }
     if (A.vals_ready) HIPCHK(hipStreamWaitEvent(s2, A.vals_ready, 0));  // the topology need not wait
+    if (A.hs) A.hs->stream_wait(s2, A.hs->nkp + 1);
     HIPCHK(hipEventRecord(c->ev[9], s2));
     {
       const uint64_t runs = (n + BS - 1) / BS;
@@ -2436,6 +2577,13 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     }
     LAUNCH_CHECK();
     HIPCHK(hipEventRecord(c->ev[10], s2));
+  };
+  auto launch_leaves = [&](bool scatter) {  // on st2, after everything enqueued on st so far
+    HIPCHK(hipEventRecord(c->ev[8], st));
+    if (A.hs && scatter == false)
+      leaves_deferred = true;
+    else
+      start_leaves(scatter);
   };
   if (early && !pd_scan) launch_leaves(true);
   if (nb > 0) {
@@ -2555,6 +2703,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     c->spec_off = 8;
     throw SpecRetry{};
   }
+  if (leaves_deferred) start_leaves(false);
   const uint64_t B = (uint32_t)hc[CTR_B];
   const uint64_t C = (uint32_t)hc[CTR_B + 3];
   if (hc[CTR_ERR]) throw KhError{KH_EINTERNAL, "topology invariant violated (group chain > 15)"};
@@ -2582,6 +2731,8 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     HIPCHK(hipStreamWaitEvent(st, c->ev[10], 0));
     HIPCHK(hipMemcpyAsync(c->h_pinned, ctr, (size_t)CTR_N * CTR_SHARDS * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (hc[CTR_ERR] == ERR_LEAF_TOPO)
+      throw KhError{KH_EINTERNAL, "leaf stage: a parent depth or sorted position out of range (corrupt topology)"};
   }
   const uint64_t lf_bytes = early ? hc[CTR_LONGB] : hc[CTR_B + 2];
   const uint64_t nlong = lpos ? hc[CTR_LONGN] : 0;
@@ -2854,6 +3005,94 @@ static Staged stage_inputs(kh_ctx* c, const uint8_t* keys, uint32_t klen, const 
   }
   HIPCHK(hipStreamSynchronize(st));  // `rel` and `seg` are host temporaries
   return Staged{(const uint8_t*)c->in_keys.p, (const uint8_t*)c->in_vals.p, (const uint64_t*)c->in_voff.p, dseg};
+}
+
+__global__ void __launch_bounds__(BS) k_voff_rebase(uint64_t* voff, uint64_t n, uint64_t v0) {
+  const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (i < n) voff[i] -= v0;
+}
+
+// bytes host src -> device dst through the context's pinned ring on c->cs (the stager thread)
+static void ring_h2d(kh_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t bytes) {
+  for (uint64_t off = 0; off < bytes; off += RING_CHUNK) {
+    const uint64_t b = std::min<uint64_t>(RING_CHUNK, bytes - off);
+    const uint32_t s = c->ring_next++ % RING_SLOTS;
+    if (c->ring_busy[s]) HIPCHK(hipEventSynchronize(c->ring_ev[s]));  // its last DMA has read the chunk
+    uint8_t* chunk = c->ring + (size_t)s * RING_CHUNK;
+    g_copy_pool.copy(chunk, src + off, b);
+    HIPCHK(hipMemcpyAsync(dst + off, chunk, b, hipMemcpyHostToDevice, c->cs));
+    HIPCHK(hipEventRecord(c->ring_ev[s], c->cs));
+    c->ring_busy[s] = true;
+  }
+}
+
+// Start streaming n host inputs (HostStage): returns the device buffers they land in; the build
+// takes H as BuildArgs::hs (or a forest commit its events) and the call's HostStage joins the
+// stager before the call returns.  Keys arrive in at most 64 parts.
+static Staged stage_host_async(kh_ctx* c, HostStage& H, const uint8_t* keys, uint32_t klen, const uint8_t* vals,
+                               const uint64_t* voff, uint64_t n) {
+  const uint64_t v0 = voff[0], vbytes = voff[n] - v0;
+  if (voff[n] < v0) throw KhError{KH_EINVAL, "voff not monotone"};
+  c->in_keys.ensure(n * klen + 64);
+  c->in_vals.ensure(vbytes + 64);
+  c->in_voff.ensure((n + 1) * 8 + 64);
+  if (!c->cs) HIPCHK(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
+  if (!c->ring) {
+    HIPCHK(hipHostMalloc((void**)&c->ring, (size_t)RING_SLOTS * RING_CHUNK, hipHostMallocDefault));
+    for (auto& e : c->ring_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  // the copy stream starts after whatever the build stream still has in flight on these buffers
+  HIPCHK(hipEventRecord(c->ev[6], c->st));
+  HIPCHK(hipStreamWaitEvent(c->cs, c->ev[6], 0));
+  // (parts of 1/64 of the keys, at least 64k: a 100M build hashes 1.56M keys a launch as they land)
+  const uint64_t per = std::max<uint64_t>((n + 63) / 64, 65536);
+  for (uint64_t e = per; ; e += per) {
+    H.kend.push_back(std::min(e, n));
+    if (e >= n) break;
+  }
+  H.nkp = (uint32_t)H.kend.size();
+  while (c->part_ev.size() < H.nkp + 2) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->part_ev.push_back(e);
+  }
+  if (!c->hworker) c->hworker.reset(new Worker());
+  uint8_t* dk = (uint8_t*)c->in_keys.p;
+  uint8_t* dv = (uint8_t*)c->in_vals.p;
+  uint64_t* doff = (uint64_t*)c->in_voff.p;
+  H.posted = true;
+  c->hworker->post([c, &H, keys, klen, vals, voff, n, v0, vbytes, dk, dv, doff] {
+    try {
+      HIPCHK(hipSetDevice(c->dev));
+      for (uint32_t p = 0; p < H.nkp; ++p) {
+        const uint64_t a = p ? H.kend[p - 1] : 0;
+        ring_h2d(c, dk + a * klen, keys + a * klen, (H.kend[p] - a) * klen);
+        HIPCHK(hipEventRecord(H.ev(p), c->cs));
+        H.publish();
+      }
+      ring_h2d(c, (uint8_t*)doff, (const uint8_t*)voff, (n + 1) * 8);
+      if (v0) hipLaunchKernelGGL(k_voff_rebase, GRID(n + 1, BS), dim3(BS), 0, c->cs, doff, n + 1, v0);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(H.ev(H.nkp), c->cs));
+      H.publish();
+      ring_h2d(c, dv, vals + v0, vbytes);
+      HIPCHK(hipEventRecord(H.ev(H.nkp + 1), c->cs));
+      H.publish();
+    } catch (KhError& e) {
+      std::lock_guard<std::mutex> lk(H.mu);
+      H.failed = true;
+      H.code = e.code;
+      H.msg = e.msg;
+      H.cv.notify_all();
+    } catch (std::exception& e) {
+      std::lock_guard<std::mutex> lk(H.mu);
+      H.failed = true;
+      H.code = KH_EINTERNAL;
+      H.msg = e.what();
+      H.cv.notify_all();
+    }
+  });
+  return Staged{dk, dv, doff, nullptr};
 }
 
 // list-trie keys: key of item i of its trie = RLP of the integer index
@@ -3459,6 +3698,7 @@ struct kh_trie {
   uint32_t flags = 0;  // KH_HASH_KEYS: the trie's key encoder; KH_EMIT_NODES: keep each commit's write-back set
   bool forest = false;
   uint32_t tid_bits = 0;  // forests: bits of the trie ids committed so far (+ headroom; 0: none yet)
+  uint32_t lo24_off = 0;  // commits left without the 24-bit op sort (a run past the tie kernel fell back)
   DevBuf recs, touched, replaced;  // node records (forest.h Recs: 128 B each), per-commit flags
   uint64_t rcap = 0, rn = 0, rdead = 0;
   DevBuf mslots;  // anchor map: 16-byte (tag, record) slots
@@ -3859,7 +4099,11 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   S.sb = segd ? (h->tid_bits ? std::max(h->tid_bits, 1u) : 32u) : 0;
   // keccak'd keys, a few ops per trie: the leading 24 composite bits (the tie kernel orders the
   // rare runs past them; 2^17 ops over the 2^(sb - 2) tries the hint allows, 2^19 in one trie)
-  if (S.sb <= 18 && nops <= (segd ? (1ull << 17) : (1ull << 19))) S.rs_lo = 40;
+  // That assumes keys spread evenly over the tries: one hot trie with thousands of slot writes
+  // (or structured unhashed keys) makes runs past the tie kernel, and the whole sort falls back
+  // to 256 bits.  Such a fallback turns the 24-bit form off for the handle's next 16 commits.
+  if (S.sb <= 18 && nops <= (segd ? (1ull << 17) : (1ull << 19)) && h->lo24_off == 0) S.rs_lo = 40;
+  if (h->lo24_off) --h->lo24_off;
   S.rs_scratch = cv.take<char>(radix_scratch_bytes(nops));
   S.scan_scratch = cv.take<char>(scan_scratch_bytes(nops + 1, 8));
   S.ctr = cv.take<unsigned long long>(CTR_N);
@@ -3901,6 +4145,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
                      segd ? F.del_trie : nullptr, K, Tid, S.ctr);
   LAUNCH_CHECK();
   sort_dedup(c, S);
+  if (S.fallback && S.rs_lo == 40) h->lo24_off = 16;
   if (!defer && F.chk && c->h_pinned[1] == F.chk_tok) throw KhError{KH_EINVAL, F.chk_msg};
   const uint64_t nd = S.m;
   uint32_t* otrie = segd ? S.sseg : sseg;  // the compaction of duplicates moves the sorted ids
@@ -4594,6 +4839,13 @@ int kh_ctx_destroy(kh_ctx* c) {
       if (e) (void)hipEventDestroy(e);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->h_res) (void)hipHostFree(c->h_res);
+    c->hworker.reset();  // (idle: every call joins its stager before returning)
+    if (c->cs) (void)hipStreamSynchronize(c->cs);
+    if (c->ring) (void)hipHostFree(c->ring);
+    for (auto& e : c->ring_ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto e : c->part_ev) (void)hipEventDestroy(e);
+    if (c->cs) (void)hipStreamDestroy(c->cs);
     if (c->own) (void)hipStreamDestroy(c->own);
     if (c->st2) (void)hipStreamDestroy(c->st2);
     delete c;
@@ -4651,8 +4903,10 @@ int kh_trie_root(const uint8_t* keys, uint32_t klen, const uint8_t* vals, const 
     kh_ctx* c = shared_ctx(current_device());
     std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->dev));
-    Staged S = stage_inputs(c, keys, klen, vals, voff, n, nullptr);
+    HostStage H(c);  // the inputs stream in behind the build (keys first)
+    Staged S = stage_host_async(c, H, keys, klen, vals, voff, n);
     BuildArgs A{S.keys, klen, S.vals, S.voff, n, nullptr, 1, 0, flags, false};
+    A.hs = &H;
     BuildOut O;
     run_build(c, A, O, stats);
     copy_root(O, 0, root32);
@@ -4905,8 +5159,10 @@ int kh_trie_root_nodes(const uint8_t* keys, uint32_t klen, const uint8_t* vals, 
     kh_ctx* c = shared_ctx(current_device());
     std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->dev));
-    Staged S = stage_inputs(c, keys, klen, vals, voff, n, nullptr);
+    HostStage H(c);  // the inputs stream in behind the build (keys first)
+    Staged S = stage_host_async(c, H, keys, klen, vals, voff, n);
     BuildArgs A{S.keys, klen, S.vals, S.voff, n, nullptr, 1, 0, flags, true};
+    A.hs = &H;
     BuildOut O;
     run_build(c, A, O, stats);
     copy_root(O, 0, root32);
@@ -5534,9 +5790,30 @@ int kh_trie_open_host(const uint8_t* keys, uint32_t klen, const uint8_t* vals, c
     kh_ctx* c = shared_ctx(current_device());
     std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->dev));
-    Staged S = stage_inputs(c, keys, klen, vals, voff, n, nullptr);
-    int rc = kh_trie_open(c, S.keys, klen, S.vals, S.voff, n, flags, root32, out);
-    if (rc != KH_OK) return rc;
+    static const uint64_t zero_off[1] = {0};
+    if (n == 0) voff = zero_off;
+    // the inputs stream in behind the open's commit: its op pass reads the keys and offsets, the
+    // values are waited for where the commit first copies them (FCommit::before_values)
+    HostStage H(c);
+    Staged S = stage_host_async(c, H, keys, klen, vals, voff, n);
+    H.stream_wait(c->st, H.nkp);
+    kh_trie* h = trie_new(c, flags, false);
+    try {
+      FCommit F;
+      F.up_keys = S.keys;
+      F.up_vals = S.vals;
+      F.up_voff = S.voff;
+      F.nup = n;
+      F.klen = klen;
+      F.before_values = [&H] { H.wait(H.nkp + 1); };
+      F.vals_ready = H.ev(H.nkp + 1);
+      forest_commit(h, F, nullptr);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    if (root32) memcpy(root32, h->root, 32);
+    *out = h;
   })
 }
 

@@ -145,8 +145,12 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
     S[g]->lo = n * g / N;
     S[g]->n = n * (g + 1) / N - S[g]->lo;
   }
+  // KH_SHARD_RCCL: the RCCL exchange even for a list that repeats a device (a communicator that
+  // accepts repeats: the tests' in-process loopback, tests/loopback) -- the JVM's distinct-device
+  // path run on a one-GPU box
+  const bool use_rccl = distinct || (flags & KH_SHARD_RCCL);
   std::vector<ncclComm_t>* comms = nullptr;
-  if (distinct) {
+  if (use_rccl) {
     Rccl& R = rccl();
     auto it = g_comms.find(dev);
     if (it == g_comms.end()) {
@@ -223,7 +227,7 @@ static void sharded_root(const int* devices, int ngpus, const uint8_t* keys, uin
                                s.cs);
     HIPCHK(hipEventRecord(s.ev_vals, s.cs));
   };
-  if (distinct) {
+  if (use_rccl) {
     Rccl& R = rccl();
     for (int part = 0; part < 2; ++part) {  // 0: keys (build streams), 1: lengths + values (exchange streams)
       NCCLCHK(R.GroupStart());

@@ -267,6 +267,7 @@ enum {
 // serialises them, so they are spread over CTR_SHARDS rows of CTR_N (one 128-byte line
 // each) by block index and summed on the host.  Row 0 holds every other counter.
 constexpr int CTR_SHARDS = 64;
+constexpr unsigned long long ERR_LEAF_TOPO = 9;  // CTR_ERR: a leaf's parent depth / sorted position out of range
 constexpr int CTR_LONGN = 16 + 7;  // longlist length (row 1, index 7: unused by the stat shards)
 constexpr int CTR_PYR = 16 + 8;    // k_pyramid's finished-block count (row 1, index 8)
 constexpr int CTR_LIST = 16 + 9;   // element builds: the re-encoded leaves listed by k_leaf_prep
@@ -1068,6 +1069,14 @@ KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, u
                             uint32_t vlen, uintptr_t vend, WAVE wave, uint32_t* inl, uint32_t* longb) {
   *inl = 0;
   *longb = 0;
+  // a corrupt topology (a parent depth outside depth0 - 1 .. 63, a sorted position past the kept
+  // keys) is flagged (CTR_ERR = ERR_LEAF_TOPO: the build returns KH_EINTERNAL before its branch
+  // levels) and the leaf skipped, instead of indexing past the stash and key buffers (round 5's
+  // r5y fault: stale boundary bytes of a speculative build put depths outside 0..63)
+  if (live && (pd < (int32_t)T.depth0 - 1 || pd > 63 || (uint64_t)si >= T.m)) {
+    T.ctr[CTR_ERR] = ERR_LEAF_TOPO;
+    live = false;
+  }
   if (!live) {
     pd = 0;
     off = 0;

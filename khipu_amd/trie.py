@@ -92,9 +92,11 @@ def trie_root(keys, vals, hash_keys=False, klen=None, stats=None):
     return out.tobytes()
 
 
-def trie_root_sharded(keys, vals, devices, hash_keys=False, klen=None, stats=None):
+def trie_root_sharded(keys, vals, devices, hash_keys=False, klen=None, stats=None, rccl=False):
     """trie_root on several GPUs of this process (kh_trie_root_sharded: nibble shards,
-    RCCL point-to-point exchange, host fold of the 16 subtrie references)."""
+    RCCL point-to-point exchange, host fold of the 16 subtrie references).  rccl=True
+    (KH_SHARD_RCCL) takes the RCCL exchange even when `devices` repeats a device, which needs
+    a communicator that accepts repeats (tests/loopback)."""
     if klen is None:
         klen = 32 if isinstance(keys, np.ndarray) or not keys else len(keys[0])
     kb, n = _keys_buf(keys, klen)
@@ -103,7 +105,7 @@ def trie_root_sharded(keys, vals, devices, hash_keys=False, klen=None, stats=Non
     dv = np.asarray(list(devices), dtype=np.int32)
     out = np.zeros(32, dtype=np.uint8)
     st = stats if stats is not None else KhStats()
-    flags = _lib.KH_HASH_KEYS if hash_keys else 0
+    flags = (_lib.KH_HASH_KEYS if hash_keys else 0) | (_lib.KH_SHARD_RCCL if rccl else 0)
     check(lib().kh_trie_root_sharded(dv.ctypes.data, len(dv), kb.ctypes.data, klen, vb.ctypes.data,
                                      np.ascontiguousarray(off, np.uint64).ctypes.data, n, flags, out.ctypes.data,
                                      ctypes.byref(st)))

@@ -24,6 +24,7 @@ def lib():
         L.emu_node_children.argtypes = [vp, ctypes.c_uint64, ctypes.c_int, vp, vp, vp]
         L.emu_set_leaf_mode.argtypes = [ctypes.c_int]
         L.emu_set_link_mode.argtypes = [ctypes.c_int]
+        L.emu_set_inject.argtypes = [ctypes.c_int, ctypes.c_uint64]
         L.emu_xlane_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
         _lib = L
     return _lib
@@ -32,6 +33,12 @@ def lib():
 def set_leaf_mode(mode):
     """0 / 1: op_leaf_in3 with the loosest / the lane's own wave bounds."""
     lib().emu_set_leaf_mode(mode)
+
+
+def set_inject(kind, j=0):
+    """corrupt input j's scattered (parent depth, sorted position) before the leaf replay:
+    1 depth 70, 2 depth depth0 - 3, 3 position m + 5; 0 off"""
+    lib().emu_set_inject(kind, j)
 
 
 def set_link_mode(mode):

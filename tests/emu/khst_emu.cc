@@ -59,6 +59,10 @@ static int g_leaf_mode = 0;
 // straight from the stash (op_branch_stream) and through the records a small level writes
 // first (op_leaf_children)
 static int g_link_mode = 0;
+// a corrupt topology injected into input g_inject_j's scattered record before the leaf replay:
+// 1 parent depth 70, 2 parent depth depth0 - 3, 3 sorted position m + 5 (op_leaf_core's guard)
+static int g_inject = 0;
+static uint64_t g_inject_j = 0;
 
 // keys: n*32 (already keccak'd), vals/voff packed; seg nullable.
 // Outputs per result r: hash (32 B), enc length, inline bytes (32 B).
@@ -215,6 +219,13 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.svoff = nullptr;  // as on the device: no sorted spans in early builds
   T.svlen = nullptr;
   for (uint64_t i = 0; i < m; ++i) op_pd_scatter(T, i);
+  if (g_inject && g_inject_j < n && pdinv[g_inject_j] != PDINV_SKIP) {
+    uint64_t& pv = pdinv[g_inject_j];
+    const uint32_t si = (uint32_t)pv;
+    const int32_t pd = g_inject == 1 ? 70 : g_inject == 2 ? (int32_t)depth0 - 3 : (int32_t)(int8_t)(uint8_t)(pv >> 32);
+    const uint64_t pos = g_inject == 3 ? m + 5 : si;
+    pv = ((uint64_t)(uint8_t)(int8_t)pd << 32) | (uint32_t)pos;
+  }
   // the device reads whole 16-byte-aligned pairs around each span: replay on a copy of
   // the values at byte 8 of a 16-byte pair, with zero pairs either side (host memory is
   // not page-granular)
@@ -243,6 +254,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       longb += lb;
     }
   }
+  if (ctr[CTR_ERR] == ERR_LEAF_TOPO) return -9;  // (the device: KH_EINTERNAL at the leaves' counter sync)
   uint64_t C = 0;
   for (uint64_t j = 0; j < B; ++j) {
     br_cbase[j] = (uint32_t)C;
@@ -334,6 +346,10 @@ extern "C" {
 
 void emu_set_leaf_mode(int mode) { g_leaf_mode = mode; }
 void emu_set_link_mode(int mode) { g_link_mode = mode; }
+void emu_set_inject(int kind, uint64_t j) {
+  g_inject = kind;
+  g_inject_j = j;
+}
 
 int emu_build(const uint8_t* keys, const uint8_t* vals, const uint64_t* voff, uint64_t n, const uint32_t* seg,
               uint64_t nseg, uint32_t depth0, uint8_t* out_hash, uint32_t* out_len, uint8_t* out_inl,

@@ -28,6 +28,9 @@ typedef jarray jbyteArray;
 typedef jarray jintArray;
 typedef jarray jlongArray;
 typedef jarray jobjectArray;
+typedef jobject jstring;
+struct _jmethodID;
+typedef struct _jmethodID* jmethodID;
 
 struct JNINativeInterface_;
 typedef const struct JNINativeInterface_* JNIEnv;
@@ -44,8 +47,15 @@ struct JNINativeInterface_ {
   void (*SetByteArrayRegion)(JNIEnv* env, jbyteArray array, jsize start, jsize len, const jbyte* buf);
   void (*SetLongArrayRegion)(JNIEnv* env, jlongArray array, jsize start, jsize len, const jlong* buf);
   void (*SetIntArrayRegion)(JNIEnv* env, jintArray array, jsize start, jsize len, const jint* buf);
-  void* (*GetPrimitiveArrayCritical)(JNIEnv* env, jarray array, jboolean* isCopy);
-  void (*ReleasePrimitiveArrayCritical)(JNIEnv* env, jarray array, void* carray, jint mode);
+  void (*GetByteArrayRegion)(JNIEnv* env, jbyteArray array, jsize start, jsize len, jbyte* buf);
+  void (*GetIntArrayRegion)(JNIEnv* env, jintArray array, jsize start, jsize len, jint* buf);
+  void* (*GetDirectBufferAddress)(JNIEnv* env, jobject buf);
+  jlong (*GetDirectBufferCapacity)(JNIEnv* env, jobject buf);
+  jmethodID (*GetStaticMethodID)(JNIEnv* env, jclass clazz, const char* name, const char* sig);
+  jobject (*CallStaticObjectMethod)(JNIEnv* env, jclass clazz, jmethodID methodID, ...);
+  jint (*Throw)(JNIEnv* env, jthrowable obj);
+  jboolean (*ExceptionCheck)(JNIEnv* env);
+  jstring (*NewStringUTF)(JNIEnv* env, const char* utf);
 };
 
 #endif

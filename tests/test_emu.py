@@ -127,3 +127,26 @@ def test_lane_spread_keccak():
     round), replayed lane by lane, == keccak.h's one-thread Keccak-f[1600] (which the oracle
     KATs pin) on 300 random states; lanes 25..31 start with garbage and must not leak in."""
     assert E.xlane_check(11, 300) == 0
+
+
+@pytest.mark.parametrize("kind", [1, 2, 3])
+@pytest.mark.parametrize("depth0", [0, 1])
+def test_corrupt_topology_is_an_error_not_a_fault(oracle, kind, depth0):
+    """the leaf path no longer trusts the scattered (parent depth, sorted
+    position): a depth outside depth0 - 1 .. 63 or a position past the kept keys sets CTR_ERR
+    (the device build returns KH_EINTERNAL at the leaves' counter sync, before any branch level)
+    and the leaf is skipped -- here replayed with such a record injected into one input; the
+    same build without it is the oracle's root."""
+    r = random.Random(5 + kind)
+    keys = [bytes(r.getrandbits(8) for _ in range(32)) for _ in range(300)]
+    vals = [C.account_value(r) for _ in keys]
+    E.set_leaf_mode(1)
+    E.set_link_mode(2)
+    try:
+        E.set_inject(kind, 17)
+        with pytest.raises(AssertionError, match="-9"):
+            E.build(keys, vals, depth0=depth0)
+    finally:
+        E.set_inject(0)
+    res, _ = E.build(keys, vals)
+    assert res[0][0] == oracle.seq_root(keys, vals)

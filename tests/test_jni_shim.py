@@ -75,3 +75,36 @@ def test_free_zeroes_the_box_before_freeing():
     body = body[:body.index("\n}\n")]
     assert body.index("SetLongArrayRegion") < body.index("kh_trie_free(")
     assert "if (!h) return;" in body
+
+
+def _driver():
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "jni_stub")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return os.path.join(ROOT, "tests", "jni_stub", "jni_driver")
+
+
+def test_no_critical_regions():
+    """a wrapper may wait for the context's mutex and run seconds of GPU work, so no
+    JNI critical region may be held across a library call (the stub jni.h no longer declares the
+    critical functions, so a use would not compile either)."""
+    with open(SHIM) as f:
+        code = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    assert "GetPrimitiveArrayCritical" not in code and "ReleasePrimitiveArrayCritical" not in code
+    for w in ("trieRootDirect", "trieRootNodesDirect", "openHostDirect", "trieRootShardedDirect"):
+        assert "Java_khipu_trie_gpu_Khst_" + w + "(" in code, w
+
+
+def test_shim_argument_checks_through_a_jnienv():
+    """The wrappers run through an in-process JNIEnv (tests/jni_stub/fake_env.c): a heap array or
+    a short buffer handed to a *Direct wrapper, and a short root hash, raise
+    IllegalArgumentException before any library call; the empty trie needs no device."""
+    import json
+    if not os.path.exists(LIB):
+        pytest.skip("libkhst.so not built (__graft_entry__.build())")
+    r = subprocess.run([_driver(), "cpu"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    got = {d["check"]: d for d in map(json.loads, r.stdout.split("\n")[:-1])}
+    for c in ("direct_keys_not_direct", "direct_voff_short", "direct_vals_short", "open_nodes_short_root"):
+        assert got[c]["pending"] == 1 and got[c]["exc"] == "java/lang/IllegalArgumentException", got[c]
+    empty = "56e81f171bcc55a6ff8345e692c0f86e5b48e01b996cadc001622fb5e363b421"
+    assert got["direct_empty"]["root"] == empty and got["array_empty"]["root"] == empty
