@@ -882,80 +882,9 @@ __device__ __forceinline__ void wave_count(unsigned long long* dst, bool f) {
   const uint64_t b = __ballot(f);
   if (b && __lane_id() == 0) atomicAdd(dst, (unsigned long long)__popcll(b));
 }
-// Early leaves (plain root builds; trie_ops.h op_leaf_core): one thread per INPUT, on the
-// second stream beside the branch topology.  Keys and packed values are read in input
-// order; the parent depth gives the header geometry, the key and value are then loaded at
-// their message shifts, and the message is assembled dword by dword (v_perm_b32) straight
-// into the Keccak state.  Every lane of a wave runs the wave-bound reductions, so threads
-// past n take part with neutral values.
-// A block takes LEAF_ITEMS runs of BS consecutive inputs, one after the other: the next run's
-// scatter record and span offsets (the first of the two dependent load rounds) are brought
-// into LDS by LDS-DMA while the current input is assembled and permuted (no registers held
-// across the permutation), and the counters are added once per wave (42.6 -> 41.9 ms in the
-// step against one input per thread, profiles/r5g_leaf_prefetch_ab_100m.json).  Blocks that
-// live for a few runs only keep the wave slots turning over for the topology kernels beside
-// them (a persistent grid starved them: the topology stream 15 -> 22 ms, the step 42.5 -> 45
-// ms, profiles/r5e_leaf_grid_ab_100m.json; forcing 7 waves per SIMD spilled and cost 1.4 ms).
-// The permutation is straight-line (keccakf<KECCAK_FULL>: no pi-renaming moves at loop
-// back-edges; 78 VGPRs and 6 waves with the 3-iteration loop, 0.9 ms slower in the step,
-// profiles/r4bp_keccak_unroll_ab_100m.json).
-constexpr uint32_t LEAF_ITEMS = 4;
-__global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
-  auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {
-    WaveBounds b;
-    b.emax = wave_max_u32(use ? e : 0u);
-    b.emin = 255u - wave_max_u32(use ? 255u - e : 0u);
-    b.Lmax = wave_max_u32(use ? lhi : 0u);
-    b.Lmin = 255u - wave_max_u32(use ? 255u - llo : 0u);
-    return b;
-  };
-  const uint64_t j0 = (uint64_t)blockIdx.x * LEAF_ITEMS * BS + threadIdx.x, jend = j0 + LEAF_ITEMS * BS;
-  // double-buffered per wave: [slot][wave][pv low / pv high dwords (2 x 64), voff[j], voff[j+1] (64 pairs)]
-  __shared__ uint32_t pbuf[2][BS / 64][64 * 6];
-  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  auto issue = [&](uint32_t slot, uint64_t j) {  // (every lane of the wave: j past n reads a clamped input)
-    typedef __attribute__((address_space(1))) void gv;
-    typedef __attribute__((address_space(3))) void lv;
-    const uint64_t jj = j < n ? j : n - 1;
-    uint32_t* b = pbuf[slot][w];
-    __builtin_amdgcn_global_load_lds((gv*)(T.pdinv + jj), (lv*)b, 4, 0, 0);
-    __builtin_amdgcn_global_load_lds((gv*)((const uint32_t*)(T.pdinv + jj) + 1), (lv*)(b + 64), 4, 0, 0);
-    __builtin_amdgcn_global_load_lds((gv*)(T.voff + jj), (lv*)(b + 128), 16, 0, 0);
-  };
-  auto take = [&](uint32_t slot, uint64_t j, uint64_t& pv, uint64_t& off, uint64_t& end) {
-    __builtin_amdgcn_s_waitcnt(0);  // (vmcnt: the slot's LDS-DMA has landed)
-    asm volatile("" ::: "memory");
-    const uint32_t* b = pbuf[slot][w];
-    pv = j < n ? ((uint64_t)b[64 + l] << 32) | b[l] : PDINV_SKIP;
-    off = ((const uint64_t*)(b + 128))[2 * l];
-    end = ((const uint64_t*)(b + 128))[2 * l + 1];
-  };
-  const uintptr_t vend = (uintptr_t)T.vals + T.voff[n];  // (once: see op_leaf_core)
-  uint64_t pv = 0, off = 0, end = 0;
-  issue(0, j0);
-  uint32_t perms = 0, inl = 0, slot = 0;
-#pragma unroll 1
-  for (uint64_t j = j0; j < jend && j - threadIdx.x % 64 < n; j += BS) {  // (wave-uniform: the wave's first input)
-    const uint64_t jn = j + BS < jend ? j + BS : n;
-    take(slot, j, pv, off, end);
-    if (j + BS < jend && jn - threadIdx.x % 64 < n) issue(slot ^ 1, jn);  // (wave-uniform: no next run past the block's)
-    slot ^= 1;
-    const bool live = pv != PDINV_SKIP;  // not an earlier put of a key put again later
-    uint32_t in1 = 0, lb = 0;
-    perms += op_leaf_core(T, live, (int32_t)(int8_t)(uint8_t)(pv >> 32), (uint32_t)pv, j, n, off,
-                          (uint32_t)(end - off), vend, wave, &in1, &lb);
-    inl += in1;
-    if (lb) atomicAdd(&T.ctr[CTR_LONGB], (unsigned long long)lb);
-  }
-  const unsigned long long sp = wave_sum((unsigned long long)perms), si = wave_sum((unsigned long long)inl);
-  if ((threadIdx.x & 63) == 0) {
-    if (sp) {
-      atomicAdd(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), sp);
-      atomicAdd(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), sp);
-    }
-    if (si) atomicAdd(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), si);
-  }
-}
+// Early leaves: k_leaf_in (csrc/leaf_kernel.hip, a compilation unit of its own: see there)
+constexpr uint32_t LEAF_ITEMS = 4;  // runs of BS inputs per block (leaf_kernel.hip)
+__global__ void k_leaf_in(Topo T, uint64_t n);
 // the same publish split in two (trie_ops.h op_leaf_link / op_leaf_move)
 __global__ void __launch_bounds__(BS) k_leaf_link(Topo T) {
   GRID_STRIDE(i, T.m) op_leaf_link(T, i);
@@ -1022,6 +951,11 @@ __global__ void __launch_bounds__(BS) k_branch_hash(Topo T, uint64_t first, uint
 // branch levels 7.91-7.95 -> 7.85-7.87 ms, reads 21.0 -> 16.3 GB at 100M
 // (profiles/r5u_branch_table12_ab_100m.json); one more child in flight spills 19 VGPRs and
 // costs 0.5 ms (r5v_branch_table12_queue_ab_100m.json).
+// V 4 / 6 take the table form only: a branch spanning T12_SPAN keys or more (rare: the top of
+// a trie, a cluster of keys) is listed for k_branch_wide, launched right after on the level.
+// With both forms in one kernel its registers were the larger form's: 128 VGPRs with 10
+// spilled to scratch (the addresses of the branch's own table entries, reloaded ~11 times
+// a thread); the table form alone fits in 127 with none.
 template <int V>
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8))) k_branch_fused(Topo T, uint64_t first, uint64_t cnt) {
   __shared__ uint64_t slots[BS * LEAF_WORDS];
@@ -1035,19 +969,46 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 8)))
     // fixed-length keys: direct window assembly; variable-length keys (branch values):
     // the byte stream through the windowed writer
     uint64_t* sl = slots + threadIdx.x * LEAF_WORDS;
-    // (leaf positions: the table form unless some branch of the wave spans 4096 keys or more)
-    const bool wide = TB && wave_any(T.br_end[j] - T.br_first[j] >= T12_SPAN);
+    const bool wide = TB && T.br_end[j] - T.br_first[j] >= T12_SPAN;
     const ChildSrc ts{nullptr, nullptr, 1, tbl + threadIdx.x, BS};
-    perms = V == 0   ? op_branch_fused(T, j, sl, 1, &in1)
-            : V == 2 ? op_branch_stream_t<SRC_REC>(T, j, sl, 1, &in1, ChildSrc{})
-            : V == 4 ? (TB && !wide ? op_branch_stream_t<SRC_T12>(T, j, sl, 1, &in1, ts)
-                                    : op_branch_stream_t<SRC_POS>(T, j, sl, 1, &in1, ChildSrc{}))
-                     : (TB && !wide ? op_branch_stream_t<SRC_T12K>(T, j, sl, 1, &in1, ts)
-                                    : op_branch_stream_t<SRC_POSK>(T, j, sl, 1, &in1, ChildSrc{}));
-    hashes = branch_hash_count(T, j, (uint32_t)perms);
-    inl = in1;
+    if (wide) {
+      T.wlist[atomicAdd(T.wcnt, 1u)] = j;
+    } else {
+      perms = V == 0   ? op_branch_fused(T, j, sl, 1, &in1)
+              : V == 2 ? op_branch_stream_t<SRC_REC>(T, j, sl, 1, &in1, ChildSrc{})
+              : V == 4 ? op_branch_stream_t<SRC_T12>(T, j, sl, 1, &in1, ts)
+                       : op_branch_stream_t<SRC_T12K>(T, j, sl, 1, &in1, ts);
+      hashes = branch_hash_count(T, opaque_u32(j), (uint32_t)perms);
+      inl = in1;
+    }
   }
   // one atomic per wave (a block-wide sum would need LDS past the 40 KB that 4 blocks per CU allow)
+  const unsigned long long sp = wave_sum(perms), sh = wave_sum(hashes), si = wave_sum(inl);
+  if ((threadIdx.x & 63) == 0) {
+    if (sp) atomicAdd(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), sp);
+    if (sh) atomicAdd(ctr_stat(T.ctr, CTR_HASHES, blockIdx.x), sh);
+    if (si) atomicAdd(ctr_stat(T.ctr, CTR_INLINE, blockIdx.x), si);
+  }
+}
+
+// The branches k_branch_fused<4 / 6> listed (spanning T12_SPAN keys or more): the per-child
+// form (every child's meta loaded as its record is placed).  Usually none at the big levels of
+// random keys: a few blocks that read the count and exit.
+template <int V>
+__global__ void __launch_bounds__(BS) k_branch_wide(Topo T) {
+  __shared__ uint64_t slots[BS * LEAF_WORDS];
+  const uint32_t nw = *(volatile const uint32_t*)T.wcnt;
+  unsigned long long perms = 0, hashes = 0, inl = 0;
+  for (uint32_t t = blockIdx.x * BS + threadIdx.x; t < nw; t += gridDim.x * BS) {
+    const uint32_t j = T.wlist[t];
+    uint32_t in1 = 0;
+    uint64_t* sl = slots + threadIdx.x * LEAF_WORDS;
+    const uint32_t p = V == 4 ? op_branch_stream_t<SRC_POS>(T, j, sl, 1, &in1, ChildSrc{})
+                              : op_branch_stream_t<SRC_POSK>(T, j, sl, 1, &in1, ChildSrc{});
+    perms += p;
+    hashes += branch_hash_count(T, j, p);
+    inl += in1;
+  }
   const unsigned long long sp = wave_sum(perms), sh = wave_sum(hashes), si = wave_sum(inl);
   if ((threadIdx.x & 63) == 0) {
     if (sp) atomicAdd(ctr_stat(T.ctr, CTR_PERMS, blockIdx.x), sp);
@@ -2299,7 +2260,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
       n * 4, n, n, n * 8, n * 4, n * 8, n * 4,  // leaves, svoff, svlen
       A.emit ? n * 32 : 0, A.emit ? nb1 * 32 : 0, A.emit ? nb1 * 32 : 0,  // hashes
       nres * 32, nres * 4, nres * 32,         // results
-      CTR_N * CTR_SHARDS * 8, 64 * 4, 80 * 4, NBUCKET * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
+      CTR_N * CTR_SHARDS * 8, 64 * 4, 80 * 4, 64 * 4, NBUCKET * ((nb1 + LV_TILE - 1) / LV_TILE) * 4, nb1 * 4,  // ctr hist lb bcnt order
       early ? n * 32 : 0, early ? n : 0, early ? n * 8 : 0,  // early leaves: stashed references, meta, pd|position
       early && !lpos ? n * 8 : 0,                                 // link slots (segmented early builds)
       A.kn ? n : 0,                           // sorted key lengths
@@ -2355,6 +2316,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   T.ctr = cv.take<unsigned long long>(CTR_N * CTR_SHARDS);
   T.depth_hist = cv.take<uint32_t>(64);
   uint32_t* lb = cv.take<uint32_t>(80);
+  uint32_t* wcnt = cv.take<uint32_t>(64);  // k_branch_wide: the wide branches of each level (zeroed below)
   const uint32_t nblk_max = (uint32_t)((nb1 + LV_TILE - 1) / LV_TILE);
   uint32_t* bcnt = cv.take<uint32_t>((uint64_t)NBUCKET * nblk_max);
   uint32_t* order = cv.take<uint32_t>(nb1);
@@ -2386,7 +2348,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   T.vlen_in = A.vlen;
 
   // results, counters, depth histogram and level bounds are carved back to back: one memset
-  HIPCHK(hipMemsetAsync(T.res_hash, 0, (size_t)((char*)(lb + 80) - (char*)T.res_hash), st));
+  HIPCHK(hipMemsetAsync(T.res_hash, 0, (size_t)((char*)(wcnt + 64) - (char*)T.res_hash), st));
 
   // stage events (kh_stats' t_keys / t_sort / t_topo / t_leaf / t_branch): not for a forest's
   // element builds, whose host is the bottleneck (the block-commit HIP API trace: every API
@@ -2706,7 +2668,12 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   if (leaves_deferred) start_leaves(false);
   const uint64_t B = (uint32_t)hc[CTR_B];
   const uint64_t C = (uint32_t)hc[CTR_B + 3];
-  if (hc[CTR_ERR]) throw KhError{KH_EINTERNAL, "topology invariant violated (group chain > 15)"};
+  if (hc[CTR_ERR]) {  // (the leaves may still run on st2: drained before the workspace is given up)
+    HIPCHK(hipStreamSynchronize(c->st2));
+    throw KhError{KH_EINTERNAL, hc[CTR_ERR] == ERR_LEAF_TOPO
+                                    ? "topology: a boundary value out of range (corrupt topology)"
+                                    : "topology invariant violated (group chain > 15)"};
+  }
   std::vector<uint32_t> lbh(65, 0);
   memcpy(lbh.data(), (const char*)hc + ((char*)lb - (char*)ctr), 65 * 4);
   if (nb == 0) std::fill(lbh.begin(), lbh.end(), 0u);
@@ -2746,6 +2713,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   T.bmsg = A.emit ? cv2.take<uint64_t>(bmsg_words) : nullptr;
   T.xmsg = A.emit ? cv2.take<uint64_t>(xmsg_words) : nullptr;
   T.lb = lb;
+  T.wlist = tlist_a;  // (the tile topology's list, free again: >= B entries)
   if (A.el) {  // element build: every capped reference kept for the forest's records
     ElemArgs& E = *A.el;
     E.outb->ensure(carve_size({B * 32, B * 4, B * 32, B * 4}));
@@ -2838,10 +2806,15 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
         Topo TL = T;
         TL.lvl_depth = (uint32_t)d;
         TL.lvl_nsh = 28 - 4 * ((uint32_t)d & 7);
-        if (pos_level_ok(T, (uint32_t)d))
+        TL.wcnt = wcnt + d;  // (zeroed with the counters; one per level)
+        const dim3 wg((unsigned)std::min<uint64_t>((cnt + BS - 1) / BS, 4u * (uint32_t)c->n_cu));
+        if (pos_level_ok(T, (uint32_t)d)) {
           hipLaunchKernelGGL(k_branch_fused<4>, GRID(cnt, BS), dim3(BS), 0, st, TL, (uint64_t)lbh[d], (uint64_t)cnt);
-        else
+          hipLaunchKernelGGL(k_branch_wide<4>, wg, dim3(BS), 0, st, TL);
+        } else {
           hipLaunchKernelGGL(k_branch_fused<6>, GRID(cnt, BS), dim3(BS), 0, st, TL, (uint64_t)lbh[d], (uint64_t)cnt);
+          hipLaunchKernelGGL(k_branch_wide<6>, wg, dim3(BS), 0, st, TL);
+        }
       } else {
         hipLaunchKernelGGL(k_branch_fused<2>, GRID(cnt, BS), dim3(BS), 0, st, T, (uint64_t)lbh[d], (uint64_t)cnt);
       }

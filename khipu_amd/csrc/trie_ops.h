@@ -232,6 +232,8 @@ struct Topo {
   uint32_t lvl_nsh;    // per level launch: 28 - 4 * the level's depth (a leaf child's nibble in sck)
   uint32_t lvl_depth;  //   and the depth itself (deeper levels: the nibble from the input key)
   uint32_t* longlist;  // [m] sorted leaves longer than one Keccak block (the leaf kernel lists them)
+  uint32_t* wlist;     // [B] per level launch: the level's branches spanning >= T12_SPAN keys (k_branch_fused
+  uint32_t* wcnt;      //   lists them for k_branch_wide), and their count (one per level launch, zeroed)
   // element builds (resident commits, forest.h; all nullable): an element is a leaf, or
   // a SUBTREE standing for an unchanged branch at depth el_db[i] whose capped reference
   // is el_bref / el_brl (its keys all share key i's first el_db nibbles)
@@ -373,8 +375,19 @@ KH_HD uint8_t lcp_value(const Topo& T, uint64_t b) {
 }
 KH_HD void op_lcp(const Topo& T, uint64_t b) { T.u[b] = lcp_value(T, b); }
 // the early leaves' scatter record of sorted leaf i from its two boundary values
+// A boundary value outside 0 / depth0 + 1 .. 64 (stale bytes: round 5's r5y fault, where a
+// speculative build's unvalued tie run left the bytes of an earlier build, leaf depths fell
+// outside 0..63 and the leaf kernel indexed past its buffers) is flagged (CTR_ERR =
+// ERR_LEAF_TOPO: the build returns KH_EINTERNAL at the topology's counter sync, before any
+// branch level) and clamped, so the leaf kernel never reads a depth out of range.  Guarded here,
+// where the depths are made (every early-leaf record passes through this function), not in the
+// leaf kernel: the same check there cost 10 % of its time (a changed register allocation).
 KH_HD void pd_scatter_vals(const Topo& T, uint64_t i, uint32_t va, uint32_t vc) {
-  const uint32_t v = va > vc ? va : vc;
+  uint32_t v = va > vc ? va : vc;
+  if (v > 64 || (v != 0 && v < T.depth0 + 1)) {
+    T.ctr[CTR_ERR] = ERR_LEAF_TOPO;
+    v = 0;
+  }
   const int32_t pd = v == 0 ? (int32_t)T.depth0 - 1 : (int32_t)v - 1;
   T.pdinv[T.sidx ? T.sidx[i] : i] = ((uint64_t)(uint8_t)(int8_t)pd << 32) | i;
 }
@@ -672,6 +685,10 @@ KH_HD void op_branch_topo(const Topo& T, const Pyr& P, uint64_t nb, uint64_t b) 
   if (T.u[b] == 0 || T.rep[b] != (uint32_t)b) return;
   uint32_t j = T.isrep_bid[b];
   uint32_t t = T.u[b];
+  if (t > 64 || t < T.depth0 + 1) {  // a corrupt boundary value (see pd_scatter_vals): no depth past the level tables
+    T.ctr[CTR_ERR] = ERR_LEAF_TOPO;
+    return;
+  }
   uint32_t d = t - 1u;
   int64_t a = T.psv[b], c = T.nsv[b];
   Parent Pp = resolve_parent(T, a, c);
@@ -1035,6 +1052,17 @@ KH_HD uint32_t below_mask(int32_t y8) {
 #else
 #define KH_NOSPEC() ((void)0)
 #endif
+// A copy of x the compiler cannot see through: table addresses computed from it are neither
+// CSE'd with nor hoisted above earlier ones.  k_branch_fused sits at its VGPR limit; without
+// this the five 64-bit addresses of its branch's own table entries (br_first, br_end, br_ext,
+// br_parent, br_depth at j), formed at entry, stayed live across the permutations for the
+// publish and were spilled to scratch (10 VGPRs, 16 scratch instructions a thread).
+KH_HD uint32_t opaque_u32(uint32_t x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  asm volatile("" : "+v"(x));
+#endif
+  return x;
+}
 // 4 / 16 bytes from a 4-byte-aligned global address
 #ifdef __HIP_DEVICE_COMPILE__
 typedef uint32_t v4u_a4 __attribute__((ext_vector_type(4), aligned(4)));
@@ -1057,6 +1085,16 @@ KH_HD void ld128_a4(uintptr_t a, uint32_t* o) { memcpy(o, (const void*)a, 16); }
 constexpr uint32_t LEAF_VD = 36;  // value dwords loaded per lane (the message's 34 + funnel)
 constexpr uint32_t LEAF_KD = 12;  // key dwords (message dwords 0..9 + funnel)
 
+// The straight-line permutation of the leaf kernel placed at a fixed offset from a 64-byte
+// boundary: KH_LEAF_PAD 4-byte s_nops after a .p2align 6 (measurement builds: -DKH_LEAF_PAD=k;
+// unset: no alignment)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(KH_LEAF_PAD)
+#define KH_STR2(x) #x
+#define KH_STR(x) KH_STR2(x)
+#define KH_LEAF_ALIGN() asm volatile(".p2align 6\n\t.rept " KH_STR(KH_LEAF_PAD) "\n\ts_nop 0\n\t.endr")
+#else
+#define KH_LEAF_ALIGN() ((void)0)
+#endif
 KH_HD uint32_t rlp_hdr_len32(uint32_t x) {  // rlp_hdr_len of a 32-bit length
   return x < 56 ? 1u : x < 0x100u ? 2u : x < 0x10000u ? 3u : x < 0x1000000u ? 4u : 5u;
 }
@@ -1069,14 +1107,6 @@ KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, u
                             uint32_t vlen, uintptr_t vend, WAVE wave, uint32_t* inl, uint32_t* longb) {
   *inl = 0;
   *longb = 0;
-  // a corrupt topology (a parent depth outside depth0 - 1 .. 63, a sorted position past the kept
-  // keys) is flagged (CTR_ERR = ERR_LEAF_TOPO: the build returns KH_EINTERNAL before its branch
-  // levels) and the leaf skipped, instead of indexing past the stash and key buffers (round 5's
-  // r5y fault: stale boundary bytes of a speculative build put depths outside 0..63)
-  if (live && (pd < (int32_t)T.depth0 - 1 || pd > 63 || (uint64_t)si >= T.m)) {
-    T.ctr[CTR_ERR] = ERR_LEAF_TOPO;
-    live = false;
-  }
   if (!live) {
     pd = 0;
     off = 0;
@@ -1198,6 +1228,7 @@ KH_HD uint32_t op_leaf_core(const Topo& T, bool live, int32_t pd, uint32_t si, u
   uint64_t* r = T.lf_eref + 4 * si;
   uint32_t perms = 0;
   if (L >= 32 || top) {  // a leaf embedded in its parent is never hashed (Node.scala:114)
+    KH_LEAF_ALIGN();
     keccakf<KECCAK_FULL>(S);
     for (int q = 0; q < 4; ++q) r[q] = lane(S, q);
     perms = 1;
@@ -1944,9 +1975,9 @@ KH_HD uint32_t op_branch_stream_t(const Topo& T, uint32_t j, uint64_t* slot, uin
         bhead[q] = base < L ? slot[q * stride] & low_bytes_mask(L - base < 8 ? L - base : 8) : 0;
       }
     ninl = hashit ? 0 : 1;
-    branch_keep(T, j, L, hb, bhead);
+    branch_keep(T, opaque_u32(j), L, hb, bhead);
   }
-  perms += branch_publish(T, j, L, hb, bhead, Slot{slot, stride}, &ninl);
+  perms += branch_publish(T, opaque_u32(j), L, hb, bhead, Slot{slot, stride}, &ninl);
   *inl = ninl;
   return perms;
 }

@@ -36,8 +36,9 @@ def set_leaf_mode(mode):
 
 
 def set_inject(kind, j=0):
-    """corrupt input j's scattered (parent depth, sorted position) before the leaf replay:
-    1 depth 70, 2 depth depth0 - 3, 3 position m + 5; 0 off"""
+    """a corrupt boundary value (stale bytes, the r5y fault): 1 u[j] = 200 before the leaves'
+    parent-depth scatter, 2 the first representative boundary from j set to 70 before the
+    branch records, 3 u[j] = 1 before the scatter (invalid under depth0 = 1); 0 off"""
     lib().emu_set_inject(kind, j)
 
 

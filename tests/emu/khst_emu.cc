@@ -59,8 +59,9 @@ static int g_leaf_mode = 0;
 // straight from the stash (op_branch_stream) and through the records a small level writes
 // first (op_leaf_children)
 static int g_link_mode = 0;
-// a corrupt topology injected into input g_inject_j's scattered record before the leaf replay:
-// 1 parent depth 70, 2 parent depth depth0 - 3, 3 sorted position m + 5 (op_leaf_core's guard)
+// a corrupt boundary value injected into u[g_inject_j] (the r5y fault: stale bytes): 1 before
+// the leaves' parent-depth scatter (value 200), 2 before the branch records (value 70), 3 the
+// scatter with value 1 under depth0 = 1 (below the first valid value 2)
 static int g_inject = 0;
 static uint64_t g_inject_j = 0;
 
@@ -195,8 +196,15 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       run += f;
     }
     B = run;
+    if (g_inject == 2)  // the first representative boundary from g_inject_j on
+      for (uint64_t b = g_inject_j; b < nb; ++b)
+        if (u[b] && rep[b] == b) {
+          u[b] = 70;
+          break;
+        }
     for (uint64_t b = 0; b < nb; ++b) {
       op_branch_topo(T, P, nb, b);
+      if (ctr[CTR_ERR] == ERR_LEAF_TOPO) return -9;  // (the device: KH_EINTERNAL at the topology's counter sync)
       if (u[b] != 0 && rep[b] == b) {
         uint32_t j = isrep[b];
         hist[br_depth[j]]++;
@@ -218,14 +226,8 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   T.longlist = lpos ? longlist.data() : nullptr;
   T.svoff = nullptr;  // as on the device: no sorted spans in early builds
   T.svlen = nullptr;
+  if ((g_inject == 1 || g_inject == 3) && g_inject_j < nb) u[g_inject_j] = g_inject == 1 ? 200 : 1;
   for (uint64_t i = 0; i < m; ++i) op_pd_scatter(T, i);
-  if (g_inject && g_inject_j < n && pdinv[g_inject_j] != PDINV_SKIP) {
-    uint64_t& pv = pdinv[g_inject_j];
-    const uint32_t si = (uint32_t)pv;
-    const int32_t pd = g_inject == 1 ? 70 : g_inject == 2 ? (int32_t)depth0 - 3 : (int32_t)(int8_t)(uint8_t)(pv >> 32);
-    const uint64_t pos = g_inject == 3 ? m + 5 : si;
-    pv = ((uint64_t)(uint8_t)(int8_t)pd << 32) | (uint32_t)pos;
-  }
   // the device reads whole 16-byte-aligned pairs around each span: replay on a copy of
   // the values at byte 8 of a 16-byte pair, with zero pairs either side (host memory is
   // not page-granular)

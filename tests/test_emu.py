@@ -129,14 +129,14 @@ def test_lane_spread_keccak():
     assert E.xlane_check(11, 300) == 0
 
 
-@pytest.mark.parametrize("kind", [1, 2, 3])
-@pytest.mark.parametrize("depth0", [0, 1])
-def test_corrupt_topology_is_an_error_not_a_fault(oracle, kind, depth0):
-    """the leaf path no longer trusts the scattered (parent depth, sorted
-    position): a depth outside depth0 - 1 .. 63 or a position past the kept keys sets CTR_ERR
-    (the device build returns KH_EINTERNAL at the leaves' counter sync, before any branch level)
-    and the leaf is skipped -- here replayed with such a record injected into one input; the
-    same build without it is the oracle's root."""
+@pytest.mark.parametrize("kind,depth0", [(1, 0), (1, 1), (2, 0), (2, 1), (3, 1)])
+def test_corrupt_boundary_is_an_error_not_a_fault(oracle, kind, depth0):
+    """a boundary value outside 0 / depth0 + 1 .. 64 (the r5y fault: a
+    speculative build's stale bytes put leaf depths outside 0..63 and the leaf kernel indexed
+    past its buffers) is flagged where depths are made -- the early leaves' parent-depth scatter
+    (pd_scatter_vals) and the branch records (op_branch_topo) -- and clamped, so no kernel reads
+    a depth out of range; the device build returns KH_EINTERNAL at the topology's counter sync.
+    Replayed with such a value injected; the same build without it is the oracle's root."""
     r = random.Random(5 + kind)
     keys = [bytes(r.getrandbits(8) for _ in range(32)) for _ in range(300)]
     vals = [C.account_value(r) for _ in keys]
