@@ -37,7 +37,16 @@ constexpr uint32_t LEAF_ITEMS = 4;  // (khst.hip sizes the grid with the same va
 // The permutation is straight-line (keccakf<KECCAK_FULL>: no pi-renaming moves at loop
 // back-edges; 78 VGPRs and 6 waves with the 3-iteration loop, 0.9 ms slower in the step,
 // profiles/r4bp_keccak_unroll_ab_100m.json).
+// KH_LEAF_SHIFT (measurement builds): N s_nops at the kernel's entry move all of its code by 4N bytes
+#if defined(KH_LEAF_SHIFT)
+#define KH_STR2(x) #x
+#define KH_STR(x) KH_STR2(x)
+#define KH_LEAF_ENTRY() asm volatile(".rept " KH_STR(KH_LEAF_SHIFT) "\n\ts_nop 0\n\t.endr")
+#else
+#define KH_LEAF_ENTRY() ((void)0)
+#endif
 __global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
+  KH_LEAF_ENTRY();
   auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {
     WaveBounds b;
     b.emax = wave_max_u32(use ? e : 0u);

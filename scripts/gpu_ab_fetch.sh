@@ -5,7 +5,7 @@
 export TMPDIR=/tmp
 tag=$1; shift
 specs=("$@")
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
 for spec in "${specs[@]}"; do
   label=${spec%%=*}; lib=${spec#*=}
   KHST_LIB_AB=$lib timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu --no-host-path > gpurun_out/ab_${tag}_${label}_$rep.json 2>/dev/null || exit 1
