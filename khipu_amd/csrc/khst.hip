@@ -1842,6 +1842,13 @@ struct kh_ctx {
   uint32_t ring_next = 0;
   std::vector<hipEvent_t> part_ev;
   std::unique_ptr<Worker> hworker;
+  // small host inputs (a commit's ops: HostPack): packed into one pinned buffer, one DMA into
+  // in_block; pack_ev marks that DMA (the next pack waits for it before reusing the buffer)
+  uint8_t* h_pack = nullptr;
+  size_t h_pack_cap = 0;
+  hipEvent_t pack_ev = nullptr;
+  bool pack_busy = false;
+  bool pack_for_block = false;  // kh_block_commit_host -> kh_block_commit: its phases wait for pack_ev
 };
 
 // Host inputs (keys, value offsets, values of kh_trie_root / kh_trie_root_nodes /
@@ -3068,6 +3075,58 @@ static Staged stage_host_async(kh_ctx* c, HostStage& H, const uint8_t* keys, uin
   return Staged{dk, dv, doff, nullptr};
 }
 
+// A commit's host inputs (kh_block_commit_host, the *_apply_host / root_of_host calls: a few MB
+// in up to 11 arrays) packed into the context's pinned buffer at the offsets they take in the
+// device staging buffer (c->in_block), value offsets rebased while they are packed, and sent
+// in ONE DMA.  Round 5 issued a pageable hipMemcpyAsync per array and a host copy of the
+// offsets, then synchronised: ~0.8 ms of a configs[2] block through the host entry point.
+struct HostPack {
+  struct Part {
+    const void* src;
+    uint64_t bytes, off, v0;  // v0 != ~0: uint64 offsets, rebased by v0 while packed
+  };
+  std::vector<Part> parts;
+  uint64_t total = 0;
+  // reserve a part; returns its offset in the staging buffers
+  uint64_t add(const void* src, uint64_t bytes, uint64_t v0 = ~0ull) {
+    total = (total + 255) & ~(uint64_t)255;
+    parts.push_back(Part{src, bytes, total, v0});
+    const uint64_t o = total;
+    total += bytes + 16;
+    return o;
+  }
+  // copy every part into pinned memory, one DMA to c->in_block on st; returns the device base
+  uint8_t* send(kh_ctx* c, hipStream_t st) {
+    c->in_block.ensure(total + 256);
+    if (!c->pack_ev) HIPCHK(hipEventCreateWithFlags(&c->pack_ev, hipEventDisableTiming));
+    if (c->pack_busy) HIPCHK(hipEventSynchronize(c->pack_ev));  // the last pack's DMA has read the buffer
+    if (c->h_pack_cap < total + 256) {
+      if (c->h_pack) HIPCHK(hipHostFree(c->h_pack));
+      c->h_pack = nullptr;
+      c->h_pack_cap = 0;
+      const size_t cap = (total + 256) * 5 / 4 + (1u << 20);
+      HIPCHK(hipHostMalloc((void**)&c->h_pack, cap, hipHostMallocDefault));
+      c->h_pack_cap = cap;
+    }
+    for (const Part& p : parts) {
+      if (!p.bytes || !p.src) continue;
+      uint8_t* dst = c->h_pack + p.off;
+      if (p.v0 == ~0ull) {
+        g_copy_pool.copy(dst, p.src, p.bytes);
+      } else {
+        const uint64_t* o = (const uint64_t*)p.src;
+        uint64_t* d = (uint64_t*)dst;
+        for (uint64_t i = 0; i < p.bytes / 8; ++i) d[i] = o[i] - p.v0;
+      }
+    }
+    uint8_t* base = (uint8_t*)c->in_block.p;
+    if (total) HIPCHK(hipMemcpyAsync(base, c->h_pack, total, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(c->pack_ev, st));
+    c->pack_busy = true;
+    return base;
+  }
+};
+
 // list-trie keys: key of item i of its trie = RLP of the integer index
 // (MptListValidator.scala:15-46, BlockGenerator.scala:157-163; RLP.scala integer
 // encoding: 0 -> 0x80, 1..127 -> the byte, else 0x80 + n and n big-endian bytes),
@@ -3667,7 +3726,15 @@ static void swap_buf(DevBuf& a, DevBuf& b) {
 
 struct kh_trie {
   kh_ctx* c = nullptr;     // the context its commits run on (kh_block_commit moves the storage phase for a call)
-  kh_ctx* home = nullptr;  // the context it was opened on: every call on the handle holds home->mu
+  kh_ctx* home = nullptr;  // the context it was opened on
+  // Handles opened through the host entry points (the shared context: the JVM's tries) run on a
+  // private context of their own (priv: streams and workspaces) and serialise on their own
+  // mutex, so commits on different handles overlap on the GPU (TxProcessor.scala:28-35 drives
+  // tries from many workers; SURVEY §8b: each handle its own HIP stream).  Handles opened on a
+  // caller's context run on it and hold its mutex (the caller owns that stream's ordering).
+  std::recursive_mutex own_mu;
+  std::recursive_mutex* lk = nullptr;  // every call on the handle holds *lk
+  kh_ctx* priv = nullptr;
   uint32_t flags = 0;  // KH_HASH_KEYS: the trie's key encoder; KH_EMIT_NODES: keep each commit's write-back set
   bool forest = false;
   uint32_t tid_bits = 0;  // forests: bits of the trie ids committed so far (+ headroom; 0: none yet)
@@ -3715,6 +3782,7 @@ struct kh_trie {
     if (ev_roots) (void)hipEventDestroy(ev_roots);
     if (pend_ev) (void)hipEventDestroy(pend_ev);
     if (pend) (void)hipHostFree(pend);
+    if (priv) (void)kh_ctx_destroy(priv);
   }
 };
 // the in-flight tail of the last commit: its map error and fresh slots (before mused is read)
@@ -3733,7 +3801,18 @@ static void trie_settle(kh_trie* h) {
 }
 
 // every entry point on a resident handle serialises on its home context (khst.h: reentrant)
-#define HANDLE_LOCK(h) std::lock_guard<std::recursive_mutex> handle_lock_((h)->home->mu)
+#define HANDLE_LOCK(h) std::lock_guard<std::recursive_mutex> handle_lock_(*(h)->lk)
+// both handles of a block commit: one mutex when they share a context, else both (std::lock:
+// no deadlock against another call locking them in the other order)
+struct PairLock {
+  std::unique_lock<std::recursive_mutex> a, b;
+  PairLock(std::recursive_mutex* x, std::recursive_mutex* y) : a(*x, std::defer_lock), b(*y, std::defer_lock) {
+    if (x == y)
+      a.lock();
+    else
+      std::lock(a, b);
+  }
+};
 
 static Recs recs_of(kh_trie* h) {
   return recs_at((uint8_t*)h->recs.p);
@@ -3990,6 +4069,7 @@ struct FCommit {  // one commit's inputs (device buffers)
   // records and the anchor map still follow): kh_block_commit's storage phase injects them
   // into the account bodies here, so the account phase need not wait for the rest
   std::function<void(hipStream_t, uint32_t)> after_roots;  // (the stream, the commit's trie count)
+  hipEvent_t inputs_ready = nullptr;  // the inputs were staged on another stream (HostPack): wait first
 };
 
 static int emit_nodes_dev(kh_ctx* c, DevBuf& out, uint64_t* n_nodes, uint64_t* rlp_len);
@@ -4029,6 +4109,7 @@ static JSeg journal_reserve(kh_trie* h, uint64_t nrec, uint64_t nmap) {
 static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   kh_ctx* c = h->c;
   hipStream_t st = c->st;
+  if (F.inputs_ready) HIPCHK(hipStreamWaitEvent(st, F.inputs_ready, 0));
   if (stats) memset(stats, 0, sizeof(*stats));
   const bool journal = !h->sps.empty();
   const uint64_t nops = F.nup + F.ndel;
@@ -4627,11 +4708,13 @@ struct Txn {
 };
 // MerklePatriciaTrie.copy (MerklePatriciaTrie.scala:556): an independent handle holding the
 // current version (records, anchor map, value heap, last roots and write-back set) in HBM
+static void make_private(kh_trie* h);
 static kh_trie* trie_copy(kh_trie* h) {
   trie_settle(h);
   std::unique_ptr<kh_trie> n(new kh_trie());
   n->c = h->c;
   n->home = h->home;
+  n->lk = &h->home->mu;
   n->flags = h->flags;
   n->forest = h->forest;
   hipStream_t st = h->c->st;
@@ -4661,6 +4744,7 @@ static kh_trie* trie_copy(kh_trie* h) {
   n->em_n = h->em_n;
   n->em_bytes = h->em_bytes;
   HIPCHK(hipStreamSynchronize(st));
+  if (h->priv) make_private(n.get());  // (a copy of a host handle commits beside it too)
   return n.release();
 }
 
@@ -4819,6 +4903,11 @@ int kh_ctx_destroy(kh_ctx* c) {
       if (e) (void)hipEventDestroy(e);
     for (auto e : c->part_ev) (void)hipEventDestroy(e);
     if (c->cs) (void)hipStreamDestroy(c->cs);
+    if (c->pack_ev) {
+      (void)hipEventSynchronize(c->pack_ev);
+      (void)hipEventDestroy(c->pack_ev);
+    }
+    if (c->h_pack) (void)hipHostFree(c->h_pack);
     if (c->own) (void)hipStreamDestroy(c->own);
     if (c->st2) (void)hipStreamDestroy(c->st2);
     delete c;
@@ -5680,10 +5769,23 @@ static kh_trie* trie_new(kh_ctx* c, uint32_t flags, bool forest) {
   kh_trie* h = new kh_trie();
   h->c = c;
   h->home = c;
+  h->lk = &c->mu;
   h->flags = flags;
   h->forest = forest;
   memcpy(h->root, EMPTY_TRIE_HASH, 32);
   return h;
+}
+// a handle of the shared context moves to a private one (kh_trie::priv) once its open has
+// completed on the shared context (its in-flight tail drained first: the private streams are
+// not ordered after the shared one)
+static void make_private(kh_trie* h) {
+  if (h->priv) return;
+  trie_settle(h);
+  HIPCHK(hipStreamSynchronize(h->c->st));
+  HIPCHK(hipStreamSynchronize(h->c->st2));
+  h->priv = ctx_new(h->home->dev);
+  h->c = h->priv;
+  h->lk = &h->own_mu;
 }
 static void check_flags(const kh_trie* h, uint32_t flags) {
   if ((flags & KH_HASH_KEYS) != (h->flags & KH_HASH_KEYS))
@@ -5753,6 +5855,13 @@ int kh_trie_open_nodes_host(const uint8_t root32[32], const uint8_t* enc, const 
     int rc = kh_trie_open_nodes(c, root32, (const uint8_t*)c->in_vals.p, (const uint64_t*)c->in_voff.p, n, flags,
                                 missing32, out);
     if (rc != KH_OK) return rc;
+    try {
+      make_private(*out);
+    } catch (...) {
+      delete *out;
+      *out = nullptr;
+      throw;
+    }
   })
 }
 
@@ -5781,6 +5890,7 @@ int kh_trie_open_host(const uint8_t* keys, uint32_t klen, const uint8_t* vals, c
       F.before_values = [&H] { H.wait(H.nkp + 1); };
       F.vals_ready = H.ev(H.nkp + 1);
       forest_commit(h, F, nullptr);
+      make_private(h);
     } catch (...) {
       delete h;
       throw;
@@ -5815,39 +5925,22 @@ int kh_trie_apply(kh_trie* h, const uint8_t* d_up_keys, const uint8_t* d_up_vals
 static FCommit stage_commit(kh_ctx* c, const uint32_t* up_trie, const uint8_t* up_keys, const uint8_t* up_vals,
                             const uint64_t* up_voff, uint64_t nup, const uint32_t* del_trie, const uint8_t* del_keys,
                             uint64_t ndel, uint32_t klen) {
-  hipStream_t st = c->st;
   const uint64_t v0 = nup ? up_voff[0] : 0, vb = nup ? up_voff[nup] - v0 : 0;
-  c->in_keys.ensure(carve_size({nup * klen, ndel * klen}));
-  c->in_vals.ensure(vb + 64);
-  c->in_voff.ensure((nup + 1) * 8 + 64);
-  c->in_seg.ensure(carve_size({nup * 4, ndel * 4}));
-  Carver ck{(char*)c->in_keys.p, 0, c->in_keys.cap};
-  uint8_t* uk = ck.take<uint8_t>(nup * klen);
-  uint8_t* dk = ck.take<uint8_t>(ndel * klen);
-  Carver cs{(char*)c->in_seg.p, 0, c->in_seg.cap};
-  uint32_t* ut = cs.take<uint32_t>(nup);
-  uint32_t* dt = cs.take<uint32_t>(ndel);
-  std::vector<uint64_t> rel(nup + 1, 0);
-  for (uint64_t i = 0; i <= nup && nup; ++i) rel[i] = up_voff[i] - v0;
-  if (nup) {
-    HIPCHK(hipMemcpyAsync(uk, up_keys, nup * klen, hipMemcpyHostToDevice, st));
-    if (vb) HIPCHK(hipMemcpyAsync(c->in_vals.p, up_vals + v0, vb, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(c->in_voff.p, rel.data(), (nup + 1) * 8, hipMemcpyHostToDevice, st));
-    if (up_trie) HIPCHK(hipMemcpyAsync(ut, up_trie, nup * 4, hipMemcpyHostToDevice, st));
-  }
-  if (ndel) {
-    HIPCHK(hipMemcpyAsync(dk, del_keys, ndel * klen, hipMemcpyHostToDevice, st));
-    if (del_trie) HIPCHK(hipMemcpyAsync(dt, del_trie, ndel * 4, hipMemcpyHostToDevice, st));
-  }
-  HIPCHK(hipStreamSynchronize(st));  // `rel` is a host temporary
+  HostPack P;
+  const uint64_t ouk = P.add(up_keys, nup * klen), odk = P.add(del_keys, ndel * klen);
+  const uint64_t ov = P.add(nup ? up_vals + v0 : nullptr, vb + (nup ? 0 : 0));
+  const uint64_t oo = P.add(up_voff, nup ? (nup + 1) * 8 : 0, v0);
+  const uint64_t out = P.add(up_trie, up_trie ? nup * 4 : 0), odt = P.add(del_trie, del_trie ? ndel * 4 : 0);
+  P.total += 64;  // (slack past the values: 8-byte word reads)
+  uint8_t* b = P.send(c, c->st);
   FCommit F;
-  F.up_trie = up_trie ? ut : nullptr;
-  F.up_keys = uk;
-  F.up_vals = (const uint8_t*)c->in_vals.p;
-  F.up_voff = (const uint64_t*)c->in_voff.p;
+  F.up_trie = up_trie ? (const uint32_t*)(b + out) : nullptr;
+  F.up_keys = b + ouk;
+  F.up_vals = b + ov;
+  F.up_voff = (const uint64_t*)(b + oo);
   F.nup = nup;
-  F.del_trie = del_trie ? dt : nullptr;
-  F.del_keys = dk;
+  F.del_trie = del_trie ? (const uint32_t*)(b + odt) : nullptr;
+  F.del_keys = b + odk;
   F.ndel = ndel;
   F.klen = klen;
   return F;
@@ -5870,8 +5963,11 @@ int kh_trie_apply_host(kh_trie* h, const uint8_t* up_keys, const uint8_t* up_val
 int kh_forest_open(kh_ctx* c, uint32_t flags, kh_trie** out) {
   if (!out) return set_err(KH_EINVAL, "null handle");
   API_TRY({
+    const bool host = !c;
     if (!c) c = shared_ctx(current_device());  // the context the *_host entry points use
-    *out = trie_new(c, flags, true);
+    std::unique_ptr<kh_trie> h(trie_new(c, flags, true));
+    if (host) make_private(h.get());
+    *out = h.release();
   })
 }
 
@@ -6027,8 +6123,8 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
                     const uint32_t* d_a_up_trie, uint64_t na_up, const uint8_t* d_a_del_keys, uint64_t na_del,
                     uint32_t a_klen, uint8_t state_root32[32], kh_stats* stats) {
   if (!state || state->forest || !storage || !storage->forest) return set_err(KH_EINVAL, "need a state trie and a forest");
-  if (state->home != storage->home) return set_err(KH_EINVAL, "state trie and forest on different contexts");
-  HANDLE_LOCK(state);
+  if (state->home->dev != storage->home->dev) return set_err(KH_EINVAL, "state trie and forest on different devices");
+  PairLock pl(state->lk, storage->lk);
   API_TRY({
     kh_ctx* c = state->c;
     HIPCHK(hipSetDevice(c->dev));
@@ -6058,6 +6154,7 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
     A.ndel = na_del;
     A.klen = a_klen;
     A.chk_msg = "an account upsert with a storage trie is not an account body";
+    if (c->pack_for_block) S.inputs_ready = A.inputs_ready = c->pack_ev;  // (host inputs: one DMA on c->st)
     // the injection's error word (never cleared: a failing call writes its own token into it)
     if (!c->ws_inject.p) {
       c->ws_inject.ensure(64);
@@ -6084,9 +6181,12 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
       }
       forest_commit(state, A, &ast);
     } else {
-      if (!c->bsub) c->bsub = ctx_new(c->dev);
+      // the storage phase on the forest's own context (private handles), or on a second context
+      // of the state trie's
+      const bool own = storage->c != c;
+      if (!own && !c->bsub) c->bsub = ctx_new(c->dev);
       if (!c->bev) HIPCHK(hipEventCreateWithFlags(&c->bev, hipEventDisableTiming));
-      kh_ctx* aux = c->bsub;
+      kh_ctx* aux = own ? storage->c : c->bsub;
       std::mutex mu;
       std::condition_variable cv;
       bool done = false, injected = false;
@@ -6175,47 +6275,36 @@ int kh_block_commit_host(kh_trie* state, kh_trie* storage, const uint32_t* s_up_
   if ((ns_up && (!s_up_trie || !s_up_voff)) || (ns_del && !s_del_trie) || (na_up && !a_up_voff))
     return set_err(KH_EINVAL, "null input");
   kh_ctx* c = state->c;
-  HANDLE_LOCK(state);
+  PairLock pl(state->lk, storage->lk);
   int rc = KH_OK;
   try {
     HIPCHK(hipSetDevice(c->dev));
     const uint64_t sv0 = ns_up ? s_up_voff[0] : 0, svb = ns_up ? s_up_voff[ns_up] - sv0 : 0;
     const uint64_t av0 = na_up ? a_up_voff[0] : 0, avb = na_up ? a_up_voff[na_up] - av0 : 0;
-    c->in_block.ensure(carve_size({ns_up * 4, ns_up * s_klen, svb + 64, (ns_up + 1) * 8, ns_del * 4, ns_del * s_klen,
-                                   na_up * a_klen, avb + 64, (na_up + 1) * 8, na_up * 4, na_del * a_klen}));
-    Carver cb{(char*)c->in_block.p, 0, c->in_block.cap};
-    uint32_t* st_ = cb.take<uint32_t>(ns_up);
-    uint8_t* sk = cb.take<uint8_t>(ns_up * s_klen);
-    uint8_t* sv = cb.take<uint8_t>(svb + 64);
-    uint64_t* so = cb.take<uint64_t>(ns_up + 1);
-    uint32_t* sdt = cb.take<uint32_t>(ns_del);
-    uint8_t* sdk = cb.take<uint8_t>(ns_del * s_klen);
-    uint8_t* ak = cb.take<uint8_t>(na_up * a_klen);
-    uint8_t* av = cb.take<uint8_t>(avb + 64);
-    uint64_t* ao = cb.take<uint64_t>(na_up + 1);
-    uint32_t* at = cb.take<uint32_t>(na_up);
-    uint8_t* adk = cb.take<uint8_t>(na_del * a_klen);
-    std::vector<uint64_t> srel(ns_up + 1, 0), arel(na_up + 1, 0);
-    for (uint64_t i = 0; ns_up && i <= ns_up; ++i) srel[i] = s_up_voff[i] - sv0;
-    for (uint64_t i = 0; na_up && i <= na_up; ++i) arel[i] = a_up_voff[i] - av0;
-    hipStream_t st = c->st;
-    auto up = [&](void* d, const void* h, uint64_t bytes) {
-      if (bytes) HIPCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
-    };
-    up(st_, s_up_trie, ns_up * 4);
-    up(sk, s_up_keys, ns_up * s_klen);
-    up(sv, s_up_vals ? s_up_vals + sv0 : nullptr, svb);
-    up(so, srel.data(), ns_up ? (ns_up + 1) * 8 : 0);
-    up(sdt, s_del_trie, ns_del * 4);
-    up(sdk, s_del_keys, ns_del * s_klen);
-    up(ak, a_up_keys, na_up * a_klen);
-    up(av, a_up_vals ? a_up_vals + av0 : nullptr, avb);
-    up(ao, arel.data(), na_up ? (na_up + 1) * 8 : 0);
-    up(at, a_up_trie, a_up_trie ? na_up * 4 : 0);
-    up(adk, a_del_keys, na_del * a_klen);
-    HIPCHK(hipStreamSynchronize(st));  // srel / arel are host temporaries
+    HostPack P;
+    const uint64_t o_st = P.add(s_up_trie, ns_up * 4), o_sk = P.add(s_up_keys, ns_up * s_klen);
+    const uint64_t o_sv = P.add(s_up_vals ? s_up_vals + sv0 : nullptr, svb), o_so = P.add(s_up_voff, ns_up ? (ns_up + 1) * 8 : 0, sv0);
+    const uint64_t o_sdt = P.add(s_del_trie, ns_del * 4), o_sdk = P.add(s_del_keys, ns_del * s_klen);
+    const uint64_t o_ak = P.add(a_up_keys, na_up * a_klen), o_av = P.add(a_up_vals ? a_up_vals + av0 : nullptr, avb);
+    const uint64_t o_ao = P.add(a_up_voff, na_up ? (na_up + 1) * 8 : 0, av0);
+    const uint64_t o_at = P.add(a_up_trie, a_up_trie ? na_up * 4 : 0), o_adk = P.add(a_del_keys, na_del * a_klen);
+    P.total += 64;
+    uint8_t* base = P.send(c, c->st);  // (the storage phase may run on another stream: pack_for_block)
+    c->pack_for_block = true;
+    uint32_t* st_ = (uint32_t*)(base + o_st);
+    uint8_t* sk = base + o_sk;
+    uint8_t* sv = base + o_sv;
+    uint64_t* so = (uint64_t*)(base + o_so);
+    uint32_t* sdt = (uint32_t*)(base + o_sdt);
+    uint8_t* sdk = base + o_sdk;
+    uint8_t* ak = base + o_ak;
+    uint8_t* av = base + o_av;
+    uint64_t* ao = (uint64_t*)(base + o_ao);
+    uint32_t* at = (uint32_t*)(base + o_at);
+    uint8_t* adk = base + o_adk;
     rc = kh_block_commit(state, storage, st_, sk, sv, so, ns_up, sdt, sdk, ns_del, s_klen, ak, av, ao,
                          a_up_trie ? at : nullptr, na_up, adk, na_del, a_klen, state_root32, stats);
+    c->pack_for_block = false;
   } catch (KhError& e) {
     return set_err(e.code, e.msg);
   } catch (std::exception& e) {
@@ -6390,11 +6479,14 @@ int kh_trie_size(const kh_trie* h, uint64_t* n) {
 
 int kh_trie_free(kh_trie* h) {
   if (!h) return KH_OK;
-  HANDLE_LOCK(h);  // (the lock is the home context's, which outlives the handle)
   API_TRY({
-    (void)hipSetDevice(h->c->dev);
-    (void)hipStreamSynchronize(h->c->st);
-    delete h;  // every DevBuf releases its HBM
+    {  // (a handle's own mutex goes with it: released before the delete)
+      HANDLE_LOCK(h);
+      (void)hipSetDevice(h->c->dev);
+      (void)hipStreamSynchronize(h->c->st);
+      (void)hipStreamSynchronize(h->c->st2);
+    }
+    delete h;  // every DevBuf releases its HBM; a private context is destroyed with it
   })
 }
 
