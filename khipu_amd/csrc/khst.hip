@@ -644,10 +644,7 @@ __device__ __forceinline__ void block_add3(unsigned long long* c0, unsigned long
 __global__ void __launch_bounds__(BS) k_branch_topo(Topo T, Pyr P, uint64_t nb) {
   topo_prio();
   unsigned long long ext = 0;
-  GRID_STRIDE(b, nb) {
-    op_branch_topo(T, P, nb, b);
-    if (T.u[b] != 0 && T.rep[b] == (uint32_t)b) ext += T.br_ext[T.isrep_bid[b]] ? 1 : 0;
-  }
+  GRID_STRIDE(b, nb) ext += op_branch_topo(T, P, nb, b);
   block_add3(ctr_stat(T.ctr, CTR_EXT, blockIdx.x), ext, nullptr, 0, nullptr, 0);
 }
 

@@ -681,13 +681,15 @@ KH_HD Parent resolve_parent(const Topo& T, int64_t a, int64_t c) {
 
 // ---- stage: branch records (thread per boundary; only reps act).  The child count
 // was left by the group's last member (op_chain): its ordinal + 2.
-KH_HD void op_branch_topo(const Topo& T, const Pyr& P, uint64_t nb, uint64_t b) {
-  if (T.u[b] == 0 || T.rep[b] != (uint32_t)b) return;
+// returns 1 when boundary b made a branch with an extension above it (k_branch_topo's
+// extension count: from the values computed here, not a second pass over u, rep and br_ext)
+KH_HD uint32_t op_branch_topo(const Topo& T, const Pyr& P, uint64_t nb, uint64_t b) {
+  if (T.u[b] == 0 || T.rep[b] != (uint32_t)b) return 0;
   uint32_t j = T.isrep_bid[b];
   uint32_t t = T.u[b];
   if (t > 64 || t < T.depth0 + 1) {  // a corrupt boundary value (see pd_scatter_vals): no depth past the level tables
     T.ctr[CTR_ERR] = ERR_LEAF_TOPO;
-    return;
+    return 0;
   }
   uint32_t d = t - 1u;
   int64_t a = T.psv[b], c = T.nsv[b];
@@ -699,6 +701,7 @@ KH_HD void op_branch_topo(const Topo& T, const Pyr& P, uint64_t nb, uint64_t b) 
   T.br_pord[j] = (uint8_t)Pp.pord;
   T.br_first[j] = (uint32_t)(a + 1);
   if (T.br_end) T.br_end[j] = c < 0 ? (uint32_t)T.m : (uint32_t)c + 1;  // boundary c follows key c
+  return (int32_t)d - Pp.pd - 1 != 0 ? 1u : 0u;
 }
 
 // ---- leaf geometry

@@ -203,12 +203,13 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
           break;
         }
     for (uint64_t b = 0; b < nb; ++b) {
-      op_branch_topo(T, P, nb, b);
+      const uint32_t xf = op_branch_topo(T, P, nb, b);
       if (ctr[CTR_ERR] == ERR_LEAF_TOPO) return -9;  // (the device: KH_EINTERNAL at the topology's counter sync)
       if (u[b] != 0 && rep[b] == b) {
         uint32_t j = isrep[b];
         hist[br_depth[j]]++;
         if (br_ext[j]) ctr[CTR_EXT]++;
+        if (xf != (br_ext[j] ? 1u : 0u)) return -8;  // (the device counts extensions from the return value)
       }
     }
   }
