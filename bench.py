@@ -47,6 +47,16 @@ sys.path.insert(0, ROOT)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 HBM_PEAK = 8.0e12
 OPS_PER_PERM = 5760  # 24 rounds x 240 int32 ops
+# The issue-rate floor of the permutation as this tree compiles it (keccak.h: 120 v_bitop3_b32,
+# 58 v_alignbit_b32 and 2 v_xor a round) at the measured cycles per wave-instruction per SIMD
+# with 8 waves per SIMD (profiles/r3zh_valu_issue_rates.txt: v_bitop3 2.61, v_alignbit 4.31 --
+# the shifts issue at half rate -- v_xor 2.70), on the same 2.4 GHz basis as the peak
+KECCAK_CYCLES_PER_WAVE_PERM = 24 * (120 * 2.61 + 58 * 4.31 + 2 * 2.70)
+
+
+def issue_floor_ms(perms):
+    """Time for `perms` permutations at the issue-rate floor (1,024 SIMDs at 2.4 GHz)."""
+    return perms / 64 * KECCAK_CYCLES_PER_WAVE_PERM / (256 * 4 * 2.4e9) * 1e3
 SEQ_SAMPLES = (20_000, 50_000, 100_000, 1_000_000)
 
 
@@ -354,7 +364,11 @@ def roofline(stats, n):
     return avg, {"kernel": dom, "bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
                  "unit": "T int32-lane-ops/s", "frac": achieved / VALU_PEAK_LANE_OPS,
                  "traffic": pmc_traffic(dom, n), "avg_ms": launch_ms, "launches_per_step": 1,
-                 "perms_per_launch": perms}
+                 "perms_per_launch": perms,
+                 "issue_floor": {"ms": issue_floor_ms(perms), "frac": issue_floor_ms(perms) / launch_ms,
+                                 "basis": "the launch's permutations alone at the measured issue rates of the "
+                                          "instructions the permutation compiles to (v_alignbit at half rate; "
+                                          "bench.py KECCAK_CYCLES_PER_WAVE_PERM)"}}
 
 
 def single(args):
@@ -394,6 +408,12 @@ def single(args):
         "topology": {k: s[k] for k in ("n_leaves", "n_branches", "n_extensions", "n_inline", "n_node_hashes",
                                        "n_node_perms", "n_key_perms", "arena_bytes", "n_levels")},
         "roofline": roof,
+        # each Keccak stage against its permutations' issue-rate floor (the leaves' and the levels'
+        # encoding work, loads and stores are on top of the floor: frac < 1 is that, plus stalls)
+        "issue_floor_by_stage": {
+            k: {"perms": p, "ms": avg[m], "floor_ms": issue_floor_ms(p), "frac": issue_floor_ms(p) / max(avg[m], 1e-9)}
+            for k, m, p in (("key_hashing", "k_hash_keys_ck", s["n_key_perms"]), ("leaves", "k_leaf_in", s["n_leaves"]),
+                            ("branch_levels", "branch_levels", s["n_node_perms"] - s["n_leaves"]))},
     }
     if not args.no_host_path:
         out["drop_in_host_path"] = host_path(addr, vals, voff, n, root)

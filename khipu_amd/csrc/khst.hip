@@ -1125,7 +1125,10 @@ __device__ __forceinline__ uint32_t row16_scan(uint32_t x) {
 // permutation runs spread over the group (keccak_xlane.h): ~3x shorter than one thread's
 // permutation, which at this occupancy is the level's latency.  Lane 0 of the group then
 // keeps and publishes the reference as op_branch_stream does.
-constexpr uint32_t XL_LEVEL = 8192;  // branches per level below which k_branch_xl runs
+#ifndef KH_XL_LEVEL
+#define KH_XL_LEVEL 8192
+#endif
+constexpr uint32_t XL_LEVEL = KH_XL_LEVEL;  // branches per level below which k_branch_xl runs
 constexpr uint32_t XL_ENC_WORDS = 68;  // 4 windows: a branch of fixed-length keys is <= 532 B
 __global__ void __launch_bounds__(64) k_branch_xl(Topo T, uint64_t first, uint64_t cnt) {
   __shared__ uint64_t enc[2][XL_ENC_WORDS];
@@ -3394,7 +3397,13 @@ __global__ void __launch_bounds__(BS) k_f_prep(const uint32_t* sidx, uint64_t n,
   isup[o] = up ? 1u : 0u;
   ulen[o] = up ? voff[s + 1] - voff[s] : 0;
 }
-constexpr uint32_t GATHER_BS = 1024;
+#ifndef KH_GATHER_BS
+#define KH_GATHER_BS 1024
+#endif
+#ifndef KH_GATHER_PER_CU
+#define KH_GATHER_PER_CU 2
+#endif
+constexpr uint32_t GATHER_BS = KH_GATHER_BS;
 __global__ void __launch_bounds__(GATHER_BS) k_f_gather(AMap M, Recs R, const uint32_t* touched, const uint8_t* replaced,
                                                  const uint32_t* tlist, const unsigned long long* ntl_p,
                                                  const uint32_t* tries, uint32_t nt, Elems E, unsigned long long* ctr) {
@@ -4151,9 +4160,11 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   // keccak'd keys, a few ops per trie: the leading 24 composite bits (the tie kernel orders the
   // rare runs past them; 2^17 ops over the 2^(sb - 2) tries the hint allows, 2^19 in one trie)
   // That assumes keys spread evenly over the tries: one hot trie with thousands of slot writes
-  // (or structured unhashed keys) makes runs past the tie kernel, and the whole sort falls back
-  // to 256 bits.  Such a fallback turns the 24-bit form off for the handle's next 16 commits.
-  if (S.sb <= 18 && nops <= (segd ? (1ull << 17) : (1ull << 19)) && h->lo24_off == 0) S.rs_lo = 40;
+  // makes runs past the tie kernel, and the whole sort falls back to 256 bits.  Such a fallback
+  // turns the 24-bit form off for the handle's next 16 commits.  Unhashed keys (structured, their
+  // leading bytes often equal) never take it.
+  if ((h->flags & KH_HASH_KEYS) && S.sb <= 18 && nops <= (segd ? (1ull << 17) : (1ull << 19)) && h->lo24_off == 0)
+    S.rs_lo = 40;
   if (h->lo24_off) --h->lo24_off;
   S.rs_scratch = cv.take<char>(radix_scratch_bytes(nops));
   S.scan_scratch = cv.take<char>(scan_scratch_bytes(nops + 1, 8));
@@ -4294,7 +4305,7 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
       hipLaunchKernelGGL(k_f_upsert_elems, GRID(nd, BS), dim3(BS), 0, st, O, (const uint32_t*)tries, nt,
                          (const uint32_t*)ur, (const uint64_t*)uo, E, hb, (uint64_t)nups, (const uint32_t*)S.sidx,
                          F.late);
-    const uint64_t gblocks = std::min<uint64_t>((uint64_t)c->n_cu * 2, (nd * 16 * 8 + GATHER_BS - 1) / GATHER_BS);
+    const uint64_t gblocks = std::min<uint64_t>((uint64_t)c->n_cu * KH_GATHER_PER_CU, (nd * 16 * 8 + GATHER_BS - 1) / GATHER_BS);
     hipLaunchKernelGGL(k_f_gather, dim3((unsigned)std::max<uint64_t>(gblocks, 1)), dim3(GATHER_BS), 0, st, map_of(h),
                        recs_of(h), (const uint32_t*)h->touched.p, (const uint8_t*)h->replaced.p,
                        (const uint32_t*)tlist, (const unsigned long long*)fctr, (const uint32_t*)tries, nt, E, fctr);
@@ -6234,6 +6245,14 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
         if (!injected) throw KhError{KH_EINTERNAL, "the block's storage phase failed"};
       };
       try {
+#ifdef KH_BC_ACCT_LOW
+        struct StSwap {
+          kh_ctx* c;
+          hipStream_t old;
+          ~StSwap() { c->st = old; }
+        } sw{c, c->st};
+        c->st = c->st2;
+#endif
         forest_commit(state, A, &ast);
       } catch (...) {
         aerr = std::current_exception();

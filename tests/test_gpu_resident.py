@@ -217,6 +217,36 @@ def test_forest_trie_id_bits(khst, oracle):
     f.close()
 
 
+@pytest.mark.parametrize("hashed", [True, False], ids=["hashed", "raw"])
+def test_forest_hot_trie(khst, oracle, hashed):
+    """A forest whose ids span 2^16 (the op sort's short 24-bit composite form is in reach) with
+    one hot contract taking ~4k slot writes per block beside ~1,500 one-op tries: the hot trie's
+    run of equal sort prefixes is past the tie kernel's limit, so the sort widens (hashed keys)
+    or never takes the short form (raw keys, whose structured leading bytes repeat); every root
+    against the oracle's tries folded put by put."""
+    from khipu_amd.device import Ctx, ResidentForest
+    r = random.Random(11)
+    f = ResidentForest(Ctx(0), hash_keys=hashed)
+    tries = {}
+    hot = 40000
+    for blk in range(3):
+        ups = []
+        for t in r.sample(range(1 << 16), 1500):
+            ups.append((t, bytes(r.getrandbits(8) for _ in range(32)), C.storage_value(r)))
+        for i in range(4000):  # raw keys of the hot trie share their first 28 bytes
+            slot = (bytes(28) + (blk * 4000 + i).to_bytes(4, "big")) if not hashed else bytes(r.getrandbits(8) for _ in range(32))
+            ups.append((hot, slot, C.storage_value(r)))
+        got = f.commit(ups, [])
+        touched = set()
+        for t, slot, v in ups:
+            tries.setdefault(t, oracle.Trie()).put(oracle.kec256(slot) if hashed else slot, v)
+            touched.add(t)
+        assert set(got) == touched, blk
+        for t in touched:
+            assert got[t] == tries[t].root_hash(), (blk, t)
+    f.close()
+
+
 @pytest.mark.parametrize("sc", C.commit_scenarios()[:4], ids=lambda s: s[0])
 def test_open_from_node_store(khst, oracle, sc):
     """kh_trie_open_nodes: a trie opened from its root hash and the
