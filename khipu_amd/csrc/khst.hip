@@ -585,8 +585,14 @@ __global__ void __launch_bounds__(TT_THREADS) k_topo_tile(Topo T, uint64_t nb, b
   __syncthreads();
   for (uint32_t k = 0; k < TOPO_TILE / TT_THREADS; ++k) {
     const uint32_t i = k * TT_THREADS + threadIdx.x;
-    const uint64_t m = __ballot(i < tn && op_tile_chain(T, P, t0, i, lpse, lnext, lrin));
+    uint32_t isr = 0;
+    const uint64_t m = __ballot(i < tn && op_tile_chain(T, P, t0, i, lpse, lnext, lrin, &isr));
     if (__lane_id() == 0) cmask[k * (TT_THREADS / 64) + wv] = m;
+    if (T.rep_bits) {  // the wave's 64 boundaries' representative flags: two bit words (every word of
+                       // the tile written; k_chain_list ORs in the listed boundaries' flags after it)
+      const uint64_t rb = __ballot(isr != 0);
+      if (__lane_id() == 0) *(uint64_t*)(T.rep_bits + ((t0 + k * TT_THREADS + 64 * wv) >> 5)) = rb;
+    }
   }
   __syncthreads();
   if (wv == 0) tile_list_out(amask, t0, &nlist[0], alist);
@@ -716,6 +722,11 @@ __global__ void __launch_bounds__(BS) k_branch_permute(Topo T, BrTab J, const ui
     if (T.br_end) T.br_end[g] = J.end[j];
     T.br_parent[g] = p == NONE ? NONE : pos[p];  // parents of neighbouring branches are neighbours
   }
+}
+// rep_pref[w] = popcount of the representative bit word w (scanned in place afterwards)
+__global__ void __launch_bounds__(BS) k_rep_popc(const uint32_t* bits, uint64_t nw, uint32_t* pref) {
+  topo_prio();
+  GRID_STRIDE(w, nw) pref[w] = (uint32_t)__popc(bits[w]);
 }
 // group reps carry level-order branch ids from here on (leaf parents, resident tables)
 __global__ void __launch_bounds__(BS) k_bid_remap(Topo T, const uint32_t* pos, uint64_t nb) {
@@ -2509,6 +2520,16 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   // block, profiles/r4w_topo_tile_block_ab_50m.json)
   constexpr uint64_t TOPO_TILE_MIN = 1u << 21;
   const bool topo_tile = nb >= TOPO_TILE_MIN;
+  // leaf-position tile builds keep the representative flags as bits (Topo::rep_bits), in the
+  // flag array's own storage (a word per 32 boundaries, every tile's 128 words written by it)
+  const bool rbits = lpos && topo_tile;
+  const uint64_t rb_words = rbits ? (nb + TOPO_TILE - 1) / TOPO_TILE * (TOPO_TILE / 32) : 0;
+  uint32_t* rb_pref = nullptr;
+  if (rbits) {
+    T.rep_bits = T.isrep_bid;
+    rb_pref = T.isrep_bid + ((rb_words + 63) & ~(uint64_t)63);
+    T.rep_pref = rb_pref;
+  }
   if (pd_scan) {  // presets for the scatter folded into the ANSV (on st)
     if (m < n) HIPCHK(hipMemsetAsync(T.pdinv, 0xFF, n * 8, st));  // dropped duplicates: PDINV_SKIP
     // every leaf a hash unless it says otherwise (k_topo_tile presets its own tile's leaves)
@@ -2609,7 +2630,14 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
       hipLaunchKernelGGL(k_chain, topo_grid(nb), dim3(BS), 0, st, T, nb);
       LAUNCH_CHECK();
     }
-    scan_exclusive<uint32_t>(T.isrep_bid, T.isrep_bid, nb, Bp, scan_scratch, st);
+    if (rbits) {  // branch ids: the prefix of the bit words' popcounts
+      hipLaunchKernelGGL(k_rep_popc, topo_grid(rb_words), dim3(BS), 0, st, (const uint32_t*)T.rep_bits, rb_words,
+                         rb_pref);
+      LAUNCH_CHECK();
+      scan_exclusive<uint32_t>(rb_pref, rb_pref, rb_words, Bp, scan_scratch, st);
+    } else {
+      scan_exclusive<uint32_t>(T.isrep_bid, T.isrep_bid, nb, Bp, scan_scratch, st);
+    }
     // branch tables in key-order ids first (k_branch_topo writes them, thread per boundary)
     Topo TJ = T;
     TJ.br_k = J.k;

@@ -171,6 +171,12 @@ struct Topo {
   uint32_t* rep;          // [m-1] group representative of b
   uint8_t* ord;           // [m-1] ordinal of b within its group
   uint32_t* isrep_bid;     // [m-1] 1 if rep, then (after scan) branch id of rep
+  // leaf-position builds with tiles (nullable): the representative flags as bits (bit b % 32 of
+  // word b / 32), written per wave by the tile kernel; a representative's branch id is
+  // rep_pref[b / 32] + the set bits below it (bid_of).  isrep_bid is not used then: the 100M-entry
+  // flag array and its scan (a write, a read, a read + write) beside the leaf kernel become 12.5 MB
+  uint32_t* rep_bits;
+  const uint32_t* rep_pref;  // [words + 1] exclusive prefix of the words' popcounts
   const uint32_t* bid_pos;  // nullable: isrep_bid holds key-order ids, their level positions (leaf-position builds skip k_bid_remap)
   uint8_t* glast;         // [nb] 1 unless a later boundary of the same group exists (preset 1)
   uint8_t* gk;            // [nb] at a group's representative: its branch's child count
@@ -512,13 +518,35 @@ KH_HD void op_ansv(const Topo& T, const Pyr& P, uint64_t b) {
   T.nsv[b] = (int32_t)ansv_right(P, b, t);
 }
 
+// representative flags in bit form (Topo::rep_bits)
+KH_HD uint32_t kh_popc(uint32_t x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return (uint32_t)__popc(x);
+#else
+  return (uint32_t)__builtin_popcount(x);
+#endif
+}
+KH_HD void rep_bit_set(const Topo& T, uint64_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+  atomicOr(&T.rep_bits[b >> 5], 1u << (b & 31));  // (k_chain_list: after the tile kernel wrote the word)
+#else
+  T.rep_bits[b >> 5] |= 1u << (b & 31);
+#endif
+}
+// key-order branch id of representative boundary b
+KH_HD uint32_t bid_of(const Topo& T, uint64_t b) {
+  if (!T.rep_bits) return T.isrep_bid[b];
+  const uint64_t w = b >> 5;
+  return T.rep_pref[w] + kh_popc(T.rep_bits[w] & ((1u << (b & 31)) - 1u));
+}
+
 // ---- stage: group representative and ordinal (walk the PSE chain, <= 14 steps)
 KH_HD void op_chain(const Topo& T, uint64_t b) {
   uint32_t t = T.u[b];
   if (t == 0) {
     T.rep[b] = NONE;
     T.ord[b] = 0;
-    T.isrep_bid[b] = 0;
+    if (!T.rep_bits) T.isrep_bid[b] = 0;
     return;
   }
   int64_t j = (int64_t)b;
@@ -534,7 +562,10 @@ KH_HD void op_chain(const Topo& T, uint64_t b) {
   }
   T.rep[b] = (uint32_t)j;
   T.ord[b] = (uint8_t)o;
-  T.isrep_bid[b] = (o == 0) ? 1u : 0u;
+  if (!T.rep_bits)
+    T.isrep_bid[b] = (o == 0) ? 1u : 0u;
+  else if (o == 0)
+    rep_bit_set(T, b);
   if (T.glast[b]) T.gk[j] = (uint8_t)(o + 2);  // the group's last member: the branch has o + 2 children
 }
 
@@ -614,14 +645,15 @@ KH_HD bool op_tile_ansv(const Topo& T, const TilePyr& P, uint64_t t0, uint32_t i
 }
 // phase 2 (after phase 1 on the whole tile): the chain walk over the tile's links; returns true
 // when op_chain must redo it: the walk leaves the tile, or b has no later member in the tile
-// while its group's range does (it may be the group's last or not)
+// while its group's range does (it may be the group's last or not).  With T.rep_bits the
+// representative flag goes to *isrep (the caller packs the wave's flags into the bit words).
 KH_HD bool op_tile_chain(const Topo& T, const TilePyr& P, uint64_t t0, uint32_t i, const int16_t* lpse,
-                         const uint8_t* lnext, const uint8_t* lrin) {
+                         const uint8_t* lnext, const uint8_t* lrin, uint32_t* isrep) {
   const uint64_t b = t0 + i;
   if (P.l0[i] == 0) {
     T.rep[b] = NONE;
     T.ord[b] = 0;
-    T.isrep_bid[b] = 0;
+    if (!T.rep_bits) T.isrep_bid[b] = 0;
     return false;
   }
   uint32_t j = i, o = 0;
@@ -639,7 +671,10 @@ KH_HD bool op_tile_chain(const Topo& T, const TilePyr& P, uint64_t t0, uint32_t 
   if (last && !lrin[j]) return true;
   T.rep[b] = (uint32_t)(t0 + j);
   T.ord[b] = (uint8_t)o;
-  T.isrep_bid[b] = o == 0 ? 1u : 0u;
+  if (T.rep_bits)
+    *isrep = o == 0 ? 1u : 0u;
+  else
+    T.isrep_bid[b] = o == 0 ? 1u : 0u;
   if (last) T.gk[t0 + j] = (uint8_t)(o + 2);  // the group's last member: o + 2 children
   return false;
 }
@@ -656,8 +691,8 @@ KH_HD Parent resolve_parent(const Topo& T, int64_t a, int64_t c) {
   const uint32_t va = a >= 0 ? T.u[a] : 0, vc = c >= 0 ? T.u[c] : 0;
   const uint32_t ra = a >= 0 ? T.rep[a] : NONE, rc = c >= 0 ? T.rep[c] : NONE;
   const uint32_t oa = a >= 0 ? T.ord[a] : 0, oc = c >= 0 ? T.ord[c] : 0;
-  uint32_t ba = (va && ra != NONE) ? T.isrep_bid[ra] : NONE;
-  uint32_t bc = (vc && rc != NONE) ? T.isrep_bid[rc] : NONE;
+  uint32_t ba = (va && ra != NONE) ? bid_of(T, ra) : NONE;
+  uint32_t bc = (vc && rc != NONE) ? bid_of(T, rc) : NONE;
   if (T.bid_pos) {
     if (ba != NONE) ba = T.bid_pos[ba];
     if (bc != NONE) bc = T.bid_pos[bc];
@@ -685,7 +720,7 @@ KH_HD Parent resolve_parent(const Topo& T, int64_t a, int64_t c) {
 // extension count: from the values computed here, not a second pass over u, rep and br_ext)
 KH_HD uint32_t op_branch_topo(const Topo& T, const Pyr& P, uint64_t nb, uint64_t b) {
   if (T.u[b] == 0 || T.rep[b] != (uint32_t)b) return 0;
-  uint32_t j = T.isrep_bid[b];
+  uint32_t j = bid_of(T, b);
   uint32_t t = T.u[b];
   if (t > 64 || t < T.depth0 + 1) {  // a corrupt boundary value (see pd_scatter_vals): no depth past the level tables
     T.ctr[CTR_ERR] = ERR_LEAF_TOPO;

@@ -43,8 +43,11 @@ static void topo_tiles(const Topo& T, const Pyr& P, uint64_t nb, uint32_t tile) 
     const TilePyr L{su.data(), sl1.data(), tn, (tn + 63) / 64};
     for (uint32_t i = 0; i < tn; ++i)
       if (op_tile_ansv(T, L, t0, i, lpse.data(), lnext.data(), lrin.data())) alist.push_back((uint32_t)(t0 + i));
-    for (uint32_t i = 0; i < tn; ++i)
-      if (op_tile_chain(T, L, t0, i, lpse.data(), lnext.data(), lrin.data())) clist.push_back((uint32_t)(t0 + i));
+    for (uint32_t i = 0; i < tn; ++i) {
+      uint32_t isr = 0;
+      if (op_tile_chain(T, L, t0, i, lpse.data(), lnext.data(), lrin.data(), &isr)) clist.push_back((uint32_t)(t0 + i));
+      if (T.rep_bits && isr) T.rep_bits[(t0 + i) >> 5] |= 1u << ((t0 + i) & 31);  // (the device's per-wave ballot words)
+    }
   }
   for (uint32_t b : alist) op_ansv(T, P, b);
   for (uint32_t b : clist) op_chain(T, b);
@@ -187,13 +190,27 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       P.sz[P.nl] = nout;
       P.nl++;
     }
+    // leaf positions: the representative flags as bits, as the device's tile builds keep them
+    const uint64_t nw = (nb + 31) / 32 + 1;
+    std::vector<uint32_t> rbits(nw, 0), rpref(nw + 1, 0);
+    if (lpos) {
+      T.rep_bits = rbits.data();
+      T.rep_pref = rpref.data();
+    }
     topo_tiles(T, P, nb, TOPO_TILE);  // (as on the device)
     if (ctr[CTR_ERR]) return -5;
     uint32_t run = 0;
-    for (uint64_t b = 0; b < nb; ++b) {
-      uint32_t f = isrep[b];
-      isrep[b] = run;
-      run += f;
+    if (lpos) {
+      for (uint64_t w = 0; w < nw; ++w) {
+        rpref[w] = run;
+        run += (uint32_t)__builtin_popcount(rbits[w]);
+      }
+    } else {
+      for (uint64_t b = 0; b < nb; ++b) {
+        uint32_t f = isrep[b];
+        isrep[b] = run;
+        run += f;
+      }
     }
     B = run;
     if (g_inject == 2)  // the first representative boundary from g_inject_j on
@@ -206,7 +223,7 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       const uint32_t xf = op_branch_topo(T, P, nb, b);
       if (ctr[CTR_ERR] == ERR_LEAF_TOPO) return -9;  // (the device: KH_EINTERNAL at the topology's counter sync)
       if (u[b] != 0 && rep[b] == b) {
-        uint32_t j = isrep[b];
+        uint32_t j = bid_of(T, b);
         hist[br_depth[j]]++;
         if (br_ext[j]) ctr[CTR_EXT]++;
         if (xf != (br_ext[j] ? 1u : 0u)) return -8;  // (the device counts extensions from the return value)
