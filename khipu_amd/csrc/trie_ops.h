@@ -719,8 +719,15 @@ KH_HD Parent resolve_parent(const Topo& T, int64_t a, int64_t c) {
 // returns 1 when boundary b made a branch with an extension above it (k_branch_topo's
 // extension count: from the values computed here, not a second pass over u, rep and br_ext)
 KH_HD uint32_t op_branch_topo(const Topo& T, const Pyr& P, uint64_t nb, uint64_t b) {
-  if (T.u[b] == 0 || T.rep[b] != (uint32_t)b) return 0;
-  uint32_t j = bid_of(T, b);
+  uint32_t j;
+  if (T.rep_bits) {  // (the bit words, 12.5 MB at 100M, instead of every boundary's value and rep)
+    const uint32_t wd = T.rep_bits[b >> 5], below = wd & ((1u << (b & 31)) - 1u);
+    if (!((wd >> (b & 31)) & 1u)) return 0;
+    j = T.rep_pref[b >> 5] + kh_popc(below);
+  } else {
+    if (T.u[b] == 0 || T.rep[b] != (uint32_t)b) return 0;
+    j = T.isrep_bid[b];
+  }
   uint32_t t = T.u[b];
   if (t > 64 || t < T.depth0 + 1) {  // a corrupt boundary value (see pd_scatter_vals): no depth past the level tables
     T.ctr[CTR_ERR] = ERR_LEAF_TOPO;
