@@ -539,7 +539,7 @@ __device__ __forceinline__ void tile_list_out(const uint64_t* mask, uint64_t t0,
   for (uint64_t r = m; r; r &= r - 1) list[s++] = (uint32_t)(t0 + 64 * lane + (uint32_t)__ffsll((long long)r) - 1);
 }
 __global__ void __launch_bounds__(TT_THREADS) k_topo_tile(Topo T, uint64_t nb, bool pd, unsigned long long* nlist,
-                                                         uint32_t* alist, uint32_t* clist) {
+                                                         uint32_t* alist, uint32_t* clist, uint8_t* pyr1) {
   __shared__ __align__(16) uint8_t su[TOPO_TILE + 16];
   __shared__ __align__(16) uint8_t sl1[64 + 16];
   __shared__ int16_t lpse[TOPO_TILE];
@@ -573,6 +573,9 @@ __global__ void __launch_bounds__(TT_THREADS) k_topo_tile(Topo T, uint64_t nb, b
     uint32_t mn = 0x7F;
     for (uint32_t q = 0; q < 64; ++q) mn = min(mn, (uint32_t)su[64 * threadIdx.x + q]);
     sl1[threadIdx.x] = (uint8_t)mn;
+    // the whole-array pyramid's first level is these minima (op_min64 over the same 64 values;
+    // past nb the tile holds 0x7F, above every boundary value): k_pyramid starts one level up
+    if (pyr1 && 64 * threadIdx.x < tn) pyr1[t0 / 64 + threadIdx.x] = (uint8_t)mn;
   }
   __syncthreads();
   const TilePyr P{su, sl1, tn, (tn + 63) / 64};
@@ -2589,11 +2592,10 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
       P.nl++;
       pp += (nout + 255) & ~(uint64_t)255;
     }
-    auto pyramid = [&] {
-      if (P.nl > 1) {  // the levels in one launch (the last block to finish the first does the rest),
-                       // after a launch per level while the next one is too big for one block
-                       // (100M keys: level 2 has 24k entries, ~0.9 ms for a lone block)
-        int from = 1;
+    auto pyramid = [&](int from) {  // (from 2: the tile kernel wrote level 1)
+      if (P.nl > from) {  // the levels in one launch (the last block to finish the first does the rest),
+                          // after a launch per level while the next one is too big for one block
+                          // (100M keys: level 2 has 24k entries, ~0.9 ms for a lone block)
         for (; from + 1 < P.nl && P.sz[from + 1] > 4 * BS; ++from) {
           hipLaunchKernelGGL(k_pyramid, GRID(P.sz[from], BS), dim3(BS), 0, st, P, from, (unsigned int*)nullptr);
           LAUNCH_CHECK();
@@ -2610,17 +2612,17 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
       // tile (k_ansv_list / k_chain_list over the whole pyramid) run beside the leaves
       unsigned long long* tcnt = ctr + CTR_TLIST;
       hipLaunchKernelGGL(k_topo_tile, dim3((unsigned)((nb + TOPO_TILE - 1) / TOPO_TILE)), dim3(TT_THREADS), 0, st, T,
-                         nb, pd_scan, tcnt, tlist_a, tlist_c);
+                         nb, pd_scan, tcnt, tlist_a, tlist_c, P.nl > 1 ? (uint8_t*)P.lv[1] : (uint8_t*)nullptr);
       LAUNCH_CHECK();
       if (pd_scan) launch_leaves(false);
-      pyramid();
+      pyramid(2);
       hipLaunchKernelGGL(k_ansv_list, topo_grid(nb / 16 + 1), dim3(BS), 0, st, T, P, (const uint32_t*)tlist_a,
                          (const unsigned long long*)tcnt);
       hipLaunchKernelGGL(k_chain_list, topo_grid(nb / 16 + 1), dim3(BS), 0, st, T, (const uint32_t*)tlist_c,
                          (const unsigned long long*)(tcnt + 1));
       LAUNCH_CHECK();
     } else {
-      pyramid();
+      pyramid(1);
       if (pd_scan)
         hipLaunchKernelGGL(k_ansv_pd, GRID(m, BS), dim3(BS), 0, st, T, P, nb);
       else

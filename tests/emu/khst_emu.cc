@@ -23,7 +23,10 @@
 using namespace khst;
 
 // The device's tile-local topology (khst.hip k_topo_tile, then k_ansv_list / k_chain_list
-// after the whole-array pyramid P) replayed tile by tile with tiles of `tile` boundaries
+// after the whole-array pyramid P) replayed tile by tile with tiles of `tile` boundaries.  With
+// the device's tile size the tile's 64-boundary minima must be the pyramid's first level (the
+// device's tile kernel writes that level; k_pyramid starts above it): g_pyr1_bad counts misses.
+static uint64_t g_pyr1_bad = 0;
 static void topo_tiles(const Topo& T, const Pyr& P, uint64_t nb, uint32_t tile) {
   std::vector<uint32_t> alist, clist;
   std::vector<uint8_t> su(TOPO_TILE + 16), sl1(64 + 16);
@@ -39,6 +42,7 @@ static void topo_tiles(const Topo& T, const Pyr& P, uint64_t nb, uint32_t tile) 
       uint32_t mn = 0x7F;
       for (uint32_t q = 0; q < 64 && 64 * w + q < TOPO_TILE; ++q) mn = std::min(mn, (uint32_t)su[64 * w + q]);
       sl1[w] = (uint8_t)mn;
+      if (tile == TOPO_TILE && P.nl > 1 && 64 * w < tn && P.lv[1][t0 / 64 + w] != (uint8_t)mn) ++g_pyr1_bad;
     }
     const TilePyr L{su.data(), sl1.data(), tn, (tn + 63) / 64};
     for (uint32_t i = 0; i < tn; ++i)
@@ -197,8 +201,10 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       T.rep_bits = rbits.data();
       T.rep_pref = rpref.data();
     }
+    g_pyr1_bad = 0;
     topo_tiles(T, P, nb, TOPO_TILE);  // (as on the device)
     if (ctr[CTR_ERR]) return -5;
+    if (g_pyr1_bad) return -10;
     uint32_t run = 0;
     if (lpos) {
       for (uint64_t w = 0; w < nw; ++w) {
