@@ -626,13 +626,11 @@ KH_HD bool op_tile_ansv(const Topo& T, const TilePyr& P, uint64_t t0, uint32_t i
   if (P.l0[j] == t) {  // the previous member of b's group
     lpse[i] = (int16_t)j;
     lnext[j] = 1;
-    T.pse[b] = (int32_t)(t0 + j);
     T.glast[t0 + j] = 0;
-    return false;
+    return false;  // (T.pse[b]: phase 2, only where a walk from outside the tile can read it)
   }
   // the group's first member: its range ends at the next strictly smaller boundary
   lpse[i] = -1;
-  T.pse[b] = -1;
   T.psv[b] = (int32_t)(t0 + j);
   const int64_t q = tile_right(P, i, t);
   if (q < 0) {
@@ -656,10 +654,20 @@ KH_HD bool op_tile_chain(const Topo& T, const TilePyr& P, uint64_t t0, uint32_t 
     if (!T.rep_bits) T.isrep_bid[b] = 0;
     return false;
   }
+  // b's link in global memory (phase 1 left it in LDS): only for groups that leave the tile, whose
+  // members op_chain may walk from a listed boundary; a group inside the tile is never walked again
+  // (0.4 GB of writes less on the critical path at 100M)
+  const int16_t own = lpse[i];
+  auto keep_link = [&] {
+    if (own != LP_OPEN) T.pse[b] = own < 0 ? -1 : (int32_t)(t0 + (uint32_t)own);
+  };
   uint32_t j = i, o = 0;
   for (;;) {
     const int16_t p = lpse[j];
-    if (p == LP_OPEN) return true;
+    if (p == LP_OPEN) {
+      keep_link();
+      return true;
+    }
     if (p < 0) break;
     j = (uint32_t)p;
     if (++o > 15) {  // impossible for a 16-ary trie: flag corruption
@@ -668,6 +676,7 @@ KH_HD bool op_tile_chain(const Topo& T, const TilePyr& P, uint64_t t0, uint32_t 
     }
   }
   const bool last = !lnext[i];
+  if (!lrin[j]) keep_link();
   if (last && !lrin[j]) return true;
   T.rep[b] = (uint32_t)(t0 + j);
   T.ord[b] = (uint8_t)o;
