@@ -458,9 +458,17 @@ __global__ void __launch_bounds__(BS) k_el_gather3(Topo T, const uint8_t* db, co
 // with the full sort).  Such a run is left unordered and unvalued, so its boundaries get 0 (as
 // between repeated keys: each key of the run a trie of its own) -- whatever the buffer held
 // from an earlier build would shape a topology whose leaf depths leave 0..63.
-__global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb, bool ties_u, const unsigned long long* tie) {
+// spec_clear: a speculative 64-bit composite sort (element builds) that met a run too long for the
+// tie kernel left it unordered: every boundary 0 (each element a trie top; no branch) until the
+// build is redone after its first sync
+__global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb, bool ties_u, const unsigned long long* tie,
+                                            bool spec_clear) {
   uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (b >= nb) return;
+  if (spec_clear && (*tie & 1)) {
+    T.u[b] = 0;
+    return;
+  }
   if (ties_u && T.sck[b] == T.sck[b + 1]) {
     if (*tie & 1) T.u[b] = 0;
     return;
@@ -2030,7 +2038,7 @@ struct SortIO {
 };
 static void sort_dedup(kh_ctx* c, SortIO& S) {
   hipStream_t st = c->st;
-  if (S.chk && S.ck_path) throw KhError{KH_EINTERNAL, "sort: a check word on the prefix path"};
+  if (S.chk && (S.ck_path || S.speculate)) throw KhError{KH_EINTERNAL, "sort: a check word on a speculative sort"};
   const uint64_t n = S.n;
   const uint64_t* K32 = S.K32;
   const uint32_t* seg = S.seg;
@@ -2130,6 +2138,12 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
     hipLaunchKernelGGL(k_tie_fix, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)cks, n, skey, idxs, sseg, S.kn,
                        T.ctr + CTR_TIE, (uint32_t)S.rs_lo);
     LAUNCH_CHECK();
+    if (S.speculate) {  // (element builds: distinct keys, exact segment bits; a long run is read at
+                        // the build's first sync, CTR_TIE, and the build redone -- no sync here)
+      tie_flags = 0;
+      ndup = 0;
+      return;
+    }
     HIPCHK(hipMemcpyAsync(c->h_pinned + 2, T.ctr + CTR_NDUP, 16, hipMemcpyDeviceToHost, st));  // [2] dups, [3] flags
     if (S.chk) HIPCHK(hipMemcpyAsync(c->h_pinned + 1, S.chk, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -2417,7 +2431,10 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   if (stage_ev) HIPCHK(hipEventRecord(c->ev[1], st));
 
   // ---- 2. sort + dedup
-  const bool spec = ck_path && !A.no_spec && c->spec_off == 0;
+  // speculative sorts (no sync for the tie kernel's flags): the plain path's 32-bit words, and the
+  // element builds' composite sort (a forest commit's elements are distinct keys, their segment
+  // bits exact: only a run past the tie kernel, rare, redoes the build)
+  const bool spec = (ck_path || (A.el && !A.kn)) && !A.no_spec && c->spec_off == 0;
   if (c->spec_off) --c->spec_off;
   uint64_t m = n;
   uint32_t* sidx = nullptr;
@@ -2544,7 +2561,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
                          T, nb, (const unsigned long long*)(ctr + CTR_TIE), tsh);
     else
       hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb, ties_u,
-                         (const unsigned long long*)(ctr + CTR_TIE));
+                         (const unsigned long long*)(ctr + CTR_TIE), spec && !ck_path);
     LAUNCH_CHECK();
   }
   // host inputs still arriving (A.hs): the leaf launch on st2 waits until the stager has recorded
