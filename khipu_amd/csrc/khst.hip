@@ -2540,9 +2540,9 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   // block, profiles/r4w_topo_tile_block_ab_50m.json)
   constexpr uint64_t TOPO_TILE_MIN = 1u << 21;
   const bool topo_tile = nb >= TOPO_TILE_MIN;
-  // leaf-position tile builds keep the representative flags as bits (Topo::rep_bits), in the
-  // flag array's own storage (a word per 32 boundaries, every tile's 128 words written by it)
-  const bool rbits = lpos && topo_tile;
+  // early tile builds keep the representative flags as bits (Topo::rep_bits), in the flag
+  // array's own storage (a word per 32 boundaries, every tile's 128 words written by it)
+  const bool rbits = early && topo_tile;
   const uint64_t rb_words = rbits ? (nb + TOPO_TILE - 1) / TOPO_TILE * (TOPO_TILE / 32) : 0;
   uint32_t* rb_pref = nullptr;
   if (rbits) {
@@ -2683,8 +2683,9 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     hipLaunchKernelGGL(k_branch_permute, topo_grid(nb), dim3(BS), 0, st, T, J, (const uint32_t*)order,
                        (const uint32_t*)Bp);
     LAUNCH_CHECK();
-    if (lpos) {  // (only the few long and top leaves resolve a parent later: through the order itself,
-                 // not a 100M-boundary remap pass beside the leaf kernel)
+    if (lpos || rbits) {  // (leaf positions: only the few long and top leaves resolve a parent later;
+                          // segmented early builds' leaf links do, one more lookup each: through the
+                          // order itself, not a 100M-boundary remap pass beside the leaf kernel)
       T.bid_pos = order;
     } else {
       hipLaunchKernelGGL(k_bid_remap, topo_grid(nb), dim3(BS), 0, st, T, (const uint32_t*)order, nb);

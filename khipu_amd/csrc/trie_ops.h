@@ -171,7 +171,7 @@ struct Topo {
   uint32_t* rep;          // [m-1] group representative of b
   uint8_t* ord;           // [m-1] ordinal of b within its group
   uint32_t* isrep_bid;     // [m-1] 1 if rep, then (after scan) branch id of rep
-  // leaf-position builds with tiles (nullable): the representative flags as bits (bit b % 32 of
+  // early builds with tiles (nullable): the representative flags as bits (bit b % 32 of
   // word b / 32), written per wave by the tile kernel; a representative's branch id is
   // rep_pref[b / 32] + the set bits below it (bid_of).  isrep_bid is not used then: the 100M-entry
   // flag array and its scan (a write, a read, a read + write) beside the leaf kernel become 12.5 MB

@@ -169,6 +169,11 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
   }
   std::vector<std::vector<uint8_t>> pyr;
   Pyr P{};
+  // the representative flags as bits, as the device's early tile builds keep them (the branch ids
+  // stay in key order here: the replay's levels list them by depth, no permutation); they live
+  // for the whole build (the leaves resolve their parents through them)
+  const uint64_t nw = (nb + 31) / 32 + 1;
+  std::vector<uint32_t> rbits(nw, 0), rpref(nw + 1, 0);
   // unsegmented builds take the device's ck path: boundary values from the sorted first
   // key words (the input keys past them), before the sorted keys are used
   std::vector<uint64_t> kin(4 * n + 4);
@@ -194,29 +199,16 @@ static int build_core(const uint8_t* keys, const uint8_t* vals, const uint64_t* 
       P.sz[P.nl] = nout;
       P.nl++;
     }
-    // leaf positions: the representative flags as bits, as the device's tile builds keep them
-    const uint64_t nw = (nb + 31) / 32 + 1;
-    std::vector<uint32_t> rbits(nw, 0), rpref(nw + 1, 0);
-    if (lpos) {
-      T.rep_bits = rbits.data();
-      T.rep_pref = rpref.data();
-    }
+    T.rep_bits = rbits.data();
+    T.rep_pref = rpref.data();
     g_pyr1_bad = 0;
     topo_tiles(T, P, nb, TOPO_TILE);  // (as on the device)
     if (ctr[CTR_ERR]) return -5;
     if (g_pyr1_bad) return -10;
     uint32_t run = 0;
-    if (lpos) {
-      for (uint64_t w = 0; w < nw; ++w) {
-        rpref[w] = run;
-        run += (uint32_t)__builtin_popcount(rbits[w]);
-      }
-    } else {
-      for (uint64_t b = 0; b < nb; ++b) {
-        uint32_t f = isrep[b];
-        isrep[b] = run;
-        run += f;
-      }
+    for (uint64_t w = 0; w < nw; ++w) {
+      rpref[w] = run;
+      run += (uint32_t)__builtin_popcount(rbits[w]);
     }
     B = run;
     if (g_inject == 2)  // the first representative boundary from g_inject_j on
