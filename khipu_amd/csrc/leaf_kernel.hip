@@ -45,12 +45,7 @@ constexpr uint32_t LEAF_ITEMS = 4;  // (khst.hip sizes the grid with the same va
 #else
 #define KH_LEAF_ENTRY() ((void)0)
 #endif
-#ifdef KH_LEAF_WAVES  // (measurement builds: a register budget for N waves per SIMD)
-#define KH_LEAF_ATTR __attribute__((amdgpu_waves_per_eu(KH_LEAF_WAVES, 8)))
-#else
-#define KH_LEAF_ATTR
-#endif
-__global__ void __launch_bounds__(BS) KH_LEAF_ATTR k_leaf_in(Topo T, uint64_t n) {
+__global__ void __launch_bounds__(BS) k_leaf_in(Topo T, uint64_t n) {
   KH_LEAF_ENTRY();
   auto wave = [](bool use, uint32_t e, uint32_t llo, uint32_t lhi) {
     WaveBounds b;
