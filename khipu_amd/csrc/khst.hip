@@ -182,9 +182,14 @@ __global__ void __launch_bounds__(BS) k_sseg_from_ck(const uint32_t* sck, uint64
 // composite sort key: segment id in the top sb bits, then the key's leading bits (big-endian)
 // (flags, nullable: |= 4 when a segment id needs more than sb bits -- a forest commit's sb is
 // a hint from the trie ids seen before; the sort is then redone with 32)
+// (rs_hdr, nullable: the radix sort's header zeroed here -- radix_sort_pairs then skips its fill
+// launch; disjoint from everything else this kernel writes)
 __global__ void __launch_bounds__(BS) k_make_ck(const uint64_t* K, const uint32_t* seg, uint32_t sb, uint64_t n,
-                                                uint64_t* ck, uint32_t* idx, unsigned long long* flags) {
+                                                uint64_t* ck, uint32_t* idx, unsigned long long* flags,
+                                                uint32_t* rs_hdr) {
   uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  if (rs_hdr)
+    for (uint64_t w = i; w < RS_HDR_BYTES / 4; w += (uint64_t)gridDim.x * BS) rs_hdr[w] = 0;
   if (i >= n) return;
   uint64_t be = bswap64(K[4 * i]);
   uint64_t c = be;
@@ -462,9 +467,10 @@ __global__ void __launch_bounds__(BS) k_el_gather3(Topo T, const uint8_t* db, co
 // tie kernel left it unordered: every boundary 0 (each element a trie top; no branch) until the
 // build is redone after its first sync
 __global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb, bool ties_u, const unsigned long long* tie,
-                                            bool spec_clear) {
+                                            bool spec_clear, bool glast) {
   uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (b >= nb) return;
+  if (glast) T.glast[b] = 1;  // (the whole-array topology's preset: no fill launch before it)
   if (spec_clear && (*tie & 1)) {
     T.u[b] = 0;
     return;
@@ -478,10 +484,13 @@ __global__ void __launch_bounds__(BS) k_lcp(Topo T, uint64_t nb, bool ties_u, co
 // every boundary was valued by the tie kernel: only a run too long for it (flag bit 0: a
 // speculative build about to be redone) gets its boundaries cleared, as in k_lcp
 __global__ void __launch_bounds__(BS) k_lcp_long_runs(Topo T, uint64_t nb, const unsigned long long* tie,
-                                                      uint32_t tsh) {
-  if (!(*tie & 1)) return;
-  for (uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * BS)
-    if ((T.sck[b] >> tsh) == (T.sck[b + 1] >> tsh)) T.u[b] = 0;
+                                                      uint32_t tsh, bool glast) {
+  const bool run = *tie & 1;
+  if (!run && !glast) return;
+  for (uint64_t b = (uint64_t)blockIdx.x * BS + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * BS) {
+    if (glast) T.glast[b] = 1;  // (the whole-array topology's preset: no fill launch before it)
+    if (run && (T.sck[b] >> tsh) == (T.sck[b + 1] >> tsh)) T.u[b] = 0;
+  }
 }
 // the 64-ary min pyramid over the boundary values: level `from` by the whole grid, the
 // (small) upper levels by the last block to finish (the counter *done starts at zero;
@@ -2125,10 +2134,10 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
   auto sort_prefix = [&] {
     if (!S.ck_ready) {
       hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, sbu, n, ck0, idx0,
-                         T.ctr + CTR_TIE);
+                         T.ctr + CTR_TIE, (uint32_t*)rs_scratch);
       LAUNCH_CHECK();
     }
-    bool flip = radix_sort_pairs<uint64_t>(ck0, idx0, ck1, idx1, n, S.rs_lo, 64, rs_scratch, st);
+    bool flip = radix_sort_pairs<uint64_t>(ck0, idx0, ck1, idx1, n, S.rs_lo, 64, rs_scratch, st, !S.ck_ready);
     cks = flip ? ck1 : ck0;
     idxs = flip ? idx1 : idx0;
     LAUNCH_CHECK();
@@ -2171,7 +2180,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
     uint64_t* ka = ck0;
     uint64_t* kb = ck1;
     hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, 0u, n, ka, ia,
-                       (unsigned long long*)nullptr);
+                       (unsigned long long*)nullptr, (uint32_t*)nullptr);
     LAUNCH_CHECK();
     auto pass = [&](int word, int bits) {
       if (word >= 0)
@@ -2558,10 +2567,10 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
   if (nb > 0) {
     if (all_u)
       hipLaunchKernelGGL(k_lcp_long_runs, dim3((unsigned)std::min<uint64_t>((nb + BS - 1) / BS, 1024)), dim3(BS), 0, st,
-                         T, nb, (const unsigned long long*)(ctr + CTR_TIE), tsh);
+                         T, nb, (const unsigned long long*)(ctr + CTR_TIE), tsh, !topo_tile);
     else
       hipLaunchKernelGGL(k_lcp, GRID(nb, BS), dim3(BS), 0, st, T, nb, ties_u,
-                         (const unsigned long long*)(ctr + CTR_TIE), spec && !ck_path);
+                         (const unsigned long long*)(ctr + CTR_TIE), spec && !ck_path, !topo_tile);
     LAUNCH_CHECK();
   }
   // host inputs still arriving (A.hs): the leaf launch on st2 waits until the stager has recorded
@@ -2621,8 +2630,7 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
         LAUNCH_CHECK();
       }
     };
-    // (k_topo_tile presets its own tile's boundaries)
-    if (!topo_tile) HIPCHK(hipMemsetAsync(T.glast, 1, (nb + 15) & ~(uint64_t)15, st));  // (whole 16-byte words)
+    // (k_topo_tile presets its own tile's boundaries; below it k_lcp / k_lcp_long_runs do)
     if (topo_tile) {
       // ANSV and chains tile by tile in LDS (k_topo_tile, the early leaves' parent depths with
       // them); the leaves start right after it; the few boundaries whose answers leave their

@@ -474,9 +474,10 @@ inline size_t radix_scratch_bytes(uint64_t n) {  // (64-bit keys: the most tiles
 // Sorts (k0, v0) on bits [lo_bit, hi_bit) (multiples of 8, at most 64 bits), using (k1, v1)
 // as ping-pong buffers.  Returns true if the result ended in (k1, v1).  n must be < 2^32.
 // Launches: a fill of the scratch header, the digit count, one per pass.
+// hdr_zeroed: the caller's previous kernel zeroed the scratch header (RS_HDR_BYTES): no fill launch
 template <typename K>
 inline bool radix_sort_pairs(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n, int lo_bit, int hi_bit,
-                             void* scratch, hipStream_t st) {
+                             void* scratch, hipStream_t st, bool hdr_zeroed = false) {
   if (n <= 1 || hi_bit <= lo_bit) return false;
   const int items = radix_items(n, sizeof(K));
   const uint64_t tiles = radix_tiles(n, sizeof(K));
@@ -485,7 +486,7 @@ inline bool radix_sort_pairs(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t 
   uint32_t* ticket = ghist + RS_MAX_PASSES * 256;
   unsigned long long* stat[2] = {(unsigned long long*)((char*)scratch + RS_HDR_PAD), nullptr};
   stat[1] = stat[0] + tiles * 256;
-  (void)hipMemsetAsync(ghist, 0, RS_HDR_BYTES, st);
+  if (!hdr_zeroed) (void)hipMemsetAsync(ghist, 0, RS_HDR_BYTES, st);
   const unsigned hgrid = (unsigned)(tiles < 1024 ? tiles : 1024);
   // (the digit count's tile is only its loop step: large sorts take RS_ITEMS keys per thread)
   if (items == RS_SMALL_ITEMS)
