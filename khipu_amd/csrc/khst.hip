@@ -179,6 +179,15 @@ __global__ void __launch_bounds__(BS) k_sseg_from_ck(const uint32_t* sck, uint64
   if (i < m) sseg[i] = sb ? sck[i] >> (32 - sb) : 0u;  // sb = 0: one segment (a 32-bit shift would be undefined)
 }
 
+// composite sort key of key word 0 (k0): segment id in the top sb bits, then the key's leading
+// bits (big-endian); flags |= 4 when the segment id needs more than sb bits
+__device__ __forceinline__ uint64_t composite_ck(uint64_t k0, const uint32_t* seg, uint32_t sb, uint64_t i,
+                                                 unsigned long long* flags) {
+  const uint64_t be = bswap64(k0);
+  if (!sb) return be;
+  if (flags && sb < 32 && (seg[i] >> sb)) atomicOr(flags, 4ULL);
+  return ((uint64_t)seg[i] << (64 - sb)) | (be >> sb);
+}
 // composite sort key: segment id in the top sb bits, then the key's leading bits (big-endian)
 // (flags, nullable: |= 4 when a segment id needs more than sb bits -- a forest commit's sb is
 // a hint from the trie ids seen before; the sort is then redone with 32)
@@ -191,14 +200,35 @@ __global__ void __launch_bounds__(BS) k_make_ck(const uint64_t* K, const uint32_
   if (rs_hdr)
     for (uint64_t w = i; w < RS_HDR_BYTES / 4; w += (uint64_t)gridDim.x * BS) rs_hdr[w] = 0;
   if (i >= n) return;
-  uint64_t be = bswap64(K[4 * i]);
-  uint64_t c = be;
-  if (sb) {
-    if (flags && sb < 32 && (seg[i] >> sb)) atomicOr(flags, 4ULL);
-    c = ((uint64_t)seg[i] << (64 - sb)) | (be >> sb);
-  }
-  ck[i] = c;
+  ck[i] = composite_ck(K[4 * i], seg, sb, i, flags);
   idx[i] = (uint32_t)i;
+}
+// A forest commit's op keys after k_f_inputs (trie ids, counters zeroed, unhashed keys copied):
+// the keys hashed (HASH: upserts then deletes), the composite sort keys made from them and the
+// radix header zeroed -- one launch where two key-hashing launches and k_make_ck were
+template <bool SHORT, bool HASH>
+__global__ void __launch_bounds__(BS) k_f_keys_ck(const uint8_t* up_keys, uint64_t nup, const uint8_t* del_keys,
+                                                  uint64_t ndel, uint32_t klen, uint64_t* K, const uint32_t* seg,
+                                                  uint32_t sb, uint64_t* ck, uint32_t* idx, unsigned long long* flags,
+                                                  uint32_t* rs_hdr) {
+  const uint64_t o = (uint64_t)blockIdx.x * BS + threadIdx.x;
+  for (uint64_t w = o; w < RS_HDR_BYTES / 4; w += (uint64_t)gridDim.x * BS) rs_hdr[w] = 0;
+  if (o >= nup + ndel) return;
+  uint64_t k0;
+  if (HASH) {
+    const uint8_t* key = o < nup ? up_keys + o * klen : del_keys + (o - nup) * klen;
+    uint64_t h[4];
+    if (SHORT)
+      kec256_short(key, klen, h);
+    else
+      kec256_msg<false>(key, klen, h);
+    for (int j = 0; j < 4; ++j) K[4 * o + j] = h[j];
+    k0 = h[0];
+  } else {
+    k0 = K[4 * o];
+  }
+  ck[o] = composite_ck(k0, seg, sb, o, flags);
+  idx[o] = (uint32_t)o;
 }
 
 // Runs of equal 32-bit sort prefixes (same segment, equal leading key bits) are
@@ -2022,6 +2052,7 @@ struct SortIO {
   const uint8_t* kn;  // variable-length keys: nibble counts (input order; nullable)
   bool ck_ready = false;  // ck_path: ck0/idx0 already hold the 32-bit sort keys (k_hash_keys_ck)
   bool ck_path = false;   // unsegmented plain build: sort (32-bit prefix, idx) only, never gather the keys
+  bool ck_made = false;   // composite path: ck0 / idx0 and the radix header already made (k_f_keys_ck)
   // 64-bit composite path: the radix range is bits [rs_lo, 64) -- 40 (the leading 24 bits) where
   // keys are few per segment, the tie kernel then orders the runs of equal leading 24 bits
   int rs_lo = 32;
@@ -2131,8 +2162,9 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
   // the 64-bit composite prefixes sorted on their top 32 bits, the keys gathered and the runs
   // of equal prefixes put in order; one sync for the flags (and the caller's check word)
   uint32_t sbu = sb;  // (a forest's hint; 32 if it was short)
+  bool made = S.ck_made;
   auto sort_prefix = [&] {
-    if (!S.ck_ready) {
+    if (!S.ck_ready && !made) {
       hipLaunchKernelGGL(k_make_ck, GRID(n, BS), dim3(BS), 0, st, (const uint64_t*)K32, seg, sbu, n, ck0, idx0,
                          T.ctr + CTR_TIE, (uint32_t*)rs_scratch);
       LAUNCH_CHECK();
@@ -2164,6 +2196,7 @@ static void sort_dedup(kh_ctx* c, SortIO& S) {
     if (tie_flags & 4) {  // a trie id past the hinted bits: again with 32
       if (S.ck_ready) throw KhError{KH_EINTERNAL, "sort: segment bits on prepared prefixes"};
       HIPCHK(hipMemsetAsync(T.ctr + CTR_NDUP, 0, 16, st));
+      made = false;  // (the prefixes again, with 32 segment bits)
       sbu = 32;
       S.sb = 32;
       S.rs_lo = 32;  // (the segment id alone fills the leading 32 bits)
@@ -4234,21 +4267,6 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   uint64_t* uoff = cv.take<uint64_t>(nops + 1);
   uint64_t* ulen = cv.take<uint64_t>(nops);
   uint32_t* ur = cv.take<uint32_t>(nops);
-  if (h->flags & KH_HASH_KEYS) {
-    if (F.nup) {
-      if (F.klen <= 135)
-        hipLaunchKernelGGL(k_hash_keys<true>, GRID(F.nup, BS), dim3(BS), 0, st, F.up_keys, F.klen, F.nup, K);
-      else
-        hipLaunchKernelGGL(k_hash_keys<false>, GRID(F.nup, BS), dim3(BS), 0, st, F.up_keys, F.klen, F.nup, K);
-    }
-    if (F.ndel) {
-      if (F.klen <= 135)
-        hipLaunchKernelGGL(k_hash_keys<true>, GRID(F.ndel, BS), dim3(BS), 0, st, F.del_keys, F.klen, F.ndel, K + 4 * F.nup);
-      else
-        hipLaunchKernelGGL(k_hash_keys<false>, GRID(F.ndel, BS), dim3(BS), 0, st, F.del_keys, F.klen, F.ndel, K + 4 * F.nup);
-    }
-    LAUNCH_CHECK();
-  }
   if (segd && ((F.nup && !F.up_trie) || (F.ndel && !F.del_trie))) throw KhError{KH_EINVAL, "forest ops need trie ids"};
   // the op keys (unless hashed above) and trie ids, upserts then deletes: one launch
   bool copy_keys = !(h->flags & KH_HASH_KEYS);
@@ -4261,7 +4279,24 @@ static void forest_commit(kh_trie* h, const FCommit& F, kh_stats* stats) {
   hipLaunchKernelGGL(k_f_inputs, GRID(nops, BS), dim3(BS), 0, st, (const uint64_t*)F.up_keys, F.nup,
                      (const uint64_t*)F.del_keys, F.ndel, copy_keys, segd ? F.up_trie : nullptr,
                      segd ? F.del_trie : nullptr, K, Tid, S.ctr);
+  // the keys hashed (the trie's key encoder) and the composite sort keys made, one launch
+  {
+    const bool hk = h->flags & KH_HASH_KEYS;
+    const uint32_t* sg = segd ? Tid : nullptr;
+    unsigned long long* fl = S.ctr + CTR_TIE;
+    uint32_t* hdr = (uint32_t*)S.rs_scratch;
+    if (hk && F.klen <= 135)
+      hipLaunchKernelGGL((k_f_keys_ck<true, true>), GRID(nops, BS), dim3(BS), 0, st, F.up_keys, F.nup, F.del_keys, F.ndel,
+                         F.klen, K, sg, S.sb, S.ck0, S.idx0, fl, hdr);
+    else if (hk)
+      hipLaunchKernelGGL((k_f_keys_ck<false, true>), GRID(nops, BS), dim3(BS), 0, st, F.up_keys, F.nup, F.del_keys,
+                         F.ndel, F.klen, K, sg, S.sb, S.ck0, S.idx0, fl, hdr);
+    else
+      hipLaunchKernelGGL((k_f_keys_ck<true, false>), GRID(nops, BS), dim3(BS), 0, st, F.up_keys, F.nup, F.del_keys,
+                         F.ndel, F.klen, K, sg, S.sb, S.ck0, S.idx0, fl, hdr);
+  }
   LAUNCH_CHECK();
+  S.ck_made = true;
   sort_dedup(c, S);
   if (S.fallback && S.rs_lo == 40) h->lo24_off = 16;
   if (!defer && F.chk && c->h_pinned[1] == F.chk_tok) throw KhError{KH_EINVAL, F.chk_msg};
