@@ -247,6 +247,38 @@ def test_forest_hot_trie(khst, oracle, hashed):
     f.close()
 
 
+@pytest.mark.parametrize("case", ["repeat", "id_past_hint", "long_run"])
+def test_forest_op_sort_edges_between_clean_blocks(khst, oracle, case):
+    """The op sort's rare paths between ordinary blocks: a clean warm block, then a block with
+    a key put twice (the later put wins), a trie id past the hinted bits (the sort redone with
+    32), or a run of equal 24-bit sort prefixes past the tie kernel (the full sort, then the
+    24-bit form off for 16 commits), then 18 clean blocks; every root against the oracle's
+    tries folded put by put."""
+    from khipu_amd.device import Ctx, ResidentForest
+    r = random.Random(31 + ["repeat", "id_past_hint", "long_run"].index(case))
+    f = ResidentForest(Ctx(0), hash_keys=True)
+    tries = {}
+    for blk in range(20):
+        ids = r.sample(range(1, 1 << 15), 30)  # (ids of 17 hinted bits: the 24-bit sort form)
+        ups = [(t, bytes(r.getrandbits(8) for _ in range(32)), C.storage_value(r)) for t in ids for _ in range(3)]
+        if blk == 1 and case == "repeat":
+            k = ups[5][1]
+            ups.append((ups[5][0], k, b"\x7f"))
+        if blk == 1 and case == "id_past_hint":
+            ups.append((1 << 30, b"\x33" * 32, b"\x05"))
+        if blk == 1 and case == "long_run":  # 12k ops in one trie: ~94 a run of the 24-bit prefix
+            ups += [(7, bytes(r.getrandbits(8) for _ in range(32)), C.storage_value(r)) for _ in range(12000)]
+        got = f.commit(ups, [])
+        touched = set()
+        for t, slot, v in ups:
+            tries.setdefault(t, oracle.Trie()).put(oracle.kec256(slot), v)
+            touched.add(t)
+        assert set(got) == touched, blk
+        for t in touched:
+            assert got[t] == tries[t].root_hash(), (case, blk, t)
+    f.close()
+
+
 @pytest.mark.parametrize("sc", C.commit_scenarios()[:4], ids=lambda s: s[0])
 def test_open_from_node_store(khst, oracle, sc):
     """kh_trie_open_nodes: a trie opened from its root hash and the
