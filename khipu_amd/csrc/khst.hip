@@ -728,14 +728,28 @@ __device__ __forceinline__ uint32_t branch_bucket(const Topo& T, uint64_t j) {
   uint32_t blocks = perms_for_len(rlp_hdr_len(payload) + payload);  // 1..4
   return (uint32_t)T.br_depth[j] * 8 + (T.br_ext[j] ? 4 : 0) + (4 - blocks);
 }
-constexpr uint32_t LV_TILE = BS * 16;  // branch ids per block: few blocks -> a short [bucket][block] table
+constexpr uint32_t LV_IT = 16;          // branch ids per thread
+constexpr uint32_t LV_TILE = BS * LV_IT;  // branch ids per block: few blocks -> a short [bucket][block] table
+// the buckets of a thread's LV_IT branch ids, their loads issued together (one round trip, not
+// LV_IT dependent ones: a block commit's element builds are latency-bound); NBUCKET past B
+__device__ __forceinline__ void level_buckets(const Topo& T, uint64_t B, uint32_t (&bk)[LV_IT]) {
+  const uint64_t j0 = (uint64_t)blockIdx.x * LV_TILE + threadIdx.x;
+#pragma unroll
+  for (uint32_t q = 0; q < LV_IT; ++q) {
+    const uint64_t j = j0 + (uint64_t)q * BS;
+    bk[q] = j < B ? branch_bucket(T, j) : NBUCKET;
+  }
+}
 __global__ void __launch_bounds__(BS) k_level_count(Topo T, const uint32_t* Bp, uint32_t* bcnt, uint32_t nblk) {
   topo_prio();
   __shared__ uint32_t h[NBUCKET];
   for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) h[q] = 0;
+  uint32_t bk[LV_IT];
+  level_buckets(T, *Bp, bk);
   __syncthreads();
-  const uint64_t B = *Bp, j0 = (uint64_t)blockIdx.x * LV_TILE;
-  for (uint64_t j = j0 + threadIdx.x; j < j0 + LV_TILE && j < B; j += BS) atomicAdd(&h[branch_bucket(T, j)], 1u);
+#pragma unroll
+  for (uint32_t q = 0; q < LV_IT; ++q)
+    if (bk[q] < NBUCKET) atomicAdd(&h[bk[q]], 1u);
   __syncthreads();
   for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) bcnt[(uint64_t)q * nblk + blockIdx.x] = h[q];
 }
@@ -748,10 +762,13 @@ __global__ void __launch_bounds__(BS) k_level_scatter(Topo T, const uint32_t* Bp
   topo_prio();
   __shared__ uint32_t base[NBUCKET];
   for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) base[q] = bbase[(uint64_t)q * nblk + blockIdx.x];
+  uint32_t bk[LV_IT];
+  level_buckets(T, *Bp, bk);
   __syncthreads();
-  const uint64_t B = *Bp, j0 = (uint64_t)blockIdx.x * LV_TILE;
-  for (uint64_t j = j0 + threadIdx.x; j < j0 + LV_TILE && j < B; j += BS)
-    pos[j] = atomicAdd(&base[branch_bucket(T, j)], 1u);
+  const uint64_t j0 = (uint64_t)blockIdx.x * LV_TILE + threadIdx.x;
+#pragma unroll
+  for (uint32_t q = 0; q < LV_IT; ++q)
+    if (bk[q] < NBUCKET) pos[j0 + (uint64_t)q * BS] = atomicAdd(&base[bk[q]], 1u);
 }
 
 // the branch tables k_branch_topo wrote in key-order ids (J), moved to level order
