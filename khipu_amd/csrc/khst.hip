@@ -6353,14 +6353,6 @@ int kh_block_commit(kh_trie* state, kh_trie* storage, const uint32_t* d_s_up_tri
         if (!injected) throw KhError{KH_EINTERNAL, "the block's storage phase failed"};
       };
       try {
-#ifdef KH_BC_ACCT_LOW
-        struct StSwap {
-          kh_ctx* c;
-          hipStream_t old;
-          ~StSwap() { c->st = old; }
-        } sw{c, c->st};
-        c->st = c->st2;
-#endif
         forest_commit(state, A, &ast);
       } catch (...) {
         aerr = std::current_exception();
