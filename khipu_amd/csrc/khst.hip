@@ -740,8 +740,18 @@ __device__ __forceinline__ void level_buckets(const Topo& T, uint64_t B, uint32_
     bk[q] = j < B ? branch_bucket(T, j) : NBUCKET;
   }
 }
-__global__ void __launch_bounds__(BS) k_level_count(Topo T, const uint32_t* Bp, uint32_t* bcnt, uint32_t nblk) {
+// The table's stride is the device's block count for the B branches, ceil(B / LV_TILE): the grid
+// is sized by the boundaries (B is not on the host yet), and a 100M build's B is a third of them --
+// the blocks past it neither write nor are scanned (the [bucket][block] stores are scattered:
+// 32-byte sectors for 4-byte counts, 0.4 GB a 100M build with the host's bound)
+__device__ __forceinline__ uint32_t level_blocks(const uint32_t* Bp) {
+  return (uint32_t)(((uint64_t)*Bp + LV_TILE - 1) / LV_TILE);
+}
+__global__ void __launch_bounds__(BS) k_level_count(Topo T, const uint32_t* Bp, uint32_t* bcnt, uint32_t* ncnt) {
   topo_prio();
+  const uint32_t nblk = level_blocks(Bp);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ncnt = NBUCKET * nblk;  // (the table scan's count)
+  if (blockIdx.x >= nblk) return;
   __shared__ uint32_t h[NBUCKET];
   for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) h[q] = 0;
   uint32_t bk[LV_IT];
@@ -758,8 +768,10 @@ __global__ void __launch_bounds__(BS) k_level_count(Topo T, const uint32_t* Bp, 
 // level order; the branch tables are then permuted to that order (k_branch_permute)
 // so a level reads its branches' fields, child records and message slots contiguously
 __global__ void __launch_bounds__(BS) k_level_scatter(Topo T, const uint32_t* Bp, const uint32_t* bbase,
-                                                      uint32_t nblk, uint32_t* pos) {
+                                                      uint32_t* pos) {
   topo_prio();
+  const uint32_t nblk = level_blocks(Bp);
+  if (blockIdx.x >= nblk) return;
   __shared__ uint32_t base[NBUCKET];
   for (uint32_t q = threadIdx.x; q < NBUCKET; q += BS) base[q] = bbase[(uint64_t)q * nblk + blockIdx.x];
   uint32_t bk[LV_IT];
@@ -802,10 +814,11 @@ __global__ void __launch_bounds__(BS) k_bid_remap(Topo T, const uint32_t* pos, u
 }
 
 // level bounds: lb[d] = first position of depth d in `order`, lb[64] = B
-__global__ void k_level_bounds(const uint32_t* bbase, uint32_t nblk, const uint32_t* Bp, uint32_t* lb) {
+__global__ void k_level_bounds(const uint32_t* bbase, const uint32_t* Bp, uint32_t* lb) {
   topo_prio();
+  const uint32_t nblk = level_blocks(Bp);
   uint32_t d = threadIdx.x;
-  if (d < 64) lb[d] = bbase[(uint64_t)d * LV_PER_DEPTH * nblk];
+  if (d < 64) lb[d] = nblk ? bbase[(uint64_t)d * LV_PER_DEPTH * nblk] : 0;
   if (d == 0) lb[64] = *Bp;
 }
 
@@ -2728,15 +2741,18 @@ static void run_build_once(kh_ctx* c, const BuildArgs& A, BuildOut& O, kh_stats*
     LAUNCH_CHECK();
     // level order (grids sized by nb; threads past B exit), then every branch id
     // becomes its level position
-    const uint32_t nblk = (uint32_t)((nb + LV_TILE - 1) / LV_TILE);
-    hipLaunchKernelGGL(k_level_count, dim3(nblk), dim3(BS), 0, st, TJ, (const uint32_t*)Bp, bcnt, nblk);
+    const uint32_t nblk = (uint32_t)((nb + LV_TILE - 1) / LV_TILE);  // (the host's bound; the device's is B's)
+    uint32_t* ncnt = lb + 72;
+    hipLaunchKernelGGL(k_level_count, dim3(nblk), dim3(BS), 0, st, TJ, (const uint32_t*)Bp, bcnt, ncnt);
     LAUNCH_CHECK();
-    scan_exclusive<uint32_t>(bcnt, bcnt, (uint64_t)NBUCKET * nblk, (uint32_t*)nullptr, scan_scratch, st);
+    // (a small table: one block scans the bound's entries, those past the device's count unread later)
+    const uint64_t nbt = (uint64_t)NBUCKET * nblk;
+    scan_exclusive<uint32_t>(bcnt, bcnt, nbt, (uint32_t*)nullptr, scan_scratch, st, true,
+                             nbt > SCAN_SMALL_MAX ? (const uint32_t*)ncnt : nullptr);
     hipLaunchKernelGGL(k_level_scatter, dim3(nblk), dim3(BS), 0, st, TJ, (const uint32_t*)Bp,
-                       (const uint32_t*)bcnt, nblk, order);
+                       (const uint32_t*)bcnt, order);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_level_bounds, dim3(1), dim3(64), 0, st, (const uint32_t*)bcnt, nblk, (const uint32_t*)Bp,
-                       lb);
+    hipLaunchKernelGGL(k_level_bounds, dim3(1), dim3(64), 0, st, (const uint32_t*)bcnt, (const uint32_t*)Bp, lb);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_branch_permute, topo_grid(nb), dim3(BS), 0, st, T, J, (const uint32_t*)order,
                        (const uint32_t*)Bp);

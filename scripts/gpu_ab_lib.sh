@@ -3,7 +3,7 @@
 #   bash scripts/gpu_ab_lib.sh TAG "label:ENV=V ..." ...   (ENV may be KHST_LIB_AB=path)
 export TMPDIR=/tmp
 tag=$1; shift
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
 for spec in "$@"; do
   label=${spec%%:*}; envs=${spec#*:}
   env $envs timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu --no-host-path > gpurun_out/ab_${tag}_${label}_$rep.json 2>/dev/null || exit 1
