@@ -42,6 +42,26 @@ def test_commit_hash_keys(khst, oracle):
     assert got == want[1]
 
 
+@pytest.mark.parametrize("klen", [135, 136, 300])
+def test_commit_long_hashed_keys(khst, oracle, klen):
+    """Keys hashed by the commit's key pass (k_f_keys_ck) at the one-block limit (135 bytes) and
+    past it (the multi-block sponge): upserts and deletes hashed in the same launch, a delete of a
+    key the same batch upserts (deletes apply after upserts), new keys and absent deletes."""
+    from khipu_amd.device import Ctx, ResidentTrie
+    r = random.Random(klen)
+    keys = [bytes(r.getrandbits(8) for _ in range(klen)) for _ in range(400)]
+    vals = [C.storage_value(r) for _ in keys]
+    t = ResidentTrie(Ctx(0), keys, vals, hash_keys=True)
+    ups = [(k, C.storage_value(r)) for k in r.sample(keys, 40)] + [
+        (bytes(r.getrandbits(8) for _ in range(klen)), b"\x09") for _ in range(10)]
+    dels = r.sample(keys, 25) + [ups[0][0], bytes(r.getrandbits(8) for _ in range(klen))]
+    got = t.commit(ups, dels, hash_keys=True)
+    want = C.oracle_commits(oracle, [oracle.kec256(k) for k in keys], vals,
+                            [([(oracle.kec256(k), v) for k, v in ups], [oracle.kec256(k) for k in dels])])
+    assert got == want[1]
+    t.close()
+
+
 def test_commit_uses_open_hash_keys(khst, oracle):
     """A storage trie opened with hash_keys=True hashes 32-byte slot keys on every commit
     without repeating the flag (the flag used to default to False); asking for
