@@ -900,14 +900,37 @@ __global__ void __launch_bounds__(BS) k_leaf_prep(Topo T, uint32_t* list, unsign
   const uint64_t a0 = (off + vmis) >> 3;                     // first aligned word of the span
   const uint32_t nw = vlen ? (uint32_t)(((off + vmis + vlen + 7) >> 3) - a0) : 0;
   const uint32_t g = ln >> 4, gl = ln & 15;
-  for (uint32_t it = 0; it < 16; ++it) {
-    uint32_t src = it * 4 + g;  // lane of the wave whose span this group copies
-    uint64_t sa = __shfl(a0, (int)src);
-    uint32_t sn = __shfl(nw, (int)src);
-    if (sn <= STAGE_WORDS) {
-      uint64_t* dst = stage + (wbase + src) * STAGE_WORDS;
-      if (gl < sn) dst[gl] = vw[sa + gl];
-      if (gl + 16 < sn) dst[gl + 16] = vw[sa + gl + 16];
+  // four spans' loads issued together, then their LDS stores (per-span conditions around each
+  // load made every one of a wave's 32 loads a round trip of its own: the latency-bound passes --
+  // a block commit's late leaves -- spent ~50 us there); a lane with nothing to load reads the
+  // values' first word instead (unused)
+  if (T.vals) {
+#pragma unroll
+    for (uint32_t it0 = 0; it0 < 16; it0 += 4) {
+      uint64_t w0[4], w1[4];
+      uint32_t sn[4];
+      uint64_t sa[4];
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t src = (it0 + q) * 4 + g;  // lane of the wave whose span this group copies
+        sa[q] = __shfl(a0, (int)src);
+        const uint32_t n = __shfl(nw, (int)src);
+        sn[q] = n <= STAGE_WORDS ? n : 0;
+      }
+      // (the wave's 16 spans here all empty -- cached elements and subtrees, most of a block
+      // commit's: no loads)
+      if (!__ballot((sn[0] | sn[1] | sn[2] | sn[3]) != 0)) continue;
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) {
+        w0[q] = vw[gl < sn[q] ? sa[q] + gl : 0];
+        w1[q] = vw[gl + 16 < sn[q] ? sa[q] + gl + 16 : 0];
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) {
+        uint64_t* dst = stage + (wbase + (it0 + q) * 4 + g) * STAGE_WORDS;
+        if (gl < sn[q]) dst[gl] = w0[q];
+        if (gl + 16 < sn[q]) dst[gl + 16] = w1[q];
+      }
     }
   }
   __syncthreads();
